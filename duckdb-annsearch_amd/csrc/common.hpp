@@ -1,0 +1,42 @@
+// common.hpp — shared host/device helpers for the MI355X ANN search backend.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdexcept>
+#include <string>
+#include <cstdio>
+
+namespace hipann {
+
+struct HipError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+#define HIPANN_CHECK(expr)                                                                             \
+    do {                                                                                               \
+        hipError_t _e = (expr);                                                                        \
+        if (_e != hipSuccess) {                                                                        \
+            throw ::hipann::HipError(std::string(#expr) + " failed: " + hipGetErrorString(_e) + " (" + \
+                                     __FILE__ + ":" + std::to_string(__LINE__) + ")");                 \
+        }                                                                                              \
+    } while (0)
+
+#define HIPANN_REQUIRE(cond, msg)                                        \
+    do {                                                                 \
+        if (!(cond)) throw ::hipann::HipError(std::string("hipann: ") + (msg)); \
+    } while (0)
+
+__host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Metric codes of the C ABI (hip_ann.h / hip_diskann_bridge.h).
+enum Metric : int { kL2 = 0, kIP = 1 };
+
+// XCD-aware block remap (cdna_hip_programming.md §5.5 T1, bijective form): blocks b and b+8 are
+// dealt to the same XCD; map so that each XCD receives a contiguous run of logical blocks.
+__device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
+    const int q = nblocks >> 3, r = nblocks & 7;
+    const int xcd = bid & 7, j = bid >> 3;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + j;
+}
+
+}  // namespace hipann

@@ -1,0 +1,490 @@
+// flat_kernels.hip — Flat (brute-force) search kernels for gfx950.
+//
+// Replaces the faiss-metal Flat pipeline (MetalIndexFlat::search, MetalIndexFlat.mm:294-369):
+//   l2_norm*.metal            → row_norms_f32
+//   simdgroup_gemm*.metal + warp/block_select.metal (nq×N distance matrix, then select)
+//                             → flat_gemm_topk: fp32 MFMA Q·Xᵀ with the L2 epilogue and a
+//                               wave-distributed top-k fused in; the nq×N matrix never exists
+//   fused_l2_topk.metal (small nq streaming scan)
+//                             → flat_scan_topk: direct Σ(q−x)², HBM-bound
+//   (host k-way merge)        → merge_parts_topk
+//
+// Distance forms follow FAISS CPU (the parity target, SURVEY §8a semantic contract):
+//   nq <  20  → direct Σ(q−x)² (fvec_L2sqr)                      → flat_scan_topk
+//   nq >= 20  → ‖q‖² + ‖x‖² − 2·q·x, clamped ≥ 0 (BLAS path)      → flat_gemm_topk
+//   IP        → q·x, best = largest (selected as key = −q·x)
+#include "common.hpp"
+#include "wave_topk.hpp"
+
+namespace hipann {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------------------------
+// ‖x‖² per row.  One wave per row, float4 loads when d % 4 == 0 (and 16-B aligned rows).
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) row_norms_f32(const float *__restrict__ x, int64_t n, int d, int vec4,
+                                                     float *__restrict__ out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= n) return;
+    const float *p = x + row * (int64_t)d;
+    float s = 0.f;
+    if (vec4) {
+        const float4 *p4 = reinterpret_cast<const float4 *>(p);
+        for (int j = lane; j < (d >> 2); j += 64) {
+            float4 v = p4[j];
+            s = fmaf(v.x, v.x, s); s = fmaf(v.y, v.y, s); s = fmaf(v.z, v.z, s); s = fmaf(v.w, v.w, s);
+        }
+    } else {
+        for (int j = lane; j < d; j += 64) s = fmaf(p[j], p[j], s);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) out[row] = s;
+}
+
+// ---------------------------------------------------------------------------------------------
+// flat_gemm_topk — fp32 MFMA (v_mfma_f32_32x32x2_f32, exact f32 fma chain) tile GEMM with a fused
+// distance epilogue and per-query top-k.  Block = 256 threads (4 waves), tile = 128 queries × 128
+// database rows, K staged through LDS in chunks of 32 (double buffered, register staging).
+//
+// Grid: nqt × nsplit blocks, XCD-remapped so that the nqt query tiles of one database split run on
+// the same XCD (they stream the same X rows: one HBM read, the rest L2 hits).  Each block walks the
+// database tiles [t0, t1) of its split and keeps, per query row, a wave-distributed list of the 64
+// best (key, row) pairs; at the end the first k go to part_d/part_i[split][q][0..k).
+// ---------------------------------------------------------------------------------------------
+constexpr int GBM = 128, GBN = 128, GBK = 32, GLD = GBK + 4;  // +4 floats: conflict-free ds_read_b128
+
+template <bool VEC4>
+__device__ __forceinline__ void gemm_stage_load(const float *__restrict__ base, int64_t row0, int64_t nrows,
+                                                int d, int k0, float4 (&r)[4]) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const int f = t + 256 * p;  // float4 index within the 128×32 tile
+        const int row = f >> 3, c4 = f & 7;
+        const int64_t grow = row0 + row;
+        const int kk = k0 + 4 * c4;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (grow < nrows) {
+            const float *src = base + grow * (int64_t)d + kk;
+            if (VEC4) {
+                if (kk < d) v = *reinterpret_cast<const float4 *>(src);
+            } else {
+                if (kk + 0 < d) v.x = src[0];
+                if (kk + 1 < d) v.y = src[1];
+                if (kk + 2 < d) v.z = src[2];
+                if (kk + 3 < d) v.w = src[3];
+            }
+        }
+        r[p] = v;
+    }
+}
+
+__device__ __forceinline__ void gemm_stage_store(float *__restrict__ lds, const float4 (&r)[4]) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const int f = t + 256 * p;
+        const int row = f >> 3, c4 = f & 7;
+        *reinterpret_cast<float4 *>(lds + row * GLD + 4 * c4) = r[p];
+    }
+}
+
+template <bool VEC4>
+__global__ void __launch_bounds__(256, 1)
+flat_gemm_topk(const float *__restrict__ Q, const float *__restrict__ qnorm, int64_t nq,
+               const float *__restrict__ X, const float *__restrict__ xnorm, int64_t N, int d, int metric,
+               int k, int nqt, int nsplit, int64_t tiles_per_split, float *__restrict__ part_d,
+               int *__restrict__ part_i) {
+    // LDS: two stages of A (queries) and B (db rows), 128×36 floats each; reused as the 128×128
+    // distance tile in the epilogue (64 KiB ≤ 72 KiB).
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float *As0 = smem;
+    float *Bs0 = smem + GBM * GLD;
+    float *As1 = smem + 2 * GBM * GLD;
+    float *Bs1 = smem + 3 * GBM * GLD;
+    float *Ct = smem;  // epilogue alias
+
+    const int nblocks = nqt * nsplit;
+    const int lb = xcd_remap(blockIdx.x, nblocks);
+    const int qt = lb % nqt;
+    const int split = lb / nqt;
+    const int64_t q0 = (int64_t)qt * GBM;
+    const int64_t ntiles = ceil_div(N, GBN);
+    const int64_t t0 = (int64_t)split * tiles_per_split;
+    const int64_t t1 = t0 + tiles_per_split < ntiles ? t0 + tiles_per_split : ntiles;
+
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int l31 = lane & 31, h = lane >> 5;
+
+    WaveList<1, int> lists[32];
+#pragma unroll
+    for (int r = 0; r < 32; ++r) lists[r].init();
+
+    const int nk = (d + GBK - 1) / GBK;
+    float4 sa[4], sb[4];
+
+    if (t0 < t1) {
+        gemm_stage_load<VEC4>(Q, q0, nq, d, 0, sa);
+        gemm_stage_load<VEC4>(X, t0 * GBN, N, d, 0, sb);
+    }
+
+    for (int64_t t = t0; t < t1; ++t) {
+        const int64_t x0 = t * GBN;
+        gemm_stage_store(As0, sa);
+        gemm_stage_store(Bs0, sb);
+        __syncthreads();
+
+        f32x16 acc[2][2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+        for (int kc = 0; kc < nk; ++kc) {
+            const float *Ab = (kc & 1) ? As1 : As0;
+            const float *Bb = (kc & 1) ? Bs1 : Bs0;
+            if (kc + 1 < nk) {
+                gemm_stage_load<VEC4>(Q, q0, nq, d, (kc + 1) * GBK, sa);
+                gemm_stage_load<VEC4>(X, x0, N, d, (kc + 1) * GBK, sb);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                f32x4 a4[2], b4[2];
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+                    a4[i] = *reinterpret_cast<const f32x4 *>(Ab + (64 * wr + 32 * i + l31) * GLD + 16 * h + 4 * u);
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    b4[j] = *reinterpret_cast<const f32x4 *>(Bb + (64 * wc + 32 * j + l31) * GLD + 16 * h + 4 * u);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+#pragma unroll
+                    for (int i = 0; i < 2; ++i)
+#pragma unroll
+                        for (int j = 0; j < 2; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[i][e], b4[j][e], acc[i][j], 0, 0, 0);
+                }
+            }
+            if (kc + 1 < nk) {
+                gemm_stage_store((kc & 1) ? As0 : As1, sa);
+                gemm_stage_store((kc & 1) ? Bs0 : Bs1, sb);
+            }
+            __syncthreads();
+        }
+
+        // Prefetch the next tile's first K chunk while the epilogue runs.
+        if (t + 1 < t1) {
+            gemm_stage_load<VEC4>(Q, q0, nq, d, 0, sa);
+            gemm_stage_load<VEC4>(X, (t + 1) * GBN, N, d, 0, sb);
+        }
+
+        // Epilogue 1: raw inner products → LDS tile Ct[128][128].
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = 64 * wr + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    const int col = 64 * wc + 32 * j + l31;
+                    Ct[row * GBN + col] = acc[i][j][r];
+                }
+        __syncthreads();
+
+        // Epilogue 2: wave `wave` owns query rows [32*wave, 32*wave+32) of the tile.
+        const int64_t xa = x0 + lane, xb = x0 + 64 + lane;
+        const bool va = xa < N, vb = xb < N;
+        float xna = 0.f, xnb = 0.f;
+        if (metric == kL2) {
+            xna = va ? xnorm[xa] : 0.f;
+            xnb = vb ? xnorm[xb] : 0.f;
+        }
+#pragma unroll
+        for (int r = 0; r < 32; ++r) {
+            const int row = 32 * wave + r;
+            const int64_t q = q0 + row;
+            if (q < nq) {  // wave-uniform
+                const float ipa = Ct[row * GBN + lane];
+                const float ipb = Ct[row * GBN + 64 + lane];
+                float ka, kb;
+                if (metric == kL2) {
+                    const float qn = qnorm[q];
+                    ka = fmaf(-2.f, ipa, qn + xna);
+                    kb = fmaf(-2.f, ipb, qn + xnb);
+                    ka = ka < 0.f ? 0.f : ka;
+                    kb = kb < 0.f ? 0.f : kb;
+                } else {
+                    ka = -ipa;
+                    kb = -ipb;
+                }
+                if (!va) ka = __builtin_inff();
+                if (!vb) kb = __builtin_inff();
+                lists[r].offer(ka, va ? (int)xa : 0x7fffffff, k - 1);
+                lists[r].offer(kb, vb ? (int)xb : 0x7fffffff, k - 1);
+            }
+        }
+        __syncthreads();
+    }
+
+    // Store the per-(split, query) partial lists.
+#pragma unroll
+    for (int r = 0; r < 32; ++r) {
+        const int64_t q = q0 + 32 * wave + r;
+        if (q < nq) {
+            const int64_t off = ((int64_t)split * nq + q) * k;
+            lists[r].store(part_d + off, part_i + off, k);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// flat_scan_topk — direct-form streaming scan for small query batches (FAISS nq < 20 path,
+// fvec_L2sqr / fvec_inner_product).  Queries live in LDS; each wave walks a contiguous range of
+// database rows, R rows at a time (R float4 row loads in flight per lane), reduces Σ(q−x)² (or
+// q·x) across the wave and keeps one top-k list per query.  HBM-bound: every X byte read once.
+// Partial lists go to part[(wave_global * nq + q) * k].
+// ---------------------------------------------------------------------------------------------
+constexpr int SCAN_MAXQ = 19;  // FAISS distance_compute_blas_threshold = 20
+constexpr int SCAN_R = 4;
+
+template <int NQ, bool VEC4>
+__global__ void __launch_bounds__(256)
+flat_scan_topk(const float *__restrict__ Q, const float *__restrict__ X, int64_t N, int d, int metric, int k,
+               int64_t rows_per_wave, float *__restrict__ part_d, int *__restrict__ part_i) {
+    extern __shared__ __attribute__((aligned(16))) float qs[];  // NQ × dpad
+    const int dpad = (d + 3) & ~3;
+    for (int i = threadIdx.x; i < NQ * dpad; i += 256) {
+        const int qi = i / dpad, j = i - qi * dpad;
+        qs[i] = j < d ? Q[(int64_t)qi * d + j] : 0.f;
+    }
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t r0 = gw * rows_per_wave;
+    int64_t r1 = r0 + rows_per_wave;
+    if (r1 > N) r1 = N;
+
+    WaveList<1, int> lists[NQ];
+#pragma unroll
+    for (int qi = 0; qi < NQ; ++qi) lists[qi].init();
+
+    // Per-lane candidate slots: after each group of 64 rows, lane j holds row (base + j).
+    float cand[NQ];
+#pragma unroll
+    for (int qi = 0; qi < NQ; ++qi) cand[qi] = __builtin_inff();
+
+    const int nd4 = dpad >> 2;
+    for (int64_t base = r0; base < r1; base += 64) {
+        const int64_t gend = (base + 64 < r1) ? base + 64 : r1;
+        for (int64_t rr = base; rr < gend; rr += SCAN_R) {
+            float acc[SCAN_R][NQ];
+#pragma unroll
+            for (int r = 0; r < SCAN_R; ++r)
+#pragma unroll
+                for (int qi = 0; qi < NQ; ++qi) acc[r][qi] = 0.f;
+            for (int j4 = lane; j4 < nd4; j4 += 64) {
+                float4 xv[SCAN_R];
+#pragma unroll
+                for (int r = 0; r < SCAN_R; ++r) {
+                    const int64_t row = rr + r;
+                    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (row < gend) {
+                        const float *src = X + row * (int64_t)d + 4 * j4;
+                        if (VEC4) v = *reinterpret_cast<const float4 *>(src);
+                        else {
+                            const int j = 4 * j4;
+                            if (j + 0 < d) v.x = src[0];
+                            if (j + 1 < d) v.y = src[1];
+                            if (j + 2 < d) v.z = src[2];
+                            if (j + 3 < d) v.w = src[3];
+                        }
+                    }
+                    xv[r] = v;
+                }
+#pragma unroll
+                for (int qi = 0; qi < NQ; ++qi) {
+                    const float4 qv = *reinterpret_cast<const float4 *>(qs + qi * dpad + 4 * j4);
+#pragma unroll
+                    for (int r = 0; r < SCAN_R; ++r) {
+                        if (metric == kL2) {
+                            float t;
+                            t = qv.x - xv[r].x; acc[r][qi] = fmaf(t, t, acc[r][qi]);
+                            t = qv.y - xv[r].y; acc[r][qi] = fmaf(t, t, acc[r][qi]);
+                            t = qv.z - xv[r].z; acc[r][qi] = fmaf(t, t, acc[r][qi]);
+                            t = qv.w - xv[r].w; acc[r][qi] = fmaf(t, t, acc[r][qi]);
+                        } else {
+                            acc[r][qi] = fmaf(qv.x, xv[r].x, acc[r][qi]);
+                            acc[r][qi] = fmaf(qv.y, xv[r].y, acc[r][qi]);
+                            acc[r][qi] = fmaf(qv.z, xv[r].z, acc[r][qi]);
+                            acc[r][qi] = fmaf(qv.w, xv[r].w, acc[r][qi]);
+                        }
+                    }
+                }
+            }
+            // Wave reductions; row rr+r lands in lane (rr + r - base).
+#pragma unroll
+            for (int r = 0; r < SCAN_R; ++r) {
+                const int slot = (int)(rr + r - base);
+#pragma unroll
+                for (int qi = 0; qi < NQ; ++qi) {
+                    float s = acc[r][qi];
+#pragma unroll
+                    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+                    if (metric != kL2) s = -s;
+                    if (lane == slot) cand[qi] = s;
+                }
+            }
+        }
+        // Offer the (up to) 64 candidates of this group.
+        const int64_t myrow = base + lane;
+        const bool valid = myrow < gend;
+#pragma unroll
+        for (int qi = 0; qi < NQ; ++qi) {
+            lists[qi].offer(valid ? cand[qi] : __builtin_inff(), valid ? (int)myrow : 0x7fffffff, k - 1);
+        }
+    }
+#pragma unroll
+    for (int qi = 0; qi < NQ; ++qi) {
+        const int64_t off = (gw * NQ + qi) * (int64_t)k;
+        lists[qi].store(part_d + off, part_i + off, k);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// merge_parts_topk — per query, the k best of nparts partial lists laid out [part][nq][k].
+// Keys are "smaller is better" (L2 distance or −IP).  One wave per query; S = ceil(k/64).
+//   in_local:  ids are int32 row numbers local to this index (label = label_offset + id)
+//   out_sign:  +1 → D = key; −1 → D = −key (IP: back to raw dot products)
+// Pads ((+inf, pad) or label < 0) become (±inf, −1).
+// ---------------------------------------------------------------------------------------------
+template <int S, typename InId>
+__global__ void __launch_bounds__(256)
+merge_parts_topk(const float *__restrict__ pd, const InId *__restrict__ pi, int nparts, int64_t nq, int k,
+                 int kout, int64_t label_offset, float in_sign, float out_sign, float *__restrict__ D,
+                 int64_t *__restrict__ I) {
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq) return;
+    const int lane = threadIdx.x & 63;
+    WaveList<S, long long> L;
+    L.init();
+    const int64_t total = (int64_t)nparts * k;
+    for (int64_t c0 = 0; c0 < total; c0 += 64) {
+        const int64_t c = c0 + lane;
+        float key = __builtin_inff();
+        long long lab = IdTraits<long long>::pad();
+        if (c < total) {
+            const int64_t p = c / k, i = c - p * k;
+            const int64_t off = (p * nq + q) * k + i;
+            const InId raw = pi[off];
+            const float v = pd[off] * in_sign;
+            if (raw >= 0 && raw != (InId)0x7fffffff && !(v == __builtin_inff())) {
+                key = v;
+                lab = (long long)raw + label_offset;
+            }
+        }
+        L.offer(key, lab, kout - 1);
+    }
+    const float pad_d = out_sign > 0.f ? __builtin_inff() : -__builtin_inff();
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const int e = s * 64 + lane;
+        if (e < kout) {
+            const bool pad = L.id[s] == IdTraits<long long>::pad();
+            D[q * kout + e] = pad ? pad_d : L.d[s] * out_sign;
+            I[q * kout + e] = pad ? -1 : (int64_t)L.id[s];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Host launchers (called from hip_ann.cpp).
+// ---------------------------------------------------------------------------------------------
+void launch_row_norms(const float *x, int64_t n, int d, float *out, hipStream_t st) {
+    if (n <= 0) return;
+    const int vec4 = (d % 4 == 0) && ((uintptr_t)x % 16 == 0);
+    hipLaunchKernelGGL(row_norms_f32, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, st, x, n, d, vec4, out);
+    HIPANN_CHECK(hipGetLastError());
+}
+
+size_t gemm_smem_bytes() { return (size_t)4 * GBM * GLD * sizeof(float); }
+
+void launch_flat_gemm_topk(const float *Q, const float *qn, int64_t nq, const float *X, const float *xn, int64_t N,
+                           int d, int metric, int k, int nsplit, int64_t tiles_per_split, float *pd, int *pi,
+                           hipStream_t st) {
+    const int nqt = (int)ceil_div(nq, GBM);
+    const bool vec4 = (d % 4 == 0) && ((uintptr_t)Q % 16 == 0) && ((uintptr_t)X % 16 == 0);
+    const size_t smem = gemm_smem_bytes();
+    dim3 grid((unsigned)(nqt * nsplit)), block(256);
+    if (vec4) {
+        hipLaunchKernelGGL(flat_gemm_topk<true>, grid, block, smem, st, Q, qn, nq, X, xn, N, d, metric, k, nqt,
+                           nsplit, tiles_per_split, pd, pi);
+    } else {
+        hipLaunchKernelGGL(flat_gemm_topk<false>, grid, block, smem, st, Q, qn, nq, X, xn, N, d, metric, k, nqt,
+                           nsplit, tiles_per_split, pd, pi);
+    }
+    HIPANN_CHECK(hipGetLastError());
+}
+
+template <int NQ>
+static void scan_dispatch(bool vec4, dim3 grid, size_t smem, hipStream_t st, const float *Q, const float *X,
+                          int64_t N, int d, int metric, int k, int64_t rpw, float *pd, int *pi) {
+    if (vec4)
+        hipLaunchKernelGGL((flat_scan_topk<NQ, true>), grid, dim3(256), smem, st, Q, X, N, d, metric, k, rpw, pd, pi);
+    else
+        hipLaunchKernelGGL((flat_scan_topk<NQ, false>), grid, dim3(256), smem, st, Q, X, N, d, metric, k, rpw, pd, pi);
+}
+
+size_t scan_smem_bytes(int nq, int d) { return (size_t)nq * ((d + 3) & ~3) * sizeof(float); }
+
+void launch_flat_scan_topk(const float *Q, int nq, const float *X, int64_t N, int d, int metric, int k,
+                           int nwaves, int64_t rows_per_wave, float *pd, int *pi, hipStream_t st) {
+    const bool vec4 = (d % 4 == 0) && ((uintptr_t)X % 16 == 0);
+    const size_t smem = scan_smem_bytes(nq, d);
+    dim3 grid((unsigned)ceil_div(nwaves, 4));
+    switch (nq) {
+#define HIPANN_SCAN_CASE(n) \
+    case n: scan_dispatch<n>(vec4, grid, smem, st, Q, X, N, d, metric, k, rows_per_wave, pd, pi); break;
+        HIPANN_SCAN_CASE(1) HIPANN_SCAN_CASE(2) HIPANN_SCAN_CASE(3) HIPANN_SCAN_CASE(4) HIPANN_SCAN_CASE(5)
+        HIPANN_SCAN_CASE(6) HIPANN_SCAN_CASE(7) HIPANN_SCAN_CASE(8) HIPANN_SCAN_CASE(9) HIPANN_SCAN_CASE(10)
+        HIPANN_SCAN_CASE(11) HIPANN_SCAN_CASE(12) HIPANN_SCAN_CASE(13) HIPANN_SCAN_CASE(14) HIPANN_SCAN_CASE(15)
+        HIPANN_SCAN_CASE(16) HIPANN_SCAN_CASE(17) HIPANN_SCAN_CASE(18) HIPANN_SCAN_CASE(19)
+#undef HIPANN_SCAN_CASE
+        default: throw HipError("flat_scan_topk: nq out of range");
+    }
+    HIPANN_CHECK(hipGetLastError());
+}
+
+template <typename InId>
+void launch_merge_parts(const float *pd, const InId *pi, int nparts, int64_t nq, int k, int kout,
+                        int64_t label_offset, float in_sign, float out_sign, float *D, int64_t *I, hipStream_t st) {
+    if (nq <= 0) return;
+    dim3 grid((unsigned)ceil_div(nq, 4)), block(256);
+    const int S = (kout + 63) / 64;
+#define HIPANN_MERGE_CASE(s)                                                                                  \
+    if (S <= s) {                                                                                             \
+        hipLaunchKernelGGL((merge_parts_topk<s, InId>), grid, block, 0, st, pd, pi, nparts, nq, k, kout, \
+                           label_offset, in_sign, out_sign, D, I);                                                          \
+        HIPANN_CHECK(hipGetLastError());                                                                      \
+        return;                                                                                               \
+    }
+    HIPANN_MERGE_CASE(1) HIPANN_MERGE_CASE(2) HIPANN_MERGE_CASE(4) HIPANN_MERGE_CASE(8) HIPANN_MERGE_CASE(16)
+    HIPANN_MERGE_CASE(32)
+#undef HIPANN_MERGE_CASE
+    throw HipError("merge: k too large");
+}
+
+template void launch_merge_parts<int>(const float *, const int *, int, int64_t, int, int, int64_t, float, float,
+                                      float *, int64_t *, hipStream_t);
+template void launch_merge_parts<long long>(const float *, const long long *, int, int64_t, int, int, int64_t, float,
+                                            float, float *, int64_t *, hipStream_t);
+
+}  // namespace hipann

@@ -1,0 +1,470 @@
+// hip_ann.cpp — C ABI (include/hip_ann.h) over the gfx950 Flat / IVFFlat search kernels.
+//
+// Reference behaviour mirrored here:
+//   MetalIndexFlat::search (faiss-metal/src/MetalIndexFlat.mm:294-369): k <= 0 throws; empty
+//     index / empty batch → (±inf, −1); effective_k = min(k, ntotal); labels int64.
+//   MetalIndexFlat::add (MetalIndexFlat.mm:173-292): append rows, ‖x‖² computed on the device.
+//   faiss_index.cpp:108-149 (EnsureGpuIndex) only needs create/search/free + availability.
+#include "../../include/hip_ann.h"
+#include "runtime.hpp"
+#include "ivf.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+
+using namespace hipann;
+
+namespace {
+
+void set_err(char *buf, int len, const char *msg) {
+    if (!buf || len <= 0) return;
+    std::strncpy(buf, msg, (size_t)len - 1);
+    buf[len - 1] = '\0';
+}
+
+template <typename F>
+int guard_int(char *eb, int el, F &&f) {
+    try {
+        return f();
+    } catch (const std::exception &e) {
+        set_err(eb, el, e.what());
+    } catch (...) {
+        set_err(eb, el, "hipann: unknown error");
+    }
+    return -1;
+}
+
+template <typename F>
+void *guard_ptr(char *eb, int el, F &&f) {
+    try {
+        return f();
+    } catch (const std::exception &e) {
+        set_err(eb, el, e.what());
+    } catch (...) {
+        set_err(eb, el, "hipann: unknown error");
+    }
+    return nullptr;
+}
+
+int g_device_count = -1;
+
+int device_count() {
+    if (g_device_count < 0) {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+        g_device_count = n;
+    }
+    return g_device_count;
+}
+
+void require_device() { HIPANN_REQUIRE(device_count() > 0, "no HIP device"); }
+
+std::vector<int> device_list(const int *devices, int ndev) {
+    std::vector<int> v;
+    if (!devices || ndev <= 0) v.push_back(0);
+    else v.assign(devices, devices + ndev);
+    for (int d : v) HIPANN_REQUIRE(d >= 0 && d < device_count(), "invalid device id " + std::to_string(d));
+    return v;
+}
+
+hipStream_t make_stream(int dev) {
+    DeviceGuard g(dev);
+    hipStream_t s;
+    HIPANN_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    return s;
+}
+
+constexpr int kFusedMaxK = 64;   // fused GEMM / scan lists: one element per lane
+constexpr int kBlasThreshold = 20;  // FAISS distance_compute_blas_threshold
+
+// Append rows to a shard's owned storage (capacity doubling, as MetalIndexFlat::add does).
+void shard_append(FlatShard &sh, int d, int metric, const float *x_host, const float *x_dev, int64_t n) {
+    if (n <= 0) return;
+    DeviceGuard g(sh.device);
+    const int64_t need = sh.n + n;
+    if (need > sh.cap || !sh.owns) {
+        int64_t cap = std::max<int64_t>(need, std::max<int64_t>(1024, sh.cap * 2));
+        DevBuf nb;
+        nb.ensure((size_t)cap * d * sizeof(float), sh.device);
+        if (sh.n > 0)
+            HIPANN_CHECK(hipMemcpyAsync(nb.get<float>(), sh.xb, (size_t)sh.n * d * sizeof(float),
+                                        hipMemcpyDeviceToDevice, sh.stream));
+        HIPANN_CHECK(hipStreamSynchronize(sh.stream));
+        std::swap(sh.xb_buf.p, nb.p);
+        std::swap(sh.xb_buf.bytes, nb.bytes);
+        sh.xb_buf.device = sh.device;
+        sh.xb = sh.xb_buf.get<float>();
+        sh.cap = cap;
+        sh.owns = true;
+        if (metric == kL2) {
+            DevBuf nn;
+            nn.ensure((size_t)cap * sizeof(float), sh.device);
+            if (sh.n > 0)
+                HIPANN_CHECK(hipMemcpyAsync(nn.get<float>(), sh.xn.get<float>(), (size_t)sh.n * sizeof(float),
+                                            hipMemcpyDeviceToDevice, sh.stream));
+            HIPANN_CHECK(hipStreamSynchronize(sh.stream));
+            std::swap(sh.xn.p, nn.p);
+            std::swap(sh.xn.bytes, nn.bytes);
+            sh.xn.device = sh.device;
+        }
+    }
+    float *dst = sh.xb + sh.n * (int64_t)d;
+    if (x_host)
+        HIPANN_CHECK(hipMemcpyAsync(dst, x_host, (size_t)n * d * sizeof(float), hipMemcpyHostToDevice, sh.stream));
+    else
+        HIPANN_CHECK(hipMemcpyAsync(dst, x_dev, (size_t)n * d * sizeof(float), hipMemcpyDeviceToDevice, sh.stream));
+    if (metric == kL2) launch_row_norms(dst, n, d, sh.xn.get<float>() + sh.n, sh.stream);
+    HIPANN_CHECK(hipStreamSynchronize(sh.stream));
+    sh.n = need;
+}
+
+}  // namespace
+
+namespace hipann {
+
+FlatIndex::~FlatIndex() {
+    for (auto &s : shards) {
+        if (s->stream) { DeviceGuard g(s->device); (void)hipStreamDestroy(s->stream); }
+    }
+}
+
+// Search one shard: queries already on the shard's device.  Writes D (nq×kout fp32: raw distances,
+// ±inf pads) and I (nq×kout int64 labels, −1 pads) on the same device, asynchronously on `st`.
+void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq, int k, int kout, float *D,
+                       int64_t *I, hipStream_t st) {
+    DeviceGuard g(sh.device);
+    const int d = ix.d, metric = ix.metric;
+    const float out_sign = metric == kIP ? -1.f : 1.f;
+    HIPANN_REQUIRE(k <= kFusedMaxK, "k > 64 is not supported by the fused GPU path yet");
+    if (nq <= 0) return;
+    if (sh.n == 0) {  // no rows: pads only
+        launch_merge_parts<int>(nullptr, nullptr, 0, nq, k, kout, sh.label_offset, 1.f, out_sign, D, I, st);
+        return;
+    }
+    HIPANN_REQUIRE(sh.n <= (int64_t)0x7ffffffe, "shard larger than 2^31-2 rows");
+    if (nq < kBlasThreshold) {
+        // direct form (fvec_L2sqr / fvec_inner_product)
+        int64_t nwaves = std::min<int64_t>(8192, std::max<int64_t>(1, ceil_div(sh.n, 512)));
+        const int64_t rpw = ceil_div(sh.n, nwaves);
+        nwaves = ceil_div(sh.n, rpw);
+        const int64_t nw_alloc = ceil_div(nwaves, 4) * 4;
+        HIPANN_REQUIRE(scan_smem_bytes((int)nq, d) <= 64 * 1024, "dimension too large for the scan path");
+        sh.part_d.ensure((size_t)nw_alloc * nq * k * sizeof(float), sh.device);
+        sh.part_i.ensure((size_t)nw_alloc * nq * k * sizeof(int), sh.device);
+        {
+            ScopedTiming t(ix.timer_main, st);
+            launch_flat_scan_topk(xq, (int)nq, sh.xb, sh.n, d, metric, k, (int)nw_alloc, rpw, sh.part_d.get<float>(),
+                                  sh.part_i.get<int>(), st);
+        }
+        ScopedTiming t(ix.timer_merge, st);
+        launch_merge_parts<int>(sh.part_d.get<float>(), sh.part_i.get<int>(), (int)nw_alloc, nq, k, kout,
+                                sh.label_offset, 1.f, out_sign, D, I, st);
+        return;
+    }
+    // BLAS form: ‖q‖² + ‖x‖² − 2 q·x on fp32 MFMA
+    const float *qn = nullptr;
+    if (metric == kL2) {
+        sh.qn.ensure((size_t)nq * sizeof(float), sh.device);
+        launch_row_norms(xq, nq, d, sh.qn.get<float>(), st);
+        qn = sh.qn.get<float>();
+    }
+    const int64_t nqt = ceil_div(nq, 128);
+    const int64_t ntiles = ceil_div(sh.n, 128);
+    int64_t nsplit = std::max<int64_t>(1, ceil_div(2048, nqt));
+    nsplit = std::min<int64_t>(nsplit, std::max<int64_t>(1, ntiles / 4));
+    if (nsplit >= 8) nsplit = nsplit / 8 * 8;
+    const int64_t tps = ceil_div(ntiles, nsplit);
+    nsplit = ceil_div(ntiles, tps);
+    HIPANN_REQUIRE(nqt * nsplit < (int64_t)0x7fffffff, "grid too large");
+    sh.part_d.ensure((size_t)nsplit * nq * k * sizeof(float), sh.device);
+    sh.part_i.ensure((size_t)nsplit * nq * k * sizeof(int), sh.device);
+    {
+        ScopedTiming t(ix.timer_main, st);
+        launch_flat_gemm_topk(xq, qn, nq, sh.xb, sh.xn.get<float>(), sh.n, d, metric, k, (int)nsplit, tps,
+                              sh.part_d.get<float>(), sh.part_i.get<int>(), st);
+    }
+    ScopedTiming t(ix.timer_merge, st);
+    launch_merge_parts<int>(sh.part_d.get<float>(), sh.part_i.get<int>(), (int)nsplit, nq, k, kout, sh.label_offset,
+                            1.f, out_sign, D, I, st);
+}
+
+}  // namespace hipann
+
+// ================================================================================================
+extern "C" {
+
+int hipann_available(void) {
+    try {
+        if (device_count() <= 0) return 0;
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, 0) != hipSuccess) return 0;
+        return std::strstr(p.gcnArchName, "gfx950") ? 1 : 0;
+    } catch (...) {
+        return 0;
+    }
+}
+
+int hipann_device_count(void) { return device_count(); }
+
+int hipann_device_info(char *buf, int buf_len) {
+    try {
+        std::string s;
+        const int n = device_count();
+        if (n <= 0) s = "HIP: no device available";
+        else {
+            hipDeviceProp_t p;
+            HIPANN_CHECK(hipGetDeviceProperties(&p, 0));
+            char tmp[512];
+            std::snprintf(tmp, sizeof tmp, "%s (%s, %d CUs, %.0f GB HBM) x%d", p.name, p.gcnArchName,
+                          p.multiProcessorCount, (double)p.totalGlobalMem / 1e9, n);
+            s = tmp;
+        }
+        set_err(buf, buf_len, s.c_str());
+        return (int)s.size();
+    } catch (...) {
+        return -1;
+    }
+}
+
+void *hipann_flat_create(int d, int metric, const float *xb, int64_t n, const int *devices, int ndev, char *eb,
+                         int el) {
+    return guard_ptr(eb, el, [&]() -> void * {
+        require_device();
+        HIPANN_REQUIRE(d > 0, "d must be > 0");
+        HIPANN_REQUIRE(metric == kL2 || metric == kIP, "metric must be 0 (L2) or 1 (IP)");
+        HIPANN_REQUIRE(n >= 0 && (n == 0 || xb), "invalid vectors");
+        auto devs = device_list(devices, ndev);
+        auto ix = std::make_unique<FlatIndex>();
+        ix->d = d;
+        ix->metric = metric;
+        const int64_t per = ceil_div(std::max<int64_t>(n, 1), (int64_t)devs.size());
+        int64_t off = 0;
+        for (size_t i = 0; i < devs.size(); ++i) {
+            auto sh = std::make_unique<FlatShard>();
+            sh->device = devs[i];
+            sh->stream = make_stream(devs[i]);
+            sh->label_offset = off;
+            const int64_t cnt = std::min<int64_t>(per, n - off);
+            if (cnt > 0) shard_append(*sh, d, metric, xb + off * (int64_t)d, nullptr, cnt);
+            off += std::max<int64_t>(cnt, 0);
+            ix->shards.push_back(std::move(sh));
+        }
+        return ix.release();
+    });
+}
+
+int hipann_flat_add(void *h, const float *xb, int64_t n, char *eb, int el) {
+    return guard_int(eb, el, [&]() -> int {
+        HIPANN_REQUIRE(h, "null index");
+        auto *ix = static_cast<IndexBase *>(h);
+        HIPANN_REQUIRE(ix->kind == Kind::Flat, "not a Flat index");
+        auto *fx = static_cast<FlatIndex *>(ix);
+        std::lock_guard<std::mutex> lk(fx->mu);
+        HIPANN_REQUIRE(n >= 0 && (n == 0 || xb), "invalid vectors");
+        // appended rows go to the last shard (labels stay contiguous)
+        auto &sh = *fx->shards.back();
+        shard_append(sh, fx->d, fx->metric, xb, nullptr, n);
+        return 0;
+    });
+}
+
+static int flat_search_host(FlatIndex &ix, int64_t nq, const float *xq, int64_t k, float *D, int64_t *I) {
+    HIPANN_REQUIRE(k > 0, "k must be > 0");
+    HIPANN_REQUIRE(k <= HIPANN_MAX_K, "k larger than HIPANN_MAX_K");
+    HIPANN_REQUIRE(nq >= 0 && (nq == 0 || (xq && D && I)), "invalid arguments");
+    const float pad = ix.metric == kIP ? -__builtin_inff() : __builtin_inff();
+    const int64_t ntot = ix.ntotal();
+    if (nq == 0) return 0;
+    if (ntot == 0) {
+        for (int64_t i = 0; i < nq * k; ++i) { D[i] = pad; I[i] = -1; }
+        return 0;
+    }
+    const int keff = (int)std::min<int64_t>(k, ntot);
+    const int kout = (int)k;
+    const size_t qbytes = (size_t)nq * ix.d * sizeof(float);
+    ix.h_q.ensure(qbytes);
+    std::memcpy(ix.h_q.p, xq, qbytes);
+    const size_t ob = (size_t)nq * kout;
+    for (auto &shp : ix.shards) {
+        FlatShard &sh = *shp;
+        DeviceGuard g(sh.device);
+        sh.q.ensure(qbytes, sh.device);
+        sh.out_d.ensure(ob * sizeof(float), sh.device);
+        sh.out_i.ensure(ob * sizeof(int64_t), sh.device);
+        HIPANN_CHECK(hipMemcpyAsync(sh.q.p, ix.h_q.p, qbytes, hipMemcpyHostToDevice, sh.stream));
+        flat_shard_search(ix, sh, nq, sh.q.get<float>(), keff, kout, sh.out_d.get<float>(), sh.out_i.get<int64_t>(),
+                          sh.stream);
+    }
+    ix.h_d.ensure(ob * sizeof(float));
+    ix.h_i.ensure(ob * sizeof(int64_t));
+    FlatShard &s0 = *ix.shards[0];
+    if (ix.shards.size() == 1) {
+        DeviceGuard g(s0.device);
+        HIPANN_CHECK(hipMemcpyAsync(ix.h_d.p, s0.out_d.p, ob * sizeof(float), hipMemcpyDeviceToHost, s0.stream));
+        HIPANN_CHECK(hipMemcpyAsync(ix.h_i.p, s0.out_i.p, ob * sizeof(int64_t), hipMemcpyDeviceToHost, s0.stream));
+        HIPANN_CHECK(hipStreamSynchronize(s0.stream));
+    } else {
+        // gather per-device partial top-k onto shard 0's device, then one device merge
+        const int np = (int)ix.shards.size();
+        ix.gather_d.ensure(ob * np * sizeof(float), s0.device);
+        ix.gather_i.ensure(ob * np * sizeof(int64_t), s0.device);
+        ix.merged_d.ensure(ob * sizeof(float), s0.device);
+        ix.merged_i.ensure(ob * sizeof(int64_t), s0.device);
+        for (int p = 0; p < np; ++p) {
+            FlatShard &sh = *ix.shards[p];
+            DeviceGuard g(sh.device);
+            HIPANN_CHECK(hipStreamSynchronize(sh.stream));
+            HIPANN_CHECK(hipMemcpyPeerAsync(ix.gather_d.get<float>() + p * ob, s0.device, sh.out_d.p, sh.device,
+                                            ob * sizeof(float), s0.stream));
+            HIPANN_CHECK(hipMemcpyPeerAsync(ix.gather_i.get<int64_t>() + p * ob, s0.device, sh.out_i.p, sh.device,
+                                            ob * sizeof(int64_t), s0.stream));
+        }
+        DeviceGuard g(s0.device);
+        const float sign = ix.metric == kIP ? -1.f : 1.f;
+        launch_merge_parts<long long>(ix.gather_d.get<float>(), ix.gather_i.get<long long>(), np, nq, kout, kout, 0,
+                                      sign, sign, ix.merged_d.get<float>(), ix.merged_i.get<int64_t>(), s0.stream);
+        HIPANN_CHECK(hipMemcpyAsync(ix.h_d.p, ix.merged_d.p, ob * sizeof(float), hipMemcpyDeviceToHost, s0.stream));
+        HIPANN_CHECK(hipMemcpyAsync(ix.h_i.p, ix.merged_i.p, ob * sizeof(int64_t), hipMemcpyDeviceToHost, s0.stream));
+        HIPANN_CHECK(hipStreamSynchronize(s0.stream));
+    }
+    std::memcpy(D, ix.h_d.p, ob * sizeof(float));
+    std::memcpy(I, ix.h_i.p, ob * sizeof(int64_t));
+    return 0;
+}
+
+int hipann_flat_search(void *h, int64_t nq, const float *xq, int64_t k, float *D, int64_t *I, char *eb, int el) {
+    return guard_int(eb, el, [&]() -> int {
+        HIPANN_REQUIRE(h, "null index");
+        auto *ix = static_cast<IndexBase *>(h);
+        HIPANN_REQUIRE(ix->kind == Kind::Flat, "not a Flat index");
+        auto *fx = static_cast<FlatIndex *>(ix);
+        std::lock_guard<std::mutex> lk(fx->mu);
+        return flat_search_host(*fx, nq, xq, k, D, I);
+    });
+}
+
+int hipann_flat_reconstruct(void *h, int64_t key, float *out, char *eb, int el) {
+    return guard_int(eb, el, [&]() -> int {
+        HIPANN_REQUIRE(h && out, "null argument");
+        auto *ix = static_cast<IndexBase *>(h);
+        HIPANN_REQUIRE(ix->kind == Kind::Flat, "not a Flat index");
+        auto *fx = static_cast<FlatIndex *>(ix);
+        std::lock_guard<std::mutex> lk(fx->mu);
+        for (auto &shp : fx->shards) {
+            FlatShard &sh = *shp;
+            if (key >= sh.label_offset && key < sh.label_offset + sh.n) {
+                DeviceGuard g(sh.device);
+                HIPANN_CHECK(hipMemcpyAsync(out, sh.xb + (key - sh.label_offset) * fx->d, (size_t)fx->d * sizeof(float),
+                                            hipMemcpyDeviceToHost, sh.stream));
+                HIPANN_CHECK(hipStreamSynchronize(sh.stream));
+                return 0;
+            }
+        }
+        throw HipError("hipann: reconstruct key out of range");
+    });
+}
+
+void *hipann_flat_create_device(int d, int metric, const float *xb_dev, int64_t n, int device, int copy,
+                                int64_t label_offset, char *eb, int el) {
+    return guard_ptr(eb, el, [&]() -> void * {
+        require_device();
+        HIPANN_REQUIRE(d > 0, "d must be > 0");
+        HIPANN_REQUIRE(metric == kL2 || metric == kIP, "metric must be 0 (L2) or 1 (IP)");
+        HIPANN_REQUIRE(device >= 0 && device < device_count(), "invalid device");
+        HIPANN_REQUIRE(n >= 0 && (n == 0 || xb_dev), "invalid vectors");
+        auto ix = std::make_unique<FlatIndex>();
+        ix->d = d;
+        ix->metric = metric;
+        auto sh = std::make_unique<FlatShard>();
+        sh->device = device;
+        sh->stream = make_stream(device);
+        sh->label_offset = label_offset;
+        if (copy) {
+            shard_append(*sh, d, metric, nullptr, xb_dev, n);
+        } else {
+            DeviceGuard g(device);
+            sh->xb = const_cast<float *>(xb_dev);
+            sh->owns = false;
+            sh->n = n;
+            sh->cap = n;
+            if (metric == kL2 && n > 0) {
+                sh->xn.ensure((size_t)n * sizeof(float), device);
+                launch_row_norms(sh->xb, n, d, sh->xn.get<float>(), sh->stream);
+                HIPANN_CHECK(hipStreamSynchronize(sh->stream));
+            }
+        }
+        ix->shards.push_back(std::move(sh));
+        return ix.release();
+    });
+}
+
+int hipann_flat_search_device(void *h, int64_t nq, const float *xq_dev, int64_t k, float *D_dev, int64_t *I_dev,
+                              void *stream, char *eb, int el) {
+    return guard_int(eb, el, [&]() -> int {
+        HIPANN_REQUIRE(h, "null index");
+        auto *ix = static_cast<IndexBase *>(h);
+        HIPANN_REQUIRE(ix->kind == Kind::Flat, "not a Flat index");
+        auto *fx = static_cast<FlatIndex *>(ix);
+        std::lock_guard<std::mutex> lk(fx->mu);
+        HIPANN_REQUIRE(fx->shards.size() == 1, "device search needs a single-device index");
+        HIPANN_REQUIRE(k > 0 && k <= HIPANN_MAX_K, "k out of range");
+        FlatShard &sh = *fx->shards[0];
+        hipStream_t st = stream ? static_cast<hipStream_t>(stream) : sh.stream;
+        const int keff = (int)std::min<int64_t>(k, std::max<int64_t>(sh.n, 1));
+        flat_shard_search(*fx, sh, nq, xq_dev, keff, (int)k, D_dev, I_dev, st);
+        return 0;
+    });
+}
+
+int hipann_merge_topk_device(int metric, int nparts, int64_t nq, int64_t k, const float *D_parts,
+                             const int64_t *I_parts, float *D_out, int64_t *I_out, void *stream, char *eb, int el) {
+    return guard_int(eb, el, [&]() -> int {
+        require_device();
+        HIPANN_REQUIRE(metric == kL2 || metric == kIP, "bad metric");
+        HIPANN_REQUIRE(k > 0 && k <= HIPANN_MAX_K && nparts >= 0, "bad arguments");
+        const float sign = metric == kIP ? -1.f : 1.f;
+        launch_merge_parts<long long>(D_parts, reinterpret_cast<const long long *>(I_parts), nparts, nq, (int)k, (int)k,
+                                      0, sign, sign, D_out, I_out, static_cast<hipStream_t>(stream));
+        return 0;
+    });
+}
+
+int64_t hipann_ntotal(void *h) { return h ? static_cast<IndexBase *>(h)->ntotal() : -1; }
+int hipann_dim(void *h) { return h ? static_cast<IndexBase *>(h)->d : -1; }
+int hipann_metric(void *h) { return h ? static_cast<IndexBase *>(h)->metric : -1; }
+int64_t hipann_memory_bytes(void *h) { return h ? static_cast<IndexBase *>(h)->memory_bytes() : -1; }
+
+void hipann_free(void *h) {
+    if (!h) return;
+    try {
+        delete static_cast<IndexBase *>(h);
+    } catch (...) {
+    }
+}
+
+int hipann_set_kernel_timing(void *h, int on) {
+    try {
+        if (!h) return -1;
+        auto *ix = static_cast<IndexBase *>(h);
+        std::lock_guard<std::mutex> lk(ix->mu);
+        ix->timer_main.reset(on != 0, 0);
+        ix->timer_merge.reset(on != 0, 0);
+        return 0;
+    } catch (...) {
+        return -1;
+    }
+}
+
+double hipann_last_kernel_ms(void *h, int which) {
+    try {
+        if (!h) return 0.0;
+        auto *ix = static_cast<IndexBase *>(h);
+        std::lock_guard<std::mutex> lk(ix->mu);
+        return which == 0 ? ix->timer_main.average_ms() : ix->timer_merge.average_ms();
+    } catch (...) {
+        return 0.0;
+    }
+}
+
+}  // extern "C"

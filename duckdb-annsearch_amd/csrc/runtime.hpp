@@ -1,0 +1,210 @@
+// runtime.hpp — device buffers, per-handle streams/scratch and the index objects behind hip_ann.h.
+#pragma once
+#include "common.hpp"
+#include <memory>
+#include <mutex>
+#include <vector>
+
+namespace hipann {
+
+struct DeviceGuard {
+    int prev = 0;
+    explicit DeviceGuard(int dev) {
+        HIPANN_CHECK(hipGetDevice(&prev));
+        if (prev != dev) HIPANN_CHECK(hipSetDevice(dev));
+    }
+    ~DeviceGuard() { (void)hipSetDevice(prev); }
+};
+
+// Device allocation that grows on demand (never shrinks) — the per-handle scratch arena.
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    int device = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) { DeviceGuard g(device); (void)hipFree(p); }
+        p = nullptr;
+        bytes = 0;
+    }
+    template <typename T> T *get() const { return static_cast<T *>(p); }
+    // Grow to at least `need` bytes on `dev`.  Contents are NOT preserved.
+    void ensure(size_t need, int dev) {
+        if (need <= bytes && dev == device && p) return;
+        release();
+        device = dev;
+        DeviceGuard g(dev);
+        size_t alloc = need < 256 ? 256 : need;
+        HIPANN_CHECK(hipMalloc(&p, alloc));
+        bytes = alloc;
+    }
+};
+
+// Pinned host staging buffer.
+struct HostBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    HostBuf() = default;
+    HostBuf(const HostBuf &) = delete;
+    HostBuf &operator=(const HostBuf &) = delete;
+    ~HostBuf() { if (p) (void)hipHostFree(p); }
+    void ensure(size_t need) {
+        if (need <= bytes && p) return;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        HIPANN_CHECK(hipHostMalloc(&p, need < 256 ? 256 : need, hipHostMallocDefault));
+        bytes = need < 256 ? 256 : need;
+    }
+    template <typename T> T *get() const { return static_cast<T *>(p); }
+};
+
+// HIP-event timing of a kernel across calls (bench.py reads the average).
+struct KernelTimer {
+    bool on = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+    size_t used = 0;
+    int device = 0;
+    ~KernelTimer() { clear(); }
+    void clear() {
+        for (auto &e : ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+        ev.clear();
+        used = 0;
+    }
+    void reset(bool enable, int dev) { clear(); on = enable; device = dev; }
+    // Returns the event pair to record around a launch (nullptr pair when off).
+    std::pair<hipEvent_t, hipEvent_t> next() {
+        if (!on) return {nullptr, nullptr};
+        if (used == ev.size()) {
+            hipEvent_t a, b;
+            HIPANN_CHECK(hipEventCreate(&a));
+            HIPANN_CHECK(hipEventCreate(&b));
+            ev.push_back({a, b});
+        }
+        return ev[used++];
+    }
+    double average_ms() {
+        if (!used) return 0.0;
+        double tot = 0.0;
+        for (size_t i = 0; i < used; ++i) {
+            HIPANN_CHECK(hipEventSynchronize(ev[i].second));
+            float ms = 0.f;
+            HIPANN_CHECK(hipEventElapsedTime(&ms, ev[i].first, ev[i].second));
+            tot += ms;
+        }
+        return tot / (double)used;
+    }
+};
+
+struct ScopedTiming {
+    hipEvent_t b;
+    hipStream_t s;
+    ScopedTiming(KernelTimer &t, hipStream_t st) : s(st) {
+        auto e = t.next();
+        b = e.second;
+        if (e.first) HIPANN_CHECK(hipEventRecord(e.first, st));
+    }
+    ~ScopedTiming() { if (b) (void)hipEventRecord(b, s); }
+};
+
+enum class Kind { Flat = 1, IVF = 2 };
+
+// One contiguous row range of a Flat index resident on one device.
+struct FlatShard {
+    int device = 0;
+    int64_t n = 0, cap = 0;
+    int64_t label_offset = 0;
+    float *xb = nullptr;  // n × d fp32 (owned unless borrowed)
+    bool owns = true;
+    DevBuf xb_buf;        // owned storage
+    DevBuf xn;            // ‖x‖² (L2 only)
+    hipStream_t stream = nullptr;
+    // scratch
+    DevBuf q, qn, part_d, part_i, out_d, out_i;
+};
+
+struct IndexBase {
+    Kind kind;
+    int d = 0;
+    int metric = kL2;
+    std::mutex mu;
+    KernelTimer timer_main, timer_merge;
+    explicit IndexBase(Kind k) : kind(k) {}
+    virtual ~IndexBase() = default;
+    virtual int64_t ntotal() const = 0;
+    virtual int64_t memory_bytes() const = 0;
+};
+
+struct FlatIndex : IndexBase {
+    std::vector<std::unique_ptr<FlatShard>> shards;
+    HostBuf h_q, h_d, h_i;
+    DevBuf gather_d, gather_i, merged_d, merged_i;  // multi-device merge on shards[0]'s device
+    FlatIndex() : IndexBase(Kind::Flat) {}
+    ~FlatIndex() override;
+    int64_t ntotal() const override {
+        int64_t t = 0;
+        for (auto &s : shards) t += s->n;
+        return t;
+    }
+    int64_t memory_bytes() const override {
+        int64_t b = 0;
+        for (auto &s : shards) b += s->n * (int64_t)d * 4 + (metric == kL2 ? s->n * 4 : 0);
+        return b;
+    }
+};
+
+// IVF: CSR lists resident on one device (sharding by lists across devices: one shard per device).
+struct IvfShard {
+    int device = 0;
+    int nlist = 0;
+    int64_t n = 0;
+    DevBuf centroids;   // nlist × d
+    DevBuf cnorm;       // ‖c‖² (L2)
+    DevBuf list_off;    // int64 nlist+1 (local row offsets)
+    DevBuf list_len;    // int nlist
+    DevBuf codes;       // n × d fp32, list-contiguous
+    DevBuf ids;         // n int64 labels
+    std::vector<int64_t> h_off;
+    std::vector<uint8_t> owned;  // per list: 1 if this shard scans it
+    hipStream_t stream = nullptr;
+    // scratch
+    DevBuf q, qn, coarse_d, coarse_i, probes, work, work_cnt, part_d, part_i, out_d, out_i;
+};
+
+struct IvfIndex : IndexBase {
+    int nlist = 0, nprobe = 1;
+    std::vector<std::unique_ptr<IvfShard>> shards;
+    std::vector<int64_t> last_probes;
+    int64_t last_nq = 0;
+    HostBuf h_q, h_d, h_i;
+    DevBuf gather_d, gather_i, merged_d, merged_i;
+    IvfIndex() : IndexBase(Kind::IVF) {}
+    ~IvfIndex() override;
+    int64_t ntotal() const override {
+        int64_t t = 0;
+        for (auto &s : shards) t += s->n;
+        return t;
+    }
+    int64_t memory_bytes() const override {
+        int64_t b = 0;
+        for (auto &s : shards) b += s->n * ((int64_t)d * 4 + 8) + (int64_t)nlist * d * 4;
+        return b;
+    }
+};
+
+// ---- kernel launchers (flat_kernels.hip, ivf_kernels.hip) ----
+void launch_row_norms(const float *x, int64_t n, int d, float *out, hipStream_t st);
+size_t gemm_smem_bytes();
+void launch_flat_gemm_topk(const float *Q, const float *qn, int64_t nq, const float *X, const float *xn, int64_t N,
+                           int d, int metric, int k, int nsplit, int64_t tiles_per_split, float *pd, int *pi,
+                           hipStream_t st);
+size_t scan_smem_bytes(int nq, int d);
+void launch_flat_scan_topk(const float *Q, int nq, const float *X, int64_t N, int d, int metric, int k, int nwaves,
+                           int64_t rows_per_wave, float *pd, int *pi, hipStream_t st);
+template <typename InId>
+void launch_merge_parts(const float *pd, const InId *pi, int nparts, int64_t nq, int k, int kout,
+                        int64_t label_offset, float in_sign, float out_sign, float *D, int64_t *I, hipStream_t st);
+
+}  // namespace hipann

@@ -1,0 +1,141 @@
+// wave_topk.hpp — wave64-distributed sorted top-k lists for CDNA4 (gfx950).
+//
+// A list of up to 64*S (key, id) pairs lives in S registers pairs of ONE wavefront: element
+// e = s*64 + lane sits in slot s of lane `lane`.  The list is kept sorted ascending by the
+// lexicographic order (key, id).  Selecting the k smallest pairs of a candidate stream by that
+// order is exactly FAISS's result: its heaps admit a candidate only when it is strictly better than
+// the current worst and break equal distances by label (faiss::CMax::cmp2 / heap_reorder), and the
+// extension's Metal selects keep "earlier index wins" on ties (warp_select.metal:37-58).  Because
+// the lexicographic top-k of a multiset does not depend on arrival order, partial lists computed by
+// different waves / blocks / GPUs merge exactly.
+//
+// Insert cost: one ballot + one popcount + one shuffle per slot — no per-lane serial loop.
+// Candidates are filtered with a wave-uniform threshold (element k-1) first, so after warm-up
+// almost no candidate reaches the insert.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hipann {
+
+constexpr int kWave = 64;
+
+template <typename IdT>
+__device__ __forceinline__ bool lex_less(float ad, IdT aid, float bd, IdT bid) {
+    return ad < bd || (ad == bd && aid < bid);
+}
+
+template <typename IdT> struct IdTraits;
+template <> struct IdTraits<int> {
+    static __device__ __forceinline__ int pad() { return 0x7fffffff; }
+};
+template <> struct IdTraits<long long> {
+    static __device__ __forceinline__ long long pad() { return 0x7fffffffffffffffLL; }
+};
+
+__device__ __forceinline__ float readlane_f(float v, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+__device__ __forceinline__ int readlane_i(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+__device__ __forceinline__ long long readlane_i(long long v, int lane) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v & 0xffffffffLL), lane);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)((unsigned long long)v >> 32), lane);
+    return (long long)(((unsigned long long)hi << 32) | lo);
+}
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+// Shift-up by one lane across the wave (lane 0 receives garbage; callers overwrite it).
+__device__ __forceinline__ float shfl_up1_f(float v) {
+    return __int_as_float(__builtin_amdgcn_ds_bpermute((int)((lane_id() - 1) & 63) << 2, __float_as_int(v)));
+}
+__device__ __forceinline__ int shfl_up1_i(int v) {
+    return __builtin_amdgcn_ds_bpermute((int)((lane_id() - 1) & 63) << 2, v);
+}
+__device__ __forceinline__ long long shfl_up1_i(long long v) {
+    const int a = (int)((lane_id() - 1) & 63) << 2;
+    const unsigned lo = (unsigned)__builtin_amdgcn_ds_bpermute(a, (int)(unsigned)(v & 0xffffffffLL));
+    const unsigned hi = (unsigned)__builtin_amdgcn_ds_bpermute(a, (int)(unsigned)((unsigned long long)v >> 32));
+    return (long long)(((unsigned long long)hi << 32) | lo);
+}
+
+// One wave-distributed list of 64*S elements.
+template <int S, typename IdT = int>
+struct WaveList {
+    float d[S];
+    IdT id[S];
+
+    __device__ __forceinline__ void init() {
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            d[s] = __builtin_inff();
+            id[s] = IdTraits<IdT>::pad();
+        }
+    }
+
+    // Threshold = element kth (0-based, wave-uniform, kth < 64*S).
+    __device__ __forceinline__ void threshold(int kth, float &td, IdT &tid) const {
+        const int s = kth >> 6, l = kth & 63;
+        float v = d[0];
+        IdT vi = id[0];
+#pragma unroll
+        for (int t = 1; t < S; ++t)
+            if (s == t) { v = d[t]; vi = id[t]; }
+        td = readlane_f(v, l);
+        tid = readlane_i(vi, l);
+    }
+
+    // Insert a wave-uniform candidate (cd, cid).  Elements pushed past 64*S are dropped.
+    __device__ __forceinline__ void insert(float cd, IdT cid) {
+        const int lane = lane_id();
+        int pos = 0;
+#pragma unroll
+        for (int s = 0; s < S; ++s) pos += __popcll(__ballot(lex_less(d[s], id[s], cd, cid)));
+#pragma unroll
+        for (int s = S - 1; s >= 0; --s) {
+            float ud = shfl_up1_f(d[s]);
+            IdT uid = shfl_up1_i(id[s]);
+            if (s > 0) {
+                // lane 0 of slot s receives lane 63 of slot s-1 (still unmodified: we go high→low)
+                float cd63 = readlane_f(d[s - 1], 63);
+                IdT ci63 = readlane_i(id[s - 1], 63);
+                if (lane == 0) { ud = cd63; uid = ci63; }
+            }
+            const int e = s * 64 + lane;
+            if (e == pos) { d[s] = cd; id[s] = cid; }
+            else if (e > pos) { d[s] = ud; id[s] = uid; }
+        }
+    }
+
+    // Offer 64 per-lane candidates (one per lane, any order).  `kth` = k-1.  Candidates whose key is
+    // +inf with the padding id never enter.
+    __device__ __forceinline__ void offer(float cd, IdT cid, int kth) {
+        float td; IdT tid;
+        threshold(kth, td, tid);
+        bool pass = lex_less(cd, cid, td, tid);
+        unsigned long long m = __ballot(pass);
+        while (m) {
+            const int j = __ffsll((unsigned long long)m) - 1;
+            m &= m - 1;
+            const float xd = readlane_f(cd, j);
+            const IdT xi = readlane_i(cid, j);
+            // re-check against the current threshold (it tightens as we insert)
+            float t2d; IdT t2i;
+            threshold(kth, t2d, t2i);
+            if (lex_less(xd, xi, t2d, t2i)) insert(xd, xi);
+        }
+    }
+
+    // Write elements [0, k) to out_d / out_i (lane-strided, coalesced).
+    template <typename IdxT>
+    __device__ __forceinline__ void store(float *out_d, IdxT *out_i, int k) const {
+        const int lane = lane_id();
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const int e = s * 64 + lane;
+            if (e < k) { out_d[e] = d[s]; out_i[e] = (IdxT)id[s]; }
+        }
+    }
+};
+
+}  // namespace hipann

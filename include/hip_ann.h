@@ -1,0 +1,142 @@
+/*
+ * hip_ann.h — C ABI of the MI355X search backend for the DuckDB `ann` extension's FAISS indexes.
+ *
+ * This is the plain-C layer that sits UNDER the extension's `GpuBackend` interface
+ * (reference: src/include/gpu_backend.hpp:12-33).  The reference implements that interface with
+ * faiss-metal (`MetalGpuBackend::CpuToGpu`, src/gpu_backend_metal.mm:42-60), which deep-copies a
+ * FAISS `IndexFlat` / `IndexIVFFlat` into a `faiss::Index` subclass whose `search()` runs on the GPU
+ * (faiss-metal/src/MetalIndexFlat.mm:294-369, faiss-metal/src/MetalIndexIVFFlat.mm:122-256).
+ * Here the GPU index is an opaque handle behind these entry points; the C++ adapter
+ * `duckdb-annsearch_amd/adapters/gpu_backend_hip.cpp` wraps them into `faiss::Index` subclasses.
+ *
+ * Conventions (mirroring the extension's Rust FFI, rust_lib/src/ffi.rs:14-23):
+ *   - every fallible call takes `char *err_buf, int err_len`; on failure it writes a NUL-terminated
+ *     message there (when err_buf != NULL) and returns -1 (int) or NULL (handle);
+ *   - the caller owns every host buffer; the library copies at create time and writes the outputs
+ *     synchronously before returning (host-pointer API);
+ *   - handles are opaque; hipann_free(NULL) is a no-op; a handle serialises its own calls with a
+ *     mutex (one HIP stream + scratch arena per handle), so concurrent DuckDB connections are safe;
+ *   - metric: 0 = L2 (squared Euclidean, ascending), 1 = inner product (raw dot, descending) —
+ *     faiss::MetricType values METRIC_INNER_PRODUCT=0 / METRIC_L2=1 are NOT used here; see HIPANN_*;
+ *   - search outputs follow MetalIndexFlat::search (MetalIndexFlat.mm:294-369): D is nq*k floats,
+ *     I is nq*k int64 labels; slots beyond min(k, ntotal) hold (+inf | -inf, -1); k <= 0 is an error;
+ *     equal distances are ordered by ascending label (FAISS heap id tie-break).
+ *
+ * There is no CPU implementation behind this ABI: without a HIP device every compute entry point
+ * fails with -1 ("no HIP device").  The CPU path is the extension's own FAISS CPU index.
+ */
+#ifndef HIP_ANN_H
+#define HIP_ANN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HIPANN_METRIC_L2 0
+#define HIPANN_METRIC_IP 1
+
+/* Largest k the GPU path serves (faiss-metal's block select tops out at 2048, MetalSelect.mm:53-57). */
+#define HIPANN_MAX_K 2048
+
+/* 1 when at least one gfx950 HIP device is usable, else 0.  Replaces
+ * MetalGpuBackend::IsAvailable (gpu_backend_metal.mm:20-31, :33-35). */
+int hipann_available(void);
+
+/* Number of visible HIP devices (0 without a GPU). */
+int hipann_device_count(void);
+
+/* Human-readable device description, e.g. "AMD Instinct MI355X (gfx950, 256 CUs, 288 GB) x8".
+ * Replaces MetalGpuBackend::DeviceInfo (gpu_backend_metal.mm:37-43) → faiss_gpu_info().device
+ * (src/faiss_fn_gpu.cpp:42-45).  Returns the string length, or -1. */
+int hipann_device_info(char *buf, int buf_len);
+
+/* ---------------------------------------------------------------------------------------------
+ * Flat (brute force) — replaces index_cpu_to_metal + MetalIndexFlat (MetalIndexFlat.mm:504-515,
+ * :173-292 add, :294-369 search).
+ * ------------------------------------------------------------------------------------------- */
+
+/* Create a Flat index over n row-major fp32 vectors `xb` (n*d floats, host memory).  Rows are
+ * sharded contiguously over `devices[0..ndev)` (NULL/0 = device 0); labels are 0..n-1. */
+void *hipann_flat_create(int d, int metric, const float *xb, int64_t n, const int *devices, int ndev,
+                         char *err_buf, int err_len);
+
+/* Append n more vectors (labels continue from ntotal) — MetalIndexFlat::add (MetalIndexFlat.mm:173-292). */
+int hipann_flat_add(void *index, const float *xb, int64_t n, char *err_buf, int err_len);
+
+/* Search nq queries `xq` (nq*d floats, host).  D: nq*k floats, I: nq*k int64 (host). */
+int hipann_flat_search(void *index, int64_t nq, const float *xq, int64_t k, float *D, int64_t *I,
+                       char *err_buf, int err_len);
+
+/* Copy vector `key` back to host (faiss::Index::reconstruct; MetalIndexFlat::reconstruct). */
+int hipann_flat_reconstruct(void *index, int64_t key, float *out, char *err_buf, int err_len);
+
+/* ---------------------------------------------------------------------------------------------
+ * Device-resident variants (inputs and outputs already in HBM).  Used by the multi-GPU sharded
+ * search (one process per GPU, partial top-k gathered over RCCL) and by bench.py, whose timed
+ * region starts with the inputs resident.  `stream` is a hipStream_t (NULL = the handle's stream);
+ * the call is asynchronous on that stream.
+ * ------------------------------------------------------------------------------------------- */
+
+/* Wrap (copy=0: borrow, caller keeps it alive) or copy (copy=1) an HBM matrix of n*d fp32 on
+ * `device`.  Labels are label_offset + row. */
+void *hipann_flat_create_device(int d, int metric, const float *xb_dev, int64_t n, int device, int copy,
+                                int64_t label_offset, char *err_buf, int err_len);
+
+int hipann_flat_search_device(void *index, int64_t nq, const float *xq_dev, int64_t k, float *D_dev,
+                              int64_t *I_dev, void *stream, char *err_buf, int err_len);
+
+/* k-way merge of `nparts` partial results laid out [part][nq][k] (device memory) into [nq][k]:
+ * the k best by (distance, label) — ascending for L2, descending for IP; -1 labels are ignored.
+ * The merge step after the RCCL allgather of per-GPU partial top-k. */
+int hipann_merge_topk_device(int metric, int nparts, int64_t nq, int64_t k, const float *D_parts,
+                             const int64_t *I_parts, float *D_out, int64_t *I_out, void *stream,
+                             char *err_buf, int err_len);
+
+/* ---------------------------------------------------------------------------------------------
+ * IVFFlat — replaces index_cpu_to_metal_ivf + MetalIndexIVFFlat (MetalIndexIVFFlat.mm:283-326,
+ * :122-256).  Lists are given in CSR form exactly as FAISS's ArrayInvertedLists hold them:
+ * list l owns rows [list_offsets[l], list_offsets[l+1]) of `codes` (raw fp32 vectors — IVFFlat
+ * stores unresidualised codes) and of `ids` (int64 labels).
+ * ------------------------------------------------------------------------------------------- */
+
+void *hipann_ivf_create(int d, int metric, int nlist, int nprobe, const float *centroids,
+                        const int64_t *list_offsets, const int64_t *ids, const float *codes,
+                        const int *devices, int ndev, char *err_buf, int err_len);
+
+int hipann_ivf_search(void *index, int64_t nq, const float *xq, int64_t k, float *D, int64_t *I,
+                      char *err_buf, int err_len);
+
+int hipann_ivf_search_device(void *index, int64_t nq, const float *xq_dev, int64_t k, float *D_dev,
+                             int64_t *I_dev, void *stream, char *err_buf, int err_len);
+
+/* Probe lists chosen by the last search (nq*nprobe int64, host) — for parity tests. */
+int hipann_ivf_last_probes(void *index, int64_t *probes, int64_t cap, char *err_buf, int err_len);
+
+int hipann_ivf_set_nprobe(void *index, int nprobe);
+
+/* ---------------------------------------------------------------------------------------------
+ * Common
+ * ------------------------------------------------------------------------------------------- */
+
+int64_t hipann_ntotal(void *index);
+int hipann_dim(void *index);
+int hipann_metric(void *index);
+/* Bytes of HBM held by the index (vectors + norms + lists). */
+int64_t hipann_memory_bytes(void *index);
+void hipann_free(void *index);
+
+/* Enable (1) / disable (0) HIP-event timing of the kernels inside each search call. */
+int hipann_set_kernel_timing(void *index, int on);
+
+/* Average device time (ms) of the dominant kernel over the last `hipann_*_search*` call, measured
+ * with HIP events on the handle's stream (0 if unknown).  `which`: 0 = main scan/GEMM kernel,
+ * 1 = merge kernel.  Used by bench.py for the roofline line. */
+double hipann_last_kernel_ms(void *index, int which);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HIP_ANN_H */
