@@ -1,0 +1,397 @@
+// ivf.cpp — IVFFlat part of the C ABI (include/hip_ann.h).
+//
+// Mirrors index_cpu_to_metal_ivf (faiss-metal/src/MetalIndexIVFFlat.mm:283-326: centroids, per-list
+// ids and raw fp32 codes copied out of a FAISS IndexIVFFlat; nprobe taken from the CPU index) and
+// MetalIndexIVFFlat::search (:122-256: k <= 0 throws, empty → (±inf, −1) pads, ids remapped to the
+// stored labels).  The parity target is FAISS CPU IndexIVFFlat::search: coarse search
+// with nprobe = min(nprobe, nlist), lists scanned with direct distances.
+#include "../../include/hip_ann.h"
+#include "ivf.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <numeric>
+
+using namespace hipann;
+
+namespace {
+
+void set_err(char *buf, int len, const char *msg) {
+    if (!buf || len <= 0) return;
+    std::strncpy(buf, msg, (size_t)len - 1);
+    buf[len - 1] = '\0';
+}
+
+template <typename F>
+int guard_int(char *eb, int el, F &&f) {
+    try {
+        return f();
+    } catch (const std::exception &e) {
+        set_err(eb, el, e.what());
+    } catch (...) {
+        set_err(eb, el, "hipann: unknown error");
+    }
+    return -1;
+}
+
+template <typename F>
+void *guard_ptr(char *eb, int el, F &&f) {
+    try {
+        return f();
+    } catch (const std::exception &e) {
+        set_err(eb, el, e.what());
+    } catch (...) {
+        set_err(eb, el, "hipann: unknown error");
+    }
+    return nullptr;
+}
+
+hipStream_t make_stream(int dev) {
+    DeviceGuard g(dev);
+    hipStream_t s;
+    HIPANN_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    return s;
+}
+
+// Borrowed-centroid coarse quantizer on the shard's device.
+std::unique_ptr<FlatIndex> make_quantizer(int d, int metric, const float *cen, int nlist, int device,
+                                          hipStream_t stream) {
+    auto q = std::make_unique<FlatIndex>();
+    q->d = d;
+    q->metric = metric;
+    auto sh = std::make_unique<FlatShard>();
+    sh->device = device;
+    sh->stream = nullptr;  // searches run on the IVF shard's stream
+    sh->xb = const_cast<float *>(cen);
+    sh->owns = false;
+    sh->n = nlist;
+    sh->cap = nlist;
+    if (metric == kL2) {
+        DeviceGuard g(device);
+        sh->xn.ensure((size_t)nlist * sizeof(float), device);
+        launch_row_norms(cen, nlist, d, sh->xn.get<float>(), stream);
+        HIPANN_CHECK(hipStreamSynchronize(stream));
+    }
+    q->shards.push_back(std::move(sh));
+    return q;
+}
+
+void upload_list_meta(IvfShard &sh, const std::vector<int64_t> &off, int nlist) {
+    DeviceGuard g(sh.device);
+    std::vector<int> len(nlist);
+    for (int l = 0; l < nlist; ++l) len[l] = (int)(off[l + 1] - off[l]);
+    sh.list_off.ensure(sizeof(int64_t) * (nlist + 1), sh.device);
+    sh.list_len.ensure(sizeof(int) * nlist, sh.device);
+    HIPANN_CHECK(hipMemcpyAsync(sh.list_off.p, off.data(), sizeof(int64_t) * (nlist + 1), hipMemcpyHostToDevice,
+                                sh.stream));
+    HIPANN_CHECK(hipMemcpyAsync(sh.list_len.p, len.data(), sizeof(int) * nlist, hipMemcpyHostToDevice, sh.stream));
+    HIPANN_CHECK(hipStreamSynchronize(sh.stream));
+}
+
+}  // namespace
+
+namespace hipann {
+
+IvfIndex::~IvfIndex() {
+    for (auto &s : shards) {
+        s->quant.reset();
+        if (s->stream) { DeviceGuard g(s->device); (void)hipStreamDestroy(s->stream); }
+    }
+}
+
+// One shard: queries on the shard's device → D/I (nq × kout) on the same device, async on `st`.
+void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, int k, int kout, float *D, int64_t *I,
+                      hipStream_t st) {
+    DeviceGuard g(sh.device);
+    const int nlist = ix.nlist, d = ix.d, metric = ix.metric;
+    const int np = std::min(ix.nprobe, nlist);
+    const float out_sign = metric == kIP ? -1.f : 1.f;
+    HIPANN_REQUIRE(k <= 64, "k > 64 is not supported by the fused GPU path yet");
+    HIPANN_REQUIRE(np <= 64, "nprobe > 64 is not supported by the GPU coarse quantizer yet");
+    if (nq <= 0) return;
+    // 1. coarse quantizer (FAISS: quantizer->search(n, x, nprobe) — Flat rules incl. nq < 20)
+    sh.coarse_d.ensure((size_t)nq * np * sizeof(float), sh.device);
+    sh.coarse_i.ensure((size_t)nq * np * sizeof(int64_t), sh.device);
+    flat_shard_search(*sh.quant, *sh.quant->shards[0], nq, xq, np, np, sh.coarse_d.get<float>(),
+                      sh.coarse_i.get<int64_t>(), st);
+    // 2. list-major work plan
+    sh.cnt.ensure(sizeof(int) * (nlist + 1), sh.device);
+    sh.bucket_off.ensure(sizeof(int) * (nlist + 1), sh.device);
+    sh.item_off.ensure(sizeof(int) * (nlist + 1), sh.device);
+    sh.cursor.ensure(sizeof(int) * (nlist + 1), sh.device);
+    sh.bucket.ensure(sizeof(int) * (size_t)nq * np, sh.device);
+    HIPANN_REQUIRE((int64_t)nq * np < (int64_t)0x7fffffff, "nq * nprobe too large");
+    launch_ivf_plan(sh.coarse_i.get<int64_t>(), nq, np, sh.list_len.get<int>(), nlist, sh.cnt.get<int>(),
+                    sh.bucket_off.get<int>(), sh.item_off.get<int>(), sh.cursor.get<int>(), sh.bucket.get<int>(), st);
+    // 3. scan
+    const size_t parts = (size_t)np * nq * k;
+    sh.part_d.ensure(parts * sizeof(float), sh.device);
+    sh.part_i.ensure(parts * sizeof(int), sh.device);
+    HIPANN_CHECK(hipMemsetAsync(sh.part_i.p, 0xff, parts * sizeof(int), st));
+    const int64_t max_items = ivf_max_items(nq, np, nlist);
+    {
+        ScopedTiming t(ix.timer_main, st);
+        launch_ivf_scan(xq, d, metric, sh.codes, sh.list_off.get<int64_t>(), sh.cnt.get<int>(),
+                        sh.bucket_off.get<int>(), sh.item_off.get<int>(), sh.bucket.get<int>(), nlist, np, nq, k,
+                        max_items, sh.part_d.get<float>(), sh.part_i.get<int>(), st);
+    }
+    // 4. merge the nprobe partial lists per query
+    ScopedTiming t(ix.timer_merge, st);
+    launch_ivf_merge(sh.part_d.get<float>(), sh.part_i.get<int>(), sh.ids, np, nq, k, kout, out_sign, D, I, st);
+}
+
+}  // namespace hipann
+
+extern "C" {
+
+void *hipann_ivf_create(int d, int metric, int nlist, int nprobe, const float *centroids, const int64_t *list_offsets,
+                        const int64_t *ids, const float *codes, const int *devices, int ndev, char *eb, int el) {
+    return guard_ptr(eb, el, [&]() -> void * {
+        int ndevs = 0;
+        if (hipGetDeviceCount(&ndevs) != hipSuccess || ndevs <= 0) throw HipError("hipann: no HIP device");
+        HIPANN_REQUIRE(d > 0 && nlist > 0, "d and nlist must be > 0");
+        HIPANN_REQUIRE(metric == kL2 || metric == kIP, "metric must be 0 (L2) or 1 (IP)");
+        HIPANN_REQUIRE(nprobe >= 1, "nprobe must be >= 1");
+        HIPANN_REQUIRE(centroids && list_offsets, "null centroids / offsets");
+        std::vector<int> devs;
+        if (!devices || ndev <= 0) devs.push_back(0);
+        else devs.assign(devices, devices + ndev);
+        for (int dv : devs) HIPANN_REQUIRE(dv >= 0 && dv < ndevs, "invalid device id");
+        const int64_t n = list_offsets[nlist];
+        HIPANN_REQUIRE(list_offsets[0] == 0 && n >= 0, "list offsets must start at 0");
+        for (int l = 0; l < nlist; ++l) HIPANN_REQUIRE(list_offsets[l + 1] >= list_offsets[l], "offsets not monotone");
+        HIPANN_REQUIRE(n == 0 || (ids && codes), "null ids / codes");
+
+        auto ix = std::make_unique<IvfIndex>();
+        ix->d = d;
+        ix->metric = metric;
+        ix->nlist = nlist;
+        ix->nprobe = nprobe;
+        // size-balanced list → shard assignment (largest first onto the least-loaded shard)
+        const int ns = (int)devs.size();
+        std::vector<int> owner(nlist, 0);
+        if (ns > 1) {
+            std::vector<int> order(nlist);
+            std::iota(order.begin(), order.end(), 0);
+            std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+                return list_offsets[a + 1] - list_offsets[a] > list_offsets[b + 1] - list_offsets[b];
+            });
+            std::vector<int64_t> load(ns, 0);
+            for (int l : order) {
+                const int s = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+                owner[l] = s;
+                load[s] += list_offsets[l + 1] - list_offsets[l];
+            }
+        }
+        for (int s = 0; s < ns; ++s) {
+            auto sh = std::make_unique<IvfShard>();
+            sh->device = devs[s];
+            sh->stream = make_stream(devs[s]);
+            DeviceGuard g(sh->device);
+            std::vector<int64_t> off(nlist + 1, 0);
+            for (int l = 0; l < nlist; ++l)
+                off[l + 1] = off[l] + (owner[l] == s ? list_offsets[l + 1] - list_offsets[l] : 0);
+            sh->n = off[nlist];
+            sh->centroids_buf.ensure(sizeof(float) * (size_t)nlist * d, sh->device);
+            HIPANN_CHECK(hipMemcpyAsync(sh->centroids_buf.p, centroids, sizeof(float) * (size_t)nlist * d,
+                                        hipMemcpyHostToDevice, sh->stream));
+            sh->centroids = sh->centroids_buf.get<float>();
+            sh->codes_buf.ensure(sizeof(float) * (size_t)std::max<int64_t>(sh->n, 1) * d, sh->device);
+            sh->ids_buf.ensure(sizeof(int64_t) * (size_t)std::max<int64_t>(sh->n, 1), sh->device);
+            for (int l = 0; l < nlist; ++l) {
+                if (owner[l] != s) continue;
+                const int64_t cnt = list_offsets[l + 1] - list_offsets[l];
+                if (!cnt) continue;
+                HIPANN_CHECK(hipMemcpyAsync(sh->codes_buf.get<float>() + off[l] * d, codes + list_offsets[l] * d,
+                                            sizeof(float) * (size_t)cnt * d, hipMemcpyHostToDevice, sh->stream));
+                HIPANN_CHECK(hipMemcpyAsync(sh->ids_buf.get<int64_t>() + off[l], ids + list_offsets[l],
+                                            sizeof(int64_t) * (size_t)cnt, hipMemcpyHostToDevice, sh->stream));
+            }
+            sh->codes = sh->codes_buf.get<float>();
+            sh->ids = sh->ids_buf.get<int64_t>();
+            HIPANN_CHECK(hipStreamSynchronize(sh->stream));
+            upload_list_meta(*sh, off, nlist);
+            sh->quant = make_quantizer(d, metric, sh->centroids, nlist, sh->device, sh->stream);
+            ix->shards.push_back(std::move(sh));
+        }
+        return ix.release();
+    });
+}
+
+void *hipann_ivf_create_device(int d, int metric, int nlist, int nprobe, const float *centroids_dev,
+                               const int64_t *list_offsets, const int64_t *ids_dev, const float *codes_dev, int device,
+                               int copy, char *eb, int el) {
+    return guard_ptr(eb, el, [&]() -> void * {
+        int ndevs = 0;
+        if (hipGetDeviceCount(&ndevs) != hipSuccess || ndevs <= 0) throw HipError("hipann: no HIP device");
+        HIPANN_REQUIRE(device >= 0 && device < ndevs, "invalid device");
+        HIPANN_REQUIRE(d > 0 && nlist > 0 && nprobe >= 1, "bad arguments");
+        HIPANN_REQUIRE(metric == kL2 || metric == kIP, "metric must be 0 (L2) or 1 (IP)");
+        HIPANN_REQUIRE(centroids_dev && list_offsets, "null centroids / offsets");
+        const int64_t n = list_offsets[nlist];
+        HIPANN_REQUIRE(list_offsets[0] == 0 && n >= 0, "list offsets must start at 0");
+        HIPANN_REQUIRE(n == 0 || (ids_dev && codes_dev), "null ids / codes");
+        auto ix = std::make_unique<IvfIndex>();
+        ix->d = d;
+        ix->metric = metric;
+        ix->nlist = nlist;
+        ix->nprobe = nprobe;
+        auto sh = std::make_unique<IvfShard>();
+        sh->device = device;
+        sh->stream = make_stream(device);
+        sh->n = n;
+        DeviceGuard g(device);
+        if (copy) {
+            sh->centroids_buf.ensure(sizeof(float) * (size_t)nlist * d, device);
+            sh->codes_buf.ensure(sizeof(float) * (size_t)std::max<int64_t>(n, 1) * d, device);
+            sh->ids_buf.ensure(sizeof(int64_t) * (size_t)std::max<int64_t>(n, 1), device);
+            HIPANN_CHECK(hipMemcpyAsync(sh->centroids_buf.p, centroids_dev, sizeof(float) * (size_t)nlist * d,
+                                        hipMemcpyDeviceToDevice, sh->stream));
+            if (n) {
+                HIPANN_CHECK(hipMemcpyAsync(sh->codes_buf.p, codes_dev, sizeof(float) * (size_t)n * d,
+                                            hipMemcpyDeviceToDevice, sh->stream));
+                HIPANN_CHECK(hipMemcpyAsync(sh->ids_buf.p, ids_dev, sizeof(int64_t) * (size_t)n,
+                                            hipMemcpyDeviceToDevice, sh->stream));
+            }
+            sh->centroids = sh->centroids_buf.get<float>();
+            sh->codes = sh->codes_buf.get<float>();
+            sh->ids = sh->ids_buf.get<int64_t>();
+        } else {
+            sh->centroids = centroids_dev;
+            sh->codes = codes_dev;
+            sh->ids = ids_dev;
+        }
+        std::vector<int64_t> off(list_offsets, list_offsets + nlist + 1);
+        upload_list_meta(*sh, off, nlist);
+        sh->quant = make_quantizer(d, metric, sh->centroids, nlist, device, sh->stream);
+        ix->shards.push_back(std::move(sh));
+        return ix.release();
+    });
+}
+
+static int ivf_search_host(IvfIndex &ix, int64_t nq, const float *xq, int64_t k, float *D, int64_t *I) {
+    HIPANN_REQUIRE(k > 0, "k must be > 0");
+    HIPANN_REQUIRE(k <= HIPANN_MAX_K, "k larger than HIPANN_MAX_K");
+    HIPANN_REQUIRE(nq >= 0 && (nq == 0 || (xq && D && I)), "invalid arguments");
+    const float pad = ix.metric == kIP ? -__builtin_inff() : __builtin_inff();
+    const int64_t ntot = ix.ntotal();
+    ix.last_nq = nq;
+    ix.last_np = std::min(ix.nprobe, ix.nlist);
+    if (nq == 0) return 0;
+    if (ntot == 0) {
+        for (int64_t i = 0; i < nq * k; ++i) { D[i] = pad; I[i] = -1; }
+        return 0;
+    }
+    const int keff = (int)std::min<int64_t>(k, ntot);
+    const int kout = (int)k;
+    const size_t qbytes = (size_t)nq * ix.d * sizeof(float);
+    ix.h_q.ensure(qbytes);
+    std::memcpy(ix.h_q.p, xq, qbytes);
+    const size_t ob = (size_t)nq * kout;
+    for (auto &shp : ix.shards) {
+        IvfShard &sh = *shp;
+        DeviceGuard g(sh.device);
+        sh.q.ensure(qbytes, sh.device);
+        sh.out_d.ensure(ob * sizeof(float), sh.device);
+        sh.out_i.ensure(ob * sizeof(int64_t), sh.device);
+        HIPANN_CHECK(hipMemcpyAsync(sh.q.p, ix.h_q.p, qbytes, hipMemcpyHostToDevice, sh.stream));
+        ivf_shard_search(ix, sh, nq, sh.q.get<float>(), keff, kout, sh.out_d.get<float>(), sh.out_i.get<int64_t>(),
+                         sh.stream);
+    }
+    ix.h_d.ensure(ob * sizeof(float));
+    ix.h_i.ensure(ob * sizeof(int64_t));
+    IvfShard &s0 = *ix.shards[0];
+    if (ix.shards.size() == 1) {
+        DeviceGuard g(s0.device);
+        HIPANN_CHECK(hipMemcpyAsync(ix.h_d.p, s0.out_d.p, ob * sizeof(float), hipMemcpyDeviceToHost, s0.stream));
+        HIPANN_CHECK(hipMemcpyAsync(ix.h_i.p, s0.out_i.p, ob * sizeof(int64_t), hipMemcpyDeviceToHost, s0.stream));
+        HIPANN_CHECK(hipStreamSynchronize(s0.stream));
+    } else {
+        const int np = (int)ix.shards.size();
+        ix.gather_d.ensure(ob * np * sizeof(float), s0.device);
+        ix.gather_i.ensure(ob * np * sizeof(int64_t), s0.device);
+        ix.merged_d.ensure(ob * sizeof(float), s0.device);
+        ix.merged_i.ensure(ob * sizeof(int64_t), s0.device);
+        for (int p = 0; p < np; ++p) {
+            IvfShard &sh = *ix.shards[p];
+            DeviceGuard g(sh.device);
+            HIPANN_CHECK(hipStreamSynchronize(sh.stream));
+            HIPANN_CHECK(hipMemcpyPeerAsync(ix.gather_d.get<float>() + p * ob, s0.device, sh.out_d.p, sh.device,
+                                            ob * sizeof(float), s0.stream));
+            HIPANN_CHECK(hipMemcpyPeerAsync(ix.gather_i.get<int64_t>() + p * ob, s0.device, sh.out_i.p, sh.device,
+                                            ob * sizeof(int64_t), s0.stream));
+        }
+        DeviceGuard g(s0.device);
+        const float sign = ix.metric == kIP ? -1.f : 1.f;
+        launch_merge_parts<long long>(ix.gather_d.get<float>(), ix.gather_i.get<long long>(), np, nq, kout, kout, 0,
+                                      sign, sign, ix.merged_d.get<float>(), ix.merged_i.get<int64_t>(), s0.stream);
+        HIPANN_CHECK(hipMemcpyAsync(ix.h_d.p, ix.merged_d.p, ob * sizeof(float), hipMemcpyDeviceToHost, s0.stream));
+        HIPANN_CHECK(hipMemcpyAsync(ix.h_i.p, ix.merged_i.p, ob * sizeof(int64_t), hipMemcpyDeviceToHost, s0.stream));
+        HIPANN_CHECK(hipStreamSynchronize(s0.stream));
+    }
+    std::memcpy(D, ix.h_d.p, ob * sizeof(float));
+    std::memcpy(I, ix.h_i.p, ob * sizeof(int64_t));
+    return 0;
+}
+
+int hipann_ivf_search(void *h, int64_t nq, const float *xq, int64_t k, float *D, int64_t *I, char *eb, int el) {
+    return guard_int(eb, el, [&]() -> int {
+        HIPANN_REQUIRE(h, "null index");
+        auto *ix = static_cast<IndexBase *>(h);
+        HIPANN_REQUIRE(ix->kind == Kind::IVF, "not an IVFFlat index");
+        auto *vx = static_cast<IvfIndex *>(ix);
+        std::lock_guard<std::mutex> lk(vx->mu);
+        return ivf_search_host(*vx, nq, xq, k, D, I);
+    });
+}
+
+int hipann_ivf_search_device(void *h, int64_t nq, const float *xq_dev, int64_t k, float *D_dev, int64_t *I_dev,
+                             void *stream, char *eb, int el) {
+    return guard_int(eb, el, [&]() -> int {
+        HIPANN_REQUIRE(h, "null index");
+        auto *ix = static_cast<IndexBase *>(h);
+        HIPANN_REQUIRE(ix->kind == Kind::IVF, "not an IVFFlat index");
+        auto *vx = static_cast<IvfIndex *>(ix);
+        std::lock_guard<std::mutex> lk(vx->mu);
+        HIPANN_REQUIRE(vx->shards.size() == 1, "device search needs a single-device index");
+        HIPANN_REQUIRE(k > 0 && k <= HIPANN_MAX_K, "k out of range");
+        IvfShard &sh = *vx->shards[0];
+        hipStream_t st = stream ? static_cast<hipStream_t>(stream) : sh.stream;
+        vx->last_nq = nq;
+        vx->last_np = std::min(vx->nprobe, vx->nlist);
+        const int keff = (int)std::min<int64_t>(k, std::max<int64_t>(sh.n, 1));
+        ivf_shard_search(*vx, sh, nq, xq_dev, keff, (int)k, D_dev, I_dev, st);
+        return 0;
+    });
+}
+
+int hipann_ivf_last_probes(void *h, int64_t *probes, int64_t cap, char *eb, int el) {
+    return guard_int(eb, el, [&]() -> int {
+        HIPANN_REQUIRE(h && probes, "null argument");
+        auto *ix = static_cast<IndexBase *>(h);
+        HIPANN_REQUIRE(ix->kind == Kind::IVF, "not an IVFFlat index");
+        auto *vx = static_cast<IvfIndex *>(ix);
+        std::lock_guard<std::mutex> lk(vx->mu);
+        const int64_t m = vx->last_nq * vx->last_np;
+        HIPANN_REQUIRE(cap >= m, "probe buffer too small");
+        if (m == 0) return 0;
+        IvfShard &sh = *vx->shards[0];
+        DeviceGuard g(sh.device);
+        HIPANN_CHECK(hipStreamSynchronize(sh.stream));
+        HIPANN_CHECK(hipDeviceSynchronize());
+        HIPANN_CHECK(hipMemcpy(probes, sh.coarse_i.p, sizeof(int64_t) * (size_t)m, hipMemcpyDeviceToHost));
+        return 0;
+    });
+}
+
+int hipann_ivf_set_nprobe(void *h, int nprobe) {
+    if (!h || nprobe < 1) return -1;
+    auto *ix = static_cast<IndexBase *>(h);
+    if (ix->kind != Kind::IVF) return -1;
+    auto *vx = static_cast<IvfIndex *>(ix);
+    std::lock_guard<std::mutex> lk(vx->mu);
+    vx->nprobe = nprobe;
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,365 @@
+// ivf_kernels.hip — IVFFlat list-major scan for gfx950.
+//
+// Replaces MetalIndexIVFFlat::search (faiss-metal/src/MetalIndexIVFFlat.mm:122-256), which loops
+// over queries on the host, gathers every probed list into fresh buffers per query and launches a
+// GEMV-shaped distance + select per query.  Here the whole batch is one pipeline on one stream:
+//
+//   coarse quantizer  : the Flat kernels with k = nprobe  (FAISS quantizer->search, same nq<20 rule)
+//   ivf_count         : histogram of (query, probe) pairs per list
+//   ivf_plan          : one block — exclusive scans → bucket offsets and work-item offsets per list
+//   ivf_fill          : scatter (query, probe) pairs into per-list buckets
+//   ivf_scan_topk     : one block per work item = (list ℓ, ≤ 32 of the queries probing ℓ).  The
+//                       list's rows stream through LDS ONCE per item (coalesced float4 loads), each
+//                       of the 4 waves computes direct Σ(q−x)² (FAISS IVFFlat scans with fvec_L2sqr)
+//                       for its 8 queries × 256 rows per tile and keeps one wave top-k list per query
+//   merge_parts_topk  : per query, the k best of its nprobe partial lists (ids mapped to labels)
+//
+// HBM traffic per batch ≈ Σ_items |ℓ|·4d  (each list read once per 32 queries probing it) instead
+// of Σ_queries Σ_probes |ℓ|·4d for the query-major reference.
+#include "common.hpp"
+#include "wave_topk.hpp"
+
+namespace hipann {
+
+constexpr int IVF_QW = 8;               // queries per wave
+constexpr int IVF_G = 4 * IVF_QW;       // queries per work item (block of 4 waves)
+constexpr int IVF_TR = 256;             // list rows per tile (4 per lane)
+constexpr int IVF_BK = 32;              // dims per LDS chunk
+constexpr int IVF_LD = IVF_BK + 4;      // padded row stride (conflict-free ds_read_b128)
+
+__global__ void ivf_count(const int64_t *__restrict__ probes, int64_t npairs, const int *__restrict__ list_len,
+                          int nlist, int *__restrict__ cnt) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npairs) return;
+    const int64_t l = probes[i];
+    if (l < 0 || l >= nlist) return;
+    if (list_len[l] <= 0) return;  // empty, or owned by another shard
+    atomicAdd(cnt + l, 1);
+}
+
+// Single block: bucket_off[l] = Σ_{<l} cnt, item_off[l] = Σ_{<l} ceil(cnt/G); cursor[l] = 0;
+// total items in item_off[nlist].
+__global__ void __launch_bounds__(1024) ivf_plan(const int *__restrict__ cnt, int nlist, int *__restrict__ bucket_off,
+                                                 int *__restrict__ item_off, int *__restrict__ cursor) {
+    __shared__ int sb[1024], si[1024];
+    __shared__ int carry_b, carry_i;
+    if (threadIdx.x == 0) { carry_b = 0; carry_i = 0; }
+    __syncthreads();
+    for (int base = 0; base < nlist; base += 1024) {
+        const int l = base + threadIdx.x;
+        const int c = l < nlist ? cnt[l] : 0;
+        sb[threadIdx.x] = c;
+        si[threadIdx.x] = (c + IVF_G - 1) / IVF_G;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
+            int vb = 0, vi = 0;
+            if ((int)threadIdx.x >= o) { vb = sb[threadIdx.x - o]; vi = si[threadIdx.x - o]; }
+            __syncthreads();
+            sb[threadIdx.x] += vb;
+            si[threadIdx.x] += vi;
+            __syncthreads();
+        }
+        if (l < nlist) {
+            bucket_off[l] = carry_b + sb[threadIdx.x] - c;
+            item_off[l] = carry_i + si[threadIdx.x] - (c + IVF_G - 1) / IVF_G;
+            cursor[l] = 0;
+        }
+        __syncthreads();
+        if (threadIdx.x == 1023) { carry_b += sb[1023]; carry_i += si[1023]; }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) { bucket_off[nlist] = carry_b; item_off[nlist] = carry_i; }
+}
+
+__global__ void ivf_fill(const int64_t *__restrict__ probes, int64_t npairs, const int *__restrict__ list_len,
+                         int nlist, const int *__restrict__ bucket_off, int *__restrict__ cursor,
+                         int *__restrict__ bucket) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npairs) return;
+    const int64_t l = probes[i];
+    if (l < 0 || l >= nlist) return;
+    if (list_len[l] <= 0) return;
+    const int pos = atomicAdd(cursor + l, 1);
+    bucket[bucket_off[l] + pos] = (int)i;  // pair index = q * nprobe + p
+}
+
+template <bool VEC4>
+__device__ __forceinline__ void ivf_stage_load(const float *__restrict__ codes, int64_t r0, int64_t r1, int d, int k0,
+                                               float4 (&st)[8]) {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+        const int f = threadIdx.x + 256 * p;
+        const int row = f >> 3, c4 = f & 7;
+        const int64_t gr = r0 + row;
+        const int kk = k0 + 4 * c4;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (gr < r1) {
+            const float *src = codes + gr * (int64_t)d + kk;
+            if (VEC4) {
+                if (kk < d) v = *reinterpret_cast<const float4 *>(src);
+            } else {
+                if (kk + 0 < d) v.x = src[0];
+                if (kk + 1 < d) v.y = src[1];
+                if (kk + 2 < d) v.z = src[2];
+                if (kk + 3 < d) v.w = src[3];
+            }
+        }
+        st[p] = v;
+    }
+}
+
+__device__ __forceinline__ void ivf_stage_store(float *__restrict__ lds, const float4 (&st)[8]) {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+        const int f = threadIdx.x + 256 * p;
+        const int row = f >> 3, c4 = f & 7;
+        *reinterpret_cast<float4 *>(lds + row * IVF_LD + 4 * c4) = st[p];
+    }
+}
+
+// Stage this item's 32 queries × IVF_BK dims (one float4 per thread) — rows beyond nqi are zero.
+template <bool VEC4>
+__device__ __forceinline__ void ivf_stage_q(const float *__restrict__ Q, const int (&qrow)[1], int d, int k0,
+                                            float4 &st) {
+    const int t = threadIdx.x;  // 256 threads = 32 queries × 8 float4
+    const int kk = k0 + 4 * (t & 7);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (qrow[0] >= 0) {
+        const float *src = Q + (int64_t)qrow[0] * d + kk;
+        if (VEC4) {
+            if (kk < d) v = *reinterpret_cast<const float4 *>(src);
+        } else {
+            if (kk + 0 < d) v.x = src[0];
+            if (kk + 1 < d) v.y = src[1];
+            if (kk + 2 < d) v.z = src[2];
+            if (kk + 3 < d) v.w = src[3];
+        }
+    }
+    st = v;
+}
+
+// part_d / part_i layout: [nprobe][nq][k]; part_i holds shard-local row numbers.
+template <bool VEC4, bool IP>
+__global__ void __launch_bounds__(256, 2)
+ivf_scan_topk(const float *__restrict__ Q, int d, const float *__restrict__ codes, const int64_t *__restrict__ list_off,
+              const int *__restrict__ cnt, const int *__restrict__ bucket_off, const int *__restrict__ item_off,
+              const int *__restrict__ bucket, int nlist, int nprobe, int64_t nq, int k, float *__restrict__ part_d,
+              int *__restrict__ part_i) {
+    // LDS: x tiles [2][IVF_TR][IVF_LD] then query tiles [2][IVF_G][IVF_LD]
+    extern __shared__ __attribute__((aligned(16))) float xs[];
+    float *qs = xs + 2 * IVF_TR * IVF_LD;
+    const int item = blockIdx.x;
+    const int total = item_off[nlist];
+    if (item >= total) return;
+    // list owning this item: the last l with item_off[l] <= item (lists with no items share their
+    // successor's offset)
+    int lo = 0, hi = nlist - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (item_off[mid] <= item) lo = mid; else hi = mid - 1;
+    }
+    const int l = lo;
+    const int g = item - item_off[l];
+    const int c = cnt[l];
+    const int q_begin = g * IVF_G;
+    const int nqi = min(IVF_G, c - q_begin);
+    const int64_t r0 = list_off[l], r1 = list_off[l + 1];
+    const int boff = bucket_off[l] + q_begin;
+
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wq0 = wave * IVF_QW;                   // this wave's first query slot
+    const int nwq = max(0, min(IVF_QW, nqi - wq0));  // queries this wave owns (wave-uniform)
+
+    // staging role: thread t stages query slot t>>3
+    int qrow[1];
+    {
+        const int slot = threadIdx.x >> 3;
+        qrow[0] = slot < nqi ? bucket[boff + slot] / nprobe : -1;
+    }
+
+    WaveList<1, int> lists[IVF_QW];
+#pragma unroll
+    for (int j = 0; j < IVF_QW; ++j) lists[j].init();
+
+    const int nk = (d + IVF_BK - 1) / IVF_BK;
+    float4 st[8], sq;
+    for (int64_t t0 = r0; t0 < r1; t0 += IVF_TR) {
+        float acc[4][IVF_QW];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int j = 0; j < IVF_QW; ++j) acc[r][j] = 0.f;
+
+        ivf_stage_load<VEC4>(codes, t0, r1, d, 0, st);
+        ivf_stage_q<VEC4>(Q, qrow, d, 0, sq);
+        ivf_stage_store(xs, st);
+        *reinterpret_cast<float4 *>(qs + (threadIdx.x >> 3) * IVF_LD + 4 * (threadIdx.x & 7)) = sq;
+        __syncthreads();
+        for (int kc = 0; kc < nk; ++kc) {
+            const float *cur = xs + (kc & 1) * IVF_TR * IVF_LD;
+            float *nxt = xs + ((kc + 1) & 1) * IVF_TR * IVF_LD;
+            const float *qcur = qs + (kc & 1) * IVF_G * IVF_LD + wq0 * IVF_LD;
+            float *qnxt = qs + ((kc + 1) & 1) * IVF_G * IVF_LD;
+            if (kc + 1 < nk) {
+                ivf_stage_load<VEC4>(codes, t0, r1, d, (kc + 1) * IVF_BK, st);
+                ivf_stage_q<VEC4>(Q, qrow, d, (kc + 1) * IVF_BK, sq);
+            }
+            if (nwq > 0) {
+#pragma unroll 2
+                for (int u = 0; u < IVF_BK / 4; ++u) {
+                    float4 xv[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        xv[r] = *reinterpret_cast<const float4 *>(cur + (lane + 64 * r) * IVF_LD + 4 * u);
+#pragma unroll
+                    for (int j = 0; j < IVF_QW; ++j) {
+                        const float4 qv = *reinterpret_cast<const float4 *>(qcur + j * IVF_LD + 4 * u);  // broadcast
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            if (IP) {
+                                acc[r][j] = fmaf(qv.x, xv[r].x, acc[r][j]);
+                                acc[r][j] = fmaf(qv.y, xv[r].y, acc[r][j]);
+                                acc[r][j] = fmaf(qv.z, xv[r].z, acc[r][j]);
+                                acc[r][j] = fmaf(qv.w, xv[r].w, acc[r][j]);
+                            } else {
+                                float t;
+                                t = qv.x - xv[r].x; acc[r][j] = fmaf(t, t, acc[r][j]);
+                                t = qv.y - xv[r].y; acc[r][j] = fmaf(t, t, acc[r][j]);
+                                t = qv.z - xv[r].z; acc[r][j] = fmaf(t, t, acc[r][j]);
+                                t = qv.w - xv[r].w; acc[r][j] = fmaf(t, t, acc[r][j]);
+                            }
+                        }
+                    }
+                }
+            }
+            if (kc + 1 < nk) {
+                ivf_stage_store(nxt, st);
+                *reinterpret_cast<float4 *>(qnxt + (threadIdx.x >> 3) * IVF_LD + 4 * (threadIdx.x & 7)) = sq;
+            }
+            __syncthreads();
+        }
+        if (nwq > 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t row = t0 + lane + 64 * r;
+                const bool v = row < r1;
+#pragma unroll
+                for (int j = 0; j < IVF_QW; ++j) {
+                    if (j < nwq) {
+                        const float key = IP ? -acc[r][j] : acc[r][j];
+                        lists[j].offer(v ? key : __builtin_inff(), v ? (int)row : 0x7fffffff, k - 1);
+                    }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < IVF_QW; ++j) {
+        if (j < nwq) {
+            const int pr = bucket[boff + wq0 + j];
+            const int64_t q = pr / nprobe, p = pr - (pr / nprobe) * nprobe;
+            const int64_t off = (p * nq + q) * (int64_t)k;
+            lists[j].store(part_d + off, part_i + off, k);
+        }
+    }
+}
+
+// Merge the nprobe partial lists per query, mapping shard-local rows to labels.
+template <int S>
+__global__ void __launch_bounds__(256)
+ivf_merge_topk(const float *__restrict__ pd, const int *__restrict__ pi, const int64_t *__restrict__ ids,
+               int nparts, int64_t nq, int k, int kout, float out_sign, float *__restrict__ D,
+               int64_t *__restrict__ I) {
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq) return;
+    const int lane = threadIdx.x & 63;
+    WaveList<S, long long> L;
+    L.init();
+    const int64_t total = (int64_t)nparts * k;
+    for (int64_t c0 = 0; c0 < total; c0 += 64) {
+        const int64_t c = c0 + lane;
+        float key = __builtin_inff();
+        long long lab = IdTraits<long long>::pad();
+        if (c < total) {
+            const int64_t p = c / k, i = c - p * k;
+            const int64_t off = (p * nq + q) * k + i;
+            const int raw = pi[off];
+            const float v = pd[off];
+            if (raw >= 0 && raw != 0x7fffffff && !(v == __builtin_inff())) {
+                key = v;
+                lab = (long long)ids[raw];
+            }
+        }
+        L.offer(key, lab, kout - 1);
+    }
+    const float pad_d = out_sign > 0.f ? __builtin_inff() : -__builtin_inff();
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const int e = s * 64 + lane;
+        if (e < kout) {
+            const bool pad = L.id[s] == IdTraits<long long>::pad();
+            D[q * kout + e] = pad ? pad_d : L.d[s] * out_sign;
+            I[q * kout + e] = pad ? -1 : (int64_t)L.id[s];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+void launch_ivf_plan(const int64_t *probes, int64_t nq, int nprobe, const int *list_len, int nlist, int *cnt,
+                     int *bucket_off, int *item_off, int *cursor, int *bucket, hipStream_t st) {
+    const int64_t npairs = nq * nprobe;
+    HIPANN_CHECK(hipMemsetAsync(cnt, 0, sizeof(int) * (size_t)nlist, st));
+    if (npairs > 0)
+        hipLaunchKernelGGL(ivf_count, dim3((unsigned)ceil_div(npairs, 256)), dim3(256), 0, st, probes, npairs, list_len,
+                           nlist, cnt);
+    hipLaunchKernelGGL(ivf_plan, dim3(1), dim3(1024), 0, st, cnt, nlist, bucket_off, item_off, cursor);
+    if (npairs > 0)
+        hipLaunchKernelGGL(ivf_fill, dim3((unsigned)ceil_div(npairs, 256)), dim3(256), 0, st, probes, npairs, list_len,
+                           nlist, bucket_off, cursor, bucket);
+    HIPANN_CHECK(hipGetLastError());
+}
+
+int64_t ivf_max_items(int64_t nq, int nprobe, int nlist) {
+    const int64_t npairs = nq * nprobe;
+    return ceil_div(npairs, IVF_G) + std::min<int64_t>(nlist, npairs);
+}
+
+size_t ivf_scan_smem_bytes() { return (size_t)2 * (IVF_TR + IVF_G) * IVF_LD * sizeof(float); }
+
+void launch_ivf_scan(const float *Q, int d, int metric, const float *codes, const int64_t *list_off, const int *cnt,
+                     const int *bucket_off, const int *item_off, const int *bucket, int nlist, int nprobe, int64_t nq,
+                     int k, int64_t max_items, float *pd, int *pi, hipStream_t st) {
+    if (max_items <= 0) return;
+    const bool vec4 = (d % 4 == 0) && ((uintptr_t)Q % 16 == 0) && ((uintptr_t)codes % 16 == 0);
+    dim3 grid((unsigned)max_items), block(256);
+    const size_t smem = ivf_scan_smem_bytes();
+#define HIPANN_IVF_LAUNCH(V, IPM)                                                                                    \
+    hipLaunchKernelGGL((ivf_scan_topk<V, IPM>), grid, block, smem, st, Q, d, codes, list_off, cnt, bucket_off, item_off, \
+                       bucket, nlist, nprobe, nq, k, pd, pi)
+    if (vec4) {
+        if (metric == kIP) HIPANN_IVF_LAUNCH(true, true); else HIPANN_IVF_LAUNCH(true, false);
+    } else {
+        if (metric == kIP) HIPANN_IVF_LAUNCH(false, true); else HIPANN_IVF_LAUNCH(false, false);
+    }
+#undef HIPANN_IVF_LAUNCH
+    HIPANN_CHECK(hipGetLastError());
+}
+
+void launch_ivf_merge(const float *pd, const int *pi, const int64_t *ids, int nparts, int64_t nq, int k, int kout,
+                      float out_sign, float *D, int64_t *I, hipStream_t st) {
+    if (nq <= 0) return;
+    dim3 grid((unsigned)ceil_div(nq, 4)), block(256);
+    const int S = (kout + 63) / 64;
+#define HIPANN_IVF_MERGE(s)                                                                                           \
+    if (S <= s) {                                                                                                     \
+        hipLaunchKernelGGL(ivf_merge_topk<s>, grid, block, 0, st, pd, pi, ids, nparts, nq, k, kout, out_sign, D, I); \
+        HIPANN_CHECK(hipGetLastError());                                                                              \
+        return;                                                                                                       \
+    }
+    HIPANN_IVF_MERGE(1) HIPANN_IVF_MERGE(2) HIPANN_IVF_MERGE(4) HIPANN_IVF_MERGE(8) HIPANN_IVF_MERGE(16)
+    HIPANN_IVF_MERGE(32)
+#undef HIPANN_IVF_MERGE
+    throw HipError("ivf merge: k too large");
+}
+
+}  // namespace hipann

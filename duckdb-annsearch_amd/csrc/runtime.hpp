@@ -155,29 +155,28 @@ struct FlatIndex : IndexBase {
     }
 };
 
-// IVF: CSR lists resident on one device (sharding by lists across devices: one shard per device).
+// IVF: CSR inverted lists resident on one device.  With several devices the lists are partitioned
+// (size-balanced); every shard keeps all centroids and an empty range for lists it does not own.
 struct IvfShard {
     int device = 0;
-    int nlist = 0;
-    int64_t n = 0;
-    DevBuf centroids;   // nlist × d
-    DevBuf cnorm;       // ‖c‖² (L2)
-    DevBuf list_off;    // int64 nlist+1 (local row offsets)
-    DevBuf list_len;    // int nlist
-    DevBuf codes;       // n × d fp32, list-contiguous
-    DevBuf ids;         // n int64 labels
-    std::vector<int64_t> h_off;
-    std::vector<uint8_t> owned;  // per list: 1 if this shard scans it
+    int64_t n = 0;                 // rows held by this shard
+    const float *centroids = nullptr;
+    const float *codes = nullptr;  // n × d fp32, list-contiguous
+    const int64_t *ids = nullptr;  // n labels
+    DevBuf centroids_buf, codes_buf, ids_buf;  // owned storage (empty when borrowed)
+    DevBuf list_off;               // int64 nlist+1 (shard-local row offsets)
+    DevBuf list_len;               // int nlist (0 = empty or not owned)
+    std::unique_ptr<FlatIndex> quant;  // coarse quantizer over `centroids` (borrowed)
     hipStream_t stream = nullptr;
     // scratch
-    DevBuf q, qn, coarse_d, coarse_i, probes, work, work_cnt, part_d, part_i, out_d, out_i;
+    DevBuf q, coarse_d, coarse_i, cnt, bucket_off, item_off, cursor, bucket, part_d, part_i, out_d, out_i;
 };
 
 struct IvfIndex : IndexBase {
     int nlist = 0, nprobe = 1;
     std::vector<std::unique_ptr<IvfShard>> shards;
-    std::vector<int64_t> last_probes;
     int64_t last_nq = 0;
+    int last_np = 0;
     HostBuf h_q, h_d, h_i;
     DevBuf gather_d, gather_i, merged_d, merged_i;
     IvfIndex() : IndexBase(Kind::IVF) {}
@@ -203,6 +202,15 @@ void launch_flat_gemm_topk(const float *Q, const float *qn, int64_t nq, const fl
 size_t scan_smem_bytes(int nq, int d);
 void launch_flat_scan_topk(const float *Q, int nq, const float *X, int64_t N, int d, int metric, int k, int nwaves,
                            int64_t rows_per_wave, float *pd, int *pi, hipStream_t st);
+void launch_ivf_plan(const int64_t *probes, int64_t nq, int nprobe, const int *list_len, int nlist, int *cnt,
+                     int *bucket_off, int *item_off, int *cursor, int *bucket, hipStream_t st);
+int64_t ivf_max_items(int64_t nq, int nprobe, int nlist);
+size_t ivf_scan_smem_bytes();
+void launch_ivf_scan(const float *Q, int d, int metric, const float *codes, const int64_t *list_off, const int *cnt,
+                     const int *bucket_off, const int *item_off, const int *bucket, int nlist, int nprobe, int64_t nq,
+                     int k, int64_t max_items, float *pd, int *pi, hipStream_t st);
+void launch_ivf_merge(const float *pd, const int *pi, const int64_t *ids, int nparts, int64_t nq, int k, int kout,
+                      float out_sign, float *D, int64_t *I, hipStream_t st);
 template <typename InId>
 void launch_merge_parts(const float *pd, const InId *pi, int nparts, int64_t nq, int k, int kout,
                         int64_t label_offset, float in_sign, float out_sign, float *D, int64_t *I, hipStream_t st);

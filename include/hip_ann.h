@@ -105,6 +105,12 @@ void *hipann_ivf_create(int d, int metric, int nlist, int nprobe, const float *c
                         const int64_t *list_offsets, const int64_t *ids, const float *codes,
                         const int *devices, int ndev, char *err_buf, int err_len);
 
+/* Device-resident IVF (single device): centroids (nlist*d), ids (n int64) and codes (n*d fp32)
+ * already in HBM on `device`, list_offsets on the host.  copy=0 borrows the buffers. */
+void *hipann_ivf_create_device(int d, int metric, int nlist, int nprobe, const float *centroids_dev,
+                               const int64_t *list_offsets, const int64_t *ids_dev, const float *codes_dev,
+                               int device, int copy, char *err_buf, int err_len);
+
 int hipann_ivf_search(void *index, int64_t nq, const float *xq, int64_t k, float *D, int64_t *I,
                       char *err_buf, int err_len);
 

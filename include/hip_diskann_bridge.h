@@ -76,6 +76,17 @@ int diskann_hip_multi_batch_distances_ids_device(void *db, const float *queries_
                                                  const unsigned int *ids_dev, const unsigned int *query_map_dev,
                                                  int total_n, int metric, float *out_dev, void *stream);
 
+/* Lock-step multi-query best-first search over the registered DB — DiskProvider::search_batch
+ * (rust_lib/src/disk_provider.rs:470-652: pop the best candidate per active query, stop when
+ * |result| >= L and it is worse than result[L-1], expand unvisited neighbours, insert_result
+ * :656-678) with every step's distances computed by the id-gather kernel.  adjacency: n*R uint32,
+ * padded with UINT32_MAX (rust_lib/src/file_format.rs:3-18).  Outputs nq*k labels (−1 past the
+ * result) and distances (FLT_MAX past the result).  stats (may be NULL): [0] distance evaluations,
+ * [1] lock-step iterations, [2] GPU calls, [3] reserved.  Returns 0 / −1 (message in err_buf). */
+int diskann_hip_search_batch(void *db, const uint32_t *adjacency, int R, const uint32_t *entry_points, int n_ep,
+                             const float *queries, int nq, int k, int l_search, int metric, int64_t *out_ids,
+                             float *out_dists, int64_t *stats, char *err_buf, int err_len);
+
 int64_t diskann_hip_db_size(void *db);
 void diskann_hip_release_db(void *db);
 
