@@ -118,8 +118,8 @@ def main():
 
     n, d, nq, k = args.n, args.d, args.nq, args.k
     metric = 0 if args.metric == "l2" else 1
-    lo = rank * n // world
-    hi = (rank + 1) * n // world
+    from sharded import shard_bounds
+    lo, hi = shard_bounds(n, rank, world)
     n_local = hi - lo
     stream = torch.cuda.current_stream().cuda_stream
 
@@ -158,23 +158,19 @@ def main():
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t_setup
 
+    from sharded import ShardedSearch, merge_topk_device_torch, shard_bounds
+
     D_loc = torch.empty((nq, k), device=dev, dtype=torch.float32)
     I_loc = torch.empty((nq, k), device=dev, dtype=torch.int64)
-    if world > 1:
-        D_all = torch.empty((world, nq, k), device=dev, dtype=torch.float32)
-        I_all = torch.empty((world, nq, k), device=dev, dtype=torch.int64)
-        D_out = torch.empty((nq, k), device=dev, dtype=torch.float32)
-        I_out = torch.empty((nq, k), device=dev, dtype=torch.int64)
+
+    def local_search(q):
+        search(nq, q.data_ptr(), k, D_loc.data_ptr(), I_loc.data_ptr(), stream)
+        return D_loc, I_loc
+
+    sharded = ShardedSearch(local_search, merge_topk_device_torch(hipann, metric))
 
     def step():
-        search(nq, xq.data_ptr(), k, D_loc.data_ptr(), I_loc.data_ptr(), stream)
-        if world > 1:
-            dist.all_gather_into_tensor(D_all, D_loc)
-            dist.all_gather_into_tensor(I_all, I_loc)
-            hipann.merge_topk_device(metric, world, nq, k, D_all.data_ptr(), I_all.data_ptr(), D_out.data_ptr(),
-                                     I_out.data_ptr(), stream)
-            return D_out, I_out
-        return D_loc, I_loc
+        return sharded.search(xq)
 
     for _ in range(args.warmup):
         step()

@@ -1,0 +1,185 @@
+//! FFI bridge to MI355X batch distance computation — drop-in replacement of
+//! rust_lib/src/metal_ffi.rs (same public API, so disk_provider.rs / provider.rs only change their
+//! `use crate::metal_ffi` to `use crate::hip_ffi`, or keep metal_ffi.rs unchanged and link
+//! libhipann.so, which also exports the `diskann_metal_*` names).
+//!
+//! The implementation lives in libhipann.so (duckdb-annsearch_amd/csrc/diskann.hip); its C ABI is
+//! include/hip_diskann_bridge.h.  Symbols are resolved at link time when the Rust static lib is
+//! linked with the C++ extension (metal_ffi.rs:5-6, CMakeLists.txt:231-236).
+//!
+//! Source only in this repository (no cargo/rustc in the build image); INTEGRATION.md shows the
+//! Cargo / CMake wiring.
+
+use std::sync::atomic::{AtomicI32, Ordering};
+
+extern "C" {
+    fn diskann_hip_available() -> i32;
+    fn diskann_hip_batch_distances(
+        query: *const f32,
+        candidates: *const f32,
+        n: i32,
+        dim: i32,
+        metric: i32,
+        out_distances: *mut f32,
+    ) -> i32;
+    fn diskann_hip_multi_batch_distances(
+        queries: *const f32,
+        candidates: *const f32,
+        query_map: *const u32,
+        total_n: i32,
+        nq: i32,
+        dim: i32,
+        metric: i32,
+        out_distances: *mut f32,
+    ) -> i32;
+    fn diskann_hip_register_db(
+        data: *const core::ffi::c_void,
+        n: i64,
+        dim: i32,
+        fmt: i32,
+        sq8_min: *const f32,
+        sq8_scale: *const f32,
+    ) -> *mut core::ffi::c_void;
+    fn diskann_hip_multi_batch_distances_ids(
+        db: *mut core::ffi::c_void,
+        queries: *const f32,
+        nq: i32,
+        ids: *const u32,
+        query_map: *const u32,
+        total_n: i32,
+        metric: i32,
+        out_distances: *mut f32,
+    ) -> i32;
+    fn diskann_hip_release_db(db: *mut core::ffi::c_void);
+}
+
+/// Cached availability: -1 = unchecked, 0 = unavailable, 1 = available (metal_ffi.rs:33-34).
+static HIP_STATUS: AtomicI32 = AtomicI32::new(-1);
+
+/// Minimum n*dim to dispatch the reference-ABI (host candidate copy) path.  On MI355X the launch +
+/// PCIe round trip is ~15-30 us (vs ~100-200 us Metal dispatch, metal_ffi.rs:36-38), so the
+/// break-even is lower than the Metal value; kept at the reference value until DESIGN.md's
+/// measured break-even replaces it.
+pub const MIN_GPU_WORK: usize = 131072;
+
+/// One-shot threshold for vector_distances() (ann_search.cpp:699).
+pub const MIN_GPU_WORK_ONESHOT: usize = 49152;
+
+pub fn is_hip_available() -> bool {
+    let status = HIP_STATUS.load(Ordering::Relaxed);
+    if status >= 0 {
+        return status == 1;
+    }
+    let avail = unsafe { diskann_hip_available() };
+    HIP_STATUS.store(avail, Ordering::Relaxed);
+    avail == 1
+}
+
+/// Same contract as metal_ffi::metal_batch_distances (metal_ffi.rs:67-95).
+pub fn hip_batch_distances(query: &[f32], candidates: &[f32], n: usize, dim: usize, metric: u8, out: &mut [f32]) -> bool {
+    if n == 0 || dim == 0 {
+        return true;
+    }
+    if n * dim < MIN_GPU_WORK || !is_hip_available() {
+        return false;
+    }
+    debug_assert_eq!(candidates.len(), n * dim);
+    debug_assert!(out.len() >= n);
+    let ret = unsafe {
+        diskann_hip_batch_distances(query.as_ptr(), candidates.as_ptr(), n as i32, dim as i32, metric as i32, out.as_mut_ptr())
+    };
+    ret == 0
+}
+
+/// Same contract as metal_ffi::metal_multi_batch_distances (metal_ffi.rs:107-141).
+pub fn hip_multi_batch_distances(
+    queries: &[f32],
+    candidates: &[f32],
+    query_map: &[u32],
+    total_n: usize,
+    nq: usize,
+    dim: usize,
+    metric: u8,
+    out: &mut [f32],
+) -> bool {
+    if total_n == 0 || nq == 0 || dim == 0 {
+        return true;
+    }
+    if !is_hip_available() {
+        return false;
+    }
+    debug_assert_eq!(queries.len(), nq * dim);
+    debug_assert_eq!(candidates.len(), total_n * dim);
+    debug_assert_eq!(query_map.len(), total_n);
+    let ret = unsafe {
+        diskann_hip_multi_batch_distances(
+            queries.as_ptr(),
+            candidates.as_ptr(),
+            query_map.as_ptr(),
+            total_n as i32,
+            nq as i32,
+            dim as i32,
+            metric as i32,
+            out.as_mut_ptr(),
+        )
+    };
+    ret == 0
+}
+
+/// HBM-resident database for DiskProvider: register once at
+/// DiskProvider::open, then each lock-step BFS step ships only (id, query) pairs.
+pub struct HipDiskDb(*mut core::ffi::c_void);
+
+unsafe impl Send for HipDiskDb {}
+unsafe impl Sync for HipDiskDb {}
+
+impl HipDiskDb {
+    /// fp32 rows (the .diskann vector segment, e.g. straight from the mmap).
+    pub fn from_f32(vectors: &[f32], n: usize, dim: usize) -> Option<Self> {
+        if !is_hip_available() {
+            return None;
+        }
+        let h = unsafe {
+            diskann_hip_register_db(vectors.as_ptr() as *const _, n as i64, dim as i32, 0, std::ptr::null(), std::ptr::null())
+        };
+        if h.is_null() { None } else { Some(HipDiskDb(h)) }
+    }
+
+    /// SQ8 codes with the provider's per-dimension min / scale (provider.rs:25-38).
+    pub fn from_sq8(codes: &[u8], n: usize, dim: usize, min: &[f32], scale: &[f32]) -> Option<Self> {
+        if !is_hip_available() {
+            return None;
+        }
+        let h = unsafe {
+            diskann_hip_register_db(codes.as_ptr() as *const _, n as i64, dim as i32, 1, min.as_ptr(), scale.as_ptr())
+        };
+        if h.is_null() { None } else { Some(HipDiskDb(h)) }
+    }
+
+    /// out[i] = dist(queries[query_map[i]], db[ids[i]]) — replaces the gather + metal_multi_batch_distances
+    /// pair of disk_provider.rs:592-610.  false ⇒ caller computes on the CPU.
+    pub fn multi_batch_distances_ids(&self, queries: &[f32], nq: usize, ids: &[u32], query_map: &[u32], metric: u8, out: &mut [f32]) -> bool {
+        if ids.is_empty() {
+            return true;
+        }
+        let ret = unsafe {
+            diskann_hip_multi_batch_distances_ids(
+                self.0,
+                queries.as_ptr(),
+                nq as i32,
+                ids.as_ptr(),
+                query_map.as_ptr(),
+                ids.len() as i32,
+                metric as i32,
+                out.as_mut_ptr(),
+            )
+        };
+        ret == 0
+    }
+}
+
+impl Drop for HipDiskDb {
+    fn drop(&mut self) {
+        unsafe { diskann_hip_release_db(self.0) }
+    }
+}

@@ -463,7 +463,7 @@ int diskann_hip_multi_batch_distances_ids_device(void *h, const float *queries_d
     auto *db = static_cast<DiskDB *>(h);
     try {
         DeviceGuard g(db->device);
-        hipStream_t st = stream ? static_cast<hipStream_t>(stream) : db->stream;
+        hipStream_t st = static_cast<hipStream_t>(stream);  // NULL = the default (null) stream
         ScopedTiming tm(db->timer, st);
         launch_ids(*db, queries_dev, ids_dev, query_map_dev, total_n, metric, out_dev, st);
         return 0;

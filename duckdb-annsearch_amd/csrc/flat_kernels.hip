@@ -16,6 +16,8 @@
 #include "common.hpp"
 #include "wave_topk.hpp"
 
+#include <algorithm>
+
 namespace hipann {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -93,12 +95,14 @@ __device__ __forceinline__ void gemm_stage_store(float *__restrict__ lds, const 
     }
 }
 
-template <bool VEC4>
+// WRITE = true: no selection — the epilogue writes the keys of every (query, row) pair of the
+// tile to keys_out[q * ldk + row] (the k > 64 path selects from that matrix with rows_topk).
+template <bool VEC4, bool WRITE = false>
 __global__ void __launch_bounds__(256, 1)
 flat_gemm_topk(const float *__restrict__ Q, const float *__restrict__ qnorm, int64_t nq,
                const float *__restrict__ X, const float *__restrict__ xnorm, int64_t N, int d, int metric,
                int k, int nqt, int nsplit, int64_t tiles_per_split, float *__restrict__ part_d,
-               int *__restrict__ part_i) {
+               int *__restrict__ part_i, float *__restrict__ keys_out = nullptr, int64_t ldk = 0) {
     // LDS: two stages of A (queries) and B (db rows), 128×36 floats each; reused as the 128×128
     // distance tile in the epilogue (64 KiB ≤ 72 KiB).
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -122,9 +126,9 @@ flat_gemm_topk(const float *__restrict__ Q, const float *__restrict__ qnorm, int
     const int wr = wave >> 1, wc = wave & 1;
     const int l31 = lane & 31, h = lane >> 5;
 
-    WaveList<1, int> lists[32];
+    WaveList<1, int> lists[WRITE ? 1 : 32];
 #pragma unroll
-    for (int r = 0; r < 32; ++r) lists[r].init();
+    for (int r = 0; r < (WRITE ? 1 : 32); ++r) lists[r].init();
 
     const int nk = (d + GBK - 1) / GBK;
     float4 sa[4], sb[4];
@@ -186,6 +190,29 @@ flat_gemm_topk(const float *__restrict__ Q, const float *__restrict__ qnorm, int
             gemm_stage_load<VEC4>(X, (t + 1) * GBN, N, d, 0, sb);
         }
 
+        if (WRITE) {  // keys straight from the accumulators to HBM
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int64_t q = q0 + 64 * wr + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+                        const int64_t x = x0 + 64 * wc + 32 * j + l31;
+                        if (q < nq && x < N) {
+                            const float ip = acc[i][j][r];
+                            float key;
+                            if (metric == kL2) {
+                                key = fmaf(-2.f, ip, qnorm[q] + xnorm[x]);
+                                key = key < 0.f ? 0.f : key;
+                            } else {
+                                key = -ip;
+                            }
+                            keys_out[q * ldk + x] = key;
+                        }
+                    }
+            continue;
+        }
         // Epilogue 1: raw inner products → LDS tile Ct[128][128].
 #pragma unroll
         for (int i = 0; i < 2; ++i)
@@ -234,6 +261,7 @@ flat_gemm_topk(const float *__restrict__ Q, const float *__restrict__ qnorm, int
         __syncthreads();
     }
 
+    if (WRITE) return;
     // Store the per-(split, query) partial lists.
 #pragma unroll
     for (int r = 0; r < 32; ++r) {
@@ -252,13 +280,13 @@ flat_gemm_topk(const float *__restrict__ Q, const float *__restrict__ qnorm, int
 // q·x) across the wave and keeps one top-k list per query.  HBM-bound: every X byte read once.
 // Partial lists go to part[(wave_global * nq + q) * k].
 // ---------------------------------------------------------------------------------------------
-constexpr int SCAN_MAXQ = 19;  // FAISS distance_compute_blas_threshold = 20
 constexpr int SCAN_R = 4;
 
-template <int NQ, bool VEC4>
+template <int NQ, bool VEC4, bool WRITE = false>
 __global__ void __launch_bounds__(256)
 flat_scan_topk(const float *__restrict__ Q, const float *__restrict__ X, int64_t N, int d, int metric, int k,
-               int64_t rows_per_wave, float *__restrict__ part_d, int *__restrict__ part_i) {
+               int64_t rows_per_wave, float *__restrict__ part_d, int *__restrict__ part_i,
+               float *__restrict__ keys_out = nullptr, int64_t ldk = 0) {
     extern __shared__ __attribute__((aligned(16))) float qs[];  // NQ × dpad
     const int dpad = (d + 3) & ~3;
     for (int i = threadIdx.x; i < NQ * dpad; i += 256) {
@@ -344,14 +372,19 @@ flat_scan_topk(const float *__restrict__ Q, const float *__restrict__ X, int64_t
                 }
             }
         }
-        // Offer the (up to) 64 candidates of this group.
+        // Offer the (up to) 64 candidates of this group (or write them out).
         const int64_t myrow = base + lane;
         const bool valid = myrow < gend;
 #pragma unroll
         for (int qi = 0; qi < NQ; ++qi) {
-            lists[qi].offer(valid ? cand[qi] : __builtin_inff(), valid ? (int)myrow : 0x7fffffff, k - 1);
+            if (WRITE) {
+                if (valid) keys_out[qi * ldk + myrow] = cand[qi];
+            } else {
+                lists[qi].offer(valid ? cand[qi] : __builtin_inff(), valid ? (int)myrow : 0x7fffffff, k - 1);
+            }
         }
     }
+    if (WRITE) return;
 #pragma unroll
     for (int qi = 0; qi < NQ; ++qi) {
         const int64_t off = (gw * NQ + qi) * (int64_t)k;
@@ -406,6 +439,56 @@ merge_parts_topk(const float *__restrict__ pd, const InId *__restrict__ pi, int 
 }
 
 // ---------------------------------------------------------------------------------------------
+// rows_topk — k > 64 path: per (query row, column segment) one wave with an S-slot list over
+// keys[q * ldk + c], c in the segment; ids = id0 + c.  Partials go to [seg][q][k].
+// ---------------------------------------------------------------------------------------------
+template <int S>
+__global__ void __launch_bounds__(256)
+rows_topk(const float *__restrict__ keys, int64_t ldk, int64_t ncols, int64_t nq, int64_t seg_len, int nseg, int k,
+          int id0, float *__restrict__ part_d, int *__restrict__ part_i) {
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= nq * nseg) return;
+    const int64_t q = w % nq, sg = w / nq;
+    const int lane = threadIdx.x & 63;
+    WaveList<S, int> L;
+    L.init();
+    const int64_t c0 = sg * seg_len;
+    const int64_t c1 = c0 + seg_len < ncols ? c0 + seg_len : ncols;
+    for (int64_t c = c0; c < c1; c += 64) {
+        const int64_t cc = c + lane;
+        const bool v = cc < c1;
+        L.offer(v ? keys[q * ldk + cc] : __builtin_inff(), v ? (int)(id0 + cc) : 0x7fffffff, k - 1);
+    }
+    const int64_t off = (sg * nq + q) * (int64_t)k;
+    L.store(part_d + off, part_i + off, k);
+}
+
+// Raw merge: nparts partial [part][nq][k] (keys, int ids) → one [nq][k] partial (keys, int ids).
+template <int S>
+__global__ void __launch_bounds__(256)
+merge_parts_raw(const float *__restrict__ pd, const int *__restrict__ pi, int nparts, int64_t nq, int k,
+                float *__restrict__ od, int *__restrict__ oi) {
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq) return;
+    const int lane = threadIdx.x & 63;
+    WaveList<S, int> L;
+    L.init();
+    const int64_t total = (int64_t)nparts * k;
+    for (int64_t c0 = 0; c0 < total; c0 += 64) {
+        const int64_t c = c0 + lane;
+        float key = __builtin_inff();
+        int id = 0x7fffffff;
+        if (c < total) {
+            const int64_t p = c / k, i = c - p * k;
+            const int64_t off = (p * nq + q) * k + i;
+            if (pi[off] >= 0) { key = pd[off]; id = pi[off]; }
+        }
+        L.offer(key, id, k - 1);
+    }
+    L.store(od + q * k, oi + q * k, k);
+}
+
+// ---------------------------------------------------------------------------------------------
 // Host launchers (called from hip_ann.cpp).
 // ---------------------------------------------------------------------------------------------
 void launch_row_norms(const float *x, int64_t n, int d, float *out, hipStream_t st) {
@@ -432,6 +515,88 @@ void launch_flat_gemm_topk(const float *Q, const float *qn, int64_t nq, const fl
                            nsplit, tiles_per_split, pd, pi);
     }
     HIPANN_CHECK(hipGetLastError());
+}
+
+size_t scan_smem_bytes(int nq, int d);
+
+void launch_flat_gemm_keys(const float *Q, const float *qn, int64_t nq, const float *X, const float *xn, int64_t N,
+                           int d, int metric, float *keys, int64_t ldk, hipStream_t st) {
+    const int nqt = (int)ceil_div(nq, GBM);
+    const int64_t ntiles = ceil_div(N, GBN);
+    const bool vec4 = (d % 4 == 0) && ((uintptr_t)Q % 16 == 0) && ((uintptr_t)X % 16 == 0);
+    const size_t smem = gemm_smem_bytes();
+    dim3 grid((unsigned)(nqt * ntiles)), block(256);
+    if (vec4)
+        hipLaunchKernelGGL((flat_gemm_topk<true, true>), grid, block, smem, st, Q, qn, nq, X, xn, N, d, metric, 1, nqt,
+                           (int)ntiles, (int64_t)1, nullptr, nullptr, keys, ldk);
+    else
+        hipLaunchKernelGGL((flat_gemm_topk<false, true>), grid, block, smem, st, Q, qn, nq, X, xn, N, d, metric, 1,
+                           nqt, (int)ntiles, (int64_t)1, nullptr, nullptr, keys, ldk);
+    HIPANN_CHECK(hipGetLastError());
+}
+
+template <int NQ>
+static void scan_keys_dispatch(bool vec4, dim3 grid, size_t smem, hipStream_t st, const float *Q, const float *X,
+                               int64_t N, int d, int metric, int64_t rpw, float *keys, int64_t ldk) {
+    if (vec4)
+        hipLaunchKernelGGL((flat_scan_topk<NQ, true, true>), grid, dim3(256), smem, st, Q, X, N, d, metric, 1, rpw,
+                           nullptr, nullptr, keys, ldk);
+    else
+        hipLaunchKernelGGL((flat_scan_topk<NQ, false, true>), grid, dim3(256), smem, st, Q, X, N, d, metric, 1, rpw,
+                           nullptr, nullptr, keys, ldk);
+}
+
+void launch_flat_scan_keys(const float *Q, int nq, const float *X, int64_t N, int d, int metric, float *keys,
+                           int64_t ldk, hipStream_t st) {
+    const bool vec4 = (d % 4 == 0) && ((uintptr_t)X % 16 == 0);
+    const size_t smem = scan_smem_bytes(nq, d);
+    int64_t nwaves = std::min<int64_t>(8192, std::max<int64_t>(1, ceil_div(N, 512)));
+    const int64_t rpw = ceil_div(N, nwaves);
+    nwaves = ceil_div(N, rpw);
+    dim3 grid((unsigned)ceil_div(nwaves, 4));
+    switch (nq) {
+#define HIPANN_SCANK_CASE(n) \
+    case n: scan_keys_dispatch<n>(vec4, grid, smem, st, Q, X, N, d, metric, rpw, keys, ldk); break;
+        HIPANN_SCANK_CASE(1) HIPANN_SCANK_CASE(2) HIPANN_SCANK_CASE(3) HIPANN_SCANK_CASE(4) HIPANN_SCANK_CASE(5)
+        HIPANN_SCANK_CASE(6) HIPANN_SCANK_CASE(7) HIPANN_SCANK_CASE(8) HIPANN_SCANK_CASE(9) HIPANN_SCANK_CASE(10)
+        HIPANN_SCANK_CASE(11) HIPANN_SCANK_CASE(12) HIPANN_SCANK_CASE(13) HIPANN_SCANK_CASE(14) HIPANN_SCANK_CASE(15)
+        HIPANN_SCANK_CASE(16) HIPANN_SCANK_CASE(17) HIPANN_SCANK_CASE(18) HIPANN_SCANK_CASE(19)
+#undef HIPANN_SCANK_CASE
+        default: throw HipError("flat_scan_keys: nq out of range");
+    }
+    HIPANN_CHECK(hipGetLastError());
+}
+
+void launch_rows_topk(const float *keys, int64_t ldk, int64_t ncols, int64_t nq, int64_t seg_len, int nseg, int k,
+                      int id0, float *pd, int *pi, hipStream_t st) {
+    const int S = (k + 63) / 64;
+    dim3 grid((unsigned)ceil_div(nq * nseg, 4)), block(256);
+#define HIPANN_ROWS_CASE(s)                                                                                       \
+    if (S <= s) {                                                                                                 \
+        hipLaunchKernelGGL(rows_topk<s>, grid, block, 0, st, keys, ldk, ncols, nq, seg_len, nseg, k, id0, pd, pi); \
+        HIPANN_CHECK(hipGetLastError());                                                                          \
+        return;                                                                                                   \
+    }
+    HIPANN_ROWS_CASE(1) HIPANN_ROWS_CASE(2) HIPANN_ROWS_CASE(4) HIPANN_ROWS_CASE(8) HIPANN_ROWS_CASE(16)
+    HIPANN_ROWS_CASE(32)
+#undef HIPANN_ROWS_CASE
+    throw HipError("rows_topk: k too large");
+}
+
+void launch_merge_raw(const float *pd, const int *pi, int nparts, int64_t nq, int k, float *od, int *oi,
+                      hipStream_t st) {
+    const int S = (k + 63) / 64;
+    dim3 grid((unsigned)ceil_div(nq, 4)), block(256);
+#define HIPANN_MRAW_CASE(s)                                                                           \
+    if (S <= s) {                                                                                     \
+        hipLaunchKernelGGL(merge_parts_raw<s>, grid, block, 0, st, pd, pi, nparts, nq, k, od, oi);    \
+        HIPANN_CHECK(hipGetLastError());                                                              \
+        return;                                                                                       \
+    }
+    HIPANN_MRAW_CASE(1) HIPANN_MRAW_CASE(2) HIPANN_MRAW_CASE(4) HIPANN_MRAW_CASE(8) HIPANN_MRAW_CASE(16)
+    HIPANN_MRAW_CASE(32)
+#undef HIPANN_MRAW_CASE
+    throw HipError("merge_raw: k too large");
 }
 
 template <int NQ>

@@ -129,6 +129,49 @@ FlatIndex::~FlatIndex() {
     }
 }
 
+// k > 64: distance keys for a column chunk into HBM (GEMM or direct scan, same forms as the fused
+// path), per-(row, segment) S-slot wave lists, and a running merge across chunks.
+static void flat_shard_search_bigk(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq, const float *qn, int k,
+                                   int kout, float *D, int64_t *I, hipStream_t st) {
+    const int d = ix.d, metric = ix.metric;
+    const float out_sign = metric == kIP ? -1.f : 1.f;
+    const int64_t budget = (int64_t)256 << 20;  // bytes of keys per chunk
+    int64_t C = std::max<int64_t>(1024, budget / (4 * std::max<int64_t>(nq, 1)));
+    C = std::min<int64_t>(C, sh.n);
+    C = (C + 127) / 128 * 128;
+    const int64_t seg_len = 8192;
+    const int nseg = (int)ceil_div(C, seg_len);
+    sh.keys.ensure((size_t)nq * C * sizeof(float), sh.device);
+    sh.part_d.ensure((size_t)(nseg + 1) * nq * k * sizeof(float), sh.device);
+    sh.part_i.ensure((size_t)(nseg + 1) * nq * k * sizeof(int), sh.device);
+    sh.run_d.ensure((size_t)nq * k * sizeof(float), sh.device);
+    sh.run_i.ensure((size_t)nq * k * sizeof(int), sh.device);
+    // running best starts empty: part 0 = pads
+    HIPANN_CHECK(hipMemsetAsync(sh.part_i.p, 0xff, (size_t)nq * k * sizeof(int), st));
+    for (int64_t c0 = 0; c0 < sh.n; c0 += C) {
+        const int64_t cn = std::min<int64_t>(C, sh.n - c0);
+        {
+            ScopedTiming t(ix.timer_main, st);
+            if (nq < kBlasThreshold)
+                launch_flat_scan_keys(xq, (int)nq, sh.xb + c0 * d, cn, d, metric, sh.keys.get<float>(), C, st);
+            else
+                launch_flat_gemm_keys(xq, qn, nq, sh.xb + c0 * d, sh.xn.get<float>() + c0, cn, d, metric,
+                                      sh.keys.get<float>(), C, st);
+        }
+        const int ns = (int)ceil_div(cn, seg_len);
+        launch_rows_topk(sh.keys.get<float>(), C, cn, nq, seg_len, ns, k, (int)c0,
+                         sh.part_d.get<float>() + (size_t)nq * k, sh.part_i.get<int>() + (size_t)nq * k, st);
+        // merge [running best, ns segment partials] → running best (then back into part 0)
+        launch_merge_raw(sh.part_d.get<float>(), sh.part_i.get<int>(), ns + 1, nq, k, sh.run_d.get<float>(),
+                         sh.run_i.get<int>(), st);
+        HIPANN_CHECK(hipMemcpyAsync(sh.part_d.p, sh.run_d.p, (size_t)nq * k * sizeof(float), hipMemcpyDeviceToDevice, st));
+        HIPANN_CHECK(hipMemcpyAsync(sh.part_i.p, sh.run_i.p, (size_t)nq * k * sizeof(int), hipMemcpyDeviceToDevice, st));
+    }
+    ScopedTiming t(ix.timer_merge, st);
+    launch_merge_parts<int>(sh.run_d.get<float>(), sh.run_i.get<int>(), 1, nq, k, kout, sh.label_offset, 1.f, out_sign,
+                            D, I, st);
+}
+
 // Search one shard: queries already on the shard's device.  Writes D (nq×kout fp32: raw distances,
 // ±inf pads) and I (nq×kout int64 labels, −1 pads) on the same device, asynchronously on `st`.
 void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq, int k, int kout, float *D,
@@ -136,13 +179,23 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
     DeviceGuard g(sh.device);
     const int d = ix.d, metric = ix.metric;
     const float out_sign = metric == kIP ? -1.f : 1.f;
-    HIPANN_REQUIRE(k <= kFusedMaxK, "k > 64 is not supported by the fused GPU path yet");
+    HIPANN_REQUIRE(k <= HIPANN_MAX_K, "k larger than HIPANN_MAX_K");
     if (nq <= 0) return;
     if (sh.n == 0) {  // no rows: pads only
         launch_merge_parts<int>(nullptr, nullptr, 0, nq, k, kout, sh.label_offset, 1.f, out_sign, D, I, st);
         return;
     }
     HIPANN_REQUIRE(sh.n <= (int64_t)0x7ffffffe, "shard larger than 2^31-2 rows");
+    if (k > kFusedMaxK) {
+        const float *qn = nullptr;
+        if (nq >= kBlasThreshold && metric == kL2) {
+            sh.qn.ensure((size_t)nq * sizeof(float), sh.device);
+            launch_row_norms(xq, nq, d, sh.qn.get<float>(), st);
+            qn = sh.qn.get<float>();
+        }
+        flat_shard_search_bigk(ix, sh, nq, xq, qn, k, kout, D, I, st);
+        return;
+    }
     if (nq < kBlasThreshold) {
         // direct form (fvec_L2sqr / fvec_inner_product)
         int64_t nwaves = std::min<int64_t>(8192, std::max<int64_t>(1, ceil_div(sh.n, 512)));
@@ -373,6 +426,10 @@ void *hipann_flat_create_device(int d, int metric, const float *xb_dev, int64_t 
         HIPANN_REQUIRE(metric == kL2 || metric == kIP, "metric must be 0 (L2) or 1 (IP)");
         HIPANN_REQUIRE(device >= 0 && device < device_count(), "invalid device");
         HIPANN_REQUIRE(n >= 0 && (n == 0 || xb_dev), "invalid vectors");
+        {   // the caller's writes to xb_dev may still be in flight on any of its streams
+            DeviceGuard g(device);
+            HIPANN_CHECK(hipDeviceSynchronize());
+        }
         auto ix = std::make_unique<FlatIndex>();
         ix->d = d;
         ix->metric = metric;
@@ -410,7 +467,7 @@ int hipann_flat_search_device(void *h, int64_t nq, const float *xq_dev, int64_t 
         HIPANN_REQUIRE(fx->shards.size() == 1, "device search needs a single-device index");
         HIPANN_REQUIRE(k > 0 && k <= HIPANN_MAX_K, "k out of range");
         FlatShard &sh = *fx->shards[0];
-        hipStream_t st = stream ? static_cast<hipStream_t>(stream) : sh.stream;
+        hipStream_t st = static_cast<hipStream_t>(stream);  // NULL = the default (null) stream
         const int keff = (int)std::min<int64_t>(k, std::max<int64_t>(sh.n, 1));
         flat_shard_search(*fx, sh, nq, xq_dev, keff, (int)k, D_dev, I_dev, st);
         return 0;

@@ -79,7 +79,13 @@ std::unique_ptr<FlatIndex> make_quantizer(int d, int metric, const float *cen, i
 void upload_list_meta(IvfShard &sh, const std::vector<int64_t> &off, int nlist) {
     DeviceGuard g(sh.device);
     std::vector<int> len(nlist);
-    for (int l = 0; l < nlist; ++l) len[l] = (int)(off[l + 1] - off[l]);
+    int64_t maxlen = 0;
+    for (int l = 0; l < nlist; ++l) {
+        HIPANN_REQUIRE(off[l + 1] - off[l] < (int64_t)0x7fffffff, "inverted list longer than 2^31-1 rows");
+        len[l] = (int)(off[l + 1] - off[l]);
+        maxlen = std::max<int64_t>(maxlen, len[l]);
+    }
+    sh.max_nch = (int)std::max<int64_t>(1, ceil_div(maxlen, ivf_chunk_rows()));
     sh.list_off.ensure(sizeof(int64_t) * (nlist + 1), sh.device);
     sh.list_len.ensure(sizeof(int) * nlist, sh.device);
     HIPANN_CHECK(hipMemcpyAsync(sh.list_off.p, off.data(), sizeof(int64_t) * (nlist + 1), hipMemcpyHostToDevice,
@@ -121,23 +127,26 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     sh.cursor.ensure(sizeof(int) * (nlist + 1), sh.device);
     sh.bucket.ensure(sizeof(int) * (size_t)nq * np, sh.device);
     HIPANN_REQUIRE((int64_t)nq * np < (int64_t)0x7fffffff, "nq * nprobe too large");
+    sh.slot_off.ensure(sizeof(int) * ((size_t)nq * np + 1), sh.device);
     launch_ivf_plan(sh.coarse_i.get<int64_t>(), nq, np, sh.list_len.get<int>(), nlist, sh.cnt.get<int>(),
-                    sh.bucket_off.get<int>(), sh.item_off.get<int>(), sh.cursor.get<int>(), sh.bucket.get<int>(), st);
-    // 3. scan
-    const size_t parts = (size_t)np * nq * k;
+                    sh.bucket_off.get<int>(), sh.item_off.get<int>(), sh.cursor.get<int>(), sh.bucket.get<int>(),
+                    sh.slot_off.get<int>(), st);
+    // 3. scan: one k-list per (query, probe, row chunk) slot — every slot is written by exactly one item
+    const size_t parts = (size_t)np * nq * sh.max_nch * k;
+    HIPANN_REQUIRE((int64_t)np * nq * sh.max_nch < (int64_t)0x7fffffff, "too many partial lists");
     sh.part_d.ensure(parts * sizeof(float), sh.device);
     sh.part_i.ensure(parts * sizeof(int), sh.device);
-    HIPANN_CHECK(hipMemsetAsync(sh.part_i.p, 0xff, parts * sizeof(int), st));
-    const int64_t max_items = ivf_max_items(nq, np, nlist);
+    const int64_t max_items = ivf_max_items(nq, np, nlist, sh.max_nch, sh.n);
     {
         ScopedTiming t(ix.timer_main, st);
         launch_ivf_scan(xq, d, metric, sh.codes, sh.list_off.get<int64_t>(), sh.cnt.get<int>(),
-                        sh.bucket_off.get<int>(), sh.item_off.get<int>(), sh.bucket.get<int>(), nlist, np, nq, k,
-                        max_items, sh.part_d.get<float>(), sh.part_i.get<int>(), st);
+                        sh.bucket_off.get<int>(), sh.item_off.get<int>(), sh.bucket.get<int>(), sh.slot_off.get<int>(),
+                        nlist, np, nq, k, max_items, sh.part_d.get<float>(), sh.part_i.get<int>(), st);
     }
-    // 4. merge the nprobe partial lists per query
+    // 4. merge each query's partial lists
     ScopedTiming t(ix.timer_merge, st);
-    launch_ivf_merge(sh.part_d.get<float>(), sh.part_i.get<int>(), sh.ids, np, nq, k, kout, out_sign, D, I, st);
+    launch_ivf_merge(sh.part_d.get<float>(), sh.part_i.get<int>(), sh.ids, sh.slot_off.get<int>(), np, nq, k, kout,
+                     out_sign, D, I, st);
 }
 
 }  // namespace hipann
@@ -241,6 +250,7 @@ void *hipann_ivf_create_device(int d, int metric, int nlist, int nprobe, const f
         sh->stream = make_stream(device);
         sh->n = n;
         DeviceGuard g(device);
+        HIPANN_CHECK(hipDeviceSynchronize());  // caller's writes to the inputs may still be in flight
         if (copy) {
             sh->centroids_buf.ensure(sizeof(float) * (size_t)nlist * d, device);
             sh->codes_buf.ensure(sizeof(float) * (size_t)std::max<int64_t>(n, 1) * d, device);
@@ -356,7 +366,7 @@ int hipann_ivf_search_device(void *h, int64_t nq, const float *xq_dev, int64_t k
         HIPANN_REQUIRE(vx->shards.size() == 1, "device search needs a single-device index");
         HIPANN_REQUIRE(k > 0 && k <= HIPANN_MAX_K, "k out of range");
         IvfShard &sh = *vx->shards[0];
-        hipStream_t st = stream ? static_cast<hipStream_t>(stream) : sh.stream;
+        hipStream_t st = static_cast<hipStream_t>(stream);  // NULL = the default (null) stream
         vx->last_nq = nq;
         vx->last_np = std::min(vx->nprobe, vx->nlist);
         const int keff = (int)std::min<int64_t>(k, std::max<int64_t>(sh.n, 1));

@@ -26,6 +26,9 @@ constexpr int IVF_G = 4 * IVF_QW;       // queries per work item (block of 4 wav
 constexpr int IVF_TR = 256;             // list rows per tile (4 per lane)
 constexpr int IVF_BK = 32;              // dims per LDS chunk
 constexpr int IVF_LD = IVF_BK + 4;      // padded row stride (conflict-free ds_read_b128)
+constexpr int IVF_CH = 2048;            // list rows per work item (big lists split into chunks)
+
+__device__ __forceinline__ int ivf_nch(int len) { return (len + IVF_CH - 1) / IVF_CH; }
 
 __global__ void ivf_count(const int64_t *__restrict__ probes, int64_t npairs, const int *__restrict__ list_len,
                           int nlist, int *__restrict__ cnt) {
@@ -37,9 +40,10 @@ __global__ void ivf_count(const int64_t *__restrict__ probes, int64_t npairs, co
     atomicAdd(cnt + l, 1);
 }
 
-// Single block: bucket_off[l] = Σ_{<l} cnt, item_off[l] = Σ_{<l} ceil(cnt/G); cursor[l] = 0;
-// total items in item_off[nlist].
-__global__ void __launch_bounds__(1024) ivf_plan(const int *__restrict__ cnt, int nlist, int *__restrict__ bucket_off,
+// Single block: bucket_off[l] = Σ_{<l} cnt, item_off[l] = Σ_{<l} ceil(cnt/G)·nch(l) (one item per
+// (query group, row chunk) of each list); cursor[l] = 0; total items in item_off[nlist].
+__global__ void __launch_bounds__(1024) ivf_plan(const int *__restrict__ cnt, const int *__restrict__ list_len,
+                                                 int nlist, int *__restrict__ bucket_off,
                                                  int *__restrict__ item_off, int *__restrict__ cursor) {
     __shared__ int sb[1024], si[1024];
     __shared__ int carry_b, carry_i;
@@ -48,8 +52,9 @@ __global__ void __launch_bounds__(1024) ivf_plan(const int *__restrict__ cnt, in
     for (int base = 0; base < nlist; base += 1024) {
         const int l = base + threadIdx.x;
         const int c = l < nlist ? cnt[l] : 0;
+        const int items = l < nlist ? ((c + IVF_G - 1) / IVF_G) * ivf_nch(list_len[l]) : 0;
         sb[threadIdx.x] = c;
-        si[threadIdx.x] = (c + IVF_G - 1) / IVF_G;
+        si[threadIdx.x] = items;
         __syncthreads();
         for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
             int vb = 0, vi = 0;
@@ -61,7 +66,7 @@ __global__ void __launch_bounds__(1024) ivf_plan(const int *__restrict__ cnt, in
         }
         if (l < nlist) {
             bucket_off[l] = carry_b + sb[threadIdx.x] - c;
-            item_off[l] = carry_i + si[threadIdx.x] - (c + IVF_G - 1) / IVF_G;
+            item_off[l] = carry_i + si[threadIdx.x] - items;
             cursor[l] = 0;
         }
         __syncthreads();
@@ -81,6 +86,40 @@ __global__ void ivf_fill(const int64_t *__restrict__ probes, int64_t npairs, con
     if (list_len[l] <= 0) return;
     const int pos = atomicAdd(cursor + l, 1);
     bucket[bucket_off[l] + pos] = (int)i;  // pair index = q * nprobe + p
+}
+
+// Single block: partial-list slots.  Pair i (= q·nprobe + p, probing list l) owns nch(l) consecutive
+// slots (one per row chunk of l; 0 if l is empty or not on this shard): slot_off = exclusive scan.
+// The slots of one query are therefore the contiguous range [slot_off[q·np], slot_off[(q+1)·np]).
+__global__ void __launch_bounds__(1024) ivf_slot_scan(const int64_t *__restrict__ probes, int64_t npairs,
+                                                      const int *__restrict__ list_len, int nlist,
+                                                      int *__restrict__ slot_off) {
+    __shared__ int sv[1024];
+    __shared__ int carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int64_t base = 0; base < npairs; base += 1024) {
+        const int64_t i = base + threadIdx.x;
+        int v = 0;
+        if (i < npairs) {
+            const int64_t l = probes[i];
+            if (l >= 0 && l < nlist) v = ivf_nch(list_len[l]);
+        }
+        sv[threadIdx.x] = v;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {
+            int t = 0;
+            if ((int)threadIdx.x >= o) t = sv[threadIdx.x - o];
+            __syncthreads();
+            sv[threadIdx.x] += t;
+            __syncthreads();
+        }
+        if (i < npairs) slot_off[i] = carry + sv[threadIdx.x] - v;
+        __syncthreads();
+        if (threadIdx.x == 1023) carry += sv[1023];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) slot_off[npairs] = carry;
 }
 
 template <bool VEC4>
@@ -138,13 +177,13 @@ __device__ __forceinline__ void ivf_stage_q(const float *__restrict__ Q, const i
     st = v;
 }
 
-// part_d / part_i layout: [nprobe][nq][k]; part_i holds shard-local row numbers.
+// part_d / part_i: one k-list per slot (slot_off, above); part_i holds shard-local row numbers.
 template <bool VEC4, bool IP>
 __global__ void __launch_bounds__(256, 2)
 ivf_scan_topk(const float *__restrict__ Q, int d, const float *__restrict__ codes, const int64_t *__restrict__ list_off,
               const int *__restrict__ cnt, const int *__restrict__ bucket_off, const int *__restrict__ item_off,
-              const int *__restrict__ bucket, int nlist, int nprobe, int64_t nq, int k, float *__restrict__ part_d,
-              int *__restrict__ part_i) {
+              const int *__restrict__ bucket, const int *__restrict__ slot_off, int nlist, int nprobe, int64_t nq,
+              int k, float *__restrict__ part_d, int *__restrict__ part_i) {
     // LDS: x tiles [2][IVF_TR][IVF_LD] then query tiles [2][IVF_G][IVF_LD]
     extern __shared__ __attribute__((aligned(16))) float xs[];
     float *qs = xs + 2 * IVF_TR * IVF_LD;
@@ -159,11 +198,15 @@ ivf_scan_topk(const float *__restrict__ Q, int d, const float *__restrict__ code
         if (item_off[mid] <= item) lo = mid; else hi = mid - 1;
     }
     const int l = lo;
-    const int g = item - item_off[l];
+    const int64_t lr0 = list_off[l], lr1 = list_off[l + 1];
+    const int nch = ivf_nch((int)(lr1 - lr0));
+    const int rem = item - item_off[l];
+    const int g = rem / nch, chunk = rem - g * nch;  // (query group, row chunk)
     const int c = cnt[l];
     const int q_begin = g * IVF_G;
     const int nqi = min(IVF_G, c - q_begin);
-    const int64_t r0 = list_off[l], r1 = list_off[l + 1];
+    const int64_t r0 = lr0 + (int64_t)chunk * IVF_CH;
+    const int64_t r1 = r0 + IVF_CH < lr1 ? r0 + IVF_CH : lr1;
     const int boff = bucket_off[l] + q_begin;
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -257,32 +300,31 @@ ivf_scan_topk(const float *__restrict__ Q, int d, const float *__restrict__ code
     for (int j = 0; j < IVF_QW; ++j) {
         if (j < nwq) {
             const int pr = bucket[boff + wq0 + j];
-            const int64_t q = pr / nprobe, p = pr - (pr / nprobe) * nprobe;
-            const int64_t off = (p * nq + q) * (int64_t)k;
+            const int64_t off = (int64_t)(slot_off[pr] + chunk) * k;
             lists[j].store(part_d + off, part_i + off, k);
         }
     }
 }
 
-// Merge the nprobe partial lists per query, mapping shard-local rows to labels.
+// Merge each query's partial lists (its contiguous slot range), mapping shard-local rows to labels.
 template <int S>
 __global__ void __launch_bounds__(256)
 ivf_merge_topk(const float *__restrict__ pd, const int *__restrict__ pi, const int64_t *__restrict__ ids,
-               int nparts, int64_t nq, int k, int kout, float out_sign, float *__restrict__ D,
-               int64_t *__restrict__ I) {
+               const int *__restrict__ slot_off, int nprobe, int64_t nq, int k, int kout, float out_sign,
+               float *__restrict__ D, int64_t *__restrict__ I) {
     const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (q >= nq) return;
     const int lane = threadIdx.x & 63;
     WaveList<S, long long> L;
     L.init();
-    const int64_t total = (int64_t)nparts * k;
+    const int64_t s0 = slot_off[q * nprobe], s1 = slot_off[(q + 1) * nprobe];
+    const int64_t total = (s1 - s0) * k;
     for (int64_t c0 = 0; c0 < total; c0 += 64) {
         const int64_t c = c0 + lane;
         float key = __builtin_inff();
         long long lab = IdTraits<long long>::pad();
         if (c < total) {
-            const int64_t p = c / k, i = c - p * k;
-            const int64_t off = (p * nq + q) * k + i;
+            const int64_t off = s0 * k + c;
             const int raw = pi[off];
             const float v = pd[off];
             if (raw >= 0 && raw != 0x7fffffff && !(v == __builtin_inff())) {
@@ -306,36 +348,41 @@ ivf_merge_topk(const float *__restrict__ pd, const int *__restrict__ pi, const i
 
 // ---------------------------------------------------------------------------------------------
 void launch_ivf_plan(const int64_t *probes, int64_t nq, int nprobe, const int *list_len, int nlist, int *cnt,
-                     int *bucket_off, int *item_off, int *cursor, int *bucket, hipStream_t st) {
+                     int *bucket_off, int *item_off, int *cursor, int *bucket, int *slot_off, hipStream_t st) {
     const int64_t npairs = nq * nprobe;
     HIPANN_CHECK(hipMemsetAsync(cnt, 0, sizeof(int) * (size_t)nlist, st));
     if (npairs > 0)
         hipLaunchKernelGGL(ivf_count, dim3((unsigned)ceil_div(npairs, 256)), dim3(256), 0, st, probes, npairs, list_len,
                            nlist, cnt);
-    hipLaunchKernelGGL(ivf_plan, dim3(1), dim3(1024), 0, st, cnt, nlist, bucket_off, item_off, cursor);
+    hipLaunchKernelGGL(ivf_plan, dim3(1), dim3(1024), 0, st, cnt, list_len, nlist, bucket_off, item_off, cursor);
+    hipLaunchKernelGGL(ivf_slot_scan, dim3(1), dim3(1024), 0, st, probes, npairs, list_len, nlist, slot_off);
     if (npairs > 0)
         hipLaunchKernelGGL(ivf_fill, dim3((unsigned)ceil_div(npairs, 256)), dim3(256), 0, st, probes, npairs, list_len,
                            nlist, bucket_off, cursor, bucket);
     HIPANN_CHECK(hipGetLastError());
 }
 
-int64_t ivf_max_items(int64_t nq, int nprobe, int nlist) {
+// Upper bound on work items given the largest list's chunk count.
+// Σ_l ceil(cnt_l/G)·nch_l ≤ Σ_l (cnt_l/G + 1)·nch_l ≤ ceil(npairs/G)·max_nch + Σ_l nch_l.
+int64_t ivf_max_items(int64_t nq, int nprobe, int nlist, int max_nch, int64_t nrows) {
     const int64_t npairs = nq * nprobe;
-    return ceil_div(npairs, IVF_G) + std::min<int64_t>(nlist, npairs);
+    return ceil_div(npairs, IVF_G) * std::max(max_nch, 1) + ceil_div(nrows, IVF_CH) + nlist;
 }
+
+int ivf_chunk_rows() { return IVF_CH; }
 
 size_t ivf_scan_smem_bytes() { return (size_t)2 * (IVF_TR + IVF_G) * IVF_LD * sizeof(float); }
 
 void launch_ivf_scan(const float *Q, int d, int metric, const float *codes, const int64_t *list_off, const int *cnt,
-                     const int *bucket_off, const int *item_off, const int *bucket, int nlist, int nprobe, int64_t nq,
-                     int k, int64_t max_items, float *pd, int *pi, hipStream_t st) {
+                     const int *bucket_off, const int *item_off, const int *bucket, const int *slot_off, int nlist,
+                     int nprobe, int64_t nq, int k, int64_t max_items, float *pd, int *pi, hipStream_t st) {
     if (max_items <= 0) return;
     const bool vec4 = (d % 4 == 0) && ((uintptr_t)Q % 16 == 0) && ((uintptr_t)codes % 16 == 0);
     dim3 grid((unsigned)max_items), block(256);
     const size_t smem = ivf_scan_smem_bytes();
 #define HIPANN_IVF_LAUNCH(V, IPM)                                                                                    \
     hipLaunchKernelGGL((ivf_scan_topk<V, IPM>), grid, block, smem, st, Q, d, codes, list_off, cnt, bucket_off, item_off, \
-                       bucket, nlist, nprobe, nq, k, pd, pi)
+                       bucket, slot_off, nlist, nprobe, nq, k, pd, pi)
     if (vec4) {
         if (metric == kIP) HIPANN_IVF_LAUNCH(true, true); else HIPANN_IVF_LAUNCH(true, false);
     } else {
@@ -345,14 +392,15 @@ void launch_ivf_scan(const float *Q, int d, int metric, const float *codes, cons
     HIPANN_CHECK(hipGetLastError());
 }
 
-void launch_ivf_merge(const float *pd, const int *pi, const int64_t *ids, int nparts, int64_t nq, int k, int kout,
-                      float out_sign, float *D, int64_t *I, hipStream_t st) {
+void launch_ivf_merge(const float *pd, const int *pi, const int64_t *ids, const int *slot_off, int nprobe, int64_t nq,
+                      int k, int kout, float out_sign, float *D, int64_t *I, hipStream_t st) {
     if (nq <= 0) return;
     dim3 grid((unsigned)ceil_div(nq, 4)), block(256);
     const int S = (kout + 63) / 64;
 #define HIPANN_IVF_MERGE(s)                                                                                           \
     if (S <= s) {                                                                                                     \
-        hipLaunchKernelGGL(ivf_merge_topk<s>, grid, block, 0, st, pd, pi, ids, nparts, nq, k, kout, out_sign, D, I); \
+        hipLaunchKernelGGL(ivf_merge_topk<s>, grid, block, 0, st, pd, pi, ids, slot_off, nprobe, nq, k, kout,       \
+                           out_sign, D, I);                                                                           \
         HIPANN_CHECK(hipGetLastError());                                                                              \
         return;                                                                                                       \
     }

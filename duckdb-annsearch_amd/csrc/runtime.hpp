@@ -123,6 +123,7 @@ struct FlatShard {
     hipStream_t stream = nullptr;
     // scratch
     DevBuf q, qn, part_d, part_i, out_d, out_i;
+    DevBuf keys, run_d, run_i, run2_d, run2_i;  // k > 64 path
 };
 
 struct IndexBase {
@@ -169,7 +170,8 @@ struct IvfShard {
     std::unique_ptr<FlatIndex> quant;  // coarse quantizer over `centroids` (borrowed)
     hipStream_t stream = nullptr;
     // scratch
-    DevBuf q, coarse_d, coarse_i, cnt, bucket_off, item_off, cursor, bucket, part_d, part_i, out_d, out_i;
+    DevBuf q, coarse_d, coarse_i, cnt, bucket_off, item_off, cursor, bucket, slot_off, part_d, part_i, out_d, out_i;
+    int max_nch = 1;  // largest list's row-chunk count
 };
 
 struct IvfIndex : IndexBase {
@@ -200,17 +202,26 @@ void launch_flat_gemm_topk(const float *Q, const float *qn, int64_t nq, const fl
                            int d, int metric, int k, int nsplit, int64_t tiles_per_split, float *pd, int *pi,
                            hipStream_t st);
 size_t scan_smem_bytes(int nq, int d);
+void launch_flat_gemm_keys(const float *Q, const float *qn, int64_t nq, const float *X, const float *xn, int64_t N,
+                           int d, int metric, float *keys, int64_t ldk, hipStream_t st);
+void launch_flat_scan_keys(const float *Q, int nq, const float *X, int64_t N, int d, int metric, float *keys,
+                           int64_t ldk, hipStream_t st);
+void launch_rows_topk(const float *keys, int64_t ldk, int64_t ncols, int64_t nq, int64_t seg_len, int nseg, int k,
+                      int id0, float *pd, int *pi, hipStream_t st);
+void launch_merge_raw(const float *pd, const int *pi, int nparts, int64_t nq, int k, float *od, int *oi,
+                      hipStream_t st);
 void launch_flat_scan_topk(const float *Q, int nq, const float *X, int64_t N, int d, int metric, int k, int nwaves,
                            int64_t rows_per_wave, float *pd, int *pi, hipStream_t st);
 void launch_ivf_plan(const int64_t *probes, int64_t nq, int nprobe, const int *list_len, int nlist, int *cnt,
-                     int *bucket_off, int *item_off, int *cursor, int *bucket, hipStream_t st);
-int64_t ivf_max_items(int64_t nq, int nprobe, int nlist);
+                     int *bucket_off, int *item_off, int *cursor, int *bucket, int *slot_off, hipStream_t st);
+int64_t ivf_max_items(int64_t nq, int nprobe, int nlist, int max_nch, int64_t nrows);
+int ivf_chunk_rows();
 size_t ivf_scan_smem_bytes();
 void launch_ivf_scan(const float *Q, int d, int metric, const float *codes, const int64_t *list_off, const int *cnt,
-                     const int *bucket_off, const int *item_off, const int *bucket, int nlist, int nprobe, int64_t nq,
-                     int k, int64_t max_items, float *pd, int *pi, hipStream_t st);
-void launch_ivf_merge(const float *pd, const int *pi, const int64_t *ids, int nparts, int64_t nq, int k, int kout,
-                      float out_sign, float *D, int64_t *I, hipStream_t st);
+                     const int *bucket_off, const int *item_off, const int *bucket, const int *slot_off, int nlist,
+                     int nprobe, int64_t nq, int k, int64_t max_items, float *pd, int *pi, hipStream_t st);
+void launch_ivf_merge(const float *pd, const int *pi, const int64_t *ids, const int *slot_off, int nprobe, int64_t nq,
+                      int k, int kout, float out_sign, float *D, int64_t *I, hipStream_t st);
 template <typename InId>
 void launch_merge_parts(const float *pd, const InId *pi, int nparts, int64_t nq, int k, int kout,
                         int64_t label_offset, float in_sign, float out_sign, float *D, int64_t *I, hipStream_t st);

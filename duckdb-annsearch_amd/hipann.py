@@ -53,6 +53,19 @@ def build(force: bool = False) -> Path:
     return LIB_PATH
 
 
+def _share_torch_hip_runtime() -> None:
+    """One HIP runtime per process.  PyTorch-ROCm ships its own libamdhip64 (SONAME libamdhip64.so.7,
+    but its libc10_hip NEEDs the unversioned name); if libhipann.so were loaded first, torch would map
+    a second runtime and see no GPU.  Importing torch first makes libhipann.so bind to torch's copy,
+    so device pointers and streams are shared.  Set HIPANN_STANDALONE=1 to skip (no torch use)."""
+    if os.environ.get("HIPANN_STANDALONE") == "1":
+        return
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
 def lib() -> C.CDLL:
     """Load libhipann.so (fails loudly if it is missing — no fallback)."""
     global _lib
@@ -61,6 +74,7 @@ def lib() -> C.CDLL:
             return _lib
         if not LIB_PATH.exists():
             raise HipAnnError(f"libhipann.so not built ({LIB_PATH}); run hipann.build()")
+        _share_torch_hip_runtime()
         L = C.CDLL(str(LIB_PATH))
         vp, f, i64p, i64, i32, cp = C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_int64), C.c_int64, C.c_int, C.c_char_p
         u32p = C.POINTER(C.c_uint32)

@@ -75,8 +75,8 @@ int hipann_flat_reconstruct(void *index, int64_t key, float *out, char *err_buf,
 /* ---------------------------------------------------------------------------------------------
  * Device-resident variants (inputs and outputs already in HBM).  Used by the multi-GPU sharded
  * search (one process per GPU, partial top-k gathered over RCCL) and by bench.py, whose timed
- * region starts with the inputs resident.  `stream` is a hipStream_t (NULL = the handle's stream);
- * the call is asynchronous on that stream.
+ * region starts with the inputs resident.  `stream` is a hipStream_t (NULL = the default/null
+ * stream, HIP's convention and PyTorch's default stream); the call is asynchronous on that stream.
  * ------------------------------------------------------------------------------------------- */
 
 /* Wrap (copy=0: borrow, caller keeps it alive) or copy (copy=1) an HBM matrix of n*d fp32 on

@@ -70,8 +70,8 @@ int diskann_hip_multi_batch_distances_ids(void *db, const float *queries, int nq
                                           const unsigned int *query_map, int total_n, int metric,
                                           float *out_distances);
 
-/* Same with every buffer already in HBM (asynchronous on `stream`, a hipStream_t; NULL = the db's
- * stream).  For benchmarking the kernel with resident inputs. */
+/* Same with every buffer already in HBM (asynchronous on `stream`, a hipStream_t; NULL = the
+ * default/null stream).  For benchmarking the kernel with resident inputs. */
 int diskann_hip_multi_batch_distances_ids_device(void *db, const float *queries_dev, int nq,
                                                  const unsigned int *ids_dev, const unsigned int *query_map_dev,
                                                  int total_n, int metric, float *out_dev, void *stream);

@@ -1,0 +1,100 @@
+"""CPU tests of the drop-in boundary: libhipann.so builds for gfx950, loads, exports every symbol the
+public headers declare, and fails loudly (never silently on the CPU) without a device."""
+from __future__ import annotations
+
+import ctypes as C
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+HEADERS = sorted((ROOT / "include").glob("*.h"))
+
+
+def declared_functions():
+    names = []
+    for h in HEADERS:
+        text = re.sub(r"/\*.*?\*/", "", h.read_text(), flags=re.S)
+        names += re.findall(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b([a-z_][a-z0-9_]+)\s*\(", text, flags=re.M)
+    return sorted(set(n for n in names if n.startswith(("hipann_", "diskann_"))))
+
+
+def test_headers_declare_the_reference_bridge_symbols():
+    names = declared_functions()
+    # metal_diskann_bridge.h:8-23 — the three reference entry points, kept under their own names too
+    for n in ("diskann_metal_available", "diskann_metal_batch_distances", "diskann_metal_multi_batch_distances",
+              "diskann_hip_available", "diskann_hip_batch_distances", "diskann_hip_multi_batch_distances"):
+        assert n in names
+    for n in ("hipann_available", "hipann_device_info", "hipann_flat_create", "hipann_flat_search",
+              "hipann_ivf_create", "hipann_ivf_search", "hipann_ivf_set_nprobe", "hipann_free"):
+        assert n in names
+
+
+def test_library_builds_and_exports_every_declared_symbol(hipann_mod):
+    lib = C.CDLL(str(hipann_mod.LIB_PATH))
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, f"declared but not exported: {missing}"
+    hipann_mod.lib()  # the Python mirror binds every entry point
+
+
+def test_library_targets_gfx950(hipann_mod):
+    blob = hipann_mod.LIB_PATH.read_bytes()
+    assert b"gfx950" in blob
+
+
+def test_no_device_behaviour(hipann_mod):
+    if hipann_mod.is_available():
+        pytest.skip("a GPU is present; no-device behaviour not observable")
+    L = hipann_mod.lib()
+    assert L.hipann_available() == 0
+    assert L.diskann_hip_available() == 0 and L.diskann_metal_available() == 0
+    assert "no" in hipann_mod.device_info().lower()
+    eb = C.create_string_buffer(256)
+    x = np.zeros((4, 3), np.float32)
+    h = L.hipann_flat_create(3, 0, x.ctypes.data_as(C.POINTER(C.c_float)), 4, None, 0, eb, 256)
+    assert not h and b"no HIP device" in eb.value
+    q = np.zeros(3, np.float32)
+    out = np.zeros(4, np.float32)
+    assert hipann_mod.diskann_hip_batch_distances(q, x, 4, 3, 0, out) == -1
+    assert not hipann_mod.hip_batch_distances(q, np.zeros((200, 1024), np.float32), 200, 1024, 0,
+                                              np.zeros(200, np.float32))
+    with pytest.raises(hipann_mod.HipAnnError):
+        hipann_mod.HipIndexFlat(3, 0, x)
+    be = hipann_mod.get_gpu_backend()
+    assert be.backend_name() == "hip" and not be.is_available()
+    assert be.device_info() == "HIP: not available"
+    with pytest.raises(RuntimeError):
+        be.cpu_to_gpu({"type": "Flat", "d": 3, "xb": x})
+
+
+def test_argument_validation_precedes_device(hipann_mod):
+    """Invalid arguments return -1 (metal_diskann_bridge.mm:162-164, :262-265) with or without a GPU."""
+    q = np.zeros(8, np.float32)
+    c = np.zeros((4, 8), np.float32)
+    out = np.zeros(4, np.float32)
+    assert hipann_mod.diskann_hip_batch_distances(q, c, 0, 8, 0, out) == -1
+    assert hipann_mod.diskann_hip_batch_distances(q, c, 4, 0, 0, out) == -1
+    assert hipann_mod.diskann_hip_batch_distances(q, c, 4, 8, 2, out) == -1
+    m = np.zeros(4, np.uint32)
+    assert hipann_mod.diskann_hip_multi_batch_distances(q, c, m, 4, 0, 8, 0, out) == -1
+    L = hipann_mod.lib()
+    assert L.diskann_metal_batch_distances(None, None, 4, 8, 0, None) == -1
+    # wrappers follow metal_ffi.rs: empty work is a successful no-op
+    assert hipann_mod.hip_batch_distances(q, c, 0, 8, 0, out)
+    assert hipann_mod.hip_multi_batch_distances(q, c, m, 0, 1, 8, 0, out)
+
+
+def test_min_gpu_work_gate(hipann_mod):
+    """metal_ffi.rs:78 — the single-query wrapper declines work below MIN_GPU_WORK (CPU computes it)."""
+    n, d = 64, 128  # 8192 < 131072
+    assert not hipann_mod.hip_batch_distances(np.zeros(d, np.float32), np.zeros((n, d), np.float32), n, d, 0,
+                                              np.zeros(n, np.float32))
+
+
+def test_free_null_is_noop(hipann_mod):
+    L = hipann_mod.lib()
+    L.hipann_free(None)
+    L.diskann_hip_release_db(None)
+    assert L.hipann_ntotal(None) == -1

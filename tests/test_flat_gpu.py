@@ -1,0 +1,242 @@
+"""GPU parity tests of the Flat path (libhipann.so) against the oracle (FAISS IndexFlat restatement).
+
+Mirrors faiss-metal/tests/test_metal_flat.mm (same shapes, same std::mt19937(42) inputs, k up to 128)
+but with a stricter pass rule than the reference's "top-1 exact" (test_metal_flat.mm:24-60): full
+id/order parity except inside near-tie windows (tests/_data.py check_topk_parity).
+"""
+from __future__ import annotations
+
+import json
+import sys
+import threading
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from _data import check_topk_parity, faiss_metal_case, mt19937_uniform
+
+pytestmark = pytest.mark.gpu
+GOLD = Path(__file__).resolve().parent / "golden"
+SQL = json.loads((GOLD / "sql_known_answers.json").read_text())
+sys.path.insert(0, str(GOLD))
+from make_golden import FLAT_CASES  # noqa: E402
+
+
+@pytest.mark.parametrize("nv,nq,d,k,metric", FLAT_CASES)
+def test_flat_faiss_metal_shapes(gpu, oracle, nv, nq, d, k, metric):
+    xb, xq = faiss_metal_case(nv, nq, d)
+    ix = gpu.HipIndexFlat(d, metric, xb)
+    D, I = ix.search(xq, k)
+    z = np.load(GOLD / "flat_mt19937.npz")
+    key = f"flat_{nv}_{nq}_{d}_{k}_{metric}"
+    Io, Do = z[key + "_I"].astype(np.int64), z[key + "_D"]
+    check_topk_parity(xb, xq, D, I, Do, Io, metric)
+    assert (I[:, 0] == Io[:, 0]).all(), "top-1 must match exactly (test_metal_flat.mm:51-59)"
+
+
+@pytest.mark.parametrize("name", [k for k in SQL if k.startswith(("faiss_basic", "edge_"))])
+def test_flat_sql_known_answers(gpu, name):
+    case = SQL[name]
+    xb = np.array(case["xb"], np.float32)
+    deleted = set(case.get("deleted", []))
+    ix = gpu.HipIndexFlat(xb.shape[1], case["metric"], xb)
+    for qc in case["queries"]:
+        k = qc["k"]
+        req = min(k + len(deleted), len(xb))  # FaissIndex::Search (src/faiss_index.cpp:713-716)
+        D, I = ix.search(np.array([qc["q"]], np.float32), req)
+        keep = [(d, i) for d, i in zip(D[0], I[0]) if i >= 0 and i not in deleted][:k]
+        ids = [int(i) for _, i in keep]
+        dists = [float(d) for d, _ in keep]
+        if "ids" in qc:
+            assert ids == qc["ids"], (ids, qc)
+        if "dists" in qc:
+            assert np.allclose(dists, qc["dists"], rtol=2.5e-7, atol=1e-9), (dists, qc["dists"])
+        if "n_below_0.01" in qc:
+            assert sum(d < 0.01 for d in dists) == qc["n_below_0.01"]
+        if "n_results" in qc:
+            assert len(ids) == qc["n_results"]
+
+
+@pytest.mark.parametrize("nq", [1, 19, 20, 21, 127, 128, 129, 300])
+@pytest.mark.parametrize("metric", [0, 1])
+def test_flat_batch_sizes_across_blas_threshold(gpu, oracle, nq, metric):
+    xb, xq = faiss_metal_case(4000, nq, 64)
+    ix = gpu.HipIndexFlat(64, metric, xb)
+    D, I = ix.search(xq, 10)
+    Do, Io = oracle.flat_search(xb, xq, 10, metric)
+    check_topk_parity(xb, xq, D, I, Do, Io, metric)
+
+
+@pytest.mark.parametrize("d", [1, 3, 5, 31, 33, 100, 130, 2048])
+def test_flat_odd_dimensions(gpu, oracle, d):
+    xb, xq = faiss_metal_case(700, 24, d)
+    for nq in (3, 24):
+        ix = gpu.HipIndexFlat(d, 0, xb)
+        D, I = ix.search(xq[:nq], 7)
+        Do, Io = oracle.flat_search(xb, xq[:nq], 7)
+        check_topk_parity(xb, xq[:nq], D, I, Do, Io, 0, min_exact=0.97 if d <= 3 else 0.99)
+
+
+@pytest.mark.parametrize("k", [1, 63, 64, 65, 200, 1000, 2048])
+def test_flat_k_range(gpu, oracle, k):
+    xb, xq = faiss_metal_case(5000, 22, 32)
+    for nq in (4, 22):
+        ix = gpu.HipIndexFlat(32, 0, xb)
+        D, I = ix.search(xq[:nq], k)
+        Do, Io = oracle.flat_search(xb, xq[:nq], k)
+        check_topk_parity(xb, xq[:nq], D, I, Do, Io, 0, min_exact=0.98)
+
+
+def test_flat_k_greater_than_ntotal_pads(gpu):
+    xb = np.array([[1, 0, 0], [0, 1, 0]], np.float32)
+    for metric, pad in ((0, np.inf), (1, -np.inf)):
+        ix = gpu.HipIndexFlat(3, metric, xb)
+        for nq in (1, 25):
+            D, I = ix.search(np.tile(np.array([[1, 0, 0]], np.float32), (nq, 1)), 100)
+            assert I.shape == (nq, 100)
+            assert (I[:, :2] == [0, 1]).all() and (I[:, 2:] == -1).all()
+            assert (D[:, 2:] == pad).all()   # MetalIndexFlat.mm:355-368 sentinels
+
+
+def test_flat_empty_index_and_batch(gpu):
+    ix = gpu.HipIndexFlat(8, 0)
+    D, I = ix.search(np.zeros((3, 8), np.float32), 4)
+    assert (I == -1).all() and np.isinf(D).all() and (D > 0).all()
+    D, I = ix.search(np.zeros((0, 8), np.float32), 4)
+    assert D.shape == (0, 4)
+    ix.add(np.eye(8, dtype=np.float32))
+    with pytest.raises(gpu.HipAnnError):
+        ix.search(np.zeros((1, 8), np.float32), 0)      # k <= 0 throws (MetalIndexFlat.mm:297)
+    with pytest.raises(gpu.HipAnnError):
+        ix.search(np.zeros((1, 8), np.float32), gpu.MAX_K + 1)
+    with pytest.raises(ValueError):
+        ix.search(np.zeros((1, 7), np.float32), 1)
+
+
+def test_flat_incremental_add_and_reconstruct(gpu, oracle):
+    xb, xq = faiss_metal_case(3000, 30, 40)
+    ix = gpu.HipIndexFlat(40, 0)
+    for s in range(0, 3000, 700):
+        ix.add(xb[s:s + 700])
+    assert ix.ntotal == 3000
+    assert np.array_equal(ix.reconstruct(1234), xb[1234])
+    D, I = ix.search(xq, 10)
+    Do, Io = oracle.flat_search(xb, xq, 10)
+    check_topk_parity(xb, xq, D, I, Do, Io)
+
+
+def test_flat_ties_order_by_label(gpu):
+    # 300 identical rows: every distance ties; FAISS returns the lowest labels in label order
+    xb = np.tile(np.array([[0.5, -0.25, 1.0, 0.0]], np.float32), (300, 1))
+    ix = gpu.HipIndexFlat(4, 0, xb)
+    for nq in (1, 40):
+        D, I = ix.search(np.zeros((nq, 4), np.float32), 37)
+        assert (I == np.arange(37)).all()
+
+
+def test_flat_multi_shard_same_device(gpu, oracle):
+    """Rows sharded over devices [0, 0] (two shards on one GPU) → peer gather + device merge."""
+    xb, xq = faiss_metal_case(5001, 30, 64)
+    ix = gpu.HipIndexFlat(64, 0, xb, devices=[0, 0])
+    D, I = ix.search(xq, 10)
+    Do, Io = oracle.flat_search(xb, xq, 10)
+    check_topk_parity(xb, xq, D, I, Do, Io)
+    D1, I1 = ix.search(xq[:5], 10)
+    check_topk_parity(xb, xq[:5], D1, I1, Do[:5], Io[:5])
+
+
+def test_flat_device_api_and_merge(gpu, oracle):
+    import torch
+    xb, xq = faiss_metal_case(6000, 64, 96)
+    dev = torch.device("cuda", 0)
+    xb_t = torch.from_numpy(xb).to(dev)
+    xq_t = torch.from_numpy(xq).to(dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    parts_D, parts_I = [], []
+    for lo, hi in ((0, 2500), (2500, 6000)):   # two "ranks"
+        sh = gpu.HipIndexFlatDevice(96, 0, xb_t[lo:hi].data_ptr(), hi - lo, 0, copy=False, label_offset=lo)
+        Dp = torch.empty((64, 10), device=dev)
+        Ip = torch.empty((64, 10), device=dev, dtype=torch.int64)
+        sh.search_device(64, xq_t.data_ptr(), 10, Dp.data_ptr(), Ip.data_ptr(), stream)
+        torch.cuda.synchronize()
+        parts_D.append(Dp)
+        parts_I.append(Ip)
+        sh.close()
+    Da, Ia = torch.stack(parts_D).contiguous(), torch.stack(parts_I).contiguous()
+    D = torch.empty((64, 10), device=dev)
+    I = torch.empty((64, 10), device=dev, dtype=torch.int64)
+    gpu.merge_topk_device(0, 2, 64, 10, Da.data_ptr(), Ia.data_ptr(), D.data_ptr(), I.data_ptr(), stream)
+    torch.cuda.synchronize()
+    Do, Io = oracle.flat_search(xb, xq, 10)
+    check_topk_parity(xb, xq, D.cpu().numpy(), I.cpu().numpy(), Do, Io)
+
+
+def test_merge_kernel_lexicographic(gpu):
+    """merge_topk_device = k smallest (key, label) of the union; pads (-1) ignored; IP descending."""
+    import torch
+    rng = np.random.default_rng(3)
+    for metric in (0, 1):
+        P, nq, k = 5, 33, 17
+        D = rng.integers(0, 6, (P, nq, k)).astype(np.float32)  # many exact ties
+        I = rng.permutation(P * nq * k).reshape(P, nq, k).astype(np.int64)
+        I[rng.random((P, nq, k)) < 0.1] = -1
+        dev = torch.device("cuda", 0)
+        Dt, It = torch.from_numpy(D).to(dev), torch.from_numpy(I).to(dev)
+        Do = torch.empty((nq, k), device=dev)
+        Io = torch.empty((nq, k), device=dev, dtype=torch.int64)
+        gpu.merge_topk_device(metric, P, nq, k, Dt.data_ptr(), It.data_ptr(), Do.data_ptr(), Io.data_ptr(), 0)
+        torch.cuda.synchronize()
+        Do, Io = Do.cpu().numpy(), Io.cpu().numpy()
+        for q in range(nq):
+            c = sorted(((D[p, q, j] if metric == 0 else -D[p, q, j]), I[p, q, j])
+                       for p in range(P) for j in range(k) if I[p, q, j] >= 0)[:k]
+            assert Io[q].tolist() == [lab for _, lab in c] + [-1] * (k - len(c))
+
+
+def test_flat_concurrent_searches_one_handle(gpu, oracle):
+    xb, xq = faiss_metal_case(3000, 50, 64)
+    ix = gpu.HipIndexFlat(64, 0, xb)
+    ref = ix.search(xq, 10)
+    out = [None] * 8
+
+    def run(t):
+        out[t] = ix.search(xq, 10)
+
+    ts = [threading.Thread(target=run, args=(t,)) for t in range(8)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    for o in out:
+        assert np.array_equal(o[1], ref[1]) and np.array_equal(o[0], ref[0])
+
+
+def test_flat_backend_cpu_to_gpu(gpu, oracle):
+    be = gpu.get_gpu_backend()
+    assert be.is_available() and be.backend_name() == "hip" and "gfx950" in be.device_info()
+    xb, xq = faiss_metal_case(1000, 10, 32)
+    g = be.cpu_to_gpu({"type": "Flat", "d": 32, "metric": 0, "xb": xb})
+    D, I = g.search(xq, 5)
+    Do, Io = oracle.flat_search(xb, xq, 5)
+    check_topk_parity(xb, xq, D, I, Do, Io)
+    back = be.gpu_to_cpu(g)
+    assert np.array_equal(back["xb"], xb)
+    with pytest.raises(RuntimeError):
+        be.cpu_to_gpu({"type": "HNSW"})
+
+
+def test_flat_large_properties(gpu, oracle):
+    """200k x 768, nq = 1024 (BLAS form): self-queries find themselves at ~0, the output is sorted, and a
+    query subset matches the oracle."""
+    import torch
+    n, d, nq = 200_000, 768, 1024
+    g = torch.Generator().manual_seed(5)
+    xb = (torch.rand((n, d), generator=g) * 2 - 1).numpy()
+    sel = np.arange(0, n, n // nq)[:nq]
+    xq = xb[sel].copy()
+    ix = gpu.HipIndexFlat(d, 0, xb)
+    D, I = ix.search(xq, 10)
+    assert (I[:, 0] == sel).all()
+    assert (np.abs(D[:, 0]) < 1e-2).all()
+    assert (np.diff(D, axis=1) >= 0).all()
+    Do, Io = oracle.flat_search(xb, xq[:64], 10)  # oracle BLAS path on a 64-query subset
+    check_topk_parity(xb, xq[:64], D[:64], I[:64], Do, Io)

@@ -1,0 +1,169 @@
+"""GPU parity tests of the IVFFlat path against the oracle (FAISS IndexIVFFlat::search restatement).
+
+Given identical centroids and inverted lists, the GPU must choose identical probe lists and return the
+oracle's ids under the Flat parity rule over the scanned set.  Shapes follow
+faiss-metal/tests/test_metal_ivfflat.mm:28-166 (nv=2000, d=64, nlist=16, nprobe=4).
+"""
+from __future__ import annotations
+
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from _data import build_ivf_lists, check_topk_parity, faiss_metal_case
+
+pytestmark = pytest.mark.gpu
+GOLD = Path(__file__).resolve().parent / "golden"
+SQL = json.loads((GOLD / "sql_known_answers.json").read_text())
+sys.path.insert(0, str(GOLD))
+from make_golden import IVF_CASES  # noqa: E402
+
+
+def _ivf(gpu, xb, nlist, nprobe, metric=0, devices=None, stride=None):
+    cen = np.ascontiguousarray(xb[:: (stride or len(xb) // nlist)][:nlist])
+    off, ids, codes = build_ivf_lists(xb, cen, metric)
+    return gpu.HipIndexIVFFlat(cen, off, ids, codes, nprobe, metric, devices=devices), (cen, off, ids, codes)
+
+
+@pytest.mark.parametrize("nv,d,nlist,nprobe,nq,k,metric", IVF_CASES)
+def test_ivf_faiss_metal_shapes(gpu, oracle, nv, d, nlist, nprobe, nq, k, metric):
+    xb, xq = faiss_metal_case(nv, nq, d)
+    ix, (cen, off, ids, codes) = _ivf(gpu, xb, nlist, nprobe, metric)
+    D, I = ix.search(xq, k)
+    z = np.load(GOLD / "ivf_mt19937.npz")
+    key = f"ivf_{nv}_{d}_{nlist}_{nprobe}_{nq}_{k}_{metric}"
+    assert np.array_equal(ix.last_probes(nq), z[key + "_P"].astype(np.int64))
+    check_topk_parity(xb, xq, D, I, z[key + "_D"], z[key + "_I"].astype(np.int64), metric)
+
+
+@pytest.mark.parametrize("nq", [1, 7, 19, 20, 64, 333])
+@pytest.mark.parametrize("metric", [0, 1])
+def test_ivf_vs_oracle_probe_sets(gpu, oracle, nq, metric):
+    xb, xq = faiss_metal_case(20000, nq, 96)
+    ix, (cen, off, ids, codes) = _ivf(gpu, xb, 64, 8, metric)
+    D, I = ix.search(xq, 10)
+    Do, Io, Po = oracle.ivf_search(cen, off, ids, codes, xq, 10, 8, metric)
+    assert np.array_equal(ix.last_probes(nq), Po)
+    check_topk_parity(xb, xq, D, I, Do, Io, metric)
+
+
+def test_ivf_full_probe_equals_flat(gpu, oracle):
+    xb, xq = faiss_metal_case(6000, 50, 48)
+    ix, _ = _ivf(gpu, xb, 32, 32)
+    D, I = ix.search(xq, 10)
+    fl = gpu.HipIndexFlat(48, 0, xb)
+    Df, If = fl.search(xq[:10], 10)       # direct form, like the IVF scan (summation order differs)
+    assert (I[:10] == If).mean() > 0.99
+    assert np.allclose(D[:10], Df, rtol=1e-5, atol=1e-5)
+    Do, Io = oracle.flat_search(xb, xq, 10)
+    check_topk_parity(xb, xq, D, I, Do, Io)
+
+
+def test_ivf_sql_known_answer(gpu):
+    case = SQL["faiss_ivfflat_exact"]
+    xb = np.array(case["xb"], np.float32)
+    cen = xb[[0, 4]].copy()
+    off, ids, codes = build_ivf_lists(xb, cen)
+    ix = gpu.HipIndexIVFFlat(cen, off, ids, codes, case["nprobe"])
+    for qc in case["queries"]:
+        D, I = ix.search(np.array([qc["q"]], np.float32), qc["k"])
+        assert I[0].tolist() == qc["ids"]
+        if "dists" in qc:
+            assert np.allclose(D[0], qc["dists"])
+
+
+def test_ivf_edge_cases(gpu, oracle):
+    xb, xq = faiss_metal_case(3000, 25, 40)
+    cen = np.ascontiguousarray(xb[:20])
+    off, ids, codes = build_ivf_lists(xb, cen)
+    # add empty lists: centroids far away
+    cen2 = np.vstack([cen, np.full((4, 40), 50.0, np.float32)])
+    off2 = np.concatenate([off, np.full(4, off[-1])])
+    ix = gpu.HipIndexIVFFlat(cen2, off2, ids, codes, 30)  # nprobe > nlist → clamped (IndexIVF::search)
+    D, I = ix.search(xq, 10)
+    Do, Io, Po = oracle.ivf_search(cen2, off2, ids, codes, xq, 10, 30)
+    assert np.array_equal(ix.last_probes(25), Po)
+    check_topk_parity(xb, xq, D, I, Do, Io)
+    # k larger than the scanned set → pads
+    ix.nprobe = 1
+    D, I = ix.search(xq[:3], 64)
+    Do, Io, _ = oracle.ivf_search(cen2, off2, ids, codes, xq[:3], 64, 1)
+    assert np.array_equal(I < 0, Io < 0)
+    # empty index
+    e = gpu.HipIndexIVFFlat(cen, np.zeros(21, np.int64), np.zeros(0, np.int64), np.zeros((0, 40), np.float32), 4)
+    D, I = e.search(xq[:2], 5)
+    assert (I == -1).all()
+    with pytest.raises(gpu.HipAnnError):
+        ix.search(xq[:1], 0)
+    with pytest.raises(gpu.HipAnnError):
+        ix.nprobe = 0
+
+
+def test_ivf_labels_are_stored_ids(gpu, oracle):
+    """index_cpu_to_metal_ivf copies per-list ids; results are those labels (MetalIndexIVFFlat.mm:243-250)."""
+    xb, xq = faiss_metal_case(2000, 8, 32)
+    cen = np.ascontiguousarray(xb[::200][:10])
+    off, ids, codes = build_ivf_lists(xb, cen)
+    labels = ids * 7 + 1_000_000_000_000  # arbitrary int64 labels
+    ix = gpu.HipIndexIVFFlat(cen, off, labels, codes, 10)
+    D, I = ix.search(xq, 5)
+    Do, Io, _ = oracle.ivf_search(cen, off, labels, codes, xq, 5, 10)
+    assert np.array_equal(I, Io)
+
+
+def test_ivf_multi_shard_same_device(gpu, oracle):
+    xb, xq = faiss_metal_case(8000, 40, 64)
+    ix, (cen, off, ids, codes) = _ivf(gpu, xb, 32, 6, devices=[0, 0])
+    D, I = ix.search(xq, 10)
+    Do, Io, _ = oracle.ivf_search(cen, off, ids, codes, xq, 10, 6)
+    check_topk_parity(xb, xq, D, I, Do, Io)
+
+
+def test_ivf_backend_and_device_api(gpu, oracle):
+    import torch
+    xb, xq = faiss_metal_case(10000, 100, 128)
+    cen = np.ascontiguousarray(xb[::100][:100])
+    off, ids, codes = build_ivf_lists(xb, cen)
+    g = gpu.get_gpu_backend().cpu_to_gpu({"type": "IVFFlat", "centroids": cen, "list_offsets": off, "ids": ids,
+                                          "codes": codes, "nprobe": 8})
+    D, I = g.search(xq, 10)
+    Do, Io, _ = oracle.ivf_search(cen, off, ids, codes, xq, 10, 8)
+    check_topk_parity(xb, xq, D, I, Do, Io)
+    dev = torch.device("cuda", 0)
+    c_t, i_t, x_t = (torch.from_numpy(a).to(dev) for a in (cen, ids, codes))
+    q_t = torch.from_numpy(xq).to(dev)
+    ix = gpu.HipIndexIVFFlat.from_device(128, 0, 100, 8, c_t.data_ptr(), off, i_t.data_ptr(), x_t.data_ptr(), 0)
+    Dt = torch.empty((100, 10), device=dev)
+    It = torch.empty((100, 10), device=dev, dtype=torch.int64)
+    ix.search_device(100, q_t.data_ptr(), 10, Dt.data_ptr(), It.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(It.cpu().numpy(), I) and np.array_equal(Dt.cpu().numpy(), D)
+
+
+def test_ivf_gpu_build_recall(gpu):
+    """ivf_build (GPU k-means + assignment + list sort) on clustered data: recall@10 vs exact ≥ 0.95."""
+    import torch
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    from ivf_build import build_ivf_shard, flat_ground_truth
+    import bench
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(7)
+    d, n = 64, 200_000
+    centres = torch.rand((256, d), generator=g, device=dev) * 2 - 1
+    xb = torch.empty((n, d), device=dev)
+    bench.gen_clustered_rows(torch, xb, 0, centres, 0.25, 42)
+    a = torch.randint(0, 256, (200,), generator=g, device=dev)
+    xq = (centres[a] + torch.randn((200, d), generator=g, device=dev) * 0.25).contiguous()
+    ix, info = build_ivf_shard(torch, gpu, xb, 0, n, 64, 8, 0, 0, 1)
+    stream = torch.cuda.current_stream().cuda_stream
+    D = torch.empty((200, 10), device=dev)
+    I = torch.empty((200, 10), device=dev, dtype=torch.int64)
+    ix.search_device(200, xq.data_ptr(), 10, D.data_ptr(), I.data_ptr(), stream)
+    gt = flat_ground_truth(torch, gpu, d, 0, xq, 10, n, 0, 1, ivf_info_tensor=ix)
+    got = I.cpu().numpy()
+    recall = np.mean([len(set(got[i]) & set(gt[i])) / 10 for i in range(200)])
+    assert recall >= 0.95, recall
+    assert info["list_size_min"] >= 0 and sum(np.diff(ix._offsets)) == n

@@ -1,0 +1,245 @@
+"""CPU tests of the oracle (the FAISS / DiskANN restatement used as the parity checker).
+
+Pins the oracle to everything the reference itself provides for this path: the SQL known answers
+(tests/golden/sql_known_answers.json, copied from test/sql/*.test) and the input generator of
+faiss-metal's GPU-vs-CPU tests (std::mt19937(42)), plus internal consistency checks.
+"""
+from __future__ import annotations
+
+import json
+import shutil
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from _data import build_ivf_lists, faiss_metal_case, mt19937_uniform
+
+GOLD = Path(__file__).resolve().parent / "golden"
+SQL = json.loads((GOLD / "sql_known_answers.json").read_text())
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="g++ not available")
+def test_mt19937_matches_libstdcxx(tmp_path):
+    src = tmp_path / "mt.cpp"
+    src.write_text('#include <random>\n#include <cstdio>\nint main(){std::mt19937 r(42);'
+                   'std::uniform_real_distribution<float> d(-1.0f,1.0f);'
+                   'for(int i=0;i<4096;i++) printf("%a\\n", d(r));}\n')
+    exe = tmp_path / "mt"
+    subprocess.run(["g++", "-O2", "-o", str(exe), str(src)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
+    ref = np.array([float.fromhex(v) for v in out], np.float32)
+    assert np.array_equal(ref, mt19937_uniform(4096))
+
+
+def _flat_entries():
+    return [(k, v) for k, v in SQL.items() if k.startswith(("faiss_basic", "edge_"))]
+
+
+@pytest.mark.parametrize("name,case", _flat_entries())
+def test_oracle_sql_known_answers_flat(oracle, name, case):
+    xb = np.array(case["xb"], np.float32)
+    deleted = set(case.get("deleted", []))
+    for qc in case["queries"]:
+        q = np.array([qc["q"]], np.float32)
+        k = qc["k"]
+        req = min(k + len(deleted), len(xb))  # FaissIndex::Search request_k (faiss_index.cpp:713-716)
+        D, I = oracle.flat_search(xb, q, req, case["metric"])
+        keep = [(d, i) for d, i in zip(D[0], I[0]) if i >= 0 and i not in deleted][:k]
+        ids = [i for _, i in keep]
+        dists = [d for d, _ in keep]
+        if "ids" in qc:
+            assert ids == qc["ids"][: len(ids)] and len(ids) == len(qc["ids"]), (ids, qc)
+        if "dists" in qc:
+            # ≤ 5 ulp: the reference printed 0.020000001 for |[1,0,0] − [0.9f,0.1f,0]|² whose exact
+            # value is 0.0200000050664; the direct fp32 form gives 0.020000005 (Oracle).
+            assert np.allclose(dists, qc["dists"], rtol=2.5e-7, atol=1e-9), (dists, qc["dists"])
+        if "n_below_0.01" in qc:
+            assert sum(d < 0.01 for d in dists) == qc["n_below_0.01"]
+        if "n_results" in qc:
+            assert len(ids) == qc["n_results"]
+
+
+def test_oracle_sql_ivfflat_exact(oracle):
+    case = SQL["faiss_ivfflat_exact"]
+    xb = np.array(case["xb"], np.float32)
+    cen = xb[[0, 4]].copy()  # any 2 centroids: nprobe = nlist makes the result exact
+    off, ids, codes = build_ivf_lists(xb, cen)
+    for qc in case["queries"]:
+        D, I, P = oracle.ivf_search(cen, off, ids, codes, np.array([qc["q"]], np.float32), qc["k"], 2)
+        assert I[0].tolist() == qc["ids"]
+        if "dists" in qc:
+            assert np.allclose(D[0], qc["dists"])
+
+
+def test_oracle_pads_and_ties(oracle):
+    xb = np.array([[1, 0], [1, 0], [0, 1]], np.float32)
+    D, I = oracle.flat_search(xb, np.array([[1, 0]], np.float32), 5)
+    assert I[0].tolist() == [0, 1, 2, -1, -1]  # tie → lower label first; pads (FLT_MAX, -1)
+    assert D[0, 3] == np.finfo(np.float32).max
+    D, I = oracle.flat_search(xb, np.array([[1, 0]], np.float32), 5, metric=1)
+    assert I[0].tolist() == [0, 1, 2, -1, -1] and D[0, 3] == -np.finfo(np.float32).max
+    # strict admission: a full heap keeps the earlier label on an exact tie at the boundary
+    D, I = oracle.flat_search(xb, np.array([[1, 0]], np.float32), 1)
+    assert I[0].tolist() == [0]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _golden_path():
+    import sys
+    sys.path.insert(0, str(GOLD))
+    yield
+
+
+def test_oracle_regression_flat(oracle):
+    from make_golden import FLAT_CASES
+    z = np.load(GOLD / "flat_mt19937.npz")
+    for (nv, nq, d, k, m) in FLAT_CASES:
+        xb, xq = faiss_metal_case(nv, nq, d)
+        D, I = oracle.flat_search(xb, xq, k, m)
+        key = f"flat_{nv}_{nq}_{d}_{k}_{m}"
+        assert np.array_equal(I, z[key + "_I"]), key
+        assert np.allclose(D, z[key + "_D"], rtol=1e-6, atol=1e-6), key
+
+
+def test_oracle_regression_ivf(oracle):
+    from make_golden import IVF_CASES
+    z = np.load(GOLD / "ivf_mt19937.npz")
+    for (nv, d, nlist, nprobe, nq, k, m) in IVF_CASES:
+        xb, xq = faiss_metal_case(nv, nq, d)
+        cen = np.ascontiguousarray(xb[:: nv // nlist][:nlist])
+        off, ids, codes = build_ivf_lists(xb, cen, m)
+        D, I, P = oracle.ivf_search(cen, off, ids, codes, xq, k, nprobe, m)
+        key = f"ivf_{nv}_{d}_{nlist}_{nprobe}_{nq}_{k}_{m}"
+        assert np.array_equal(P, z[key + "_P"]) and np.array_equal(I, z[key + "_I"]), key
+        assert np.array_equal(off, z[key + "_off"])
+
+
+def test_oracle_blas_vs_direct_forms_agree(oracle):
+    """nq < 20 (direct) and nq >= 20 (norms + GEMM) must give the same neighbours up to near ties."""
+    xb, xq = faiss_metal_case(3000, 40, 96)
+    Db, Ib = oracle.flat_search(xb, xq, 10)          # BLAS form
+    Dd = np.empty_like(Db)
+    Id = np.empty_like(Ib)
+    for s in range(0, 40, 10):
+        Dd[s:s + 10], Id[s:s + 10] = oracle.flat_search(xb, xq[s:s + 10], 10)  # direct form
+    assert (Ib == Id).mean() > 0.99
+    assert np.allclose(Db, Dd, rtol=1e-4, atol=1e-4)
+
+
+def test_oracle_ivf_full_probe_equals_flat(oracle):
+    xb, xq = faiss_metal_case(2000, 10, 64)
+    cen = np.ascontiguousarray(xb[::125][:16])
+    off, ids, codes = build_ivf_lists(xb, cen)
+    D, I, _ = oracle.ivf_search(cen, off, ids, codes, xq, 10, 16)
+    Df, If = oracle.flat_search(xb, xq, 10)  # nq < 20: same direct distance as the IVF scan
+    assert np.array_equal(I, If)
+    assert np.array_equal(D, Df)
+
+
+def test_oracle_sq8_codec(oracle):
+    z = np.load(GOLD / "sq8_qvectors.npz")
+    xb = np.array(SQL["diskann_sq8_top1"]["xb"], np.float32)
+    mins, scale = oracle.sq8_train(xb)
+    codes = oracle.sq8_encode(xb, mins, scale)
+    dec = oracle.sq8_decode(codes, mins, scale)
+    assert np.array_equal(codes, z["codes"]) and np.array_equal(dec, z["decoded"])
+    assert np.all(np.abs(dec - xb) <= scale / 255 / 2 + 1e-7)
+    # constant dimension → scale 1 (provider.rs:187-190)
+    m2, s2 = oracle.sq8_train(np.ones((3, 2), np.float32))
+    assert s2.tolist() == [1.0, 1.0] and m2.tolist() == [1.0, 1.0]
+    # rounding: half away from zero, clamped
+    c = oracle.sq8_encode(np.array([[0.5 / 255], [2.0], [-1.0]], np.float32), np.array([0.0], np.float32),
+                          np.array([1.0], np.float32))
+    assert c[:, 0].tolist() == [1, 255, 0]
+
+
+def test_oracle_sql_diskann_known_answers(oracle):
+    case = SQL["diskann_batch"]
+    xb = np.array(case["xb"], np.float32)
+    n = len(xb)
+    adj = np.array([[j for j in range(n) if j != i] for i in range(n)], np.uint32)  # complete graph
+    qs = np.array([qc["q"] for qc in case["queries"]], np.float32)
+    ids, dists, _ = oracle.diskann_search_batch(adj, [0], qs, 2, 8, vecs=xb)
+    for i, qc in enumerate(case["queries"]):
+        assert ids[i].tolist() == qc["ids"] and np.allclose(dists[i], qc["dists"])
+    sq = SQL["diskann_sq8_top1"]
+    xb = np.array(sq["xb"], np.float32)
+    n = len(xb)
+    adj = np.array([[j for j in range(n) if j != i] for i in range(n)], np.uint32)
+    mins, scale = oracle.sq8_train(xb)
+    codes = oracle.sq8_encode(xb, mins, scale)
+    qs = np.array([qc["q"] for qc in sq["queries"]], np.float32)
+    ids, _, _ = oracle.diskann_search_batch(adj, [0], qs, 3, 8, codes=codes, mins=mins, scale=scale)
+    assert [r[0] for r in ids.tolist()] == [qc["top1"] for qc in sq["queries"]]
+
+
+def test_oracle_bfs_regression_and_quality(oracle):
+    z = np.load(GOLD / "bfs_2k.npz")
+    a = mt19937_uniform(2000 * 32 + 20 * 32, seed=7)
+    x, qs = a[: 2000 * 32].reshape(2000, 32), a[2000 * 32:].reshape(20, 32)
+    ids, dists, st = oracle.diskann_search_batch(z["adj"], [0, 999], qs, 10, 48, vecs=x)
+    assert np.array_equal(ids, z["ids"]) and np.array_equal(dists, z["dists"])
+    assert [st["evals"], st["steps"]] == z["stats"].tolist()
+    _, ex = oracle.flat_search(x, qs, 10)
+    recall = np.mean([len(set(ids[i]) & set(ex[i])) / 10 for i in range(20)])
+    assert recall > 0.8
+
+
+def test_rust_binary_search_semantics():
+    """The oracle's insert_result uses Rust's binary_search_by (std >= 1.82); restated in Python."""
+    def bs(a, x):
+        size, base = len(a), 0
+        if size == 0:
+            return 0
+        while size > 1:
+            half = size // 2
+            mid = base + half
+            base = base if a[mid] > x else mid
+            size -= half
+        if not (a[base] < x) and not (a[base] > x):
+            return base
+        return base + (1 if a[base] < x else 0)
+    import bisect
+    rng = np.random.default_rng(1)
+    for _ in range(500):
+        a = sorted(rng.integers(0, 20, rng.integers(0, 30)).tolist())
+        x = int(rng.integers(-1, 21))
+        p = bs(a, x)
+        assert bisect.bisect_left(a, x) <= p <= bisect.bisect_right(a, x)
+
+
+def test_diskann_file_roundtrip(tmp_path):
+    import diskann_format as F
+    x = mt19937_uniform(50 * 8).reshape(50, 8)
+    adj = np.full((50, 4), 0xFFFFFFFF, np.uint32)
+    adj[:, :3] = (np.arange(50)[:, None] + np.arange(1, 4)[None, :]) % 50
+    mins, scale = x.min(0), x.max(0) - x.min(0)
+    codes = np.round((x - mins) / scale * 255).clip(0, 255).astype(np.uint8)
+    p = tmp_path / "t.diskann"
+    F.write_index(p, x, adj, [0, 7], metric=1, build_complexity=64, sq8=(mins, scale, codes))
+    f = F.open_index(p)
+    assert (f.num_vectors, f.dimension, f.max_degree, f.metric, f.build_complexity) == (50, 8, 4, 1, 64)
+    assert f.entry_points.tolist() == [0, 7]
+    assert np.array_equal(f.vectors, x) and np.array_equal(f.adjacency, adj)
+    assert f.neighbors(3).tolist() == [4, 5, 6]
+    assert np.array_equal(f.sq8_codes, codes) and np.array_equal(f.sq8_min, mins)
+    raw = p.read_bytes()
+    (tmp_path / "bad.diskann").write_bytes(b"XANN" + raw[4:])
+    with pytest.raises(ValueError, match="magic"):
+        F.open_index(tmp_path / "bad.diskann")
+    (tmp_path / "short.diskann").write_bytes(raw[:100])
+    with pytest.raises(ValueError, match="too small"):
+        F.open_index(tmp_path / "short.diskann")
+
+
+def test_cpu_baseline_leg_runs():
+    from oracle import cpu_baseline as CB
+    xb, xq = faiss_metal_case(3000, 32, 64)
+    qps, dt, nth = CB.flat_blas_qps(xb, xq, 10, 3000)
+    assert qps > 0 and nth >= 1
+    cen = np.ascontiguousarray(xb[::300][:10])
+    off, ids, codes = build_ivf_lists(xb, cen)
+    qps, dt, nth = CB.ivf_qps(cen, off, ids, codes, xq, 10, 4)
+    assert qps > 0
