@@ -98,6 +98,33 @@ def gen_clustered_rows(torch, out, row0, centres, sigma, seed):
     return out
 
 
+def lowrank_basis(torch, r_dim, d, gen):
+    """Random r×d matrix with orthonormal rows (QR of a gaussian), scaled so rows of z·B have O(1) entries."""
+    g = torch.randn((d, r_dim), generator=gen, device=gen.device)
+    q, _ = torch.linalg.qr(g)
+    return (q.T.contiguous() * (d / r_dim) ** 0.5 / 3.0).contiguous()
+
+
+def gen_lowrank_rows(torch, out, row0, basis, eta, seed):
+    """Rows = z·B + eta·N(0, I_d), z ~ N(0, I_r): a low-intrinsic-dimension gaussian (chunk-seeded)."""
+    n = out.shape[0]
+    r_dim, d = basis.shape
+    r = 0
+    while r < n:
+        g_row = row0 + r
+        chunk = g_row // CHUNK
+        off = g_row - chunk * CHUNK
+        take = min(CHUNK - off, n - r)
+        gen = torch.Generator(device=out.device)
+        gen.manual_seed(seed * 1_000_003 + chunk)
+        z = torch.randn((CHUNK, r_dim), generator=gen, device=out.device, dtype=torch.float32)
+        noise = torch.randn((CHUNK, d), generator=gen, device=out.device, dtype=torch.float32)
+        blk = torch.addmm(noise.mul_(eta), z, basis)
+        out[r:r + take].copy_(blk[off:off + take])
+        r += take
+    return out
+
+
 def main():
     args = parse()
     import torch
@@ -140,21 +167,32 @@ def main():
         from ivf_build import build_ivf_shard  # duckdb-annsearch_amd/ivf_build.py
         gc = torch.Generator(device=dev)
         gc.manual_seed(7)
-        n_centres = 4096
-        sigma = float(os.environ.get("HIPANN_IVF_SIGMA", "0.35"))
-        centres = (torch.rand((n_centres, d), generator=gc, device=dev) * 2 - 1)
+        data_model = os.environ.get("HIPANN_IVF_DATA", "lowrank")
         xb = torch.empty((n_local, d), device=dev, dtype=torch.float32)
-        gen_clustered_rows(torch, xb, lo, centres, sigma, 42)
-        a = torch.randint(0, n_centres, (nq,), generator=gq, device=dev)
-        xq = (centres[a] + torch.randn((nq, d), generator=gq, device=dev) * sigma).contiguous()
+        if data_model == "lowrank":
+            r_dim = int(os.environ.get("HIPANN_IVF_RANK", "16"))
+            eta = float(os.environ.get("HIPANN_IVF_NOISE", "0.02"))
+            basis = lowrank_basis(torch, r_dim, d, gc)
+            gen_lowrank_rows(torch, xb, lo, basis, eta, 42)
+            xq = torch.empty((nq, d), device=dev, dtype=torch.float32)
+            gen_lowrank_rows(torch, xq, 0, basis, eta, 4242)
+            data_desc = f"low-rank gaussian, intrinsic dim {r_dim}, noise {eta}"
+        else:
+            n_centres = int(os.environ.get("HIPANN_IVF_CENTRES", "4096"))
+            sigma = float(os.environ.get("HIPANN_IVF_SIGMA", "0.35"))
+            centres = (torch.rand((n_centres, d), generator=gc, device=dev) * 2 - 1)
+            gen_clustered_rows(torch, xb, lo, centres, sigma, 42)
+            a = torch.randint(0, n_centres, (nq,), generator=gq, device=dev)
+            xq = (centres[a] + torch.randn((nq, d), generator=gq, device=dev) * sigma).contiguous()
+            data_desc = f"{n_centres} gaussian centres, sigma={sigma}"
         index, ivf_info = build_ivf_shard(torch, hipann, xb, lo, n, args.nlist, args.nprobe, metric, rank, world,
                                           centres_seed=1234)
         del xb  # lists hold a list-ordered copy
         torch.cuda.empty_cache()
         search = index.search_device
         extra.update(ivf_info)
-        workload = (f"FAISS IVFFlat nlist={args.nlist} nprobe={args.nprobe}, {n // 1_000_000}Mx{d} fp32 clustered "
-                    f"(sigma={sigma}), batch={nq}, k={k}")
+        workload = (f"FAISS IVFFlat nlist={args.nlist} nprobe={args.nprobe}, {n // 1_000_000}Mx{d} fp32 "
+                    f"({data_desc}), batch={nq}, k={k}")
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t_setup
 
@@ -180,6 +218,8 @@ def main():
         probes = index.last_probes(nq)
         extra["scan_bytes_per_batch_local"] = scan_bytes(index, probes, d)
         extra["distinct_lists_probed"] = int(np.unique(probes[probes >= 0]).size)
+        from ivf_build import scan_pairs
+        extra["scanned_pairs_per_batch_local"] = scan_pairs(index, probes)
 
     # ---------------- timed region ----------------
     index.set_kernel_timing(True)
@@ -230,7 +270,9 @@ def main():
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "ivf_scan_topk",
                 "kernel_ms": round(kern_ms, 3), "merge_ms": round(merge_ms, 3),
-                "algorithmic": "sum over distinct probed lists |l|*(4d+8) B per launch"}
+                "algorithmic": "sum over distinct probed lists |l|*(4d+8) B per launch",
+                "valu_tflops": round(3.0 * d * extra.get("scanned_pairs_per_batch_local", 0) / (kern_ms * 1e-3) / 1e12, 2)
+                if kern_ms > 0 else None}
 
     # ---------------- CPU baseline (rank 0, N=1 only) ----------------
     cpu = None

@@ -16,13 +16,35 @@ from __future__ import annotations
 import numpy as np
 
 
-def kmeans(torch, hipann, x, nlist: int, niter: int = 25, seed: int = 1234, metric: int = 0):
+def kmeans_pp_init(torch, x, nlist: int, g):
+    """k-means++ seeding (D² sampling).  FAISS seeds with a random sample; on well-separated clusters in
+    high dimension that start leaves averaged centroids that absorb neighbouring clusters (lists of 10×
+    the mean), so the build uses D² seeding instead (IVF build)."""
+    m = x.shape[0]
+    xn = (x * x).sum(1)
+    first = int(torch.randint(0, m, (1,), generator=g))
+    cen = [x[first]]
+    d2 = (xn - 2 * (x @ x[first]) + xn[first]).clamp_min_(0)
+    u = torch.rand((nlist,), generator=g).to(x.device)
+    for i in range(1, nlist):
+        cdf = torch.cumsum(d2, 0)
+        idx = int(torch.searchsorted(cdf, u[i] * cdf[-1]).clamp_max(m - 1))
+        c = x[idx]
+        cen.append(c)
+        d2 = torch.minimum(d2, (xn - 2 * (x @ c) + xn[idx]).clamp_min_(0))
+    return torch.stack(cen).contiguous()
+
+
+def kmeans(torch, hipann, x, nlist: int, niter: int = 25, seed: int = 1234, metric: int = 0, init: str = "kmeans++"):
     """Lloyd k-means on the GPU (assignment through the Flat kernels).  x: (m, d) CUDA fp32."""
     m, d = x.shape
     g = torch.Generator(device="cpu")
     g.manual_seed(seed)
-    perm = torch.randperm(m, generator=g)[:nlist].to(x.device)
-    cen = x[perm].clone()
+    if init == "kmeans++":
+        cen = kmeans_pp_init(torch, x, nlist, g)
+    else:
+        perm = torch.randperm(m, generator=g)[:nlist].to(x.device)
+        cen = x[perm].clone()
     stream = torch.cuda.current_stream().cuda_stream
     D = torch.empty((m, 1), device=x.device, dtype=torch.float32)
     I = torch.empty((m, 1), device=x.device, dtype=torch.int64)
@@ -104,6 +126,13 @@ def scan_bytes(index, probes: np.ndarray, d: int) -> float:
     sizes = np.diff(index._offsets)
     distinct = np.unique(probes[probes >= 0])
     return float(sizes[distinct].sum()) * (4 * d + 8)
+
+
+def scan_pairs(index, probes: np.ndarray) -> int:
+    """(query, row) distance evaluations of one batch on this shard: Σ_q Σ_p |l(q, p)|."""
+    sizes = np.diff(index._offsets)
+    p = probes[probes >= 0]
+    return int(sizes[p].sum())
 
 
 def flat_ground_truth(torch, hipann, d: int, metric: int, xq, k: int, n_total: int, rank: int, world: int,
