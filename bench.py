@@ -296,7 +296,7 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (generated on device: uniform U(-1,1) for flat, gaussian clusters for ivf)",
+            "data": "synthetic (generated on device: U(-1,1) rows for flat; low-intrinsic-dimension gaussian rows for ivf)",
             "config": {"workload": workload, "global_batch": nq, "n": n, "d": d, "k": k,
                        "parallelism": f"shard{world}"},
             "recall_at_10": recall,
