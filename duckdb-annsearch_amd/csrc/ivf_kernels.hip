@@ -21,11 +21,13 @@
 
 namespace hipann {
 
-constexpr int IVF_QW = 8;               // queries per wave
-constexpr int IVF_G = 4 * IVF_QW;       // queries per work item (block of 4 waves)
+constexpr int IVF_WAVES = 8;            // waves per work item (block)
+constexpr int IVF_THREADS = 64 * IVF_WAVES;
+constexpr int IVF_G = 32;               // queries per work item
+constexpr int IVF_QW = IVF_G / IVF_WAVES;  // queries per wave
 constexpr int IVF_TR = 256;             // list rows per tile (4 per lane)
-constexpr int IVF_BK = 32;              // dims per LDS chunk
-constexpr int IVF_LD = IVF_BK + 4;      // padded row stride (conflict-free ds_read_b128)
+constexpr int IVF_BK = 24;              // dims per LDS chunk
+constexpr int IVF_LD = IVF_BK + 4;      // padded row stride: 28 dwords → 16 rows hit 16 distinct b128 slots
 constexpr int IVF_CH = 2048;            // list rows per work item (big lists split into chunks)
 
 __device__ __forceinline__ int ivf_nch(int len) { return (len + IVF_CH - 1) / IVF_CH; }
@@ -122,13 +124,17 @@ __global__ void __launch_bounds__(1024) ivf_slot_scan(const int64_t *__restrict_
     if (threadIdx.x == 0) slot_off[npairs] = carry;
 }
 
+// Row staging: IVF_TR rows × IVF_BK dims = IVF_TR·IVF_BK/4 float4, IVF_SP per thread.
+constexpr int IVF_F4 = IVF_BK / 4;                 // float4 per staged row segment
+constexpr int IVF_SP = IVF_TR * IVF_F4 / IVF_THREADS;  // float4 staged per thread
+
 template <bool VEC4>
 __device__ __forceinline__ void ivf_stage_load(const float *__restrict__ codes, int64_t r0, int64_t r1, int d, int k0,
-                                               float4 (&st)[8]) {
+                                               float4 (&st)[IVF_SP]) {
 #pragma unroll
-    for (int p = 0; p < 8; ++p) {
-        const int f = threadIdx.x + 256 * p;
-        const int row = f >> 3, c4 = f & 7;
+    for (int p = 0; p < IVF_SP; ++p) {
+        const int f = threadIdx.x + IVF_THREADS * p;
+        const int row = f / IVF_F4, c4 = f - (f / IVF_F4) * IVF_F4;
         const int64_t gr = r0 + row;
         const int kk = k0 + 4 * c4;
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -147,24 +153,23 @@ __device__ __forceinline__ void ivf_stage_load(const float *__restrict__ codes, 
     }
 }
 
-__device__ __forceinline__ void ivf_stage_store(float *__restrict__ lds, const float4 (&st)[8]) {
+__device__ __forceinline__ void ivf_stage_store(float *__restrict__ lds, const float4 (&st)[IVF_SP]) {
 #pragma unroll
-    for (int p = 0; p < 8; ++p) {
-        const int f = threadIdx.x + 256 * p;
-        const int row = f >> 3, c4 = f & 7;
+    for (int p = 0; p < IVF_SP; ++p) {
+        const int f = threadIdx.x + IVF_THREADS * p;
+        const int row = f / IVF_F4, c4 = f - (f / IVF_F4) * IVF_F4;
         *reinterpret_cast<float4 *>(lds + row * IVF_LD + 4 * c4) = st[p];
     }
 }
 
-// Stage this item's 32 queries × IVF_BK dims (one float4 per thread) — rows beyond nqi are zero.
+// Query staging: thread t < IVF_G·IVF_F4 stages float4 (t % IVF_F4) of query slot t / IVF_F4.
 template <bool VEC4>
-__device__ __forceinline__ void ivf_stage_q(const float *__restrict__ Q, const int (&qrow)[1], int d, int k0,
-                                            float4 &st) {
-    const int t = threadIdx.x;  // 256 threads = 32 queries × 8 float4
-    const int kk = k0 + 4 * (t & 7);
+__device__ __forceinline__ void ivf_stage_q(const float *__restrict__ Q, int qrow, int d, int k0, float4 &st) {
+    const int t = threadIdx.x;
+    const int kk = k0 + 4 * (t - (t / IVF_F4) * IVF_F4);
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (qrow[0] >= 0) {
-        const float *src = Q + (int64_t)qrow[0] * d + kk;
+    if (qrow >= 0) {
+        const float *src = Q + (int64_t)qrow * d + kk;
         if (VEC4) {
             if (kk < d) v = *reinterpret_cast<const float4 *>(src);
         } else {
@@ -177,9 +182,47 @@ __device__ __forceinline__ void ivf_stage_q(const float *__restrict__ Q, const i
     st = v;
 }
 
+// One K chunk (IVF_BK dims) for NW queries × 4 rows per lane.  Query values are LDS broadcasts
+// (wave-uniform address); row values are per-lane ds_read_b128.  Direct form: t = q − x, acc += t².
+template <int NW, bool IP>
+__device__ __forceinline__ void ivf_chunk(const float *__restrict__ cur, const float *__restrict__ qcur,
+                                          float (&acc)[4][IVF_QW], int lane) {
+#pragma unroll 1
+    for (int u = 0; u < IVF_F4; ++u) {
+        float4 xv[4], qv[NW];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xv[r] = *reinterpret_cast<const float4 *>(cur + (lane + 64 * r) * IVF_LD + 4 * u);
+#pragma unroll
+        for (int j = 0; j < NW; ++j) qv[j] = *reinterpret_cast<const float4 *>(qcur + j * IVF_LD + 4 * u);
+#pragma unroll
+        for (int j = 0; j < NW; ++j) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                if (IP) {
+                    acc[r][j] = fmaf(qv[j].x, xv[r].x, acc[r][j]);
+                    acc[r][j] = fmaf(qv[j].y, xv[r].y, acc[r][j]);
+                    acc[r][j] = fmaf(qv[j].z, xv[r].z, acc[r][j]);
+                    acc[r][j] = fmaf(qv[j].w, xv[r].w, acc[r][j]);
+                } else {
+                    float t;
+                    t = qv[j].x - xv[r].x; acc[r][j] = fmaf(t, t, acc[r][j]);
+                    t = qv[j].y - xv[r].y; acc[r][j] = fmaf(t, t, acc[r][j]);
+                    t = qv[j].z - xv[r].z; acc[r][j] = fmaf(t, t, acc[r][j]);
+                    t = qv[j].w - xv[r].w; acc[r][j] = fmaf(t, t, acc[r][j]);
+                }
+            }
+        }
+    }
+}
+
 // part_d / part_i: one k-list per slot (slot_off, above); part_i holds shard-local row numbers.
+//
+// Occupancy: LDS = 2·(IVF_TR + IVF_G)·IVF_LD·4 B = 64.5 KiB → 2 blocks of IVF_WAVES waves per CU
+// (≤ 128 VGPRs at 8 waves: four waves per SIMD).  A lone wave can issue a VALU op only every 4
+// cycles (MI355X_MICROARCH.md, "vector-instruction ISSUE cost"), and the per-K-chunk barrier and
+// LDS/VMEM waits need other waves on the SIMD to cover them.
 template <bool VEC4, bool IP>
-__global__ void __launch_bounds__(256, 2)
+__global__ void __launch_bounds__(IVF_THREADS, 2 * IVF_THREADS / 256)
 ivf_scan_topk(const float *__restrict__ Q, int d, const float *__restrict__ codes, const int64_t *__restrict__ list_off,
               const int *__restrict__ cnt, const int *__restrict__ bucket_off, const int *__restrict__ item_off,
               const int *__restrict__ bucket, const int *__restrict__ slot_off, int nlist, int nprobe, int64_t nq,
@@ -202,22 +245,25 @@ ivf_scan_topk(const float *__restrict__ Q, int d, const float *__restrict__ code
     const int nch = ivf_nch((int)(lr1 - lr0));
     const int rem = item - item_off[l];
     const int g = rem / nch, chunk = rem - g * nch;  // (query group, row chunk)
+    // the list's c probing queries are split evenly over ng = ceil(c / G) groups
     const int c = cnt[l];
-    const int q_begin = g * IVF_G;
-    const int nqi = min(IVF_G, c - q_begin);
+    const int ng = (c + IVF_G - 1) / IVF_G;
+    const int q_begin = (int)((int64_t)g * c / ng), q_end = (int)((int64_t)(g + 1) * c / ng);
+    const int nqi = q_end - q_begin;
     const int64_t r0 = lr0 + (int64_t)chunk * IVF_CH;
     const int64_t r1 = r0 + IVF_CH < lr1 ? r0 + IVF_CH : lr1;
     const int boff = bucket_off[l] + q_begin;
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int wq0 = wave * IVF_QW;                   // this wave's first query slot
-    const int nwq = max(0, min(IVF_QW, nqi - wq0));  // queries this wave owns (wave-uniform)
+    // this wave's query slots [wq0, wq0 + nwq): the group's queries split evenly over the 4 waves
+    const int wq0 = __builtin_amdgcn_readfirstlane(wave * nqi / IVF_WAVES);
+    const int nwq = __builtin_amdgcn_readfirstlane((wave + 1) * nqi / IVF_WAVES - wave * nqi / IVF_WAVES);
 
-    // staging role: thread t stages query slot t>>3
-    int qrow[1];
-    {
-        const int slot = threadIdx.x >> 3;
-        qrow[0] = slot < nqi ? bucket[boff + slot] / nprobe : -1;
+    // staging role: thread t stages query slot t / IVF_F4
+    int qrow = -1;
+    if (threadIdx.x < IVF_G * IVF_F4) {
+        const int slot = threadIdx.x / IVF_F4;
+        if (slot < nqi) qrow = bucket[boff + slot] / nprobe;
     }
 
     WaveList<1, int> lists[IVF_QW];
@@ -225,7 +271,7 @@ ivf_scan_topk(const float *__restrict__ Q, int d, const float *__restrict__ code
     for (int j = 0; j < IVF_QW; ++j) lists[j].init();
 
     const int nk = (d + IVF_BK - 1) / IVF_BK;
-    float4 st[8], sq;
+    float4 st[IVF_SP], sq;
     for (int64_t t0 = r0; t0 < r1; t0 += IVF_TR) {
         float acc[4][IVF_QW];
 #pragma unroll
@@ -236,7 +282,8 @@ ivf_scan_topk(const float *__restrict__ Q, int d, const float *__restrict__ code
         ivf_stage_load<VEC4>(codes, t0, r1, d, 0, st);
         ivf_stage_q<VEC4>(Q, qrow, d, 0, sq);
         ivf_stage_store(xs, st);
-        *reinterpret_cast<float4 *>(qs + (threadIdx.x >> 3) * IVF_LD + 4 * (threadIdx.x & 7)) = sq;
+        if (threadIdx.x < IVF_G * IVF_F4)
+            *reinterpret_cast<float4 *>(qs + (threadIdx.x / IVF_F4) * IVF_LD + 4 * (threadIdx.x % IVF_F4)) = sq;
         __syncthreads();
         for (int kc = 0; kc < nk; ++kc) {
             const float *cur = xs + (kc & 1) * IVF_TR * IVF_LD;
@@ -247,51 +294,33 @@ ivf_scan_topk(const float *__restrict__ Q, int d, const float *__restrict__ code
                 ivf_stage_load<VEC4>(codes, t0, r1, d, (kc + 1) * IVF_BK, st);
                 ivf_stage_q<VEC4>(Q, qrow, d, (kc + 1) * IVF_BK, sq);
             }
-            if (nwq > 0) {
-#pragma unroll 2
-                for (int u = 0; u < IVF_BK / 4; ++u) {
-                    float4 xv[4];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        xv[r] = *reinterpret_cast<const float4 *>(cur + (lane + 64 * r) * IVF_LD + 4 * u);
-#pragma unroll
-                    for (int j = 0; j < IVF_QW; ++j) {
-                        const float4 qv = *reinterpret_cast<const float4 *>(qcur + j * IVF_LD + 4 * u);  // broadcast
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            if (IP) {
-                                acc[r][j] = fmaf(qv.x, xv[r].x, acc[r][j]);
-                                acc[r][j] = fmaf(qv.y, xv[r].y, acc[r][j]);
-                                acc[r][j] = fmaf(qv.z, xv[r].z, acc[r][j]);
-                                acc[r][j] = fmaf(qv.w, xv[r].w, acc[r][j]);
-                            } else {
-                                float t;
-                                t = qv.x - xv[r].x; acc[r][j] = fmaf(t, t, acc[r][j]);
-                                t = qv.y - xv[r].y; acc[r][j] = fmaf(t, t, acc[r][j]);
-                                t = qv.z - xv[r].z; acc[r][j] = fmaf(t, t, acc[r][j]);
-                                t = qv.w - xv[r].w; acc[r][j] = fmaf(t, t, acc[r][j]);
-                            }
-                        }
-                    }
-                }
+            switch (nwq) {  // wave-uniform: one branch per K chunk, operand loads hoisted inside
+                case 8: if constexpr (IVF_QW >= 8) ivf_chunk<8, IP>(cur, qcur, acc, lane); break;
+                case 7: if constexpr (IVF_QW >= 7) ivf_chunk<7, IP>(cur, qcur, acc, lane); break;
+                case 6: if constexpr (IVF_QW >= 6) ivf_chunk<6, IP>(cur, qcur, acc, lane); break;
+                case 5: if constexpr (IVF_QW >= 5) ivf_chunk<5, IP>(cur, qcur, acc, lane); break;
+                case 4: if constexpr (IVF_QW >= 4) ivf_chunk<4, IP>(cur, qcur, acc, lane); break;
+                case 3: if constexpr (IVF_QW >= 3) ivf_chunk<3, IP>(cur, qcur, acc, lane); break;
+                case 2: if constexpr (IVF_QW >= 2) ivf_chunk<2, IP>(cur, qcur, acc, lane); break;
+                case 1: if constexpr (IVF_QW >= 1) ivf_chunk<1, IP>(cur, qcur, acc, lane); break;
+                default: break;
             }
             if (kc + 1 < nk) {
                 ivf_stage_store(nxt, st);
-                *reinterpret_cast<float4 *>(qnxt + (threadIdx.x >> 3) * IVF_LD + 4 * (threadIdx.x & 7)) = sq;
+                if (threadIdx.x < IVF_G * IVF_F4)
+                    *reinterpret_cast<float4 *>(qnxt + (threadIdx.x / IVF_F4) * IVF_LD + 4 * (threadIdx.x % IVF_F4)) = sq;
             }
             __syncthreads();
         }
-        if (nwq > 0) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int64_t row = t0 + lane + 64 * r;
-                const bool v = row < r1;
+        for (int r = 0; r < 4; ++r) {
+            const int64_t row = t0 + lane + 64 * r;
+            const bool v = row < r1;
 #pragma unroll
-                for (int j = 0; j < IVF_QW; ++j) {
-                    if (j < nwq) {
-                        const float key = IP ? -acc[r][j] : acc[r][j];
-                        lists[j].offer(v ? key : __builtin_inff(), v ? (int)row : 0x7fffffff, k - 1);
-                    }
+            for (int j = 0; j < IVF_QW; ++j) {
+                if (j < nwq) {
+                    const float key = IP ? -acc[r][j] : acc[r][j];
+                    lists[j].offer(v ? key : __builtin_inff(), v ? (int)row : 0x7fffffff, k - 1);
                 }
             }
         }
@@ -378,7 +407,7 @@ void launch_ivf_scan(const float *Q, int d, int metric, const float *codes, cons
                      int nprobe, int64_t nq, int k, int64_t max_items, float *pd, int *pi, hipStream_t st) {
     if (max_items <= 0) return;
     const bool vec4 = (d % 4 == 0) && ((uintptr_t)Q % 16 == 0) && ((uintptr_t)codes % 16 == 0);
-    dim3 grid((unsigned)max_items), block(256);
+    dim3 grid((unsigned)max_items), block(IVF_THREADS);
     const size_t smem = ivf_scan_smem_bytes();
 #define HIPANN_IVF_LAUNCH(V, IPM)                                                                                    \
     hipLaunchKernelGGL((ivf_scan_topk<V, IPM>), grid, block, smem, st, Q, d, codes, list_off, cnt, bucket_off, item_off, \
