@@ -94,6 +94,16 @@ void upload_list_meta(IvfShard &sh, const std::vector<int64_t> &off, int nlist) 
     HIPANN_CHECK(hipStreamSynchronize(sh.stream));
 }
 
+// ‖x‖² of every stored row (L2 only): the decomposed scan form reads it with the codes
+// (faiss-metal stores the same norms with its lists, MetalIndexIVFFlat.mm:313-318).
+void compute_row_norms(IvfShard &sh, int d, int metric) {
+    if (metric != kL2 || sh.n == 0) return;
+    DeviceGuard g(sh.device);
+    sh.xnorm.ensure(sizeof(float) * (size_t)sh.n, sh.device);
+    launch_row_norms(sh.codes, sh.n, d, sh.xnorm.get<float>(), sh.stream);
+    HIPANN_CHECK(hipStreamSynchronize(sh.stream));
+}
+
 }  // namespace
 
 namespace hipann {
@@ -137,11 +147,20 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     sh.part_d.ensure(parts * sizeof(float), sh.device);
     sh.part_i.ensure(parts * sizeof(int), sh.device);
     const int64_t max_items = ivf_max_items(nq, np, nlist, sh.max_nch, sh.n);
+    // the decomposed form needs float4 rows; other shapes take the direct kernel (also on the GPU)
+    const int form = ix.form == kFormDecomposed && ivf_dot_supported(xq, d, sh.codes) ? kFormDecomposed : kFormDirect;
+    const float *qn = nullptr;
+    if (form == kFormDecomposed && metric == kL2) {
+        sh.qn.ensure(sizeof(float) * (size_t)nq, sh.device);
+        launch_row_norms(xq, nq, d, sh.qn.get<float>(), st);
+        qn = sh.qn.get<float>();
+    }
     {
         ScopedTiming t(ix.timer_main, st);
-        launch_ivf_scan(xq, d, metric, sh.codes, sh.list_off.get<int64_t>(), sh.cnt.get<int>(),
-                        sh.bucket_off.get<int>(), sh.item_off.get<int>(), sh.bucket.get<int>(), sh.slot_off.get<int>(),
-                        nlist, np, nq, k, max_items, sh.part_d.get<float>(), sh.part_i.get<int>(), st);
+        launch_ivf_scan(xq, qn, d, metric, form, sh.codes, sh.xnorm.get<float>(), sh.list_off.get<int64_t>(),
+                        sh.cnt.get<int>(), sh.bucket_off.get<int>(), sh.item_off.get<int>(), sh.bucket.get<int>(),
+                        sh.slot_off.get<int>(), nlist, np, nq, k, max_items, sh.part_d.get<float>(),
+                        sh.part_i.get<int>(), st);
     }
     // 4. merge each query's partial lists
     ScopedTiming t(ix.timer_merge, st);
@@ -220,6 +239,7 @@ void *hipann_ivf_create(int d, int metric, int nlist, int nprobe, const float *c
             sh->ids = sh->ids_buf.get<int64_t>();
             HIPANN_CHECK(hipStreamSynchronize(sh->stream));
             upload_list_meta(*sh, off, nlist);
+            compute_row_norms(*sh, d, metric);
             sh->quant = make_quantizer(d, metric, sh->centroids, nlist, sh->device, sh->stream);
             ix->shards.push_back(std::move(sh));
         }
@@ -273,6 +293,7 @@ void *hipann_ivf_create_device(int d, int metric, int nlist, int nprobe, const f
         }
         std::vector<int64_t> off(list_offsets, list_offsets + nlist + 1);
         upload_list_meta(*sh, off, nlist);
+        compute_row_norms(*sh, d, metric);
         sh->quant = make_quantizer(d, metric, sh->centroids, nlist, device, sh->stream);
         ix->shards.push_back(std::move(sh));
         return ix.release();
@@ -402,6 +423,23 @@ int hipann_ivf_set_nprobe(void *h, int nprobe) {
     std::lock_guard<std::mutex> lk(vx->mu);
     vx->nprobe = nprobe;
     return 0;
+}
+
+int hipann_ivf_set_form(void *h, int form) {
+    if (!h || (form != kFormDecomposed && form != kFormDirect)) return -1;
+    auto *ix = static_cast<IndexBase *>(h);
+    if (ix->kind != Kind::IVF) return -1;
+    auto *vx = static_cast<IvfIndex *>(ix);
+    std::lock_guard<std::mutex> lk(vx->mu);
+    vx->form = form;
+    return 0;
+}
+
+int hipann_ivf_get_form(void *h) {
+    if (!h) return -1;
+    auto *ix = static_cast<IndexBase *>(h);
+    if (ix->kind != Kind::IVF) return -1;
+    return static_cast<IvfIndex *>(ix)->form;
 }
 
 }  // extern "C"

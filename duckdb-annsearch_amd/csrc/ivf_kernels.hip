@@ -125,31 +125,36 @@ __global__ void __launch_bounds__(1024) ivf_slot_scan(const int64_t *__restrict_
 }
 
 // Row staging: IVF_TR rows × IVF_BK dims = IVF_TR·IVF_BK/4 float4, IVF_SP per thread.
-constexpr int IVF_F4 = IVF_BK / 4;                 // float4 per staged row segment
+constexpr int IVF_F4 = IVF_BK / 4;                     // float4 per staged row segment
 constexpr int IVF_SP = IVF_TR * IVF_F4 / IVF_THREADS;  // float4 staged per thread
 
+// Branch-free staging: rows past the chunk re-load the chunk's last row (their results are never
+// offered) and query slots past the group re-load its first query, so no load is predicated on the
+// row; only VEC4 == false (d % 4 != 0 or unaligned) pays per-element bounds checks.
 template <bool VEC4>
-__device__ __forceinline__ void ivf_stage_load(const float *__restrict__ codes, int64_t r0, int64_t r1, int d, int k0,
-                                               float4 (&st)[IVF_SP]) {
+__device__ __forceinline__ float4 ivf_ld4(const float *__restrict__ src, int kk, int d) {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (VEC4) {
+        if (kk < d) v = *reinterpret_cast<const float4 *>(src);
+    } else {
+        if (kk + 0 < d) v.x = src[0];
+        if (kk + 1 < d) v.y = src[1];
+        if (kk + 2 < d) v.z = src[2];
+        if (kk + 3 < d) v.w = src[3];
+    }
+    return v;
+}
+
+template <bool VEC4>
+__device__ __forceinline__ void ivf_stage_load(const float *__restrict__ codes, int64_t r0, int64_t rlast, int d,
+                                               int k0, float4 (&st)[IVF_SP]) {
 #pragma unroll
     for (int p = 0; p < IVF_SP; ++p) {
         const int f = threadIdx.x + IVF_THREADS * p;
         const int row = f / IVF_F4, c4 = f - (f / IVF_F4) * IVF_F4;
-        const int64_t gr = r0 + row;
+        const int64_t gr = r0 + row < rlast ? r0 + row : rlast;
         const int kk = k0 + 4 * c4;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (gr < r1) {
-            const float *src = codes + gr * (int64_t)d + kk;
-            if (VEC4) {
-                if (kk < d) v = *reinterpret_cast<const float4 *>(src);
-            } else {
-                if (kk + 0 < d) v.x = src[0];
-                if (kk + 1 < d) v.y = src[1];
-                if (kk + 2 < d) v.z = src[2];
-                if (kk + 3 < d) v.w = src[3];
-            }
-        }
-        st[p] = v;
+        st[p] = ivf_ld4<VEC4>(codes + gr * (int64_t)d + kk, kk, d);
     }
 }
 
@@ -162,56 +167,117 @@ __device__ __forceinline__ void ivf_stage_store(float *__restrict__ lds, const f
     }
 }
 
-// Query staging: thread t < IVF_G·IVF_F4 stages float4 (t % IVF_F4) of query slot t / IVF_F4.
-template <bool VEC4>
-__device__ __forceinline__ void ivf_stage_q(const float *__restrict__ Q, int qrow, int d, int k0, float4 &st) {
-    const int t = threadIdx.x;
-    const int kk = k0 + 4 * (t - (t / IVF_F4) * IVF_F4);
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (qrow >= 0) {
-        const float *src = Q + (int64_t)qrow * d + kk;
-        if (VEC4) {
-            if (kk < d) v = *reinterpret_cast<const float4 *>(src);
-        } else {
-            if (kk + 0 < d) v.x = src[0];
-            if (kk + 1 < d) v.y = src[1];
-            if (kk + 2 < d) v.z = src[2];
-            if (kk + 3 < d) v.w = src[3];
-        }
-    }
-    st = v;
+// One K chunk (IVF_BK dims) for NW queries × 4 rows per lane.  Query values are LDS broadcasts
+// (wave-uniform address); row values are per-lane ds_read_b128.  Direct form on packed f32 pairs
+// (v_pk_add_f32 / v_pk_fma_f32, the only way to the 64 FLOP/clk/SIMD f32 VALU rate): each (row,
+// query) accumulates even and odd dimensions in the two halves of a float2, summed at the end —
+// a 2-way split of the sum, as FAISS's own SIMD fvec_L2sqr splits it 8 ways.
+typedef float ivf_f2 __attribute__((ext_vector_type(2)));
+typedef float ivf_f4 __attribute__((ext_vector_type(4)));
+
+// a − b on a packed pair.  The backend splits a v2f32 fsub into two v_sub_f32 (and folds
+// fma(b, −1, a) back into that fsub), so the packed form is spelled out.
+__device__ __forceinline__ ivf_f2 ivf_pk_sub(ivf_f2 a, ivf_f2 b) {
+    ivf_f2 r;
+    asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
 }
 
-// One K chunk (IVF_BK dims) for NW queries × 4 rows per lane.  Query values are LDS broadcasts
-// (wave-uniform address); row values are per-lane ds_read_b128.  Direct form: t = q − x, acc += t².
 template <int NW, bool IP>
 __device__ __forceinline__ void ivf_chunk(const float *__restrict__ cur, const float *__restrict__ qcur,
-                                          float (&acc)[4][IVF_QW], int lane) {
+                                          ivf_f2 (&acc)[4][NW > 0 ? NW : 1], int lane) {
 #pragma unroll 1
     for (int u = 0; u < IVF_F4; ++u) {
-        float4 xv[4], qv[NW];
+        ivf_f4 xv[4], qv[NW > 0 ? NW : 1];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) xv[r] = *reinterpret_cast<const float4 *>(cur + (lane + 64 * r) * IVF_LD + 4 * u);
+        for (int r = 0; r < 4; ++r) xv[r] = *reinterpret_cast<const ivf_f4 *>(cur + (lane + 64 * r) * IVF_LD + 4 * u);
 #pragma unroll
-        for (int j = 0; j < NW; ++j) qv[j] = *reinterpret_cast<const float4 *>(qcur + j * IVF_LD + 4 * u);
+        for (int j = 0; j < NW; ++j) qv[j] = *reinterpret_cast<const ivf_f4 *>(qcur + j * IVF_LD + 4 * u);
 #pragma unroll
         for (int j = 0; j < NW; ++j) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 if (IP) {
-                    acc[r][j] = fmaf(qv[j].x, xv[r].x, acc[r][j]);
-                    acc[r][j] = fmaf(qv[j].y, xv[r].y, acc[r][j]);
-                    acc[r][j] = fmaf(qv[j].z, xv[r].z, acc[r][j]);
-                    acc[r][j] = fmaf(qv[j].w, xv[r].w, acc[r][j]);
+                    acc[r][j] = __builtin_elementwise_fma(qv[j].xy, xv[r].xy, acc[r][j]);
+                    acc[r][j] = __builtin_elementwise_fma(qv[j].zw, xv[r].zw, acc[r][j]);
                 } else {
-                    float t;
-                    t = qv[j].x - xv[r].x; acc[r][j] = fmaf(t, t, acc[r][j]);
-                    t = qv[j].y - xv[r].y; acc[r][j] = fmaf(t, t, acc[r][j]);
-                    t = qv[j].z - xv[r].z; acc[r][j] = fmaf(t, t, acc[r][j]);
-                    t = qv[j].w - xv[r].w; acc[r][j] = fmaf(t, t, acc[r][j]);
+                    ivf_f2 t = ivf_pk_sub(qv[j].xy, xv[r].xy);
+                    acc[r][j] = __builtin_elementwise_fma(t, t, acc[r][j]);
+                    t = ivf_pk_sub(qv[j].zw, xv[r].zw);
+                    acc[r][j] = __builtin_elementwise_fma(t, t, acc[r][j]);
                 }
             }
         }
+    }
+}
+
+// The whole (list chunk × query group) item for a wave owning NW query slots (NW may be 0: the wave
+// still stages and meets every barrier).  Every wave of the block runs the same tile / K loop trip
+// counts, so the barriers line up across waves with different NW.
+template <int NW, bool VEC4, bool IP>
+__device__ __forceinline__ void ivf_scan_item(const float *__restrict__ Q, int d, const float *__restrict__ codes,
+                                              int64_t r0, int64_t r1, int qrow, int wq0, const int *__restrict__ bucket,
+                                              int boff, const int *__restrict__ slot_off, int chunk, int k,
+                                              float *__restrict__ xs, float *__restrict__ qs,
+                                              float *__restrict__ part_d, int *__restrict__ part_i) {
+    constexpr int NA = NW > 0 ? NW : 1;
+    const int lane = threadIdx.x & 63;
+    const bool qstager = threadIdx.x < IVF_G * IVF_F4;
+    const int qslot = threadIdx.x / IVF_F4, qc4 = threadIdx.x - (threadIdx.x / IVF_F4) * IVF_F4;
+    const float *qsrc = Q + (int64_t)qrow * d;
+    WaveList<1, int> lists[NA];
+#pragma unroll
+    for (int j = 0; j < NA; ++j) lists[j].init();
+
+    const int nk = (d + IVF_BK - 1) / IVF_BK;
+    float4 st[IVF_SP], sq = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t t0 = r0; t0 < r1; t0 += IVF_TR) {
+        ivf_f2 acc[4][NA];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int j = 0; j < NA; ++j) acc[r][j] = ivf_f2{0.f, 0.f};
+
+        ivf_stage_load<VEC4>(codes, t0, r1 - 1, d, 0, st);
+        if (qstager) sq = ivf_ld4<VEC4>(qsrc + 4 * qc4, 4 * qc4, d);
+        ivf_stage_store(xs, st);
+        if (qstager) *reinterpret_cast<float4 *>(qs + qslot * IVF_LD + 4 * qc4) = sq;
+        __syncthreads();
+        for (int kc = 0; kc < nk; ++kc) {
+            const float *cur = xs + (kc & 1) * IVF_TR * IVF_LD;
+            float *nxt = xs + ((kc + 1) & 1) * IVF_TR * IVF_LD;
+            const float *qcur = qs + (kc & 1) * IVF_G * IVF_LD + wq0 * IVF_LD;
+            float *qnxt = qs + ((kc + 1) & 1) * IVF_G * IVF_LD;
+            const bool more = kc + 1 < nk;
+            if (more) {
+                const int k1 = (kc + 1) * IVF_BK;
+                ivf_stage_load<VEC4>(codes, t0, r1 - 1, d, k1, st);
+                if (qstager) sq = ivf_ld4<VEC4>(qsrc + k1 + 4 * qc4, k1 + 4 * qc4, d);
+            }
+            if (NW > 0) ivf_chunk<NW, IP>(cur, qcur, acc, lane);
+            if (more) {
+                ivf_stage_store(nxt, st);
+                if (qstager) *reinterpret_cast<float4 *>(qnxt + qslot * IVF_LD + 4 * qc4) = sq;
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int64_t row = t0 + lane + 64 * r;
+            const bool v = row < r1;
+#pragma unroll
+            for (int j = 0; j < NW; ++j) {
+                const float sum = acc[r][j].x + acc[r][j].y;
+                const float key = IP ? -sum : sum;
+                lists[j].offer(v ? key : __builtin_inff(), v ? (int)row : 0x7fffffff, k - 1);
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+        const int pr = bucket[boff + wq0 + j];
+        const int64_t off = (int64_t)(slot_off[pr] + chunk) * k;
+        lists[j].store(part_d + off, part_i + off, k);
     }
 }
 
@@ -254,85 +320,249 @@ ivf_scan_topk(const float *__restrict__ Q, int d, const float *__restrict__ code
     const int64_t r1 = r0 + IVF_CH < lr1 ? r0 + IVF_CH : lr1;
     const int boff = bucket_off[l] + q_begin;
 
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    // this wave's query slots [wq0, wq0 + nwq): the group's queries split evenly over the 4 waves
+    const int wave = threadIdx.x >> 6;
+    // this wave's query slots [wq0, wq0 + nwq): the group's queries split evenly over the waves
     const int wq0 = __builtin_amdgcn_readfirstlane(wave * nqi / IVF_WAVES);
     const int nwq = __builtin_amdgcn_readfirstlane((wave + 1) * nqi / IVF_WAVES - wave * nqi / IVF_WAVES);
-
-    // staging role: thread t stages query slot t / IVF_F4
-    int qrow = -1;
+    // staging role: thread t stages query slot t / IVF_F4 (slots past the group re-load slot 0)
+    int qrow = 0;
     if (threadIdx.x < IVF_G * IVF_F4) {
         const int slot = threadIdx.x / IVF_F4;
-        if (slot < nqi) qrow = bucket[boff + slot] / nprobe;
+        qrow = bucket[boff + (slot < nqi ? slot : 0)] / nprobe;
     }
+    switch (nwq) {
+        case 0: ivf_scan_item<0, VEC4, IP>(Q, d, codes, r0, r1, qrow, wq0, bucket, boff, slot_off, chunk, k, xs, qs, part_d, part_i); break;
+        case 1: ivf_scan_item<1, VEC4, IP>(Q, d, codes, r0, r1, qrow, wq0, bucket, boff, slot_off, chunk, k, xs, qs, part_d, part_i); break;
+        case 2: ivf_scan_item<2, VEC4, IP>(Q, d, codes, r0, r1, qrow, wq0, bucket, boff, slot_off, chunk, k, xs, qs, part_d, part_i); break;
+        case 3: ivf_scan_item<3, VEC4, IP>(Q, d, codes, r0, r1, qrow, wq0, bucket, boff, slot_off, chunk, k, xs, qs, part_d, part_i); break;
+        default: ivf_scan_item<IVF_QW, VEC4, IP>(Q, d, codes, r0, r1, qrow, wq0, bucket, boff, slot_off, chunk, k, xs, qs, part_d, part_i); break;
+    }
+}
 
-    WaveList<1, int> lists[IVF_QW];
-#pragma unroll
-    for (int j = 0; j < IVF_QW; ++j) lists[j].init();
+// ---------------------------------------------------------------------------------------------
+// ivf_scan_dot — the decomposed form ‖q‖² + ‖x‖² − 2·q·x (clamped ≥ 0; IP: q·x), as faiss-metal's
+// IVF path and FAISS's GPU IVFFlat compute it (norms stored with the lists, MetalIndexIVFFlat.mm:
+// 305-318).  One FMA per (query, row, dim) instead of the direct form's subtract + FMA, so the
+// VALU floor halves; the kernel is register-blocked to keep LDS traffic below the FMA rate.
+//
+// Work item and outputs as ivf_scan_topk (same plan, slots and IVF_G / IVF_CH), items ordered
+// (list, row chunk, query group) with the group fastest and dealt XCD-contiguously, so the groups
+// that re-read one row chunk run together on one XCD and share its L2.
+//
+// Block: 4 waves, 2 blocks per CU (2 waves per SIMD, ≤ 256 VGPRs).  Wave w owns ≤ DT_NW = 8 of the
+// item's ≤ 32 queries and every row of the tile: DT_R = 8 rows per lane (tile = 512 rows), an 8 × 8
+// accumulator block per lane, so each K step issues 16 ds_read_b128 for 256 FMAs.
+//
+// Staging: LDS-DMA (global_load_lds_dwordx4) into a 3-stage ring, raw barrier + counted vmcnt, two
+// chunks in flight.  Per stage: x = [512 rows][3 float4] (BK = 12 dims; 3 is odd ⇒ the per-lane
+// ds_read_b128 of 16 consecutive rows hits 16 distinct bank groups), then each wave's query block
+// [8 queries][3 float4].  Per chunk a wave issues DT_XPW = 6 x pieces + 1 query piece.
+constexpr int DT_WAVES = 4;
+constexpr int DT_THREADS = 64 * DT_WAVES;
+constexpr int DT_R = 8;
+constexpr int DT_NW = 8;
+constexpr int DT_TR = 64 * DT_R;
+constexpr int DT_BK = 12;
+constexpr int DT_F4 = DT_BK / 4;
+constexpr int DT_XF4 = DT_TR * DT_F4;               // 1536 float4 of rows per stage
+constexpr int DT_XPW = DT_XF4 / 64 / DT_WAVES;      // 6 x pieces per wave per chunk
+constexpr int DT_QF4 = DT_NW * DT_F4;               // 24 float4 of queries per wave per stage
+constexpr int DT_STAGE_F4 = DT_XF4 + DT_WAVES * DT_QF4;
+constexpr int DT_STAGES = 3;
+static_assert(DT_WAVES * DT_NW == IVF_G, "a dot item covers one IVF_G query group");
+static_assert(IVF_CH % DT_TR == 0, "row chunks are whole tiles");
+static_assert(DT_XPW * 64 * DT_WAVES == DT_XF4 && DT_QF4 <= 64, "piece split");
+static_assert(DT_XPW + 1 == 7, "IVF_DT_WAIT's vmcnt literal is the pieces per chunk");
+static_assert((64 % DT_F4) == 1 && ((DT_XPW * 64) % DT_F4) == 0, "c4 of x piece i is (lane + i) % 3");
 
-    const int nk = (d + IVF_BK - 1) / IVF_BK;
-    float4 st[IVF_SP], sq;
-    for (int64_t t0 = r0; t0 < r1; t0 += IVF_TR) {
-        float acc[4][IVF_QW];
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int j = 0; j < IVF_QW; ++j) acc[r][j] = 0.f;
+typedef __attribute__((address_space(3))) void *ivf_lds_ptr;
+typedef __attribute__((address_space(1))) void *ivf_gbl_ptr;
 
-        ivf_stage_load<VEC4>(codes, t0, r1, d, 0, st);
-        ivf_stage_q<VEC4>(Q, qrow, d, 0, sq);
-        ivf_stage_store(xs, st);
-        if (threadIdx.x < IVF_G * IVF_F4)
-            *reinterpret_cast<float4 *>(qs + (threadIdx.x / IVF_F4) * IVF_LD + 4 * (threadIdx.x % IVF_F4)) = sq;
-        __syncthreads();
-        for (int kc = 0; kc < nk; ++kc) {
-            const float *cur = xs + (kc & 1) * IVF_TR * IVF_LD;
-            float *nxt = xs + ((kc + 1) & 1) * IVF_TR * IVF_LD;
-            const float *qcur = qs + (kc & 1) * IVF_G * IVF_LD + wq0 * IVF_LD;
-            float *qnxt = qs + ((kc + 1) & 1) * IVF_G * IVF_LD;
-            if (kc + 1 < nk) {
-                ivf_stage_load<VEC4>(codes, t0, r1, d, (kc + 1) * IVF_BK, st);
-                ivf_stage_q<VEC4>(Q, qrow, d, (kc + 1) * IVF_BK, sq);
+__device__ __forceinline__ void ivf_glds16(const float *src, float *lds_wave_base) {
+    __builtin_amdgcn_global_load_lds((ivf_gbl_ptr)(src), (ivf_lds_ptr)(lds_wave_base), 16, 0, 0);
+}
+
+// Wait for this wave's pieces of the chunk about to be read (leaving the next chunk's 7 in flight,
+// or none), then a raw barrier: past it every wave's pieces of that chunk have landed and every wave
+// has finished reading the stage the next issue overwrites.  "memory" pins LDS accesses around it.
+#define IVF_DT_WAIT(N) asm volatile("s_waitcnt vmcnt(" #N ")\n\ts_barrier" ::: "memory")
+
+template <int NW, bool IP>
+__device__ __forceinline__ void ivf_dot_item(int d, const float *__restrict__ codes, const float *__restrict__ xn,
+                                             int64_t r0, int64_t r1, const float *qsrc, const float *qn, int wq0,
+                                             const int *__restrict__ bucket, int boff, int nprobe,
+                                             const int *__restrict__ slot_off, int chunk, int k, float *ring,
+                                             float *__restrict__ part_d, int *__restrict__ part_i) {
+    constexpr int NA = NW > 0 ? NW : 1;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nk = (d + DT_BK - 1) / DT_BK;
+    const int ntile = (int)((r1 - r0 + DT_TR - 1) / DT_TR);
+    const int total = ntile * nk;
+
+    // ---- issue side: this wave's x pieces p = wave·6 + i cover float4 s = 64p + lane = (row, c4) ----
+    int it_kc = 0;
+    int64_t it_t0 = r0;
+    const float *xb[DT_XPW];
+    auto issue = [&](int buf) {
+        float *stage = ring + (size_t)buf * DT_STAGE_F4 * 4;
+        if (it_kc == 0) {
+#pragma unroll
+            for (int i = 0; i < DT_XPW; ++i) {
+                const int srow = (64 * (wave * DT_XPW + i) + lane) / DT_F4;
+                const int64_t row = it_t0 + srow < r1 ? it_t0 + srow : r1 - 1;  // past the chunk: any valid row
+                xb[i] = codes + row * (int64_t)d;
             }
-            switch (nwq) {  // wave-uniform: one branch per K chunk, operand loads hoisted inside
-                case 8: if constexpr (IVF_QW >= 8) ivf_chunk<8, IP>(cur, qcur, acc, lane); break;
-                case 7: if constexpr (IVF_QW >= 7) ivf_chunk<7, IP>(cur, qcur, acc, lane); break;
-                case 6: if constexpr (IVF_QW >= 6) ivf_chunk<6, IP>(cur, qcur, acc, lane); break;
-                case 5: if constexpr (IVF_QW >= 5) ivf_chunk<5, IP>(cur, qcur, acc, lane); break;
-                case 4: if constexpr (IVF_QW >= 4) ivf_chunk<4, IP>(cur, qcur, acc, lane); break;
-                case 3: if constexpr (IVF_QW >= 3) ivf_chunk<3, IP>(cur, qcur, acc, lane); break;
-                case 2: if constexpr (IVF_QW >= 2) ivf_chunk<2, IP>(cur, qcur, acc, lane); break;
-                case 1: if constexpr (IVF_QW >= 1) ivf_chunk<1, IP>(cur, qcur, acc, lane); break;
-                default: break;
-            }
-            if (kc + 1 < nk) {
-                ivf_stage_store(nxt, st);
-                if (threadIdx.x < IVF_G * IVF_F4)
-                    *reinterpret_cast<float4 *>(qnxt + (threadIdx.x / IVF_F4) * IVF_LD + 4 * (threadIdx.x % IVF_F4)) = sq;
-            }
-            __syncthreads();
         }
+        const int k0 = it_kc * DT_BK;
+        const bool full = k0 + DT_BK <= d;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int64_t row = t0 + lane + 64 * r;
-            const bool v = row < r1;
+        for (int i = 0; i < DT_XPW; ++i) {
+            int kk = k0 + 4 * ((lane + i) % DT_F4);
+            if (!full) kk = kk < d ? kk : d - 4;  // past d: any valid float4 (never read)
+            ivf_glds16(xb[i] + kk, stage + (size_t)(wave * DT_XPW + i) * 64 * 4);
+        }
+        if (lane < DT_QF4) {
+            int kk = k0 + 4 * (lane % DT_F4);
+            if (!full) kk = kk < d ? kk : d - 4;
+            ivf_glds16(qsrc + kk, stage + (size_t)(DT_XF4 + wave * DT_QF4) * 4);
+        }
+        if (++it_kc == nk) { it_kc = 0; it_t0 += DT_TR; }
+    };
+
+    // ---- compute side ----
+    WaveList<1, int> lists[NA];
 #pragma unroll
-            for (int j = 0; j < IVF_QW; ++j) {
-                if (j < nwq) {
-                    const float key = IP ? -acc[r][j] : acc[r][j];
-                    lists[j].offer(v ? key : __builtin_inff(), v ? (int)row : 0x7fffffff, k - 1);
+    for (int j = 0; j < NA; ++j) lists[j].init();
+    float qnv[NA];
+#pragma unroll
+    for (int j = 0; j < NA; ++j) qnv[j] = (!IP && j < NW) ? qn[bucket[boff + wq0 + j] / nprobe] : 0.f;
+    float acc[DT_R][NA];
+#pragma unroll
+    for (int r = 0; r < DT_R; ++r)
+#pragma unroll
+        for (int j = 0; j < NA; ++j) acc[r][j] = 0.f;
+
+    issue(0);
+    if (total > 1) issue(1);
+    int kc = 0, buf = 0;
+    int64_t t0 = r0;
+    for (int c = 0; c < total; ++c) {
+        if (c + 1 < total) IVF_DT_WAIT(7); else IVF_DT_WAIT(0);
+        if (c + 2 < total) issue(buf == 0 ? DT_STAGES - 1 : buf - 1);
+        const float *X = ring + (size_t)buf * DT_STAGE_F4 * 4;
+        const float *Qw = X + (size_t)(DT_XF4 + wave * DT_QF4) * 4;
+        const int k0 = kc * DT_BK;
+        const int nu = d - k0 >= DT_BK ? DT_F4 : (d - k0) / 4;
+        if (NW > 0) {
+#pragma unroll 1
+            for (int u = 0; u < nu; ++u) {
+                float4 xv[DT_R], qv[NA];
+#pragma unroll
+                for (int r = 0; r < DT_R; ++r)
+                    xv[r] = *reinterpret_cast<const float4 *>(X + ((lane + 64 * r) * DT_F4 + u) * 4);
+#pragma unroll
+                for (int j = 0; j < NW; ++j) qv[j] = *reinterpret_cast<const float4 *>(Qw + (j * DT_F4 + u) * 4);
+#pragma unroll
+                for (int j = 0; j < NW; ++j)
+#pragma unroll
+                    for (int r = 0; r < DT_R; ++r) acc[r][j] = fmaf(qv[j].x, xv[r].x, acc[r][j]);
+#pragma unroll
+                for (int j = 0; j < NW; ++j)
+#pragma unroll
+                    for (int r = 0; r < DT_R; ++r) acc[r][j] = fmaf(qv[j].y, xv[r].y, acc[r][j]);
+#pragma unroll
+                for (int j = 0; j < NW; ++j)
+#pragma unroll
+                    for (int r = 0; r < DT_R; ++r) acc[r][j] = fmaf(qv[j].z, xv[r].z, acc[r][j]);
+#pragma unroll
+                for (int j = 0; j < NW; ++j)
+#pragma unroll
+                    for (int r = 0; r < DT_R; ++r) acc[r][j] = fmaf(qv[j].w, xv[r].w, acc[r][j]);
+            }
+        }
+        if (++kc == nk) {  // tile done: offer its rows
+            if (NW > 0) {
+#pragma unroll
+                for (int r = 0; r < DT_R; ++r) {
+                    const int64_t row = t0 + lane + 64 * r;
+                    const bool v = row < r1;
+                    const float xnr = (!IP && v) ? xn[row] : 0.f;
+#pragma unroll
+                    for (int j = 0; j < NW; ++j) {
+                        float key;
+                        if (IP) {
+                            key = -acc[r][j];
+                        } else {
+                            key = fmaf(-2.f, acc[r][j], qnv[j] + xnr);
+                            key = key < 0.f ? 0.f : key;
+                        }
+                        lists[j].offer(v ? key : __builtin_inff(), v ? (int)row : 0x7fffffff, k - 1);
+                        acc[r][j] = 0.f;
+                    }
                 }
             }
+            kc = 0;
+            t0 += DT_TR;
         }
+        buf = buf == DT_STAGES - 1 ? 0 : buf + 1;
     }
 #pragma unroll
-    for (int j = 0; j < IVF_QW; ++j) {
-        if (j < nwq) {
-            const int pr = bucket[boff + wq0 + j];
-            const int64_t off = (int64_t)(slot_off[pr] + chunk) * k;
-            lists[j].store(part_d + off, part_i + off, k);
-        }
+    for (int j = 0; j < NW; ++j) {
+        const int pr = bucket[boff + wq0 + j];
+        const int64_t off = (int64_t)(slot_off[pr] + chunk) * k;
+        lists[j].store(part_d + off, part_i + off, k);
     }
+}
+
+template <bool IP>
+__global__ void __launch_bounds__(DT_THREADS, 2 * DT_THREADS / 256)
+ivf_scan_dot(const float *__restrict__ Q, const float *__restrict__ qn, int d, const float *__restrict__ codes,
+             const float *__restrict__ xn, const int64_t *__restrict__ list_off, const int *__restrict__ cnt,
+             const int *__restrict__ bucket_off, const int *__restrict__ item_off, const int *__restrict__ bucket,
+             const int *__restrict__ slot_off, int nlist, int nprobe, int k, float *__restrict__ part_d,
+             int *__restrict__ part_i) {
+    extern __shared__ __attribute__((aligned(16))) float ring[];
+    const int total = item_off[nlist];
+    if ((int)blockIdx.x >= total) return;
+    const int item = xcd_remap((int)blockIdx.x, total);
+    int lo = 0, hi = nlist - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (item_off[mid] <= item) lo = mid; else hi = mid - 1;
+    }
+    const int l = lo;
+    const int64_t lr0 = list_off[l], lr1 = list_off[l + 1];
+    const int c = cnt[l];
+    const int ng = (c + IVF_G - 1) / IVF_G;
+    const int rem = item - item_off[l];
+    const int chunk = rem / ng, g = rem - chunk * ng;  // (row chunk, query group), group fastest
+    const int q_begin = (int)((int64_t)g * c / ng), q_end = (int)((int64_t)(g + 1) * c / ng);
+    const int nqi = q_end - q_begin;
+    const int64_t r0 = lr0 + (int64_t)chunk * IVF_CH;
+    const int64_t r1 = r0 + IVF_CH < lr1 ? r0 + IVF_CH : lr1;
+    const int boff = bucket_off[l] + q_begin;
+
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wq0 = __builtin_amdgcn_readfirstlane(wave * nqi / DT_WAVES);
+    const int nwq = __builtin_amdgcn_readfirstlane((wave + 1) * nqi / DT_WAVES - wave * nqi / DT_WAVES);
+    // query-piece lanes: slot lane / 3 of this wave's block (slots past nwq re-load the wave's first)
+    const int qslot = lane / DT_F4 < nwq ? lane / DT_F4 : 0;
+    const float *qsrc = Q + (int64_t)(bucket[boff + wq0 + qslot] / nprobe) * d;
+#define HIPANN_DOT_ITEM(NW)                                                                                         \
+    ivf_dot_item<NW, IP>(d, codes, xn, r0, r1, qsrc, qn, wq0, bucket, boff, nprobe, slot_off, chunk, k, ring, part_d, \
+                         part_i)
+    switch (nwq) {
+        case 0: HIPANN_DOT_ITEM(0); break;
+        case 1: HIPANN_DOT_ITEM(1); break;
+        case 2: HIPANN_DOT_ITEM(2); break;
+        case 3: HIPANN_DOT_ITEM(3); break;
+        case 4: HIPANN_DOT_ITEM(4); break;
+        case 5: HIPANN_DOT_ITEM(5); break;
+        case 6: HIPANN_DOT_ITEM(6); break;
+        case 7: HIPANN_DOT_ITEM(7); break;
+        default: HIPANN_DOT_ITEM(8); break;
+    }
+#undef HIPANN_DOT_ITEM
 }
 
 // Merge each query's partial lists (its contiguous slot range), mapping shard-local rows to labels.
@@ -401,23 +631,41 @@ int64_t ivf_max_items(int64_t nq, int nprobe, int nlist, int max_nch, int64_t nr
 int ivf_chunk_rows() { return IVF_CH; }
 
 size_t ivf_scan_smem_bytes() { return (size_t)2 * (IVF_TR + IVF_G) * IVF_LD * sizeof(float); }
+static size_t ivf_scan_dot_smem_bytes() { return (size_t)DT_STAGES * DT_STAGE_F4 * 16; }
 
-void launch_ivf_scan(const float *Q, int d, int metric, const float *codes, const int64_t *list_off, const int *cnt,
-                     const int *bucket_off, const int *item_off, const int *bucket, const int *slot_off, int nlist,
-                     int nprobe, int64_t nq, int k, int64_t max_items, float *pd, int *pi, hipStream_t st) {
+bool ivf_dot_supported(const float *Q, int d, const float *codes) {
+    return (d % 4 == 0) && ((uintptr_t)Q % 16 == 0) && ((uintptr_t)codes % 16 == 0);
+}
+
+void launch_ivf_scan(const float *Q, const float *qn, int d, int metric, int form, const float *codes,
+                     const float *xn, const int64_t *list_off, const int *cnt, const int *bucket_off,
+                     const int *item_off, const int *bucket, const int *slot_off, int nlist, int nprobe, int64_t nq,
+                     int k, int64_t max_items, float *pd, int *pi, hipStream_t st) {
     if (max_items <= 0) return;
-    const bool vec4 = (d % 4 == 0) && ((uintptr_t)Q % 16 == 0) && ((uintptr_t)codes % 16 == 0);
-    dim3 grid((unsigned)max_items), block(IVF_THREADS);
-    const size_t smem = ivf_scan_smem_bytes();
-#define HIPANN_IVF_LAUNCH(V, IPM)                                                                                    \
-    hipLaunchKernelGGL((ivf_scan_topk<V, IPM>), grid, block, smem, st, Q, d, codes, list_off, cnt, bucket_off, item_off, \
-                       bucket, slot_off, nlist, nprobe, nq, k, pd, pi)
-    if (vec4) {
-        if (metric == kIP) HIPANN_IVF_LAUNCH(true, true); else HIPANN_IVF_LAUNCH(true, false);
+    HIPANN_REQUIRE(max_items < (int64_t)0x7fffffff, "too many IVF work items");
+    if (form == kFormDecomposed) {
+        HIPANN_REQUIRE(ivf_dot_supported(Q, d, codes), "decomposed IVF scan needs d % 4 == 0 and 16-B aligned data");
+        HIPANN_REQUIRE(metric == kIP || (qn && xn), "decomposed L2 scan needs query and row norms");
+        dim3 grid((unsigned)max_items), block(DT_THREADS);
+        const size_t smem = ivf_scan_dot_smem_bytes();
+#define HIPANN_DOT_ARGS Q, qn, d, codes, xn, list_off, cnt, bucket_off, item_off, bucket, slot_off, nlist, nprobe, k, pd, pi
+        if (metric == kIP) hipLaunchKernelGGL((ivf_scan_dot<true>), grid, block, smem, st, HIPANN_DOT_ARGS);
+        else hipLaunchKernelGGL((ivf_scan_dot<false>), grid, block, smem, st, HIPANN_DOT_ARGS);
+#undef HIPANN_DOT_ARGS
     } else {
-        if (metric == kIP) HIPANN_IVF_LAUNCH(false, true); else HIPANN_IVF_LAUNCH(false, false);
+        const bool vec4 = ivf_dot_supported(Q, d, codes);
+        dim3 grid((unsigned)max_items), block(IVF_THREADS);
+        const size_t smem = ivf_scan_smem_bytes();
+#define HIPANN_IVF_ARGS Q, d, codes, list_off, cnt, bucket_off, item_off, bucket, slot_off, nlist, nprobe, nq, k, pd, pi
+        if (vec4) {
+            if (metric == kIP) hipLaunchKernelGGL((ivf_scan_topk<true, true>), grid, block, smem, st, HIPANN_IVF_ARGS);
+            else hipLaunchKernelGGL((ivf_scan_topk<true, false>), grid, block, smem, st, HIPANN_IVF_ARGS);
+        } else {
+            if (metric == kIP) hipLaunchKernelGGL((ivf_scan_topk<false, true>), grid, block, smem, st, HIPANN_IVF_ARGS);
+            else hipLaunchKernelGGL((ivf_scan_topk<false, false>), grid, block, smem, st, HIPANN_IVF_ARGS);
+        }
+#undef HIPANN_IVF_ARGS
     }
-#undef HIPANN_IVF_LAUNCH
     HIPANN_CHECK(hipGetLastError());
 }
 

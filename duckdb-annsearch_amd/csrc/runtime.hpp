@@ -167,15 +167,17 @@ struct IvfShard {
     DevBuf centroids_buf, codes_buf, ids_buf;  // owned storage (empty when borrowed)
     DevBuf list_off;               // int64 nlist+1 (shard-local row offsets)
     DevBuf list_len;               // int nlist (0 = empty or not owned)
+    DevBuf xnorm;                  // ‖x‖² per row (L2; the decomposed scan form)
     std::unique_ptr<FlatIndex> quant;  // coarse quantizer over `centroids` (borrowed)
     hipStream_t stream = nullptr;
     // scratch
-    DevBuf q, coarse_d, coarse_i, cnt, bucket_off, item_off, cursor, bucket, slot_off, part_d, part_i, out_d, out_i;
+    DevBuf q, qn, coarse_d, coarse_i, cnt, bucket_off, item_off, cursor, bucket, slot_off, part_d, part_i, out_d, out_i;
     int max_nch = 1;  // largest list's row-chunk count
 };
 
 struct IvfIndex : IndexBase {
     int nlist = 0, nprobe = 1;
+    int form = kFormDecomposed;
     std::vector<std::unique_ptr<IvfShard>> shards;
     int64_t last_nq = 0;
     int last_np = 0;
@@ -190,7 +192,7 @@ struct IvfIndex : IndexBase {
     }
     int64_t memory_bytes() const override {
         int64_t b = 0;
-        for (auto &s : shards) b += s->n * ((int64_t)d * 4 + 8) + (int64_t)nlist * d * 4;
+        for (auto &s : shards) b += s->n * ((int64_t)d * 4 + 8 + (metric == kL2 ? 4 : 0)) + (int64_t)nlist * d * 4;
         return b;
     }
 };
@@ -217,9 +219,11 @@ void launch_ivf_plan(const int64_t *probes, int64_t nq, int nprobe, const int *l
 int64_t ivf_max_items(int64_t nq, int nprobe, int nlist, int max_nch, int64_t nrows);
 int ivf_chunk_rows();
 size_t ivf_scan_smem_bytes();
-void launch_ivf_scan(const float *Q, int d, int metric, const float *codes, const int64_t *list_off, const int *cnt,
-                     const int *bucket_off, const int *item_off, const int *bucket, const int *slot_off, int nlist,
-                     int nprobe, int64_t nq, int k, int64_t max_items, float *pd, int *pi, hipStream_t st);
+bool ivf_dot_supported(const float *Q, int d, const float *codes);
+void launch_ivf_scan(const float *Q, const float *qn, int d, int metric, int form, const float *codes,
+                     const float *xn, const int64_t *list_off, const int *cnt, const int *bucket_off,
+                     const int *item_off, const int *bucket, const int *slot_off, int nlist, int nprobe, int64_t nq,
+                     int k, int64_t max_items, float *pd, int *pi, hipStream_t st);
 void launch_ivf_merge(const float *pd, const int *pi, const int64_t *ids, const int *slot_off, int nprobe, int64_t nq,
                       int k, int kout, float out_sign, float *D, int64_t *I, hipStream_t st);
 template <typename InId>

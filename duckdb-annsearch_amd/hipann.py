@@ -95,6 +95,8 @@ def lib() -> C.CDLL:
             "hipann_ivf_search_device": ([vp, i64, vp, i64, vp, vp, vp, cp, i32], i32),
             "hipann_ivf_last_probes": ([vp, i64p, i64, cp, i32], i32),
             "hipann_ivf_set_nprobe": ([vp, i32], i32),
+            "hipann_ivf_set_form": ([vp, i32], i32),
+            "hipann_ivf_get_form": ([vp], i32),
             "hipann_ntotal": ([vp], i64),
             "hipann_dim": ([vp], i32),
             "hipann_metric": ([vp], i32),
@@ -320,6 +322,18 @@ class HipIndexIVFFlat(_Handle):
         if lib().hipann_ivf_set_nprobe(self._h, int(v)) != 0:
             raise HipAnnError("nprobe must be >= 1")
         self._nprobe = int(v)
+
+    FORM_DECOMPOSED = 0  # ‖q‖² + ‖x‖² − 2 q·x (FAISS GPU / faiss-metal IVF form; default)
+    FORM_DIRECT = 1      # Σ(q − x)² (FAISS CPU IndexIVFFlat scanner form)
+
+    @property
+    def form(self) -> int:
+        return int(lib().hipann_ivf_get_form(self._h))
+
+    @form.setter
+    def form(self, v: int) -> None:
+        if lib().hipann_ivf_set_form(self._h, int(v)) != 0:
+            raise HipAnnError("form must be 0 (decomposed) or 1 (direct)")
 
     def search(self, x, k: int) -> Tuple[np.ndarray, np.ndarray]:
         x = _f32_2d(x, self.d)

@@ -122,6 +122,17 @@ int hipann_ivf_last_probes(void *index, int64_t *probes, int64_t cap, char *err_
 
 int hipann_ivf_set_nprobe(void *index, int nprobe);
 
+/* List-scan distance form.  HIPANN_IVF_FORM_DECOMPOSED (default): ‖q‖² + ‖x‖² − 2·q·x clamped ≥ 0
+ * (IP: q·x), with ‖x‖² stored per row — the form faiss-metal's IVF path and FAISS's GPU IVFFlat use
+ * (MetalIndexIVFFlat.mm:305-318), one FMA per dimension.  HIPANN_IVF_FORM_DIRECT: Σ(q−x)², the form
+ * of FAISS's CPU IndexIVFFlat scanner (subtract + FMA per dimension).  Both run on the GPU; the
+ * decomposed form needs d % 4 == 0 and 16-B aligned data and falls back to the direct kernel
+ * otherwise.  Returns 0, or −1 for a bad handle / form. */
+#define HIPANN_IVF_FORM_DECOMPOSED 0
+#define HIPANN_IVF_FORM_DIRECT 1
+int hipann_ivf_set_form(void *index, int form);
+int hipann_ivf_get_form(void *index);
+
 /* ---------------------------------------------------------------------------------------------
  * Common
  * ------------------------------------------------------------------------------------------- */

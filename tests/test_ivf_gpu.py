@@ -41,13 +41,46 @@ def test_ivf_faiss_metal_shapes(gpu, oracle, nv, d, nlist, nprobe, nq, k, metric
 
 @pytest.mark.parametrize("nq", [1, 7, 19, 20, 64, 333])
 @pytest.mark.parametrize("metric", [0, 1])
-def test_ivf_vs_oracle_probe_sets(gpu, oracle, nq, metric):
+@pytest.mark.parametrize("form", [0, 1])
+def test_ivf_vs_oracle_probe_sets(gpu, oracle, nq, metric, form):
     xb, xq = faiss_metal_case(20000, nq, 96)
     ix, (cen, off, ids, codes) = _ivf(gpu, xb, 64, 8, metric)
+    ix.form = form
+    assert ix.form == form
     D, I = ix.search(xq, 10)
     Do, Io, Po = oracle.ivf_search(cen, off, ids, codes, xq, 10, 8, metric)
     assert np.array_equal(ix.last_probes(nq), Po)
     check_topk_parity(xb, xq, D, I, Do, Io, metric)
+
+
+@pytest.mark.parametrize("d", [4, 8, 12, 20, 44, 77, 132, 768])
+@pytest.mark.parametrize("metric", [0, 1])
+@pytest.mark.parametrize("form", [0, 1])
+def test_ivf_dims(gpu, oracle, d, metric, form):
+    """Dimensions around the scans' LDS chunks (12 dims decomposed, 24 direct: partial last chunk,
+    d < one chunk) and d % 4 != 0 (the decomposed form falls back to the direct kernel)."""
+    xb, xq = faiss_metal_case(3000, 40, d)
+    ix, (cen, off, ids, codes) = _ivf(gpu, xb, 8, 3, metric)
+    ix.form = form
+    D, I = ix.search(xq, 10)
+    Do, Io, Po = oracle.ivf_search(cen, off, ids, codes, xq, 10, 3, metric)
+    assert np.array_equal(ix.last_probes(40), Po)
+    check_topk_parity(xb, xq, D, I, Do, Io, metric)
+
+
+@pytest.mark.parametrize("nq", [5, 70])
+@pytest.mark.parametrize("form", [0, 1])
+def test_ivf_long_lists(gpu, oracle, nq, form):
+    """Lists longer than one work item's row chunk (2048 rows) and ragged 256-row tiles; with nq = 70 a
+    list's probing queries split over several query groups."""
+    xb, xq = faiss_metal_case(21000, nq, 64)
+    ix, (cen, off, ids, codes) = _ivf(gpu, xb, 4, 2)
+    ix.form = form
+    assert np.diff(off).max() > 2048
+    D, I = ix.search(xq, 20)
+    Do, Io, Po = oracle.ivf_search(cen, off, ids, codes, xq, 20, 2, 0)
+    assert np.array_equal(ix.last_probes(nq), Po)
+    check_topk_parity(xb, xq, D, I, Do, Io)
 
 
 def test_ivf_full_probe_equals_flat(gpu, oracle):
