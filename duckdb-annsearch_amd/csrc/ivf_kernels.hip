@@ -349,31 +349,35 @@ ivf_scan_topk(const float *__restrict__ Q, int d, const float *__restrict__ code
 // (list, row chunk, query group) with the group fastest and dealt XCD-contiguously, so the groups
 // that re-read one row chunk run together on one XCD and share its L2.
 //
-// Block: 4 waves, 2 blocks per CU (2 waves per SIMD, ≤ 256 VGPRs).  Wave w owns ≤ DT_NW = 8 of the
-// item's ≤ 32 queries and every row of the tile: DT_R = 8 rows per lane (tile = 512 rows), an 8 × 8
-// accumulator block per lane, so each K step issues 16 ds_read_b128 for 256 FMAs.
+// Block: 4 waves, 2 blocks per CU.  Wave w owns ≤ DT_NW = 8 of the item's ≤ 32 queries and every
+// row of the tile: DT_R = 4 rows per lane (tile = 256 rows), a 4 × 8 accumulator block per lane, so
+// each 4-dim step issues 12 ds_read_b128 for 128 FMAs.
 //
-// Staging: LDS-DMA (global_load_lds_dwordx4) into a 3-stage ring, raw barrier + counted vmcnt, two
-// chunks in flight.  Per stage: x = [512 rows][3 float4] (BK = 12 dims; 3 is odd ⇒ the per-lane
-// ds_read_b128 of 16 consecutive rows hits 16 distinct bank groups), then each wave's query block
-// [8 queries][3 float4].  Per chunk a wave issues DT_XPW = 6 x pieces + 1 query piece.
+// Staging: LDS-DMA (global_load_lds_dwordx4) into two stages, one chunk in flight while the other
+// is read.  A chunk is DT_BK = 32 dims = one whole 128-B line of each row: every line is fetched
+// by one chunk of one item (narrower chunks leave a line to be re-read by the next chunk after the
+// XCD's L2 has streamed other blocks' rows through — measured 2× FETCH_SIZE at 12-dim chunks).
+// Stage image: x = [256 rows][8 float4] with the float4 index XOR-swizzled by (row >> 1) & 7
+// (applied on the DMA's per-lane SOURCE address — the DMA destination is lane-linear), so the
+// per-lane ds_read_b128 of 16 consecutive rows hits 16 distinct bank groups; then each wave's
+// query block [8 queries][8 float4].  Per chunk a wave issues DT_XPW = 8 x pieces (8 rows × one
+// line each) + 1 query piece.
 constexpr int DT_WAVES = 4;
 constexpr int DT_THREADS = 64 * DT_WAVES;
-constexpr int DT_R = 8;
+constexpr int DT_R = 4;
 constexpr int DT_NW = 8;
 constexpr int DT_TR = 64 * DT_R;
-constexpr int DT_BK = 12;
+constexpr int DT_BK = 32;
 constexpr int DT_F4 = DT_BK / 4;
-constexpr int DT_XF4 = DT_TR * DT_F4;               // 1536 float4 of rows per stage
-constexpr int DT_XPW = DT_XF4 / 64 / DT_WAVES;      // 6 x pieces per wave per chunk
-constexpr int DT_QF4 = DT_NW * DT_F4;               // 24 float4 of queries per wave per stage
+constexpr int DT_XF4 = DT_TR * DT_F4;               // 2048 float4 of rows per stage
+constexpr int DT_XPW = DT_XF4 / 64 / DT_WAVES;      // 8 x pieces per wave per chunk
+constexpr int DT_QF4 = DT_NW * DT_F4;               // 64 float4 of queries per wave per stage
 constexpr int DT_STAGE_F4 = DT_XF4 + DT_WAVES * DT_QF4;
-constexpr int DT_STAGES = 3;
+constexpr int DT_STAGES = 2;
 static_assert(DT_WAVES * DT_NW == IVF_G, "a dot item covers one IVF_G query group");
 static_assert(IVF_CH % DT_TR == 0, "row chunks are whole tiles");
-static_assert(DT_XPW * 64 * DT_WAVES == DT_XF4 && DT_QF4 <= 64, "piece split");
-static_assert(DT_XPW + 1 == 7, "IVF_DT_WAIT's vmcnt literal is the pieces per chunk");
-static_assert((64 % DT_F4) == 1 && ((DT_XPW * 64) % DT_F4) == 0, "c4 of x piece i is (lane + i) % 3");
+static_assert(DT_XPW * 64 * DT_WAVES == DT_XF4 && DT_QF4 == 64, "piece split");
+static_assert(DT_F4 == 8 && DT_R * 64 == DT_WAVES * DT_XPW * 8, "one piece = 8 rows x 8 float4");
 
 typedef __attribute__((address_space(3))) void *ivf_lds_ptr;
 typedef __attribute__((address_space(1))) void *ivf_gbl_ptr;
@@ -382,10 +386,10 @@ __device__ __forceinline__ void ivf_glds16(const float *src, float *lds_wave_bas
     __builtin_amdgcn_global_load_lds((ivf_gbl_ptr)(src), (ivf_lds_ptr)(lds_wave_base), 16, 0, 0);
 }
 
-// Wait for this wave's pieces of the chunk about to be read (leaving the next chunk's 7 in flight,
-// or none), then a raw barrier: past it every wave's pieces of that chunk have landed and every wave
-// has finished reading the stage the next issue overwrites.  "memory" pins LDS accesses around it.
-#define IVF_DT_WAIT(N) asm volatile("s_waitcnt vmcnt(" #N ")\n\ts_barrier" ::: "memory")
+// Wait for this wave's pieces of the chunk about to be read, then a raw barrier: past it every
+// wave's pieces have landed and every wave has finished reading the stage the next issue
+// overwrites.  "memory" pins LDS accesses around it.
+#define IVF_DT_WAIT() asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory")
 
 template <int NW, bool IP>
 __device__ __forceinline__ void ivf_dot_item(int d, const float *__restrict__ codes, const float *__restrict__ xn,
@@ -399,31 +403,34 @@ __device__ __forceinline__ void ivf_dot_item(int d, const float *__restrict__ co
     const int ntile = (int)((r1 - r0 + DT_TR - 1) / DT_TR);
     const int total = ntile * nk;
 
-    // ---- issue side: this wave's x pieces p = wave·6 + i cover float4 s = 64p + lane = (row, c4) ----
+    // ---- issue side: x piece i of wave w = rows w·64 + 8i + lane/8, one line each; lane's float4
+    // (lane & 7) of the line holds logical float4 (lane & 7) ^ swz(row) ----
+    const int prow = wave * 64 + (lane >> 3);
+    int xc4[DT_XPW];
+#pragma unroll
+    for (int i = 0; i < DT_XPW; ++i) xc4[i] = 4 * ((lane & 7) ^ ((4 * i + (lane >> 4)) & 7));
+    const int qc4 = 4 * (lane & 7);
     int it_kc = 0;
     int64_t it_t0 = r0;
-    const float *xb[DT_XPW];
     auto issue = [&](int buf) {
         float *stage = ring + (size_t)buf * DT_STAGE_F4 * 4;
-        if (it_kc == 0) {
+        const int k0 = it_kc * DT_BK;
+        const bool full_k = k0 + DT_BK <= d;
+        if (it_t0 + DT_TR <= r1 && full_k) {  // interior tile, whole chunk: no clamps
+            const float *base = codes + (it_t0 + prow) * (int64_t)d + k0;
+#pragma unroll
+            for (int i = 0; i < DT_XPW; ++i)
+                ivf_glds16(base + (int64_t)(8 * i) * d + xc4[i], stage + (size_t)(wave * DT_XPW + i) * 64 * 4);
+        } else {  // rows past the chunk re-load its last row, dims past d any valid float4 (never read)
 #pragma unroll
             for (int i = 0; i < DT_XPW; ++i) {
-                const int srow = (64 * (wave * DT_XPW + i) + lane) / DT_F4;
-                const int64_t row = it_t0 + srow < r1 ? it_t0 + srow : r1 - 1;  // past the chunk: any valid row
-                xb[i] = codes + row * (int64_t)d;
+                const int64_t row = it_t0 + prow + 8 * i < r1 ? it_t0 + prow + 8 * i : r1 - 1;
+                const int kk = k0 + xc4[i] < d ? k0 + xc4[i] : d - 4;
+                ivf_glds16(codes + row * (int64_t)d + kk, stage + (size_t)(wave * DT_XPW + i) * 64 * 4);
             }
         }
-        const int k0 = it_kc * DT_BK;
-        const bool full = k0 + DT_BK <= d;
-#pragma unroll
-        for (int i = 0; i < DT_XPW; ++i) {
-            int kk = k0 + 4 * ((lane + i) % DT_F4);
-            if (!full) kk = kk < d ? kk : d - 4;  // past d: any valid float4 (never read)
-            ivf_glds16(xb[i] + kk, stage + (size_t)(wave * DT_XPW + i) * 64 * 4);
-        }
-        if (lane < DT_QF4) {
-            int kk = k0 + 4 * (lane % DT_F4);
-            if (!full) kk = kk < d ? kk : d - 4;
+        {
+            const int kk = k0 + qc4 < d ? k0 + qc4 : d - 4;
             ivf_glds16(qsrc + kk, stage + (size_t)(DT_XF4 + wave * DT_QF4) * 4);
         }
         if (++it_kc == nk) { it_kc = 0; it_t0 += DT_TR; }
@@ -442,24 +449,24 @@ __device__ __forceinline__ void ivf_dot_item(int d, const float *__restrict__ co
 #pragma unroll
         for (int j = 0; j < NA; ++j) acc[r][j] = 0.f;
 
+    const int swz = (lane >> 1) & 7;  // (row >> 1) & 7 of rows lane + 64r
     issue(0);
-    if (total > 1) issue(1);
     int kc = 0, buf = 0;
     int64_t t0 = r0;
     for (int c = 0; c < total; ++c) {
-        if (c + 1 < total) IVF_DT_WAIT(7); else IVF_DT_WAIT(0);
-        if (c + 2 < total) issue(buf == 0 ? DT_STAGES - 1 : buf - 1);
+        IVF_DT_WAIT();
+        if (c + 1 < total) issue(buf ^ 1);
         const float *X = ring + (size_t)buf * DT_STAGE_F4 * 4;
         const float *Qw = X + (size_t)(DT_XF4 + wave * DT_QF4) * 4;
         const int k0 = kc * DT_BK;
         const int nu = d - k0 >= DT_BK ? DT_F4 : (d - k0) / 4;
         if (NW > 0) {
-#pragma unroll 1
+#pragma unroll 2
             for (int u = 0; u < nu; ++u) {
                 float4 xv[DT_R], qv[NA];
+                const float *xl = X + (lane * DT_F4 + (u ^ swz)) * 4;
 #pragma unroll
-                for (int r = 0; r < DT_R; ++r)
-                    xv[r] = *reinterpret_cast<const float4 *>(X + ((lane + 64 * r) * DT_F4 + u) * 4);
+                for (int r = 0; r < DT_R; ++r) xv[r] = *reinterpret_cast<const float4 *>(xl + r * 64 * DT_F4 * 4);
 #pragma unroll
                 for (int j = 0; j < NW; ++j) qv[j] = *reinterpret_cast<const float4 *>(Qw + (j * DT_F4 + u) * 4);
 #pragma unroll
@@ -504,7 +511,7 @@ __device__ __forceinline__ void ivf_dot_item(int d, const float *__restrict__ co
             kc = 0;
             t0 += DT_TR;
         }
-        buf = buf == DT_STAGES - 1 ? 0 : buf + 1;
+        buf ^= 1;
     }
 #pragma unroll
     for (int j = 0; j < NW; ++j) {
@@ -545,7 +552,7 @@ ivf_scan_dot(const float *__restrict__ Q, const float *__restrict__ qn, int d, c
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wq0 = __builtin_amdgcn_readfirstlane(wave * nqi / DT_WAVES);
     const int nwq = __builtin_amdgcn_readfirstlane((wave + 1) * nqi / DT_WAVES - wave * nqi / DT_WAVES);
-    // query-piece lanes: slot lane / 3 of this wave's block (slots past nwq re-load the wave's first)
+    // query-piece lane: slot lane / 8 of this wave's block (slots past nwq re-load the wave's first)
     const int qslot = lane / DT_F4 < nwq ? lane / DT_F4 : 0;
     const float *qsrc = Q + (int64_t)(bucket[boff + wq0 + qslot] / nprobe) * d;
 #define HIPANN_DOT_ITEM(NW)                                                                                         \
