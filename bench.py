@@ -220,6 +220,10 @@ def main():
         extra["distinct_lists_probed"] = int(np.unique(probes[probes >= 0]).size)
         from ivf_build import scan_pairs
         extra["scanned_pairs_per_batch_local"] = scan_pairs(index, probes)
+        from ivf_build import scan_group_rows
+        extra["group_rows_per_batch_local"] = scan_group_rows(index, probes)
+        cnt = np.bincount(probes[probes >= 0].ravel(), minlength=args.nlist)
+        extra["probes_per_list_p50_p90_max"] = [int(np.percentile(cnt, 50)), int(np.percentile(cnt, 90)), int(cnt.max())]
 
     # ---------------- timed region ----------------
     index.set_kernel_timing(True)

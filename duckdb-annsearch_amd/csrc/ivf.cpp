@@ -138,7 +138,10 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     sh.bucket.ensure(sizeof(int) * (size_t)nq * np, sh.device);
     HIPANN_REQUIRE((int64_t)nq * np < (int64_t)0x7fffffff, "nq * nprobe too large");
     sh.slot_off.ensure(sizeof(int) * ((size_t)nq * np + 1), sh.device);
-    launch_ivf_plan(sh.coarse_i.get<int64_t>(), nq, np, sh.list_len.get<int>(), nlist, sh.cnt.get<int>(),
+    // the decomposed form needs float4 rows; other shapes take the direct kernel (also on the GPU)
+    const int form = ix.form == kFormDecomposed && ivf_dot_supported(xq, d, sh.codes) ? kFormDecomposed : kFormDirect;
+    const int group = ivf_group_size(form);
+    launch_ivf_plan(sh.coarse_i.get<int64_t>(), nq, np, sh.list_len.get<int>(), nlist, group, sh.cnt.get<int>(),
                     sh.bucket_off.get<int>(), sh.item_off.get<int>(), sh.cursor.get<int>(), sh.bucket.get<int>(),
                     sh.slot_off.get<int>(), st);
     // 3. scan: one k-list per (query, probe, row chunk) slot — every slot is written by exactly one item
@@ -146,9 +149,7 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     HIPANN_REQUIRE((int64_t)np * nq * sh.max_nch < (int64_t)0x7fffffff, "too many partial lists");
     sh.part_d.ensure(parts * sizeof(float), sh.device);
     sh.part_i.ensure(parts * sizeof(int), sh.device);
-    const int64_t max_items = ivf_max_items(nq, np, nlist, sh.max_nch, sh.n);
-    // the decomposed form needs float4 rows; other shapes take the direct kernel (also on the GPU)
-    const int form = ix.form == kFormDecomposed && ivf_dot_supported(xq, d, sh.codes) ? kFormDecomposed : kFormDirect;
+    const int64_t max_items = ivf_max_items(nq, np, nlist, sh.max_nch, sh.n, group);
     const float *qn = nullptr;
     if (form == kFormDecomposed && metric == kL2) {
         sh.qn.ensure(sizeof(float) * (size_t)nq, sh.device);

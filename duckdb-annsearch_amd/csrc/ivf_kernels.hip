@@ -42,10 +42,10 @@ __global__ void ivf_count(const int64_t *__restrict__ probes, int64_t npairs, co
     atomicAdd(cnt + l, 1);
 }
 
-// Single block: bucket_off[l] = Σ_{<l} cnt, item_off[l] = Σ_{<l} ceil(cnt/G)·nch(l) (one item per
+// Single block: bucket_off[l] = Σ_{<l} cnt, item_off[l] = Σ_{<l} ceil(cnt/group)·nch(l) (one item per
 // (query group, row chunk) of each list); cursor[l] = 0; total items in item_off[nlist].
 __global__ void __launch_bounds__(1024) ivf_plan(const int *__restrict__ cnt, const int *__restrict__ list_len,
-                                                 int nlist, int *__restrict__ bucket_off,
+                                                 int nlist, int group, int *__restrict__ bucket_off,
                                                  int *__restrict__ item_off, int *__restrict__ cursor) {
     __shared__ int sb[1024], si[1024];
     __shared__ int carry_b, carry_i;
@@ -54,7 +54,7 @@ __global__ void __launch_bounds__(1024) ivf_plan(const int *__restrict__ cnt, co
     for (int base = 0; base < nlist; base += 1024) {
         const int l = base + threadIdx.x;
         const int c = l < nlist ? cnt[l] : 0;
-        const int items = l < nlist ? ((c + IVF_G - 1) / IVF_G) * ivf_nch(list_len[l]) : 0;
+        const int items = l < nlist ? ((c + group - 1) / group) * ivf_nch(list_len[l]) : 0;
         sb[threadIdx.x] = c;
         si[threadIdx.x] = items;
         __syncthreads();
@@ -345,39 +345,45 @@ ivf_scan_topk(const float *__restrict__ Q, int d, const float *__restrict__ code
 // 305-318).  One FMA per (query, row, dim) instead of the direct form's subtract + FMA, so the
 // VALU floor halves; the kernel is register-blocked to keep LDS traffic below the FMA rate.
 //
-// Work item and outputs as ivf_scan_topk (same plan, slots and IVF_G / IVF_CH), items ordered
+// Work item and outputs as ivf_scan_topk (same plan and slots, IVF_CH-row chunks, but groups of
+// ≤ DT_G = 64 queries), items ordered
 // (list, row chunk, query group) with the group fastest and dealt XCD-contiguously, so the groups
 // that re-read one row chunk run together on one XCD and share its L2.
 //
-// Block: 4 waves, 2 blocks per CU.  Wave w owns ≤ DT_NW = 8 of the item's ≤ 32 queries and every
-// row of the tile: DT_R = 4 rows per lane (tile = 256 rows), a 4 × 8 accumulator block per lane, so
-// each 4-dim step issues 12 ds_read_b128 for 128 FMAs.
+// Block: 4 waves, 2 blocks per CU.  Wave w owns ≤ DT_NW = 16 of the item's ≤ DT_G = 64 queries
+// (so a list probed by up to 64 queries of the batch is streamed once) and every row of the tile:
+// DT_R = 4 rows per lane (tile = 256 rows); per 4-dim step it reads its 4 rows' float4 once and
+// applies them to its queries in blocks of ≤ 8 (8 broadcast ds_read_b128 + 128 FMAs per block).
 //
 // Staging: LDS-DMA (global_load_lds_dwordx4) into two stages, one chunk in flight while the other
-// is read.  A chunk is DT_BK = 32 dims = one whole 128-B line of each row: every line is fetched
-// by one chunk of one item (narrower chunks leave a line to be re-read by the next chunk after the
-// XCD's L2 has streamed other blocks' rows through — measured 2× FETCH_SIZE at 12-dim chunks).
-// Stage image: x = [256 rows][8 float4] with the float4 index XOR-swizzled by (row >> 1) & 7
-// (applied on the DMA's per-lane SOURCE address — the DMA destination is lane-linear), so the
-// per-lane ds_read_b128 of 16 consecutive rows hits 16 distinct bank groups; then each wave's
-// query block [8 queries][8 float4].  Per chunk a wave issues DT_XPW = 8 x pieces (8 rows × one
-// line each) + 1 query piece.
+// is read.  A chunk is DT_BK = 32 dims = one whole 128-B line of each row, so every line is fetched
+// by one chunk of one item (12-dim chunks, whose lines span three chunks, were re-fetched after the
+// XCD's L2 had streamed other blocks' rows through: 2× FETCH_SIZE).  Stage image: x = [256 rows]
+// [8 float4] with the float4 index XOR-swizzled by (row >> 1) & 7 (applied on the DMA's per-lane
+// SOURCE address — the DMA destination is lane-linear) so that the per-lane ds_read_b128 of 16
+// consecutive rows hits 16 distinct bank groups; then each wave's query block [16 queries][8 float4].
+// Per chunk a wave issues DT_XPW = 8 x pieces (8 rows × one line each) + 1 or 2 query pieces.
 constexpr int DT_WAVES = 4;
 constexpr int DT_THREADS = 64 * DT_WAVES;
 constexpr int DT_R = 4;
-constexpr int DT_NW = 8;
+constexpr int DT_NW = 16;
+constexpr int DT_G = DT_WAVES * DT_NW;
+constexpr int DT_QB = 8;                            // queries per register block
 constexpr int DT_TR = 64 * DT_R;
 constexpr int DT_BK = 32;
-constexpr int DT_F4 = DT_BK / 4;
-constexpr int DT_XF4 = DT_TR * DT_F4;               // 2048 float4 of rows per stage
-constexpr int DT_XPW = DT_XF4 / 64 / DT_WAVES;      // 8 x pieces per wave per chunk
-constexpr int DT_QF4 = DT_NW * DT_F4;               // 64 float4 of queries per wave per stage
+constexpr int DT_F4 = DT_BK / 4;                    // float4 per row per chunk
+constexpr int DT_RP = 64 / DT_F4;                   // rows per x piece
+constexpr int DT_SWZ = 16 / DT_F4;                  // rows sharing one swizzle value
+constexpr int DT_XF4 = DT_TR * DT_F4;               // float4 of rows per stage
+constexpr int DT_XPW = DT_XF4 / 64 / DT_WAVES;      // x pieces per wave per chunk
+constexpr int DT_QF4 = DT_NW * DT_F4;               // float4 of queries per wave per stage
 constexpr int DT_STAGE_F4 = DT_XF4 + DT_WAVES * DT_QF4;
 constexpr int DT_STAGES = 2;
-static_assert(DT_WAVES * DT_NW == IVF_G, "a dot item covers one IVF_G query group");
 static_assert(IVF_CH % DT_TR == 0, "row chunks are whole tiles");
-static_assert(DT_XPW * 64 * DT_WAVES == DT_XF4 && DT_QF4 == 64, "piece split");
-static_assert(DT_F4 == 8 && DT_R * 64 == DT_WAVES * DT_XPW * 8, "one piece = 8 rows x 8 float4");
+static_assert(DT_XPW * 64 * DT_WAVES == DT_XF4 && DT_QF4 == 128, "piece split");
+static_assert((DT_F4 & (DT_F4 - 1)) == 0 && DT_F4 <= 16 && (DT_TR / DT_WAVES) % (DT_SWZ * DT_F4) == 0,
+              "swizzle: a wave's rows start on a swizzle period");
+static_assert(DT_STAGES * DT_STAGE_F4 * 16 * 2 <= 160 * 1024, "two blocks per CU");
 
 typedef __attribute__((address_space(3))) void *ivf_lds_ptr;
 typedef __attribute__((address_space(1))) void *ivf_gbl_ptr;
@@ -386,105 +392,126 @@ __device__ __forceinline__ void ivf_glds16(const float *src, float *lds_wave_bas
     __builtin_amdgcn_global_load_lds((ivf_gbl_ptr)(src), (ivf_lds_ptr)(lds_wave_base), 16, 0, 0);
 }
 
-// Wait for this wave's pieces of the chunk about to be read, then a raw barrier: past it every
-// wave's pieces have landed and every wave has finished reading the stage the next issue
-// overwrites.  "memory" pins LDS accesses around it.
-#define IVF_DT_WAIT() asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory")
+// Wait until at most N of this wave's DMA instructions are outstanding, then a raw barrier: past it
+// every wave's pieces of the chunk to be read have landed and every wave has finished reading the
+// stage the next issue overwrites.  "memory" pins LDS accesses around it.
+template <int N>
+__device__ __forceinline__ void ivf_dt_wait_barrier() {
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+// acc[r][J0 + j] += q_j · x_r over one float4 of dims, for the NB queries J0 .. J0 + NB − 1
+template <int NB, int J0, int NA>
+__device__ __forceinline__ void ivf_dot_block(const float *__restrict__ Qw, int u, const float4 (&xv)[DT_R],
+                                              float (&acc)[DT_R][NA]) {
+    float4 qv[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) qv[j] = *reinterpret_cast<const float4 *>(Qw + ((J0 + j) * DT_F4 + u) * 4);
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int r = 0; r < DT_R; ++r) acc[r][J0 + j] = fmaf(qv[j].x, xv[r].x, acc[r][J0 + j]);
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int r = 0; r < DT_R; ++r) acc[r][J0 + j] = fmaf(qv[j].y, xv[r].y, acc[r][J0 + j]);
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int r = 0; r < DT_R; ++r) acc[r][J0 + j] = fmaf(qv[j].z, xv[r].z, acc[r][J0 + j]);
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+#pragma unroll
+        for (int r = 0; r < DT_R; ++r) acc[r][J0 + j] = fmaf(qv[j].w, xv[r].w, acc[r][J0 + j]);
+}
 
 template <int NW, bool IP>
 __device__ __forceinline__ void ivf_dot_item(int d, const float *__restrict__ codes, const float *__restrict__ xn,
-                                             int64_t r0, int64_t r1, const float *qsrc, const float *qn, int wq0,
-                                             const int *__restrict__ bucket, int boff, int nprobe,
-                                             const int *__restrict__ slot_off, int chunk, int k, float *ring,
-                                             float *__restrict__ part_d, int *__restrict__ part_i) {
+                                             int64_t r0, int64_t r1, const float *qsrc0, const float *qsrc1,
+                                             const float *qn, int wq0, const int *__restrict__ bucket, int boff,
+                                             int nprobe, const int *__restrict__ slot_off, int chunk, int k,
+                                             float *ring, float *__restrict__ part_d, int *__restrict__ part_i) {
     constexpr int NA = NW > 0 ? NW : 1;
+    constexpr int QP = NW > DT_QB ? 2 : 1;       // query pieces per chunk
+    constexpr int PIECES = DT_XPW + QP;          // DMA instructions per wave per chunk
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nk = (d + DT_BK - 1) / DT_BK;
     const int ntile = (int)((r1 - r0 + DT_TR - 1) / DT_TR);
     const int total = ntile * nk;
 
-    // ---- issue side: x piece i of wave w = rows w·64 + 8i + lane/8, one line each; lane's float4
-    // (lane & 7) of the line holds logical float4 (lane & 7) ^ swz(row) ----
-    const int prow = wave * 64 + (lane >> 3);
+    // ---- issue side: x piece i of wave w = rows w·(TR/WAVES) + i·RP + lane / F4; the lane's float4
+    // slot (lane % F4) of its row holds logical float4 (lane % F4) ^ swz(row) ----
+    const int prow = wave * (DT_TR / DT_WAVES) + lane / DT_F4;
     int xc4[DT_XPW];
 #pragma unroll
-    for (int i = 0; i < DT_XPW; ++i) xc4[i] = 4 * ((lane & 7) ^ ((4 * i + (lane >> 4)) & 7));
-    const int qc4 = 4 * (lane & 7);
-    int it_kc = 0;
+    for (int i = 0; i < DT_XPW; ++i)
+        xc4[i] = 4 * ((lane % DT_F4) ^ (((i * DT_RP + lane / DT_F4) / DT_SWZ) & (DT_F4 - 1)));
+    const int qc4 = 4 * (lane % DT_F4);
+    int it_kc = 0, it_buf = 0;
     int64_t it_t0 = r0;
-    auto issue = [&](int buf) {
-        float *stage = ring + (size_t)buf * DT_STAGE_F4 * 4;
+    auto issue = [&]() {
+        float *stage = ring + (size_t)it_buf * DT_STAGE_F4 * 4;
         const int k0 = it_kc * DT_BK;
         const bool full_k = k0 + DT_BK <= d;
         if (it_t0 + DT_TR <= r1 && full_k) {  // interior tile, whole chunk: no clamps
             const float *base = codes + (it_t0 + prow) * (int64_t)d + k0;
 #pragma unroll
             for (int i = 0; i < DT_XPW; ++i)
-                ivf_glds16(base + (int64_t)(8 * i) * d + xc4[i], stage + (size_t)(wave * DT_XPW + i) * 64 * 4);
+                ivf_glds16(base + (int64_t)(DT_RP * i) * d + xc4[i], stage + (size_t)(wave * DT_XPW + i) * 64 * 4);
         } else {  // rows past the chunk re-load its last row, dims past d any valid float4 (never read)
 #pragma unroll
             for (int i = 0; i < DT_XPW; ++i) {
-                const int64_t row = it_t0 + prow + 8 * i < r1 ? it_t0 + prow + 8 * i : r1 - 1;
+                const int64_t row = it_t0 + prow + DT_RP * i < r1 ? it_t0 + prow + DT_RP * i : r1 - 1;
                 const int kk = k0 + xc4[i] < d ? k0 + xc4[i] : d - 4;
                 ivf_glds16(codes + row * (int64_t)d + kk, stage + (size_t)(wave * DT_XPW + i) * 64 * 4);
             }
         }
-        {
-            const int kk = k0 + qc4 < d ? k0 + qc4 : d - 4;
-            ivf_glds16(qsrc + kk, stage + (size_t)(DT_XF4 + wave * DT_QF4) * 4);
-        }
+        const int kq = k0 + qc4 < d ? k0 + qc4 : d - 4;
+        float *qdst = stage + (size_t)(DT_XF4 + wave * DT_QF4) * 4;
+        ivf_glds16(qsrc0 + kq, qdst);
+        if (QP == 2) ivf_glds16(qsrc1 + kq, qdst + 64 * 4);
         if (++it_kc == nk) { it_kc = 0; it_t0 += DT_TR; }
+        it_buf = it_buf == DT_STAGES - 1 ? 0 : it_buf + 1;
     };
 
     // ---- compute side ----
     WaveList<1, int> lists[NA];
 #pragma unroll
     for (int j = 0; j < NA; ++j) lists[j].init();
-    float qnv[NA];
-#pragma unroll
-    for (int j = 0; j < NA; ++j) qnv[j] = (!IP && j < NW) ? qn[bucket[boff + wq0 + j] / nprobe] : 0.f;
+    // ‖q_j‖² held by lane j (read back with readlane in the epilogue: no per-query SGPRs)
+    const float qn_lane = (!IP && lane < NW) ? qn[bucket[boff + wq0 + lane] / nprobe] : 0.f;
     float acc[DT_R][NA];
 #pragma unroll
     for (int r = 0; r < DT_R; ++r)
 #pragma unroll
         for (int j = 0; j < NA; ++j) acc[r][j] = 0.f;
 
-    const int swz = (lane >> 1) & 7;  // (row >> 1) & 7 of rows lane + 64r
-    issue(0);
+    const int swz = (lane / DT_SWZ) & (DT_F4 - 1);  // swz(row) of rows lane + 64r
+#pragma unroll
+    for (int s = 0; s < DT_STAGES - 1; ++s)
+        if (s < total) issue();
     int kc = 0, buf = 0;
     int64_t t0 = r0;
     for (int c = 0; c < total; ++c) {
-        IVF_DT_WAIT();
-        if (c + 1 < total) issue(buf ^ 1);
+        // chunks c+1 .. c+STAGES-2 may stay in flight
+        const int ahead = total - 1 - c;
+        if (ahead >= DT_STAGES - 2) ivf_dt_wait_barrier<(DT_STAGES - 2) * PIECES>();
+        else if (ahead == 1) ivf_dt_wait_barrier<PIECES>();
+        else ivf_dt_wait_barrier<0>();
+        if (c + DT_STAGES - 1 < total) issue();
         const float *X = ring + (size_t)buf * DT_STAGE_F4 * 4;
         const float *Qw = X + (size_t)(DT_XF4 + wave * DT_QF4) * 4;
         const int k0 = kc * DT_BK;
         const int nu = d - k0 >= DT_BK ? DT_F4 : (d - k0) / 4;
         if (NW > 0) {
-#pragma unroll 2
+#pragma unroll 1
             for (int u = 0; u < nu; ++u) {
-                float4 xv[DT_R], qv[NA];
+                float4 xv[DT_R];
                 const float *xl = X + (lane * DT_F4 + (u ^ swz)) * 4;
 #pragma unroll
                 for (int r = 0; r < DT_R; ++r) xv[r] = *reinterpret_cast<const float4 *>(xl + r * 64 * DT_F4 * 4);
-#pragma unroll
-                for (int j = 0; j < NW; ++j) qv[j] = *reinterpret_cast<const float4 *>(Qw + (j * DT_F4 + u) * 4);
-#pragma unroll
-                for (int j = 0; j < NW; ++j)
-#pragma unroll
-                    for (int r = 0; r < DT_R; ++r) acc[r][j] = fmaf(qv[j].x, xv[r].x, acc[r][j]);
-#pragma unroll
-                for (int j = 0; j < NW; ++j)
-#pragma unroll
-                    for (int r = 0; r < DT_R; ++r) acc[r][j] = fmaf(qv[j].y, xv[r].y, acc[r][j]);
-#pragma unroll
-                for (int j = 0; j < NW; ++j)
-#pragma unroll
-                    for (int r = 0; r < DT_R; ++r) acc[r][j] = fmaf(qv[j].z, xv[r].z, acc[r][j]);
-#pragma unroll
-                for (int j = 0; j < NW; ++j)
-#pragma unroll
-                    for (int r = 0; r < DT_R; ++r) acc[r][j] = fmaf(qv[j].w, xv[r].w, acc[r][j]);
+                if constexpr (NW > 0) ivf_dot_block<(NW < DT_QB ? NW : DT_QB), 0, NA>(Qw, u, xv, acc);
+                if constexpr (NW > DT_QB) ivf_dot_block<NW - DT_QB, DT_QB, NA>(Qw, u, xv, acc);
             }
         }
         if (++kc == nk) {  // tile done: offer its rows
@@ -500,7 +527,9 @@ __device__ __forceinline__ void ivf_dot_item(int d, const float *__restrict__ co
                         if (IP) {
                             key = -acc[r][j];
                         } else {
-                            key = fmaf(-2.f, acc[r][j], qnv[j] + xnr);
+                            const float qnj = __builtin_bit_cast(
+                                float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, qn_lane), j));
+                            key = fmaf(-2.f, acc[r][j], qnj + xnr);
                             key = key < 0.f ? 0.f : key;
                         }
                         lists[j].offer(v ? key : __builtin_inff(), v ? (int)row : 0x7fffffff, k - 1);
@@ -511,7 +540,7 @@ __device__ __forceinline__ void ivf_dot_item(int d, const float *__restrict__ co
             kc = 0;
             t0 += DT_TR;
         }
-        buf ^= 1;
+        buf = buf == DT_STAGES - 1 ? 0 : buf + 1;
     }
 #pragma unroll
     for (int j = 0; j < NW; ++j) {
@@ -540,7 +569,7 @@ ivf_scan_dot(const float *__restrict__ Q, const float *__restrict__ qn, int d, c
     const int l = lo;
     const int64_t lr0 = list_off[l], lr1 = list_off[l + 1];
     const int c = cnt[l];
-    const int ng = (c + IVF_G - 1) / IVF_G;
+    const int ng = (c + DT_G - 1) / DT_G;
     const int rem = item - item_off[l];
     const int chunk = rem / ng, g = rem - chunk * ng;  // (row chunk, query group), group fastest
     const int q_begin = (int)((int64_t)g * c / ng), q_end = (int)((int64_t)(g + 1) * c / ng);
@@ -552,12 +581,14 @@ ivf_scan_dot(const float *__restrict__ Q, const float *__restrict__ qn, int d, c
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wq0 = __builtin_amdgcn_readfirstlane(wave * nqi / DT_WAVES);
     const int nwq = __builtin_amdgcn_readfirstlane((wave + 1) * nqi / DT_WAVES - wave * nqi / DT_WAVES);
-    // query-piece lane: slot lane / 8 of this wave's block (slots past nwq re-load the wave's first)
-    const int qslot = lane / DT_F4 < nwq ? lane / DT_F4 : 0;
-    const float *qsrc = Q + (int64_t)(bucket[boff + wq0 + qslot] / nprobe) * d;
+    // query-piece lanes: piece h, lane → slot (64h + lane) / DT_F4 of this wave's block (slots past nwq
+    // re-load the wave's first query)
+    const int s0 = lane / DT_F4, s1 = (64 + lane) / DT_F4;
+    const float *qsrc0 = Q + (int64_t)(bucket[boff + wq0 + (s0 < nwq ? s0 : 0)] / nprobe) * d;
+    const float *qsrc1 = Q + (int64_t)(bucket[boff + wq0 + (s1 < nwq ? s1 : 0)] / nprobe) * d;
 #define HIPANN_DOT_ITEM(NW)                                                                                         \
-    ivf_dot_item<NW, IP>(d, codes, xn, r0, r1, qsrc, qn, wq0, bucket, boff, nprobe, slot_off, chunk, k, ring, part_d, \
-                         part_i)
+    ivf_dot_item<NW, IP>(d, codes, xn, r0, r1, qsrc0, qsrc1, qn, wq0, bucket, boff, nprobe, slot_off, chunk, k, ring, \
+                         part_d, part_i)
     switch (nwq) {
         case 0: HIPANN_DOT_ITEM(0); break;
         case 1: HIPANN_DOT_ITEM(1); break;
@@ -567,7 +598,15 @@ ivf_scan_dot(const float *__restrict__ Q, const float *__restrict__ qn, int d, c
         case 5: HIPANN_DOT_ITEM(5); break;
         case 6: HIPANN_DOT_ITEM(6); break;
         case 7: HIPANN_DOT_ITEM(7); break;
-        default: HIPANN_DOT_ITEM(8); break;
+        case 8: HIPANN_DOT_ITEM(8); break;
+        case 9: HIPANN_DOT_ITEM(9); break;
+        case 10: HIPANN_DOT_ITEM(10); break;
+        case 11: HIPANN_DOT_ITEM(11); break;
+        case 12: HIPANN_DOT_ITEM(12); break;
+        case 13: HIPANN_DOT_ITEM(13); break;
+        case 14: HIPANN_DOT_ITEM(14); break;
+        case 15: HIPANN_DOT_ITEM(15); break;
+        default: HIPANN_DOT_ITEM(16); break;
     }
 #undef HIPANN_DOT_ITEM
 }
@@ -613,14 +652,16 @@ ivf_merge_topk(const float *__restrict__ pd, const int *__restrict__ pi, const i
 }
 
 // ---------------------------------------------------------------------------------------------
-void launch_ivf_plan(const int64_t *probes, int64_t nq, int nprobe, const int *list_len, int nlist, int *cnt,
-                     int *bucket_off, int *item_off, int *cursor, int *bucket, int *slot_off, hipStream_t st) {
+void launch_ivf_plan(const int64_t *probes, int64_t nq, int nprobe, const int *list_len, int nlist, int group,
+                     int *cnt, int *bucket_off, int *item_off, int *cursor, int *bucket, int *slot_off,
+                     hipStream_t st) {
     const int64_t npairs = nq * nprobe;
     HIPANN_CHECK(hipMemsetAsync(cnt, 0, sizeof(int) * (size_t)nlist, st));
     if (npairs > 0)
         hipLaunchKernelGGL(ivf_count, dim3((unsigned)ceil_div(npairs, 256)), dim3(256), 0, st, probes, npairs, list_len,
                            nlist, cnt);
-    hipLaunchKernelGGL(ivf_plan, dim3(1), dim3(1024), 0, st, cnt, list_len, nlist, bucket_off, item_off, cursor);
+    hipLaunchKernelGGL(ivf_plan, dim3(1), dim3(1024), 0, st, cnt, list_len, nlist, group, bucket_off, item_off,
+                       cursor);
     hipLaunchKernelGGL(ivf_slot_scan, dim3(1), dim3(1024), 0, st, probes, npairs, list_len, nlist, slot_off);
     if (npairs > 0)
         hipLaunchKernelGGL(ivf_fill, dim3((unsigned)ceil_div(npairs, 256)), dim3(256), 0, st, probes, npairs, list_len,
@@ -630,10 +671,12 @@ void launch_ivf_plan(const int64_t *probes, int64_t nq, int nprobe, const int *l
 
 // Upper bound on work items given the largest list's chunk count.
 // Σ_l ceil(cnt_l/G)·nch_l ≤ Σ_l (cnt_l/G + 1)·nch_l ≤ ceil(npairs/G)·max_nch + Σ_l nch_l.
-int64_t ivf_max_items(int64_t nq, int nprobe, int nlist, int max_nch, int64_t nrows) {
+int64_t ivf_max_items(int64_t nq, int nprobe, int nlist, int max_nch, int64_t nrows, int group) {
     const int64_t npairs = nq * nprobe;
-    return ceil_div(npairs, IVF_G) * std::max(max_nch, 1) + ceil_div(nrows, IVF_CH) + nlist;
+    return ceil_div(npairs, (int64_t)group) * std::max(max_nch, 1) + ceil_div(nrows, IVF_CH) + nlist;
 }
+
+int ivf_group_size(int form) { return form == kFormDecomposed ? DT_G : IVF_G; }
 
 int ivf_chunk_rows() { return IVF_CH; }
 

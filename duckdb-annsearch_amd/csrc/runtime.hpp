@@ -214,9 +214,11 @@ void launch_merge_raw(const float *pd, const int *pi, int nparts, int64_t nq, in
                       hipStream_t st);
 void launch_flat_scan_topk(const float *Q, int nq, const float *X, int64_t N, int d, int metric, int k, int nwaves,
                            int64_t rows_per_wave, float *pd, int *pi, hipStream_t st);
-void launch_ivf_plan(const int64_t *probes, int64_t nq, int nprobe, const int *list_len, int nlist, int *cnt,
-                     int *bucket_off, int *item_off, int *cursor, int *bucket, int *slot_off, hipStream_t st);
-int64_t ivf_max_items(int64_t nq, int nprobe, int nlist, int max_nch, int64_t nrows);
+void launch_ivf_plan(const int64_t *probes, int64_t nq, int nprobe, const int *list_len, int nlist, int group,
+                     int *cnt, int *bucket_off, int *item_off, int *cursor, int *bucket, int *slot_off,
+                     hipStream_t st);
+int64_t ivf_max_items(int64_t nq, int nprobe, int nlist, int max_nch, int64_t nrows, int group);
+int ivf_group_size(int form);  // queries per work item of the form's scan kernel
 int ivf_chunk_rows();
 size_t ivf_scan_smem_bytes();
 bool ivf_dot_supported(const float *Q, int d, const float *codes);

@@ -135,6 +135,14 @@ def scan_pairs(index, probes: np.ndarray) -> int:
     return int(sizes[p].sum())
 
 
+def scan_group_rows(index, probes: np.ndarray, group: int = 32) -> int:
+    """Rows the scan kernel streams per batch: every list once per group of ≤ `group` of its probing
+    queries, Σ_l ⌈c_l / group⌉·|l| (≥ the distinct-list rows when a list is probed by > group queries)."""
+    sizes = np.diff(index._offsets)
+    c = np.bincount(probes[probes >= 0].ravel(), minlength=len(sizes))
+    return int((-(-c // group) * sizes).sum())
+
+
 def flat_ground_truth(torch, hipann, d: int, metric: int, xq, k: int, n_total: int, rank: int, world: int,
                       ivf_info_tensor=None):
     """Exact top-k over the whole (sharded) database with the Flat kernels; labels mapped through the
