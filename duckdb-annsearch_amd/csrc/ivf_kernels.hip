@@ -363,10 +363,10 @@ ivf_scan_topk(const float *__restrict__ Q, int d, const float *__restrict__ code
 // SOURCE address — the DMA destination is lane-linear) so that the per-lane ds_read_b128 of 16
 // consecutive rows hits 16 distinct bank groups; then each wave's query block [16 queries][8 float4].
 // Per chunk a wave issues DT_XPW = 8 x pieces (8 rows × one line each) + 1 or 2 query pieces.
-constexpr int DT_WAVES = 4;
+constexpr int DT_WAVES = 8;
 constexpr int DT_THREADS = 64 * DT_WAVES;
 constexpr int DT_R = 4;
-constexpr int DT_NW = 16;
+constexpr int DT_NW = 8;
 constexpr int DT_G = DT_WAVES * DT_NW;
 constexpr int DT_QB = 8;                            // queries per register block
 constexpr int DT_TR = 64 * DT_R;
@@ -380,7 +380,7 @@ constexpr int DT_QF4 = DT_NW * DT_F4;               // float4 of queries per wav
 constexpr int DT_STAGE_F4 = DT_XF4 + DT_WAVES * DT_QF4;
 constexpr int DT_STAGES = 2;
 static_assert(IVF_CH % DT_TR == 0, "row chunks are whole tiles");
-static_assert(DT_XPW * 64 * DT_WAVES == DT_XF4 && DT_QF4 == 128, "piece split");
+static_assert(DT_XPW * 64 * DT_WAVES == DT_XF4 && DT_QF4 % 64 == 0 && DT_QF4 <= 128, "piece split");
 static_assert((DT_F4 & (DT_F4 - 1)) == 0 && DT_F4 <= 16 && (DT_TR / DT_WAVES) % (DT_SWZ * DT_F4) == 0,
               "swizzle: a wave's rows start on a swizzle period");
 static_assert(DT_STAGES * DT_STAGE_F4 * 16 * 2 <= 160 * 1024, "two blocks per CU");
@@ -550,8 +550,27 @@ __device__ __forceinline__ void ivf_dot_item(int d, const float *__restrict__ co
     }
 }
 
+// nwq (wave-uniform) → ivf_dot_item<nwq>
+template <int N, bool IP>
+__device__ __forceinline__ void ivf_dot_dispatch(int nwq, int d, const float *codes, const float *xn, int64_t r0,
+                                                 int64_t r1, const float *qsrc0, const float *qsrc1, const float *qn,
+                                                 int wq0, const int *bucket, int boff, int nprobe, const int *slot_off,
+                                                 int chunk, int k, float *ring, float *part_d, int *part_i) {
+    if constexpr (N >= DT_NW) {
+        ivf_dot_item<DT_NW, IP>(d, codes, xn, r0, r1, qsrc0, qsrc1, qn, wq0, bucket, boff, nprobe, slot_off, chunk, k,
+                                ring, part_d, part_i);
+    } else {
+        if (nwq == N)
+            ivf_dot_item<N, IP>(d, codes, xn, r0, r1, qsrc0, qsrc1, qn, wq0, bucket, boff, nprobe, slot_off, chunk, k,
+                                ring, part_d, part_i);
+        else
+            ivf_dot_dispatch<N + 1, IP>(nwq, d, codes, xn, r0, r1, qsrc0, qsrc1, qn, wq0, bucket, boff, nprobe,
+                                        slot_off, chunk, k, ring, part_d, part_i);
+    }
+}
+
 template <bool IP>
-__global__ void __launch_bounds__(DT_THREADS, 2 * DT_THREADS / 256)
+__global__ void __launch_bounds__(DT_THREADS, 2 * DT_THREADS / 256)  // 2 blocks per CU
 ivf_scan_dot(const float *__restrict__ Q, const float *__restrict__ qn, int d, const float *__restrict__ codes,
              const float *__restrict__ xn, const int64_t *__restrict__ list_off, const int *__restrict__ cnt,
              const int *__restrict__ bucket_off, const int *__restrict__ item_off, const int *__restrict__ bucket,
@@ -586,29 +605,8 @@ ivf_scan_dot(const float *__restrict__ Q, const float *__restrict__ qn, int d, c
     const int s0 = lane / DT_F4, s1 = (64 + lane) / DT_F4;
     const float *qsrc0 = Q + (int64_t)(bucket[boff + wq0 + (s0 < nwq ? s0 : 0)] / nprobe) * d;
     const float *qsrc1 = Q + (int64_t)(bucket[boff + wq0 + (s1 < nwq ? s1 : 0)] / nprobe) * d;
-#define HIPANN_DOT_ITEM(NW)                                                                                         \
-    ivf_dot_item<NW, IP>(d, codes, xn, r0, r1, qsrc0, qsrc1, qn, wq0, bucket, boff, nprobe, slot_off, chunk, k, ring, \
-                         part_d, part_i)
-    switch (nwq) {
-        case 0: HIPANN_DOT_ITEM(0); break;
-        case 1: HIPANN_DOT_ITEM(1); break;
-        case 2: HIPANN_DOT_ITEM(2); break;
-        case 3: HIPANN_DOT_ITEM(3); break;
-        case 4: HIPANN_DOT_ITEM(4); break;
-        case 5: HIPANN_DOT_ITEM(5); break;
-        case 6: HIPANN_DOT_ITEM(6); break;
-        case 7: HIPANN_DOT_ITEM(7); break;
-        case 8: HIPANN_DOT_ITEM(8); break;
-        case 9: HIPANN_DOT_ITEM(9); break;
-        case 10: HIPANN_DOT_ITEM(10); break;
-        case 11: HIPANN_DOT_ITEM(11); break;
-        case 12: HIPANN_DOT_ITEM(12); break;
-        case 13: HIPANN_DOT_ITEM(13); break;
-        case 14: HIPANN_DOT_ITEM(14); break;
-        case 15: HIPANN_DOT_ITEM(15); break;
-        default: HIPANN_DOT_ITEM(16); break;
-    }
-#undef HIPANN_DOT_ITEM
+ivf_dot_dispatch<0, IP>(nwq, d, codes, xn, r0, r1, qsrc0, qsrc1, qn, wq0, bucket, boff, nprobe, slot_off, chunk, k,
+                           ring, part_d, part_i);
 }
 
 // Merge each query's partial lists (its contiguous slot range), mapping shard-local rows to labels.
