@@ -19,6 +19,8 @@
 #include "common.hpp"
 #include "wave_topk.hpp"
 
+#include <utility>
+
 namespace hipann {
 
 constexpr int IVF_WAVES = 8;            // waves per work item (block)
@@ -363,27 +365,51 @@ ivf_scan_topk(const float *__restrict__ Q, int d, const float *__restrict__ code
 // SOURCE address — the DMA destination is lane-linear) so that the per-lane ds_read_b128 of 16
 // consecutive rows hits 16 distinct bank groups; then each wave's query block [16 queries][8 float4].
 // Per chunk a wave issues DT_XPW = 8 x pieces (8 rows × one line each) + 1 or 2 query pieces.
-constexpr int DT_WAVES = 8;
+#ifndef HIPANN_DT_WAVES
+#define HIPANN_DT_WAVES 8
+#endif
+#ifndef HIPANN_DT_NW
+#define HIPANN_DT_NW 8
+#endif
+#ifndef HIPANN_DT_BK
+#define HIPANN_DT_BK 32
+#endif
+#ifndef HIPANN_DT_BLOCKS
+#define HIPANN_DT_BLOCKS 2
+#endif
+constexpr int DT_WAVES = HIPANN_DT_WAVES;
 constexpr int DT_THREADS = 64 * DT_WAVES;
+constexpr int DT_BLOCKS = HIPANN_DT_BLOCKS;         // resident blocks per CU (LDS and VGPR budget)
 constexpr int DT_R = 4;
-constexpr int DT_NW = 8;
+constexpr int DT_NW = HIPANN_DT_NW;
 constexpr int DT_G = DT_WAVES * DT_NW;
-constexpr int DT_QB = 8;                            // queries per register block
+#ifndef HIPANN_DT_QB
+#define HIPANN_DT_QB 4
+#endif
+#ifndef HIPANN_DT_PF
+#define HIPANN_DT_PF 0
+#endif
+constexpr int DT_QB = HIPANN_DT_QB;                 // queries per register block (q float4 live at once)
+constexpr bool DT_PF = HIPANN_DT_PF;
+#ifndef HIPANN_DT_EXPERIMENT
+#define HIPANN_DT_EXPERIMENT 0  // tuning builds only: 1 = skip the FMAs, 2 = skip the row DMA (wrong results)
+#endif                // L2 prefetch of the chunk after the one being DMA'd
 constexpr int DT_TR = 64 * DT_R;
-constexpr int DT_BK = 32;
+constexpr int DT_BK = HIPANN_DT_BK;
 constexpr int DT_F4 = DT_BK / 4;                    // float4 per row per chunk
 constexpr int DT_RP = 64 / DT_F4;                   // rows per x piece
 constexpr int DT_SWZ = 16 / DT_F4;                  // rows sharing one swizzle value
 constexpr int DT_XF4 = DT_TR * DT_F4;               // float4 of rows per stage
 constexpr int DT_XPW = DT_XF4 / 64 / DT_WAVES;      // x pieces per wave per chunk
-constexpr int DT_QF4 = DT_NW * DT_F4;               // float4 of queries per wave per stage
+constexpr int DT_QF4 = (DT_NW * DT_F4 + 63) / 64 * 64;  // float4 of queries per wave per stage (whole pieces)
 constexpr int DT_STAGE_F4 = DT_XF4 + DT_WAVES * DT_QF4;
 constexpr int DT_STAGES = 2;
+constexpr bool DT_DPP = false;  // q via DPP row_newbcast: measured 7% slower than LDS broadcast reads
 static_assert(IVF_CH % DT_TR == 0, "row chunks are whole tiles");
 static_assert(DT_XPW * 64 * DT_WAVES == DT_XF4 && DT_QF4 % 64 == 0 && DT_QF4 <= 128, "piece split");
 static_assert((DT_F4 & (DT_F4 - 1)) == 0 && DT_F4 <= 16 && (DT_TR / DT_WAVES) % (DT_SWZ * DT_F4) == 0,
               "swizzle: a wave's rows start on a swizzle period");
-static_assert(DT_STAGES * DT_STAGE_F4 * 16 * 2 <= 160 * 1024, "two blocks per CU");
+static_assert(DT_STAGES * DT_STAGE_F4 * 16 * DT_BLOCKS <= 160 * 1024, "DT_BLOCKS blocks per CU");
 
 typedef __attribute__((address_space(3))) void *ivf_lds_ptr;
 typedef __attribute__((address_space(1))) void *ivf_gbl_ptr;
@@ -396,11 +422,37 @@ __device__ __forceinline__ void ivf_glds16(const float *src, float *lds_wave_bas
 // every wave's pieces of the chunk to be read have landed and every wave has finished reading the
 // stage the next issue overwrites.  "memory" pins LDS accesses around it.
 template <int N>
-__device__ __forceinline__ void ivf_dt_wait_barrier() {
-    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+__device__ __forceinline__ void ivf_dt_wait_barrier(float &pf, float (&xnv)[DT_R]) {
+    static_assert(DT_R == 4, "operand list");
+    asm volatile("s_waitcnt vmcnt(%5)\n\ts_barrier"
+                 : "+v"(pf), "+v"(xnv[0]), "+v"(xnv[1]), "+v"(xnv[2]), "+v"(xnv[3])
+                 : "n"(N)
+                 : "memory");
+}
+
+// L2 prefetch: a dword load per 128-B line of the chunk after the one being DMA'd, into the sink
+// register pf.  pf is read and written by every prefetch and by every wait, so it stays one live
+// register for the whole loop (never reused while a prefetch into it is in flight); nothing reads
+// its value.  The wait leaves the newest prefetch outstanding (vmcnt(1)).
+__device__ __forceinline__ void ivf_prefetch_line(float &pf, const float *p) {
+    asm volatile("global_load_dword %0, %1, off" : "+v"(pf) : "v"(p) : "memory");
+}
+
+// ‖x‖² of the lane's 4 rows of the tile being started, loaded behind the compiler's back (a plain
+// load would make it wait vmcnt(0) — draining the DMA ring — at the first use): issued right after
+// a barrier, ahead of that chunk's DMA and prefetch, so the next barrier's vmcnt(1) retires it long
+// before the tile's epilogue reads it.  Rows past the chunk read any valid element (never offered).
+__device__ __forceinline__ void ivf_load_norms(float (&xnv)[DT_R], const float *xn, int64_t t0, int64_t r1,
+                                               int lane) {
+#pragma unroll
+    for (int r = 0; r < DT_R; ++r) {
+        const int64_t row = t0 + lane + 64 * r < r1 ? t0 + lane + 64 * r : r1 - 1;
+        asm volatile("global_load_dword %0, %1, off" : "=v"(xnv[r]) : "v"(xn + row) : "memory");
+    }
 }
 
 // acc[r][J0 + j] += q_j · x_r over one float4 of dims, for the NB queries J0 .. J0 + NB − 1
+// (q broadcast from LDS: one ds_read_b128 per query).
 template <int NB, int J0, int NA>
 __device__ __forceinline__ void ivf_dot_block(const float *__restrict__ Qw, int u, const float4 (&xv)[DT_R],
                                               float (&acc)[DT_R][NA]) {
@@ -425,6 +477,64 @@ __device__ __forceinline__ void ivf_dot_block(const float *__restrict__ Qw, int 
         for (int r = 0; r < DT_R; ++r) acc[r][J0 + j] = fmaf(qv[j].w, xv[r].w, acc[r][J0 + j]);
 }
 
+// acc += bcast16(q, lane N of each 16-lane row) · x — v_fmac_f32 with a DPP row_newbcast source.
+// The backend does not fold v_mov_b32_dpp into v_fma_f32 (VOP3), so the VOP2 form is spelled out.
+// q comes straight from a ds_read (no VALU write in front of the DPP read: no wait states needed).
+template <int N>
+__device__ __forceinline__ void ivf_fmac_bcast(float &acc, float q, float x) {
+    asm("v_fmac_f32_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(q), "v"(x), "n"(N));
+}
+
+template <int C>
+__device__ __forceinline__ float ivf_comp(const float4 &v) {
+    if constexpr (C == 0) return v.x;
+    else if constexpr (C == 1) return v.y;
+    else if constexpr (C == 2) return v.z;
+    else return v.w;
+}
+
+// component C of one 4-dim step for queries J0 + Js (compile-time j for the DPP lane select)
+template <int C, int J0, int NA, int NH, int... Js>
+__device__ __forceinline__ void ivf_dpp_comp(std::integer_sequence<int, Js...>, const float (&V)[NH],
+                                             const float4 (&xv)[DT_R], float (&acc)[DT_R][NA]) {
+    (
+        [&] {
+#pragma unroll
+            for (int r = 0; r < DT_R; ++r)
+                ivf_fmac_bcast<4 * (Js & 3) + C>(acc[r][J0 + Js], V[Js >> 2], ivf_comp<C>(xv[r]));
+        }(),
+        ...);
+}
+
+// Same contract as ivf_dot_block, q values via DPP: lane m of each 16-lane row of V[h] holds
+// q_{J0 + 4h + m/4}[4u + m%4], so a 4-dim step costs ⌈NB/4⌉ ds_read_b32 instead of NB ds_read_b128.
+template <int NB, int J0, int NA>
+__device__ __forceinline__ void ivf_dot_block_dpp(const float *__restrict__ Qw, int u, int lane,
+                                                  const float4 (&xv)[DT_R], float (&acc)[DT_R][NA]) {
+    constexpr int NH = (NB + 3) / 4;
+    float V[NH];
+    const int m = lane & 15;
+#pragma unroll
+    for (int h = 0; h < NH; ++h) V[h] = Qw[(J0 + 4 * h + (m >> 2)) * DT_BK + 4 * u + (m & 3)];
+    using Seq = std::make_integer_sequence<int, NB>;
+    ivf_dpp_comp<0, J0, NA, NH>(Seq{}, V, xv, acc);
+    ivf_dpp_comp<1, J0, NA, NH>(Seq{}, V, xv, acc);
+    ivf_dpp_comp<2, J0, NA, NH>(Seq{}, V, xv, acc);
+    ivf_dpp_comp<3, J0, NA, NH>(Seq{}, V, xv, acc);
+}
+
+// all NW queries of the wave, in register blocks of ≤ DT_QB
+template <int NW, int J0, int NA>
+__device__ __forceinline__ void ivf_dot_blocks(const float *__restrict__ Qw, int u, int lane, const float4 (&xv)[DT_R],
+                                               float (&acc)[DT_R][NA]) {
+    if constexpr (NW - J0 > 0) {
+        constexpr int NB = NW - J0 < DT_QB ? NW - J0 : DT_QB;
+        if constexpr (DT_DPP) ivf_dot_block_dpp<NB, J0, NA>(Qw, u, lane, xv, acc);
+        else ivf_dot_block<NB, J0, NA>(Qw, u, xv, acc);
+        ivf_dot_blocks<NW, J0 + NB, NA>(Qw, u, lane, xv, acc);
+    }
+}
+
 template <int NW, bool IP>
 __device__ __forceinline__ void ivf_dot_item(int d, const float *__restrict__ codes, const float *__restrict__ xn,
                                              int64_t r0, int64_t r1, const float *qsrc0, const float *qsrc1,
@@ -432,7 +542,7 @@ __device__ __forceinline__ void ivf_dot_item(int d, const float *__restrict__ co
                                              int nprobe, const int *__restrict__ slot_off, int chunk, int k,
                                              float *ring, float *__restrict__ part_d, int *__restrict__ part_i) {
     constexpr int NA = NW > 0 ? NW : 1;
-    constexpr int QP = NW > DT_QB ? 2 : 1;       // query pieces per chunk
+    constexpr int QP = NW * DT_F4 > 64 ? 2 : 1;  // query pieces per chunk
     constexpr int PIECES = DT_XPW + QP;          // DMA instructions per wave per chunk
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int nk = (d + DT_BK - 1) / DT_BK;
@@ -442,27 +552,28 @@ __device__ __forceinline__ void ivf_dot_item(int d, const float *__restrict__ co
     // ---- issue side: x piece i of wave w = rows w·(TR/WAVES) + i·RP + lane / F4; the lane's float4
     // slot (lane % F4) of its row holds logical float4 (lane % F4) ^ swz(row) ----
     const int prow = wave * (DT_TR / DT_WAVES) + lane / DT_F4;
-    int xc4[DT_XPW];
-#pragma unroll
-    for (int i = 0; i < DT_XPW; ++i)
-        xc4[i] = 4 * ((lane % DT_F4) ^ (((i * DT_RP + lane / DT_F4) / DT_SWZ) & (DT_F4 - 1)));
+    // (recomputed per issue: registers are the scarce resource here)
+    auto xc4 = [&](int i) { return 4 * ((lane % DT_F4) ^ (((i * DT_RP + lane / DT_F4) / DT_SWZ) & (DT_F4 - 1))); };
     const int qc4 = 4 * (lane % DT_F4);
     int it_kc = 0, it_buf = 0;
     int64_t it_t0 = r0;
+    float pf = 0.f, xnv[DT_R] = {0.f, 0.f, 0.f, 0.f};
+    static_assert(!DT_PF || (DT_STAGES == 2 && DT_TR / DT_WAVES == 32), "one prefetch dword per wave lane pair per chunk");
     auto issue = [&]() {
         float *stage = ring + (size_t)it_buf * DT_STAGE_F4 * 4;
         const int k0 = it_kc * DT_BK;
         const bool full_k = k0 + DT_BK <= d;
-        if (it_t0 + DT_TR <= r1 && full_k) {  // interior tile, whole chunk: no clamps
+        if (HIPANN_DT_EXPERIMENT == 2) {
+        } else if (it_t0 + DT_TR <= r1 && full_k) {  // interior tile, whole chunk: no clamps
             const float *base = codes + (it_t0 + prow) * (int64_t)d + k0;
 #pragma unroll
             for (int i = 0; i < DT_XPW; ++i)
-                ivf_glds16(base + (int64_t)(DT_RP * i) * d + xc4[i], stage + (size_t)(wave * DT_XPW + i) * 64 * 4);
+                ivf_glds16(base + (int64_t)(DT_RP * i) * d + xc4(i), stage + (size_t)(wave * DT_XPW + i) * 64 * 4);
         } else {  // rows past the chunk re-load its last row, dims past d any valid float4 (never read)
 #pragma unroll
             for (int i = 0; i < DT_XPW; ++i) {
                 const int64_t row = it_t0 + prow + DT_RP * i < r1 ? it_t0 + prow + DT_RP * i : r1 - 1;
-                const int kk = k0 + xc4[i] < d ? k0 + xc4[i] : d - 4;
+                const int kk = k0 + xc4(i) < d ? k0 + xc4(i) : d - 4;
                 ivf_glds16(codes + row * (int64_t)d + kk, stage + (size_t)(wave * DT_XPW + i) * 64 * 4);
             }
         }
@@ -472,6 +583,12 @@ __device__ __forceinline__ void ivf_dot_item(int d, const float *__restrict__ co
         if (QP == 2) ivf_glds16(qsrc1 + kq, qdst + 64 * 4);
         if (++it_kc == nk) { it_kc = 0; it_t0 += DT_TR; }
         it_buf = it_buf == DT_STAGES - 1 ? 0 : it_buf + 1;
+        // warm L2 with the next chunk's lines: rows wave·(TR/WAVES) + (lane % 32), one dword per line
+        if constexpr (DT_PF) {
+            const int64_t prow_pf = it_t0 + wave * (DT_TR / DT_WAVES) + (lane & 31);
+            const int64_t row = prow_pf < r1 ? prow_pf : r1 - 1;
+            ivf_prefetch_line(pf, codes + row * (int64_t)d + it_kc * DT_BK);
+        }
     };
 
     // ---- compute side ----
@@ -493,11 +610,10 @@ __device__ __forceinline__ void ivf_dot_item(int d, const float *__restrict__ co
     int kc = 0, buf = 0;
     int64_t t0 = r0;
     for (int c = 0; c < total; ++c) {
-        // chunks c+1 .. c+STAGES-2 may stay in flight
-        const int ahead = total - 1 - c;
-        if (ahead >= DT_STAGES - 2) ivf_dt_wait_barrier<(DT_STAGES - 2) * PIECES>();
-        else if (ahead == 1) ivf_dt_wait_barrier<PIECES>();
-        else ivf_dt_wait_barrier<0>();
+        // chunk c's pieces (and any norms issued before them) landed; the prefetch issued after
+        // them may stay in flight
+        ivf_dt_wait_barrier<DT_PF ? 1 : 0>(pf, xnv);
+        if (!IP && NW > 0 && kc == 0) ivf_load_norms(xnv, xn, t0, r1, lane);
         if (c + DT_STAGES - 1 < total) issue();
         const float *X = ring + (size_t)buf * DT_STAGE_F4 * 4;
         const float *Qw = X + (size_t)(DT_XF4 + wave * DT_QF4) * 4;
@@ -510,17 +626,20 @@ __device__ __forceinline__ void ivf_dot_item(int d, const float *__restrict__ co
                 const float *xl = X + (lane * DT_F4 + (u ^ swz)) * 4;
 #pragma unroll
                 for (int r = 0; r < DT_R; ++r) xv[r] = *reinterpret_cast<const float4 *>(xl + r * 64 * DT_F4 * 4);
-                if constexpr (NW > 0) ivf_dot_block<(NW < DT_QB ? NW : DT_QB), 0, NA>(Qw, u, xv, acc);
-                if constexpr (NW > DT_QB) ivf_dot_block<NW - DT_QB, DT_QB, NA>(Qw, u, xv, acc);
+                if (HIPANN_DT_EXPERIMENT != 1) ivf_dot_blocks<NW, 0, NA>(Qw, u, lane, xv, acc);
+                else acc[0][0] += xv[0].x + xv[1].y + xv[2].z + xv[3].w;
             }
         }
         if (++kc == nk) {  // tile done: offer its rows
             if (NW > 0) {
+                if (nk == 1)  // the norms were issued in this very chunk: no barrier has retired them yet
+                    asm volatile("s_waitcnt vmcnt(0)"
+                                 : "+v"(pf), "+v"(xnv[0]), "+v"(xnv[1]), "+v"(xnv[2]), "+v"(xnv[3])::"memory");
 #pragma unroll
                 for (int r = 0; r < DT_R; ++r) {
                     const int64_t row = t0 + lane + 64 * r;
                     const bool v = row < r1;
-                    const float xnr = (!IP && v) ? xn[row] : 0.f;
+                    const float xnr = xnv[r];
 #pragma unroll
                     for (int j = 0; j < NW; ++j) {
                         float key;
@@ -542,6 +661,7 @@ __device__ __forceinline__ void ivf_dot_item(int d, const float *__restrict__ co
         }
         buf = buf == DT_STAGES - 1 ? 0 : buf + 1;
     }
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(pf)::"memory");  // retire the last prefetch before pf dies
 #pragma unroll
     for (int j = 0; j < NW; ++j) {
         const int pr = bucket[boff + wq0 + j];
@@ -570,7 +690,7 @@ __device__ __forceinline__ void ivf_dot_dispatch(int nwq, int d, const float *co
 }
 
 template <bool IP>
-__global__ void __launch_bounds__(DT_THREADS, 2 * DT_THREADS / 256)  // 2 blocks per CU
+__global__ void __launch_bounds__(DT_THREADS, DT_BLOCKS * DT_THREADS / 256)
 ivf_scan_dot(const float *__restrict__ Q, const float *__restrict__ qn, int d, const float *__restrict__ codes,
              const float *__restrict__ xn, const int64_t *__restrict__ list_off, const int *__restrict__ cnt,
              const int *__restrict__ bucket_off, const int *__restrict__ item_off, const int *__restrict__ bucket,

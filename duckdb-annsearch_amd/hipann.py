@@ -27,7 +27,7 @@ from typing import Optional, Sequence, Tuple
 import numpy as np
 
 HERE = Path(__file__).resolve().parent
-LIB_PATH = HERE / "libhipann.so"
+LIB_PATH = Path(os.environ["HIPANN_LIB"]) if os.environ.get("HIPANN_LIB") else HERE / "libhipann.so"  # override: tuning builds
 
 METRIC_L2 = 0
 METRIC_INNER_PRODUCT = 1
