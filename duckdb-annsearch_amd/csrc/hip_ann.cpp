@@ -224,8 +224,10 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
     }
     const int64_t nqt = ceil_div(nq, 128);
     const int64_t ntiles = ceil_div(sh.n, 128);
+    // ≈2048 blocks; small tables (an IVF coarse quantizer: 1024 centroids = 8 tiles) go down to one
+    // column tile per block rather than leaving CUs idle
     int64_t nsplit = std::max<int64_t>(1, ceil_div(2048, nqt));
-    nsplit = std::min<int64_t>(nsplit, std::max<int64_t>(1, ntiles / 4));
+    nsplit = std::min<int64_t>(nsplit, ntiles);
     if (nsplit >= 8) nsplit = nsplit / 8 * 8;
     const int64_t tps = ceil_div(ntiles, nsplit);
     nsplit = ceil_div(ntiles, tps);
