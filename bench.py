@@ -270,13 +270,24 @@ def main():
                 "algorithmic": f"2*nq*N_local*d = {flops:.4g} FLOP per launch"}
     else:
         b_alg = extra.get("scan_bytes_per_batch_local", 0.0)
+        dot = index.form == hipann.HipIndexIVFFlat.FORM_DECOMPOSED
+        kname = "ivf_scan_dot" if dot else "ivf_scan_topk"
+        fpp = 2.0 if dot else 3.0  # VALU flop per (query, row, dim): fma vs sub + fma
         achieved = b_alg / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "ivf_scan_topk",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kname,
                 "kernel_ms": round(kern_ms, 3), "merge_ms": round(merge_ms, 3),
                 "algorithmic": "sum over distinct probed lists |l|*(4d+8) B per launch",
-                "valu_tflops": round(3.0 * d * extra.get("scanned_pairs_per_batch_local", 0) / (kern_ms * 1e-3) / 1e12, 2)
+                "form": "decomposed" if dot else "direct",
+                "valu_tflops": round(fpp * d * extra.get("scanned_pairs_per_batch_local", 0) / (kern_ms * 1e-3) / 1e12, 2)
                 if kern_ms > 0 else None}
+
+    tb, tsrc = pmc_traffic(args.workload, roof["kernel"])
+    if tb is not None and world == 1:
+        roof["traffic"] = round(tb / 1e9, 3)
+        roof["traffic_unit"] = "GB per launch (PMC FETCH_SIZE x1024 x2, gfx950 correction)"
+        roof["traffic_source"] = tsrc
+        roof["algorithmic_per_launch"] = round((b_alg if args.workload == "ivf" else 4.0 * n_local * d) / 1e9, 3)
 
     # ---------------- CPU baseline (rank 0, N=1 only) ----------------
     cpu = None
@@ -313,6 +324,20 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(workload: str, kernel: str):
+    """HBM bytes per launch of `kernel` from the newest committed FETCH_SIZE pass
+    (profiles/rNN/pmc_<workload>.json, written by tools/pmc_traffic.py from a separate
+    `rocprofv3 --pmc FETCH_SIZE` run of this same command), or None."""
+    for f in sorted((ROOT / "profiles").glob(f"r*/pmc_{workload}.json"), reverse=True):
+        try:
+            js = json.loads(f.read_text())
+        except Exception:
+            continue
+        if js.get("kernel") == kernel:
+            return js.get("hbm_bytes_per_launch"), str(f.relative_to(ROOT))
+    return None, None
 
 
 def cpu_baseline(args, torch, xq, index, extra, n, d, k, metric):

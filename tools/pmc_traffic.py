@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""Per-launch HBM traffic of one kernel from a rocprofv3 ``--pmc FETCH_SIZE`` pass.
+
+MI355X_MICROARCH.md (§HBM, §rocprofv3 PMC slots) prescribes the recipe this follows:
+  * FETCH_SIZE is collected in its own pass (it takes 3 of the 4 TCC slots; no WRITE_SIZE beside it,
+    and no -s/-r/trace domains beside --pmc);
+  * FETCH_SIZE is in KiB (counter_defs.yaml: (...)/1024), so bytes = 1024 · FETCH_SIZE;
+  * on gfx950 FETCH_SIZE reports exactly half the bytes of a wide coalesced streaming read
+    (128-B requests tallied at 64 B), so bytes are doubled before comparing with a byte count.
+
+Usage:
+  python tools/pmc_traffic.py <rocprofv3 -d dir> <kernel-name substring> [--skip N] [--out file.json]
+The dispatches of the kernel (after skipping the first N, e.g. warm-up) are averaged.
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def find_csv(root: str, suffix: str) -> list[str]:
+    return sorted(glob.glob(os.path.join(root, "**", f"*{suffix}"), recursive=True))
+
+
+def traffic(root: str, kernel: str, skip: int = 0) -> dict:
+    files = find_csv(root, "counter_collection.csv")
+    if not files:
+        raise SystemExit(f"no counter_collection.csv under {root}")
+    per_dispatch: dict[tuple, float] = {}
+    for f in files:
+        with open(f, newline="") as fh:
+            for row in csv.DictReader(fh):
+                if kernel not in row.get("Kernel_Name", ""):
+                    continue
+                if row.get("Counter_Name") != "FETCH_SIZE":
+                    continue
+                key = (f, int(row.get("Dispatch_Id", 0)))
+                per_dispatch[key] = per_dispatch.get(key, 0.0) + float(row["Counter_Value"])
+    vals = [v for _, v in sorted(per_dispatch.items(), key=lambda kv: kv[0][1])][skip:]
+    if not vals:
+        raise SystemExit(f"no FETCH_SIZE rows for kernel '{kernel}' in {files}")
+    kib = sum(vals) / len(vals)
+    return {
+        "kernel": kernel,
+        "dispatches": len(vals),
+        "fetch_size_kib_avg": kib,
+        "hbm_bytes_per_launch": 2.0 * 1024.0 * kib,  # KiB → B, ×2 gfx950 correction (MI355X_MICROARCH.md §HBM)
+        "recipe": "rocprofv3 --pmc FETCH_SIZE (own pass); bytes = 2 * 1024 * FETCH_SIZE",
+    }
+
+
+def main() -> None:
+    p = argparse.ArgumentParser()
+    p.add_argument("dir")
+    p.add_argument("kernel")
+    p.add_argument("--skip", type=int, default=0)
+    p.add_argument("--out")
+    a = p.parse_args()
+    res = traffic(a.dir, a.kernel, a.skip)
+    js = json.dumps(res, indent=1)
+    if a.out:
+        with open(a.out, "w") as fh:
+            fh.write(js + "\n")
+    print(js)
+
+
+if __name__ == "__main__":
+    sys.exit(main())
