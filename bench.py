@@ -187,6 +187,7 @@ def main():
             data_desc = f"{n_centres} gaussian centres, sigma={sigma}"
         index, ivf_info = build_ivf_shard(torch, hipann, xb, lo, n, args.nlist, args.nprobe, metric, rank, world,
                                           centres_seed=1234)
+        index.form = int(os.environ.get("HIPANN_IVF_FORM", "0"))  # A/B: 1 direct, 2 decomposed on VALU
         del xb  # lists hold a list-ordered copy
         torch.cuda.empty_cache()
         search = index.search_device
@@ -270,16 +271,17 @@ def main():
                 "algorithmic": f"2*nq*N_local*d = {flops:.4g} FLOP per launch"}
     else:
         b_alg = extra.get("scan_bytes_per_batch_local", 0.0)
-        dot = index.form == hipann.HipIndexIVFFlat.FORM_DECOMPOSED
-        kname = "ivf_scan_dot" if dot else "ivf_scan_topk"
-        fpp = 2.0 if dot else 3.0  # VALU flop per (query, row, dim): fma vs sub + fma
+        form = index.form
+        kname, fname = {0: ("ivf_scan_mfma", "decomposed, fp32 MFMA"), 1: ("ivf_scan_topk", "direct, VALU"),
+                        2: ("ivf_scan_dot", "decomposed, VALU")}[form]
+        fpp = 3.0 if form == 1 else 2.0  # flop per (query, row, dim): sub + fma vs fma
         achieved = b_alg / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kname,
                 "kernel_ms": round(kern_ms, 3), "merge_ms": round(merge_ms, 3),
                 "algorithmic": "sum over distinct probed lists |l|*(4d+8) B per launch",
-                "form": "decomposed" if dot else "direct",
-                "valu_tflops": round(fpp * d * extra.get("scanned_pairs_per_batch_local", 0) / (kern_ms * 1e-3) / 1e12, 2)
+                "form": fname,
+                "scan_tflops": round(fpp * d * extra.get("scanned_pairs_per_batch_local", 0) / (kern_ms * 1e-3) / 1e12, 2)
                 if kern_ms > 0 else None}
 
     tb, tsrc = pmc_traffic(args.workload, roof["kernel"])

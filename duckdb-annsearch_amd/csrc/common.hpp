@@ -30,9 +30,10 @@ __host__ __device__ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + 
 
 // Metric codes of the C ABI (hip_ann.h / hip_diskann_bridge.h).
 enum Metric : int { kL2 = 0, kIP = 1 };
-// IVF list-scan distance form (hipann_ivf_set_form): ‖q‖²+‖x‖²−2q·x (FAISS GPU / faiss-metal IVF) or
-// the direct Σ(q−x)² of FAISS's CPU IndexIVFFlat scanner.
-enum IvfForm : int { kFormDecomposed = 0, kFormDirect = 1 };
+// IVF list-scan distance form (hipann_ivf_set_form): ‖q‖²+‖x‖²−2q·x (FAISS GPU / faiss-metal IVF) on the
+// matrix cores, or the direct Σ(q−x)² of FAISS's CPU IndexIVFFlat scanner.
+// kFormDecomposedValu: the same form on the VALU kernel (ivf_scan_dot), kept for A/B measurement.
+enum IvfForm : int { kFormDecomposed = 0, kFormDirect = 1, kFormDecomposedValu = 2 };
 
 // XCD-aware block remap (cdna_hip_programming.md §5.5 T1, bijective form): blocks b and b+8 are
 // dealt to the same XCD; map so that each XCD receives a contiguous run of logical blocks.

@@ -139,8 +139,11 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     HIPANN_REQUIRE((int64_t)nq * np < (int64_t)0x7fffffff, "nq * nprobe too large");
     sh.slot_off.ensure(sizeof(int) * ((size_t)nq * np + 1), sh.device);
     // the decomposed form needs float4 rows; other shapes take the direct kernel (also on the GPU)
-    const int form = ix.form == kFormDecomposed && ivf_dot_supported(xq, d, sh.codes) ? kFormDecomposed : kFormDirect;
-    const int group = ivf_group_size(form);
+    // the decomposed forms need float4 rows (else the direct kernel, also on the GPU); the MFMA kernel
+    // keeps 16-lane lists (k <= 16) and the item's queries in LDS (else the VALU decomposed kernel)
+    int form = ix.form != kFormDirect && ivf_dot_supported(xq, d, sh.codes) ? ix.form : kFormDirect;
+    if (form == kFormDecomposed && !ivf_mfma_supported(xq, d, sh.codes, k)) form = kFormDecomposedValu;
+    const int group = ivf_group_size(form, d);
     launch_ivf_plan(sh.coarse_i.get<int64_t>(), nq, np, sh.list_len.get<int>(), nlist, group, sh.cnt.get<int>(),
                     sh.bucket_off.get<int>(), sh.item_off.get<int>(), sh.cursor.get<int>(), sh.bucket.get<int>(),
                     sh.slot_off.get<int>(), st);
@@ -151,16 +154,22 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     sh.part_i.ensure(parts * sizeof(int), sh.device);
     const int64_t max_items = ivf_max_items(nq, np, nlist, sh.max_nch, sh.n, group);
     const float *qn = nullptr;
-    if (form == kFormDecomposed && metric == kL2) {
+    if (form != kFormDirect && metric == kL2) {
         sh.qn.ensure(sizeof(float) * (size_t)nq, sh.device);
         launch_row_norms(xq, nq, d, sh.qn.get<float>(), st);
         qn = sh.qn.get<float>();
+    }
+    unsigned *qbound = nullptr;
+    if (form == kFormDecomposed) {  // every query's bound starts at +inf (order-preserving bits 0xff800000)
+        sh.qbound.ensure(sizeof(unsigned) * (size_t)nq, sh.device);
+        qbound = sh.qbound.get<unsigned>();
+        HIPANN_CHECK(hipMemsetD32Async((hipDeviceptr_t)qbound, 0xff800000, (size_t)nq, st));
     }
     {
         ScopedTiming t(ix.timer_main, st);
         launch_ivf_scan(xq, qn, d, metric, form, sh.codes, sh.xnorm.get<float>(), sh.list_off.get<int64_t>(),
                         sh.cnt.get<int>(), sh.bucket_off.get<int>(), sh.item_off.get<int>(), sh.bucket.get<int>(),
-                        sh.slot_off.get<int>(), nlist, np, nq, k, max_items, sh.part_d.get<float>(),
+                        sh.slot_off.get<int>(), nlist, np, nq, k, max_items, qbound, sh.part_d.get<float>(),
                         sh.part_i.get<int>(), st);
     }
     // 4. merge each query's partial lists
@@ -427,7 +436,7 @@ int hipann_ivf_set_nprobe(void *h, int nprobe) {
 }
 
 int hipann_ivf_set_form(void *h, int form) {
-    if (!h || (form != kFormDecomposed && form != kFormDirect)) return -1;
+    if (!h || (form != kFormDecomposed && form != kFormDirect && form != kFormDecomposedValu)) return -1;
     auto *ix = static_cast<IndexBase *>(h);
     if (ix->kind != Kind::IVF) return -1;
     auto *vx = static_cast<IvfIndex *>(ix);

@@ -794,7 +794,15 @@ int64_t ivf_max_items(int64_t nq, int nprobe, int nlist, int max_nch, int64_t nr
     return ceil_div(npairs, (int64_t)group) * std::max(max_nch, 1) + ceil_div(nrows, IVF_CH) + nlist;
 }
 
-int ivf_group_size(int form) { return form == kFormDecomposed ? DT_G : IVF_G; }
+int ivf_mfma_group(int d);  // ivf_mfma.hip
+void launch_ivf_scan_mfma(const float *Q, const float *qn, int d, int metric, const float *codes, const float *xn,
+                          const int64_t *list_off, const int *cnt, const int *bucket_off, const int *item_off,
+                          const int *bucket, const int *slot_off, int nlist, int nprobe, int k, int64_t max_items,
+                          unsigned *qbound, float *pd, int *pi, hipStream_t st);
+
+int ivf_group_size(int form, int d) {
+    return form == kFormDecomposed ? ivf_mfma_group(d) : form == kFormDecomposedValu ? DT_G : IVF_G;
+}
 
 int ivf_chunk_rows() { return IVF_CH; }
 
@@ -808,10 +816,15 @@ bool ivf_dot_supported(const float *Q, int d, const float *codes) {
 void launch_ivf_scan(const float *Q, const float *qn, int d, int metric, int form, const float *codes,
                      const float *xn, const int64_t *list_off, const int *cnt, const int *bucket_off,
                      const int *item_off, const int *bucket, const int *slot_off, int nlist, int nprobe, int64_t nq,
-                     int k, int64_t max_items, float *pd, int *pi, hipStream_t st) {
+                     int k, int64_t max_items, unsigned *qbound, float *pd, int *pi, hipStream_t st) {
     if (max_items <= 0) return;
     HIPANN_REQUIRE(max_items < (int64_t)0x7fffffff, "too many IVF work items");
     if (form == kFormDecomposed) {
+        launch_ivf_scan_mfma(Q, qn, d, metric, codes, xn, list_off, cnt, bucket_off, item_off, bucket, slot_off, nlist,
+                             nprobe, k, max_items, qbound, pd, pi, st);
+        return;
+    }
+    if (form == kFormDecomposedValu) {
         HIPANN_REQUIRE(ivf_dot_supported(Q, d, codes), "decomposed IVF scan needs d % 4 == 0 and 16-B aligned data");
         HIPANN_REQUIRE(metric == kIP || (qn && xn), "decomposed L2 scan needs query and row norms");
         dim3 grid((unsigned)max_items), block(DT_THREADS);

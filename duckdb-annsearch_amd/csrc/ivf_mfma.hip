@@ -1,0 +1,430 @@
+// ivf_mfma.hip — IVFFlat list scan on the fp32 matrix cores (gfx950), decomposed form.
+//
+// Replaces the per-query GEMV-shaped distance + select of MetalIndexIVFFlat::search
+// (faiss-metal/src/MetalIndexIVFFlat.mm:122-256, norms stored with the lists at :305-318).  Same
+// work plan as the VALU kernels in ivf_kernels.hip (ivf_count / ivf_plan / ivf_fill, slots from
+// ivf_slot_scan): an item is (list ℓ, 2048-row chunk of ℓ, group of ≤ G of the queries probing ℓ),
+// and every (query, probe, chunk) slot receives exactly one k-list.
+//
+// The block computes the item's (queries × rows) block of q·x with v_mfma_f32_16x16x4_f32 (exact
+// fp32 products, fp32 accumulation: a k-ordered fmaf chain, MI355X_MICROARCH.md §Matrix cores) and
+// turns it into  L2: max(0, ‖q‖² + ‖x‖² − 2·q·x)  /  IP: key = −q·x  in registers.
+//
+// Data movement (the list scan streams each probed list once per batch, so HBM is the roofline):
+//   * the item's ≤ G queries are copied once into LDS, all d dims (G = 48 at d = 768: 149 KiB),
+//     row stride ≡ 8 dwords (mod 64) so the A-fragment reads (16 queries × one float4) are
+//     conflict-free;
+//   * rows go straight from HBM into the MFMA B operand: lane (g, m) loads row m's dims
+//     16s + 4g .. +3 of a 16-row tile (global_load_dwordx4), P = 6 sixteen-dim steps ahead in a
+//     register ring — ≈ 12 KiB in flight per wave, 96 KiB per CU, with no LDS round trip and no
+//     barrier in the main loop (cdna_hip_programming.md §5: operand streamed once per block and not
+//     shared across waves → load straight to VGPRs, deep unroll).
+// Block: 8 waves, one block per CU (LDS).  Wave w takes the item's 32-row passes w, w + 8, … and
+// multiplies each pass (2 row tiles) by every query tile (QT ≤ 3): 8·QT MFMAs per 16 dims.
+//
+// Selection: the accumulator of tile (qt, r) holds, in DPP row g (lanes 16g .. 16g + 15), query
+// qt·16 + 4g + v of register v against the tile's 16 rows (lane m = row).  Each wave keeps, per
+// query, a sorted list of the k ≤ 16 best (key, row) in one 16-lane DPP row of a register pair — the
+// same lanes that hold that query's candidates — so one register pair serves 4 queries and a tile
+// merges into the lists with no cross-row traffic: when a 16-row batch has a candidate below a
+// lane's cached k-th, the batch is bitonic-sorted inside the rows and merged (reverse + min + 4
+// half-cleaner stages), four queries at a time, every exchange a DPP operand.  At the end of the item
+// the 8 waves' lists are merged pairwise through LDS (3 rounds) and wave 0 writes the k-lists.
+#include "common.hpp"
+#include "wave_topk.hpp"
+
+#include <algorithm>
+
+namespace hipann {
+
+typedef float mf_f32x4 __attribute__((ext_vector_type(4)));
+
+#ifndef HIPANN_MF_EXPERIMENT
+#define HIPANN_MF_EXPERIMENT 0  // tuning builds only (wrong results): 1 no selection, 2 no row loads, 3 no MFMA
+#endif
+
+constexpr int MF_WAVES = 8;
+constexpr int MF_THREADS = 64 * MF_WAVES;
+constexpr int MF_CH = 2048;   // rows per item (= IVF_CH of ivf_kernels.hip)
+constexpr int MF_PASS = 32;   // rows per wave pass (2 MFMA row tiles)
+constexpr int MF_RT = 2;      // row tiles per pass
+constexpr int MF_P = 6;       // sixteen-dim steps in flight per wave (register ring depth)
+constexpr int MF_QTMAX = 3;   // query tiles per item (G ≤ 48)
+constexpr int MF_KMAX = 16;   // lists are 16-lane DPP rows
+constexpr size_t MF_LDS_MAX = 160 * 1024;
+
+// Dims per query row in LDS (16-dim steps padded to a multiple of the ring depth, zero-filled) and
+// the row stride (≡ 8 dwords mod 64: conflict-free ds_read_b128 of 16 rows × one float4).
+__host__ __device__ inline int mf_nsub(int d) { return (int)ceil_div(ceil_div(d, 16), MF_P) * MF_P; }
+__host__ __device__ inline int mf_stride(int d) { return mf_nsub(d) * 16 + 8; }
+inline int mf_group(int d) {
+    const int g = (int)(MF_LDS_MAX / ((size_t)mf_stride(d) * 4)) / 16 * 16;
+    return g < 16 * MF_QTMAX ? g : 16 * MF_QTMAX;
+}
+
+// ---- 16-lane (DPP row) sorted lists ---------------------------------------------------------
+// Every exchange partner of the networks below is lane m ^ X inside a 16-lane row, X ∈ {1,2,3,4,7,
+// 8,15}: a DPP operand modifier (quad_perm / row_half_mirror / row_mirror / row_ror:8), so a stage
+// costs a few VALU ops instead of an LDS-pipe shuffle round trip (ds_bpermute / ds_swizzle latency
+// chained through 15 stages made the first version of this epilogue latency-bound).
+template <int CTRL>
+__device__ __forceinline__ int mf_dpp(int x) {
+    return __builtin_amdgcn_update_dpp(x, x, CTRL, 0xF, 0xF, false);
+}
+template <int X>
+__device__ __forceinline__ int row_xor(int x) {
+    if constexpr (X == 1) return mf_dpp<0xB1>(x);              // quad_perm [1,0,3,2]
+    else if constexpr (X == 2) return mf_dpp<0x4E>(x);         // quad_perm [2,3,0,1]
+    else if constexpr (X == 3) return mf_dpp<0x1B>(x);         // quad_perm [3,2,1,0]
+    else if constexpr (X == 7) return mf_dpp<0x141>(x);        // row_half_mirror
+    else if constexpr (X == 15) return mf_dpp<0x140>(x);       // row_mirror
+    else if constexpr (X == 8) return mf_dpp<0x128>(x);        // row_ror:8
+    else { static_assert(X == 4, "row_xor"); return mf_dpp<0x1B>(mf_dpp<0x141>(x)); }  // (m ^ 7) ^ 3
+}
+template <int X>
+__device__ __forceinline__ float row_xor(float x) { return __int_as_float(row_xor<X>(__float_as_int(x))); }
+
+template <int X>
+__device__ __forceinline__ uint64_t row_xor(uint64_t x) {
+    const unsigned lo = (unsigned)row_xor<X>((int)(unsigned)x), hi = (unsigned)row_xor<X>((int)(unsigned)(x >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// (key, id) packed into one u64 whose unsigned order is the lexicographic (key, id) order: high word
+// = the key's order-preserving bits, low word = the shard-local row (pad 0x7fffffff; an empty slot
+// is ~0).  One v_cmp_lt_u64 per comparison.
+__device__ __forceinline__ unsigned mf_sortable(float f) {
+    const unsigned u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float mf_unsortable(unsigned s) {
+    return __uint_as_float((s & 0x80000000u) ? (s & 0x7fffffffu) : ~s);
+}
+constexpr uint64_t MF_EMPTY = ~0ull;
+constexpr unsigned MF_PAD_ID = 0x7fffffffu;
+
+// Compare-exchange with lane m ^ X: the lower lane of the pair keeps the smaller, the upper the larger.
+template <int X>
+__device__ __forceinline__ void row_cx(uint64_t &p, bool upper) {
+    const uint64_t o = row_xor<X>(p);
+    p = ((o < p) != upper) ? o : p;
+}
+// Ascending bitonic sort of the 16 packed pairs of every DPP row (mirror form: per block size s a
+// mirror stage m ^ (s − 1), then half-cleaners m ^ s/4 … m ^ 1; every stage ascending).
+__device__ __forceinline__ void row_sort16(uint64_t &p, int m) {
+    row_cx<1>(p, m & 1);
+    row_cx<3>(p, m & 2);
+    row_cx<1>(p, m & 1);
+    row_cx<7>(p, m & 4);
+    row_cx<2>(p, m & 2);
+    row_cx<1>(p, m & 1);
+    row_cx<15>(p, m & 8);
+    row_cx<4>(p, m & 4);
+    row_cx<2>(p, m & 2);
+    row_cx<1>(p, m & 1);
+}
+// Merge a row-sorted run c into the row-sorted list l: the 16 smallest of the union (min against
+// the reversed run is bitonic; four half-cleaner stages sort it).
+__device__ __forceinline__ void row_merge16(uint64_t &l, uint64_t c, int m) {
+    const uint64_t r = row_xor<15>(c);
+    l = r < l ? r : l;
+    row_cx<8>(l, m & 8);
+    row_cx<4>(l, m & 4);
+    row_cx<2>(l, m & 2);
+    row_cx<1>(l, m & 1);
+}
+// Element kth of every row's list, broadcast to the row's lanes (the row's admission threshold).
+__device__ __forceinline__ uint64_t row_kth(uint64_t l, int kth, int g) {
+    const unsigned lo = (unsigned)l, hi = (unsigned)(l >> 32);
+    unsigned rl[4], rh[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        rl[r] = (unsigned)__builtin_amdgcn_readlane((int)lo, 16 * r + kth);
+        rh[r] = (unsigned)__builtin_amdgcn_readlane((int)hi, 16 * r + kth);
+    }
+    const unsigned sl = g == 0 ? rl[0] : g == 1 ? rl[1] : g == 2 ? rl[2] : rl[3];
+    const unsigned sh = g == 0 ? rh[0] : g == 1 ? rh[1] : g == 2 ? rh[2] : rh[3];
+    return ((uint64_t)sh << 32) | sl;
+}
+
+// ---- one wave's share of an item -----------------------------------------------------------------
+template <int QT, bool IP>
+__device__ __forceinline__ void mf_item(int d, const float *__restrict__ codes, const float *__restrict__ xn,
+                                        int64_t r0, int64_t r1, int nqi, const float *__restrict__ qs, int stride,
+                                        const float (&qn)[QT][4], const unsigned (&qb)[QT][4],
+                                        const int *__restrict__ bucket, int boff, int nprobe,
+                                        const int *__restrict__ slot_off, int chunk, int k, float *smem,
+                                        unsigned *__restrict__ qbound, float *__restrict__ part_d,
+                                        int *__restrict__ part_i) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int m = lane & 15, g = lane >> 4;
+    const int nsub = mf_nsub(d);               // 16-dim steps per pass (multiple of MF_P)
+    const int npass_all = (int)ceil_div(r1 - r0, MF_PASS);
+    const int npass = npass_all > wave ? (npass_all - wave + MF_WAVES - 1) / MF_WAVES : 0;  // wave-uniform
+    const int nstep = npass * nsub;
+
+    // query validity of the accumulator registers: query qt·16 + 4g + v
+    bool qv[QT][4];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) qv[qt][v] = qt * 16 + 4 * g + v < nqi;
+
+    // Lists start as k copies of (bound, pad): the query's best known k-th key over the items that
+    // finished before this one (qbound, any list of this shard), so only rows that can still reach
+    // the query's final top-k are ever merged.  Pad entries never reach the output (the merge kernel
+    // drops id 0x7fffffff).
+    uint64_t lst[QT][4], thr[QT][4];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const uint64_t b = ((uint64_t)qb[qt][v] << 32) | MF_PAD_ID;
+            lst[qt][v] = m < k ? b : MF_EMPTY;
+            thr[qt][v] = b;
+        }
+
+    // ---- row stream: step t = (pass i, dim step s); lane loads rows (pass row0 + 16r + m), dims
+    // 16s + 4g.  The loads are unconditional (past the wave's last step they re-read its last step):
+    // a load under a branch makes hipcc fall back to vmcnt(0) at the loop head, draining the ring.
+    auto row_of = [&](int i, int r) -> int64_t {
+        const int64_t row = r0 + (int64_t)(wave + MF_WAVES * i) * MF_PASS + 16 * r + m;
+        return row < r1 ? row : r1 - 1;
+    };
+    const int ilast = npass > 0 ? npass - 1 : 0;
+    const float *rp[MF_RT];   // row bases (+ 4g) of the pass the load stream is in
+    int ld_i = 0, ld_s = 0;   // stream position of the next load (wave-uniform)
+    auto set_pass = [&](int i) {
+#pragma unroll
+        for (int r = 0; r < MF_RT; ++r) rp[r] = codes + row_of(i, r) * (int64_t)d + 4 * g;
+    };
+    auto next_load = [&](mf_f32x4 (&dst)[MF_RT]) {
+        const int s = ld_i <= ilast ? ld_s : nsub - 1;
+        const int kk = 16 * s + 4 * g < d ? 16 * s : d - 4 - 4 * g;  // dims past d: any valid float4
+#pragma unroll
+        for (int r = 0; r < MF_RT; ++r) dst[r] = *reinterpret_cast<const mf_f32x4 *>(rp[r] + kk);
+        if (++ld_s == nsub) {
+            ld_s = 0;
+            ++ld_i;
+            set_pass(ld_i <= ilast ? ld_i : ilast);
+        }
+    };
+
+    mf_f32x4 ring[MF_P][MF_RT];
+    float xnr[MF_RT] = {0.f, 0.f};
+    if (npass > 0) {
+        set_pass(0);
+#pragma unroll
+        for (int p = 0; p < MF_P; ++p) next_load(ring[p]);
+        if (!IP) {
+#pragma unroll
+            for (int r = 0; r < MF_RT; ++r) xnr[r] = xn[row_of(0, r)];
+        }
+    }
+
+    mf_f32x4 acc[QT][MF_RT];
+    for (int i = 0; i < npass; ++i) {
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+            for (int r = 0; r < MF_RT; ++r) acc[qt][r] = mf_f32x4{0.f, 0.f, 0.f, 0.f};
+        float xnr_next[MF_RT] = {0.f, 0.f};
+        if (!IP) {
+#pragma unroll
+            for (int r = 0; r < MF_RT; ++r) xnr_next[r] = xn[row_of(i + 1 <= ilast ? i + 1 : ilast, r)];
+        }
+        for (int s0 = 0; s0 < nsub; s0 += MF_P) {
+#pragma unroll
+            for (int p = 0; p < MF_P; ++p) {
+                const int s = s0 + p;
+                mf_f32x4 qa[QT];
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt)
+                    qa[qt] = *reinterpret_cast<const mf_f32x4 *>(qs + (qt * 16 + m) * stride + 16 * s + 4 * g);
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                        for (int r = 0; r < MF_RT; ++r)
+                            if (HIPANN_MF_EXPERIMENT != 3)
+                                acc[qt][r] = __builtin_amdgcn_mfma_f32_16x16x4f32(qa[qt][e], ring[p][r][e], acc[qt][r], 0, 0, 0);
+                            else
+                                acc[qt][r][e] += qa[qt][e] + ring[p][r][e];
+                if (HIPANN_MF_EXPERIMENT != 2) next_load(ring[p]);
+            }
+        }
+        // ---- pass epilogue: keys, filter, merge ----
+        const int64_t prow0 = r0 + (int64_t)(wave + MF_WAVES * i) * MF_PASS;
+#pragma unroll
+        for (int r = 0; r < MF_RT; ++r) {
+            const int64_t row = prow0 + 16 * r + m;
+            const bool rok = row < r1;
+            const unsigned rid = rok ? (unsigned)row : MF_PAD_ID;
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    float key;
+                    if (IP) {
+                        key = -acc[qt][r][v];
+                    } else {
+                        key = fmaf(-2.f, acc[qt][r][v], qn[qt][v] + xnr[r]);
+                        key = key < 0.f ? 0.f : key;
+                    }
+                    const bool ok = rok && qv[qt][v];
+                    key = ok ? key : __builtin_inff();
+                    uint64_t cp = ok ? (((uint64_t)mf_sortable(key) << 32) | rid) : MF_EMPTY;
+                    if (HIPANN_MF_EXPERIMENT == 1) {
+                        lst[qt][v] += cp;
+                    } else if (__ballot(cp < thr[qt][v])) {
+                        row_sort16(cp, m);
+                        row_merge16(lst[qt][v], cp, m);
+                        thr[qt][v] = row_kth(lst[qt][v], k - 1, g);
+                    }
+                }
+        }
+#pragma unroll
+        for (int r = 0; r < MF_RT; ++r) xnr[r] = xnr_next[r];
+    }
+
+    // ---- merge the 8 waves' lists: rounds of (upper half writes → barrier → lower half merges) ----
+    // the query image is dead once every wave has left its main loop (first barrier)
+    uint64_t *scratch = reinterpret_cast<uint64_t *>(smem);
+#pragma unroll 1
+    for (int half = MF_WAVES / 2; half > 0; half >>= 1) {
+        __syncthreads();
+        if (wave >= half && wave < 2 * half) {
+            uint64_t *dst = scratch + (size_t)(wave - half) * QT * 4 * 64;
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                for (int v = 0; v < 4; ++v)
+                    dst[(qt * 4 + v) * 64 + lane] = lst[qt][v];
+        }
+        __syncthreads();
+        if (wave < half) {
+            const uint64_t *src = scratch + (size_t)wave * QT * 4 * 64;
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) row_merge16(lst[qt][v], src[(qt * 4 + v) * 64 + lane], m);
+        }
+    }
+    if (wave == 0 && m < k) {
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const int q = qt * 16 + 4 * g + v;
+                if (q < nqi) {
+                    const int pr = bucket[boff + q];
+                    const int64_t off = (int64_t)(slot_off[pr] + chunk) * k + m;
+                    const uint64_t e = lst[qt][v];
+                    const unsigned id = (unsigned)e;
+                    const bool real = e != MF_EMPTY && id != MF_PAD_ID;
+                    part_d[off] = real ? mf_unsortable((unsigned)(e >> 32)) : __builtin_inff();
+                    part_i[off] = real ? (int)id : (int)MF_PAD_ID;
+                    // a real k-th tightens the query's bound for the items that start later
+                    if (m == k - 1 && real) atomicMin(qbound + pr / nprobe, (unsigned)(e >> 32));
+                }
+            }
+    }
+}
+
+template <bool IP>
+__global__ void __launch_bounds__(MF_THREADS, 2)
+ivf_scan_mfma(const float *__restrict__ Q, const float *__restrict__ qnorm, int d, const float *__restrict__ codes,
+              const float *__restrict__ xn, const int64_t *__restrict__ list_off, const int *__restrict__ cnt,
+              const int *__restrict__ bucket_off, const int *__restrict__ item_off, const int *__restrict__ bucket,
+              const int *__restrict__ slot_off, int nlist, int nprobe, int group, int k,
+              unsigned *__restrict__ qbound, float *__restrict__ part_d, int *__restrict__ part_i) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int total = item_off[nlist];
+    if ((int)blockIdx.x >= total) return;
+    const int item = xcd_remap((int)blockIdx.x, total);
+    int lo = 0, hi = nlist - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (item_off[mid] <= item) lo = mid; else hi = mid - 1;
+    }
+    const int l = lo;
+    const int64_t lr0 = list_off[l], lr1 = list_off[l + 1];
+    const int c = cnt[l];
+    const int ng = (c + group - 1) / group;
+    const int rem = item - item_off[l];
+    const int chunk = rem / ng, grp = rem - chunk * ng;  // (row chunk, query group), group fastest
+    const int q_begin = (int)((int64_t)grp * c / ng), q_end = (int)((int64_t)(grp + 1) * c / ng);
+    const int nqi = q_end - q_begin;
+    const int64_t r0 = lr0 + (int64_t)chunk * MF_CH;
+    const int64_t r1 = r0 + MF_CH < lr1 ? r0 + MF_CH : lr1;
+    const int boff = bucket_off[l] + q_begin;
+    const int nqt = (nqi + 15) >> 4;
+
+    // ---- the item's queries → LDS: [query][stride] fp32, dims ≥ d zero ----
+    const int stride = mf_stride(d);
+    const int nf4 = mf_nsub(d) * 4;
+    for (int t = threadIdx.x; t < nqi * nf4; t += MF_THREADS) {
+        const int q = t / nf4, f = t - (t / nf4) * nf4;
+        const float *src = Q + (int64_t)(bucket[boff + q] / nprobe) * d;
+        mf_f32x4 v = mf_f32x4{0.f, 0.f, 0.f, 0.f};
+        if (4 * f < d) v = *reinterpret_cast<const mf_f32x4 *>(src + 4 * f);
+        *reinterpret_cast<mf_f32x4 *>(smem + q * stride + 4 * f) = v;
+    }
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, g = lane >> 4;
+#define MF_ARGS d, codes, xn, r0, r1, nqi, smem, stride, qn, qb, bucket, boff, nprobe, slot_off, chunk, k, smem, \
+                qbound, part_d, part_i
+#define MF_QN(QTV)                                                                                          \
+    float qn[QTV][4];                                                                                       \
+    unsigned qb[QTV][4];                                                                                    \
+    _Pragma("unroll") for (int qt = 0; qt < QTV; ++qt) _Pragma("unroll") for (int v = 0; v < 4; ++v) {      \
+        const int q = qt * 16 + 4 * g + v;                                                                  \
+        const int qi = q < nqi ? bucket[boff + q] / nprobe : 0;                                             \
+        qn[qt][v] = (!IP && q < nqi) ? qnorm[qi] : 0.f;                                                     \
+        qb[qt][v] = q < nqi ? __atomic_load_n(qbound + qi, __ATOMIC_RELAXED) : 0xffffffffu;                 \
+    }
+    if (nqt <= 1) {
+        MF_QN(1)
+        mf_item<1, IP>(MF_ARGS);
+    } else if (nqt == 2) {
+        MF_QN(2)
+        mf_item<2, IP>(MF_ARGS);
+    } else {
+        MF_QN(3)
+        mf_item<3, IP>(MF_ARGS);
+    }
+#undef MF_QN
+#undef MF_ARGS
+}
+
+bool ivf_mfma_supported(const float *Q, int d, const float *codes, int k) {
+    return (d % 4 == 0) && ((uintptr_t)Q % 16 == 0) && ((uintptr_t)codes % 16 == 0) && k >= 1 && k <= MF_KMAX &&
+           mf_group(d) >= 16;
+}
+
+int ivf_mfma_group(int d) { return mf_group(d); }
+
+void launch_ivf_scan_mfma(const float *Q, const float *qn, int d, int metric, const float *codes, const float *xn,
+                          const int64_t *list_off, const int *cnt, const int *bucket_off, const int *item_off,
+                          const int *bucket, const int *slot_off, int nlist, int nprobe, int k, int64_t max_items,
+                          unsigned *qbound, float *pd, int *pi, hipStream_t st) {
+    if (max_items <= 0) return;
+    HIPANN_REQUIRE(max_items < (int64_t)0x7fffffff, "too many IVF work items");
+    HIPANN_REQUIRE(ivf_mfma_supported(Q, d, codes, k), "MFMA IVF scan needs d % 4 == 0, 16-B aligned data, k <= 16");
+    HIPANN_REQUIRE(metric == kIP || (qn && xn), "decomposed L2 scan needs query and row norms");
+    const int group = mf_group(d);
+    const size_t merge = (size_t)(MF_WAVES / 2) * MF_QTMAX * 4 * 64 * sizeof(float2);  // end-of-item scratch
+    const size_t smem = std::max((size_t)group * mf_stride(d) * 4, merge);
+    dim3 grid((unsigned)max_items), block(MF_THREADS);
+#define MF_LAUNCH_ARGS Q, qn, d, codes, xn, list_off, cnt, bucket_off, item_off, bucket, slot_off, nlist, nprobe, group, k, \
+                       qbound, pd, pi
+    if (metric == kIP) hipLaunchKernelGGL((ivf_scan_mfma<true>), grid, block, smem, st, MF_LAUNCH_ARGS);
+    else hipLaunchKernelGGL((ivf_scan_mfma<false>), grid, block, smem, st, MF_LAUNCH_ARGS);
+#undef MF_LAUNCH_ARGS
+    HIPANN_CHECK(hipGetLastError());
+}
+
+}  // namespace hipann

@@ -172,6 +172,7 @@ struct IvfShard {
     hipStream_t stream = nullptr;
     // scratch
     DevBuf q, qn, coarse_d, coarse_i, cnt, bucket_off, item_off, cursor, bucket, slot_off, part_d, part_i, out_d, out_i;
+    DevBuf qbound;                 // per query: best known k-th key (order-preserving u32; MFMA scan)
     int max_nch = 1;  // largest list's row-chunk count
 };
 
@@ -197,7 +198,7 @@ struct IvfIndex : IndexBase {
     }
 };
 
-// ---- kernel launchers (flat_kernels.hip, ivf_kernels.hip) ----
+// ---- kernel launchers (flat_kernels.hip, ivf_kernels.hip, ivf_mfma.hip) ----
 void launch_row_norms(const float *x, int64_t n, int d, float *out, hipStream_t st);
 size_t gemm_smem_bytes();
 void launch_flat_gemm_topk(const float *Q, const float *qn, int64_t nq, const float *X, const float *xn, int64_t N,
@@ -218,14 +219,20 @@ void launch_ivf_plan(const int64_t *probes, int64_t nq, int nprobe, const int *l
                      int *cnt, int *bucket_off, int *item_off, int *cursor, int *bucket, int *slot_off,
                      hipStream_t st);
 int64_t ivf_max_items(int64_t nq, int nprobe, int nlist, int max_nch, int64_t nrows, int group);
-int ivf_group_size(int form);  // queries per work item of the form's scan kernel
+int ivf_group_size(int form, int d);  // queries per work item of the form's scan kernel
 int ivf_chunk_rows();
 size_t ivf_scan_smem_bytes();
 bool ivf_dot_supported(const float *Q, int d, const float *codes);
 void launch_ivf_scan(const float *Q, const float *qn, int d, int metric, int form, const float *codes,
                      const float *xn, const int64_t *list_off, const int *cnt, const int *bucket_off,
                      const int *item_off, const int *bucket, const int *slot_off, int nlist, int nprobe, int64_t nq,
-                     int k, int64_t max_items, float *pd, int *pi, hipStream_t st);
+                     int k, int64_t max_items, unsigned *qbound, float *pd, int *pi, hipStream_t st);
+bool ivf_mfma_supported(const float *Q, int d, const float *codes, int k);
+int ivf_mfma_group(int d);
+void launch_ivf_scan_mfma(const float *Q, const float *qn, int d, int metric, const float *codes, const float *xn,
+                          const int64_t *list_off, const int *cnt, const int *bucket_off, const int *item_off,
+                          const int *bucket, const int *slot_off, int nlist, int nprobe, int k, int64_t max_items,
+                          unsigned *qbound, float *pd, int *pi, hipStream_t st);
 void launch_ivf_merge(const float *pd, const int *pi, const int64_t *ids, const int *slot_off, int nprobe, int64_t nq,
                       int k, int kout, float out_sign, float *D, int64_t *I, hipStream_t st);
 template <typename InId>

@@ -59,6 +59,29 @@ __device__ __forceinline__ long long shfl_up1_i(long long v) {
     return (long long)(((unsigned long long)hi << 32) | lo);
 }
 
+// Compare-exchange with lane ^ stride in (key, id) lexicographic order: keep the smaller pair when
+// keep_min, else the larger.  Both lanes see the same pair, so the exchange is consistent.
+template <typename IdT>
+__device__ __forceinline__ void wave_cmpx(float &k, IdT &id, int stride, bool keep_min) {
+    const float ok = __shfl_xor(k, stride);
+    const IdT oid = __shfl_xor(id, stride);
+    const bool take = keep_min ? lex_less(ok, oid, k, id) : lex_less(k, id, ok, oid);
+    if (take) { k = ok; id = oid; }
+}
+
+// Bitonic sort of one (key, id) per lane, ascending across the wave (21 compare-exchange stages).
+template <typename IdT>
+__device__ __forceinline__ void wave_sort(float &k, IdT &id) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int size = 2; size <= 64; size <<= 1)
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            const bool up = (lane & size) == 0;  // size = 64: every lane ascending
+            wave_cmpx(k, id, stride, ((lane & stride) == 0) == up);
+        }
+}
+
 // One wave-distributed list of 64*S elements.
 template <int S, typename IdT = int>
 struct WaveList {
@@ -124,6 +147,19 @@ struct WaveList {
             threshold(kth, t2d, t2i);
             if (lex_less(xd, xi, t2d, t2i)) insert(xd, xi);
         }
+    }
+
+    // Bulk merge (S = 1): (ck, cid) is a wave-sorted ascending run of 64 candidates (wave_sort).
+    // min(list, reverse(run)) is bitonic and holds the 64 smallest of the union; six half-cleaner
+    // stages sort it.  ≈ 7 shuffle stages, independent of how many candidates enter.
+    __device__ __forceinline__ void merge_sorted(float ck, IdT cid) {
+        static_assert(S == 1, "bulk merge is for one-slot lists");
+        const int lane = lane_id();
+        const float rk = __shfl(ck, 63 - lane);
+        const IdT rid = __shfl(cid, 63 - lane);
+        if (lex_less(rk, rid, d[0], id[0])) { d[0] = rk; id[0] = rid; }
+#pragma unroll
+        for (int stride = 32; stride > 0; stride >>= 1) wave_cmpx(d[0], id[0], stride, (lane & stride) == 0);
     }
 
     // Write elements [0, k) to out_d / out_i (lane-strided, coalesced).

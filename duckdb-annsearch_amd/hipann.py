@@ -323,8 +323,9 @@ class HipIndexIVFFlat(_Handle):
             raise HipAnnError("nprobe must be >= 1")
         self._nprobe = int(v)
 
-    FORM_DECOMPOSED = 0  # ‖q‖² + ‖x‖² − 2 q·x (FAISS GPU / faiss-metal IVF form; default)
-    FORM_DIRECT = 1      # Σ(q − x)² (FAISS CPU IndexIVFFlat scanner form)
+    FORM_DECOMPOSED = 0       # ‖q‖² + ‖x‖² − 2 q·x on the fp32 matrix cores (FAISS GPU / faiss-metal IVF form; default)
+    FORM_DIRECT = 1           # Σ(q − x)² (FAISS CPU IndexIVFFlat scanner form)
+    FORM_DECOMPOSED_VALU = 2  # the decomposed form on the VALU kernel (A/B measurement)
 
     @property
     def form(self) -> int:
@@ -333,7 +334,7 @@ class HipIndexIVFFlat(_Handle):
     @form.setter
     def form(self, v: int) -> None:
         if lib().hipann_ivf_set_form(self._h, int(v)) != 0:
-            raise HipAnnError("form must be 0 (decomposed) or 1 (direct)")
+            raise HipAnnError("form must be 0 (decomposed), 1 (direct) or 2 (decomposed, VALU)")
 
     def search(self, x, k: int) -> Tuple[np.ndarray, np.ndarray]:
         x = _f32_2d(x, self.d)

@@ -124,12 +124,15 @@ int hipann_ivf_set_nprobe(void *index, int nprobe);
 
 /* List-scan distance form.  HIPANN_IVF_FORM_DECOMPOSED (default): ‖q‖² + ‖x‖² − 2·q·x clamped ≥ 0
  * (IP: q·x), with ‖x‖² stored per row — the form faiss-metal's IVF path and FAISS's GPU IVFFlat use
- * (MetalIndexIVFFlat.mm:305-318), one FMA per dimension.  HIPANN_IVF_FORM_DIRECT: Σ(q−x)², the form
- * of FAISS's CPU IndexIVFFlat scanner (subtract + FMA per dimension).  Both run on the GPU; the
- * decomposed form needs d % 4 == 0 and 16-B aligned data and falls back to the direct kernel
- * otherwise.  Returns 0, or −1 for a bad handle / form. */
+ * (MetalIndexIVFFlat.mm:305-318), computed on the fp32 matrix cores (exact fp32 products, fp32
+ * accumulation).  HIPANN_IVF_FORM_DIRECT: Σ(q−x)², the form of FAISS's CPU IndexIVFFlat scanner
+ * (subtract + FMA per dimension, VALU).  HIPANN_IVF_FORM_DECOMPOSED_VALU: the decomposed form on the
+ * VALU kernel (kept for A/B measurement).  All run on the GPU; the decomposed forms need d % 4 == 0
+ * and 16-B aligned data and fall back to the direct kernel otherwise.  Returns 0, or −1 for a bad
+ * handle / form. */
 #define HIPANN_IVF_FORM_DECOMPOSED 0
 #define HIPANN_IVF_FORM_DIRECT 1
+#define HIPANN_IVF_FORM_DECOMPOSED_VALU 2
 int hipann_ivf_set_form(void *index, int form);
 int hipann_ivf_get_form(void *index);
 
