@@ -86,12 +86,27 @@ void upload_list_meta(IvfShard &sh, const std::vector<int64_t> &off, int nlist) 
         maxlen = std::max<int64_t>(maxlen, len[l]);
     }
     sh.max_nch = (int)std::max<int64_t>(1, ceil_div(maxlen, ivf_chunk_rows()));
+    sh.h_off = off;
     sh.list_off.ensure(sizeof(int64_t) * (nlist + 1), sh.device);
     sh.list_len.ensure(sizeof(int) * nlist, sh.device);
     HIPANN_CHECK(hipMemcpyAsync(sh.list_off.p, off.data(), sizeof(int64_t) * (nlist + 1), hipMemcpyHostToDevice,
                                 sh.stream));
     HIPANN_CHECK(hipMemcpyAsync(sh.list_len.p, len.data(), sizeof(int) * nlist, hipMemcpyHostToDevice, sh.stream));
     HIPANN_CHECK(hipStreamSynchronize(sh.stream));
+}
+
+// The MFMA scan's tiled copy of the codes (built once, at the first search that uses it).
+void ensure_tiled_codes(IvfShard &sh, int d, int nlist, hipStream_t st) {
+    if (sh.codes_t.p || sh.n == 0) return;
+    std::vector<int64_t> tp(nlist + 1, 0);
+    for (int l = 0; l < nlist; ++l) tp[l + 1] = tp[l] + ceil_div(sh.h_off[l + 1] - sh.h_off[l], 32);
+    const int64_t pf = ivf_mfma_pass_floats(d);
+    sh.codes_t.ensure(sizeof(float) * (size_t)std::max<int64_t>(tp[nlist], 1) * pf, sh.device);
+    sh.tpass_off.ensure(sizeof(int64_t) * (nlist + 1), sh.device);
+    HIPANN_CHECK(hipMemcpyAsync(sh.tpass_off.p, tp.data(), sizeof(int64_t) * (nlist + 1), hipMemcpyHostToDevice, st));
+    launch_ivf_tile_codes(sh.codes, sh.list_off.get<int64_t>(), sh.tpass_off.get<int64_t>(), nlist, tp[nlist], d,
+                          sh.codes_t.get<float>(), st);
+    HIPANN_CHECK(hipStreamSynchronize(st));  // tp (host) is released on return
 }
 
 // ‖x‖² of every stored row (L2 only): the decomposed scan form reads it with the codes
@@ -165,16 +180,24 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
         qbound = sh.qbound.get<unsigned>();
         HIPANN_CHECK(hipMemsetD32Async((hipDeviceptr_t)qbound, 0xff800000, (size_t)nq, st));
     }
+    if (form == kFormDecomposed) ensure_tiled_codes(sh, d, nlist, st);
     {
         ScopedTiming t(ix.timer_main, st);
-        launch_ivf_scan(xq, qn, d, metric, form, sh.codes, sh.xnorm.get<float>(), sh.list_off.get<int64_t>(),
-                        sh.cnt.get<int>(), sh.bucket_off.get<int>(), sh.item_off.get<int>(), sh.bucket.get<int>(),
-                        sh.slot_off.get<int>(), nlist, np, nq, k, max_items, qbound, sh.part_d.get<float>(),
-                        sh.part_i.get<int>(), st);
+        if (form == kFormDecomposed)
+            launch_ivf_scan_mfma(xq, qn, d, metric, sh.codes_t.get<float>(), sh.tpass_off.get<int64_t>(),
+                                 sh.xnorm.get<float>(), sh.list_off.get<int64_t>(), sh.cnt.get<int>(),
+                                 sh.bucket_off.get<int>(), sh.item_off.get<int>(), sh.bucket.get<int>(),
+                                 sh.slot_off.get<int>(), nlist, np, k, max_items, qbound, sh.part_d.get<float>(),
+                                 sh.part_i.get<int>(), st);
+        else
+            launch_ivf_scan(xq, qn, d, metric, form, sh.codes, sh.xnorm.get<float>(), sh.list_off.get<int64_t>(),
+                            sh.cnt.get<int>(), sh.bucket_off.get<int>(), sh.item_off.get<int>(), sh.bucket.get<int>(),
+                            sh.slot_off.get<int>(), nlist, np, nq, k, max_items, qbound, sh.part_d.get<float>(),
+                            sh.part_i.get<int>(), st);
     }
     // 4. merge each query's partial lists
     ScopedTiming t(ix.timer_merge, st);
-    launch_ivf_merge(sh.part_d.get<float>(), sh.part_i.get<int>(), sh.ids, sh.slot_off.get<int>(), np, nq, k, kout,
+    launch_ivf_merge(sh.part_d.get<float>(), sh.part_i.get<int>(), sh.ids, sh.n, sh.slot_off.get<int>(), np, nq, k, kout,
                      out_sign, D, I, st);
 }
 

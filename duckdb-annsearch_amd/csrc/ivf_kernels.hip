@@ -733,7 +733,7 @@ ivf_dot_dispatch<0, IP>(nwq, d, codes, xn, r0, r1, qsrc0, qsrc1, qn, wq0, bucket
 template <int S>
 __global__ void __launch_bounds__(256)
 ivf_merge_topk(const float *__restrict__ pd, const int *__restrict__ pi, const int64_t *__restrict__ ids,
-               const int *__restrict__ slot_off, int nprobe, int64_t nq, int k, int kout, float out_sign,
+               int64_t nrows, const int *__restrict__ slot_off, int nprobe, int64_t nq, int k, int kout, float out_sign,
                float *__restrict__ D, int64_t *__restrict__ I) {
     const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (q >= nq) return;
@@ -750,7 +750,7 @@ ivf_merge_topk(const float *__restrict__ pd, const int *__restrict__ pi, const i
             const int64_t off = s0 * k + c;
             const int raw = pi[off];
             const float v = pd[off];
-            if (raw >= 0 && raw != 0x7fffffff && !(v == __builtin_inff())) {
+            if (raw >= 0 && raw < nrows && !(v == __builtin_inff())) {  // pads: 0x7fffffff >= nrows
                 key = v;
                 lab = (long long)ids[raw];
             }
@@ -795,10 +795,6 @@ int64_t ivf_max_items(int64_t nq, int nprobe, int nlist, int max_nch, int64_t nr
 }
 
 int ivf_mfma_group(int d);  // ivf_mfma.hip
-void launch_ivf_scan_mfma(const float *Q, const float *qn, int d, int metric, const float *codes, const float *xn,
-                          const int64_t *list_off, const int *cnt, const int *bucket_off, const int *item_off,
-                          const int *bucket, const int *slot_off, int nlist, int nprobe, int k, int64_t max_items,
-                          unsigned *qbound, float *pd, int *pi, hipStream_t st);
 
 int ivf_group_size(int form, int d) {
     return form == kFormDecomposed ? ivf_mfma_group(d) : form == kFormDecomposedValu ? DT_G : IVF_G;
@@ -819,11 +815,7 @@ void launch_ivf_scan(const float *Q, const float *qn, int d, int metric, int for
                      int k, int64_t max_items, unsigned *qbound, float *pd, int *pi, hipStream_t st) {
     if (max_items <= 0) return;
     HIPANN_REQUIRE(max_items < (int64_t)0x7fffffff, "too many IVF work items");
-    if (form == kFormDecomposed) {
-        launch_ivf_scan_mfma(Q, qn, d, metric, codes, xn, list_off, cnt, bucket_off, item_off, bucket, slot_off, nlist,
-                             nprobe, k, max_items, qbound, pd, pi, st);
-        return;
-    }
+    HIPANN_REQUIRE(form != kFormDecomposed, "the MFMA scan is launched with its tiled codes (launch_ivf_scan_mfma)");
     if (form == kFormDecomposedValu) {
         HIPANN_REQUIRE(ivf_dot_supported(Q, d, codes), "decomposed IVF scan needs d % 4 == 0 and 16-B aligned data");
         HIPANN_REQUIRE(metric == kIP || (qn && xn), "decomposed L2 scan needs query and row norms");
@@ -850,14 +842,14 @@ void launch_ivf_scan(const float *Q, const float *qn, int d, int metric, int for
     HIPANN_CHECK(hipGetLastError());
 }
 
-void launch_ivf_merge(const float *pd, const int *pi, const int64_t *ids, const int *slot_off, int nprobe, int64_t nq,
+void launch_ivf_merge(const float *pd, const int *pi, const int64_t *ids, int64_t nrows, const int *slot_off, int nprobe, int64_t nq,
                       int k, int kout, float out_sign, float *D, int64_t *I, hipStream_t st) {
     if (nq <= 0) return;
     dim3 grid((unsigned)ceil_div(nq, 4)), block(256);
     const int S = (kout + 63) / 64;
 #define HIPANN_IVF_MERGE(s)                                                                                           \
     if (S <= s) {                                                                                                     \
-        hipLaunchKernelGGL(ivf_merge_topk<s>, grid, block, 0, st, pd, pi, ids, slot_off, nprobe, nq, k, kout,       \
+        hipLaunchKernelGGL(ivf_merge_topk<s>, grid, block, 0, st, pd, pi, ids, nrows, slot_off, nprobe, nq, k, kout, \
                            out_sign, D, I);                                                                           \
         HIPANN_CHECK(hipGetLastError());                                                                              \
         return;                                                                                                       \

@@ -43,12 +43,22 @@ typedef float mf_f32x4 __attribute__((ext_vector_type(4)));
 #define HIPANN_MF_EXPERIMENT 0  // tuning builds only (wrong results): 1 no selection, 2 no row loads, 3 no MFMA
 #endif
 
-constexpr int MF_WAVES = 8;
+#ifndef HIPANN_MF_WAVES
+#define HIPANN_MF_WAVES 8
+#endif
+#ifndef HIPANN_MF_P
+#define HIPANN_MF_P 6
+#endif
+#ifndef HIPANN_MF_QPF
+#define HIPANN_MF_QPF 0
+#endif
+constexpr int MF_WAVES = HIPANN_MF_WAVES;
 constexpr int MF_THREADS = 64 * MF_WAVES;
 constexpr int MF_CH = 2048;   // rows per item (= IVF_CH of ivf_kernels.hip)
 constexpr int MF_PASS = 32;   // rows per wave pass (2 MFMA row tiles)
 constexpr int MF_RT = 2;      // row tiles per pass
-constexpr int MF_P = 6;       // sixteen-dim steps in flight per wave (register ring depth)
+constexpr int MF_P = HIPANN_MF_P;  // sixteen-dim steps in flight per wave (register ring depth)
+constexpr bool MF_QPF = HIPANN_MF_QPF;  // read the next step's query fragments before this step's MFMAs
 constexpr int MF_QTMAX = 3;   // query tiles per item (G ≤ 48)
 constexpr int MF_KMAX = 16;   // lists are 16-lane DPP rows
 constexpr size_t MF_LDS_MAX = 160 * 1024;
@@ -149,7 +159,8 @@ __device__ __forceinline__ uint64_t row_kth(uint64_t l, int kth, int g) {
 
 // ---- one wave's share of an item -----------------------------------------------------------------
 template <int QT, bool IP>
-__device__ __forceinline__ void mf_item(int d, const float *__restrict__ codes, const float *__restrict__ xn,
+__device__ __forceinline__ void mf_item(int d, const float *__restrict__ codes_t, int64_t tp0,
+                                        const float *__restrict__ xn,
                                         int64_t r0, int64_t r1, int nqi, const float *__restrict__ qs, int stride,
                                         const float (&qn)[QT][4], const unsigned (&qb)[QT][4],
                                         const int *__restrict__ bucket, int boff, int nprobe,
@@ -185,25 +196,26 @@ __device__ __forceinline__ void mf_item(int d, const float *__restrict__ codes, 
             thr[qt][v] = b;
         }
 
-    // ---- row stream: step t = (pass i, dim step s); lane loads rows (pass row0 + 16r + m), dims
-    // 16s + 4g.  The loads are unconditional (past the wave's last step they re-read its last step):
-    // a load under a branch makes hipcc fall back to vmcnt(0) at the loop head, draining the ring.
+    // ---- row stream: step t = (pass i, dim step s).  In the tiled copy a pass's step is 2 KiB
+    // contiguous, [row tile r][lane (g, m)][float4]: lane (g, m) of tile r holds row 16r + m, dims
+    // 16s + 4g .. +3, so each load is one fully coalesced 1 KiB wave-instruction and a pass streams
+    // 96 KiB (d = 768) of consecutive HBM.  The loads are unconditional (past the wave's last step
+    // they re-read it): a load under a branch makes hipcc fall back to vmcnt(0) at the loop head.
     auto row_of = [&](int i, int r) -> int64_t {
         const int64_t row = r0 + (int64_t)(wave + MF_WAVES * i) * MF_PASS + 16 * r + m;
         return row < r1 ? row : r1 - 1;
     };
     const int ilast = npass > 0 ? npass - 1 : 0;
-    const float *rp[MF_RT];   // row bases (+ 4g) of the pass the load stream is in
+    const float *rp;          // this lane's float4 in step 0 of the pass the load stream is in
     int ld_i = 0, ld_s = 0;   // stream position of the next load (wave-uniform)
     auto set_pass = [&](int i) {
-#pragma unroll
-        for (int r = 0; r < MF_RT; ++r) rp[r] = codes + row_of(i, r) * (int64_t)d + 4 * g;
+        rp = codes_t + ((tp0 + wave + MF_WAVES * i) * nsub) * (MF_RT * 256) + 4 * lane;
     };
     auto next_load = [&](mf_f32x4 (&dst)[MF_RT]) {
         const int s = ld_i <= ilast ? ld_s : nsub - 1;
-        const int kk = 16 * s + 4 * g < d ? 16 * s : d - 4 - 4 * g;  // dims past d: any valid float4
 #pragma unroll
-        for (int r = 0; r < MF_RT; ++r) dst[r] = *reinterpret_cast<const mf_f32x4 *>(rp[r] + kk);
+        for (int r = 0; r < MF_RT; ++r)
+            dst[r] = *reinterpret_cast<const mf_f32x4 *>(rp + (int64_t)s * (MF_RT * 256) + r * 256);
         if (++ld_s == nsub) {
             ld_s = 0;
             ++ld_i;
@@ -224,6 +236,12 @@ __device__ __forceinline__ void mf_item(int d, const float *__restrict__ codes, 
     }
 
     mf_f32x4 acc[QT][MF_RT];
+    uint64_t sink = 0;
+    mf_f32x4 qnext[QT];
+    if (MF_QPF) {
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) qnext[qt] = *reinterpret_cast<const mf_f32x4 *>(qs + (qt * 16 + m) * stride + 4 * g);
+    }
     for (int i = 0; i < npass; ++i) {
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt)
@@ -239,9 +257,18 @@ __device__ __forceinline__ void mf_item(int d, const float *__restrict__ codes, 
             for (int p = 0; p < MF_P; ++p) {
                 const int s = s0 + p;
                 mf_f32x4 qa[QT];
+                if (MF_QPF) {
+                    const int sn = s + 1 < nsub ? s + 1 : 0;
 #pragma unroll
-                for (int qt = 0; qt < QT; ++qt)
-                    qa[qt] = *reinterpret_cast<const mf_f32x4 *>(qs + (qt * 16 + m) * stride + 16 * s + 4 * g);
+                    for (int qt = 0; qt < QT; ++qt) {
+                        qa[qt] = qnext[qt];
+                        qnext[qt] = *reinterpret_cast<const mf_f32x4 *>(qs + (qt * 16 + m) * stride + 16 * sn + 4 * g);
+                    }
+                } else {
+#pragma unroll
+                    for (int qt = 0; qt < QT; ++qt)
+                        qa[qt] = *reinterpret_cast<const mf_f32x4 *>(qs + (qt * 16 + m) * stride + 16 * s + 4 * g);
+                }
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -277,7 +304,7 @@ __device__ __forceinline__ void mf_item(int d, const float *__restrict__ codes, 
                     key = ok ? key : __builtin_inff();
                     uint64_t cp = ok ? (((uint64_t)mf_sortable(key) << 32) | rid) : MF_EMPTY;
                     if (HIPANN_MF_EXPERIMENT == 1) {
-                        lst[qt][v] += cp;
+                        sink ^= cp;  // keeps the keys live; the lists (and ids) stay valid
                     } else if (__ballot(cp < thr[qt][v])) {
                         row_sort16(cp, m);
                         row_merge16(lst[qt][v], cp, m);
@@ -288,6 +315,8 @@ __device__ __forceinline__ void mf_item(int d, const float *__restrict__ codes, 
 #pragma unroll
         for (int r = 0; r < MF_RT; ++r) xnr[r] = xnr_next[r];
     }
+
+    if (HIPANN_MF_EXPERIMENT == 1 && sink == 1) part_d[0] = 0.f;
 
     // ---- merge the 8 waves' lists: rounds of (upper half writes → barrier → lower half merges) ----
     // the query image is dead once every wave has left its main loop (first barrier)
@@ -334,8 +363,9 @@ __device__ __forceinline__ void mf_item(int d, const float *__restrict__ codes, 
 }
 
 template <bool IP>
-__global__ void __launch_bounds__(MF_THREADS, 2)
-ivf_scan_mfma(const float *__restrict__ Q, const float *__restrict__ qnorm, int d, const float *__restrict__ codes,
+__global__ void __launch_bounds__(MF_THREADS, MF_WAVES / 4)
+ivf_scan_mfma(const float *__restrict__ Q, const float *__restrict__ qnorm, int d, const float *__restrict__ codes_t,
+              const int64_t *__restrict__ tpass_off,
               const float *__restrict__ xn, const int64_t *__restrict__ list_off, const int *__restrict__ cnt,
               const int *__restrict__ bucket_off, const int *__restrict__ item_off, const int *__restrict__ bucket,
               const int *__restrict__ slot_off, int nlist, int nprobe, int group, int k,
@@ -375,7 +405,8 @@ ivf_scan_mfma(const float *__restrict__ Q, const float *__restrict__ qnorm, int 
     __syncthreads();
 
     const int lane = threadIdx.x & 63, g = lane >> 4;
-#define MF_ARGS d, codes, xn, r0, r1, nqi, smem, stride, qn, qb, bucket, boff, nprobe, slot_off, chunk, k, smem, \
+    const int64_t tp0 = tpass_off[l] + (int64_t)chunk * (MF_CH / MF_PASS);
+#define MF_ARGS d, codes_t, tp0, xn, r0, r1, nqi, smem, stride, qn, qb, bucket, boff, nprobe, slot_off, chunk, k, smem, \
                 qbound, part_d, part_i
 #define MF_QN(QTV)                                                                                          \
     float qn[QTV][4];                                                                                       \
@@ -400,6 +431,44 @@ ivf_scan_mfma(const float *__restrict__ Q, const float *__restrict__ qnorm, int 
 #undef MF_ARGS
 }
 
+// Tiled copy of the list-contiguous row-major codes: one block per 32-row pass (list found by binary
+// search over the pass offsets); element (pass, step s, tile r, lane (g, m), e) = row 32·p + 16r + m
+// of the list, dim 16s + 4g + e, zero past the list's end and past d.
+__global__ void __launch_bounds__(256)
+ivf_tile_codes(const float *__restrict__ codes, const int64_t *__restrict__ list_off,
+               const int64_t *__restrict__ tpass_off, int nlist, int d, int nsub, float *__restrict__ dst) {
+    const int64_t pass = blockIdx.x;
+    int lo = 0, hi = nlist - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (tpass_off[mid] <= pass) lo = mid; else hi = mid - 1;
+    }
+    const int64_t len = list_off[lo + 1] - list_off[lo];
+    const int64_t prow = (pass - tpass_off[lo]) * MF_PASS;
+    const int nf4 = nsub * MF_RT * 64;
+    for (int t = threadIdx.x; t < nf4; t += 256) {
+        const int s = t / (MF_RT * 64), rem = t - s * (MF_RT * 64);
+        const int r = rem >> 6, lane = rem & 63, g = lane >> 4, m = lane & 15;
+        const int64_t row = prow + 16 * r + m;
+        const int dim = 16 * s + 4 * g;
+        mf_f32x4 v = mf_f32x4{0.f, 0.f, 0.f, 0.f};
+        if (row < len && dim < d) v = *reinterpret_cast<const mf_f32x4 *>(codes + (list_off[lo] + row) * (int64_t)d + dim);
+        *reinterpret_cast<mf_f32x4 *>(dst + (pass * nf4 + t) * 4) = v;
+    }
+}
+
+int64_t ivf_mfma_pass_floats(int d) { return (int64_t)mf_nsub(d) * MF_RT * 256; }
+
+void launch_ivf_tile_codes(const float *codes, const int64_t *list_off, const int64_t *tpass_off, int nlist,
+                           int64_t total_pass, int d, float *dst, hipStream_t st) {
+    if (total_pass <= 0) return;
+    HIPANN_REQUIRE(d % 4 == 0 && (uintptr_t)codes % 16 == 0, "tiled codes need d % 4 == 0 and 16-B aligned rows");
+    HIPANN_REQUIRE(total_pass < (int64_t)0x7fffffff, "too many passes");
+    hipLaunchKernelGGL(ivf_tile_codes, dim3((unsigned)total_pass), dim3(256), 0, st, codes, list_off, tpass_off, nlist,
+                       d, mf_nsub(d), dst);
+    HIPANN_CHECK(hipGetLastError());
+}
+
 bool ivf_mfma_supported(const float *Q, int d, const float *codes, int k) {
     return (d % 4 == 0) && ((uintptr_t)Q % 16 == 0) && ((uintptr_t)codes % 16 == 0) && k >= 1 && k <= MF_KMAX &&
            mf_group(d) >= 16;
@@ -407,19 +476,20 @@ bool ivf_mfma_supported(const float *Q, int d, const float *codes, int k) {
 
 int ivf_mfma_group(int d) { return mf_group(d); }
 
-void launch_ivf_scan_mfma(const float *Q, const float *qn, int d, int metric, const float *codes, const float *xn,
+void launch_ivf_scan_mfma(const float *Q, const float *qn, int d, int metric, const float *codes_t,
+                          const int64_t *tpass_off, const float *xn,
                           const int64_t *list_off, const int *cnt, const int *bucket_off, const int *item_off,
                           const int *bucket, const int *slot_off, int nlist, int nprobe, int k, int64_t max_items,
                           unsigned *qbound, float *pd, int *pi, hipStream_t st) {
     if (max_items <= 0) return;
     HIPANN_REQUIRE(max_items < (int64_t)0x7fffffff, "too many IVF work items");
-    HIPANN_REQUIRE(ivf_mfma_supported(Q, d, codes, k), "MFMA IVF scan needs d % 4 == 0, 16-B aligned data, k <= 16");
+    HIPANN_REQUIRE(ivf_mfma_supported(Q, d, codes_t, k), "MFMA IVF scan needs d % 4 == 0, 16-B aligned data, k <= 16");
     HIPANN_REQUIRE(metric == kIP || (qn && xn), "decomposed L2 scan needs query and row norms");
     const int group = mf_group(d);
     const size_t merge = (size_t)(MF_WAVES / 2) * MF_QTMAX * 4 * 64 * sizeof(float2);  // end-of-item scratch
     const size_t smem = std::max((size_t)group * mf_stride(d) * 4, merge);
     dim3 grid((unsigned)max_items), block(MF_THREADS);
-#define MF_LAUNCH_ARGS Q, qn, d, codes, xn, list_off, cnt, bucket_off, item_off, bucket, slot_off, nlist, nprobe, group, k, \
+#define MF_LAUNCH_ARGS Q, qn, d, codes_t, tpass_off, xn, list_off, cnt, bucket_off, item_off, bucket, slot_off, nlist, nprobe, group, k, \
                        qbound, pd, pi
     if (metric == kIP) hipLaunchKernelGGL((ivf_scan_mfma<true>), grid, block, smem, st, MF_LAUNCH_ARGS);
     else hipLaunchKernelGGL((ivf_scan_mfma<false>), grid, block, smem, st, MF_LAUNCH_ARGS);

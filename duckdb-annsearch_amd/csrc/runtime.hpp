@@ -173,6 +173,10 @@ struct IvfShard {
     // scratch
     DevBuf q, qn, coarse_d, coarse_i, cnt, bucket_off, item_off, cursor, bucket, slot_off, part_d, part_i, out_d, out_i;
     DevBuf qbound;                 // per query: best known k-th key (order-preserving u32; MFMA scan)
+    // MFMA scan copy of the codes, built at the first search that uses it: per list, 32-row passes of
+    // [16-dim step][2 row tiles][64 lanes][float4] (ivf_mfma.hip), zero-padded rows / dims
+    std::vector<int64_t> h_off;    // host copy of list_off
+    DevBuf codes_t, tpass_off;     // tiled codes; int64 nlist+1 pass offsets
     int max_nch = 1;  // largest list's row-chunk count
 };
 
@@ -229,11 +233,15 @@ void launch_ivf_scan(const float *Q, const float *qn, int d, int metric, int for
                      int k, int64_t max_items, unsigned *qbound, float *pd, int *pi, hipStream_t st);
 bool ivf_mfma_supported(const float *Q, int d, const float *codes, int k);
 int ivf_mfma_group(int d);
-void launch_ivf_scan_mfma(const float *Q, const float *qn, int d, int metric, const float *codes, const float *xn,
+int64_t ivf_mfma_pass_floats(int d);  // floats per 32-row pass of the tiled codes
+void launch_ivf_tile_codes(const float *codes, const int64_t *list_off, const int64_t *tpass_off, int nlist,
+                           int64_t total_pass, int d, float *dst, hipStream_t st);
+void launch_ivf_scan_mfma(const float *Q, const float *qn, int d, int metric, const float *codes_t,
+                          const int64_t *tpass_off, const float *xn,
                           const int64_t *list_off, const int *cnt, const int *bucket_off, const int *item_off,
                           const int *bucket, const int *slot_off, int nlist, int nprobe, int k, int64_t max_items,
                           unsigned *qbound, float *pd, int *pi, hipStream_t st);
-void launch_ivf_merge(const float *pd, const int *pi, const int64_t *ids, const int *slot_off, int nprobe, int64_t nq,
+void launch_ivf_merge(const float *pd, const int *pi, const int64_t *ids, int64_t nrows, const int *slot_off, int nprobe, int64_t nq,
                       int k, int kout, float out_sign, float *D, int64_t *I, hipStream_t st);
 template <typename InId>
 void launch_merge_parts(const float *pd, const InId *pi, int nparts, int64_t nq, int k, int kout,
