@@ -77,6 +77,7 @@ hipStream_t make_stream(int dev) {
 
 constexpr int kFusedMaxK = 64;   // fused GEMM / scan lists: one element per lane
 constexpr int kBlasThreshold = 20;  // FAISS distance_compute_blas_threshold
+constexpr int64_t kSmallTable = 16384;  // rows: below this, GEMM keys + per-query selection
 
 // Append rows to a shard's owned storage (capacity doubling, as MetalIndexFlat::add does).
 void shard_append(FlatShard &sh, int d, int metric, const float *x_host, const float *x_dev, int64_t n) {
@@ -186,7 +187,10 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
         return;
     }
     HIPANN_REQUIRE(sh.n <= (int64_t)0x7ffffffe, "shard larger than 2^31-2 rows");
-    if (k > kFusedMaxK) {
+    // Large k, or a small table (an IVF coarse quantizer: nq x nlist keys are a few MB): the GEMM writes
+    // the key matrix and one wave per query selects — the fused epilogue would spend its time
+    // filling empty lists, one query tile per CU.
+    if (k > kFusedMaxK || (nq >= kBlasThreshold && sh.n <= kSmallTable)) {
         const float *qn = nullptr;
         if (nq >= kBlasThreshold && metric == kL2) {
             sh.qn.ensure((size_t)nq * sizeof(float), sh.device);

@@ -98,18 +98,26 @@ __global__ void ivf_fill(const int64_t *__restrict__ probes, int64_t npairs, con
 __global__ void __launch_bounds__(1024) ivf_slot_scan(const int64_t *__restrict__ probes, int64_t npairs,
                                                       const int *__restrict__ list_len, int nlist,
                                                       int *__restrict__ slot_off) {
+    // per round, thread t owns the contiguous pairs base + [32t, 32t + 32): all 32 probe loads, then
+    // all 32 list-length loads are independent (two memory latencies per round, not 64), then a
+    // local scan, one block scan of the 1024 sums and the writes
+    constexpr int PER = 32;
     __shared__ int sv[1024];
     __shared__ int carry;
     if (threadIdx.x == 0) carry = 0;
     __syncthreads();
-    for (int64_t base = 0; base < npairs; base += 1024) {
-        const int64_t i = base + threadIdx.x;
-        int v = 0;
-        if (i < npairs) {
-            const int64_t l = probes[i];
-            if (l >= 0 && l < nlist) v = ivf_nch(list_len[l]);
-        }
-        sv[threadIdx.x] = v;
+    for (int64_t base = 0; base < npairs; base += 1024 * PER) {
+        const int64_t i0 = base + (int64_t)threadIdx.x * PER;
+        int64_t l[PER];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) l[j] = i0 + j < npairs ? probes[i0 + j] : -1;
+        int v[PER];
+#pragma unroll
+        for (int j = 0; j < PER; ++j) v[j] = (l[j] >= 0 && l[j] < nlist) ? ivf_nch(list_len[l[j]]) : 0;
+        int sum = 0;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) sum += v[j];
+        sv[threadIdx.x] = sum;
         __syncthreads();
         for (int o = 1; o < 1024; o <<= 1) {
             int t = 0;
@@ -118,7 +126,12 @@ __global__ void __launch_bounds__(1024) ivf_slot_scan(const int64_t *__restrict_
             sv[threadIdx.x] += t;
             __syncthreads();
         }
-        if (i < npairs) slot_off[i] = carry + sv[threadIdx.x] - v;
+        int run = carry + sv[threadIdx.x] - sum;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            if (i0 + j < npairs) slot_off[i0 + j] = run;
+            run += v[j];
+        }
         __syncthreads();
         if (threadIdx.x == 1023) carry += sv[1023];
         __syncthreads();
@@ -651,7 +664,7 @@ __device__ __forceinline__ void ivf_dot_item(int d, const float *__restrict__ co
                             key = fmaf(-2.f, acc[r][j], qnj + xnr);
                             key = key < 0.f ? 0.f : key;
                         }
-                        lists[j].offer(v ? key : __builtin_inff(), v ? (int)row : 0x7fffffff, k - 1);
+                        lists[j].template offer<false>(v ? key : __builtin_inff(), v ? (int)row : 0x7fffffff, k - 1);
                         acc[r][j] = 0.f;
                     }
                 }

@@ -19,6 +19,7 @@
 namespace hipann {
 
 constexpr int kWave = 64;
+constexpr int kBulkOffer = 12;  // WaveList<1>::offer: more entrants than this → sort + bulk merge
 
 template <typename IdT>
 __device__ __forceinline__ bool lex_less(float ad, IdT aid, float bd, IdT bid) {
@@ -131,12 +132,25 @@ struct WaveList {
     }
 
     // Offer 64 per-lane candidates (one per lane, any order).  `kth` = k-1.  Candidates whose key is
-    // +inf with the padding id never enter.
+    // +inf with the padding id never enter.  BULK = false keeps the serial insert only (smaller code,
+    // for kernels at a register budget edge).
+    template <bool BULK = true>
     __device__ __forceinline__ void offer(float cd, IdT cid, int kth) {
         float td; IdT tid;
         threshold(kth, td, tid);
         bool pass = lex_less(cd, cid, td, tid);
         unsigned long long m = __ballot(pass);
+        if constexpr (S == 1 && BULK) {
+            // many entrants (an empty list, the first tiles of a scan): one bitonic sort of the
+            // passing candidates + a bulk merge instead of one serial insert each
+            if (__popcll(m) > kBulkOffer) {
+                float ck = pass ? cd : __builtin_inff();
+                IdT ci = pass ? cid : IdTraits<IdT>::pad();
+                wave_sort(ck, ci);
+                merge_sorted(ck, ci);
+                return;
+            }
+        }
         while (m) {
             const int j = __ffsll((unsigned long long)m) - 1;
             m &= m - 1;

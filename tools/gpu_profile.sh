@@ -11,6 +11,6 @@ mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/stats" -o run -- \
     python3 "$root/bench.py" --workload "$wl" --no-cpu-baseline "$@" > "$out/stats.log" 2>&1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/pmc" -o run -- \
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$kern" --output-format csv -d "$out/pmc" -o run -- \
     python3 "$root/bench.py" --workload "$wl" --no-cpu-baseline "$@" > "$out/pmc.log" 2>&1
 python3 "$root/tools/pmc_traffic.py" "$out/pmc" "$kern" --skip 3 --out "$root/gpurun_out/pmc_$wl.json"
