@@ -44,9 +44,12 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", choices=["flat", "ivf"], default=os.environ.get("HIPANN_BENCH_WORKLOAD", "ivf"))
-    p.add_argument("--n", type=int, default=10_000_000)
-    p.add_argument("--d", type=int, default=768)
+    p.add_argument("--workload", choices=["flat", "ivf", "diskann"],
+                   default=os.environ.get("HIPANN_BENCH_WORKLOAD", "ivf"))
+    p.add_argument("--n", type=int, default=None, help="rows (10M; 1M for diskann)")
+    p.add_argument("--d", type=int, default=None, help="dimension (768; 1536 for diskann)")
+    p.add_argument("--l-search", type=int, default=128, help="diskann L_search")
+    p.add_argument("--degree", type=int, default=64, help="diskann graph degree R")
     p.add_argument("--nq", type=int, default=1024)
     p.add_argument("--k", type=int, default=10)
     p.add_argument("--nlist", type=int, default=1024)
@@ -54,7 +57,12 @@ def parse():
     p.add_argument("--metric", choices=["l2", "ip"], default="l2")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU sample duration")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.n is None:
+        a.n = 1_000_000 if a.workload == "diskann" else 10_000_000
+    if a.d is None:
+        a.d = 1536 if a.workload == "diskann" else 768
+    return a
 
 
 CHUNK = 125_000  # generation granularity (divides 10M / {1,2,4,8})
@@ -145,6 +153,9 @@ def main():
 
     n, d, nq, k = args.n, args.d, args.nq, args.k
     metric = 0 if args.metric == "l2" else 1
+    if args.workload == "diskann":
+        run_diskann(args, torch, dist, hipann, rank, world, dev)
+        return
     from sharded import shard_bounds
     lo, hi = shard_bounds(n, rank, world)
     n_local = hi - lo
@@ -323,6 +334,142 @@ def main():
         }
         if extra:
             line["ivf"] = {kk: v for kk, v in extra.items() if kk != "scan_bytes_per_batch_local"}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def run_diskann(args, torch, dist, hipann, rank, world, dev):
+    """C4 (SURVEY §8d): DiskProvider::search_batch over 1M x 1536 SQ8, L_search=128, R=64, nq=1024.
+
+    Graph traversal does not shard, so N GPUs run N replicas (each holds the whole SQ8 DB and answers
+    its own 1024-query batch; weak scaling, no collective).  A step = one lock-step BFS batch through
+    diskann_hip_search_batch (host BFS, every step's distances on the GPU by the id-gather kernel).
+    Roofline: the SQ8 id-gather kernel, algorithmic bytes per distance = d (codes) + 4 (id) +
+    4 (query_map) + 4 (out), summed over the timed launches."""
+    import diskann_build as DB
+
+    n, d, nq, k, L, R = args.n, args.d, args.nq, args.k, args.l_search, args.degree
+    metric = 0 if args.metric == "l2" else 1
+    t_setup = time.perf_counter()
+    gc = torch.Generator(device=dev)
+    gc.manual_seed(8)
+    r_dim = int(os.environ.get("HIPANN_DISKANN_RANK", "16"))
+    eta = float(os.environ.get("HIPANN_DISKANN_NOISE", "0.02"))
+    basis = lowrank_basis(torch, r_dim, d, gc)
+    xb = torch.empty((n, d), device=dev, dtype=torch.float32)
+    gen_lowrank_rows(torch, xb, 0, basis, eta, 42)
+    xq = torch.empty((nq, d), device=dev, dtype=torch.float32)
+    gen_lowrank_rows(torch, xq, 0, basis, eta, 4242 + rank)
+    codes, mins, scale = DB.sq8_encode(torch, xb)
+    adj_t, medoid = DB.knn_graph(torch, xb, R=R, n_random=R // 4, seed=8)
+    torch.cuda.synchronize()
+    t_graph = time.perf_counter() - t_setup
+    adj = DB.adjacency_u32(torch, adj_t)
+    del adj_t
+    codes_h = codes.cpu().numpy()
+    db = hipann.DiskannDeviceDB(codes_h, hipann.DiskannDeviceDB.FMT_SQ8, mins.cpu().numpy(), scale.cpu().numpy())
+    del codes
+    torch.cuda.empty_cache()
+    xq_h = xq.cpu().numpy()
+    eps = np.array([medoid], np.uint32)
+    setup_s = time.perf_counter() - t_setup
+
+    def step():
+        return db.search_batch(adj, eps, xq_h, k, L, metric)
+
+    for _ in range(args.warmup):
+        step()
+    db.set_kernel_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    evals = 0
+    bfs_steps = []
+    for _ in range(args.steps):
+        ids, dd, st = step()
+        evals += st["evals"]
+        bfs_steps.append(st["steps"])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_total_ms, launches = db.kernel_stats()
+    db.set_kernel_timing(False)
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    qps = world * nq * args.steps / elapsed
+
+    gt = DB.exact_topk(torch, xb, xq, k, metric).cpu().numpy()
+    recall = float(np.mean([len(set(ids[i]) & set(gt[i])) / k for i in range(nq)]))
+    bytes_per_eval = d + 12
+    achieved = evals * bytes_per_eval / (kern_total_ms * 1e-3) / 1e9 if kern_total_ms > 0 else 0.0
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "dist_ids_sq8",
+            "kernel_ms_per_launch": round(kern_total_ms / max(launches, 1), 4),
+            "kernel_ms_per_batch": round(kern_total_ms / args.steps, 3),
+            "launches_per_batch": launches / args.steps,
+            "distances_per_batch": evals // args.steps,
+            "algorithmic": f"distances x (d + 12) B = {bytes_per_eval} B per distance (SQ8 code row + id + "
+                           f"query_map + out), summed over the timed launches"}
+    tb, tsrc = pmc_traffic("diskann", "dist_ids_sq8")
+    if tb is not None and world == 1:
+        roof["traffic"] = round(tb / 1e9, 4)
+        roof["traffic_unit"] = "GB per launch (PMC FETCH_SIZE)"
+        roof["traffic_source"] = tsrc
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            from oracle import oracle as O
+            c_h = codes_h
+            m_h, s_h = mins.cpu().numpy(), scale.cpu().numpy()
+            s0 = 16
+            t1 = time.perf_counter()
+            O.diskann_search_batch(adj, eps, xq_h[:s0], k, L, metric, codes=c_h, mins=m_h, scale=s_h)
+            dt0 = time.perf_counter() - t1
+            s1 = int(min(nq, max(s0, s0 * args.cpu_seconds / max(dt0, 1e-3))))
+            t1 = time.perf_counter()
+            O.diskann_search_batch(adj, eps, xq_h[:s1], k, L, metric, codes=c_h, mins=m_h, scale=s_h)
+            dt = time.perf_counter() - t1
+            cpu = {"value": round(s1 / dt, 2), "unit": "queries/s", "cores": O.num_threads(), "kind": "port",
+                   "sample": f"first {s1} of {nq} queries ({dt:.1f} s) through the C oracle's "
+                             f"DiskProvider::search_batch restatement (lock-step BFS on the host, SQ8 "
+                             f"distances OpenMP over each step's candidates) on the same graph and codes"}
+        except Exception as e:
+            log(f"[bench] cpu baseline failed: {e!r}")
+            cpu = {"value": None, "error": repr(e)}
+
+    if rank == 0:
+        line = {
+            "metric": "queries/sec @ recall@10>=0.95 (DiskANN DiskProvider batch path, 1Mx1536 sq8, L_search=128)",
+            "value": round(qps, 1),
+            "unit": "queries/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8 codes, f32 accumulate",
+            "data": f"synthetic (generated on device: low-rank gaussian rows, intrinsic dim {r_dim}, noise {eta}; "
+                    f"SQ8-encoded; graph = {R - R // 4} exact cell-local nearest neighbours + {R // 4} random "
+                    f"edges, medoid entry point)",
+            "config": {"workload": f"DISKANN DiskProvider batch-distance, {n // 1_000_000}Mx{d} sq8, "
+                                   f"L_search={L}, R={R}, batch={nq}, k={k}",
+                       "global_batch": nq * world, "n": n, "d": d, "k": k,
+                       "parallelism": f"replicas{world}"},
+            "recall_at_10": recall,
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "setup_s": round(setup_s, 1),
+            "diskann": {"graph_build_s": round(t_graph, 1), "bfs_steps_per_batch": int(np.mean(bfs_steps)),
+                        "bfs_threads": int(os.environ.get("HIPANN_BFS_THREADS", "16"))},
+        }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -25,8 +25,10 @@
 #include <algorithm>
 #include <cfloat>
 #include <cstring>
-#include <queue>
-#include <unordered_set>
+#include <atomic>
+#include <cstdlib>
+#include <functional>
+#include <thread>
 #include <vector>
 
 namespace hipann {
@@ -77,12 +79,14 @@ __global__ void __launch_bounds__(256) dist_rows(const float *__restrict__ queri
 template <bool IP, bool VEC4>
 __global__ void __launch_bounds__(256) dist_ids_f32(const float *__restrict__ queries, const float *__restrict__ db,
                                                     const unsigned *__restrict__ ids, const unsigned *__restrict__ qmap,
-                                                    int total_n, int d, float *__restrict__ out) {
+                                                    int total_n, int d, int64_t n, float *__restrict__ out) {
     const int lane = threadIdx.x & 63;
     const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (w >= total_n) return;
+    const unsigned id = ids[w];
+    if (id >= n) return;  // empty slot of the BFS's fixed per-query layout
     const float *q = queries + (int64_t)qmap[w] * d;
-    const float *c = db + (int64_t)ids[w] * d;
+    const float *c = db + (int64_t)id * d;
     float s = 0.f;
     if (VEC4) {
         const float4 *q4 = reinterpret_cast<const float4 *>(q);
@@ -116,17 +120,18 @@ template <bool IP>
 __global__ void __launch_bounds__(256) dist_ids_sq8(const float *__restrict__ queries, const uint8_t *__restrict__ codes,
                                                     const float2 *__restrict__ ab_g, const unsigned *__restrict__ ids,
                                                     const unsigned *__restrict__ qmap, int total_n, int d,
-                                                    float *__restrict__ out) {
+                                                    int64_t n, float *__restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) float2 ab[];
     for (int j = threadIdx.x; j < d; j += 256) ab[j] = ab_g[j];
     __syncthreads();
     const int hl = threadIdx.x & 31;
     const int64_t c = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
-    const bool valid = c < total_n;
+    const unsigned id = c < total_n ? ids[c] : 0xffffffffu;
+    const bool valid = id < n;  // also skips empty slots of the BFS's fixed per-query layout
     float s = 0.f;
     if (valid) {
         const float *q = queries + (int64_t)qmap[c] * d;
-        const uint8_t *row = codes + (int64_t)ids[c] * d;
+        const uint8_t *row = codes + (int64_t)id * d;
         for (int j0 = hl * 16; j0 < d; j0 += 32 * 16) {
             const uint4 raw = *reinterpret_cast<const uint4 *>(row + j0);
             const unsigned wv[4] = {raw.x, raw.y, raw.z, raw.w};
@@ -155,12 +160,14 @@ __global__ void __launch_bounds__(256) dist_ids_sq8_scalar(const float *__restri
                                                            const uint8_t *__restrict__ codes,
                                                            const float2 *__restrict__ ab, const unsigned *__restrict__ ids,
                                                            const unsigned *__restrict__ qmap, int total_n, int d,
-                                                           float *__restrict__ out) {
+                                                           int64_t n, float *__restrict__ out) {
     const int lane = threadIdx.x & 63;
     const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (w >= total_n) return;
+    const unsigned id = ids[w];
+    if (id >= n) return;
     const float *q = queries + (int64_t)qmap[w] * d;
-    const uint8_t *row = codes + (int64_t)ids[w] * d;
+    const uint8_t *row = codes + (int64_t)id * d;
     float s = 0.f;
     for (int j = lane; j < d; j += 64) {
         const float2 p = ab[j];
@@ -248,11 +255,11 @@ void launch_ids(DiskDB &db, const float *q, const unsigned *ids, const unsigned 
         const bool v4 = (d % 4 == 0) && ((uintptr_t)q % 16 == 0);
         dim3 grid((unsigned)ceil_div(total_n, 4)), block(256);
         if (metric == kIP) {
-            if (v4) hipLaunchKernelGGL((dist_ids_f32<true, true>), grid, block, 0, st, q, x, ids, m, total_n, d, out);
-            else hipLaunchKernelGGL((dist_ids_f32<true, false>), grid, block, 0, st, q, x, ids, m, total_n, d, out);
+            if (v4) hipLaunchKernelGGL((dist_ids_f32<true, true>), grid, block, 0, st, q, x, ids, m, total_n, d, db.n, out);
+            else hipLaunchKernelGGL((dist_ids_f32<true, false>), grid, block, 0, st, q, x, ids, m, total_n, d, db.n, out);
         } else {
-            if (v4) hipLaunchKernelGGL((dist_ids_f32<false, true>), grid, block, 0, st, q, x, ids, m, total_n, d, out);
-            else hipLaunchKernelGGL((dist_ids_f32<false, false>), grid, block, 0, st, q, x, ids, m, total_n, d, out);
+            if (v4) hipLaunchKernelGGL((dist_ids_f32<false, true>), grid, block, 0, st, q, x, ids, m, total_n, d, db.n, out);
+            else hipLaunchKernelGGL((dist_ids_f32<false, false>), grid, block, 0, st, q, x, ids, m, total_n, d, db.n, out);
         }
     } else {
         const uint8_t *x = db.data.get<uint8_t>();
@@ -260,12 +267,12 @@ void launch_ids(DiskDB &db, const float *q, const unsigned *ids, const unsigned 
         if (d % 16 == 0 && (uintptr_t)q % 16 == 0 && d * sizeof(float2) <= 64 * 1024) {
             dim3 grid((unsigned)ceil_div(total_n, 8)), block(256);
             const size_t smem = (size_t)d * sizeof(float2);
-            if (metric == kIP) hipLaunchKernelGGL(dist_ids_sq8<true>, grid, block, smem, st, q, x, ab, ids, m, total_n, d, out);
-            else hipLaunchKernelGGL(dist_ids_sq8<false>, grid, block, smem, st, q, x, ab, ids, m, total_n, d, out);
+            if (metric == kIP) hipLaunchKernelGGL(dist_ids_sq8<true>, grid, block, smem, st, q, x, ab, ids, m, total_n, d, db.n, out);
+            else hipLaunchKernelGGL(dist_ids_sq8<false>, grid, block, smem, st, q, x, ab, ids, m, total_n, d, db.n, out);
         } else {
             dim3 grid((unsigned)ceil_div(total_n, 4)), block(256);
-            if (metric == kIP) hipLaunchKernelGGL(dist_ids_sq8_scalar<true>, grid, block, 0, st, q, x, ab, ids, m, total_n, d, out);
-            else hipLaunchKernelGGL(dist_ids_sq8_scalar<false>, grid, block, 0, st, q, x, ab, ids, m, total_n, d, out);
+            if (metric == kIP) hipLaunchKernelGGL(dist_ids_sq8_scalar<true>, grid, block, 0, st, q, x, ab, ids, m, total_n, d, db.n, out);
+            else hipLaunchKernelGGL(dist_ids_sq8_scalar<false>, grid, block, 0, st, q, x, ab, ids, m, total_n, d, db.n, out);
         }
     }
     HIPANN_CHECK(hipGetLastError());
@@ -301,21 +308,132 @@ size_t rust_binary_search(const std::vector<Cand> &res, float dist) {
     return base + (p < dist ? 1 : 0);
 }
 
-struct QState {
-    std::unordered_set<uint32_t> visited;
-    std::priority_queue<Cand, std::vector<Cand>, CandGreater> cands;
-    std::vector<Cand> result;
-    bool active = true;
+// Visited set: open addressing over u32 ids (linear probing, power-of-two capacity, load ≤ 1/2).
+// Same membership semantics as the reference's hashbrown::HashSet<u32>; only speed differs.
+struct VisitedSet {
+    std::vector<uint32_t> slot;  // kEmpty = unused
+    uint32_t mask = 0;
+    size_t count = 0;
+    static constexpr uint32_t kEmpty = 0xffffffffu;
+    void init(size_t expect) {
+        size_t cap = 64;
+        while (cap < 2 * expect) cap <<= 1;
+        slot.assign(cap, kEmpty);
+        mask = (uint32_t)(cap - 1);
+        count = 0;
+    }
+    static uint32_t hash(uint32_t v) { return (v * 0x9E3779B1u) ^ (v >> 15); }
+    // Returns true if v was newly inserted (HashSet::insert).  v == kEmpty is stored out of band.
+    bool insert(uint32_t v) {
+        if (v == kEmpty) {
+            const bool fresh = !has_max;
+            has_max = true;
+            return fresh;
+        }
+        if (2 * (count + 1) > slot.size()) grow();
+        uint32_t i = hash(v) & mask;
+        for (;;) {
+            const uint32_t x = slot[i];
+            if (x == v) return false;
+            if (x == kEmpty) { slot[i] = v; ++count; return true; }
+            i = (i + 1) & mask;
+        }
+    }
+    bool has_max = false;
+
+  private:
+    void grow() {
+        std::vector<uint32_t> old;
+        old.swap(slot);
+        slot.assign(old.size() * 2, kEmpty);
+        mask = (uint32_t)(slot.size() - 1);
+        for (uint32_t v : old) {
+            if (v == kEmpty) continue;
+            uint32_t i = hash(v) & mask;
+            while (slot[i] != kEmpty) i = (i + 1) & mask;
+            slot[i] = v;
+        }
+    }
 };
 
-// insert_result (disk_provider.rs:656-678)
+struct QState {
+    VisitedSet visited;
+    std::vector<Cand> cands;  // binary min-heap on (d, id) (CandGreater): BinaryHeap<Reverse<..>>
+    std::vector<Cand> result;  // sorted by d, at most l entries
+    bool active = true;
+    int nnew = 0;  // candidates this query put into the current lock-step batch
+};
+
+// insert_result (disk_provider.rs:656-678).  (d, id) pairs in `cands` are unique (ids pass the
+// visited set once), so any binary heap pops them in the same order as Rust's BinaryHeap.
 void insert_result(QState &s, size_t l, float dist, uint32_t nb) {
     if (s.result.size() < l || dist < s.result.back().d) {
         const size_t pos = rust_binary_search(s.result, dist);
         s.result.insert(s.result.begin() + (ptrdiff_t)pos, Cand{dist, nb});
         if (s.result.size() > l) s.result.resize(l);
-        s.cands.push(Cand{dist, nb});
+        s.cands.push_back(Cand{dist, nb});
+        std::push_heap(s.cands.begin(), s.cands.end(), CandGreater());
     }
+}
+
+// Fork-join pool for the per-step host phases of the lock-step BFS: the calling thread is worker 0,
+// the others spin on a generation counter (the phases are ~0.1 ms apart, too short for a futex
+// round trip) and exit when the search returns.
+class SpinPool {
+  public:
+    explicit SpinPool(int nthreads) : n_(nthreads < 1 ? 1 : nthreads) {
+        for (int t = 1; t < n_; ++t) th_.emplace_back([this, t] { worker(t); });
+    }
+    ~SpinPool() {
+        stop_.store(true, std::memory_order_release);
+        gen_.fetch_add(1, std::memory_order_acq_rel);
+        for (auto &t : th_) t.join();
+    }
+    int size() const { return n_; }
+    // Runs fn(tid) on every worker and returns when all have finished.  Exceptions must not escape fn.
+    template <typename F> void run(F &&fn) {
+        if (n_ == 1) { fn(0); return; }
+        std::function<void(int)> job(fn);
+        job_ = &job;
+        pending_.store(n_ - 1, std::memory_order_release);
+        gen_.fetch_add(1, std::memory_order_acq_rel);
+        fn(0);
+        while (pending_.load(std::memory_order_acquire) != 0) spin_pause();
+        job_ = nullptr;
+    }
+
+  private:
+    static void spin_pause() { __builtin_ia32_pause(); }
+    void worker(int tid) {
+        uint64_t seen = 0;
+        for (;;) {
+            uint64_t g;
+            int idle = 0;
+            while ((g = gen_.load(std::memory_order_acquire)) == seen) {
+                spin_pause();
+                if (++idle > 4096) { std::this_thread::yield(); idle = 0; }
+            }
+            seen = g;
+            if (stop_.load(std::memory_order_acquire)) return;
+            (*job_)(tid);
+            pending_.fetch_sub(1, std::memory_order_acq_rel);
+        }
+    }
+    int n_;
+    std::vector<std::thread> th_;
+    std::atomic<uint64_t> gen_{0};
+    std::atomic<int> pending_{0};
+    std::atomic<bool> stop_{false};
+    std::function<void(int)> *job_ = nullptr;
+};
+
+int bfs_threads(int nq) {
+    int t = 16;  // the GPU box's CPU share per GPU
+    if (const char *e = std::getenv("HIPANN_BFS_THREADS")) t = std::atoi(e);
+    const int hw = (int)std::thread::hardware_concurrency();
+    if (hw > 0) t = std::min(t, hw);
+    t = std::min(t, std::max(1, nq / 16));  // ≥ 16 queries per thread
+    return std::max(1, t);
 }
 
 }  // namespace
@@ -474,6 +592,32 @@ int diskann_hip_multi_batch_distances_ids_device(void *h, const float *queries_d
 
 int64_t diskann_hip_db_size(void *h) { return h ? static_cast<DiskDB *>(h)->n : -1; }
 
+int diskann_hip_set_kernel_timing(void *h, int on) {
+    if (!h) return -1;
+    auto *db = static_cast<DiskDB *>(h);
+    try {
+        std::lock_guard<std::mutex> lk(db->mu);
+        db->timer.reset(on != 0, db->device);
+        return 0;
+    } catch (...) {
+        return -1;
+    }
+}
+
+int diskann_hip_kernel_stats(void *h, double *total_ms, int64_t *launches) {
+    if (!h || !total_ms || !launches) return -1;
+    auto *db = static_cast<DiskDB *>(h);
+    try {
+        std::lock_guard<std::mutex> lk(db->mu);
+        DeviceGuard g(db->device);
+        *launches = (int64_t)db->timer.used;
+        *total_ms = db->timer.average_ms() * (double)db->timer.used;
+        return 0;
+    } catch (...) {
+        return -1;
+    }
+}
+
 void diskann_hip_release_db(void *h) {
     if (!h) return;
     try {
@@ -505,10 +649,15 @@ int diskann_hip_search_batch(void *h, const uint32_t *adj, int R, const uint32_t
         }
         const size_t l = (size_t)std::max(l_search, k);
         const hipStream_t st = db->stream;
-        // queries resident for the whole search
+        // Fixed per-query slot layout: query qi owns slots [qi*S, qi*S + S) of every lock-step batch,
+        // S = max(R, n_ep); unused slots hold UINT32_MAX and the kernel skips them.  The query map is
+        // therefore constant (uploaded once) and the host phases run per query in parallel with no
+        // compaction step.  Per query the candidate order is the reference's (neighbour order).
+        const size_t S = (size_t)std::max(R, n_ep);
+        const size_t cap = (size_t)nq * S;
+        HIPANN_REQUIRE(cap <= (size_t)INT32_MAX, "nq * max(R, n_ep) exceeds INT32_MAX");
         db->q.ensure((size_t)nq * dim * 4 + 16, db->device);
         HIPANN_CHECK(hipMemcpyAsync(db->q.p, queries, (size_t)nq * dim * 4, hipMemcpyHostToDevice, st));
-        const size_t cap = (size_t)nq * std::max(R, n_ep);
         db->ids.ensure(cap * 4, db->device);
         db->m.ensure(cap * 4, db->device);
         db->out.ensure(cap * 4, db->device);
@@ -518,70 +667,136 @@ int diskann_hip_search_batch(void *h, const uint32_t *adj, int R, const uint32_t
         uint32_t *hid = db->hids.get<uint32_t>();
         uint32_t *hm = db->hm.get<uint32_t>();
         float *hout = db->hout.get<float>();
-        auto gpu_dists = [&](size_t tot) {
-            HIPANN_CHECK(hipMemcpyAsync(db->ids.p, hid, tot * 4, hipMemcpyHostToDevice, st));
-            HIPANN_CHECK(hipMemcpyAsync(db->m.p, hm, tot * 4, hipMemcpyHostToDevice, st));
-            launch_ids(*db, db->q.get<float>(), db->ids.get<unsigned>(), db->m.get<unsigned>(), (int)tot, metric,
-                       db->out.get<float>(), st);
-            HIPANN_CHECK(hipMemcpyAsync(hout, db->out.p, tot * 4, hipMemcpyDeviceToHost, st));
+        for (size_t i = 0; i < cap; ++i) hm[i] = (uint32_t)(i / S);
+        HIPANN_CHECK(hipMemcpyAsync(db->m.p, hm, cap * 4, hipMemcpyHostToDevice, st));
+        // Only the slot prefix up to the last query with work is shipped each step.
+        auto gpu_dists = [&](size_t span) {
+            HIPANN_CHECK(hipMemcpyAsync(db->ids.p, hid, span * 4, hipMemcpyHostToDevice, st));
+            {
+                ScopedTiming tm(db->timer, st);
+                launch_ids(*db, db->q.get<float>(), db->ids.get<unsigned>(), db->m.get<unsigned>(), (int)span, metric,
+                           db->out.get<float>(), st);
+            }
+            HIPANN_CHECK(hipMemcpyAsync(hout, db->out.p, span * 4, hipMemcpyDeviceToHost, st));
             HIPANN_CHECK(hipStreamSynchronize(st));
-            nevals += (int64_t)tot;
             ncalls++;
         };
-        std::vector<QState> S((size_t)nq);
+        std::vector<QState> Sq((size_t)nq);
+        SpinPool pool(bfs_threads(nq));
+        const int T = pool.size();
+        auto chunk = [&](int t, int &q0, int &q1) {
+            q0 = (int)((int64_t)nq * t / T);
+            q1 = (int)((int64_t)nq * (t + 1) / T);
+        };
+        // per-thread reductions: [0] active queries, [1] distances, [2] last query with work + 1
+        std::vector<int64_t> red((size_t)T * 3 * 8, 0);  // padded against false sharing
+        auto reduce = [&](int j) {
+            int64_t v = 0;
+            for (int t = 0; t < T; ++t) v = (j == 2) ? std::max(v, red[(size_t)t * 24 + j]) : v + red[(size_t)t * 24 + j];
+            return v;
+        };
         // seed entry points (disk_provider.rs:524-538)
-        {
-            size_t tot = 0;
-            for (int qi = 0; qi < nq; ++qi) {
-                S[qi].visited.reserve(l * 2);
+        pool.run([&](int t) {
+            int q0, q1;
+            chunk(t, q0, q1);
+            int64_t tot = 0, last = 0;
+            for (int qi = q0; qi < q1; ++qi) {
+                QState &s = Sq[qi];
+                s.visited.init(std::max<size_t>(l * 2, 1024));
+                s.cands.reserve(l * 2);
+                s.result.reserve(l + 1);
+                uint32_t *slot = hid + (size_t)qi * S;
+                int cnt = 0;
                 for (int e = 0; e < n_ep; ++e) {
                     const uint32_t ep = eps[e];
-                    if (S[qi].visited.insert(ep).second && ep < N) {
-                        hid[tot] = ep;
-                        hm[tot] = (uint32_t)qi;
-                        tot++;
-                    }
+                    if (s.visited.insert(ep) && ep < N) slot[cnt++] = ep;
                 }
+                for (size_t j = (size_t)cnt; j < S; ++j) slot[j] = 0xffffffffu;
+                s.nnew = cnt;
+                tot += cnt;
+                if (cnt) last = qi + 1;
             }
-            if (tot) gpu_dists(tot);
-            for (size_t i = 0; i < tot; ++i) {
-                QState &s = S[hm[i]];
-                s.cands.push(Cand{hout[i], hid[i]});
-                s.result.push_back(Cand{hout[i], hid[i]});
-            }
-            for (auto &s : S)
-                std::stable_sort(s.result.begin(), s.result.end(), [](const Cand &a, const Cand &b) { return a.d < b.d; });
+            red[(size_t)t * 24 + 1] = tot;
+            red[(size_t)t * 24 + 2] = last;
+        });
+        if (reduce(1)) {
+            gpu_dists((size_t)reduce(2) * S);
+            nevals += reduce(1);
         }
-        for (;;) {
-            int active = 0;
-            for (auto &s : S) active += s.active ? 1 : 0;
-            if (!active) break;
-            nsteps++;
-            size_t tot = 0;
-            for (int qi = 0; qi < nq; ++qi) {
-                QState &s = S[qi];
-                if (!s.active) continue;
-                if (s.cands.empty()) { s.active = false; continue; }
-                const Cand c = s.cands.top();
-                s.cands.pop();
-                if (s.result.size() >= l && c.d > s.result[l - 1].d) { s.active = false; continue; }
-                const uint32_t *nbr = adj + (size_t)c.id * R;
-                for (int r = 0; r < R; ++r) {
-                    const uint32_t nb = nbr[r];
-                    if (nb == 0xffffffffu) break;
-                    if (nb >= N) continue;
-                    if (!s.visited.insert(nb).second) continue;
-                    hid[tot] = nb;
-                    hm[tot] = (uint32_t)qi;
-                    tot++;
+        pool.run([&](int t) {
+            int q0, q1;
+            chunk(t, q0, q1);
+            for (int qi = q0; qi < q1; ++qi) {
+                QState &s = Sq[qi];
+                const uint32_t *slot = hid + (size_t)qi * S;
+                const float *dd = hout + (size_t)qi * S;
+                for (int j = 0; j < s.nnew; ++j) {
+                    s.cands.push_back(Cand{dd[j], slot[j]});
+                    std::push_heap(s.cands.begin(), s.cands.end(), CandGreater());
+                    s.result.push_back(Cand{dd[j], slot[j]});
                 }
+                std::stable_sort(s.result.begin(), s.result.end(), [](const Cand &x, const Cand &y) { return x.d < y.d; });
             }
+        });
+        // Lock-step iterations (disk_provider.rs:545-652).  One fork-join per step: the insert phase of
+        // step s (results of its GPU call) and the pop/expand phase of step s+1 run back to back per query.
+        bool first = true;
+        for (;;) {
+            pool.run([&](int t) {
+                int q0, q1;
+                chunk(t, q0, q1);
+                int64_t head = 0, tot = 0, last = 0;
+                for (int qi = q0; qi < q1; ++qi) {
+                    QState &s = Sq[qi];
+                    uint32_t *slot = hid + (size_t)qi * S;
+                    if (!first) {
+                        const float *dd = hout + (size_t)qi * S;
+                        for (int j = 0; j < s.nnew; ++j) insert_result(s, l, dd[j], slot[j]);
+                    }
+                    const int prev = s.nnew;  // slots >= prev are already empty
+                    s.nnew = 0;
+                    head += s.active ? 1 : 0;  // the reference's loop-head active count
+                    if (s.active) {
+                        if (s.cands.empty()) {
+                            s.active = false;
+                        } else {
+                            std::pop_heap(s.cands.begin(), s.cands.end(), CandGreater());
+                            const Cand c = s.cands.back();
+                            s.cands.pop_back();
+                            if (s.result.size() >= l && c.d > s.result[l - 1].d) {
+                                s.active = false;
+                            } else {
+                                const uint32_t *nbr = adj + (size_t)c.id * R;
+                                int cnt = 0;
+                                for (int r = 0; r < R; ++r) {
+                                    const uint32_t nb = nbr[r];
+                                    if (nb == 0xffffffffu) break;  // get_neighbors trims at the first sentinel
+                                    if (nb >= N) continue;
+                                    if (!s.visited.insert(nb)) continue;
+                                    slot[cnt++] = nb;
+                                }
+                                s.nnew = cnt;
+                            }
+                        }
+                    }
+                    for (int j = s.nnew; j < prev; ++j) slot[j] = 0xffffffffu;
+                    tot += s.nnew;
+                    if (s.nnew) last = qi + 1;
+                }
+                red[(size_t)t * 24 + 0] = head;
+                red[(size_t)t * 24 + 1] = tot;
+                red[(size_t)t * 24 + 2] = last;
+            });
+            first = false;
+            const int64_t head = reduce(0), tot = reduce(1);
+            if (!head) break;  // no active query at the loop head
+            nsteps++;
             if (!tot) continue;
-            gpu_dists(tot);
-            for (size_t i = 0; i < tot; ++i) insert_result(S[hm[i]], l, hout[i], hid[i]);
+            gpu_dists((size_t)reduce(2) * S);
+            nevals += tot;
         }
         for (int qi = 0; qi < nq; ++qi) {
-            const auto &r = S[qi].result;
+            const auto &r = Sq[qi].result;
             for (int j = 0; j < k; ++j) {
                 if ((size_t)j < r.size()) {
                     out_ids[(size_t)qi * k + j] = r[j].id;

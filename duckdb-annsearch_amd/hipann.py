@@ -115,6 +115,8 @@ def lib() -> C.CDLL:
             "diskann_hip_multi_batch_distances_ids_device": ([vp, vp, i32, vp, vp, i32, i32, vp, vp], i32),
             "diskann_hip_db_size": ([vp], i64),
             "diskann_hip_release_db": ([vp], None),
+            "diskann_hip_set_kernel_timing": ([vp, i32], i32),
+            "diskann_hip_kernel_stats": ([vp, C.POINTER(C.c_double), i64p], i32),
             "diskann_hip_search_batch": ([vp, C.POINTER(C.c_uint32), i32, C.POINTER(C.c_uint32), i32, f, i32, i32,
                                           i32, i32, i64p, f, i64p, cp, i32], i32),
         }
@@ -518,6 +520,18 @@ class DiskannDeviceDB:
         if rc != 0:
             raise HipAnnError("diskann_hip_multi_batch_distances_ids failed")
         return out
+
+    def set_kernel_timing(self, on: bool) -> None:
+        """Record HIP events around every id-gather launch from now on (resets the record)."""
+        if lib().diskann_hip_set_kernel_timing(self._h, 1 if on else 0) != 0:
+            raise HipAnnError("diskann_hip_set_kernel_timing failed")
+
+    def kernel_stats(self) -> Tuple[float, int]:
+        """(summed kernel ms, launches) since set_kernel_timing(True)."""
+        ms, n = C.c_double(0.0), C.c_int64(0)
+        if lib().diskann_hip_kernel_stats(self._h, C.byref(ms), C.byref(n)) != 0:
+            raise HipAnnError("diskann_hip_kernel_stats failed")
+        return ms.value, n.value
 
     def search_batch(self, adjacency: np.ndarray, entry_points, queries, k: int, l_search: int,
                      metric: int = METRIC_L2):

@@ -88,6 +88,11 @@ int diskann_hip_search_batch(void *db, const uint32_t *adjacency, int R, const u
                              float *out_dists, int64_t *stats, char *err_buf, int err_len);
 
 int64_t diskann_hip_db_size(void *db);
+
+/* Measurement: record HIP events around every id-gather kernel launch of `db` (on its stream) from now
+ * on (on != 0; resets the record), and read back the summed kernel time and the launch count. */
+int diskann_hip_set_kernel_timing(void *db, int on);
+int diskann_hip_kernel_stats(void *db, double *total_ms, int64_t *launches);
 void diskann_hip_release_db(void *db);
 
 #ifdef __cplusplus

@@ -184,3 +184,41 @@ def test_bfs_from_diskann_file(gpu, oracle, tmp_path):
     oi, od, ost = oracle.diskann_search_batch(f.adjacency, f.entry_points, qs, 10, 40, codes=f.sq8_codes,
                                               mins=f.sq8_min, scale=f.sq8_scale)
     assert (ids == oi).mean() >= 0.99
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+@pytest.mark.parametrize("fmt", [0, 1])
+def test_bfs_many_queries_parallel_host(gpu, oracle, metric, fmt):
+    """nq = 600 spreads the host BFS phases over worker threads (fixed per-query slot layout); a ragged
+    graph (u32::MAX padding after a varying degree, out-of-range ids, duplicate neighbours) and
+    duplicate entry points exercise the visited/skip rules of disk_provider.rs:556-577."""
+    rng = np.random.default_rng(11)
+    n, d, R = 4000, 48, 24
+    x = rng.standard_normal((n, d)).astype(np.float32)
+    qs = (x[rng.integers(0, n, 600)] + 0.1 * rng.standard_normal((600, d))).astype(np.float32)
+    _, nn = oracle.flat_search(x, x, R - 4 + 1, 0)
+    adj = np.full((n, R), 0xFFFFFFFF, np.uint32)
+    adj[:, : R - 4] = nn[:, 1:]
+    adj[:, R - 4: R - 2] = rng.integers(0, n, (n, 2))
+    adj[::7, R - 2] = n + 5          # out of range: skipped, not a sentinel
+    adj[::5, 3] = adj[::5, 2]        # duplicate neighbour
+    deg = rng.integers(R // 2, R + 1, n)
+    adj[np.arange(R)[None, :] >= deg[:, None]] = 0xFFFFFFFF
+    eps = [17, 17, 2500]
+    if fmt == 0:
+        db = gpu.DiskannDeviceDB(x, 0)
+        kw = dict(vecs=x)
+    else:
+        mins, scale = oracle.sq8_train(x)
+        codes = oracle.sq8_encode(x, mins, scale)
+        db = gpu.DiskannDeviceDB(codes, 1, mins, scale)
+        kw = dict(codes=codes, mins=mins, scale=scale)
+    ids, dists, st = db.search_batch(adj, eps, qs, 10, 40, metric)
+    oi, od, ost = oracle.diskann_search_batch(adj, eps, qs, 10, 40, metric, **kw)
+    assert (ids == oi).mean() >= 0.99
+    same = ids == oi
+    assert np.allclose(dists[same], od[same], rtol=1e-5, atol=1e-5)
+    assert abs(st["evals"] - ost["evals"]) <= 0.01 * ost["evals"]
+    assert abs(st["steps"] - ost["steps"]) <= 2
+    # every row sorted ascending (insert_result keeps the list ordered)
+    assert np.all(np.diff(dists, axis=1) >= 0)
