@@ -17,6 +17,7 @@
 #include "wave_topk.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace hipann {
 
@@ -274,6 +275,193 @@ flat_gemm_topk(const float *__restrict__ Q, const float *__restrict__ qnorm, int
 }
 
 // ---------------------------------------------------------------------------------------------
+// flat_gemm_topk2 — the fused path (k ≤ 64) with the selection state out of the register file.
+//
+// Same arithmetic as flat_gemm_topk (v_mfma_f32_32x32x2_f32, K chunks of 32, ‖q‖²+‖x‖²−2q·x clamped,
+// or −q·x), different ownership: wave w owns the 32 query rows [32w, 32w+32) of the 128×128 tile
+// across ALL 128 columns (acc[j], j = column block of 32), so a query's candidates never leave its
+// wave.  Each query's sorted k-list lives in LDS; each lane holds the k-th key of the 16 queries its
+// accumulator rows belong to (thr[r]: row (r&3) + 8(r>>2) + 4·half).  The epilogue compares the 64
+// keys a lane holds with those thresholds straight from the accumulators (no LDS tile); a ballot per
+// accumulator row sends the rare passing rows to the slow path, which loads that query's list into
+// a WaveList, offers the 128 candidates (exact lexicographic admission) and writes it back.
+//
+// Registers ≈ 64 acc + 32 staging + 20 operands + 32 thr/‖q‖² + misc → ≤ 256 → 2 waves per SIMD; LDS
+// = 64 KiB staging (XOR-swizzled, no padding) + 128·k·8 B lists → 2 blocks per CU for k ≤ 16.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int g2_swz(int row, int c4) { return c4 ^ ((row >> 1) & 7); }
+
+__device__ __forceinline__ void g2_stage_store(float *__restrict__ lds, const float4 (&r)[4]) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const int f = t + 256 * p;
+        const int row = f >> 3, c4 = f & 7;
+        *reinterpret_cast<float4 *>(lds + row * GBK + 4 * g2_swz(row, c4)) = r[p];
+    }
+}
+
+size_t gemm2_smem_bytes(int k) { return (size_t)4 * GBM * GBK * sizeof(float) + (size_t)GBM * k * 8; }
+
+template <bool VEC4, bool L2M>
+__global__ void __launch_bounds__(256, 2)
+flat_gemm_topk2(const float *__restrict__ Q, const float *__restrict__ qnorm, int64_t nq,
+                const float *__restrict__ X, const float *__restrict__ xnorm, int64_t N, int d, int k, int nqt,
+                int nsplit, int64_t tiles_per_split, float *__restrict__ part_d, int *__restrict__ part_i) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float *As0 = smem;
+    float *Bs0 = smem + GBM * GBK;
+    float *As1 = smem + 2 * GBM * GBK;
+    float *Bs1 = smem + 3 * GBM * GBK;
+    float *Ld = smem + 4 * GBM * GBK;               // [128][k] keys
+    int *Li = reinterpret_cast<int *>(Ld + GBM * k);  // [128][k] ids
+
+    const int nblocks = nqt * nsplit;
+    const int lb = xcd_remap(blockIdx.x, nblocks);
+    const int qt = lb % nqt;
+    const int split = lb / nqt;
+    const int64_t q0 = (int64_t)qt * GBM;
+    const int64_t ntiles = ceil_div(N, GBN);
+    const int64_t t0 = (int64_t)split * tiles_per_split;
+    const int64_t t1 = t0 + tiles_per_split < ntiles ? t0 + tiles_per_split : ntiles;
+
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int l31 = lane & 31, h = lane >> 5;
+    const int arow = 32 * wave + l31;  // A operand row of this lane
+
+    for (int e = tid; e < GBM * k; e += 256) {
+        Ld[e] = __builtin_inff();
+        Li[e] = 0x7fffffff;
+    }
+    // thresholds / ‖q‖² of the lane's accumulator rows; rows past nq never admit anything
+    float thr[16], qnv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int64_t q = q0 + 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * h;
+        thr[r] = q < nq ? __builtin_inff() : -__builtin_inff();
+        qnv[r] = (L2M && q < nq) ? qnorm[q] : 0.f;
+    }
+    __syncthreads();
+
+    const int nk = (d + GBK - 1) / GBK;
+    float4 sa[4], sb[4];
+    if (t0 < t1) {
+        gemm_stage_load<VEC4>(Q, q0, nq, d, 0, sa);
+        gemm_stage_load<VEC4>(X, t0 * GBN, N, d, 0, sb);
+    }
+
+    for (int64_t t = t0; t < t1; ++t) {
+        const int64_t x0 = t * GBN;
+        g2_stage_store(As0, sa);
+        g2_stage_store(Bs0, sb);
+        float xnv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t x = x0 + 32 * j + l31;
+            xnv[j] = (L2M && x < N) ? xnorm[x] : 0.f;
+        }
+        __syncthreads();
+
+        f32x16 acc[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+
+        for (int kc = 0; kc < nk; ++kc) {
+            const float *Ab = (kc & 1) ? As1 : As0;
+            const float *Bb = (kc & 1) ? Bs1 : Bs0;
+            if (kc + 1 < nk) {
+                gemm_stage_load<VEC4>(Q, q0, nq, d, (kc + 1) * GBK, sa);
+                gemm_stage_load<VEC4>(X, x0, N, d, (kc + 1) * GBK, sb);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const f32x4 a4 = *reinterpret_cast<const f32x4 *>(Ab + arow * GBK + 4 * g2_swz(arow, 4 * h + u));
+                f32x4 b4[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int brow = 32 * j + l31;
+                    b4[j] = *reinterpret_cast<const f32x4 *>(Bb + brow * GBK + 4 * g2_swz(brow, 4 * h + u));
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[e], b4[j][e], acc[j], 0, 0, 0);
+            }
+            if (kc + 1 < nk) {
+                g2_stage_store((kc & 1) ? As0 : As1, sa);
+                g2_stage_store((kc & 1) ? Bs0 : Bs1, sb);
+            }
+            __syncthreads();
+        }
+
+        if (t + 1 < t1) {
+            gemm_stage_load<VEC4>(Q, q0, nq, d, 0, sa);
+            gemm_stage_load<VEC4>(X, (t + 1) * GBN, N, d, 0, sb);
+        }
+
+        // epilogue: keys straight from the accumulators, filtered by the per-row thresholds
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            float key[4];
+            bool any = false;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float ip = acc[j][r];
+                float kv;
+                if (L2M) {
+                    kv = fmaf(-2.f, ip, qnv[r] + xnv[j]);
+                    kv = kv < 0.f ? 0.f : kv;
+                } else {
+                    kv = -ip;
+                }
+                if (x0 + 32 * j + l31 >= N) kv = __builtin_inff();
+                key[j] = kv;
+                any |= kv <= thr[r];
+            }
+            const unsigned long long m = __ballot(any);
+            if (m == 0ull) continue;
+            // slow path (rare after the first tiles): each half of the wave is one query
+#pragma unroll
+            for (int hh = 0; hh < 2; ++hh) {
+                if (((m >> (32 * hh)) & 0xffffffffull) == 0ull) continue;
+                const int ql = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * hh;
+                const int src = 32 * hh + l31;
+                const float c0 = __shfl(key[0], src), c1 = __shfl(key[1], src);
+                const float c2 = __shfl(key[2], src), c3 = __shfl(key[3], src);
+                const float v0 = lane < 32 ? c0 : c1, v1 = lane < 32 ? c2 : c3;
+                const int64_t col0 = x0 + (lane < 32 ? 0 : 32) + l31, col1 = col0 + 64;
+                WaveList<1, int> L;
+                L.d[0] = lane < k ? Ld[ql * k + lane] : __builtin_inff();
+                L.id[0] = lane < k ? Li[ql * k + lane] : 0x7fffffff;
+                L.offer(v0, col0 < N ? (int)col0 : 0x7fffffff, k - 1);
+                L.offer(v1, col1 < N ? (int)col1 : 0x7fffffff, k - 1);
+                if (lane < k) {
+                    Ld[ql * k + lane] = L.d[0];
+                    Li[ql * k + lane] = L.id[0];
+                }
+                const float nt = readlane_f(L.d[0], k - 1);
+                if (h == hh) thr[r] = nt;
+            }
+        }
+    }
+
+    // per-(split, query) partial lists (each wave wrote only its own rows: no barrier needed)
+    for (int r = 0; r < 32; ++r) {
+        const int ql = 32 * wave + r;
+        const int64_t q = q0 + ql;
+        if (q < nq && lane < k) {
+            const int64_t off = ((int64_t)split * nq + q) * k;
+            part_d[off + lane] = Ld[ql * k + lane];
+            part_i[off + lane] = Li[ql * k + lane];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // flat_scan_topk — direct-form streaming scan for small query batches (FAISS nq < 20 path,
 // fvec_L2sqr / fvec_inner_product).  Queries live in LDS; each wave walks a contiguous range of
 // database rows, R rows at a time (R float4 row loads in flight per lane), reduces Σ(q−x)² (or
@@ -505,8 +693,21 @@ void launch_flat_gemm_topk(const float *Q, const float *qn, int64_t nq, const fl
                            hipStream_t st) {
     const int nqt = (int)ceil_div(nq, GBM);
     const bool vec4 = (d % 4 == 0) && ((uintptr_t)Q % 16 == 0) && ((uintptr_t)X % 16 == 0);
-    const size_t smem = gemm_smem_bytes();
     dim3 grid((unsigned)(nqt * nsplit)), block(256);
+    static const int v1 = [] { const char *e = std::getenv("HIPANN_FLAT_V1"); return e ? std::atoi(e) : 0; }();
+    if (!v1) {
+        const size_t smem2 = gemm2_smem_bytes(k);
+        if (metric == kL2) {
+            if (vec4) hipLaunchKernelGGL((flat_gemm_topk2<true, true>), grid, block, smem2, st, Q, qn, nq, X, xn, N, d, k, nqt, nsplit, tiles_per_split, pd, pi);
+            else hipLaunchKernelGGL((flat_gemm_topk2<false, true>), grid, block, smem2, st, Q, qn, nq, X, xn, N, d, k, nqt, nsplit, tiles_per_split, pd, pi);
+        } else {
+            if (vec4) hipLaunchKernelGGL((flat_gemm_topk2<true, false>), grid, block, smem2, st, Q, qn, nq, X, xn, N, d, k, nqt, nsplit, tiles_per_split, pd, pi);
+            else hipLaunchKernelGGL((flat_gemm_topk2<false, false>), grid, block, smem2, st, Q, qn, nq, X, xn, N, d, k, nqt, nsplit, tiles_per_split, pd, pi);
+        }
+        HIPANN_CHECK(hipGetLastError());
+        return;
+    }
+    const size_t smem = gemm_smem_bytes();
     if (vec4) {
         hipLaunchKernelGGL(flat_gemm_topk<true>, grid, block, smem, st, Q, qn, nq, X, xn, N, d, metric, k, nqt,
                            nsplit, tiles_per_split, pd, pi);
