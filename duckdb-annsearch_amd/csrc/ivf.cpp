@@ -137,8 +137,8 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     const int nlist = ix.nlist, d = ix.d, metric = ix.metric;
     const int np = std::min(ix.nprobe, nlist);
     const float out_sign = metric == kIP ? -1.f : 1.f;
-    HIPANN_REQUIRE(k <= 64, "k > 64 is not supported by the fused GPU path yet");
-    HIPANN_REQUIRE(np <= 64, "nprobe > 64 is not supported by the GPU coarse quantizer yet");
+    // k > 64: per-slot direct scan + LDS sort (ivf_scan_slot_bigk), same plan / merge
+    const bool bigk = k > 64;
     if (nq <= 0) return;
     // 1. coarse quantizer (FAISS: quantizer->search(n, x, nprobe) — Flat rules incl. nq < 20)
     sh.coarse_d.ensure((size_t)nq * np * sizeof(float), sh.device);
@@ -156,7 +156,7 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     // the decomposed form needs float4 rows; other shapes take the direct kernel (also on the GPU)
     // the decomposed forms need float4 rows (else the direct kernel, also on the GPU); the MFMA kernel
     // keeps 16-lane lists (k <= 16) and the item's queries in LDS (else the VALU decomposed kernel)
-    int form = ix.form != kFormDirect && ivf_dot_supported(xq, d, sh.codes) ? ix.form : kFormDirect;
+    int form = ix.form != kFormDirect && !bigk && ivf_dot_supported(xq, d, sh.codes) ? ix.form : kFormDirect;
     if (form == kFormDecomposed && !ivf_mfma_supported(xq, d, sh.codes, k)) form = kFormDecomposedValu;
     const int group = ivf_group_size(form, d);
     launch_ivf_plan(sh.coarse_i.get<int64_t>(), nq, np, sh.list_len.get<int>(), nlist, group, sh.cnt.get<int>(),
@@ -183,7 +183,11 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     if (form == kFormDecomposed) ensure_tiled_codes(sh, d, nlist, st);
     {
         ScopedTiming t(ix.timer_main, st);
-        if (form == kFormDecomposed)
+        if (bigk)
+            launch_ivf_scan_bigk(xq, d, metric, sh.codes, sh.list_off.get<int64_t>(), sh.coarse_i.get<int64_t>(),
+                                 nq * np, np, sh.slot_off.get<int>(), nq * np * std::max(sh.max_nch, 1), k,
+                                 sh.part_d.get<float>(), sh.part_i.get<int>(), st);
+        else if (form == kFormDecomposed)
             launch_ivf_scan_mfma(xq, qn, d, metric, sh.codes_t.get<float>(), sh.tpass_off.get<int64_t>(),
                                  sh.xnorm.get<float>(), sh.list_off.get<int64_t>(), sh.cnt.get<int>(),
                                  sh.bucket_off.get<int>(), sh.item_off.get<int>(), sh.bucket.get<int>(),

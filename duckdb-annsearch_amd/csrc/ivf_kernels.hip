@@ -783,6 +783,97 @@ ivf_merge_topk(const float *__restrict__ pd, const int *__restrict__ pi, const i
 }
 
 // ---------------------------------------------------------------------------------------------
+// ivf_scan_slot_bigk — the k > 64 path (faiss-metal's select handles k ≤ 2048, MetalSelect.mm:31-74).
+// One block per partial-list slot (pair q·nprobe + p, row chunk c of the probed list): the query in
+// LDS, every chunk row's direct-form key (FAISS IVFFlatScanner: Σ(q−x)², or −q·x) computed by one
+// wave per row, then the ≤ 2048 (key, row) pairs bitonic-sorted in LDS and the first k written.
+// Query-major (each list is re-read per probing query): a correctness path for large k, not the
+// throughput path.
+// ---------------------------------------------------------------------------------------------
+template <bool IP>
+__global__ void __launch_bounds__(256)
+ivf_scan_slot_bigk(const float *__restrict__ Q, int d, const float *__restrict__ codes,
+                   const int64_t *__restrict__ list_off, const int64_t *__restrict__ probes, int64_t npairs,
+                   int nprobe, const int *__restrict__ slot_off, int k, float *__restrict__ part_d,
+                   int *__restrict__ part_i) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    float *sk = sm;                                          // [IVF_CH] keys
+    int *si = reinterpret_cast<int *>(sm + IVF_CH);          // [IVF_CH] rows
+    float *qv = sm + 2 * IVF_CH;                             // [d] query
+    const int slot = blockIdx.x;
+    if (slot >= slot_off[npairs]) return;  // the grid is sized for the worst case
+    // pair owning this slot: the last i with slot_off[i] <= slot (pairs with no slots are skipped)
+    int64_t lo = 0, hi = npairs - 1;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (slot_off[mid] <= slot) lo = mid; else hi = mid - 1;
+    }
+    const int64_t pair = lo;
+    const int chunk = slot - slot_off[pair];
+    const int64_t l = probes[pair];
+    const int64_t r0 = list_off[l] + (int64_t)chunk * IVF_CH;
+    const int64_t r1 = r0 + IVF_CH < list_off[l + 1] ? r0 + IVF_CH : list_off[l + 1];
+    const int len = (int)(r1 - r0);
+    const float *q = Q + (pair / nprobe) * (int64_t)d;
+    for (int j = threadIdx.x; j < d; j += 256) qv[j] = q[j];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int r = wave; r < IVF_CH; r += 4) {
+        float acc = 0.f;
+        if (r < len) {
+            const float *x = codes + (r0 + r) * (int64_t)d;
+            for (int j = lane; j < d; j += 64) {
+                if (IP) acc = fmaf(qv[j], x[j], acc);
+                else { const float t = qv[j] - x[j]; acc = fmaf(t, t, acc); }
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+        }
+        if (lane == 0) {
+            sk[r] = r < len ? (IP ? -acc : acc) : __builtin_inff();
+            si[r] = r < len ? (int)(r0 + r) : 0x7fffffff;
+        }
+    }
+    __syncthreads();
+    // bitonic sort of IVF_CH pairs, ascending (key, row)
+    for (int size = 2; size <= IVF_CH; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int t = threadIdx.x; t < IVF_CH / 2; t += 256) {
+                const int a = 2 * t - (t & (stride - 1)), b = a + stride;
+                const bool up = (a & size) == 0;
+                const float ka = sk[a], kb = sk[b];
+                const int ia = si[a], ib = si[b];
+                const bool b_less = kb < ka || (kb == ka && ib < ia);
+                if (b_less == up) { sk[a] = kb; sk[b] = ka; si[a] = ib; si[b] = ia; }
+            }
+            __syncthreads();
+        }
+    }
+    const int64_t off = (int64_t)slot * k;
+    for (int e = threadIdx.x; e < k; e += 256) {
+        part_d[off + e] = e < IVF_CH ? sk[e] : __builtin_inff();
+        part_i[off + e] = e < IVF_CH ? si[e] : 0x7fffffff;
+    }
+}
+
+void launch_ivf_scan_bigk(const float *Q, int d, int metric, const float *codes, const int64_t *list_off,
+                          const int64_t *probes, int64_t npairs, int nprobe, const int *slot_off, int64_t nslots,
+                          int k, float *pd, int *pi, hipStream_t st) {
+    if (nslots <= 0) return;
+    HIPANN_REQUIRE(nslots < (int64_t)0x7fffffff, "too many slots");
+    const size_t smem = (size_t)2 * IVF_CH * 4 + (size_t)d * 4;
+    HIPANN_REQUIRE(smem <= 64 * 1024, "dimension too large for the k > 64 IVF path");
+    dim3 grid((unsigned)nslots), block(256);
+    if (metric == kIP)
+        hipLaunchKernelGGL(ivf_scan_slot_bigk<true>, grid, block, smem, st, Q, d, codes, list_off, probes, npairs,
+                           nprobe, slot_off, k, pd, pi);
+    else
+        hipLaunchKernelGGL(ivf_scan_slot_bigk<false>, grid, block, smem, st, Q, d, codes, list_off, probes, npairs,
+                           nprobe, slot_off, k, pd, pi);
+    HIPANN_CHECK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------------------------
 void launch_ivf_plan(const int64_t *probes, int64_t nq, int nprobe, const int *list_len, int nlist, int group,
                      int *cnt, int *bucket_off, int *item_off, int *cursor, int *bucket, int *slot_off,
                      hipStream_t st) {

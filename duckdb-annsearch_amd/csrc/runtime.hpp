@@ -225,6 +225,9 @@ void launch_ivf_plan(const int64_t *probes, int64_t nq, int nprobe, const int *l
 int64_t ivf_max_items(int64_t nq, int nprobe, int nlist, int max_nch, int64_t nrows, int group);
 int ivf_group_size(int form, int d);  // queries per work item of the form's scan kernel
 int ivf_chunk_rows();
+void launch_ivf_scan_bigk(const float *Q, int d, int metric, const float *codes, const int64_t *list_off,
+                          const int64_t *probes, int64_t npairs, int nprobe, const int *slot_off, int64_t nslots,
+                          int k, float *pd, int *pi, hipStream_t st);
 size_t ivf_scan_smem_bytes();
 bool ivf_dot_supported(const float *Q, int d, const float *codes);
 void launch_ivf_scan(const float *Q, const float *qn, int d, int metric, int form, const float *codes,

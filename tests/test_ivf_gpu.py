@@ -217,3 +217,32 @@ def test_ivf_gpu_build_recall(gpu):
     recall = np.mean([len(set(got[i]) & set(gt[i])) / 10 for i in range(200)])
     assert recall >= 0.95, recall
     assert info["list_size_min"] >= 0 and sum(np.diff(ix._offsets)) == n
+
+
+@pytest.mark.parametrize("k", [65, 100, 257, 1000])
+@pytest.mark.parametrize("metric", [0, 1])
+def test_ivf_large_k(gpu, oracle, k, metric):
+    """k > 64 (faiss-metal selects up to k = 2048, MetalSelect.mm:31-74): the per-slot scan + LDS sort
+    path, lists longer than one 2048-row chunk (a probed list contributes several slots), k larger
+    than some probed lists and than a chunk tail."""
+    xb, xq = faiss_metal_case(12000, 37, 40)
+    ix, (cen, off, ids, codes) = _ivf(gpu, xb, 8, 3, metric)
+    D, I = ix.search(xq, k)
+    Do, Io, Po = oracle.ivf_search(cen, off, ids, codes, xq, k, 3, metric)
+    assert np.array_equal(ix.last_probes(len(xq)), Po)
+    check_topk_parity(xb, xq, D, I, Do, Io, metric)
+
+
+@pytest.mark.parametrize("nprobe", [65, 100, 256])
+@pytest.mark.parametrize("k", [10, 64])
+def test_ivf_large_nprobe(gpu, oracle, nprobe, k):
+    """nprobe > 64 (the coarse quantizer takes the Flat large-k path); nprobe = nlist equals Flat."""
+    xb, xq = faiss_metal_case(30000, 50, 32)
+    ix, (cen, off, ids, codes) = _ivf(gpu, xb, 256, nprobe)
+    D, I = ix.search(xq, k)
+    Do, Io, Po = oracle.ivf_search(cen, off, ids, codes, xq, k, nprobe)
+    assert np.array_equal(ix.last_probes(len(xq)), Po)
+    check_topk_parity(xb, xq, D, I, Do, Io)
+    if nprobe == 256:
+        Df, If_ = oracle.flat_search(xb, xq, k)
+        check_topk_parity(xb, xq, D, I, Df, If_)
