@@ -50,6 +50,9 @@ def parse():
     p.add_argument("--d", type=int, default=None, help="dimension (768; 1536 for diskann)")
     p.add_argument("--l-search", type=int, default=128, help="diskann L_search")
     p.add_argument("--degree", type=int, default=64, help="diskann graph degree R")
+    p.add_argument("--diskann-host-bfs", action="store_true",
+                   help="diskann: the reference-shaped host BFS (one id-gather launch per step) instead of the "
+                        "GPU-resident traversal")
     p.add_argument("--nq", type=int, default=1024)
     p.add_argument("--k", type=int, default=10)
     p.add_argument("--nlist", type=int, default=1024)
@@ -343,10 +346,13 @@ def run_diskann(args, torch, dist, hipann, rank, world, dev):
     """C4 (SURVEY §8d): DiskProvider::search_batch over 1M x 1536 SQ8, L_search=128, R=64, nq=1024.
 
     Graph traversal does not shard, so N GPUs run N replicas (each holds the whole SQ8 DB and answers
-    its own 1024-query batch; weak scaling, no collective).  A step = one lock-step BFS batch through
-    diskann_hip_search_batch (host BFS, every step's distances on the GPU by the id-gather kernel).
-    Roofline: the SQ8 id-gather kernel, algorithmic bytes per distance = d (codes) + 4 (id) +
-    4 (query_map) + 4 (out), summed over the timed launches."""
+    its own 1024-query batch; weak scaling, no collective).  A step = one BFS batch of nq queries:
+      * default: diskann_hip_search_batch_resident_device — the traversal on the GPU (one wavefront per
+        query, DB + adjacency + visited bitmaps in HBM); roofline of that kernel, algorithmic bytes =
+        distances x d (SQ8 code rows) + expansions x 4R (adjacency rows);
+      * --diskann-host-bfs: diskann_hip_search_batch — the reference's structure (host lock-step BFS,
+        one id-gather launch per step); roofline of the id-gather kernel, d + 12 B per distance
+        (code row + id + query_map + out)."""
     import diskann_build as DB
 
     n, d, nq, k, L, R = args.n, args.d, args.nq, args.k, args.l_search, args.degree
@@ -373,9 +379,19 @@ def run_diskann(args, torch, dist, hipann, rank, world, dev):
     torch.cuda.empty_cache()
     xq_h = xq.cpu().numpy()
     eps = np.array([medoid], np.uint32)
+    resident = not args.diskann_host_bfs
+    stream = torch.cuda.current_stream().cuda_stream
+    if resident:
+        db.register_graph(adj)
+        I_dev = torch.empty((nq, k), device=dev, dtype=torch.int64)
+        D_dev = torch.empty((nq, k), device=dev, dtype=torch.float32)
     setup_s = time.perf_counter() - t_setup
 
     def step():
+        if resident:
+            st = db.search_batch_resident_device(eps, nq, xq.data_ptr(), k, L, I_dev.data_ptr(), D_dev.data_ptr(),
+                                                 metric, stream)
+            return None, None, st
         return db.search_batch(adj, eps, xq_h, k, L, metric)
 
     for _ in range(args.warmup):
@@ -385,11 +401,13 @@ def run_diskann(args, torch, dist, hipann, rank, world, dev):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    evals = 0
+    evals = pops = requeries = 0
     bfs_steps = []
     for _ in range(args.steps):
         ids, dd, st = step()
         evals += st["evals"]
+        pops += st.get("pops", 0)
+        requeries += st.get("host_requeries", 0)
         bfs_steps.append(st["steps"])
     torch.cuda.synchronize()
     if world > 1:
@@ -402,20 +420,33 @@ def run_diskann(args, torch, dist, hipann, rank, world, dev):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     qps = world * nq * args.steps / elapsed
+    if resident:
+        ids = I_dev.cpu().numpy()
 
     gt = DB.exact_topk(torch, xb, xq, k, metric).cpu().numpy()
     recall = float(np.mean([len(set(ids[i]) & set(gt[i])) / k for i in range(nq)]))
-    bytes_per_eval = d + 12
-    achieved = evals * bytes_per_eval / (kern_total_ms * 1e-3) / 1e9 if kern_total_ms > 0 else 0.0
+    if resident:
+        # per distance: the SQ8 code row (d B); per expansion: the adjacency row (4R B)
+        b_alg = evals * d + pops * 4 * R
+        achieved = b_alg / (kern_total_ms * 1e-3) / 1e9 if kern_total_ms > 0 else 0.0
+        kname = "diskann_bfs"
+        alg = (f"distances x d B (SQ8 code rows) + expansions x 4R B (adjacency rows) = "
+               f"{b_alg / args.steps / 1e9:.3f} GB per batch (one launch per batch)")
+    else:
+        b_alg = evals * (d + 12)
+        achieved = b_alg / (kern_total_ms * 1e-3) / 1e9 if kern_total_ms > 0 else 0.0
+        kname = "dist_ids_sq8"
+        alg = (f"distances x (d + 12) B = {d + 12} B per distance (SQ8 code row + id + query_map + out), summed "
+               f"over the timed launches")
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": "dist_ids_sq8",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kname,
             "kernel_ms_per_launch": round(kern_total_ms / max(launches, 1), 4),
             "kernel_ms_per_batch": round(kern_total_ms / args.steps, 3),
             "launches_per_batch": launches / args.steps,
             "distances_per_batch": evals // args.steps,
-            "algorithmic": f"distances x (d + 12) B = {bytes_per_eval} B per distance (SQ8 code row + id + "
-                           f"query_map + out), summed over the timed launches"}
-    tb, tsrc = pmc_traffic("diskann", "dist_ids_sq8")
+            "expansions_per_batch": pops // args.steps if resident else None,
+            "algorithmic": alg}
+    tb, tsrc = pmc_traffic("diskann", kname)
     if tb is not None and world == 1:
         roof["traffic"] = round(tb / 1e9, 4)
         roof["traffic_unit"] = "GB per launch (PMC FETCH_SIZE)"
@@ -468,7 +499,10 @@ def run_diskann(args, torch, dist, hipann, rank, world, dev):
             "cpu_baseline": cpu,
             "setup_s": round(setup_s, 1),
             "diskann": {"graph_build_s": round(t_graph, 1), "bfs_steps_per_batch": int(np.mean(bfs_steps)),
-                        "bfs_threads": int(os.environ.get("HIPANN_BFS_THREADS", "16"))},
+                        "traversal": "GPU-resident (one wavefront per query)" if resident else
+                                     f"host lock-step BFS ({os.environ.get('HIPANN_BFS_THREADS', '16')} threads) + "
+                                     f"per-step id-gather launches",
+                        "host_requeries": requeries},
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -33,6 +33,12 @@
 
 namespace hipann {
 
+bool diskann_bfs_supported(int d, int fmt, int R, int n_ep, int L, uint32_t N);
+void launch_diskann_bfs(const float *Q, int nq, int d, int fmt, const void *data, const float2 *ab,
+                        const uint32_t *adj, int R, uint32_t N, const uint32_t *eps, int n_ep, int k, int L,
+                        int metric, uint32_t *visited, int64_t vwords, int64_t *out_ids, float *out_d, int *flags,
+                        unsigned long long *stats, hipStream_t st);
+
 __device__ __forceinline__ float wave_sum(float s) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
@@ -241,6 +247,10 @@ struct DiskDB {
     DevBuf q, ids, m, out;
     HostBuf hids, hm, hout;
     KernelTimer timer;
+    // resident graph + BFS scratch (diskann_hip_register_graph / _search_batch_resident)
+    int R = 0;
+    DevBuf adj_dev, visited, flags, bstats, eps_dev;
+    std::vector<uint32_t> adj_host;
     ~DiskDB() {
         if (stream) { DeviceGuard g(device); (void)hipStreamDestroy(stream); }
     }
@@ -434,6 +444,180 @@ int bfs_threads(int nq) {
     if (hw > 0) t = std::min(t, hw);
     t = std::min(t, std::max(1, nq / 16));  // ≥ 16 queries per thread
     return std::max(1, t);
+}
+
+// Host-driven lock-step BFS (the reference's structure: host state, one id-gather launch per step).
+// Caller holds db.mu and the device.  Also the fallback of the resident path for flagged queries.
+void host_bfs(DiskDB *db, const uint32_t *adj, int R, const uint32_t *eps, int n_ep, const float *queries, int nq,
+              int k, int l_search, int metric, int64_t *out_ids, float *out_d, int64_t *stats) {
+    const uint32_t N = (uint32_t)db->n;
+    const int dim = db->dim;
+    int64_t nevals = 0, nsteps = 0, ncalls = 0;
+    if (nq == 0) {
+        if (stats) { stats[0] = stats[1] = stats[2] = stats[3] = 0; }
+        return;
+    }
+    const size_t l = (size_t)std::max(l_search, k);
+    const hipStream_t st = db->stream;
+    // Fixed per-query slot layout: query qi owns slots [qi*S, qi*S + S) of every lock-step batch,
+    // S = max(R, n_ep); unused slots hold UINT32_MAX and the kernel skips them.  The query map is
+    // therefore constant (uploaded once) and the host phases run per query in parallel with no
+    // compaction step.  Per query the candidate order is the reference's (neighbour order).
+    const size_t S = (size_t)std::max(R, n_ep);
+    const size_t cap = (size_t)nq * S;
+    HIPANN_REQUIRE(cap <= (size_t)INT32_MAX, "nq * max(R, n_ep) exceeds INT32_MAX");
+    db->q.ensure((size_t)nq * dim * 4 + 16, db->device);
+    HIPANN_CHECK(hipMemcpyAsync(db->q.p, queries, (size_t)nq * dim * 4, hipMemcpyHostToDevice, st));
+    db->ids.ensure(cap * 4, db->device);
+    db->m.ensure(cap * 4, db->device);
+    db->out.ensure(cap * 4, db->device);
+    db->hids.ensure(cap * 4);
+    db->hm.ensure(cap * 4);
+    db->hout.ensure(cap * 4);
+    uint32_t *hid = db->hids.get<uint32_t>();
+    uint32_t *hm = db->hm.get<uint32_t>();
+    float *hout = db->hout.get<float>();
+    for (size_t i = 0; i < cap; ++i) hm[i] = (uint32_t)(i / S);
+    HIPANN_CHECK(hipMemcpyAsync(db->m.p, hm, cap * 4, hipMemcpyHostToDevice, st));
+    // Only the slot prefix up to the last query with work is shipped each step.
+    auto gpu_dists = [&](size_t span) {
+        HIPANN_CHECK(hipMemcpyAsync(db->ids.p, hid, span * 4, hipMemcpyHostToDevice, st));
+        {
+            ScopedTiming tm(db->timer, st);
+            launch_ids(*db, db->q.get<float>(), db->ids.get<unsigned>(), db->m.get<unsigned>(), (int)span, metric,
+                       db->out.get<float>(), st);
+        }
+        HIPANN_CHECK(hipMemcpyAsync(hout, db->out.p, span * 4, hipMemcpyDeviceToHost, st));
+        HIPANN_CHECK(hipStreamSynchronize(st));
+        ncalls++;
+    };
+    std::vector<QState> Sq((size_t)nq);
+    SpinPool pool(bfs_threads(nq));
+    const int T = pool.size();
+    auto chunk = [&](int t, int &q0, int &q1) {
+        q0 = (int)((int64_t)nq * t / T);
+        q1 = (int)((int64_t)nq * (t + 1) / T);
+    };
+    // per-thread reductions: [0] active queries, [1] distances, [2] last query with work + 1
+    std::vector<int64_t> red((size_t)T * 3 * 8, 0);  // padded against false sharing
+    auto reduce = [&](int j) {
+        int64_t v = 0;
+        for (int t = 0; t < T; ++t) v = (j == 2) ? std::max(v, red[(size_t)t * 24 + j]) : v + red[(size_t)t * 24 + j];
+        return v;
+    };
+    // seed entry points (disk_provider.rs:524-538)
+    pool.run([&](int t) {
+        int q0, q1;
+        chunk(t, q0, q1);
+        int64_t tot = 0, last = 0;
+        for (int qi = q0; qi < q1; ++qi) {
+            QState &s = Sq[qi];
+            s.visited.init(std::max<size_t>(l * 2, 1024));
+            s.cands.reserve(l * 2);
+            s.result.reserve(l + 1);
+            uint32_t *slot = hid + (size_t)qi * S;
+            int cnt = 0;
+            for (int e = 0; e < n_ep; ++e) {
+                const uint32_t ep = eps[e];
+                if (s.visited.insert(ep) && ep < N) slot[cnt++] = ep;
+            }
+            for (size_t j = (size_t)cnt; j < S; ++j) slot[j] = 0xffffffffu;
+            s.nnew = cnt;
+            tot += cnt;
+            if (cnt) last = qi + 1;
+        }
+        red[(size_t)t * 24 + 1] = tot;
+        red[(size_t)t * 24 + 2] = last;
+    });
+    if (reduce(1)) {
+        gpu_dists((size_t)reduce(2) * S);
+        nevals += reduce(1);
+    }
+    pool.run([&](int t) {
+        int q0, q1;
+        chunk(t, q0, q1);
+        for (int qi = q0; qi < q1; ++qi) {
+            QState &s = Sq[qi];
+            const uint32_t *slot = hid + (size_t)qi * S;
+            const float *dd = hout + (size_t)qi * S;
+            for (int j = 0; j < s.nnew; ++j) {
+                s.cands.push_back(Cand{dd[j], slot[j]});
+                std::push_heap(s.cands.begin(), s.cands.end(), CandGreater());
+                s.result.push_back(Cand{dd[j], slot[j]});
+            }
+            std::stable_sort(s.result.begin(), s.result.end(), [](const Cand &x, const Cand &y) { return x.d < y.d; });
+        }
+    });
+    // Lock-step iterations (disk_provider.rs:545-652).  One fork-join per step: the insert phase of
+    // step s (results of its GPU call) and the pop/expand phase of step s+1 run back to back per query.
+    bool first = true;
+    for (;;) {
+        pool.run([&](int t) {
+            int q0, q1;
+            chunk(t, q0, q1);
+            int64_t head = 0, tot = 0, last = 0;
+            for (int qi = q0; qi < q1; ++qi) {
+                QState &s = Sq[qi];
+                uint32_t *slot = hid + (size_t)qi * S;
+                if (!first) {
+                    const float *dd = hout + (size_t)qi * S;
+                    for (int j = 0; j < s.nnew; ++j) insert_result(s, l, dd[j], slot[j]);
+                }
+                const int prev = s.nnew;  // slots >= prev are already empty
+                s.nnew = 0;
+                head += s.active ? 1 : 0;  // the reference's loop-head active count
+                if (s.active) {
+                    if (s.cands.empty()) {
+                        s.active = false;
+                    } else {
+                        std::pop_heap(s.cands.begin(), s.cands.end(), CandGreater());
+                        const Cand c = s.cands.back();
+                        s.cands.pop_back();
+                        if (s.result.size() >= l && c.d > s.result[l - 1].d) {
+                            s.active = false;
+                        } else {
+                            const uint32_t *nbr = adj + (size_t)c.id * R;
+                            int cnt = 0;
+                            for (int r = 0; r < R; ++r) {
+                                const uint32_t nb = nbr[r];
+                                if (nb == 0xffffffffu) break;  // get_neighbors trims at the first sentinel
+                                if (nb >= N) continue;
+                                if (!s.visited.insert(nb)) continue;
+                                slot[cnt++] = nb;
+                            }
+                            s.nnew = cnt;
+                        }
+                    }
+                }
+                for (int j = s.nnew; j < prev; ++j) slot[j] = 0xffffffffu;
+                tot += s.nnew;
+                if (s.nnew) last = qi + 1;
+            }
+            red[(size_t)t * 24 + 0] = head;
+            red[(size_t)t * 24 + 1] = tot;
+            red[(size_t)t * 24 + 2] = last;
+        });
+        first = false;
+        const int64_t head = reduce(0), tot = reduce(1);
+        if (!head) break;  // no active query at the loop head
+        nsteps++;
+        if (!tot) continue;
+        gpu_dists((size_t)reduce(2) * S);
+        nevals += tot;
+    }
+    for (int qi = 0; qi < nq; ++qi) {
+        const auto &r = Sq[qi].result;
+        for (int j = 0; j < k; ++j) {
+            if ((size_t)j < r.size()) {
+                out_ids[(size_t)qi * k + j] = r[j].id;
+                out_d[(size_t)qi * k + j] = r[j].d;
+            } else {
+                out_ids[(size_t)qi * k + j] = -1;
+                out_d[(size_t)qi * k + j] = FLT_MAX;
+            }
+        }
+    }
+    if (stats) { stats[0] = nevals; stats[1] = nsteps; stats[2] = ncalls; stats[3] = 0; }
 }
 
 }  // namespace
@@ -640,174 +824,159 @@ int diskann_hip_search_batch(void *h, const uint32_t *adj, int R, const uint32_t
         auto *db = static_cast<DiskDB *>(h);
         std::lock_guard<std::mutex> lk(db->mu);
         DeviceGuard g(db->device);
+        host_bfs(db, adj, R, eps, n_ep, queries, nq, k, l_search, metric, out_ids, out_d, stats);
+        return 0;
+    } catch (const std::exception &e) {
+        set_err(eb, el, e.what());
+    } catch (...) {
+        set_err(eb, el, "hipann: unknown error");
+    }
+    return -1;
+}
+
+int diskann_hip_register_graph(void *h, const uint32_t *adj, int R) {
+    if (!h || !adj || R <= 0) return -1;
+    auto *db = static_cast<DiskDB *>(h);
+    try {
+        std::lock_guard<std::mutex> lk(db->mu);
+        DeviceGuard g(db->device);
+        const size_t cnt = (size_t)db->n * R;
+        db->adj_host.assign(adj, adj + cnt);
+        db->adj_dev.ensure(cnt * 4 + 16, db->device);
+        if (cnt) HIPANN_CHECK(hipMemcpyAsync(db->adj_dev.p, adj, cnt * 4, hipMemcpyHostToDevice, db->stream));
+        HIPANN_CHECK(hipStreamSynchronize(db->stream));
+        db->R = R;
+        return 0;
+    } catch (...) {
+        return -1;
+    }
+}
+
+// Resident search: queries / outputs in HBM, asynchronous launch on `stream`, then a wait for the
+// per-query flags (the rare flagged queries and unsupported shapes go through host_bfs).
+int diskann_hip_search_batch_resident_device(void *h, const uint32_t *eps, int n_ep, const float *queries_dev, int nq,
+                                             int k, int l_search, int metric, int64_t *out_ids_dev,
+                                             float *out_d_dev, int64_t *stats, void *stream, char *eb, int el) {
+    try {
+        HIPANN_REQUIRE(h && (n_ep == 0 || eps) && (nq == 0 || (queries_dev && out_ids_dev && out_d_dev)),
+                       "null argument");
+        HIPANN_REQUIRE(nq >= 0 && k > 0 && n_ep >= 0, "bad arguments");
+        HIPANN_REQUIRE(metric == kL2 || metric == kIP, "metric must be 0 or 1");
+        auto *db = static_cast<DiskDB *>(h);
+        std::lock_guard<std::mutex> lk(db->mu);
+        HIPANN_REQUIRE(db->R > 0, "no graph registered (diskann_hip_register_graph)");
+        DeviceGuard g(db->device);
+        const hipStream_t st = stream ? static_cast<hipStream_t>(stream) : db->stream;
+        if (stats) { stats[0] = stats[1] = stats[2] = stats[3] = 0; }
+        if (nq == 0) return 0;
         const uint32_t N = (uint32_t)db->n;
-        const int dim = db->dim;
-        int64_t nevals = 0, nsteps = 0, ncalls = 0;
-        if (nq == 0) {
-            if (stats) { stats[0] = stats[1] = stats[2] = stats[3] = 0; }
-            return 0;
-        }
-        const size_t l = (size_t)std::max(l_search, k);
-        const hipStream_t st = db->stream;
-        // Fixed per-query slot layout: query qi owns slots [qi*S, qi*S + S) of every lock-step batch,
-        // S = max(R, n_ep); unused slots hold UINT32_MAX and the kernel skips them.  The query map is
-        // therefore constant (uploaded once) and the host phases run per query in parallel with no
-        // compaction step.  Per query the candidate order is the reference's (neighbour order).
-        const size_t S = (size_t)std::max(R, n_ep);
-        const size_t cap = (size_t)nq * S;
-        HIPANN_REQUIRE(cap <= (size_t)INT32_MAX, "nq * max(R, n_ep) exceeds INT32_MAX");
-        db->q.ensure((size_t)nq * dim * 4 + 16, db->device);
-        HIPANN_CHECK(hipMemcpyAsync(db->q.p, queries, (size_t)nq * dim * 4, hipMemcpyHostToDevice, st));
-        db->ids.ensure(cap * 4, db->device);
-        db->m.ensure(cap * 4, db->device);
-        db->out.ensure(cap * 4, db->device);
-        db->hids.ensure(cap * 4);
-        db->hm.ensure(cap * 4);
-        db->hout.ensure(cap * 4);
-        uint32_t *hid = db->hids.get<uint32_t>();
-        uint32_t *hm = db->hm.get<uint32_t>();
-        float *hout = db->hout.get<float>();
-        for (size_t i = 0; i < cap; ++i) hm[i] = (uint32_t)(i / S);
-        HIPANN_CHECK(hipMemcpyAsync(db->m.p, hm, cap * 4, hipMemcpyHostToDevice, st));
-        // Only the slot prefix up to the last query with work is shipped each step.
-        auto gpu_dists = [&](size_t span) {
-            HIPANN_CHECK(hipMemcpyAsync(db->ids.p, hid, span * 4, hipMemcpyHostToDevice, st));
-            {
+        const int L = std::max(l_search, std::min<int>(k, (int)std::min<int64_t>(db->n, INT32_MAX)));
+        const int kk = k;
+        std::vector<int> flags((size_t)nq, 0);
+        const bool gpu_ok = db->n > 0 && diskann_bfs_supported(db->dim, db->fmt, db->R, n_ep, L, N);
+        int64_t gsteps = 0, gevals = 0, gpops = 0;
+        if (gpu_ok) {
+            const int64_t vwords = ((int64_t)N + 31) / 32;
+            // bound the visited bitmaps to ~2 GiB: sub-batches of queries
+            const int64_t per = std::max<int64_t>(1, std::min<int64_t>(nq, ((int64_t)2 << 30) / (vwords * 4)));
+            db->visited.ensure((size_t)per * vwords * 4, db->device);
+            db->flags.ensure((size_t)nq * 4, db->device);
+            db->bstats.ensure(24, db->device);
+            db->eps_dev.ensure((size_t)std::max(n_ep, 1) * 4, db->device);
+            if (n_ep) HIPANN_CHECK(hipMemcpyAsync(db->eps_dev.p, eps, (size_t)n_ep * 4, hipMemcpyHostToDevice, st));
+            HIPANN_CHECK(hipMemsetAsync(db->bstats.p, 0, 24, st));
+            for (int64_t q0 = 0; q0 < nq; q0 += per) {
+                const int64_t qn = std::min<int64_t>(per, nq - q0);
+                HIPANN_CHECK(hipMemsetAsync(db->visited.p, 0, (size_t)qn * vwords * 4, st));
                 ScopedTiming tm(db->timer, st);
-                launch_ids(*db, db->q.get<float>(), db->ids.get<unsigned>(), db->m.get<unsigned>(), (int)span, metric,
-                           db->out.get<float>(), st);
+                launch_diskann_bfs(queries_dev + q0 * db->dim, (int)qn, db->dim, db->fmt, db->data.p,
+                                   db->ab.get<float2>(), db->adj_dev.get<uint32_t>(), db->R, N,
+                                   db->eps_dev.get<uint32_t>(), n_ep, kk, L, metric, db->visited.get<uint32_t>(),
+                                   vwords, out_ids_dev + q0 * kk, out_d_dev + q0 * kk, db->flags.get<int>() + q0,
+                                   db->bstats.get<unsigned long long>(), st);
             }
-            HIPANN_CHECK(hipMemcpyAsync(hout, db->out.p, span * 4, hipMemcpyDeviceToHost, st));
+            unsigned long long hs[3] = {0, 0, 0};
+            HIPANN_CHECK(hipMemcpyAsync(flags.data(), db->flags.p, (size_t)nq * 4, hipMemcpyDeviceToHost, st));
+            HIPANN_CHECK(hipMemcpyAsync(hs, db->bstats.p, 24, hipMemcpyDeviceToHost, st));
             HIPANN_CHECK(hipStreamSynchronize(st));
-            ncalls++;
-        };
-        std::vector<QState> Sq((size_t)nq);
-        SpinPool pool(bfs_threads(nq));
-        const int T = pool.size();
-        auto chunk = [&](int t, int &q0, int &q1) {
-            q0 = (int)((int64_t)nq * t / T);
-            q1 = (int)((int64_t)nq * (t + 1) / T);
-        };
-        // per-thread reductions: [0] active queries, [1] distances, [2] last query with work + 1
-        std::vector<int64_t> red((size_t)T * 3 * 8, 0);  // padded against false sharing
-        auto reduce = [&](int j) {
-            int64_t v = 0;
-            for (int t = 0; t < T; ++t) v = (j == 2) ? std::max(v, red[(size_t)t * 24 + j]) : v + red[(size_t)t * 24 + j];
-            return v;
-        };
-        // seed entry points (disk_provider.rs:524-538)
-        pool.run([&](int t) {
-            int q0, q1;
-            chunk(t, q0, q1);
-            int64_t tot = 0, last = 0;
-            for (int qi = q0; qi < q1; ++qi) {
-                QState &s = Sq[qi];
-                s.visited.init(std::max<size_t>(l * 2, 1024));
-                s.cands.reserve(l * 2);
-                s.result.reserve(l + 1);
-                uint32_t *slot = hid + (size_t)qi * S;
-                int cnt = 0;
-                for (int e = 0; e < n_ep; ++e) {
-                    const uint32_t ep = eps[e];
-                    if (s.visited.insert(ep) && ep < N) slot[cnt++] = ep;
-                }
-                for (size_t j = (size_t)cnt; j < S; ++j) slot[j] = 0xffffffffu;
-                s.nnew = cnt;
-                tot += cnt;
-                if (cnt) last = qi + 1;
-            }
-            red[(size_t)t * 24 + 1] = tot;
-            red[(size_t)t * 24 + 2] = last;
-        });
-        if (reduce(1)) {
-            gpu_dists((size_t)reduce(2) * S);
-            nevals += reduce(1);
+            gevals = (int64_t)hs[0];
+            gsteps = (int64_t)hs[1];
+            gpops = (int64_t)hs[2];
+        } else {
+            std::fill(flags.begin(), flags.end(), 1);
         }
-        pool.run([&](int t) {
-            int q0, q1;
-            chunk(t, q0, q1);
-            for (int qi = q0; qi < q1; ++qi) {
-                QState &s = Sq[qi];
-                const uint32_t *slot = hid + (size_t)qi * S;
-                const float *dd = hout + (size_t)qi * S;
-                for (int j = 0; j < s.nnew; ++j) {
-                    s.cands.push_back(Cand{dd[j], slot[j]});
-                    std::push_heap(s.cands.begin(), s.cands.end(), CandGreater());
-                    s.result.push_back(Cand{dd[j], slot[j]});
-                }
-                std::stable_sort(s.result.begin(), s.result.end(), [](const Cand &x, const Cand &y) { return x.d < y.d; });
+        // host BFS for flagged queries (exact; queries are independent)
+        std::vector<int> redo;
+        for (int i = 0; i < nq; ++i)
+            if (flags[i]) redo.push_back(i);
+        int64_t hsteps = 0, hevals = 0;
+        if (!redo.empty()) {
+            const int nr = (int)redo.size(), dim = db->dim;
+            std::vector<float> qh((size_t)nr * dim);
+            for (int j = 0; j < nr; ++j)
+                HIPANN_CHECK(hipMemcpyAsync(qh.data() + (size_t)j * dim, queries_dev + (size_t)redo[j] * dim,
+                                            (size_t)dim * 4, hipMemcpyDeviceToHost, st));
+            HIPANN_CHECK(hipStreamSynchronize(st));
+            std::vector<int64_t> oi((size_t)nr * kk);
+            std::vector<float> od((size_t)nr * kk);
+            int64_t hst[4] = {0, 0, 0, 0};
+            host_bfs(db, db->adj_host.data(), db->R, eps, n_ep, qh.data(), nr, kk, l_search, metric, oi.data(),
+                     od.data(), hst);
+            for (int j = 0; j < nr; ++j) {
+                HIPANN_CHECK(hipMemcpyAsync(out_ids_dev + (size_t)redo[j] * kk, oi.data() + (size_t)j * kk,
+                                            (size_t)kk * 8, hipMemcpyHostToDevice, st));
+                HIPANN_CHECK(hipMemcpyAsync(out_d_dev + (size_t)redo[j] * kk, od.data() + (size_t)j * kk,
+                                            (size_t)kk * 4, hipMemcpyHostToDevice, st));
             }
-        });
-        // Lock-step iterations (disk_provider.rs:545-652).  One fork-join per step: the insert phase of
-        // step s (results of its GPU call) and the pop/expand phase of step s+1 run back to back per query.
-        bool first = true;
-        for (;;) {
-            pool.run([&](int t) {
-                int q0, q1;
-                chunk(t, q0, q1);
-                int64_t head = 0, tot = 0, last = 0;
-                for (int qi = q0; qi < q1; ++qi) {
-                    QState &s = Sq[qi];
-                    uint32_t *slot = hid + (size_t)qi * S;
-                    if (!first) {
-                        const float *dd = hout + (size_t)qi * S;
-                        for (int j = 0; j < s.nnew; ++j) insert_result(s, l, dd[j], slot[j]);
-                    }
-                    const int prev = s.nnew;  // slots >= prev are already empty
-                    s.nnew = 0;
-                    head += s.active ? 1 : 0;  // the reference's loop-head active count
-                    if (s.active) {
-                        if (s.cands.empty()) {
-                            s.active = false;
-                        } else {
-                            std::pop_heap(s.cands.begin(), s.cands.end(), CandGreater());
-                            const Cand c = s.cands.back();
-                            s.cands.pop_back();
-                            if (s.result.size() >= l && c.d > s.result[l - 1].d) {
-                                s.active = false;
-                            } else {
-                                const uint32_t *nbr = adj + (size_t)c.id * R;
-                                int cnt = 0;
-                                for (int r = 0; r < R; ++r) {
-                                    const uint32_t nb = nbr[r];
-                                    if (nb == 0xffffffffu) break;  // get_neighbors trims at the first sentinel
-                                    if (nb >= N) continue;
-                                    if (!s.visited.insert(nb)) continue;
-                                    slot[cnt++] = nb;
-                                }
-                                s.nnew = cnt;
-                            }
-                        }
-                    }
-                    for (int j = s.nnew; j < prev; ++j) slot[j] = 0xffffffffu;
-                    tot += s.nnew;
-                    if (s.nnew) last = qi + 1;
-                }
-                red[(size_t)t * 24 + 0] = head;
-                red[(size_t)t * 24 + 1] = tot;
-                red[(size_t)t * 24 + 2] = last;
-            });
-            first = false;
-            const int64_t head = reduce(0), tot = reduce(1);
-            if (!head) break;  // no active query at the loop head
-            nsteps++;
-            if (!tot) continue;
-            gpu_dists((size_t)reduce(2) * S);
-            nevals += tot;
+            HIPANN_CHECK(hipStreamSynchronize(st));
+            hevals = hst[0];
+            hsteps = hst[1];
         }
-        for (int qi = 0; qi < nq; ++qi) {
-            const auto &r = Sq[qi].result;
-            for (int j = 0; j < k; ++j) {
-                if ((size_t)j < r.size()) {
-                    out_ids[(size_t)qi * k + j] = r[j].id;
-                    out_d[(size_t)qi * k + j] = r[j].d;
-                } else {
-                    out_ids[(size_t)qi * k + j] = -1;
-                    out_d[(size_t)qi * k + j] = FLT_MAX;
-                }
-            }
+        if (stats) {
+            stats[0] = gevals + hevals;
+            stats[1] = std::max(gsteps, hsteps);
+            stats[2] = gpops;
+            stats[3] = (int64_t)redo.size();
         }
-        if (stats) { stats[0] = nevals; stats[1] = nsteps; stats[2] = ncalls; stats[3] = 0; }
+        return 0;
+    } catch (const std::exception &e) {
+        set_err(eb, el, e.what());
+    } catch (...) {
+        set_err(eb, el, "hipann: unknown error");
+    }
+    return -1;
+}
+
+int diskann_hip_search_batch_resident(void *h, const uint32_t *eps, int n_ep, const float *queries, int nq, int k,
+                                      int l_search, int metric, int64_t *out_ids, float *out_d, int64_t *stats,
+                                      char *eb, int el) {
+    try {
+        HIPANN_REQUIRE(h && (nq == 0 || (queries && out_ids && out_d)), "null argument");
+        HIPANN_REQUIRE(nq >= 0 && k > 0, "bad arguments");
+        auto *db = static_cast<DiskDB *>(h);
+        DevBuf q, oi, od;
+        int dev;
+        {
+            std::lock_guard<std::mutex> lk(db->mu);
+            dev = db->device;
+        }
+        DeviceGuard g(dev);
+        const size_t qb = (size_t)std::max(nq, 1) * db->dim * 4, ob = (size_t)std::max(nq, 1) * k;
+        q.ensure(qb, dev);
+        oi.ensure(ob * 8, dev);
+        od.ensure(ob * 4, dev);
+        hipStream_t st;
+        HIPANN_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        struct SG { hipStream_t s; ~SG() { (void)hipStreamDestroy(s); } } sg{st};
+        if (nq) HIPANN_CHECK(hipMemcpyAsync(q.p, queries, (size_t)nq * db->dim * 4, hipMemcpyHostToDevice, st));
+        const int rc = diskann_hip_search_batch_resident_device(h, eps, n_ep, q.get<float>(), nq, k, l_search, metric,
+                                                                oi.get<int64_t>(), od.get<float>(), stats, st, eb, el);
+        if (rc != 0) return rc;
+        if (nq) {
+            HIPANN_CHECK(hipMemcpyAsync(out_ids, oi.p, (size_t)nq * k * 8, hipMemcpyDeviceToHost, st));
+            HIPANN_CHECK(hipMemcpyAsync(out_d, od.p, (size_t)nq * k * 4, hipMemcpyDeviceToHost, st));
+        }
+        HIPANN_CHECK(hipStreamSynchronize(st));
         return 0;
     } catch (const std::exception &e) {
         set_err(eb, el, e.what());

@@ -116,6 +116,11 @@ def lib() -> C.CDLL:
             "diskann_hip_db_size": ([vp], i64),
             "diskann_hip_release_db": ([vp], None),
             "diskann_hip_set_kernel_timing": ([vp, i32], i32),
+            "diskann_hip_register_graph": ([vp, C.POINTER(C.c_uint32), i32], i32),
+            "diskann_hip_search_batch_resident": ([vp, C.POINTER(C.c_uint32), i32, f, i32, i32, i32, i32, i64p, f,
+                                                   i64p, cp, i32], i32),
+            "diskann_hip_search_batch_resident_device": ([vp, C.POINTER(C.c_uint32), i32, vp, i32, i32, i32, i32, vp,
+                                                          vp, i64p, vp, cp, i32], i32),
             "diskann_hip_kernel_stats": ([vp, C.POINTER(C.c_double), i64p], i32),
             "diskann_hip_search_batch": ([vp, C.POINTER(C.c_uint32), i32, C.POINTER(C.c_uint32), i32, f, i32, i32,
                                           i32, i32, i64p, f, i64p, cp, i32], i32),
@@ -532,6 +537,47 @@ class DiskannDeviceDB:
         if lib().diskann_hip_kernel_stats(self._h, C.byref(ms), C.byref(n)) != 0:
             raise HipAnnError("diskann_hip_kernel_stats failed")
         return ms.value, n.value
+
+    def register_graph(self, adjacency: np.ndarray) -> None:
+        """Upload the n x R adjacency (u32::MAX padding) for search_batch_resident."""
+        adj = np.ascontiguousarray(adjacency, np.uint32)
+        if adj.ndim != 2 or adj.shape[0] != self.n:
+            raise HipAnnError("adjacency must be (n, R)")
+        if lib().diskann_hip_register_graph(self._h, _ptr(adj, C.c_uint32), adj.shape[1]) != 0:
+            raise HipAnnError("diskann_hip_register_graph failed")
+
+    def search_batch_resident(self, entry_points, queries, k: int, l_search: int, metric: int = METRIC_L2):
+        """DiskProvider::search_batch with the traversal itself on the GPU (one wavefront per query).
+        Returns (ids, dists, stats)."""
+        eps = np.ascontiguousarray(entry_points, np.uint32)
+        q = np.ascontiguousarray(queries, np.float32)
+        nq = q.shape[0]
+        kk = min(k, self.n)
+        out_i = np.empty((nq, kk), np.int64)
+        out_d = np.empty((nq, kk), np.float32)
+        stats = np.zeros(4, np.int64)
+        eb = _err()
+        rc = lib().diskann_hip_search_batch_resident(self._h, _ptr(eps, C.c_uint32), eps.size, _ptr(q, C.c_float),
+                                                     nq, kk, l_search, metric, _ptr(out_i, C.c_int64),
+                                                     _ptr(out_d, C.c_float), _ptr(stats, C.c_int64), eb, 1024)
+        _check(rc, eb)
+        return out_i, out_d, {"evals": int(stats[0]), "steps": int(stats[1]), "pops": int(stats[2]),
+                              "host_requeries": int(stats[3])}
+
+    def search_batch_resident_device(self, entry_points, nq: int, q_ptr: int, k: int, l_search: int, i_ptr: int,
+                                     d_ptr: int, metric: int = METRIC_L2, stream: int = 0):
+        """Device-pointer form (queries nq x dim fp32, outputs nq x k int64 / fp32 in HBM)."""
+        eps = np.ascontiguousarray(entry_points, np.uint32)
+        stats = np.zeros(4, np.int64)
+        eb = _err()
+        rc = lib().diskann_hip_search_batch_resident_device(self._h, _ptr(eps, C.c_uint32), eps.size,
+                                                            C.c_void_p(q_ptr), nq, k, l_search, metric,
+                                                            C.c_void_p(i_ptr), C.c_void_p(d_ptr),
+                                                            _ptr(stats, C.c_int64), C.c_void_p(stream or None), eb,
+                                                            1024)
+        _check(rc, eb)
+        return {"evals": int(stats[0]), "steps": int(stats[1]), "pops": int(stats[2]),
+                "host_requeries": int(stats[3])}
 
     def search_batch(self, adjacency: np.ndarray, entry_points, queries, k: int, l_search: int,
                      metric: int = METRIC_L2):

@@ -87,6 +87,32 @@ int diskann_hip_search_batch(void *db, const uint32_t *adjacency, int R, const u
                              const float *queries, int nq, int k, int l_search, int metric, int64_t *out_ids,
                              float *out_dists, int64_t *stats, char *err_buf, int err_len);
 
+/* ---- extension: GPU-resident traversal ---------------------------------------------------------
+ * The whole DiskProvider::search_batch (disk_provider.rs:470-678) on the device: one wavefront per
+ * query runs the reference's state machine (sorted result list of L, pop of the smallest unexpanded
+ * (dist, id), neighbour expansion up to the first u32::MAX, visited set, insert_result with Rust's
+ * binary_search_by) against the HBM-resident DB and adjacency — no per-step host round trip.
+ * Results equal diskann_hip_search_batch's up to fp32 summation order.  Shapes the kernel does not
+ * cover (R > 64, n_ep > 64, L > 256, d beyond 2048 SQ8 / 2048 fp32 or not a multiple of 16 / 4) and
+ * the rare query whose boundary-tie spill list overflows run through the host BFS transparently.
+ * stats (may be NULL): [0] distance evaluations, [1] max BFS steps over queries (the lock-step count),
+ * [2] node expansions (pops) on the GPU, [3] queries re-run on the host. */
+
+/* Upload the graph (n x R uint32 adjacency, padded with UINT32_MAX) next to the registered DB. */
+int diskann_hip_register_graph(void *db, const uint32_t *adjacency, int R);
+
+/* Host pointers; synchronous. */
+int diskann_hip_search_batch_resident(void *db, const uint32_t *entry_points, int n_ep, const float *queries, int nq,
+                                      int k, int l_search, int metric, int64_t *out_ids, float *out_dists,
+                                      int64_t *stats, char *err_buf, int err_len);
+
+/* queries / out_ids / out_dists in HBM; launched on `stream` (hipStream_t, NULL = the DB's stream); returns
+ * after the traversal finished (it reads back the per-query flags). */
+int diskann_hip_search_batch_resident_device(void *db, const uint32_t *entry_points, int n_ep,
+                                             const float *queries_dev, int nq, int k, int l_search, int metric,
+                                             int64_t *out_ids_dev, float *out_dists_dev, int64_t *stats, void *stream,
+                                             char *err_buf, int err_len);
+
 int64_t diskann_hip_db_size(void *db);
 
 /* Measurement: record HIP events around every id-gather kernel launch of `db` (on its stream) from now

@@ -222,3 +222,110 @@ def test_bfs_many_queries_parallel_host(gpu, oracle, metric, fmt):
     assert abs(st["steps"] - ost["steps"]) <= 2
     # every row sorted ascending (insert_result keeps the list ordered)
     assert np.all(np.diff(dists, axis=1) >= 0)
+
+
+def _ragged_graph(oracle, x, R, rng, extra_random=2):
+    n = len(x)
+    _, nn = oracle.flat_search(x, x, R - extra_random - 2 + 1, 0)
+    adj = np.full((n, R), 0xFFFFFFFF, np.uint32)
+    adj[:, : R - extra_random - 2] = nn[:, 1:]
+    adj[:, R - extra_random - 2: R - 2] = rng.integers(0, n, (n, extra_random))
+    adj[::7, R - 2] = n + 5          # out of range: skipped, not a sentinel
+    adj[::5, 3] = adj[::5, 2]        # duplicate neighbour
+    deg = rng.integers(R // 2, R + 1, n)
+    adj[np.arange(R)[None, :] >= deg[:, None]] = 0xFFFFFFFF
+    return adj
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+@pytest.mark.parametrize("fmt", [0, 1])
+@pytest.mark.parametrize("L", [40, 128, 200])
+def test_resident_bfs_matches_oracle(gpu, oracle, metric, fmt, L):
+    """GPU-resident traversal (one wavefront per query) vs the DiskProvider::search_batch restatement on
+    a ragged graph (sentinel padding, out-of-range ids, duplicate neighbours, duplicate entry points)."""
+    rng = np.random.default_rng(5)
+    n, d, R = 5000, 64, 32
+    x = rng.standard_normal((n, d)).astype(np.float32)
+    qs = (x[rng.integers(0, n, 300)] + 0.1 * rng.standard_normal((300, d))).astype(np.float32)
+    adj = _ragged_graph(oracle, x, R, rng)
+    eps = [17, 17, 2500, n + 3]
+    if fmt == 0:
+        db = gpu.DiskannDeviceDB(x, 0)
+        kw = dict(vecs=x)
+    else:
+        mins, scale = oracle.sq8_train(x)
+        codes = oracle.sq8_encode(x, mins, scale)
+        db = gpu.DiskannDeviceDB(codes, 1, mins, scale)
+        kw = dict(codes=codes, mins=mins, scale=scale)
+    db.register_graph(adj)
+    ids, dists, st = db.search_batch_resident(eps, qs, 10, L, metric)
+    assert st["pops"] > 0 and st["host_requeries"] == 0
+    oi, od, ost = oracle.diskann_search_batch(adj, eps, qs, 10, L, metric, **kw)
+    assert (ids == oi).mean() >= 0.99
+    same = ids == oi
+    assert np.allclose(dists[same], od[same], rtol=1e-5, atol=1e-4)
+    assert abs(st["evals"] - ost["evals"]) <= 0.01 * ost["evals"]
+    assert abs(st["steps"] - ost["steps"]) <= 2
+    assert np.all(np.diff(dists, axis=1) >= 0)
+
+
+@pytest.mark.parametrize("fmt", [0, 1])
+@pytest.mark.parametrize("L", [8, 24, 64])
+def test_resident_bfs_exact_ties(gpu, oracle, fmt, L):
+    """Small-integer data: every distance is exact in fp32 on both sides, and duplicated rows make exact
+    ties everywhere (the result-list binary search, boundary evictions, the spill list).  The GPU
+    traversal must then reproduce the oracle's ids, distances, evaluation count and step count exactly."""
+    rng = np.random.default_rng(9)
+    n, d, R = 3000, 16, 24
+    base = rng.integers(0, 4, (n // 4, d)).astype(np.float32)
+    x = np.repeat(base, 4, axis=0)[rng.permutation(n)]          # every row 4x
+    x[0, :] = 0.0
+    x[1, :] = 255.0                                              # SQ8: min 0, scale 255 → code == value
+    if fmt == 1:
+        x[2:] = np.clip(x[2:], 0, 3)
+    qs = rng.integers(0, 4, (200, d)).astype(np.float32)
+    adj = _ragged_graph(oracle, x, R, rng, extra_random=4)
+    if fmt == 0:
+        db = gpu.DiskannDeviceDB(x, 0)
+        kw = dict(vecs=x)
+    else:
+        mins, scale = oracle.sq8_train(x)
+        assert np.all(mins == 0) and np.all(scale == 255)
+        codes = oracle.sq8_encode(x, mins, scale)
+        db = gpu.DiskannDeviceDB(codes, 1, mins, scale)
+        kw = dict(codes=codes, mins=mins, scale=scale)
+    db.register_graph(adj)
+    ids, dists, st = db.search_batch_resident([0, 7], qs, 10, L)
+    oi, od, ost = oracle.diskann_search_batch(adj, [0, 7], qs, 10, L, 0, **kw)
+    assert np.array_equal(ids, oi)
+    assert np.array_equal(dists, od)
+    assert st["evals"] == ost["evals"]
+    assert st["steps"] == ost["steps"]
+
+
+def test_resident_bfs_host_fallback_shapes(gpu, oracle):
+    """Shapes outside the kernel (R > 64) run through the host BFS with identical semantics."""
+    rng = np.random.default_rng(2)
+    n, d, R = 1500, 32, 80
+    x = rng.standard_normal((n, d)).astype(np.float32)
+    qs = x[:50] + 0.05
+    adj = _ragged_graph(oracle, x, R, rng)
+    db = gpu.DiskannDeviceDB(x, 0)
+    db.register_graph(adj)
+    ids, dists, st = db.search_batch_resident([3], qs, 10, 32)
+    assert st["pops"] == 0 and st["host_requeries"] == 50
+    hi, hd, _ = db.search_batch(adj, [3], qs, 10, 32)
+    assert np.array_equal(ids, hi)
+
+
+def test_resident_bfs_sql_known_answers(gpu, oracle):
+    case = SQL["diskann_batch"]
+    xb = np.array(case["xb"], np.float32)
+    n = len(xb)
+    adj = np.array([[j for j in range(n) if j != i] for i in range(n)], np.uint32)
+    qs = np.array([qc["q"] for qc in case["queries"]], np.float32)
+    db = gpu.DiskannDeviceDB(xb, 0)
+    db.register_graph(adj)
+    ids, dists, _ = db.search_batch_resident([0], qs, 2, 8)
+    for i, qc in enumerate(case["queries"]):
+        assert ids[i].tolist() == qc["ids"] and np.allclose(dists[i], qc["dists"])
