@@ -499,7 +499,7 @@ def run_diskann(args, torch, dist, hipann, rank, world, dev):
             "cpu_baseline": cpu,
             "setup_s": round(setup_s, 1),
             "diskann": {"graph_build_s": round(t_graph, 1), "bfs_steps_per_batch": int(np.mean(bfs_steps)),
-                        "traversal": "GPU-resident (one wavefront per query)" if resident else
+                        "traversal": "GPU-resident (one 2-wavefront workgroup per query)" if resident else
                                      f"host lock-step BFS ({os.environ.get('HIPANN_BFS_THREADS', '16')} threads) + "
                                      f"per-step id-gather launches",
                         "host_requeries": requeries},

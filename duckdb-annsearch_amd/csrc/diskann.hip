@@ -881,10 +881,10 @@ int diskann_hip_search_batch_resident_device(void *h, const uint32_t *eps, int n
             const int64_t per = std::max<int64_t>(1, std::min<int64_t>(nq, ((int64_t)2 << 30) / (vwords * 4)));
             db->visited.ensure((size_t)per * vwords * 4, db->device);
             db->flags.ensure((size_t)nq * 4, db->device);
-            db->bstats.ensure(24, db->device);
+            db->bstats.ensure(80, db->device);
             db->eps_dev.ensure((size_t)std::max(n_ep, 1) * 4, db->device);
             if (n_ep) HIPANN_CHECK(hipMemcpyAsync(db->eps_dev.p, eps, (size_t)n_ep * 4, hipMemcpyHostToDevice, st));
-            HIPANN_CHECK(hipMemsetAsync(db->bstats.p, 0, 24, st));
+            HIPANN_CHECK(hipMemsetAsync(db->bstats.p, 0, 80, st));
             for (int64_t q0 = 0; q0 < nq; q0 += per) {
                 const int64_t qn = std::min<int64_t>(per, nq - q0);
                 HIPANN_CHECK(hipMemsetAsync(db->visited.p, 0, (size_t)qn * vwords * 4, st));
@@ -895,10 +895,17 @@ int diskann_hip_search_batch_resident_device(void *h, const uint32_t *eps, int n
                                    vwords, out_ids_dev + q0 * kk, out_d_dev + q0 * kk, db->flags.get<int>() + q0,
                                    db->bstats.get<unsigned long long>(), st);
             }
-            unsigned long long hs[3] = {0, 0, 0};
+            unsigned long long hs[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
             HIPANN_CHECK(hipMemcpyAsync(flags.data(), db->flags.p, (size_t)nq * 4, hipMemcpyDeviceToHost, st));
-            HIPANN_CHECK(hipMemcpyAsync(hs, db->bstats.p, 24, hipMemcpyDeviceToHost, st));
+            HIPANN_CHECK(hipMemcpyAsync(hs, db->bstats.p, 80, hipMemcpyDeviceToHost, st));
             HIPANN_CHECK(hipStreamSynchronize(st));
+            if (hs[3] + hs[4] + hs[5] + hs[6] + hs[7] + hs[8]) {  // tuning builds (HIPANN_BFS_PROF)
+                const double st = (double)std::max<unsigned long long>(hs[2], 1);
+                std::fprintf(stderr,
+                             "[bfs-prof] wave-0 cycles per step: select %.0f adjacency %.0f dedupe %.0f visited %.0f "
+                             "dist %.0f insert %.0f\n",
+                             hs[3] / st, hs[4] / st, hs[5] / st, hs[6] / st, hs[7] / st, hs[8] / st);
+            }
             gevals = (int64_t)hs[0];
             gsteps = (int64_t)hs[1];
             gpops = (int64_t)hs[2];

@@ -3,10 +3,12 @@
 // The reference runs the lock-step best-first search on the host and ships every step's candidate
 // vectors to the GPU (rust_lib/src/disk_provider.rs:470-678 → metal_diskann_bridge.mm:255-323): one
 // PCIe round trip per step, host hash sets and heaps.  Here the whole traversal of a query runs in
-// one wavefront with the database (fp32 rows or SQ8 codes), the adjacency (N × R u32) and a per-query
-// visited bitmap resident in HBM.
+// one workgroup of W = 2 wavefronts with the database (fp32 rows or SQ8 codes), the adjacency (N × R
+// u32) and a per-query visited bitmap resident in HBM.  Wave 0 runs the state machine; each step's
+// fresh neighbours are split over the W waves for the distance gather (P rows in flight per wave,
+// unconditional loads, packed-fp32 arithmetic, one reduce-scatter butterfly for P rows).
 //
-// Exactness.  The wave reproduces the reference's per-query state machine step for step:
+// Exactness.  Wave 0 reproduces the reference's per-query state machine step for step:
 //   * result: the sorted list of ≤ L (dist, id), register-resident (element e = s·64 + lane in slot
 //     s), insert position by Rust's slice::binary_search_by with partial_cmp (std ≥ 1.82), shift,
 //     truncate to L (insert_result, disk_provider.rs:656-678);
@@ -32,6 +34,18 @@
 
 namespace hipann {
 namespace {
+
+#ifndef HIPANN_BFS_W
+#define HIPANN_BFS_W 2  // wavefronts per query (tuning builds: -DHIPANN_BFS_W=1/4)
+#endif
+#ifndef HIPANN_BFS_PROF
+#define HIPANN_BFS_PROF 0  // tuning builds: per-phase shader-clock totals of wave 0 into stats[3..6]
+#endif
+#ifndef HIPANN_BFS_RV
+#define HIPANN_BFS_RV 128  // VGPRs of row data in flight per lane (rows_in_flight)
+#endif
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr unsigned kNone = 0xffffffffu;
 constexpr unsigned kExpanded = 0x80000000u;
@@ -63,17 +77,33 @@ __device__ __forceinline__ uint64_t wmin_u64(uint64_t v) {
     }
     return v;
 }
-__device__ __forceinline__ float up1_f(float v, int lane) {
-    return __int_as_float(__builtin_amdgcn_ds_bpermute(((lane - 1) & 63) << 2, __float_as_int(v)));
+// lane i ← lane i − 1 (DPP wave_shr:1; lane 0 keeps its own value and is overwritten by the caller)
+__device__ __forceinline__ float up1_f(float v, int) {
+    const int x = __float_as_int(v);
+    return __int_as_float(__builtin_amdgcn_update_dpp(x, x, 0x138, 0xF, 0xF, false));
 }
-__device__ __forceinline__ unsigned up1_u(unsigned v, int lane) {
-    return (unsigned)__builtin_amdgcn_ds_bpermute(((lane - 1) & 63) << 2, (int)v);
+__device__ __forceinline__ unsigned up1_u(unsigned v, int) {
+    return (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x138, 0xF, 0xF, false);
 }
 
-// dims per 16-byte chunk: 16 SQ8 codes or 4 floats; lane `l`, chunk t covers chunk index l + 64t
-template <bool SQ8> struct Fmt {
-    static constexpr int kDims = SQ8 ? 16 : 4;
+// Row chunks: 8 SQ8 codes (8 B; 1536 codes = 3 chunks per lane exactly) or 4 floats (16 B); lane `l`,
+// chunk t covers chunk index l + 64t.
+template <bool SQ8> struct Fmt;
+template <> struct Fmt<true> {
+    static constexpr int kDims = 8;
+    using Chunk = uint2;
 };
+template <> struct Fmt<false> {
+    static constexpr int kDims = 4;
+    using Chunk = uint4;
+};
+// Rows in flight per wave for a row of `vg` VGPRs per lane: the largest power of two ≤ 32 within a
+// budget of HIPANN_BFS_RV VGPRs of row data.
+constexpr int rows_in_flight(int vg) {
+    int p = 1;
+    while (p < 32 && 2 * p * vg <= HIPANN_BFS_RV) p *= 2;
+    return p;
+}
 
 template <int S>
 struct ResultList {
@@ -93,8 +123,22 @@ struct ResultList {
         for (int t = 1; t < S; ++t) if (s == t) v = id[t];
         return rl_u(v, e & 63);
     }
-    // slice::binary_search_by(|p| p.0.partial_cmp(&dist).unwrap_or(Equal)).unwrap_or_else(|e| e)
-    __device__ __forceinline__ int rust_pos(float dist, int len) const {
+    // slice::binary_search_by(|p| p.0.partial_cmp(&dist).unwrap_or(Equal)).unwrap_or_else(|e| e).
+    // With no element equal to dist and no NaN on either side the answer is the unique insertion
+    // point, the count of elements < dist (two ballots); otherwise Rust's probe sequence decides
+    // which of the equal elements it lands on, replayed exactly by rust_pos_probe.
+    __device__ __forceinline__ int rust_pos(float dist, int len, int lane) const {
+        int lt = 0;
+        bool special = dist != dist;
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const bool in = s * 64 + lane < len;
+            lt += __popcll(__ballot(in && d[s] < dist));
+            special |= __ballot(in && (d[s] == dist || d[s] != d[s])) != 0;
+        }
+        return special ? rust_pos_probe(dist, len) : lt;
+    }
+    __device__ __forceinline__ int rust_pos_probe(float dist, int len) const {
         if (len == 0) return 0;
         int size = len, base = 0;
         while (size > 1) {
@@ -129,109 +173,169 @@ struct ResultList {
     }
 };
 
-template <int S, int T, bool SQ8, bool IP>
-__global__ void __launch_bounds__(64)
+// Cross-lane xor exchange: DPP inside a 16-lane row (offsets 1, 2, 4, 8), ds_bpermute beyond.
+// `o` is a compile-time constant after unrolling, so only one branch survives.
+__device__ __forceinline__ float xshfl(float x, int o) {
+    const int v = __float_as_int(x);
+    int r;
+    if (o == 1) r = __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false);        // quad_perm [1,0,3,2]
+    else if (o == 2) r = __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    else if (o == 4) {                                                                // (m ^ 7) ^ 3
+        const int h = __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false);
+        r = __builtin_amdgcn_update_dpp(h, h, 0x1B, 0xF, 0xF, false);
+    } else if (o == 8) r = __builtin_amdgcn_update_dpp(v, v, 0x128, 0xF, 0xF, false);  // row_ror:8
+    else return __shfl_xor(x, o);
+    return __int_as_float(r);
+}
+
+// Sum over the 64 lanes of P per-lane partials at once (reduce-scatter butterfly): step s halves the
+// live values by exchanging with lane ^ (32 >> s), so P rows cost P − 1 + 6 − log2 P exchanges instead
+// of 6·P.  On return, lanes [64/P·r, 64/P·(r+1)) hold the total of row r.
+template <int P>
+__device__ __forceinline__ float reduce_rows(float (&v)[P], int lane) {
+    constexpr int LP = P >= 64 ? 6 : P >= 32 ? 5 : P >= 16 ? 4 : P >= 8 ? 3 : P >= 4 ? 2 : P >= 2 ? 1 : 0;
+    static_assert((1 << LP) == P, "P must be a power of two <= 64");
+#pragma unroll
+    for (int s = 0; s < LP; ++s) {
+        const int o = 32 >> s, half = P >> (s + 1);
+        const int bm = (lane & o) ? -1 : 0;  // bit-mask selects: a `b ? v[i] : v[i + half]` becomes a
+#pragma unroll                               // dynamically indexed (scratch) array in hipcc
+        for (int i = 0; i < half; ++i) {
+            const int lo = __float_as_int(v[i]), hi = __float_as_int(v[i + half]);
+            const float send = __int_as_float((lo & bm) | (hi & ~bm));
+            const float keep = __int_as_float((hi & bm) | (lo & ~bm));
+            v[i] = keep + xshfl(send, o);
+        }
+    }
+    float x = v[0];
+#pragma unroll
+    for (int o = 32 >> LP; o >= 1; o >>= 1) x += xshfl(x, o);
+    return x;
+}
+
+// One block of W wavefronts per query.  Wave 0 owns the search state (result list, spill list, stop
+// rule) and does the expansions; a step's fresh neighbours go to all W waves through LDS, each wave
+// loads its share of the rows with P rows in flight, and the distances come back through LDS for
+// wave 0's inserts (two barriers per step; steps without fresh neighbours stay inside wave 0).
+template <int S, int T, int W, bool SQ8, bool IP>
+__global__ void __launch_bounds__(64 * W)
 diskann_bfs(const float *__restrict__ Qs, int nq, int d, const uint8_t *__restrict__ data,
             const float2 *__restrict__ ab, const uint32_t *__restrict__ adj, int R, uint32_t N,
             const uint32_t *__restrict__ eps, int n_ep, int k, int L, uint32_t *__restrict__ visited,
             int64_t vwords, int64_t *__restrict__ out_ids, float *__restrict__ out_d, int *__restrict__ flags,
             unsigned long long *__restrict__ stats) {
     constexpr int DC = Fmt<SQ8>::kDims;
-    constexpr int P = 8 / T;  // rows in flight per distance batch
+    using Chunk = typename Fmt<SQ8>::Chunk;
+    constexpr int CB = (int)sizeof(Chunk);
+    constexpr int P = rows_in_flight(T * CB / 4);  // rows in flight per wave
+    constexpr int LP = P >= 32 ? 5 : P >= 16 ? 4 : P >= 8 ? 3 : P >= 4 ? 2 : P >= 2 ? 1 : 0;
+    __shared__ uint32_t s_ids[64];  // this step's fresh neighbours, in neighbour order
+    __shared__ float s_dist[64];    // their distances
+    __shared__ int s_cnt;           // how many; −1 = the query is done
+    __shared__ __attribute__((aligned(16))) uint32_t s_nb[64];  // wave 0: the expansion's neighbour ids
     const int qi = blockIdx.x;
     if (qi >= nq) return;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const size_t rowbytes = SQ8 ? (size_t)d : (size_t)d * 4;
     uint32_t *vis = visited + (int64_t)qi * vwords;
     const float *q = Qs + (int64_t)qi * d;
 
-    // per-lane query terms for the lane's dims (chunk t: dims DC·(lane + 64t) ..)
-    float qp[T][DC], av[T][DC];
+    // per-lane query terms for the lane's dims (chunk t: dims DC·(lane + 64t) ..), as pairs for the
+    // packed-fp32 VALU (v_pk_fma_f32: two lanes of arithmetic per instruction)
+    f32x2 qp[T][DC / 2], av[T][DC / 2];
     float cq = 0.f;
 #pragma unroll
     for (int t = 0; t < T; ++t)
 #pragma unroll
         for (int e = 0; e < DC; ++e) {
             const int dim = DC * (lane + 64 * t) + e;
-            float qv = 0.f, a = 0.f, b = 0.f;
-            if (dim < d) {
-                qv = q[dim];
-                if (SQ8) { const float2 p = ab[dim]; a = p.x; b = p.y; }
-            }
+            // unconditional (clamped) loads: a branch per element serialises them on vmcnt(0)
+            const bool in = dim < d;
+            const int dc = in ? dim : 0;
+            float qv = in ? q[dc] : 0.f, a = 0.f, b = 0.f;
             if (SQ8) {
-                if (IP) { qp[t][e] = qv * a; cq = fmaf(qv, b, cq); }
-                else { qp[t][e] = qv - b; }
-                av[t][e] = a;
-            } else {
-                qp[t][e] = qv;
-                av[t][e] = 0.f;
+                const float2 p = ab[dc];
+                a = in ? p.x : 0.f;
+                b = in ? p.y : 0.f;
             }
+            float x, y;
+            if (SQ8) {
+                if (IP) { x = qv * a; cq = fmaf(qv, b, cq); }
+                else { x = qv - b; }
+                y = a;
+            } else {
+                x = qv;
+                y = 0.f;
+            }
+            qp[t][e >> 1][e & 1] = x;
+            av[t][e >> 1][e & 1] = y;
         }
     if (SQ8 && IP) cq = wsum(cq);
 
-    auto load_row = [&](uint32_t rid, uint4 (&v)[T]) {
+    auto load_row = [&](uint32_t rid, Chunk (&v)[T]) {
         const uint8_t *base = data + (size_t)rid * rowbytes;
 #pragma unroll
         for (int t = 0; t < T; ++t) {
-            const size_t off = (size_t)16 * (lane + 64 * t);
-            v[t] = off < rowbytes ? *reinterpret_cast<const uint4 *>(base + off) : make_uint4(0, 0, 0, 0);
+            // unconditional loads (a load under a branch costs a vmcnt(0) per row): past the row's
+            // end a lane re-reads the row's first chunk and the value is zeroed afterwards
+            const size_t off = (size_t)CB * (lane + 64 * t);
+            const bool in = off < rowbytes;
+            const Chunk c = *reinterpret_cast<const Chunk *>(base + (in ? off : 0));
+            v[t] = in ? c : Chunk{};
         }
     };
-    auto row_dist = [&](const uint4 (&v)[T]) -> float {
-        float acc = 0.f;
+    // this lane's partial of one row's distance (the cross-lane sum is reduce_rows)
+    auto row_part = [&](const Chunk (&v)[T]) -> float {
+        f32x2 acc = {0.f, 0.f};
 #pragma unroll
         for (int t = 0; t < T; ++t) {
-            const unsigned w[4] = {v[t].x, v[t].y, v[t].z, v[t].w};
-            if (SQ8) {
+            if constexpr (SQ8) {
+                const unsigned w[2] = {v[t].x, v[t].y};
 #pragma unroll
-                for (int e = 0; e < 16; ++e) {
-                    const float c = (float)((w[e >> 2] >> (8 * (e & 3))) & 0xffu);
-                    if (IP) acc = fmaf(qp[t][e], c, acc);
-                    else { const float tt = fmaf(-c, av[t][e], qp[t][e]); acc = fmaf(tt, tt, acc); }
+                for (int e = 0; e < 4; ++e) {
+                    const unsigned ww = w[e >> 1] >> (16 * (e & 1));
+                    const f32x2 c = {(float)(ww & 0xffu), (float)((ww >> 8) & 0xffu)};
+                    if (IP) acc = __builtin_elementwise_fma(qp[t][e], c, acc);
+                    else {
+                        const f32x2 tt = __builtin_elementwise_fma(-c, av[t][e], qp[t][e]);
+                        acc = __builtin_elementwise_fma(tt, tt, acc);
+                    }
                 }
             } else {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float x = __uint_as_float(w[e]);
-                    if (IP) acc = fmaf(qp[t][e], x, acc);
-                    else { const float tt = qp[t][e] - x; acc = fmaf(tt, tt, acc); }
+                for (int e = 0; e < 2; ++e) {
+                    const f32x2 x = {__uint_as_float(e ? v[t].z : v[t].x), __uint_as_float(e ? v[t].w : v[t].y)};
+                    if (IP) acc = __builtin_elementwise_fma(qp[t][e], x, acc);
+                    else {
+                        const f32x2 tt = qp[t][e] - x;
+                        acc = __builtin_elementwise_fma(tt, tt, acc);
+                    }
                 }
             }
         }
-        acc = wsum(acc);
-        return IP ? -(acc + cq) : acc;
+        return acc[0] + acc[1];
     };
-    // distances of the rows named by `nb` on the lanes of mask m (lane-indexed result)
-    auto dists = [&](uint64_t m, uint32_t nb) -> float {
-        float mine = 0.f;
-        while (m) {
-            int js[P];
-            uint32_t ids[P];
-            int cnt = 0;
+    // Distances of the step's fresh rows s_ids[0, cnt) into s_dist: wave w takes a contiguous share,
+    // P rows in flight at a time (rows past the share re-load its last row; their sums are dropped).
+    auto dist_phase = [&](int cnt) {
+        const int per = (cnt + W - 1) / W;
+        const int r_begin = wave * per;
+        const int r_end = cnt < r_begin + per ? cnt : r_begin + per;
+        for (int r0 = r_begin; r0 < r_end; r0 += P) {
+            Chunk v[P][T];
 #pragma unroll
             for (int p = 0; p < P; ++p) {
-                js[p] = -1;
-                ids[p] = 0;
-                if (m) {
-                    const int j = __ffsll((unsigned long long)m) - 1;
-                    m &= m - 1;
-                    js[p] = j;
-                    ids[p] = rl_u(nb, j);
-                    cnt++;
-                }
+                const int r = r0 + p < r_end ? r0 + p : r_end - 1;
+                load_row((uint32_t)__builtin_amdgcn_readfirstlane((int)s_ids[r]), v[p]);
             }
-            uint4 v[P][T];
+            float part[P];
 #pragma unroll
-            for (int p = 0; p < P; ++p)
-                if (p < cnt) load_row(ids[p], v[p]);
-#pragma unroll
-            for (int p = 0; p < P; ++p)
-                if (p < cnt) {
-                    const float dd = row_dist(v[p]);
-                    if (lane == js[p]) mine = dd;
-                }
+            for (int p = 0; p < P; ++p) part[p] = row_part(v[p]);
+            const float tot = reduce_rows<P>(part, lane);
+            const int r = r0 + (lane >> (6 - LP));
+            if ((lane & ((64 >> LP) - 1)) == 0 && r < r_end) s_dist[r] = IP ? -(tot + cq) : tot;
         }
-        return mine;
     };
 
     ResultList<S> res;
@@ -244,8 +348,24 @@ diskann_bfs(const float *__restrict__ Qs, int nq, int d, const uint8_t *__restri
     unsigned long long evals = 0;
     int steps = 0;
 
+    const uint64_t lanes_below = (1ull << lane) - 1;  // lane 63: all lower lanes (no overflow)
+#if HIPANN_BFS_PROF
+    unsigned long long tprof[6] = {0, 0, 0, 0, 0, 0};
+    long long tmark = clock64();
+#define BFS_T(i)                            \
+    do {                                    \
+        const long long t1_ = clock64();    \
+        tprof[i] += (unsigned long long)(t1_ - tmark); \
+        tmark = t1_;                        \
+    } while (0)
+#else
+#define BFS_T(i) \
+    do {         \
+    } while (0)
+#endif
+
     // ---- seeds (disk_provider.rs:524-538): visited insert in order, distance, push, stable sort ----
-    {
+    if (wave == 0) {
         const uint32_t ep = lane < n_ep ? eps[lane] : kNone;
         const bool ok = lane < n_ep && ep < N;
         bool dup = false;
@@ -259,10 +379,17 @@ diskann_bfs(const float *__restrict__ Qs, int nq, int d, const uint8_t *__restri
         if (fresh) atomicOr(vis + (ep >> 5), 1u << (ep & 31));
         const uint64_t m = __ballot(fresh);
         evals += __popcll(m);
-        const float dd = dists(m, ep);
-        // stable sort by distance: key (dist, lane) lexicographic; non-seeds last
-        float key = fresh ? dd : __builtin_inff();
-        int src = fresh ? lane : 64 + lane;
+        if (fresh) s_ids[__popcll(m & lanes_below)] = ep;
+        if (lane == 0) s_cnt = __popcll(m);
+    }
+    __syncthreads();
+    if (s_cnt > 0) dist_phase(s_cnt);
+    __syncthreads();
+    if (wave == 0) {
+        // stable sort by distance: key (dist, rank) lexicographic (rank = seed order); non-seeds last
+        const int c = s_cnt;
+        float key = lane < c ? s_dist[lane] : __builtin_inff();
+        int src = lane < c ? lane : 64 + lane;
 #pragma unroll
         for (int size = 2; size <= 64; size <<= 1)
 #pragma unroll
@@ -273,14 +400,17 @@ diskann_bfs(const float *__restrict__ Qs, int nq, int d, const uint8_t *__restri
                 const bool o_less = ok2 < key || (ok2 == key && os < src);  // (key, src) pairs are unique
                 if (keep_min == o_less) { key = ok2; src = os; }
             }
-        len = __popcll(m);
-        const uint32_t sid = __shfl(ep, src & 63);
+        len = c;
+        const uint32_t sid = s_ids[src & 63];
         if (lane < len) { res.d[0] = key; res.id[0] = sid; }
         if (len > L) flag = 1;  // more seeds than L: host path
     }
 
     // ---- lock-step iterations of this query (disk_provider.rs:545-652) ----
-    while (!flag) {
+    for (;;) {
+      int cnt = -1;  // fresh neighbours of this step's expansion (−1: the query is done)
+      if (wave == 0) {
+        while (!flag) {
         steps++;
         const float thr = len >= L ? res.get_d(L - 1) : __builtin_inff();
         uint64_t best = ~0ull;
@@ -330,36 +460,63 @@ diskann_bfs(const float *__restrict__ Qs, int nq, int d, const uint8_t *__restri
                 nspill--;
             }
         }
+        BFS_T(0);
         // expand: neighbours up to the first sentinel, ids < N, visited insert in order
         const uint32_t nb = lane < R ? adj[(size_t)cid * R + lane] : kNone;
         const uint64_t sent = __ballot(lane < R && nb == kNone);
+        BFS_T(1);
         const int first = sent ? __ffsll((unsigned long long)sent) - 1 : R;
         const bool valid = lane < first && nb < N;
+        // first occurrence wins: compare with every earlier lane's id through LDS broadcast reads
+        // (invalid lanes hold 0x80000000 | lane, which no id < N ≤ 2^31 − 1 equals)
+        s_nb[lane] = valid ? nb : (0x80000000u | (unsigned)lane);
+        __builtin_amdgcn_wave_barrier();
         bool dup = false;
-        uint64_t vm = __ballot(valid);
-        while (vm) {
-            const int i = __ffsll((unsigned long long)vm) - 1;
-            vm &= vm - 1;
-            if (valid && lane > i && nb == rl_u(nb, i)) dup = true;
+        for (int i = 0; i < first; i += 4) {
+            const uint4 w = *reinterpret_cast<const uint4 *>(s_nb + i);
+            dup |= (i < lane && w.x == nb) | (i + 1 < lane && w.y == nb) | (i + 2 < lane && w.z == nb) |
+                   (i + 3 < lane && w.w == nb);
         }
+        dup = dup && valid;
+        __builtin_amdgcn_wave_barrier();
+        BFS_T(2);
         bool fresh = false;
         if (valid && !dup) {
             const unsigned bit = 1u << (nb & 31);
             fresh = !(atomicOr(vis + (nb >> 5), bit) & bit);
         }
         const uint64_t m = __ballot(fresh);
+        BFS_T(3);
         if (!m) continue;
         evals += __popcll(m);
-        const float dd = dists(m, nb);
+        if (fresh) s_ids[__popcll(m & lanes_below)] = nb;  // neighbour order
+        cnt = __popcll(m);
+        break;
+        }  // while (!flag)
+        if (lane == 0) s_cnt = cnt;
+      }  // wave 0
+      __syncthreads();
+      cnt = s_cnt;
+      if (cnt < 0) break;
+      dist_phase(cnt);
+      __syncthreads();
+      if (wave == 0) {
+        BFS_T(4);
         // insert_result in neighbour order
-        uint64_t mm = m;
-        while (mm) {
-            const int j = __ffsll((unsigned long long)mm) - 1;
-            mm &= mm - 1;
+        const float dd = lane < cnt ? s_dist[lane] : 0.f;
+        const unsigned nbr = lane < cnt ? s_ids[lane] : kNone;
+        // The threshold result[L−1] only falls once the list is full, so a candidate at or above the
+        // step's starting threshold is rejected whenever its turn comes: visit only the others.
+        const bool full = len >= L;
+        const float thr0 = full ? res.get_d(len - 1) : 0.f;
+        uint64_t am = __ballot(lane < cnt && (!full || dd < thr0));
+        while (am) {
+            const int j = __ffsll((unsigned long long)am) - 1;
+            am &= am - 1;
             const float dj = rl_f(dd, j);
-            const unsigned idj = rl_u(nb, j);
+            const unsigned idj = rl_u(nbr, j);
             if (!(len < L || dj < res.get_d(len - 1))) continue;
-            const int pos = res.rust_pos(dj, len);
+            const int pos = res.rust_pos(dj, len, lane);
             float evd = 0.f;
             unsigned evi = kNone;
             if (len == L) { evd = res.get_d(L - 1); evi = res.get_id(L - 1); }
@@ -379,7 +536,15 @@ diskann_bfs(const float *__restrict__ Qs, int nq, int d, const uint8_t *__restri
                 }
             }
         }
+        BFS_T(5);
+      }
     }
+    if (wave != 0) return;
+#if HIPANN_BFS_PROF
+    if (lane == 0)
+        for (int i = 0; i < 6; ++i) atomicAdd(stats + 3 + i, tprof[i]);
+#endif
+#undef BFS_T
 
     // ---- first k of the result (ffi.rs:759-762 padding) ----
     for (int e0 = 0; e0 < k; e0 += 64) {
@@ -404,10 +569,10 @@ diskann_bfs(const float *__restrict__ Qs, int nq, int d, const uint8_t *__restri
 
 }  // namespace
 
-// S: result slots per lane (L ≤ 64·S); T: 16-byte chunks per lane (d ≤ 64·T·dims-per-chunk)
+// S: result slots per lane (L ≤ 64·S); T: row chunks per lane (8 codes or 4 floats each)
 bool diskann_bfs_supported(int d, int fmt, int R, int n_ep, int L, uint32_t N) {
-    const int dc = fmt == 1 ? 16 : 4;
-    return d > 0 && d % dc == 0 && d <= 64 * dc * (fmt == 1 ? 2 : 8) && R > 0 && R <= 64 && n_ep >= 0 &&
+    const int dc = fmt == 1 ? 8 : 4;
+    return d > 0 && d % dc == 0 && d <= 64 * dc * (fmt == 1 ? 4 : 8) && R > 0 && R <= 64 && n_ep >= 0 &&
            n_ep <= 64 && L >= 1 && L <= 256 && N <= 0x7fffffffu;
 }
 
@@ -416,26 +581,30 @@ void launch_diskann_bfs(const float *Q, int nq, int d, int fmt, const void *data
                         int metric, uint32_t *visited, int64_t vwords, int64_t *out_ids, float *out_d, int *flags,
                         unsigned long long *stats, hipStream_t st) {
     if (nq <= 0) return;
-    const int dc = fmt == 1 ? 16 : 4;
-    const int chunks = (d / dc + 63) / 64;  // 16-B chunks per lane
-    const int T = chunks <= 1 ? 1 : chunks <= 2 ? 2 : chunks <= 4 ? 4 : 8;
+    HIPANN_REQUIRE(diskann_bfs_supported(d, fmt, R, n_ep, L, N), "diskann_bfs: unsupported shape");
+    const int dc = fmt == 1 ? 8 : 4;
+    const int chunks = (d / dc + 63) / 64;  // row chunks per lane
     const bool s2 = L <= 128;
     const uint8_t *x = static_cast<const uint8_t *>(data);
-    dim3 grid((unsigned)nq), block(64);
-#define HIPANN_BFS(S_, T_, SQ_, IP_)                                                                           \
-    hipLaunchKernelGGL((diskann_bfs<S_, T_, SQ_, IP_>), grid, block, 0, st, Q, nq, d, x, ab, adj, R, N, eps, n_ep, \
+    constexpr int W = HIPANN_BFS_W;
+    dim3 grid((unsigned)nq), block(64 * W);
+#define HIPANN_BFS(S_, T_, SQ_, IP_)                                                                              \
+    hipLaunchKernelGGL((diskann_bfs<S_, T_, W, SQ_, IP_>), grid, block, 0, st, Q, nq, d, x, ab, adj, R, N, eps, n_ep, \
                        k, L, visited, vwords, out_ids, out_d, flags, stats)
 #define HIPANN_BFS_S(T_, SQ_, IP_) \
     do { if (s2) HIPANN_BFS(2, T_, SQ_, IP_); else HIPANN_BFS(4, T_, SQ_, IP_); } while (0)
 #define HIPANN_BFS_M(T_, SQ_) \
     do { if (metric == 1) HIPANN_BFS_S(T_, SQ_, true); else HIPANN_BFS_S(T_, SQ_, false); } while (0)
     if (fmt == 1) {
-        if (T == 1) HIPANN_BFS_M(1, true);
-        else HIPANN_BFS_M(2, true);
+        if (chunks <= 1) HIPANN_BFS_M(1, true);
+        else if (chunks <= 2) HIPANN_BFS_M(2, true);
+        else if (chunks <= 3) HIPANN_BFS_M(3, true);
+        else HIPANN_BFS_M(4, true);
     } else {
-        if (T == 1) HIPANN_BFS_M(1, false);
-        else if (T == 2) HIPANN_BFS_M(2, false);
-        else if (T == 4) HIPANN_BFS_M(4, false);
+        if (chunks <= 1) HIPANN_BFS_M(1, false);
+        else if (chunks <= 2) HIPANN_BFS_M(2, false);
+        else if (chunks <= 4) HIPANN_BFS_M(4, false);
+        else if (chunks <= 6) HIPANN_BFS_M(6, false);
         else HIPANN_BFS_M(8, false);
     }
 #undef HIPANN_BFS_M

@@ -547,7 +547,7 @@ class DiskannDeviceDB:
             raise HipAnnError("diskann_hip_register_graph failed")
 
     def search_batch_resident(self, entry_points, queries, k: int, l_search: int, metric: int = METRIC_L2):
-        """DiskProvider::search_batch with the traversal itself on the GPU (one wavefront per query).
+        """DiskProvider::search_batch with the traversal itself on the GPU (one 2-wavefront workgroup per query).
         Returns (ids, dists, stats)."""
         eps = np.ascontiguousarray(entry_points, np.uint32)
         q = np.ascontiguousarray(queries, np.float32)
