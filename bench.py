@@ -287,7 +287,9 @@ def main():
         b_alg = extra.get("scan_bytes_per_batch_local", 0.0)
         form = index.form
         kname, fname = {0: ("ivf_scan_mfma", "decomposed, fp32 MFMA"), 1: ("ivf_scan_topk", "direct, VALU"),
-                        2: ("ivf_scan_dot", "decomposed, VALU")}[form]
+                        2: ("ivf_scan_dot", "decomposed, VALU"),
+                        3: ("ivf_scan_mfma_bf", "decomposed, bf16 MFMA over a 3-term split (6 products)"),
+                        4: ("ivf_scan_mfma_bf", "decomposed, bf16 MFMA over a 2-term split (3 products)")}[form]
         fpp = 3.0 if form == 1 else 2.0  # flop per (query, row, dim): sub + fma vs fma
         achieved = b_alg / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -33,7 +33,11 @@ enum Metric : int { kL2 = 0, kIP = 1 };
 // IVF list-scan distance form (hipann_ivf_set_form): ‖q‖²+‖x‖²−2q·x (FAISS GPU / faiss-metal IVF) on the
 // matrix cores, or the direct Σ(q−x)² of FAISS's CPU IndexIVFFlat scanner.
 // kFormDecomposedValu: the same form on the VALU kernel (ivf_scan_dot), kept for A/B measurement.
-enum IvfForm : int { kFormDecomposed = 0, kFormDirect = 1, kFormDecomposedValu = 2 };
+// kFormSplit3 / kFormSplit2: the decomposed form on the bf16 matrix cores over a 3-term (fp32-level
+// products) / 2-term bf16 split of both operands (ivf_mfma.hip, split-bf16 variant).
+enum IvfForm : int { kFormDecomposed = 0, kFormDirect = 1, kFormDecomposedValu = 2, kFormSplit3 = 3, kFormSplit2 = 4 };
+__host__ __device__ inline bool ivf_form_split(int f) { return f == kFormSplit3 || f == kFormSplit2; }
+__host__ __device__ inline int ivf_form_terms(int f) { return f == kFormSplit3 ? 3 : 2; }
 
 // XCD-aware block remap (cdna_hip_programming.md §5.5 T1, bijective form): blocks b and b+8 are
 // dealt to the same XCD; map so that each XCD receives a contiguous run of logical blocks.

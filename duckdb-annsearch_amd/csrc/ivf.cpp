@@ -157,7 +157,9 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     // the decomposed forms need float4 rows (else the direct kernel, also on the GPU); the MFMA kernel
     // keeps 16-lane lists (k <= 16) and the item's queries in LDS (else the VALU decomposed kernel)
     int form = ix.form != kFormDirect && !bigk && ivf_dot_supported(xq, d, sh.codes) ? ix.form : kFormDirect;
+    if (ivf_form_split(form) && !ivf_mfma_bf_supported(xq, d, sh.codes, k, ivf_form_terms(form))) form = kFormDecomposed;
     if (form == kFormDecomposed && !ivf_mfma_supported(xq, d, sh.codes, k)) form = kFormDecomposedValu;
+    const bool tiled = form == kFormDecomposed || ivf_form_split(form);  // the matrix-core scans
     const int group = ivf_group_size(form, d);
     launch_ivf_plan(sh.coarse_i.get<int64_t>(), nq, np, sh.list_len.get<int>(), nlist, group, sh.cnt.get<int>(),
                     sh.bucket_off.get<int>(), sh.item_off.get<int>(), sh.cursor.get<int>(), sh.bucket.get<int>(),
@@ -175,18 +177,26 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
         qn = sh.qn.get<float>();
     }
     unsigned *qbound = nullptr;
-    if (form == kFormDecomposed) {  // every query's bound starts at +inf (order-preserving bits 0xff800000)
+    if (tiled) {  // every query's bound starts at +inf (order-preserving bits 0xff800000)
         sh.qbound.ensure(sizeof(unsigned) * (size_t)nq, sh.device);
         qbound = sh.qbound.get<unsigned>();
         HIPANN_CHECK(hipMemsetD32Async((hipDeviceptr_t)qbound, 0xff800000, (size_t)nq, st));
     }
-    if (form == kFormDecomposed) ensure_tiled_codes(sh, d, nlist, st);
+    if (tiled) ensure_tiled_codes(sh, d, nlist, st);
+    if (ivf_form_split(form))
+        sh.qsplit.ensure((size_t)ivf_mfma_bf_qsplit_bytes(nq, d, ivf_form_terms(form)), sh.device);
     {
         ScopedTiming t(ix.timer_main, st);
         if (bigk)
             launch_ivf_scan_bigk(xq, d, metric, sh.codes, sh.list_off.get<int64_t>(), sh.coarse_i.get<int64_t>(),
                                  nq * np, np, sh.slot_off.get<int>(), nq * np * std::max(sh.max_nch, 1), k,
                                  sh.part_d.get<float>(), sh.part_i.get<int>(), st);
+        else if (ivf_form_split(form))
+            launch_ivf_scan_mfma_bf(ivf_form_terms(form), xq, nq, sh.qsplit.p, qn, d, metric, sh.codes_t.get<float>(),
+                                    sh.tpass_off.get<int64_t>(), sh.xnorm.get<float>(), sh.list_off.get<int64_t>(),
+                                    sh.cnt.get<int>(), sh.bucket_off.get<int>(), sh.item_off.get<int>(),
+                                    sh.bucket.get<int>(), sh.slot_off.get<int>(), nlist, np, k, max_items, qbound,
+                                    sh.part_d.get<float>(), sh.part_i.get<int>(), st);
         else if (form == kFormDecomposed)
             launch_ivf_scan_mfma(xq, qn, d, metric, sh.codes_t.get<float>(), sh.tpass_off.get<int64_t>(),
                                  sh.xnorm.get<float>(), sh.list_off.get<int64_t>(), sh.cnt.get<int>(),
@@ -463,7 +473,7 @@ int hipann_ivf_set_nprobe(void *h, int nprobe) {
 }
 
 int hipann_ivf_set_form(void *h, int form) {
-    if (!h || (form != kFormDecomposed && form != kFormDirect && form != kFormDecomposedValu)) return -1;
+    if (!h || form < kFormDecomposed || form > kFormSplit2) return -1;
     auto *ix = static_cast<IndexBase *>(h);
     if (ix->kind != Kind::IVF) return -1;
     auto *vx = static_cast<IvfIndex *>(ix);

@@ -898,9 +898,11 @@ int64_t ivf_max_items(int64_t nq, int nprobe, int nlist, int max_nch, int64_t nr
     return ceil_div(npairs, (int64_t)group) * std::max(max_nch, 1) + ceil_div(nrows, IVF_CH) + nlist;
 }
 
-int ivf_mfma_group(int d);  // ivf_mfma.hip
+int ivf_mfma_group(int d);            // ivf_mfma.hip
+int ivf_mfma_bf_group(int d, int np);  // ivf_mfma.hip
 
 int ivf_group_size(int form, int d) {
+    if (ivf_form_split(form)) return ivf_mfma_bf_group(d, ivf_form_terms(form));
     return form == kFormDecomposed ? ivf_mfma_group(d) : form == kFormDecomposedValu ? DT_G : IVF_G;
 }
 

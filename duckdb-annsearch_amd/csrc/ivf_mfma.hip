@@ -173,7 +173,7 @@ __device__ __forceinline__ void mf_item(int d, const float *__restrict__ codes_t
     const int nsub = mf_nsub(d);               // 16-dim steps per pass (multiple of MF_P)
     const int npass_all = (int)ceil_div(r1 - r0, MF_PASS);
     const int npass = npass_all > wave ? (npass_all - wave + MF_WAVES - 1) / MF_WAVES : 0;  // wave-uniform
-    const int nstep = npass * nsub;
+
 
     // query validity of the accumulator registers: query qt·16 + 4g + v
     bool qv[QT][4];
@@ -494,6 +494,418 @@ void launch_ivf_scan_mfma(const float *Q, const float *qn, int d, int metric, co
     if (metric == kIP) hipLaunchKernelGGL((ivf_scan_mfma<true>), grid, block, smem, st, MF_LAUNCH_ARGS);
     else hipLaunchKernelGGL((ivf_scan_mfma<false>), grid, block, smem, st, MF_LAUNCH_ARGS);
 #undef MF_LAUNCH_ARGS
+    HIPANN_CHECK(hipGetLastError());
+}
+
+
+// ================================================================================================
+// Split-bf16 variant (forms kFormSplit3 / kFormSplit2): the same item / pass / ring / selection
+// structure, but q·x runs on v_mfma_f32_16x16x32_bf16 (16× the fp32 matrix rate) over an NP-term
+// bf16 split of both operands, x = x₁ + x₂ (+ x₃), each term the round-to-nearest bf16 of what the
+// previous ones leave (exact fp32 subtractions):
+//   NP = 3: products x₁y₁ + x₁y₂ + x₂y₁ + x₁y₃ + x₃y₁ + x₂y₂ (every term ≥ 2⁻²⁴ relative), the
+//           dropped ones ≤ 2⁻²⁶ relative — fp32-level products, fp32 accumulation;
+//   NP = 2: x₁y₁ + x₁y₂ + x₂y₁, ≈ 2⁻¹⁶ relative per product (bf16x3 in the usual naming).
+// The item's queries are split once into LDS ([query][term][32-dim super-step][g][8 bf16]); rows are
+// split in registers as they arrive, once per item for all of its queries.  k-slot order inside a
+// super-step follows the tiled codes: lane (g, m) holds dims 32S + 4g + j and 32S + 16 + 4g + j
+// (j < 4) of row m — the same order is used for the query terms, so any permutation of dims is
+// harmless (q·x does not depend on it).
+typedef __bf16 mb_bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 mb_bf16x2 __attribute__((ext_vector_type(2)));
+typedef float mb_f32x2 __attribute__((ext_vector_type(2)));
+constexpr int MB_PS = MF_P / 2;  // super-steps (two 16-dim steps) in flight per wave
+
+__device__ __forceinline__ unsigned mb_pack(float a, float b) {
+    const mb_bf16x2 v = __builtin_convertvector((mb_f32x2){a, b}, mb_bf16x2);
+    return __builtin_bit_cast(unsigned, v);
+}
+// bf16 pair → the two fp32 values (low half first)
+__device__ __forceinline__ float mb_lo(unsigned p) { return __uint_as_float(p << 16); }
+__device__ __forceinline__ float mb_hi(unsigned p) { return __uint_as_float(p & 0xffff0000u); }
+
+template <int NP>
+struct MbTerms {
+    uint4 t[NP];  // term j: 8 bf16 (k-slot order), two per dword
+};
+// Split 8 fp32 (k-slot order: a = slots 0-3, b = slots 4-7) into NP bf16 terms.
+template <int NP>
+__device__ __forceinline__ MbTerms<NP> mb_split(const mf_f32x4 &a, const mf_f32x4 &b) {
+    MbTerms<NP> o;
+    // pairs as packed fp32 (v_pk_add_f32 does both subtractions of a pair)
+    mb_f32x2 x[4] = {{a[0], a[1]}, {a[2], a[3]}, {b[0], b[1]}, {b[2], b[3]}};
+    unsigned w[NP][4];
+#pragma unroll
+    for (int j = 0; j < NP; ++j)
+#pragma unroll
+        for (int pr = 0; pr < 4; ++pr) {
+            const unsigned pk = mb_pack(x[pr][0], x[pr][1]);
+            w[j][pr] = pk;
+            if (j + 1 < NP) x[pr] -= (mb_f32x2){mb_lo(pk), mb_hi(pk)};
+        }
+#pragma unroll
+    for (int j = 0; j < NP; ++j) o.t[j] = make_uint4(w[j][0], w[j][1], w[j][2], w[j][3]);
+    return o;
+}
+__host__ __device__ inline int mb_nsuper(int d) { return mf_nsub(d) / 2; }  // mf_nsub is a multiple of 6
+// LDS dwords per query for one of NH dim phases: NP terms × super-steps/NH × 4 groups × 4 dwords, + 8
+// (≡ 8 mod 64)
+__host__ __device__ inline int mb_stride(int d, int np, int nh) { return np * (mb_nsuper(d) / nh) * 16 + 8; }
+inline int mb_group_nh(int d, int np, int nh) {
+    const int g = (int)(MF_LDS_MAX / ((size_t)mb_stride(d, np, nh) * 4)) / 16 * 16;
+    return g < 16 * MF_QTMAX ? g : 16 * MF_QTMAX;
+}
+// Dim phases: the whole split query image in LDS when 48 queries fit (NH = 1), else the image of one
+// half of the dims at a time (NH = 2: 3 terms × 768 dims × 48 queries = 221 KiB > 160 KiB of LDS),
+// swapped between the halves of every 32-row pass (needs MB_PS | super-steps per half).
+inline int mb_phases(int d, int np) {
+    if (mb_group_nh(d, np, 1) >= 16 * MF_QTMAX) return 1;
+    return mb_nsuper(d) % (2 * MB_PS) == 0 ? 2 : 1;
+}
+inline int mb_group(int d, int np) { return mb_group_nh(d, np, mb_phases(d, np)); }
+
+__device__ __forceinline__ mf_f32x4 mb_mfma(const uint4 &a, const uint4 &b, const mf_f32x4 &c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(mb_bf16x8, a), __builtin_bit_cast(mb_bf16x8, b),
+                                                   c, 0, 0, 0);
+}
+
+// Copy the item's queries' split terms for dim phase h (super-steps [h·nsup/NH, (h+1)·nsup/NH)) from the
+// batch's split image qsplit [query][term][super-step][g][4 dwords] into LDS [query][term][S][g][4].
+template <int NP, int NH>
+__device__ __forceinline__ void mb_fill(unsigned *qs, const uint4 *__restrict__ qsplit, int nsup, int stride, int h,
+                                        int nqi, const int *__restrict__ bucket, int boff, int nprobe) {
+    const int nsh = nsup / NH;
+    const int per_q = NP * nsh * 4;
+    for (int t = threadIdx.x; t < nqi * per_q; t += MF_THREADS) {
+        const int q = t / per_q, rr = t - q * per_q;
+        const int j = rr / (nsh * 4), r2 = rr - j * (nsh * 4);
+        const int Sl = r2 >> 2, gg = r2 & 3;
+        const int gq = bucket[boff + q] / nprobe;
+        const uint4 v = qsplit[(((int64_t)gq * NP + j) * nsup + h * nsh + Sl) * 4 + gg];
+        *reinterpret_cast<uint4 *>(qs + q * stride + ((j * nsh + Sl) * 4 + gg) * 4) = v;
+    }
+}
+
+template <int QT, bool IP, int NP, int NH>
+__device__ __forceinline__ void mb_item(int d, const float *__restrict__ codes_t, int64_t tp0,
+                                        const float *__restrict__ xn, int64_t r0, int64_t r1, int nqi,
+                                        unsigned *__restrict__ qs, int stride, const uint4 *__restrict__ qsplit,
+                                        const float (&qn)[QT][4],
+                                        const unsigned (&qb)[QT][4], const int *__restrict__ bucket, int boff,
+                                        int nprobe, const int *__restrict__ slot_off, int chunk, int k, float *smem,
+                                        unsigned *__restrict__ qbound, float *__restrict__ part_d,
+                                        int *__restrict__ part_i) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int m = lane & 15, g = lane >> 4;
+    const int nsub = mf_nsub(d);
+    const int nsup = nsub / 2;
+    const int nsh = nsup / NH;  // super-steps per dim phase
+    const int npass_all = (int)ceil_div(r1 - r0, MF_PASS);
+    const int npass = npass_all > wave ? (npass_all - wave + MF_WAVES - 1) / MF_WAVES : 0;
+    // with NH > 1 every wave walks the same number of pass slots (the image swaps are block-wide)
+    const int nslots = NH > 1 ? (int)ceil_div(npass_all, MF_WAVES) : npass;
+
+    bool qv[QT][4];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) qv[qt][v] = qt * 16 + 4 * g + v < nqi;
+    uint64_t lst[QT][4], thr[QT][4];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const uint64_t b = ((uint64_t)qb[qt][v] << 32) | MF_PAD_ID;
+            lst[qt][v] = m < k ? b : MF_EMPTY;
+            thr[qt][v] = b;
+        }
+
+    auto row_of = [&](int i, int r) -> int64_t {
+        const int64_t row = r0 + (int64_t)(wave + MF_WAVES * i) * MF_PASS + 16 * r + m;
+        return row < r1 ? row : r1 - 1;
+    };
+    const int ilast = npass > 0 ? npass - 1 : 0;
+    const float *rp;
+    int ld_i = 0, ld_s = 0;  // stream position (16-dim steps), wave-uniform
+    auto set_pass = [&](int i) { rp = codes_t + ((tp0 + wave + MF_WAVES * i) * nsub) * (MF_RT * 256) + 4 * lane; };
+    auto next_load = [&](mf_f32x4 (&dst)[MF_RT]) {
+        const int s = ld_i <= ilast ? ld_s : nsub - 1;
+#pragma unroll
+        for (int r = 0; r < MF_RT; ++r)
+            dst[r] = *reinterpret_cast<const mf_f32x4 *>(rp + (int64_t)s * (MF_RT * 256) + r * 256);
+        if (++ld_s == nsub) {
+            ld_s = 0;
+            ++ld_i;
+            set_pass(ld_i <= ilast ? ld_i : ilast);
+        }
+    };
+
+    mf_f32x4 ring[MB_PS][2][MF_RT];  // [super-step slot][half][row tile]
+    float xnr[MF_RT] = {0.f, 0.f};
+    if (npass > 0) {
+        set_pass(0);
+#pragma unroll
+        for (int p = 0; p < MB_PS; ++p) {
+            next_load(ring[p][0]);
+            next_load(ring[p][1]);
+        }
+        if (!IP) {
+#pragma unroll
+            for (int r = 0; r < MF_RT; ++r) xnr[r] = xn[row_of(0, r)];
+        }
+    }
+    const unsigned *qrow[QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) qrow[qt] = qs + (qt * 16 + m) * stride + 4 * g;
+
+    mf_f32x4 acc[QT][MF_RT];
+    for (int i = 0; i < nslots; ++i) {
+        const bool has = i < npass;  // wave-uniform; false only in the last slot of a ragged item
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+            for (int r = 0; r < MF_RT; ++r) acc[qt][r] = mf_f32x4{0.f, 0.f, 0.f, 0.f};
+        float xnr_next[MF_RT] = {0.f, 0.f};
+        if (!IP && has) {
+#pragma unroll
+            for (int r = 0; r < MF_RT; ++r) xnr_next[r] = xn[row_of(i + 1 <= ilast ? i + 1 : ilast, r)];
+        }
+        for (int h = 0; h < NH; ++h) {
+        if (NH > 1) {
+            __syncthreads();  // every wave is done with the previous phase's image
+            mb_fill<NP, NH>(qs, qsplit, nsup, stride, h, nqi, bucket, boff, nprobe);
+            __syncthreads();
+        }
+        if (has)
+        for (int S0 = 0; S0 < nsh; S0 += MB_PS) {
+#pragma unroll
+            for (int p = 0; p < MB_PS; ++p) {
+                const int S = S0 + p;
+                uint4 qa[QT][NP];
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                    for (int j = 0; j < NP; ++j)
+                        qa[qt][j] = *reinterpret_cast<const uint4 *>(qrow[qt] + (j * nsh + S) * 16);
+                MbTerms<NP> xb[MF_RT];
+#pragma unroll
+                for (int r = 0; r < MF_RT; ++r) xb[r] = mb_split<NP>(ring[p][0][r], ring[p][1][r]);
+                next_load(ring[p][0]);
+                next_load(ring[p][1]);
+                // products, small terms first per accumulator chain position (independent chains
+                // interleave: consecutive MFMAs hit different accumulators)
+#pragma unroll
+                for (int t = 0; t < (NP == 3 ? 6 : 3); ++t) {
+                    const int ja = NP == 3 ? (t == 0 ? 1 : t == 1 ? 0 : t == 2 ? 2 : t == 3 ? 0 : t == 4 ? 1 : 0)
+                                           : (t == 0 ? 1 : t == 1 ? 0 : 0);
+                    const int jb = NP == 3 ? (t == 0 ? 1 : t == 1 ? 2 : t == 2 ? 0 : t == 3 ? 1 : t == 4 ? 0 : 0)
+                                           : (t == 0 ? 0 : t == 1 ? 1 : 0);
+#pragma unroll
+                    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                        for (int r = 0; r < MF_RT; ++r) acc[qt][r] = mb_mfma(qa[qt][ja], xb[r].t[jb], acc[qt][r]);
+                }
+            }
+        }
+        }  // dim phases
+        if (!has) continue;
+        const int64_t prow0 = r0 + (int64_t)(wave + MF_WAVES * i) * MF_PASS;
+#pragma unroll
+        for (int r = 0; r < MF_RT; ++r) {
+            const int64_t row = prow0 + 16 * r + m;
+            const bool rok = row < r1;
+            const unsigned rid = rok ? (unsigned)row : MF_PAD_ID;
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    float key;
+                    if (IP) {
+                        key = -acc[qt][r][v];
+                    } else {
+                        key = fmaf(-2.f, acc[qt][r][v], qn[qt][v] + xnr[r]);
+                        key = key < 0.f ? 0.f : key;
+                    }
+                    const bool ok = rok && qv[qt][v];
+                    uint64_t cp = ok ? (((uint64_t)mf_sortable(key) << 32) | rid) : MF_EMPTY;
+                    if (__ballot(cp < thr[qt][v])) {
+                        row_sort16(cp, m);
+                        row_merge16(lst[qt][v], cp, m);
+                        thr[qt][v] = row_kth(lst[qt][v], k - 1, g);
+                    }
+                }
+        }
+#pragma unroll
+        for (int r = 0; r < MF_RT; ++r) xnr[r] = xnr_next[r];
+    }
+
+    uint64_t *scratch = reinterpret_cast<uint64_t *>(smem);
+#pragma unroll 1
+    for (int half = MF_WAVES / 2; half > 0; half >>= 1) {
+        __syncthreads();
+        if (wave >= half && wave < 2 * half) {
+            uint64_t *dst = scratch + (size_t)(wave - half) * QT * 4 * 64;
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) dst[(qt * 4 + v) * 64 + lane] = lst[qt][v];
+        }
+        __syncthreads();
+        if (wave < half) {
+            const uint64_t *src = scratch + (size_t)wave * QT * 4 * 64;
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) row_merge16(lst[qt][v], src[(qt * 4 + v) * 64 + lane], m);
+        }
+    }
+    if (wave == 0 && m < k) {
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const int q = qt * 16 + 4 * g + v;
+                if (q < nqi) {
+                    const int pr = bucket[boff + q];
+                    const int64_t off = (int64_t)(slot_off[pr] + chunk) * k + m;
+                    const uint64_t e = lst[qt][v];
+                    const unsigned id = (unsigned)e;
+                    const bool real = e != MF_EMPTY && id != MF_PAD_ID;
+                    part_d[off] = real ? mf_unsortable((unsigned)(e >> 32)) : __builtin_inff();
+                    part_i[off] = real ? (int)id : (int)MF_PAD_ID;
+                    if (m == k - 1 && real) atomicMin(qbound + pr / nprobe, (unsigned)(e >> 32));
+                }
+            }
+    }
+}
+
+template <bool IP, int NP, int NH>
+__global__ void __launch_bounds__(MF_THREADS, MF_WAVES / 4)
+ivf_scan_mfma_bf(const uint4 *__restrict__ qsplit, const float *__restrict__ qnorm, int d, const float *__restrict__ codes_t,
+                 const int64_t *__restrict__ tpass_off, const float *__restrict__ xn,
+                 const int64_t *__restrict__ list_off, const int *__restrict__ cnt, const int *__restrict__ bucket_off,
+                 const int *__restrict__ item_off, const int *__restrict__ bucket, const int *__restrict__ slot_off,
+                 int nlist, int nprobe, int group, int k, unsigned *__restrict__ qbound, float *__restrict__ part_d,
+                 int *__restrict__ part_i) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int total = item_off[nlist];
+    if ((int)blockIdx.x >= total) return;
+    const int item = xcd_remap((int)blockIdx.x, total);
+    int lo = 0, hi = nlist - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (item_off[mid] <= item) lo = mid; else hi = mid - 1;
+    }
+    const int l = lo;
+    const int64_t lr0 = list_off[l], lr1 = list_off[l + 1];
+    const int c = cnt[l];
+    const int ng = (c + group - 1) / group;
+    const int rem = item - item_off[l];
+    const int chunk = rem / ng, grp = rem - chunk * ng;
+    const int q_begin = (int)((int64_t)grp * c / ng), q_end = (int)((int64_t)(grp + 1) * c / ng);
+    const int nqi = q_end - q_begin;
+    const int64_t r0 = lr0 + (int64_t)chunk * MF_CH;
+    const int64_t r1 = r0 + MF_CH < lr1 ? r0 + MF_CH : lr1;
+    const int boff = bucket_off[l] + q_begin;
+    const int nqt = (nqi + 15) >> 4;
+
+    // ---- the item's queries' split terms → LDS [query][term][S][g][8 bf16] (all dims, or per phase) ----
+    unsigned *qs = reinterpret_cast<unsigned *>(smem);
+    const int stride = mb_stride(d, NP, NH);
+    if (NH == 1) mb_fill<NP, 1>(qs, qsplit, mb_nsuper(d), stride, 0, nqi, bucket, boff, nprobe);
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, g = lane >> 4;
+    const int64_t tp0 = tpass_off[l] + (int64_t)chunk * (MF_CH / MF_PASS);
+#define MB_ARGS d, codes_t, tp0, xn, r0, r1, nqi, qs, stride, qsplit, qn, qb, bucket, boff, nprobe, slot_off, chunk, k, smem, \
+                qbound, part_d, part_i
+#define MB_QN(QTV)                                                                                          \
+    float qn[QTV][4];                                                                                       \
+    unsigned qb[QTV][4];                                                                                    \
+    _Pragma("unroll") for (int qt = 0; qt < QTV; ++qt) _Pragma("unroll") for (int v = 0; v < 4; ++v) {      \
+        const int q = qt * 16 + 4 * g + v;                                                                  \
+        const int qi = q < nqi ? bucket[boff + q] / nprobe : 0;                                             \
+        qn[qt][v] = (!IP && q < nqi) ? qnorm[qi] : 0.f;                                                     \
+        qb[qt][v] = q < nqi ? __atomic_load_n(qbound + qi, __ATOMIC_RELAXED) : 0xffffffffu;                 \
+    }
+    if (nqt <= 1) {
+        MB_QN(1)
+        mb_item<1, IP, NP, NH>(MB_ARGS);
+    } else if (nqt == 2) {
+        MB_QN(2)
+        mb_item<2, IP, NP, NH>(MB_ARGS);
+    } else {
+        MB_QN(3)
+        mb_item<3, IP, NP, NH>(MB_ARGS);
+    }
+#undef MB_QN
+#undef MB_ARGS
+}
+
+// The batch's queries split once into NP bf16 terms: qsplit [query][term][super-step][g][8 bf16], k-slot
+// order of the tiled codes (dims 32S + 4g + j and 32S + 16 + 4g + j, j < 4; zero past d).
+template <int NP>
+__global__ void __launch_bounds__(256) ivf_split_queries(const float *__restrict__ Q, int64_t nq, int d, int nsup,
+                                                         uint4 *__restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= nq * nsup * 4) return;
+    const int64_t q = t / (nsup * 4);
+    const int rr = (int)(t - q * (nsup * 4));
+    const int S = rr >> 2, gg = rr & 3;
+    const float *src = Q + q * d;
+    const int d0 = 32 * S + 4 * gg, d1 = d0 + 16;
+    mf_f32x4 a = mf_f32x4{0.f, 0.f, 0.f, 0.f}, b = a;
+    if (d0 < d) a = *reinterpret_cast<const mf_f32x4 *>(src + d0);
+    if (d1 < d) b = *reinterpret_cast<const mf_f32x4 *>(src + d1);
+    const MbTerms<NP> sp = mb_split<NP>(a, b);
+#pragma unroll
+    for (int j = 0; j < NP; ++j) out[((q * NP + j) * nsup + S) * 4 + gg] = sp.t[j];
+}
+
+int ivf_mfma_bf_group(int d, int np) { return mb_group(d, np); }
+
+int64_t ivf_mfma_bf_qsplit_bytes(int64_t nq, int d, int np) { return nq * np * mb_nsuper(d) * 64; }
+
+bool ivf_mfma_bf_supported(const float *Q, int d, const float *codes, int k, int np) {
+    return ivf_mfma_supported(Q, d, codes, k) && mb_group(d, np) >= 16;
+}
+
+void launch_ivf_scan_mfma_bf(int np, const float *Q, int64_t nq, void *qsplit, const float *qn, int d, int metric,
+                             const float *codes_t, const int64_t *tpass_off, const float *xn, const int64_t *list_off,
+                             const int *cnt, const int *bucket_off, const int *item_off, const int *bucket,
+                             const int *slot_off, int nlist, int nprobe, int k, int64_t max_items, unsigned *qbound,
+                             float *pd, int *pi, hipStream_t st) {
+    if (max_items <= 0 || nq <= 0) return;
+    HIPANN_REQUIRE(np == 2 || np == 3, "split-bf16 scan: 2 or 3 terms");
+    HIPANN_REQUIRE(max_items < (int64_t)0x7fffffff, "too many IVF work items");
+    HIPANN_REQUIRE(qsplit, "split-bf16 scan: no query image buffer");
+    HIPANN_REQUIRE(ivf_mfma_bf_supported(Q, d, codes_t, k, np), "split-bf16 IVF scan needs d % 4 == 0, 16-B aligned data, k <= 16");
+    HIPANN_REQUIRE(metric == kIP || (qn && xn), "decomposed L2 scan needs query and row norms");
+    const int nsup = mb_nsuper(d);
+    const int64_t nthr = nq * nsup * 4;
+    uint4 *qs = static_cast<uint4 *>(qsplit);
+    if (np == 3) hipLaunchKernelGGL(ivf_split_queries<3>, dim3((unsigned)ceil_div(nthr, 256)), dim3(256), 0, st, Q, nq, d, nsup, qs);
+    else hipLaunchKernelGGL(ivf_split_queries<2>, dim3((unsigned)ceil_div(nthr, 256)), dim3(256), 0, st, Q, nq, d, nsup, qs);
+    const int nh = mb_phases(d, np);
+    const int group = mb_group(d, np);
+    const size_t merge = (size_t)(MF_WAVES / 2) * MF_QTMAX * 4 * 64 * sizeof(float2);
+    const size_t smem = std::max((size_t)group * mb_stride(d, np, nh) * 4, merge);
+    dim3 grid((unsigned)max_items), block(MF_THREADS);
+#define MB_LAUNCH_ARGS qs, qn, d, codes_t, tpass_off, xn, list_off, cnt, bucket_off, item_off, bucket, slot_off, nlist, nprobe, \
+                       group, k, qbound, pd, pi
+#define MB_LAUNCH(NP_, NH_)                                                                                         \
+    do {                                                                                                            \
+        if (metric == kIP) hipLaunchKernelGGL((ivf_scan_mfma_bf<true, NP_, NH_>), grid, block, smem, st, MB_LAUNCH_ARGS); \
+        else hipLaunchKernelGGL((ivf_scan_mfma_bf<false, NP_, NH_>), grid, block, smem, st, MB_LAUNCH_ARGS);       \
+    } while (0)
+    if (np == 3) {
+        if (nh == 2) MB_LAUNCH(3, 2); else MB_LAUNCH(3, 1);
+    } else {
+        if (nh == 2) MB_LAUNCH(2, 2); else MB_LAUNCH(2, 1);
+    }
+#undef MB_LAUNCH
+#undef MB_LAUNCH_ARGS
     HIPANN_CHECK(hipGetLastError());
 }
 

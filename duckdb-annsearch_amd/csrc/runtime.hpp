@@ -173,6 +173,7 @@ struct IvfShard {
     // scratch
     DevBuf q, qn, coarse_d, coarse_i, cnt, bucket_off, item_off, cursor, bucket, slot_off, part_d, part_i, out_d, out_i;
     DevBuf qbound;                 // per query: best known k-th key (order-preserving u32; MFMA scan)
+    DevBuf qsplit;                 // split-bf16 scans: the batch's queries as bf16 terms
     // MFMA scan copy of the codes, built at the first search that uses it: per list, 32-row passes of
     // [16-dim step][2 row tiles][64 lanes][float4] (ivf_mfma.hip), zero-padded rows / dims
     std::vector<int64_t> h_off;    // host copy of list_off
@@ -223,6 +224,14 @@ void launch_ivf_plan(const int64_t *probes, int64_t nq, int nprobe, const int *l
                      int *cnt, int *bucket_off, int *item_off, int *cursor, int *bucket, int *slot_off,
                      hipStream_t st);
 int64_t ivf_max_items(int64_t nq, int nprobe, int nlist, int max_nch, int64_t nrows, int group);
+int ivf_mfma_bf_group(int d, int np);
+bool ivf_mfma_bf_supported(const float *Q, int d, const float *codes, int k, int np);
+int64_t ivf_mfma_bf_qsplit_bytes(int64_t nq, int d, int np);
+void launch_ivf_scan_mfma_bf(int np, const float *Q, int64_t nq, void *qsplit, const float *qn, int d, int metric,
+                             const float *codes_t, const int64_t *tpass_off, const float *xn, const int64_t *list_off,
+                             const int *cnt, const int *bucket_off, const int *item_off, const int *bucket,
+                             const int *slot_off, int nlist, int nprobe, int k, int64_t max_items, unsigned *qbound,
+                             float *pd, int *pi, hipStream_t st);
 int ivf_group_size(int form, int d);  // queries per work item of the form's scan kernel
 int ivf_chunk_rows();
 void launch_ivf_scan_bigk(const float *Q, int d, int metric, const float *codes, const int64_t *list_off,

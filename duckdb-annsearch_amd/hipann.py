@@ -333,6 +333,8 @@ class HipIndexIVFFlat(_Handle):
     FORM_DECOMPOSED = 0       # ‖q‖² + ‖x‖² − 2 q·x on the fp32 matrix cores (FAISS GPU / faiss-metal IVF form; default)
     FORM_DIRECT = 1           # Σ(q − x)² (FAISS CPU IndexIVFFlat scanner form)
     FORM_DECOMPOSED_VALU = 2  # the decomposed form on the VALU kernel (A/B measurement)
+    FORM_SPLIT3 = 3           # decomposed, q·x on the bf16 matrix cores over a 3-term bf16 split (6 products)
+    FORM_SPLIT2 = 4           # decomposed, 2-term bf16 split (3 products, ~2^-16 relative per product)
 
     @property
     def form(self) -> int:
@@ -341,7 +343,7 @@ class HipIndexIVFFlat(_Handle):
     @form.setter
     def form(self, v: int) -> None:
         if lib().hipann_ivf_set_form(self._h, int(v)) != 0:
-            raise HipAnnError("form must be 0 (decomposed), 1 (direct) or 2 (decomposed, VALU)")
+            raise HipAnnError("form must be 0 (decomposed), 1 (direct), 2 (decomposed, VALU), 3 or 4 (split bf16)")
 
     def search(self, x, k: int) -> Tuple[np.ndarray, np.ndarray]:
         x = _f32_2d(x, self.d)

@@ -133,6 +133,11 @@ int hipann_ivf_set_nprobe(void *index, int nprobe);
 #define HIPANN_IVF_FORM_DECOMPOSED 0
 #define HIPANN_IVF_FORM_DIRECT 1
 #define HIPANN_IVF_FORM_DECOMPOSED_VALU 2
+/* HIPANN_IVF_FORM_SPLIT3: the decomposed form with q·x on the bf16 matrix cores over a 3-term bf16 split
+ * of both operands (six cross products, fp32-level per product, fp32 accumulation);
+ * HIPANN_IVF_FORM_SPLIT2: a 2-term split (three products, ≈2^-16 relative per product). */
+#define HIPANN_IVF_FORM_SPLIT3 3
+#define HIPANN_IVF_FORM_SPLIT2 4
 int hipann_ivf_set_form(void *index, int form);
 int hipann_ivf_get_form(void *index);
 

@@ -41,7 +41,7 @@ def test_ivf_faiss_metal_shapes(gpu, oracle, nv, d, nlist, nprobe, nq, k, metric
 
 @pytest.mark.parametrize("nq", [1, 7, 19, 20, 64, 333])
 @pytest.mark.parametrize("metric", [0, 1])
-@pytest.mark.parametrize("form", [0, 1, 2])
+@pytest.mark.parametrize("form", [0, 1, 2, 3, 4])
 def test_ivf_vs_oracle_probe_sets(gpu, oracle, nq, metric, form):
     xb, xq = faiss_metal_case(20000, nq, 96)
     ix, (cen, off, ids, codes) = _ivf(gpu, xb, 64, 8, metric)
@@ -55,7 +55,7 @@ def test_ivf_vs_oracle_probe_sets(gpu, oracle, nq, metric, form):
 
 @pytest.mark.parametrize("d", [4, 8, 12, 20, 44, 77, 132, 768])
 @pytest.mark.parametrize("metric", [0, 1])
-@pytest.mark.parametrize("form", [0, 1, 2])
+@pytest.mark.parametrize("form", [0, 1, 2, 3, 4])
 def test_ivf_dims(gpu, oracle, d, metric, form):
     """Dimensions around the scans' LDS chunks (32 dims MFMA, 32 VALU-decomposed, 24 direct: partial
     last chunk, d < one chunk) and d % 4 != 0 (the decomposed forms fall back to the direct kernel)."""
@@ -69,7 +69,7 @@ def test_ivf_dims(gpu, oracle, d, metric, form):
 
 
 @pytest.mark.parametrize("nq", [5, 70])
-@pytest.mark.parametrize("form", [0, 1, 2])
+@pytest.mark.parametrize("form", [0, 1, 2, 3, 4])
 def test_ivf_long_lists(gpu, oracle, nq, form):
     """Lists longer than one work item's row chunk (2048 rows) and ragged 256-row tiles; with nq = 70 a
     list's probing queries split over several query groups."""
@@ -85,7 +85,8 @@ def test_ivf_long_lists(gpu, oracle, nq, form):
 
 @pytest.mark.parametrize("nq", [1, 15, 16, 17, 31, 33, 47, 48, 49, 64, 65, 130])
 @pytest.mark.parametrize("d,metric", [(96, 0), (100, 0), (96, 1)])
-def test_ivf_mfma_query_tiles(gpu, oracle, nq, d, metric):
+@pytest.mark.parametrize("form", [0, 3, 4])
+def test_ivf_mfma_query_tiles(gpu, oracle, nq, d, metric, form):
     """One list probed by every query: items of 1-4 16-query tiles (every wave → work mapping of the
     MFMA scan, incl. the idle wave at 3 tiles and the list merges at 1-2 tiles), several query groups
     (nq > 64), 3 row chunks with a ragged last tile, and a partial last 32-dim chunk (d = 100)."""
@@ -94,7 +95,7 @@ def test_ivf_mfma_query_tiles(gpu, oracle, nq, d, metric):
     off = np.array([0, len(xb)], np.int64)
     ids = np.arange(len(xb), dtype=np.int64)
     ix = gpu.HipIndexIVFFlat(cen, off, ids, xb, 1, metric)
-    assert ix.form == 0
+    ix.form = form
     D, I = ix.search(xq, 10)
     Do, Io, Po = oracle.ivf_search(cen, off, ids, xb, xq, 10, 1, metric)
     check_topk_parity(xb, xq, D, I, Do, Io, metric)
