@@ -59,6 +59,7 @@ def parse():
     p.add_argument("--nprobe", type=int, default=32)
     p.add_argument("--metric", choices=["l2", "ip"], default="l2")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-alt-forms", action="store_true", help="ivf: skip timing the other list-scan forms")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU sample duration")
     a = p.parse_args()
     if a.n is None:
@@ -201,7 +202,9 @@ def main():
             data_desc = f"{n_centres} gaussian centres, sigma={sigma}"
         index, ivf_info = build_ivf_shard(torch, hipann, xb, lo, n, args.nlist, args.nprobe, metric, rank, world,
                                           centres_seed=1234)
-        index.form = int(os.environ.get("HIPANN_IVF_FORM", "0"))  # A/B: 1 direct, 2 decomposed on VALU
+        # list-scan form (hipann_ivf_set_form): 5 = the library default (2-term split-bf16 scan as a
+        # filter + exact fp32 direct-form rerank); A/B: 0 fp32 MFMA, 3/4 split scans, 1/2 VALU
+        index.form = int(os.environ.get("HIPANN_IVF_FORM", "5"))
         del xb  # lists hold a list-ordered copy
         torch.cuda.empty_cache()
         search = index.search_device
@@ -275,6 +278,38 @@ def main():
     else:
         recall = 1.0  # exact search (parity tests: ids identical to the FAISS restatement)
 
+    # ---------------- the other fp32-level list-scan forms, same batch (IVF, 1 GPU) ----------------
+    alt = None
+    if args.workload == "ivf" and world == 1 and not args.no_alt_forms:
+        alt = {}
+        base_form = index.form
+        names = {0: "fp32_mfma (exact fp32 products)", 3: "split3 (3-term bf16 split, 6 products)",
+                 5: "split2_exact (default)"}
+        for f in (3, 0):
+            if f == base_form:
+                continue
+            index.form = f
+            step()
+            torch.cuda.synchronize()
+            index.set_kernel_timing(True)
+            ta = time.perf_counter()
+            for _ in range(5):
+                step()
+            torch.cuda.synchronize()
+            el = time.perf_counter() - ta
+            kms = index.kernel_ms(0)
+            index.set_kernel_timing(False)
+            _, Ia = step()
+            torch.cuda.synchronize()
+            rec = None
+            if gt is not None:
+                got = Ia.cpu().numpy()
+                rec = float(np.mean([len(set(got[i]) & set(gt[i])) / k for i in range(nq)]))
+            alt[names[f]] = {"queries_per_s": round(nq * 5 / el, 1), "scan_kernel_ms": round(kms, 3),
+                             "recall_at_10": rec}
+        index.form = base_form
+        extra["rerank_fallbacks_total"] = index.rerank_fallbacks()
+
     # ---------------- roofline of the dominant kernel ----------------
     if args.workload == "flat":
         flops = 2.0 * nq * n_local * d
@@ -289,7 +324,9 @@ def main():
         kname, fname = {0: ("ivf_scan_mfma", "decomposed, fp32 MFMA"), 1: ("ivf_scan_topk", "direct, VALU"),
                         2: ("ivf_scan_dot", "decomposed, VALU"),
                         3: ("ivf_scan_mfma_bf", "decomposed, bf16 MFMA over a 3-term split (6 products)"),
-                        4: ("ivf_scan_mfma_bf", "decomposed, bf16 MFMA over a 2-term split (3 products)")}[form]
+                        4: ("ivf_scan_mfma_bf", "decomposed, bf16 MFMA over a 2-term split (3 products)"),
+                        5: ("ivf_scan_mfma_bf", "bf16 MFMA 2-term split scan as a filter (16 per list) + exact fp32 "
+                            "direct-form rerank, bound-checked (merge_ms includes the rerank)")}[form]
         fpp = 3.0 if form == 1 else 2.0  # flop per (query, row, dim): sub + fma vs fma
         achieved = b_alg / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -339,6 +376,13 @@ def main():
         }
         if extra:
             line["ivf"] = {kk: v for kk, v in extra.items() if kk != "scan_bytes_per_batch_local"}
+        if alt:
+            line["ivf_other_forms"] = alt
+        if args.workload == "ivf" and index.form == 5:
+            line["precision"] = ("returned distances are fp32 direct-form Σ(q−x)² (FAISS CPU IVFFlatScanner arithmetic); "
+                                 "the bf16 2-term split scan only prunes, and a per-query bound "
+                                 "(|scan key − exact| ≤ 2^-12·(|q|²+max|x|²)) proves no pruned row reaches the top-k "
+                                 "(failures re-run on the 3-term path)")
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -35,7 +35,17 @@ enum Metric : int { kL2 = 0, kIP = 1 };
 // kFormDecomposedValu: the same form on the VALU kernel (ivf_scan_dot), kept for A/B measurement.
 // kFormSplit3 / kFormSplit2: the decomposed form on the bf16 matrix cores over a 3-term (fp32-level
 // products) / 2-term bf16 split of both operands (ivf_mfma.hip, split-bf16 variant).
-enum IvfForm : int { kFormDecomposed = 0, kFormDirect = 1, kFormDecomposedValu = 2, kFormSplit3 = 3, kFormSplit2 = 4 };
+// kFormSplit2Exact: the 2-term scan keeps the kRerankK best per list and every returned distance is
+// recomputed exactly in the direct form, with a per-query bound check (ivf_rerank_topk); k <= kRerankMaxK.
+enum IvfForm : int {
+    kFormDecomposed = 0,
+    kFormDirect = 1,
+    kFormDecomposedValu = 2,
+    kFormSplit3 = 3,
+    kFormSplit2 = 4,
+    kFormSplit2Exact = 5
+};
+constexpr int kRerankK = 16, kRerankMaxK = 12;
 __host__ __device__ inline bool ivf_form_split(int f) { return f == kFormSplit3 || f == kFormSplit2; }
 __host__ __device__ inline int ivf_form_terms(int f) { return f == kFormSplit3 ? 3 : 2; }
 

@@ -131,8 +131,29 @@ IvfIndex::~IvfIndex() {
 }
 
 // One shard: queries on the shard's device → D/I (nq × kout) on the same device, async on `st`.
+// max‖x‖² of the shard (once): the rerank's error bound
+float shard_xmax2(IvfShard &sh, int d, hipStream_t st) {
+    if (sh.xmax2 >= 0.f) return sh.xmax2;
+    const float *xn = sh.xnorm.get<float>();
+    if (!xn) {
+        sh.tmpnorm.ensure(sizeof(float) * (size_t)std::max<int64_t>(sh.n, 1), sh.device);
+        launch_row_norms(sh.codes, sh.n, d, sh.tmpnorm.get<float>(), st);
+        xn = sh.tmpnorm.get<float>();
+    }
+    sh.nflag.ensure(sizeof(int), sh.device);
+    launch_ivf_max_norm(xn, sh.n, sh.nflag.get<unsigned>(), st);
+    unsigned bits = 0;
+    HIPANN_CHECK(hipMemcpyAsync(&bits, sh.nflag.p, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    HIPANN_CHECK(hipStreamSynchronize(st));
+    sh.tmpnorm.release();
+    float v;
+    std::memcpy(&v, &bits, sizeof(v));
+    sh.xmax2 = v;
+    return v;
+}
+
 void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, int k, int kout, float *D, int64_t *I,
-                      hipStream_t st) {
+                      hipStream_t st, int form_override) {
     DeviceGuard g(sh.device);
     const int nlist = ix.nlist, d = ix.d, metric = ix.metric;
     const int np = std::min(ix.nprobe, nlist);
@@ -156,9 +177,18 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     // the decomposed form needs float4 rows; other shapes take the direct kernel (also on the GPU)
     // the decomposed forms need float4 rows (else the direct kernel, also on the GPU); the MFMA kernel
     // keeps 16-lane lists (k <= 16) and the item's queries in LDS (else the VALU decomposed kernel)
-    int form = ix.form != kFormDirect && !bigk && ivf_dot_supported(xq, d, sh.codes) ? ix.form : kFormDirect;
-    if (ivf_form_split(form) && !ivf_mfma_bf_supported(xq, d, sh.codes, k, ivf_form_terms(form))) form = kFormDecomposed;
-    if (form == kFormDecomposed && !ivf_mfma_supported(xq, d, sh.codes, k)) form = kFormDecomposedValu;
+    int req = form_override >= 0 ? form_override : ix.form;
+    // kFormSplit2Exact: the 2-term scan keeps kRerankK per list, the rerank makes the results exact
+    // (k > kRerankMaxK leaves too little margin: the 3-term scan instead)
+    const bool want_exact = req == kFormSplit2Exact;
+    if (want_exact) req = kout <= kRerankMaxK ? kFormSplit2 : kFormSplit3;
+    const int k_user = k;
+    const int kscan = want_exact && req == kFormSplit2 ? kRerankK : k;
+    int form = req != kFormDirect && !bigk && ivf_dot_supported(xq, d, sh.codes) ? req : kFormDirect;
+    if (ivf_form_split(form) && !ivf_mfma_bf_supported(xq, d, sh.codes, kscan, ivf_form_terms(form))) form = kFormDecomposed;
+    if (form == kFormDecomposed && !ivf_mfma_supported(xq, d, sh.codes, kscan)) form = kFormDecomposedValu;
+    const bool exact = want_exact && form == kFormSplit2;
+    k = kscan;  // per-list k of the scan (the output keeps kout)
     const bool tiled = form == kFormDecomposed || ivf_form_split(form);  // the matrix-core scans
     const int group = ivf_group_size(form, d);
     launch_ivf_plan(sh.coarse_i.get<int64_t>(), nq, np, sh.list_len.get<int>(), nlist, group, sh.cnt.get<int>(),
@@ -209,10 +239,39 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
                             sh.slot_off.get<int>(), nlist, np, nq, k, max_items, qbound, sh.part_d.get<float>(),
                             sh.part_i.get<int>(), st);
     }
-    // 4. merge each query's partial lists
-    ScopedTiming t(ix.timer_merge, st);
-    launch_ivf_merge(sh.part_d.get<float>(), sh.part_i.get<int>(), sh.ids, sh.n, sh.slot_off.get<int>(), np, nq, k, kout,
-                     out_sign, D, I, st);
+    // 4. merge each query's partial lists (kFormSplit2Exact: merge + exact rerank + bound check)
+    if (!exact) {
+        ScopedTiming t(ix.timer_merge, st);
+        launch_ivf_merge(sh.part_d.get<float>(), sh.part_i.get<int>(), sh.ids, sh.n, sh.slot_off.get<int>(), np, nq, k,
+                         kout, out_sign, D, I, st);
+        return;
+    }
+    const float xmax2 = shard_xmax2(sh, d, st);
+    sh.nflag.ensure(sizeof(int), sh.device);
+    sh.flagged.ensure(sizeof(int) * (size_t)nq, sh.device);
+    HIPANN_CHECK(hipMemsetAsync(sh.nflag.p, 0, sizeof(int), st));
+    {
+        ScopedTiming t(ix.timer_merge, st);
+        launch_ivf_rerank(sh.part_d.get<float>(), sh.part_i.get<int>(), sh.slot_off.get<int>(), np, nq, k, kout, metric,
+                          xq, sh.codes, d, sh.ids, sh.n, xmax2, D, I, sh.nflag.get<int>(), sh.flagged.get<int>(), st);
+    }
+    int nf = 0;
+    HIPANN_CHECK(hipMemcpyAsync(&nf, sh.nflag.p, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPANN_CHECK(hipStreamSynchronize(st));
+    if (nf <= 0) return;
+    // flagged queries: re-run on the 3-term path (the batch's probe lists are kept for last_probes)
+    ix.rerank_fallbacks += nf;
+    const size_t pbytes = sizeof(int64_t) * (size_t)nq * np;
+    sh.coarse_save.ensure(pbytes, sh.device);
+    HIPANN_CHECK(hipMemcpyAsync(sh.coarse_save.p, sh.coarse_i.p, pbytes, hipMemcpyDeviceToDevice, st));
+    sh.fq.ensure(sizeof(float) * (size_t)nf * d, sh.device);
+    sh.fD.ensure(sizeof(float) * (size_t)nf * kout, sh.device);
+    sh.fI.ensure(sizeof(int64_t) * (size_t)nf * kout, sh.device);
+    launch_ivf_gather_queries(xq, sh.flagged.get<int>(), nf, d, sh.fq.get<float>(), st);
+    ivf_shard_search(ix, sh, nf, sh.fq.get<float>(), k_user, kout, sh.fD.get<float>(),
+                     sh.fI.get<int64_t>(), st, kFormSplit3);
+    launch_ivf_scatter_results(sh.fD.get<float>(), sh.fI.get<int64_t>(), sh.flagged.get<int>(), nf, kout, D, I, st);
+    HIPANN_CHECK(hipMemcpyAsync(sh.coarse_i.p, sh.coarse_save.p, pbytes, hipMemcpyDeviceToDevice, st));
 }
 
 }  // namespace hipann
@@ -473,13 +532,20 @@ int hipann_ivf_set_nprobe(void *h, int nprobe) {
 }
 
 int hipann_ivf_set_form(void *h, int form) {
-    if (!h || form < kFormDecomposed || form > kFormSplit2) return -1;
+    if (!h || form < kFormDecomposed || form > kFormSplit2Exact) return -1;
     auto *ix = static_cast<IndexBase *>(h);
     if (ix->kind != Kind::IVF) return -1;
     auto *vx = static_cast<IvfIndex *>(ix);
     std::lock_guard<std::mutex> lk(vx->mu);
     vx->form = form;
     return 0;
+}
+
+int64_t hipann_ivf_rerank_fallbacks(void *h) {
+    if (!h) return -1;
+    auto *ix = static_cast<IndexBase *>(h);
+    if (ix->kind != Kind::IVF) return -1;
+    return static_cast<IvfIndex *>(ix)->rerank_fallbacks;
 }
 
 int hipann_ivf_get_form(void *h) {

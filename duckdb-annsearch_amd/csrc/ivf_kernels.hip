@@ -19,6 +19,7 @@
 #include "common.hpp"
 #include "wave_topk.hpp"
 
+#include <algorithm>
 #include <utility>
 
 namespace hipann {
@@ -964,6 +965,173 @@ void launch_ivf_merge(const float *pd, const int *pi, const int64_t *ids, int64_
     HIPANN_IVF_MERGE(32)
 #undef HIPANN_IVF_MERGE
     throw HipError("ivf merge: k too large");
+}
+
+}  // namespace hipann
+
+namespace hipann {
+
+// ---------------------------------------------------------------------------------------------
+// ivf_rerank_topk — form kFormSplit2Exact.  The 2-term split-bf16 scan (≈2⁻¹⁶ relative per product)
+// only prunes; the results are exact.  Per query (one wave): merge the partial lists to the
+// kRerankK = 16 best (scan key, row); recompute those rows' distances in the FAISS CPU scanner's
+// direct form (Σ(q−x)², or −q·x for IP; fp32, IVFFlatScanner / fvec_L2sqr); order them by (distance,
+// label) and write the first kout.
+// Exactness check: every row the scan pruned has a scan key ≥ K16, the 16th merged key (slot lists,
+// the running per-query bound and the merge all keep the 16 best), and |scan key − exact distance| ≤
+// E = 2⁻¹²·(‖q‖² + max‖x‖²) (the dropped split terms, ≤ 3·2⁻¹⁶·‖q‖‖x‖ per q·x, doubled, plus fp32
+// rounding of the norms and of both sums, with margin).  A query whose kout-th exact distance is not
+// < K16 − E (or < −K16... for IP the same bound on −q·x) is flagged; the host re-runs the flagged
+// queries on the 3-term path.  With fewer than 16 merged candidates nothing was pruned.
+// ---------------------------------------------------------------------------------------------
+template <bool IP>
+__global__ void __launch_bounds__(256)
+ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const int *__restrict__ slot_off,
+                int nprobe, int64_t nq, int k, int kout, const float *__restrict__ Q,
+                const float *__restrict__ codes, int d, const int64_t *__restrict__ ids, int64_t nrows, float xmax2,
+                float *__restrict__ D, int64_t *__restrict__ I, int *__restrict__ nflag, int *__restrict__ flagged) {
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq) return;
+    const int lane = threadIdx.x & 63;
+    // 1. the kRerankK best (scan key, row) of the query's partial lists
+    WaveList<1, int> L;
+    L.init();
+    const int64_t s0 = slot_off[q * nprobe], s1 = slot_off[(q + 1) * nprobe];
+    const int64_t total = (s1 - s0) * k;
+    for (int64_t c0 = 0; c0 < total; c0 += 64) {
+        const int64_t c = c0 + lane;
+        float key = __builtin_inff();
+        int row = IdTraits<int>::pad();
+        if (c < total) {
+            const int64_t off = s0 * k + c;
+            const int raw = pi[off];
+            const float v = pd[off];
+            if (raw >= 0 && raw < nrows && !(v == __builtin_inff())) {
+                key = v;
+                row = raw;
+            }
+        }
+        L.offer(key, row, kRerankK - 1);
+    }
+    const int myrow = L.id[0];
+    const bool real = lane < kRerankK && myrow != IdTraits<int>::pad();
+    const int ncand = __popcll(__ballot(real));
+    const float k16 = readlane_f(L.d[0], kRerankK - 1);
+    // 2. exact direct-form distances of the candidates (4 rows in flight, wave reduction per row)
+    const float *qp = Q + q * (int64_t)d;
+    float qq = 0.f;
+    for (int e = lane; e < d; e += 64) qq = fmaf(qp[e], qp[e], qq);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) qq += __shfl_xor(qq, o);
+    float mine = __builtin_inff();
+    for (int r0 = 0; r0 < ncand; r0 += 4) {
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        const float *xr[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int r = r0 + u < ncand ? r0 + u : ncand - 1;
+            xr[u] = codes + (int64_t)__builtin_amdgcn_readlane(myrow, r) * d;
+        }
+        for (int e = lane; e < d; e += 64) {
+            const float qv = qp[e];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const float xv = xr[u][e];
+                if (IP) acc[u] = fmaf(qv, xv, acc[u]);
+                else {
+                    const float t = qv - xv;
+                    acc[u] = fmaf(t, t, acc[u]);
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            float a = acc[u];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+            if (lane == r0 + u) mine = IP ? -a : a;
+        }
+    }
+    // 3. (distance, label) order, first kout
+    WaveList<1, long long> R;
+    R.init();
+    const long long lab = real ? (long long)ids[myrow] : IdTraits<long long>::pad();
+    R.offer(real ? mine : __builtin_inff(), lab, kout - 1);
+    // 4. exactness check
+    const float dk = readlane_f(R.d[0], kout - 1);
+    const float E = 0x1p-12f * (qq + xmax2);
+    if (ncand == kRerankK && !(dk < k16 - E) && lane == 0) flagged[atomicAdd(nflag, 1)] = (int)q;
+    const float pad_d = IP ? -__builtin_inff() : __builtin_inff();
+    if (lane < kout) {
+        const bool pad = R.id[0] == IdTraits<long long>::pad();
+        D[q * kout + lane] = pad ? pad_d : (IP ? -R.d[0] : R.d[0]);
+        I[q * kout + lane] = pad ? -1 : (int64_t)R.id[0];
+    }
+}
+
+// max over rows of ‖x‖² (non-negative floats order as their bit patterns)
+__global__ void __launch_bounds__(256) ivf_max_norm(const float *__restrict__ xn, int64_t n, unsigned *__restrict__ out) {
+    float m = 0.f;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) m = fmaxf(m, xn[i]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+}
+
+__global__ void __launch_bounds__(256) ivf_gather_queries(const float *__restrict__ Q, const int *__restrict__ idx, int nf,
+                                                          int d, float *__restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= (int64_t)nf * d) return;
+    const int j = (int)(t / d), e = (int)(t - (int64_t)j * d);
+    out[t] = Q[(int64_t)idx[j] * d + e];
+}
+
+__global__ void __launch_bounds__(256) ivf_scatter_results(const float *__restrict__ Df, const int64_t *__restrict__ If,
+                                                           const int *__restrict__ idx, int nf, int kout,
+                                                           float *__restrict__ D, int64_t *__restrict__ I) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= (int64_t)nf * kout) return;
+    const int j = (int)(t / kout), e = (int)(t - (int64_t)j * kout);
+    D[(int64_t)idx[j] * kout + e] = Df[t];
+    I[(int64_t)idx[j] * kout + e] = If[t];
+}
+
+void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int nprobe, int64_t nq, int k, int kout,
+                       int metric, const float *Q, const float *codes, int d, const int64_t *ids, int64_t nrows,
+                       float xmax2, float *D, int64_t *I, int *nflag, int *flagged, hipStream_t st) {
+    if (nq <= 0) return;
+    HIPANN_REQUIRE(k == kRerankK && kout >= 1 && kout <= kRerankMaxK, "ivf rerank: k / kout out of range");
+    dim3 grid((unsigned)ceil_div(nq, 4)), block(256);
+    if (metric == kIP)
+        hipLaunchKernelGGL(ivf_rerank_topk<true>, grid, block, 0, st, pd, pi, slot_off, nprobe, nq, k, kout, Q, codes, d,
+                           ids, nrows, xmax2, D, I, nflag, flagged);
+    else
+        hipLaunchKernelGGL(ivf_rerank_topk<false>, grid, block, 0, st, pd, pi, slot_off, nprobe, nq, k, kout, Q, codes,
+                           d, ids, nrows, xmax2, D, I, nflag, flagged);
+    HIPANN_CHECK(hipGetLastError());
+}
+
+void launch_ivf_max_norm(const float *xn, int64_t n, unsigned *out, hipStream_t st) {
+    HIPANN_CHECK(hipMemsetAsync(out, 0, sizeof(unsigned), st));
+    if (n <= 0) return;
+    const unsigned blocks = (unsigned)std::min<int64_t>(1024, ceil_div(n, 256));
+    hipLaunchKernelGGL(ivf_max_norm, dim3(blocks), dim3(256), 0, st, xn, n, out);
+    HIPANN_CHECK(hipGetLastError());
+}
+
+void launch_ivf_gather_queries(const float *Q, const int *idx, int nf, int d, float *out, hipStream_t st) {
+    if (nf <= 0) return;
+    hipLaunchKernelGGL(ivf_gather_queries, dim3((unsigned)ceil_div((int64_t)nf * d, 256)), dim3(256), 0, st, Q, idx, nf,
+                       d, out);
+    HIPANN_CHECK(hipGetLastError());
+}
+
+void launch_ivf_scatter_results(const float *Df, const int64_t *If, const int *idx, int nf, int kout, float *D,
+                                int64_t *I, hipStream_t st) {
+    if (nf <= 0) return;
+    hipLaunchKernelGGL(ivf_scatter_results, dim3((unsigned)ceil_div((int64_t)nf * kout, 256)), dim3(256), 0, st, Df, If,
+                       idx, nf, kout, D, I);
+    HIPANN_CHECK(hipGetLastError());
 }
 
 }  // namespace hipann

@@ -34,6 +34,7 @@
 #include "wave_topk.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace hipann {
 
@@ -558,8 +559,12 @@ inline int mb_group_nh(int d, int np, int nh) {
 // Dim phases: the whole split query image in LDS when 48 queries fit (NH = 1), else the image of one
 // half of the dims at a time (NH = 2: 3 terms × 768 dims × 48 queries = 221 KiB > 160 KiB of LDS),
 // swapped between the halves of every 32-row pass (needs MB_PS | super-steps per half).
+// Measured at 10M × 768 (nprobe 32 of 1024, 3 terms): NH = 2 with 48-query items 7.19 ms against NH = 1
+// with 32-query items 6.28 ms — the per-pass image swaps (block barriers, L2 → LDS refills) cost more
+// than the second group's row re-reads, so NH = 2 is opt-in (HIPANN_IVF_PHASES=2, tuning only).
 inline int mb_phases(int d, int np) {
-    if (mb_group_nh(d, np, 1) >= 16 * MF_QTMAX) return 1;
+    static const int want = [] { const char *e = std::getenv("HIPANN_IVF_PHASES"); return e ? std::atoi(e) : 1; }();
+    if (want < 2 || mb_group_nh(d, np, 1) >= 16 * MF_QTMAX) return 1;
     return mb_nsuper(d) % (2 * MB_PS) == 0 ? 2 : 1;
 }
 inline int mb_group(int d, int np) { return mb_group_nh(d, np, mb_phases(d, np)); }

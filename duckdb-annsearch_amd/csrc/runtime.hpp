@@ -174,6 +174,10 @@ struct IvfShard {
     DevBuf q, qn, coarse_d, coarse_i, cnt, bucket_off, item_off, cursor, bucket, slot_off, part_d, part_i, out_d, out_i;
     DevBuf qbound;                 // per query: best known k-th key (order-preserving u32; MFMA scan)
     DevBuf qsplit;                 // split-bf16 scans: the batch's queries as bf16 terms
+    // kFormSplit2Exact: max row ‖x‖² (for the rerank's error bound; −1 until computed), the flagged
+    // queries of the last batch and the re-run's buffers
+    float xmax2 = -1.f;
+    DevBuf nflag, flagged, fq, fD, fI, coarse_save, tmpnorm;
     // MFMA scan copy of the codes, built at the first search that uses it: per list, 32-row passes of
     // [16-dim step][2 row tiles][64 lanes][float4] (ivf_mfma.hip), zero-padded rows / dims
     std::vector<int64_t> h_off;    // host copy of list_off
@@ -183,7 +187,8 @@ struct IvfShard {
 
 struct IvfIndex : IndexBase {
     int nlist = 0, nprobe = 1;
-    int form = kFormDecomposed;
+    int form = kFormSplit2Exact;
+    int64_t rerank_fallbacks = 0;  // queries re-run on the 3-term path by the exactness check
     std::vector<std::unique_ptr<IvfShard>> shards;
     int64_t last_nq = 0;
     int last_np = 0;
@@ -227,6 +232,13 @@ int64_t ivf_max_items(int64_t nq, int nprobe, int nlist, int max_nch, int64_t nr
 int ivf_mfma_bf_group(int d, int np);
 bool ivf_mfma_bf_supported(const float *Q, int d, const float *codes, int k, int np);
 int64_t ivf_mfma_bf_qsplit_bytes(int64_t nq, int d, int np);
+void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int nprobe, int64_t nq, int k, int kout,
+                       int metric, const float *Q, const float *codes, int d, const int64_t *ids, int64_t nrows,
+                       float xmax2, float *D, int64_t *I, int *nflag, int *flagged, hipStream_t st);
+void launch_ivf_max_norm(const float *xn, int64_t n, unsigned *out, hipStream_t st);
+void launch_ivf_gather_queries(const float *Q, const int *idx, int nf, int d, float *out, hipStream_t st);
+void launch_ivf_scatter_results(const float *Df, const int64_t *If, const int *idx, int nf, int kout, float *D,
+                                int64_t *I, hipStream_t st);
 void launch_ivf_scan_mfma_bf(int np, const float *Q, int64_t nq, void *qsplit, const float *qn, int d, int metric,
                              const float *codes_t, const int64_t *tpass_off, const float *xn, const int64_t *list_off,
                              const int *cnt, const int *bucket_off, const int *item_off, const int *bucket,

@@ -97,6 +97,7 @@ def lib() -> C.CDLL:
             "hipann_ivf_set_nprobe": ([vp, i32], i32),
             "hipann_ivf_set_form": ([vp, i32], i32),
             "hipann_ivf_get_form": ([vp], i32),
+            "hipann_ivf_rerank_fallbacks": ([vp], i64),
             "hipann_ntotal": ([vp], i64),
             "hipann_dim": ([vp], i32),
             "hipann_metric": ([vp], i32),
@@ -330,11 +331,12 @@ class HipIndexIVFFlat(_Handle):
             raise HipAnnError("nprobe must be >= 1")
         self._nprobe = int(v)
 
-    FORM_DECOMPOSED = 0       # ‖q‖² + ‖x‖² − 2 q·x on the fp32 matrix cores (FAISS GPU / faiss-metal IVF form; default)
+    FORM_DECOMPOSED = 0       # ‖q‖² + ‖x‖² − 2 q·x on the fp32 matrix cores (FAISS GPU / faiss-metal IVF form)
     FORM_DIRECT = 1           # Σ(q − x)² (FAISS CPU IndexIVFFlat scanner form)
     FORM_DECOMPOSED_VALU = 2  # the decomposed form on the VALU kernel (A/B measurement)
     FORM_SPLIT3 = 3           # decomposed, q·x on the bf16 matrix cores over a 3-term bf16 split (6 products)
     FORM_SPLIT2 = 4           # decomposed, 2-term bf16 split (3 products, ~2^-16 relative per product)
+    FORM_SPLIT2_EXACT = 5     # default: the SPLIT2 scan as a filter + exact direct-form rerank with a bound check
 
     @property
     def form(self) -> int:
@@ -343,7 +345,8 @@ class HipIndexIVFFlat(_Handle):
     @form.setter
     def form(self, v: int) -> None:
         if lib().hipann_ivf_set_form(self._h, int(v)) != 0:
-            raise HipAnnError("form must be 0 (decomposed), 1 (direct), 2 (decomposed, VALU), 3 or 4 (split bf16)")
+            raise HipAnnError("form must be 0 (decomposed), 1 (direct), 2 (decomposed, VALU), 3 or 4 (split bf16), "
+                              "5 (split bf16 + exact rerank)")
 
     def search(self, x, k: int) -> Tuple[np.ndarray, np.ndarray]:
         x = _f32_2d(x, self.d)
@@ -359,6 +362,10 @@ class HipIndexIVFFlat(_Handle):
         eb = _err()
         _check(lib().hipann_ivf_search_device(self._h, nq, C.c_void_p(xq_ptr), k, C.c_void_p(d_ptr),
                                               C.c_void_p(i_ptr), C.c_void_p(stream or None), eb, 1024), eb)
+
+    def rerank_fallbacks(self) -> int:
+        """Queries the exact form's bound check re-ran on the 3-term path since creation."""
+        return int(lib().hipann_ivf_rerank_fallbacks(self._h))
 
     def last_probes(self, nq: int) -> np.ndarray:
         P = np.empty((nq, min(self._nprobe, self.nlist)), np.int64)

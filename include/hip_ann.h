@@ -122,7 +122,7 @@ int hipann_ivf_last_probes(void *index, int64_t *probes, int64_t cap, char *err_
 
 int hipann_ivf_set_nprobe(void *index, int nprobe);
 
-/* List-scan distance form.  HIPANN_IVF_FORM_DECOMPOSED (default): ‖q‖² + ‖x‖² − 2·q·x clamped ≥ 0
+/* List-scan distance form.  HIPANN_IVF_FORM_DECOMPOSED: ‖q‖² + ‖x‖² − 2·q·x clamped ≥ 0
  * (IP: q·x), with ‖x‖² stored per row — the form faiss-metal's IVF path and FAISS's GPU IVFFlat use
  * (MetalIndexIVFFlat.mm:305-318), computed on the fp32 matrix cores (exact fp32 products, fp32
  * accumulation).  HIPANN_IVF_FORM_DIRECT: Σ(q−x)², the form of FAISS's CPU IndexIVFFlat scanner
@@ -138,8 +138,16 @@ int hipann_ivf_set_nprobe(void *index, int nprobe);
  * HIPANN_IVF_FORM_SPLIT2: a 2-term split (three products, ≈2^-16 relative per product). */
 #define HIPANN_IVF_FORM_SPLIT3 3
 #define HIPANN_IVF_FORM_SPLIT2 4
+/* HIPANN_IVF_FORM_SPLIT2_EXACT (default): the SPLIT2 scan keeps the 16 best rows per list only as a
+ * filter; every returned distance is recomputed in the direct form Σ(q−x)² (IP: q·x) in fp32, ordered by
+ * (distance, label), and a per-query bound (|scan key − exact| ≤ 2^-12·(‖q‖² + max‖x‖²)) proves that no
+ * pruned row could enter the top-k — queries that fail it are re-run on SPLIT3.  k ≤ 12 (larger k: SPLIT3).
+ * The search call then synchronises its stream once (the flag count). */
+#define HIPANN_IVF_FORM_SPLIT2_EXACT 5
 int hipann_ivf_set_form(void *index, int form);
 int hipann_ivf_get_form(void *index);
+/* Queries re-run on HIPANN_IVF_FORM_SPLIT3 by the exact form's bound check since the index was created. */
+int64_t hipann_ivf_rerank_fallbacks(void *index);
 
 /* ---------------------------------------------------------------------------------------------
  * Common
