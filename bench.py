@@ -33,6 +33,7 @@ sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 FP32_MFMA_PEAK_TF = 157.3  # MI355X_MICROARCH.md: fp32 MFMA = fp32 vector peak
+BF16_MFMA_PEAK_TF = 16 * FP32_MFMA_PEAK_TF  # dense bf16 MFMA = 16x the fp32 matrix rate (~2.5 PF)
 
 
 def log(*a):
@@ -59,7 +60,7 @@ def parse():
     p.add_argument("--nprobe", type=int, default=32)
     p.add_argument("--metric", choices=["l2", "ip"], default="l2")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--no-alt-forms", action="store_true", help="ivf: skip timing the other list-scan forms")
+    p.add_argument("--no-alt-forms", action="store_true", help="ivf/flat: skip timing the other distance forms")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU sample duration")
     a = p.parse_args()
     if a.n is None:
@@ -176,6 +177,9 @@ def main():
         xq = (torch.rand((nq, d), generator=gq, device=dev, dtype=torch.float32) * 2 - 1).contiguous()
         index = hipann.HipIndexFlatDevice(d, metric, xb.data_ptr(), n_local, local_rank, copy=False,
                                           label_offset=lo)
+        # batched q·x form (hipann_flat_set_form): 1 = the library default (3-term split-bf16 products,
+        # fp32-level); A/B: 0 exact fp32 MFMA, 2 two-term split
+        index.form = int(os.environ.get("HIPANN_FLAT_FORM", "1"))
         search = index.search_device
         workload = f"FAISS Flat {'L2' if metric == 0 else 'IP'}, {n // 1_000_000}Mx{d} fp32, batch={nq}, k={k}"
     else:
@@ -310,14 +314,48 @@ def main():
         index.form = base_form
         extra["rerank_fallbacks_total"] = index.rerank_fallbacks()
 
+    if args.workload == "flat" and world == 1 and not args.no_alt_forms:
+        alt = {}
+        base_form = index.form
+        for f, nm in ((0, "fp32_mfma (exact fp32 products)"), (1, "split3 (3-term bf16 split, 6 products; default)")):
+            if f == base_form:
+                continue
+            index.form = f
+            step()
+            torch.cuda.synchronize()
+            index.set_kernel_timing(True)
+            ta = time.perf_counter()
+            for _ in range(3):
+                step()
+            torch.cuda.synchronize()
+            el = time.perf_counter() - ta
+            kms = index.kernel_ms(0)
+            index.set_kernel_timing(False)
+            _, Ia = step()
+            torch.cuda.synchronize()
+            same = float((Ia == Ir).float().mean().item())
+            alt[nm] = {"queries_per_s": round(nq * 3 / el, 1), "kernel_ms": round(kms, 3),
+                       "ids_equal_to_reported_form": round(same, 5)}
+        index.form = base_form
+
     # ---------------- roofline of the dominant kernel ----------------
     if args.workload == "flat":
         flops = 2.0 * nq * n_local * d
-        achieved = flops / (kern_ms * 1e-3) / 1e12 if kern_ms > 0 else 0.0
-        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TF, "unit": "TFLOP/s",
-                "frac": round(achieved / FP32_MFMA_PEAK_TF, 4), "traffic": None,
-                "kernel": "flat_gemm_topk", "kernel_ms": round(kern_ms, 3), "merge_ms": round(merge_ms, 3),
-                "algorithmic": f"2*nq*N_local*d = {flops:.4g} FLOP per launch"}
+        fform = index.form
+        if fform == 0:
+            kname, terms, peak, fdesc = "flat_gemm_topk2", 1, FP32_MFMA_PEAK_TF, "fp32 MFMA (v_mfma_f32_32x32x2_f32)"
+        else:
+            terms = 6 if fform == 1 else 3
+            kname, peak = "flat_gemm_topk_bf", BF16_MFMA_PEAK_TF
+            fdesc = (f"bf16 MFMA (v_mfma_f32_32x32x16_bf16) over a {3 if fform == 1 else 2}-term split: "
+                     f"{terms} bf16 products per fp32 product")
+        achieved = terms * flops / (kern_ms * 1e-3) / 1e12 if kern_ms > 0 else 0.0
+        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4), "traffic": None,
+                "kernel": kname, "kernel_ms": round(kern_ms, 3), "merge_ms": round(merge_ms, 3),
+                "algorithmic": f"{terms} x 2*nq*N_local*d = {terms * flops:.4g} MFMA FLOP per launch",
+                "form": fdesc,
+                "fp32_equivalent_tflops": round(flops / (kern_ms * 1e-3) / 1e12, 2) if kern_ms > 0 else None}
     else:
         b_alg = extra.get("scan_bytes_per_batch_local", 0.0)
         form = index.form
@@ -377,7 +415,7 @@ def main():
         if extra:
             line["ivf"] = {kk: v for kk, v in extra.items() if kk != "scan_bytes_per_batch_local"}
         if alt:
-            line["ivf_other_forms"] = alt
+            line["ivf_other_forms" if args.workload == "ivf" else "flat_other_forms"] = alt
         if args.workload == "ivf" and index.form == 5:
             line["precision"] = ("returned distances are fp32 direct-form Σ(q−x)² (FAISS CPU IVFFlatScanner arithmetic); "
                                  "the bf16 2-term split scan only prunes, and a per-query bound "

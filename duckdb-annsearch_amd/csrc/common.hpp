@@ -46,6 +46,10 @@ enum IvfForm : int {
     kFormSplit2Exact = 5
 };
 constexpr int kRerankK = 16, kRerankMaxK = 12;
+// Flat BLAS-path (nq >= kBlasThreshold) q·x form (hipann_flat_set_form): exact fp32 MFMA products
+// (flat_gemm_topk2), or the fp32-level 3-term split-bf16 products on the bf16 matrix cores
+// (flat_gemm_topk_bf, the default); kFlatSplit2 is the 2-term split (≈2^-16 relative, A/B only).
+enum FlatForm : int { kFlatFp32 = 0, kFlatSplit3 = 1, kFlatSplit2 = 2 };
 __host__ __device__ inline bool ivf_form_split(int f) { return f == kFormSplit3 || f == kFormSplit2; }
 __host__ __device__ inline int ivf_form_terms(int f) { return f == kFormSplit3 ? 3 : 2; }
 

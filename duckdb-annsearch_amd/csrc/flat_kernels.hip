@@ -303,6 +303,73 @@ __device__ __forceinline__ void g2_stage_store(float *__restrict__ lds, const fl
 
 size_t gemm2_smem_bytes(int k) { return (size_t)4 * GBM * GBK * sizeof(float) + (size_t)GBM * k * 8; }
 
+// Epilogue of one 128×128 tile (wave = 32 query rows × 128 columns): keys straight from the
+// accumulators, filtered by the per-row thresholds; rows with a passing key go through the WaveList.
+template <bool L2M>
+__device__ __forceinline__ void g2_epilogue(const f32x16 (&acc)[4], float (&thr)[16], const float (&qnv)[16],
+                                            const float (&xnv)[4], int64_t x0, int64_t N, float *__restrict__ Ld,
+                                            int *__restrict__ Li, int k, int wave, int lane) {
+    const int l31 = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        float key[4];
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float ip = acc[j][r];
+            float kv;
+            if (L2M) {
+                kv = fmaf(-2.f, ip, qnv[r] + xnv[j]);
+                kv = kv < 0.f ? 0.f : kv;
+            } else {
+                kv = -ip;
+            }
+            if (x0 + 32 * j + l31 >= N) kv = __builtin_inff();
+            key[j] = kv;
+            any |= kv <= thr[r];
+        }
+        const unsigned long long m = __ballot(any);
+        if (m == 0ull) continue;
+        // slow path (rare after the first tiles): each half of the wave is one query
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            if (((m >> (32 * hh)) & 0xffffffffull) == 0ull) continue;
+            const int ql = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            const int src = 32 * hh + l31;
+            const float c0 = __shfl(key[0], src), c1 = __shfl(key[1], src);
+            const float c2 = __shfl(key[2], src), c3 = __shfl(key[3], src);
+            const float v0 = lane < 32 ? c0 : c1, v1 = lane < 32 ? c2 : c3;
+            const int64_t col0 = x0 + (lane < 32 ? 0 : 32) + l31, col1 = col0 + 64;
+            WaveList<1, int> L;
+            L.d[0] = lane < k ? Ld[ql * k + lane] : __builtin_inff();
+            L.id[0] = lane < k ? Li[ql * k + lane] : 0x7fffffff;
+            L.offer(v0, col0 < N ? (int)col0 : 0x7fffffff, k - 1);
+            L.offer(v1, col1 < N ? (int)col1 : 0x7fffffff, k - 1);
+            if (lane < k) {
+                Ld[ql * k + lane] = L.d[0];
+                Li[ql * k + lane] = L.id[0];
+            }
+            const float nt = readlane_f(L.d[0], k - 1);
+            if (h == hh) thr[r] = nt;
+        }
+    }
+}
+
+// per-(split, query) partial lists (each wave wrote only its own rows: no barrier needed)
+__device__ __forceinline__ void g2_write_parts(const float *__restrict__ Ld, const int *__restrict__ Li, int64_t q0,
+                                               int64_t nq, int k, int split, int wave, int lane,
+                                               float *__restrict__ part_d, int *__restrict__ part_i) {
+    for (int r = 0; r < 32; ++r) {
+        const int ql = 32 * wave + r;
+        const int64_t q = q0 + ql;
+        if (q < nq && lane < k) {
+            const int64_t off = ((int64_t)split * nq + q) * k;
+            part_d[off + lane] = Ld[ql * k + lane];
+            part_i[off + lane] = Li[ql * k + lane];
+        }
+    }
+}
+
 template <bool VEC4, bool L2M>
 __global__ void __launch_bounds__(256, 2)
 flat_gemm_topk2(const float *__restrict__ Q, const float *__restrict__ qnorm, int64_t nq,
@@ -403,62 +470,221 @@ flat_gemm_topk2(const float *__restrict__ Q, const float *__restrict__ qnorm, in
             gemm_stage_load<VEC4>(X, (t + 1) * GBN, N, d, 0, sb);
         }
 
-        // epilogue: keys straight from the accumulators, filtered by the per-row thresholds
+        g2_epilogue<L2M>(acc, thr, qnv, xnv, x0, N, Ld, Li, k, wave, lane);
+    }
+    g2_write_parts(Ld, Li, q0, nq, k, split, wave, lane, part_d, part_i);
+}
+
+// ---------------------------------------------------------------------------------------------
+// flat_gemm_topk_bf — flat_gemm_topk2 with q·x on the bf16 matrix cores (v_mfma_f32_32x32x16_bf16,
+// 16× the fp32 matrix rate) over an NP-term round-to-nearest bf16 split of both operands: x = x₁ + x₂
+// + x₃, each term the bf16 rounding of what the previous ones leave (exact fp32 subtractions).
+//   NP = 3: x₁y₁ + x₁y₂ + x₂y₁ + x₁y₃ + x₃y₁ + x₂y₂ (the dropped products are ≤ 2⁻²⁶ relative):
+//           fp32-level products, fp32 accumulation — the split of the IVF forms (ivf_mfma.hip).
+//   NP = 2: x₁y₁ + x₁y₂ + x₂y₁, ≈ 2⁻¹⁶ relative per product (tuning / A-B only).
+// Operands:
+//   * queries: split once per batch (flat_split_queries) into qsplit [query][term][dpad] bf16 (dpad =
+//     d rounded up to 32, zero-filled).  Each lane loads its A fragments (8 bf16 per MFMA) straight
+//     from L2, one K chunk ahead: a 128-query tile's image is 128·dpad·2·NP B (590 KB at d = 768, 3
+//     terms), re-read per database tile like flat_gemm_topk2's LDS-staged queries;
+//   * database rows: the 128×32 fp32 chunk is loaded exactly as in flat_gemm_topk2 (coalesced float4
+//     per lane, register staging one chunk ahead) and split while it is stored to LDS as
+//     [term][16-B group c][row ^ 4c][8 bf16]: the XOR keeps the b64 stores (4 groups of one row per
+//     lane octet) and the b128 fragment reads (32 consecutive rows per group) conflict-free.
+// MFMA s ∈ {0, 1} of a 32-dim chunk: lane half h holds dims 16s + 8h .. +7 of its A row and B column
+// (group c = 2s + h).  Tile, grid, thresholds and the epilogue are flat_gemm_topk2's; LDS = 2 stages ×
+// NP × 8 KiB + 128·k·8 B of lists → 2 blocks per CU for k ≤ 32 at NP = 3.
+// ---------------------------------------------------------------------------------------------
+typedef __bf16 fb_bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 fb_bf16x2 __attribute__((ext_vector_type(2)));
+typedef float fb_f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ unsigned fb_pack(float a, float b) {
+    const fb_bf16x2 v = __builtin_convertvector((fb_f32x2){a, b}, fb_bf16x2);
+    return __builtin_bit_cast(unsigned, v);
+}
+__device__ __forceinline__ float fb_lo(unsigned p) { return __uint_as_float(p << 16); }
+__device__ __forceinline__ float fb_hi(unsigned p) { return __uint_as_float(p & 0xffff0000u); }
+
+// 4 fp32 → NP terms of 4 bf16 (two dwords each)
+template <int NP>
+__device__ __forceinline__ void fb_split4(const float4 &v, uint2 (&o)[NP]) {
+    fb_f32x2 x0 = {v.x, v.y}, x1 = {v.z, v.w};
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            float key[4];
-            bool any = false;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float ip = acc[j][r];
-                float kv;
-                if (L2M) {
-                    kv = fmaf(-2.f, ip, qnv[r] + xnv[j]);
-                    kv = kv < 0.f ? 0.f : kv;
-                } else {
-                    kv = -ip;
-                }
-                if (x0 + 32 * j + l31 >= N) kv = __builtin_inff();
-                key[j] = kv;
-                any |= kv <= thr[r];
-            }
-            const unsigned long long m = __ballot(any);
-            if (m == 0ull) continue;
-            // slow path (rare after the first tiles): each half of the wave is one query
-#pragma unroll
-            for (int hh = 0; hh < 2; ++hh) {
-                if (((m >> (32 * hh)) & 0xffffffffull) == 0ull) continue;
-                const int ql = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * hh;
-                const int src = 32 * hh + l31;
-                const float c0 = __shfl(key[0], src), c1 = __shfl(key[1], src);
-                const float c2 = __shfl(key[2], src), c3 = __shfl(key[3], src);
-                const float v0 = lane < 32 ? c0 : c1, v1 = lane < 32 ? c2 : c3;
-                const int64_t col0 = x0 + (lane < 32 ? 0 : 32) + l31, col1 = col0 + 64;
-                WaveList<1, int> L;
-                L.d[0] = lane < k ? Ld[ql * k + lane] : __builtin_inff();
-                L.id[0] = lane < k ? Li[ql * k + lane] : 0x7fffffff;
-                L.offer(v0, col0 < N ? (int)col0 : 0x7fffffff, k - 1);
-                L.offer(v1, col1 < N ? (int)col1 : 0x7fffffff, k - 1);
-                if (lane < k) {
-                    Ld[ql * k + lane] = L.d[0];
-                    Li[ql * k + lane] = L.id[0];
-                }
-                const float nt = readlane_f(L.d[0], k - 1);
-                if (h == hh) thr[r] = nt;
-            }
+    for (int j = 0; j < NP; ++j) {
+        const unsigned p0 = fb_pack(x0[0], x0[1]), p1 = fb_pack(x1[0], x1[1]);
+        o[j] = make_uint2(p0, p1);
+        if (j + 1 < NP) {
+            x0 -= (fb_f32x2){fb_lo(p0), fb_hi(p0)};
+            x1 -= (fb_f32x2){fb_lo(p1), fb_hi(p1)};
         }
+    }
+}
+
+// LDS B stage: NP terms × 4 groups × 128 rows × 16 B
+constexpr int FB_STAGE16 = 4 * GBN;  // 16-B units per term
+__device__ __forceinline__ int fb_slot(int c, int row) { return c * GBN + (row ^ (c << 2)); }
+
+template <int NP>
+__device__ __forceinline__ void fb_stage_store(uint2 *__restrict__ lds, const float4 (&r)[4]) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const int f = t + 256 * p;
+        const int row = f >> 3, c4 = f & 7;
+        uint2 o[NP];
+        fb_split4<NP>(r[p], o);
+        const int s = 2 * fb_slot(c4 >> 1, row) + (c4 & 1);
+#pragma unroll
+        for (int j = 0; j < NP; ++j) lds[j * 2 * FB_STAGE16 + s] = o[j];
+    }
+}
+
+// term pairs (A term, B term) of the products, smallest first
+template <int NP>
+struct FbProducts;
+template <>
+struct FbProducts<3> {
+    static constexpr int n = 6;
+    __device__ static constexpr int a(int i) { return i == 0 ? 2 : i == 1 ? 0 : i == 2 ? 1 : i == 3 ? 0 : i == 4 ? 1 : 0; }
+    __device__ static constexpr int b(int i) { return i == 0 ? 0 : i == 1 ? 2 : i == 2 ? 1 : i == 3 ? 1 : i == 4 ? 0 : 0; }
+};
+template <>
+struct FbProducts<2> {
+    static constexpr int n = 3;
+    __device__ static constexpr int a(int i) { return i == 0 ? 1 : 0; }
+    __device__ static constexpr int b(int i) { return i == 1 ? 1 : 0; }
+};
+
+size_t gemm_bf_smem_bytes(int np, int k) { return (size_t)2 * np * FB_STAGE16 * 16 + (size_t)GBM * k * 8; }
+
+template <bool VEC4, bool L2M, int NP>
+__global__ void __launch_bounds__(256, 2)
+flat_gemm_topk_bf(const uint4 *__restrict__ qsplit, int dpad, const float *__restrict__ qnorm, int64_t nq,
+                  const float *__restrict__ X, const float *__restrict__ xnorm, int64_t N, int d, int k, int nqt,
+                  int nsplit, int64_t tiles_per_split, float *__restrict__ part_d, int *__restrict__ part_i) {
+    extern __shared__ __attribute__((aligned(16))) uint4 smem_bf[];
+    uint4 *Bs0 = smem_bf;
+    uint4 *Bs1 = smem_bf + NP * FB_STAGE16;
+    float *Ld = reinterpret_cast<float *>(smem_bf + 2 * NP * FB_STAGE16);  // [128][k] keys
+    int *Li = reinterpret_cast<int *>(Ld + GBM * k);                        // [128][k] ids
+
+    const int nblocks = nqt * nsplit;
+    const int lb = xcd_remap(blockIdx.x, nblocks);
+    const int qt = lb % nqt;
+    const int split = lb / nqt;
+    const int64_t q0 = (int64_t)qt * GBM;
+    const int64_t ntiles = ceil_div(N, GBN);
+    const int64_t t0 = (int64_t)split * tiles_per_split;
+    const int64_t t1 = t0 + tiles_per_split < ntiles ? t0 + tiles_per_split : ntiles;
+
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int l31 = lane & 31, h = lane >> 5;
+
+    for (int e = tid; e < GBM * k; e += 256) {
+        Ld[e] = __builtin_inff();
+        Li[e] = 0x7fffffff;
+    }
+    float thr[16], qnv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int64_t q = q0 + 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * h;
+        thr[r] = q < nq ? __builtin_inff() : -__builtin_inff();
+        qnv[r] = (L2M && q < nq) ? qnorm[q] : 0.f;
+    }
+    // this lane's A row (rows past nq re-read the last query; their thresholds admit nothing)
+    int64_t qa = q0 + 32 * wave + l31;
+    qa = qa < nq ? qa : nq - 1;
+    const int dq = dpad >> 3;  // 16-B units per query term
+    const uint4 *qrow = qsplit + qa * NP * dq + h;
+    __syncthreads();
+
+    const int nk = dpad / GBK;
+    float4 sb[4];
+    uint4 af[NP][2], an[NP][2];
+    if (t0 < t1) {
+        gemm_stage_load<VEC4>(X, t0 * GBN, N, d, 0, sb);
+#pragma unroll
+        for (int j = 0; j < NP; ++j)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) af[j][s] = qrow[j * dq + 2 * s];
     }
 
-    // per-(split, query) partial lists (each wave wrote only its own rows: no barrier needed)
-    for (int r = 0; r < 32; ++r) {
-        const int ql = 32 * wave + r;
-        const int64_t q = q0 + ql;
-        if (q < nq && lane < k) {
-            const int64_t off = ((int64_t)split * nq + q) * k;
-            part_d[off + lane] = Ld[ql * k + lane];
-            part_i[off + lane] = Li[ql * k + lane];
+    for (int64_t t = t0; t < t1; ++t) {
+        const int64_t x0 = t * GBN;
+        fb_stage_store<NP>(reinterpret_cast<uint2 *>(Bs0), sb);
+        float xnv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t x = x0 + 32 * j + l31;
+            xnv[j] = (L2M && x < N) ? xnorm[x] : 0.f;
         }
+        __syncthreads();
+
+        f32x16 acc[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+
+        for (int kc = 0; kc < nk; ++kc) {
+            const uint4 *Bb = (kc & 1) ? Bs1 : Bs0;
+            if (kc + 1 < nk) gemm_stage_load<VEC4>(X, x0, N, d, (kc + 1) * GBK, sb);
+            const int kn = kc + 1 < nk ? kc + 1 : 0;  // the next tile starts over at chunk 0
+#pragma unroll
+            for (int j = 0; j < NP; ++j)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) an[j][s] = qrow[j * dq + 4 * kn + 2 * s];
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int c = 2 * s + h;
+#pragma unroll
+                for (int jb = 0; jb < 4; ++jb) {
+                    uint4 bt[NP];
+#pragma unroll
+                    for (int j = 0; j < NP; ++j) bt[j] = Bb[j * FB_STAGE16 + fb_slot(c, 32 * jb + l31)];
+#pragma unroll
+                    for (int pr = 0; pr < FbProducts<NP>::n; ++pr)
+                        acc[jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                            __builtin_bit_cast(fb_bf16x8, af[FbProducts<NP>::a(pr)][s]),
+                            __builtin_bit_cast(fb_bf16x8, bt[FbProducts<NP>::b(pr)]), acc[jb], 0, 0, 0);
+                }
+            }
+            if (kc + 1 < nk) fb_stage_store<NP>(reinterpret_cast<uint2 *>((kc & 1) ? Bs0 : Bs1), sb);
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < NP; ++j)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) af[j][s] = an[j][s];
+        }
+
+        if (t + 1 < t1) gemm_stage_load<VEC4>(X, (t + 1) * GBN, N, d, 0, sb);
+        g2_epilogue<L2M>(acc, thr, qnv, xnv, x0, N, Ld, Li, k, wave, lane);
     }
+    g2_write_parts(Ld, Li, q0, nq, k, split, wave, lane, part_d, part_i);
+}
+
+// The batch's queries split once into NP bf16 terms: qsplit [query][term][dpad] (dims in order, zero
+// past d).  One thread per 4 dims.
+template <int NP>
+__global__ void __launch_bounds__(256) flat_split_queries(const float *__restrict__ Q, int64_t nq, int d, int dpad,
+                                                          uint2 *__restrict__ qs) {
+    const int ng = dpad >> 2;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= nq * ng) return;
+    const int64_t q = i / ng;
+    const int g = (int)(i - q * ng), dim = 4 * g;
+    const float *src = Q + q * (int64_t)d + dim;
+    float4 v;
+    v.x = dim + 0 < d ? src[0] : 0.f;
+    v.y = dim + 1 < d ? src[1] : 0.f;
+    v.z = dim + 2 < d ? src[2] : 0.f;
+    v.w = dim + 3 < d ? src[3] : 0.f;
+    uint2 o[NP];
+    fb_split4<NP>(v, o);
+#pragma unroll
+    for (int j = 0; j < NP; ++j) qs[(q * NP + j) * ng + g] = o[j];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -716,6 +942,41 @@ void launch_flat_gemm_topk(const float *Q, const float *qn, int64_t nq, const fl
                            nsplit, tiles_per_split, pd, pi);
     }
     HIPANN_CHECK(hipGetLastError());
+}
+
+int flat_bf_dpad(int d) { return (d + GBK - 1) / GBK * GBK; }
+size_t flat_bf_qsplit_bytes(int64_t nq, int d, int np) { return (size_t)nq * np * flat_bf_dpad(d) * 2; }
+
+template <int NP>
+static void launch_flat_gemm_topk_bf_t(const float *Q, const float *qn, int64_t nq, void *qsplit, const float *X,
+                                       const float *xn, int64_t N, int d, int metric, int k, int nsplit,
+                                       int64_t tiles_per_split, float *pd, int *pi, hipStream_t st) {
+    const int dpad = flat_bf_dpad(d);
+    const int64_t ng = nq * (dpad / 4);
+    hipLaunchKernelGGL(flat_split_queries<NP>, dim3((unsigned)ceil_div(ng, 256)), dim3(256), 0, st, Q, nq, d, dpad,
+                       reinterpret_cast<uint2 *>(qsplit));
+    HIPANN_CHECK(hipGetLastError());
+    const int nqt = (int)ceil_div(nq, GBM);
+    const bool vec4 = (d % 4 == 0) && ((uintptr_t)X % 16 == 0);
+    const size_t smem = gemm_bf_smem_bytes(NP, k);
+    HIPANN_REQUIRE(smem <= 160 * 1024, "k too large for the split-bf16 Flat kernel");
+    dim3 grid((unsigned)(nqt * nsplit)), block(256);
+    const uint4 *qs = reinterpret_cast<const uint4 *>(qsplit);
+    if (metric == kL2) {
+        if (vec4) hipLaunchKernelGGL((flat_gemm_topk_bf<true, true, NP>), grid, block, smem, st, qs, dpad, qn, nq, X, xn, N, d, k, nqt, nsplit, tiles_per_split, pd, pi);
+        else hipLaunchKernelGGL((flat_gemm_topk_bf<false, true, NP>), grid, block, smem, st, qs, dpad, qn, nq, X, xn, N, d, k, nqt, nsplit, tiles_per_split, pd, pi);
+    } else {
+        if (vec4) hipLaunchKernelGGL((flat_gemm_topk_bf<true, false, NP>), grid, block, smem, st, qs, dpad, qn, nq, X, xn, N, d, k, nqt, nsplit, tiles_per_split, pd, pi);
+        else hipLaunchKernelGGL((flat_gemm_topk_bf<false, false, NP>), grid, block, smem, st, qs, dpad, qn, nq, X, xn, N, d, k, nqt, nsplit, tiles_per_split, pd, pi);
+    }
+    HIPANN_CHECK(hipGetLastError());
+}
+
+void launch_flat_gemm_topk_bf(int np, const float *Q, const float *qn, int64_t nq, void *qsplit, const float *X,
+                              const float *xn, int64_t N, int d, int metric, int k, int nsplit, int64_t tiles_per_split,
+                              float *pd, int *pi, hipStream_t st) {
+    if (np == 2) launch_flat_gemm_topk_bf_t<2>(Q, qn, nq, qsplit, X, xn, N, d, metric, k, nsplit, tiles_per_split, pd, pi, st);
+    else launch_flat_gemm_topk_bf_t<3>(Q, qn, nq, qsplit, X, xn, N, d, metric, k, nsplit, tiles_per_split, pd, pi, st);
 }
 
 size_t scan_smem_bytes(int nq, int d);

@@ -240,8 +240,15 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
     sh.part_i.ensure((size_t)nsplit * nq * k * sizeof(int), sh.device);
     {
         ScopedTiming t(ix.timer_main, st);
-        launch_flat_gemm_topk(xq, qn, nq, sh.xb, sh.xn.get<float>(), sh.n, d, metric, k, (int)nsplit, tps,
-                              sh.part_d.get<float>(), sh.part_i.get<int>(), st);
+        if (ix.form == kFlatFp32) {
+            launch_flat_gemm_topk(xq, qn, nq, sh.xb, sh.xn.get<float>(), sh.n, d, metric, k, (int)nsplit, tps,
+                                  sh.part_d.get<float>(), sh.part_i.get<int>(), st);
+        } else {
+            const int np = ix.form == kFlatSplit2 ? 2 : 3;
+            sh.qsplit.ensure(flat_bf_qsplit_bytes(nq, d, np), sh.device);
+            launch_flat_gemm_topk_bf(np, xq, qn, nq, sh.qsplit.get<void>(), sh.xb, sh.xn.get<float>(), sh.n, d, metric,
+                                     k, (int)nsplit, tps, sh.part_d.get<float>(), sh.part_i.get<int>(), st);
+        }
     }
     ScopedTiming t(ix.timer_merge, st);
     launch_merge_parts<int>(sh.part_d.get<float>(), sh.part_i.get<int>(), (int)nsplit, nq, k, kout, sh.label_offset,
@@ -497,6 +504,23 @@ int64_t hipann_ntotal(void *h) { return h ? static_cast<IndexBase *>(h)->ntotal(
 int hipann_dim(void *h) { return h ? static_cast<IndexBase *>(h)->d : -1; }
 int hipann_metric(void *h) { return h ? static_cast<IndexBase *>(h)->metric : -1; }
 int64_t hipann_memory_bytes(void *h) { return h ? static_cast<IndexBase *>(h)->memory_bytes() : -1; }
+
+int hipann_flat_set_form(void *h, int form) {
+    if (!h || form < kFlatFp32 || form > kFlatSplit2) return -1;
+    auto *ix = static_cast<IndexBase *>(h);
+    if (ix->kind != Kind::Flat) return -1;
+    auto *fx = static_cast<FlatIndex *>(ix);
+    std::lock_guard<std::mutex> lk(fx->mu);
+    fx->form = form;
+    return 0;
+}
+
+int hipann_flat_get_form(void *h) {
+    if (!h) return -1;
+    auto *ix = static_cast<IndexBase *>(h);
+    if (ix->kind != Kind::Flat) return -1;
+    return static_cast<FlatIndex *>(ix)->form;
+}
 
 void hipann_free(void *h) {
     if (!h) return;

@@ -57,6 +57,7 @@ hipStream_t make_stream(int dev) {
 std::unique_ptr<FlatIndex> make_quantizer(int d, int metric, const float *cen, int nlist, int device,
                                           hipStream_t stream) {
     auto q = std::make_unique<FlatIndex>();
+    q->form = kFlatFp32;  // coarse assignment stays on exact fp32 products
     q->d = d;
     q->metric = metric;
     auto sh = std::make_unique<FlatShard>();

@@ -124,6 +124,7 @@ struct FlatShard {
     // scratch
     DevBuf q, qn, part_d, part_i, out_d, out_i;
     DevBuf keys, run_d, run_i, run2_d, run2_i;  // k > 64 path
+    DevBuf qsplit;                              // split-bf16 form: the batch's queries as bf16 terms
 };
 
 struct IndexBase {
@@ -140,6 +141,7 @@ struct IndexBase {
 
 struct FlatIndex : IndexBase {
     std::vector<std::unique_ptr<FlatShard>> shards;
+    int form = kFlatSplit3;  // BLAS-path q·x form (FlatForm)
     HostBuf h_q, h_d, h_i;
     DevBuf gather_d, gather_i, merged_d, merged_i;  // multi-device merge on shards[0]'s device
     FlatIndex() : IndexBase(Kind::Flat) {}
@@ -214,6 +216,10 @@ size_t gemm_smem_bytes();
 void launch_flat_gemm_topk(const float *Q, const float *qn, int64_t nq, const float *X, const float *xn, int64_t N,
                            int d, int metric, int k, int nsplit, int64_t tiles_per_split, float *pd, int *pi,
                            hipStream_t st);
+size_t flat_bf_qsplit_bytes(int64_t nq, int d, int np);
+void launch_flat_gemm_topk_bf(int np, const float *Q, const float *qn, int64_t nq, void *qsplit, const float *X,
+                              const float *xn, int64_t N, int d, int metric, int k, int nsplit, int64_t tiles_per_split,
+                              float *pd, int *pi, hipStream_t st);
 size_t scan_smem_bytes(int nq, int d);
 void launch_flat_gemm_keys(const float *Q, const float *qn, int64_t nq, const float *X, const float *xn, int64_t N,
                            int d, int metric, float *keys, int64_t ldk, hipStream_t st);

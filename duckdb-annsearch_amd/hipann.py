@@ -88,6 +88,8 @@ def lib() -> C.CDLL:
             "hipann_flat_reconstruct": ([vp, i64, f, cp, i32], i32),
             "hipann_flat_create_device": ([i32, i32, vp, i64, i32, i32, i64, cp, i32], vp),
             "hipann_flat_search_device": ([vp, i64, vp, i64, vp, vp, vp, cp, i32], i32),
+            "hipann_flat_set_form": ([vp, i32], i32),
+            "hipann_flat_get_form": ([vp], i32),
             "hipann_merge_topk_device": ([i32, i32, i64, i64, vp, vp, vp, vp, vp, cp, i32], i32),
             "hipann_ivf_create": ([i32, i32, i32, i32, f, i64p, i64p, f, C.POINTER(C.c_int), i32, cp, i32], vp),
             "hipann_ivf_create_device": ([i32, i32, i32, i32, vp, i64p, vp, vp, i32, i32, cp, i32], vp),
@@ -217,7 +219,24 @@ class _Handle:
         return self._h
 
 
-class HipIndexFlat(_Handle):
+class _FlatForm:
+    """q·x form of the batched (nq >= 20) Flat path — hipann_flat_set_form (hip_ann.h)."""
+
+    FORM_FP32 = 0    # exact fp32 products on the fp32 matrix cores
+    FORM_SPLIT3 = 1  # default: 3-term split-bf16 products (fp32-level) on the bf16 matrix cores
+    FORM_SPLIT2 = 2  # 2-term split (~2^-16 relative per product; measurement only)
+
+    @property
+    def form(self) -> int:
+        return int(lib().hipann_flat_get_form(self._h))
+
+    @form.setter
+    def form(self, v: int) -> None:
+        if lib().hipann_flat_set_form(self._h, int(v)) != 0:
+            raise HipAnnError("form must be 0 (fp32), 1 (split bf16, 3 terms) or 2 (split bf16, 2 terms)")
+
+
+class HipIndexFlat(_FlatForm, _Handle):
     """Flat index on MI355X — MetalIndexFlat's API (MetalIndexFlat.h:45-101)."""
 
     def __init__(self, d: int, metric: int = METRIC_L2, xb=None, devices: Optional[Sequence[int]] = None):
@@ -252,7 +271,7 @@ class HipIndexFlat(_Handle):
         return out
 
 
-class HipIndexFlatDevice(_Handle):
+class HipIndexFlatDevice(_FlatForm, _Handle):
     """Flat shard over an HBM-resident matrix (torch CUDA tensor or raw pointer) — the sharded /
     benchmark path.  ``search_device`` is asynchronous on ``stream``."""
 

@@ -72,6 +72,18 @@ int hipann_flat_search(void *index, int64_t nq, const float *xq, int64_t k, floa
 /* Copy vector `key` back to host (faiss::Index::reconstruct; MetalIndexFlat::reconstruct). */
 int hipann_flat_reconstruct(void *index, int64_t key, float *out, char *err_buf, int err_len);
 
+/* q·x form of the batched (nq >= 20, FAISS's BLAS threshold) distance path, ‖q‖² + ‖x‖² − 2·q·x.
+ * HIPANN_FLAT_FORM_FP32: exact fp32 products on the fp32 matrix cores (v_mfma_f32_32x32x2_f32).
+ * HIPANN_FLAT_FORM_SPLIT3 (default): both operands split into three round-to-nearest bf16 terms, the
+ * six products above 2^-26 relative on the bf16 matrix cores, fp32 accumulation — fp32-level products
+ * at several times the fp32 rate.  HIPANN_FLAT_FORM_SPLIT2: two terms, three products (≈2^-16
+ * relative per product; measurement only).  Returns 0, or -1 for a bad handle / form. */
+#define HIPANN_FLAT_FORM_FP32 0
+#define HIPANN_FLAT_FORM_SPLIT3 1
+#define HIPANN_FLAT_FORM_SPLIT2 2
+int hipann_flat_set_form(void *index, int form);
+int hipann_flat_get_form(void *index);
+
 /* ---------------------------------------------------------------------------------------------
  * Device-resident variants (inputs and outputs already in HBM).  Used by the multi-GPU sharded
  * search (one process per GPU, partial top-k gathered over RCCL) and by bench.py, whose timed
