@@ -177,9 +177,9 @@ def main():
         xq = (torch.rand((nq, d), generator=gq, device=dev, dtype=torch.float32) * 2 - 1).contiguous()
         index = hipann.HipIndexFlatDevice(d, metric, xb.data_ptr(), n_local, local_rank, copy=False,
                                           label_offset=lo)
-        # batched q·x form (hipann_flat_set_form): 1 = the library default (3-term split-bf16 products,
-        # fp32-level); A/B: 0 exact fp32 MFMA, 2 two-term split
-        index.form = int(os.environ.get("HIPANN_FLAT_FORM", "1"))
+        # batched q·x form (hipann_flat_set_form): 3 = the library default (2-term split-bf16 scan as a
+        # filter + exact direct-form rerank); A/B: 0 exact fp32 MFMA, 1 three-term split, 2 two-term split
+        index.form = int(os.environ.get("HIPANN_FLAT_FORM", "3"))
         search = index.search_device
         workload = f"FAISS Flat {'L2' if metric == 0 else 'IP'}, {n // 1_000_000}Mx{d} fp32, batch={nq}, k={k}"
     else:
@@ -317,7 +317,7 @@ def main():
     if args.workload == "flat" and world == 1 and not args.no_alt_forms:
         alt = {}
         base_form = index.form
-        for f, nm in ((0, "fp32_mfma (exact fp32 products)"), (1, "split3 (3-term bf16 split, 6 products; default)")):
+        for f, nm in ((0, "fp32_mfma (exact fp32 products)"), (1, "split3 (3-term bf16 split, 6 products)")):
             if f == base_form:
                 continue
             index.form = f
@@ -349,6 +349,9 @@ def main():
             kname, peak = "flat_gemm_topk_bf", BF16_MFMA_PEAK_TF
             fdesc = (f"bf16 MFMA (v_mfma_f32_32x32x16_bf16) over a {3 if fform == 1 else 2}-term split: "
                      f"{terms} bf16 products per fp32 product")
+            if fform == 3:
+                fdesc += ("; the scan keeps 16 per (split, query) as a filter, merge_ms = exact direct-form "
+                          "rerank of the 16 + bound check")
         achieved = terms * flops / (kern_ms * 1e-3) / 1e12 if kern_ms > 0 else 0.0
         roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": None,
@@ -416,6 +419,12 @@ def main():
             line["ivf"] = {kk: v for kk, v in extra.items() if kk != "scan_bytes_per_batch_local"}
         if alt:
             line["ivf_other_forms" if args.workload == "ivf" else "flat_other_forms"] = alt
+        if args.workload == "flat" and index.form == 3:
+            line["precision"] = ("returned distances are fp32 direct-form Σ(q−x)² of the returned rows; the bf16 2-term "
+                                 "split scan only prunes, and a per-query bound (|scan key − exact| ≤ "
+                                 "2^-12·(|q|²+max|x|²)) proves no pruned row reaches the top-k (failures re-run on the "
+                                 "3-term path)")
+            line["flat"] = {"rerank_fallbacks_total": index.rerank_fallbacks()}
         if args.workload == "ivf" and index.form == 5:
             line["precision"] = ("returned distances are fp32 direct-form Σ(q−x)² (FAISS CPU IVFFlatScanner arithmetic); "
                                  "the bf16 2-term split scan only prunes, and a per-query bound "

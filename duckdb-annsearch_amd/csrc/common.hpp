@@ -48,8 +48,11 @@ enum IvfForm : int {
 constexpr int kRerankK = 16, kRerankMaxK = 12;
 // Flat BLAS-path (nq >= kBlasThreshold) q·x form (hipann_flat_set_form): exact fp32 MFMA products
 // (flat_gemm_topk2), or the fp32-level 3-term split-bf16 products on the bf16 matrix cores
-// (flat_gemm_topk_bf, the default); kFlatSplit2 is the 2-term split (≈2^-16 relative, A/B only).
-enum FlatForm : int { kFlatFp32 = 0, kFlatSplit3 = 1, kFlatSplit2 = 2 };
+// (flat_gemm_topk_bf); kFlatSplit2 is the 2-term split (≈2^-16 relative, A/B only).  kFlatSplit2Exact
+// (default): the 2-term scan keeps kRerankK rows per database split and query as a filter, every
+// returned distance is recomputed exactly in the direct form with the IVF exact form's bound check
+// (ivf_rerank_topk), failures re-run on kFlatSplit3; kout <= kRerankMaxK (else kFlatSplit3).
+enum FlatForm : int { kFlatFp32 = 0, kFlatSplit3 = 1, kFlatSplit2 = 2, kFlatSplit2Exact = 3 };
 __host__ __device__ inline bool ivf_form_split(int f) { return f == kFormSplit3 || f == kFormSplit2; }
 __host__ __device__ inline int ivf_form_terms(int f) { return f == kFormSplit3 ? 3 : 2; }
 

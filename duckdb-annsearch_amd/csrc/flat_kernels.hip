@@ -356,14 +356,17 @@ __device__ __forceinline__ void g2_epilogue(const f32x16 (&acc)[4], float (&thr)
 }
 
 // per-(split, query) partial lists (each wave wrote only its own rows: no barrier needed)
+// qmajor = 0: part[split][q][k] (merge_parts); qmajor = 1: part[q][split][k] (the exact form's rerank reads a
+// query's lists contiguously)
 __device__ __forceinline__ void g2_write_parts(const float *__restrict__ Ld, const int *__restrict__ Li, int64_t q0,
                                                int64_t nq, int k, int split, int wave, int lane,
-                                               float *__restrict__ part_d, int *__restrict__ part_i) {
+                                               float *__restrict__ part_d, int *__restrict__ part_i, int nsplit = 0,
+                                               int qmajor = 0) {
     for (int r = 0; r < 32; ++r) {
         const int ql = 32 * wave + r;
         const int64_t q = q0 + ql;
         if (q < nq && lane < k) {
-            const int64_t off = ((int64_t)split * nq + q) * k;
+            const int64_t off = (qmajor ? q * nsplit + split : (int64_t)split * nq + q) * k;
             part_d[off + lane] = Ld[ql * k + lane];
             part_i[off + lane] = Li[ql * k + lane];
         }
@@ -489,8 +492,10 @@ flat_gemm_topk2(const float *__restrict__ Q, const float *__restrict__ qnorm, in
 //     terms), re-read per database tile like flat_gemm_topk2's LDS-staged queries;
 //   * database rows: the 128×32 fp32 chunk is loaded exactly as in flat_gemm_topk2 (coalesced float4
 //     per lane, register staging one chunk ahead) and split while it is stored to LDS as
-//     [term][16-B group c][row ^ 4c][8 bf16]: the XOR keeps the b64 stores (4 groups of one row per
-//     lane octet) and the b128 fragment reads (32 consecutive rows per group) conflict-free.
+//     [term][16-B group c][row ^ 2c][8 bf16]: the XOR keeps the b64 stores (16-lane groups = 2 rows × 4
+//     groups × 2 halves, banks (a/4) mod 32) and the b128 fragment reads (16-lane groups of 16 distinct
+//     rows mod 16, banks (a/4) mod 64) conflict-free (MI355X_MICROARCH.md LDS table; row ^ 4c left the
+//     stores 2-way conflicted: SQ_LDS_BANK_CONFLICT = 24 % of LDS cycles).
 // MFMA s ∈ {0, 1} of a 32-dim chunk: lane half h holds dims 16s + 8h .. +7 of its A row and B column
 // (group c = 2s + h).  Tile, grid, thresholds and the epilogue are flat_gemm_topk2's; LDS = 2 stages ×
 // NP × 8 KiB + 128·k·8 B of lists → 2 blocks per CU for k ≤ 32 at NP = 3.
@@ -506,24 +511,27 @@ __device__ __forceinline__ unsigned fb_pack(float a, float b) {
 __device__ __forceinline__ float fb_lo(unsigned p) { return __uint_as_float(p << 16); }
 __device__ __forceinline__ float fb_hi(unsigned p) { return __uint_as_float(p & 0xffff0000u); }
 
-// 4 fp32 → NP terms of 4 bf16 (two dwords each)
+// 4 fp32 → NP terms of 4 bf16 (two dwords each).  Scalar subtractions: v_pk_add_f32 beside MFMAs
+// costs far more than its issue slot (MI355X_MICROARCH.md, price of one filler beside MFMAs).
 template <int NP>
 __device__ __forceinline__ void fb_split4(const float4 &v, uint2 (&o)[NP]) {
-    fb_f32x2 x0 = {v.x, v.y}, x1 = {v.z, v.w};
+    float a = v.x, b = v.y, c = v.z, e = v.w;
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
-        const unsigned p0 = fb_pack(x0[0], x0[1]), p1 = fb_pack(x1[0], x1[1]);
+        const unsigned p0 = fb_pack(a, b), p1 = fb_pack(c, e);
         o[j] = make_uint2(p0, p1);
         if (j + 1 < NP) {
-            x0 -= (fb_f32x2){fb_lo(p0), fb_hi(p0)};
-            x1 -= (fb_f32x2){fb_lo(p1), fb_hi(p1)};
+            a -= fb_lo(p0);
+            b -= fb_hi(p0);
+            c -= fb_lo(p1);
+            e -= fb_hi(p1);
         }
     }
 }
 
 // LDS B stage: NP terms × 4 groups × 128 rows × 16 B
 constexpr int FB_STAGE16 = 4 * GBN;  // 16-B units per term
-__device__ __forceinline__ int fb_slot(int c, int row) { return c * GBN + (row ^ (c << 2)); }
+__device__ __forceinline__ int fb_slot(int c, int row) { return c * GBN + (row ^ (c << 1)); }
 
 template <int NP>
 __device__ __forceinline__ void fb_stage_store(uint2 *__restrict__ lds, const float4 (&r)[4]) {
@@ -562,7 +570,8 @@ template <bool VEC4, bool L2M, int NP>
 __global__ void __launch_bounds__(256, 2)
 flat_gemm_topk_bf(const uint4 *__restrict__ qsplit, int dpad, const float *__restrict__ qnorm, int64_t nq,
                   const float *__restrict__ X, const float *__restrict__ xnorm, int64_t N, int d, int k, int nqt,
-                  int nsplit, int64_t tiles_per_split, float *__restrict__ part_d, int *__restrict__ part_i) {
+                  int nsplit, int64_t tiles_per_split, float *__restrict__ part_d, int *__restrict__ part_i,
+                  int qmajor) {
     extern __shared__ __attribute__((aligned(16))) uint4 smem_bf[];
     uint4 *Bs0 = smem_bf;
     uint4 *Bs1 = smem_bf + NP * FB_STAGE16;
@@ -662,7 +671,7 @@ flat_gemm_topk_bf(const uint4 *__restrict__ qsplit, int dpad, const float *__res
         if (t + 1 < t1) gemm_stage_load<VEC4>(X, (t + 1) * GBN, N, d, 0, sb);
         g2_epilogue<L2M>(acc, thr, qnv, xnv, x0, N, Ld, Li, k, wave, lane);
     }
-    g2_write_parts(Ld, Li, q0, nq, k, split, wave, lane, part_d, part_i);
+    g2_write_parts(Ld, Li, q0, nq, k, split, wave, lane, part_d, part_i, nsplit, qmajor);
 }
 
 // The batch's queries split once into NP bf16 terms: qsplit [query][term][dpad] (dims in order, zero
@@ -950,7 +959,7 @@ size_t flat_bf_qsplit_bytes(int64_t nq, int d, int np) { return (size_t)nq * np 
 template <int NP>
 static void launch_flat_gemm_topk_bf_t(const float *Q, const float *qn, int64_t nq, void *qsplit, const float *X,
                                        const float *xn, int64_t N, int d, int metric, int k, int nsplit,
-                                       int64_t tiles_per_split, float *pd, int *pi, hipStream_t st) {
+                                       int64_t tiles_per_split, float *pd, int *pi, int qmajor, hipStream_t st) {
     const int dpad = flat_bf_dpad(d);
     const int64_t ng = nq * (dpad / 4);
     hipLaunchKernelGGL(flat_split_queries<NP>, dim3((unsigned)ceil_div(ng, 256)), dim3(256), 0, st, Q, nq, d, dpad,
@@ -963,20 +972,20 @@ static void launch_flat_gemm_topk_bf_t(const float *Q, const float *qn, int64_t 
     dim3 grid((unsigned)(nqt * nsplit)), block(256);
     const uint4 *qs = reinterpret_cast<const uint4 *>(qsplit);
     if (metric == kL2) {
-        if (vec4) hipLaunchKernelGGL((flat_gemm_topk_bf<true, true, NP>), grid, block, smem, st, qs, dpad, qn, nq, X, xn, N, d, k, nqt, nsplit, tiles_per_split, pd, pi);
-        else hipLaunchKernelGGL((flat_gemm_topk_bf<false, true, NP>), grid, block, smem, st, qs, dpad, qn, nq, X, xn, N, d, k, nqt, nsplit, tiles_per_split, pd, pi);
+        if (vec4) hipLaunchKernelGGL((flat_gemm_topk_bf<true, true, NP>), grid, block, smem, st, qs, dpad, qn, nq, X, xn, N, d, k, nqt, nsplit, tiles_per_split, pd, pi, qmajor);
+        else hipLaunchKernelGGL((flat_gemm_topk_bf<false, true, NP>), grid, block, smem, st, qs, dpad, qn, nq, X, xn, N, d, k, nqt, nsplit, tiles_per_split, pd, pi, qmajor);
     } else {
-        if (vec4) hipLaunchKernelGGL((flat_gemm_topk_bf<true, false, NP>), grid, block, smem, st, qs, dpad, qn, nq, X, xn, N, d, k, nqt, nsplit, tiles_per_split, pd, pi);
-        else hipLaunchKernelGGL((flat_gemm_topk_bf<false, false, NP>), grid, block, smem, st, qs, dpad, qn, nq, X, xn, N, d, k, nqt, nsplit, tiles_per_split, pd, pi);
+        if (vec4) hipLaunchKernelGGL((flat_gemm_topk_bf<true, false, NP>), grid, block, smem, st, qs, dpad, qn, nq, X, xn, N, d, k, nqt, nsplit, tiles_per_split, pd, pi, qmajor);
+        else hipLaunchKernelGGL((flat_gemm_topk_bf<false, false, NP>), grid, block, smem, st, qs, dpad, qn, nq, X, xn, N, d, k, nqt, nsplit, tiles_per_split, pd, pi, qmajor);
     }
     HIPANN_CHECK(hipGetLastError());
 }
 
 void launch_flat_gemm_topk_bf(int np, const float *Q, const float *qn, int64_t nq, void *qsplit, const float *X,
                               const float *xn, int64_t N, int d, int metric, int k, int nsplit, int64_t tiles_per_split,
-                              float *pd, int *pi, hipStream_t st) {
-    if (np == 2) launch_flat_gemm_topk_bf_t<2>(Q, qn, nq, qsplit, X, xn, N, d, metric, k, nsplit, tiles_per_split, pd, pi, st);
-    else launch_flat_gemm_topk_bf_t<3>(Q, qn, nq, qsplit, X, xn, N, d, metric, k, nsplit, tiles_per_split, pd, pi, st);
+                              float *pd, int *pi, int qmajor, hipStream_t st) {
+    if (np == 2) launch_flat_gemm_topk_bf_t<2>(Q, qn, nq, qsplit, X, xn, N, d, metric, k, nsplit, tiles_per_split, pd, pi, qmajor, st);
+    else launch_flat_gemm_topk_bf_t<3>(Q, qn, nq, qsplit, X, xn, N, d, metric, k, nsplit, tiles_per_split, pd, pi, qmajor, st);
 }
 
 size_t scan_smem_bytes(int nq, int d);

@@ -118,6 +118,7 @@ void shard_append(FlatShard &sh, int d, int metric, const float *x_host, const f
     if (metric == kL2) launch_row_norms(dst, n, d, sh.xn.get<float>() + sh.n, sh.stream);
     HIPANN_CHECK(hipStreamSynchronize(sh.stream));
     sh.n = need;
+    sh.xmax2 = -1.f;  // new rows: the exact form's bound is recomputed
 }
 
 }  // namespace
@@ -175,8 +176,29 @@ static void flat_shard_search_bigk(FlatIndex &ix, FlatShard &sh, int64_t nq, con
 
 // Search one shard: queries already on the shard's device.  Writes D (nq×kout fp32: raw distances,
 // ±inf pads) and I (nq×kout int64 labels, −1 pads) on the same device, asynchronously on `st`.
+// max‖x‖² of the shard (once per row set): the exact form's error bound
+static float flat_xmax2(FlatShard &sh, int d, hipStream_t st) {
+    if (sh.xmax2 >= 0.f) return sh.xmax2;
+    const float *xn = sh.xn.get<float>();
+    if (!xn) {
+        sh.tmpnorm.ensure(sizeof(float) * (size_t)std::max<int64_t>(sh.n, 1), sh.device);
+        launch_row_norms(sh.xb, sh.n, d, sh.tmpnorm.get<float>(), st);
+        xn = sh.tmpnorm.get<float>();
+    }
+    sh.nflag.ensure(sizeof(int), sh.device);
+    launch_ivf_max_norm(xn, sh.n, sh.nflag.get<unsigned>(), st);
+    unsigned bits = 0;
+    HIPANN_CHECK(hipMemcpyAsync(&bits, sh.nflag.p, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    HIPANN_CHECK(hipStreamSynchronize(st));
+    sh.tmpnorm.release();
+    float v;
+    std::memcpy(&v, &bits, sizeof(v));
+    sh.xmax2 = v;
+    return v;
+}
+
 void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq, int k, int kout, float *D,
-                       int64_t *I, hipStream_t st) {
+                       int64_t *I, hipStream_t st, int form_override) {
     DeviceGuard g(sh.device);
     const int d = ix.d, metric = ix.metric;
     const float out_sign = metric == kIP ? -1.f : 1.f;
@@ -236,23 +258,56 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
     const int64_t tps = ceil_div(ntiles, nsplit);
     nsplit = ceil_div(ntiles, tps);
     HIPANN_REQUIRE(nqt * nsplit < (int64_t)0x7fffffff, "grid too large");
+    int form = form_override >= 0 ? form_override : ix.form;
+    const bool exact = form == kFlatSplit2Exact && kout <= kRerankMaxK;
+    if (form == kFlatSplit2Exact && !exact) form = kFlatSplit3;
+    const int k_user = k;
+    if (exact) k = kRerankK;  // the scan keeps 16 per (split, query); the rerank returns kout
     sh.part_d.ensure((size_t)nsplit * nq * k * sizeof(float), sh.device);
     sh.part_i.ensure((size_t)nsplit * nq * k * sizeof(int), sh.device);
     {
         ScopedTiming t(ix.timer_main, st);
-        if (ix.form == kFlatFp32) {
+        if (form == kFlatFp32) {
             launch_flat_gemm_topk(xq, qn, nq, sh.xb, sh.xn.get<float>(), sh.n, d, metric, k, (int)nsplit, tps,
                                   sh.part_d.get<float>(), sh.part_i.get<int>(), st);
         } else {
-            const int np = ix.form == kFlatSplit2 ? 2 : 3;
+            const int np = form == kFlatSplit3 ? 3 : 2;
             sh.qsplit.ensure(flat_bf_qsplit_bytes(nq, d, np), sh.device);
             launch_flat_gemm_topk_bf(np, xq, qn, nq, sh.qsplit.get<void>(), sh.xb, sh.xn.get<float>(), sh.n, d, metric,
-                                     k, (int)nsplit, tps, sh.part_d.get<float>(), sh.part_i.get<int>(), st);
+                                     k, (int)nsplit, tps, sh.part_d.get<float>(), sh.part_i.get<int>(), exact ? 1 : 0,
+                                     st);
         }
     }
-    ScopedTiming t(ix.timer_merge, st);
-    launch_merge_parts<int>(sh.part_d.get<float>(), sh.part_i.get<int>(), (int)nsplit, nq, k, kout, sh.label_offset,
-                            1.f, out_sign, D, I, st);
+    if (!exact) {
+        ScopedTiming t(ix.timer_merge, st);
+        launch_merge_parts<int>(sh.part_d.get<float>(), sh.part_i.get<int>(), (int)nsplit, nq, k, kout, sh.label_offset,
+                                1.f, out_sign, D, I, st);
+        return;
+    }
+    // exact form: merge each query's nsplit lists to the 16 best scan keys, recompute those rows in the
+    // direct form, bound-check (ivf_rerank_topk, slot lists query-major); flagged queries re-run on split3
+    const float xmax2 = flat_xmax2(sh, d, st);
+    sh.nflag.ensure(sizeof(int), sh.device);
+    sh.flagged.ensure(sizeof(int) * (size_t)nq, sh.device);
+    HIPANN_CHECK(hipMemsetAsync(sh.nflag.p, 0, sizeof(int), st));
+    {
+        ScopedTiming t(ix.timer_merge, st);
+        launch_ivf_rerank(sh.part_d.get<float>(), sh.part_i.get<int>(), nullptr, (int)nsplit, nq, k, kout, metric, xq,
+                          sh.xb, d, nullptr, sh.n, sh.label_offset, xmax2, D, I, sh.nflag.get<int>(),
+                          sh.flagged.get<int>(), st);
+    }
+    int nf = 0;
+    HIPANN_CHECK(hipMemcpyAsync(&nf, sh.nflag.p, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPANN_CHECK(hipStreamSynchronize(st));
+    if (nf <= 0) return;
+    ix.rerank_fallbacks += nf;
+    sh.fq.ensure(sizeof(float) * (size_t)nf * d, sh.device);
+    sh.fD.ensure(sizeof(float) * (size_t)nf * kout, sh.device);
+    sh.fI.ensure(sizeof(int64_t) * (size_t)nf * kout, sh.device);
+    launch_ivf_gather_queries(xq, sh.flagged.get<int>(), nf, d, sh.fq.get<float>(), st);
+    flat_shard_search(ix, sh, nf, sh.fq.get<float>(), k_user, kout, sh.fD.get<float>(), sh.fI.get<int64_t>(), st,
+                      kFlatSplit3);
+    launch_ivf_scatter_results(sh.fD.get<float>(), sh.fI.get<int64_t>(), sh.flagged.get<int>(), nf, kout, D, I, st);
 }
 
 }  // namespace hipann
@@ -506,13 +561,20 @@ int hipann_metric(void *h) { return h ? static_cast<IndexBase *>(h)->metric : -1
 int64_t hipann_memory_bytes(void *h) { return h ? static_cast<IndexBase *>(h)->memory_bytes() : -1; }
 
 int hipann_flat_set_form(void *h, int form) {
-    if (!h || form < kFlatFp32 || form > kFlatSplit2) return -1;
+    if (!h || form < kFlatFp32 || form > kFlatSplit2Exact) return -1;
     auto *ix = static_cast<IndexBase *>(h);
     if (ix->kind != Kind::Flat) return -1;
     auto *fx = static_cast<FlatIndex *>(ix);
     std::lock_guard<std::mutex> lk(fx->mu);
     fx->form = form;
     return 0;
+}
+
+int64_t hipann_flat_rerank_fallbacks(void *h) {
+    if (!h) return -1;
+    auto *ix = static_cast<IndexBase *>(h);
+    if (ix->kind != Kind::Flat) return -1;
+    return static_cast<FlatIndex *>(ix)->rerank_fallbacks;
 }
 
 int hipann_flat_get_form(void *h) {

@@ -254,7 +254,7 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     {
         ScopedTiming t(ix.timer_merge, st);
         launch_ivf_rerank(sh.part_d.get<float>(), sh.part_i.get<int>(), sh.slot_off.get<int>(), np, nq, k, kout, metric,
-                          xq, sh.codes, d, sh.ids, sh.n, xmax2, D, I, sh.nflag.get<int>(), sh.flagged.get<int>(), st);
+                          xq, sh.codes, d, sh.ids, sh.n, 0, xmax2, D, I, sh.nflag.get<int>(), sh.flagged.get<int>(), st);
     }
     int nf = 0;
     HIPANN_CHECK(hipMemcpyAsync(&nf, sh.nflag.p, sizeof(int), hipMemcpyDeviceToHost, st));

@@ -988,15 +988,19 @@ template <bool IP>
 __global__ void __launch_bounds__(256)
 ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const int *__restrict__ slot_off,
                 int nprobe, int64_t nq, int k, int kout, const float *__restrict__ Q,
-                const float *__restrict__ codes, int d, const int64_t *__restrict__ ids, int64_t nrows, float xmax2,
-                float *__restrict__ D, int64_t *__restrict__ I, int *__restrict__ nflag, int *__restrict__ flagged) {
+                const float *__restrict__ codes, int d, const int64_t *__restrict__ ids, int64_t nrows,
+                int64_t label_offset, float xmax2, float *__restrict__ D, int64_t *__restrict__ I,
+                int *__restrict__ nflag, int *__restrict__ flagged) {
     const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (q >= nq) return;
     const int lane = threadIdx.x & 63;
     // 1. the kRerankK best (scan key, row) of the query's partial lists
     WaveList<1, int> L;
     L.init();
-    const int64_t s0 = slot_off[q * nprobe], s1 = slot_off[(q + 1) * nprobe];
+    // slot_off == nullptr: the query's lists are the nprobe consecutive slots [q·nprobe, (q+1)·nprobe)
+    // (the Flat exact form: one list per database split, query-major)
+    const int64_t s0 = slot_off ? slot_off[q * nprobe] : q * nprobe;
+    const int64_t s1 = slot_off ? slot_off[(q + 1) * nprobe] : (q + 1) * nprobe;
     const int64_t total = (s1 - s0) * k;
     for (int64_t c0 = 0; c0 < total; c0 += 64) {
         const int64_t c = c0 + lane;
@@ -1055,7 +1059,7 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
     // 3. (distance, label) order, first kout
     WaveList<1, long long> R;
     R.init();
-    const long long lab = real ? (long long)ids[myrow] : IdTraits<long long>::pad();
+    const long long lab = real ? (long long)(ids ? ids[myrow] : label_offset + myrow) : IdTraits<long long>::pad();
     R.offer(real ? mine : __builtin_inff(), lab, kout - 1);
     // 4. exactness check
     const float dk = readlane_f(R.d[0], kout - 1);
@@ -1098,16 +1102,17 @@ __global__ void __launch_bounds__(256) ivf_scatter_results(const float *__restri
 
 void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int nprobe, int64_t nq, int k, int kout,
                        int metric, const float *Q, const float *codes, int d, const int64_t *ids, int64_t nrows,
-                       float xmax2, float *D, int64_t *I, int *nflag, int *flagged, hipStream_t st) {
+                       int64_t label_offset, float xmax2, float *D, int64_t *I, int *nflag, int *flagged,
+                       hipStream_t st) {
     if (nq <= 0) return;
     HIPANN_REQUIRE(k == kRerankK && kout >= 1 && kout <= kRerankMaxK, "ivf rerank: k / kout out of range");
     dim3 grid((unsigned)ceil_div(nq, 4)), block(256);
     if (metric == kIP)
         hipLaunchKernelGGL(ivf_rerank_topk<true>, grid, block, 0, st, pd, pi, slot_off, nprobe, nq, k, kout, Q, codes, d,
-                           ids, nrows, xmax2, D, I, nflag, flagged);
+                           ids, nrows, label_offset, xmax2, D, I, nflag, flagged);
     else
         hipLaunchKernelGGL(ivf_rerank_topk<false>, grid, block, 0, st, pd, pi, slot_off, nprobe, nq, k, kout, Q, codes,
-                           d, ids, nrows, xmax2, D, I, nflag, flagged);
+                           d, ids, nrows, label_offset, xmax2, D, I, nflag, flagged);
     HIPANN_CHECK(hipGetLastError());
 }
 

@@ -125,6 +125,10 @@ struct FlatShard {
     DevBuf q, qn, part_d, part_i, out_d, out_i;
     DevBuf keys, run_d, run_i, run2_d, run2_i;  // k > 64 path
     DevBuf qsplit;                              // split-bf16 form: the batch's queries as bf16 terms
+    // kFlatSplit2Exact: max row ‖x‖² (the rerank's error bound; −1 until computed / after an add), the
+    // flagged queries of the last batch and the re-run's buffers
+    float xmax2 = -1.f;
+    DevBuf nflag, flagged, fq, fD, fI, tmpnorm;
 };
 
 struct IndexBase {
@@ -141,7 +145,8 @@ struct IndexBase {
 
 struct FlatIndex : IndexBase {
     std::vector<std::unique_ptr<FlatShard>> shards;
-    int form = kFlatSplit3;  // BLAS-path q·x form (FlatForm)
+    int form = kFlatSplit2Exact;  // BLAS-path q·x form (FlatForm)
+    int64_t rerank_fallbacks = 0;  // queries re-run on the 3-term path by the exact form's bound check
     HostBuf h_q, h_d, h_i;
     DevBuf gather_d, gather_i, merged_d, merged_i;  // multi-device merge on shards[0]'s device
     FlatIndex() : IndexBase(Kind::Flat) {}
@@ -219,7 +224,7 @@ void launch_flat_gemm_topk(const float *Q, const float *qn, int64_t nq, const fl
 size_t flat_bf_qsplit_bytes(int64_t nq, int d, int np);
 void launch_flat_gemm_topk_bf(int np, const float *Q, const float *qn, int64_t nq, void *qsplit, const float *X,
                               const float *xn, int64_t N, int d, int metric, int k, int nsplit, int64_t tiles_per_split,
-                              float *pd, int *pi, hipStream_t st);
+                              float *pd, int *pi, int qmajor, hipStream_t st);
 size_t scan_smem_bytes(int nq, int d);
 void launch_flat_gemm_keys(const float *Q, const float *qn, int64_t nq, const float *X, const float *xn, int64_t N,
                            int d, int metric, float *keys, int64_t ldk, hipStream_t st);
@@ -240,7 +245,8 @@ bool ivf_mfma_bf_supported(const float *Q, int d, const float *codes, int k, int
 int64_t ivf_mfma_bf_qsplit_bytes(int64_t nq, int d, int np);
 void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int nprobe, int64_t nq, int k, int kout,
                        int metric, const float *Q, const float *codes, int d, const int64_t *ids, int64_t nrows,
-                       float xmax2, float *D, int64_t *I, int *nflag, int *flagged, hipStream_t st);
+                       int64_t label_offset, float xmax2, float *D, int64_t *I, int *nflag, int *flagged,
+                       hipStream_t st);
 void launch_ivf_max_norm(const float *xn, int64_t n, unsigned *out, hipStream_t st);
 void launch_ivf_gather_queries(const float *Q, const int *idx, int nf, int d, float *out, hipStream_t st);
 void launch_ivf_scatter_results(const float *Df, const int64_t *If, const int *idx, int nf, int kout, float *D,

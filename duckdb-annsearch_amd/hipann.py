@@ -90,6 +90,7 @@ def lib() -> C.CDLL:
             "hipann_flat_search_device": ([vp, i64, vp, i64, vp, vp, vp, cp, i32], i32),
             "hipann_flat_set_form": ([vp, i32], i32),
             "hipann_flat_get_form": ([vp], i32),
+            "hipann_flat_rerank_fallbacks": ([vp], i64),
             "hipann_merge_topk_device": ([i32, i32, i64, i64, vp, vp, vp, vp, vp, cp, i32], i32),
             "hipann_ivf_create": ([i32, i32, i32, i32, f, i64p, i64p, f, C.POINTER(C.c_int), i32, cp, i32], vp),
             "hipann_ivf_create_device": ([i32, i32, i32, i32, vp, i64p, vp, vp, i32, i32, cp, i32], vp),
@@ -222,9 +223,10 @@ class _Handle:
 class _FlatForm:
     """q·x form of the batched (nq >= 20) Flat path — hipann_flat_set_form (hip_ann.h)."""
 
-    FORM_FP32 = 0    # exact fp32 products on the fp32 matrix cores
-    FORM_SPLIT3 = 1  # default: 3-term split-bf16 products (fp32-level) on the bf16 matrix cores
-    FORM_SPLIT2 = 2  # 2-term split (~2^-16 relative per product; measurement only)
+    FORM_FP32 = 0          # exact fp32 products on the fp32 matrix cores
+    FORM_SPLIT3 = 1        # 3-term split-bf16 products (fp32-level) on the bf16 matrix cores
+    FORM_SPLIT2 = 2        # 2-term split (~2^-16 relative per product; measurement only)
+    FORM_SPLIT2_EXACT = 3  # default: the 2-term scan as a filter + exact direct-form rerank with a bound check
 
     @property
     def form(self) -> int:
@@ -233,7 +235,12 @@ class _FlatForm:
     @form.setter
     def form(self, v: int) -> None:
         if lib().hipann_flat_set_form(self._h, int(v)) != 0:
-            raise HipAnnError("form must be 0 (fp32), 1 (split bf16, 3 terms) or 2 (split bf16, 2 terms)")
+            raise HipAnnError("form must be 0 (fp32), 1 (split bf16, 3 terms), 2 (split bf16, 2 terms) or "
+                              "3 (split bf16 + exact rerank)")
+
+    def rerank_fallbacks(self) -> int:
+        """Queries the exact form's bound check re-ran on the 3-term path since creation."""
+        return int(lib().hipann_flat_rerank_fallbacks(self._h))
 
 
 class HipIndexFlat(_FlatForm, _Handle):

@@ -74,15 +74,22 @@ int hipann_flat_reconstruct(void *index, int64_t key, float *out, char *err_buf,
 
 /* q·x form of the batched (nq >= 20, FAISS's BLAS threshold) distance path, ‖q‖² + ‖x‖² − 2·q·x.
  * HIPANN_FLAT_FORM_FP32: exact fp32 products on the fp32 matrix cores (v_mfma_f32_32x32x2_f32).
- * HIPANN_FLAT_FORM_SPLIT3 (default): both operands split into three round-to-nearest bf16 terms, the
+ * HIPANN_FLAT_FORM_SPLIT3: both operands split into three round-to-nearest bf16 terms, the
  * six products above 2^-26 relative on the bf16 matrix cores, fp32 accumulation — fp32-level products
  * at several times the fp32 rate.  HIPANN_FLAT_FORM_SPLIT2: two terms, three products (≈2^-16
- * relative per product; measurement only).  Returns 0, or -1 for a bad handle / form. */
+ * relative per product; measurement only).  HIPANN_FLAT_FORM_SPLIT2_EXACT (default): the SPLIT2 scan
+ * keeps the 16 best rows per database split and query only as a filter; every returned distance is
+ * recomputed in FAISS's direct fp32 form (Σ(q−x)² / q·x) and a per-query bound (|scan key − exact| ≤
+ * 2^-12·(‖q‖² + max‖x‖²)) proves no pruned row reaches the top-k — queries that fail it re-run on
+ * SPLIT3 (k ≤ 12; larger k use SPLIT3).  Returns 0, or -1 for a bad handle / form. */
 #define HIPANN_FLAT_FORM_FP32 0
 #define HIPANN_FLAT_FORM_SPLIT3 1
 #define HIPANN_FLAT_FORM_SPLIT2 2
+#define HIPANN_FLAT_FORM_SPLIT2_EXACT 3
 int hipann_flat_set_form(void *index, int form);
 int hipann_flat_get_form(void *index);
+/* Queries re-run on HIPANN_FLAT_FORM_SPLIT3 by the exact form's bound check since the index was created. */
+int64_t hipann_flat_rerank_fallbacks(void *index);
 
 /* ---------------------------------------------------------------------------------------------
  * Device-resident variants (inputs and outputs already in HBM).  Used by the multi-GPU sharded

@@ -242,39 +242,61 @@ def test_flat_large_properties(gpu, oracle):
     check_topk_parity(xb, xq[:64], D[:64], I[:64], Do, Io)
 
 
-@pytest.mark.parametrize("form", [0, 1, 2])
+@pytest.mark.parametrize("form", [0, 1, 2, 3])
 @pytest.mark.parametrize("metric", [0, 1])
 @pytest.mark.parametrize("nq,d", [(20, 64), (129, 33), (300, 768), (64, 5)])
 def test_flat_forms_blas_path(gpu, oracle, form, metric, nq, d):
-    """hipann_flat_set_form: the fp32 (0) and 3-term split-bf16 (1, default) forms of the batched path
-    both meet the fp32 parity rule; the 2-term split (2, measurement only) keeps ≈2^-16 relative
-    products, so only its recall against the oracle is checked."""
-    xb, xq = faiss_metal_case(3000, nq, d)
+    """hipann_flat_set_form: the fp32 (0), 3-term split-bf16 (1) and exact (3, default: 2-term filter +
+    direct-form rerank) forms of the batched path meet the fp32 parity rule; the 2-term split (2,
+    measurement only) keeps ≈2^-16 relative products, so only its recall is checked."""
+    xb, xq = faiss_metal_case(20000, nq, d)  # > 16384 rows: the fused path (smaller tables select from keys)
     ix = gpu.HipIndexFlat(d, metric, xb)
-    assert ix.form == ix.FORM_SPLIT3
+    assert ix.form == ix.FORM_SPLIT2_EXACT
     ix.form = form
     assert ix.form == form
     D, I = ix.search(xq, 10)
     Do, Io = oracle.flat_search(xb, xq, 10, metric)
-    if form in (0, 1):
+    if form != 2:
         check_topk_parity(xb, xq, D, I, Do, Io, metric)
     else:
         hit = np.mean([len(set(a) & set(b)) / 10 for a, b in zip(I.tolist(), Io.tolist())])
         assert hit >= 0.97, hit
     with pytest.raises(gpu.HipAnnError):
-        ix.form = 3
+        ix.form = 4
 
 
-def test_flat_split3_matches_fp32_form_at_scale(gpu):
-    """Large-size property: the split-bf16 form returns the fp32 form's lists except inside near-tie
-    windows (distances within the fp32 rounding scale), on 200k × 128 with 512 queries."""
+def test_flat_exact_form_ties_fall_back(gpu, oracle):
+    """Exact form with 40 copies of every row: the 16 kept scan candidates are all ties, the bound check
+    cannot exclude a pruned copy, so every query re-runs on the 3-term path; results keep parity."""
+    base, xq = faiss_metal_case(500, 64, 48)
+    xb = np.repeat(base, 40, axis=0)  # 20000 rows: the fused path
+    ix = gpu.HipIndexFlat(48, 0, xb)
+    D, I = ix.search(xq, 10)
+    Do, Io = oracle.flat_search(xb, xq, 10, 0)
+    check_topk_parity(xb, xq, D, I, Do, Io, 0)
+    assert ix.rerank_fallbacks() == 64
+
+
+def test_flat_exact_form_large_k_uses_split3(gpu, oracle):
+    xb, xq = faiss_metal_case(20000, 40, 32)
+    ix = gpu.HipIndexFlat(32, 1, xb)
+    D, I = ix.search(xq, 50)   # k > 12: the 3-term path, no rerank
+    Do, Io = oracle.flat_search(xb, xq, 50, 1)
+    check_topk_parity(xb, xq, D, I, Do, Io, 1)
+    assert ix.rerank_fallbacks() == 0
+
+
+def test_flat_exact_form_matches_fp32_form_at_scale(gpu):
+    """Large-size property: the exact form (2-term split filter + direct-form rerank) returns the fp32
+    form's lists except inside near-tie windows (distances within the fp32 rounding scale), on
+    200k × 128 with 512 queries."""
     rng = np.random.default_rng(7)
     xb = rng.standard_normal((200_000, 128), dtype=np.float32)
     xq = rng.standard_normal((512, 128), dtype=np.float32)
     ix = gpu.HipIndexFlat(128, 0, xb)
     ix.form = ix.FORM_FP32
     D0, I0 = ix.search(xq, 10)
-    ix.form = ix.FORM_SPLIT3
+    ix.form = ix.FORM_SPLIT2_EXACT
     D1, I1 = ix.search(xq, 10)
     scale = np.sum(xq.astype(np.float64) ** 2, 1)[:, None] + np.max(np.sum(xb.astype(np.float64) ** 2, 1))
     assert (np.abs(D1 - D0) <= 1e-5 * scale).all()
