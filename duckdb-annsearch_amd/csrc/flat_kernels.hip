@@ -533,12 +533,39 @@ __device__ __forceinline__ void fb_split4(const float4 &v, uint2 (&o)[NP]) {
 constexpr int FB_STAGE16 = 4 * GBN;  // 16-B units per term
 __device__ __forceinline__ int fb_slot(int c, int row) { return c * GBN + (row ^ (c << 1)); }
 
-template <int NP>
-__device__ __forceinline__ void fb_stage_store(uint2 *__restrict__ lds, const float4 (&r)[4]) {
+// Row-chunk load for a T-thread block: the 128×32 fp32 chunk as 1024 float4, 1024/T per thread.
+template <bool VEC4, int T>
+__device__ __forceinline__ void fb_stage_load(const float *__restrict__ base, int64_t row0, int64_t nrows, int d,
+                                              int k0, float4 (&r)[1024 / T]) {
     const int t = threadIdx.x;
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-        const int f = t + 256 * p;
+    for (int p = 0; p < 1024 / T; ++p) {
+        const int f = t + T * p;
+        const int row = f >> 3, c4 = f & 7;
+        const int64_t grow = row0 + row;
+        const int kk = k0 + 4 * c4;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (grow < nrows) {
+            const float *src = base + grow * (int64_t)d + kk;
+            if (VEC4) {
+                if (kk < d) v = *reinterpret_cast<const float4 *>(src);
+            } else {
+                if (kk + 0 < d) v.x = src[0];
+                if (kk + 1 < d) v.y = src[1];
+                if (kk + 2 < d) v.z = src[2];
+                if (kk + 3 < d) v.w = src[3];
+            }
+        }
+        r[p] = v;
+    }
+}
+
+template <int NP, int T>
+__device__ __forceinline__ void fb_stage_store(uint2 *__restrict__ lds, const float4 (&r)[1024 / T]) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int p = 0; p < 1024 / T; ++p) {
+        const int f = t + T * p;
         const int row = f >> 3, c4 = f & 7;
         uint2 o[NP];
         fb_split4<NP>(r[p], o);
@@ -564,25 +591,26 @@ struct FbProducts<2> {
     __device__ static constexpr int b(int i) { return i == 1 ? 1 : 0; }
 };
 
-size_t gemm_bf_smem_bytes(int np, int k) { return (size_t)2 * np * FB_STAGE16 * 16 + (size_t)GBM * k * 8; }
+size_t gemm_bf_smem_bytes(int np, int k, int w) { return (size_t)2 * np * FB_STAGE16 * 16 + (size_t)32 * w * k * 8; }
 
-template <bool VEC4, bool L2M, int NP>
-__global__ void __launch_bounds__(256, 2)
+template <bool VEC4, bool L2M, int NP, int W>
+__global__ void __launch_bounds__(64 * W, 8 / W)
 flat_gemm_topk_bf(const uint4 *__restrict__ qsplit, int dpad, const float *__restrict__ qnorm, int64_t nq,
                   const float *__restrict__ X, const float *__restrict__ xnorm, int64_t N, int d, int k, int nqt,
                   int nsplit, int64_t tiles_per_split, float *__restrict__ part_d, int *__restrict__ part_i,
                   int qmajor) {
+    constexpr int TH = 64 * W, QM = 32 * W;  // threads; query rows per block (32 per wave)
     extern __shared__ __attribute__((aligned(16))) uint4 smem_bf[];
     uint4 *Bs0 = smem_bf;
     uint4 *Bs1 = smem_bf + NP * FB_STAGE16;
-    float *Ld = reinterpret_cast<float *>(smem_bf + 2 * NP * FB_STAGE16);  // [128][k] keys
-    int *Li = reinterpret_cast<int *>(Ld + GBM * k);                        // [128][k] ids
+    float *Ld = reinterpret_cast<float *>(smem_bf + 2 * NP * FB_STAGE16);  // [QM][k] keys
+    int *Li = reinterpret_cast<int *>(Ld + QM * k);                         // [QM][k] ids
 
     const int nblocks = nqt * nsplit;
     const int lb = xcd_remap(blockIdx.x, nblocks);
     const int qt = lb % nqt;
     const int split = lb / nqt;
-    const int64_t q0 = (int64_t)qt * GBM;
+    const int64_t q0 = (int64_t)qt * QM;
     const int64_t ntiles = ceil_div(N, GBN);
     const int64_t t0 = (int64_t)split * tiles_per_split;
     const int64_t t1 = t0 + tiles_per_split < ntiles ? t0 + tiles_per_split : ntiles;
@@ -591,7 +619,7 @@ flat_gemm_topk_bf(const uint4 *__restrict__ qsplit, int dpad, const float *__res
     const int wave = tid >> 6, lane = tid & 63;
     const int l31 = lane & 31, h = lane >> 5;
 
-    for (int e = tid; e < GBM * k; e += 256) {
+    for (int e = tid; e < QM * k; e += TH) {
         Ld[e] = __builtin_inff();
         Li[e] = 0x7fffffff;
     }
@@ -610,10 +638,10 @@ flat_gemm_topk_bf(const uint4 *__restrict__ qsplit, int dpad, const float *__res
     __syncthreads();
 
     const int nk = dpad / GBK;
-    float4 sb[4];
+    float4 sb[1024 / TH];
     uint4 af[NP][2], an[NP][2];
     if (t0 < t1) {
-        gemm_stage_load<VEC4>(X, t0 * GBN, N, d, 0, sb);
+        fb_stage_load<VEC4, TH>(X, t0 * GBN, N, d, 0, sb);
 #pragma unroll
         for (int j = 0; j < NP; ++j)
 #pragma unroll
@@ -622,7 +650,7 @@ flat_gemm_topk_bf(const uint4 *__restrict__ qsplit, int dpad, const float *__res
 
     for (int64_t t = t0; t < t1; ++t) {
         const int64_t x0 = t * GBN;
-        fb_stage_store<NP>(reinterpret_cast<uint2 *>(Bs0), sb);
+        fb_stage_store<NP, TH>(reinterpret_cast<uint2 *>(Bs0), sb);
         float xnv[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -639,7 +667,7 @@ flat_gemm_topk_bf(const uint4 *__restrict__ qsplit, int dpad, const float *__res
 
         for (int kc = 0; kc < nk; ++kc) {
             const uint4 *Bb = (kc & 1) ? Bs1 : Bs0;
-            if (kc + 1 < nk) gemm_stage_load<VEC4>(X, x0, N, d, (kc + 1) * GBK, sb);
+            if (kc + 1 < nk) fb_stage_load<VEC4, TH>(X, x0, N, d, (kc + 1) * GBK, sb);
             const int kn = kc + 1 < nk ? kc + 1 : 0;  // the next tile starts over at chunk 0
 #pragma unroll
             for (int j = 0; j < NP; ++j)
@@ -660,7 +688,7 @@ flat_gemm_topk_bf(const uint4 *__restrict__ qsplit, int dpad, const float *__res
                             __builtin_bit_cast(fb_bf16x8, bt[FbProducts<NP>::b(pr)]), acc[jb], 0, 0, 0);
                 }
             }
-            if (kc + 1 < nk) fb_stage_store<NP>(reinterpret_cast<uint2 *>((kc & 1) ? Bs0 : Bs1), sb);
+            if (kc + 1 < nk) fb_stage_store<NP, TH>(reinterpret_cast<uint2 *>((kc & 1) ? Bs0 : Bs1), sb);
             __syncthreads();
 #pragma unroll
             for (int j = 0; j < NP; ++j)
@@ -668,7 +696,7 @@ flat_gemm_topk_bf(const uint4 *__restrict__ qsplit, int dpad, const float *__res
                 for (int s = 0; s < 2; ++s) af[j][s] = an[j][s];
         }
 
-        if (t + 1 < t1) gemm_stage_load<VEC4>(X, (t + 1) * GBN, N, d, 0, sb);
+        if (t + 1 < t1) fb_stage_load<VEC4, TH>(X, (t + 1) * GBN, N, d, 0, sb);
         g2_epilogue<L2M>(acc, thr, qnv, xnv, x0, N, Ld, Li, k, wave, lane);
     }
     g2_write_parts(Ld, Li, q0, nq, k, split, wave, lane, part_d, part_i, nsplit, qmajor);
@@ -965,18 +993,27 @@ static void launch_flat_gemm_topk_bf_t(const float *Q, const float *qn, int64_t 
     hipLaunchKernelGGL(flat_split_queries<NP>, dim3((unsigned)ceil_div(ng, 256)), dim3(256), 0, st, Q, nq, d, dpad,
                        reinterpret_cast<uint2 *>(qsplit));
     HIPANN_CHECK(hipGetLastError());
-    const int nqt = (int)ceil_div(nq, GBM);
+    // Block shape: 4 waves (128 queries, two blocks per CU) or 8 waves (256 queries, one block per CU, one
+    // row staging shared by twice the MFMAs).  Measured at 10M × 768: 2 terms 60.3 ms (4) vs 65.6 ms (8),
+    // 3 terms 90.6 ms (4) vs 86.2 ms (8).  HIPANN_FLAT_BF_WAVES=4|8 overrides (A/B).
+    static const int Wenv = [] { const char *e = std::getenv("HIPANN_FLAT_BF_WAVES"); return e ? std::atoi(e) : 0; }();
+    const int W = Wenv == 4 || Wenv == 8 ? Wenv : (NP == 3 ? 8 : 4);
+    const int nqt = (int)ceil_div(nq, 32 * W);
     const bool vec4 = (d % 4 == 0) && ((uintptr_t)X % 16 == 0);
-    const size_t smem = gemm_bf_smem_bytes(NP, k);
+    const size_t smem = gemm_bf_smem_bytes(NP, k, W);
     HIPANN_REQUIRE(smem <= 160 * 1024, "k too large for the split-bf16 Flat kernel");
-    dim3 grid((unsigned)(nqt * nsplit)), block(256);
+    dim3 grid((unsigned)(nqt * nsplit)), block(64 * W);
     const uint4 *qs = reinterpret_cast<const uint4 *>(qsplit);
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, grid, block, smem, st, qs, dpad, qn, nq, X, xn, N, d, k, nqt, nsplit, tiles_per_split,
+                           pd, pi, qmajor);
+    };
     if (metric == kL2) {
-        if (vec4) hipLaunchKernelGGL((flat_gemm_topk_bf<true, true, NP>), grid, block, smem, st, qs, dpad, qn, nq, X, xn, N, d, k, nqt, nsplit, tiles_per_split, pd, pi, qmajor);
-        else hipLaunchKernelGGL((flat_gemm_topk_bf<false, true, NP>), grid, block, smem, st, qs, dpad, qn, nq, X, xn, N, d, k, nqt, nsplit, tiles_per_split, pd, pi, qmajor);
+        if (vec4) W == 8 ? go(flat_gemm_topk_bf<true, true, NP, 8>) : go(flat_gemm_topk_bf<true, true, NP, 4>);
+        else W == 8 ? go(flat_gemm_topk_bf<false, true, NP, 8>) : go(flat_gemm_topk_bf<false, true, NP, 4>);
     } else {
-        if (vec4) hipLaunchKernelGGL((flat_gemm_topk_bf<true, false, NP>), grid, block, smem, st, qs, dpad, qn, nq, X, xn, N, d, k, nqt, nsplit, tiles_per_split, pd, pi, qmajor);
-        else hipLaunchKernelGGL((flat_gemm_topk_bf<false, false, NP>), grid, block, smem, st, qs, dpad, qn, nq, X, xn, N, d, k, nqt, nsplit, tiles_per_split, pd, pi, qmajor);
+        if (vec4) W == 8 ? go(flat_gemm_topk_bf<true, false, NP, 8>) : go(flat_gemm_topk_bf<true, false, NP, 4>);
+        else W == 8 ? go(flat_gemm_topk_bf<false, false, NP, 8>) : go(flat_gemm_topk_bf<false, false, NP, 4>);
     }
     HIPANN_CHECK(hipGetLastError());
 }
