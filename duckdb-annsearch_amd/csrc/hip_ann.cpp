@@ -146,6 +146,27 @@ static void flat_shard_search_bigk(FlatIndex &ix, FlatShard &sh, int64_t nq, con
     sh.keys.ensure((size_t)nq * C * sizeof(float), sh.device);
     sh.part_d.ensure((size_t)(nseg + 1) * nq * k * sizeof(float), sh.device);
     sh.part_i.ensure((size_t)(nseg + 1) * nq * k * sizeof(int), sh.device);
+    if (sh.n <= C) {  // one chunk (an IVF coarse quantizer): the segment lists go straight to the output merge
+        {
+            ScopedTiming t(ix.timer_main, st);
+            if (nq < kBlasThreshold)
+                launch_flat_scan_keys(xq, (int)nq, sh.xb, sh.n, d, metric, sh.keys.get<float>(), C, st);
+            else
+                launch_flat_gemm_keys(xq, qn, nq, sh.xb, sh.xn.get<float>(), sh.n, d, metric, sh.keys.get<float>(), C,
+                                      st);
+        }
+        // short rows: 256-column segments, so a 1024-centroid row is selected by 4 waves, not 1
+        const int64_t sl = sh.n <= seg_len && k <= 64 ? 256 : seg_len;
+        const int ns = (int)ceil_div(sh.n, sl);
+        sh.part_d.ensure((size_t)ns * nq * k * sizeof(float), sh.device);
+        sh.part_i.ensure((size_t)ns * nq * k * sizeof(int), sh.device);
+        launch_rows_topk(sh.keys.get<float>(), C, sh.n, nq, sl, ns, k, 0, sh.part_d.get<float>(), sh.part_i.get<int>(),
+                         st);
+        ScopedTiming t(ix.timer_merge, st);
+        launch_merge_parts<int>(sh.part_d.get<float>(), sh.part_i.get<int>(), ns, nq, k, kout, sh.label_offset, 1.f,
+                                out_sign, D, I, st);
+        return;
+    }
     sh.run_d.ensure((size_t)nq * k * sizeof(float), sh.device);
     sh.run_i.ensure((size_t)nq * k * sizeof(int), sh.device);
     // running best starts empty: part 0 = pads

@@ -99,42 +99,54 @@ __global__ void ivf_fill(const int64_t *__restrict__ probes, int64_t npairs, con
 __global__ void __launch_bounds__(1024) ivf_slot_scan(const int64_t *__restrict__ probes, int64_t npairs,
                                                       const int *__restrict__ list_len, int nlist,
                                                       int *__restrict__ slot_off) {
-    // per round, thread t owns the contiguous pairs base + [32t, 32t + 32): all 32 probe loads, then
-    // all 32 list-length loads are independent (two memory latencies per round, not 64), then a
-    // local scan, one block scan of the 1024 sums and the writes
-    constexpr int PER = 32;
-    __shared__ int sv[1024];
-    __shared__ int carry;
-    if (threadIdx.x == 0) carry = 0;
-    __syncthreads();
-    for (int64_t base = 0; base < npairs; base += 1024 * PER) {
-        const int64_t i0 = base + (int64_t)threadIdx.x * PER;
-        int64_t l[PER];
+    // Per round, wave w owns the contiguous pairs base + [1024w, 1024w + 1024) as 16 chunks of 64: lane
+    // i of chunk j is pair 64j + i, so the 16 probe loads and the 16 list-length gathers of a lane are
+    // coalesced across the wave and all independent (two memory latencies per round); each chunk is
+    // then scanned with shuffles and the 16 wave totals are combined in LDS.  (The first version gave
+    // each thread 32 consecutive pairs — strided loads — and a 10-step block scan: 43 µs at 32K pairs.)
+    constexpr int J = 16;  // (32 spilled at 1024 threads per block)
+    __shared__ int wsum[16];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int carry = 0;
+    for (int64_t base = 0; base < npairs; base += 16 * 64 * J) {
+        const int64_t seg = base + (int64_t)wave * 64 * J;
+        int l[J];  // list ids fit 32 bits (64-bit ids spilled at 1024 threads per block)
 #pragma unroll
-        for (int j = 0; j < PER; ++j) l[j] = i0 + j < npairs ? probes[i0 + j] : -1;
-        int v[PER];
-#pragma unroll
-        for (int j = 0; j < PER; ++j) v[j] = (l[j] >= 0 && l[j] < nlist) ? ivf_nch(list_len[l[j]]) : 0;
-        int sum = 0;
-#pragma unroll
-        for (int j = 0; j < PER; ++j) sum += v[j];
-        sv[threadIdx.x] = sum;
-        __syncthreads();
-        for (int o = 1; o < 1024; o <<= 1) {
-            int t = 0;
-            if ((int)threadIdx.x >= o) t = sv[threadIdx.x - o];
-            __syncthreads();
-            sv[threadIdx.x] += t;
-            __syncthreads();
+        for (int j = 0; j < J; ++j) {
+            const int64_t i = seg + 64 * j + lane;
+            const int64_t pv = i < npairs ? probes[i] : -1;
+            l[j] = pv >= 0 && pv < nlist ? (int)pv : -1;
         }
-        int run = carry + sv[threadIdx.x] - sum;
+        int v[J];
 #pragma unroll
-        for (int j = 0; j < PER; ++j) {
-            if (i0 + j < npairs) slot_off[i0 + j] = run;
-            run += v[j];
+        for (int j = 0; j < J; ++j) v[j] = l[j] >= 0 ? ivf_nch(list_len[l[j]]) : 0;
+        int run = 0;
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            int x = v[j];
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int t = __shfl_up(x, o);
+                if (lane >= o) x += t;
+            }
+            const int tot = __shfl(x, 63);
+            v[j] = run + x - v[j];  // exclusive offset inside the wave's segment
+            run += tot;
         }
+        if (lane == 0) wsum[wave] = run;
         __syncthreads();
-        if (threadIdx.x == 1023) carry += sv[1023];
+        int off = carry, total = 0;
+        for (int w2 = 0; w2 < 16; ++w2) {
+            const int t = wsum[w2];
+            off += w2 < wave ? t : 0;
+            total += t;
+        }
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const int64_t i = seg + 64 * j + lane;
+            if (i < npairs) slot_off[i] = off + v[j];
+        }
+        carry += total;
         __syncthreads();
     }
     if (threadIdx.x == 0) slot_off[npairs] = carry;
