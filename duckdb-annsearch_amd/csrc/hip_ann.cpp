@@ -326,8 +326,11 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
     sh.fD.ensure(sizeof(float) * (size_t)nf * kout, sh.device);
     sh.fI.ensure(sizeof(int64_t) * (size_t)nf * kout, sh.device);
     launch_ivf_gather_queries(xq, sh.flagged.get<int>(), nf, d, sh.fq.get<float>(), st);
-    flat_shard_search(ix, sh, nf, sh.fq.get<float>(), k_user, kout, sh.fD.get<float>(), sh.fI.get<int64_t>(), st,
-                      kFlatSplit3);
+    {
+        TimerPause p0(ix.timer_main), p1(ix.timer_merge);
+        flat_shard_search(ix, sh, nf, sh.fq.get<float>(), k_user, kout, sh.fD.get<float>(), sh.fI.get<int64_t>(), st,
+                          kFlatSplit3);
+    }
     launch_ivf_scatter_results(sh.fD.get<float>(), sh.fI.get<int64_t>(), sh.flagged.get<int>(), nf, kout, D, I, st);
 }
 

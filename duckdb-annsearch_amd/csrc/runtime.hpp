@@ -109,6 +109,15 @@ struct ScopedTiming {
     ~ScopedTiming() { if (b) (void)hipEventRecord(b, s); }
 };
 
+// Pauses a timer for a scope (the exact forms' re-runs of flagged queries stay out of the main kernel's
+// timing, which the roofline reads).
+struct TimerPause {
+    KernelTimer &t;
+    bool was;
+    explicit TimerPause(KernelTimer &tt) : t(tt), was(tt.on) { t.on = false; }
+    ~TimerPause() { t.on = was; }
+};
+
 enum class Kind { Flat = 1, IVF = 2 };
 
 // One contiguous row range of a Flat index resident on one device.
