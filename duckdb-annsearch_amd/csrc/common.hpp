@@ -46,6 +46,10 @@ enum IvfForm : int {
     kFormSplit2Exact = 5
 };
 constexpr int kRerankK = 16, kRerankMaxK = 12;
+// Flat exact form, IP: 32 candidates per (split, query).  At 10M × 768 (U(-1,1) rows) 16 left ≈0.2% of
+// the IP queries failing the bound (each a re-scan of the shard: 61 → 67 ms per batch), 32 none (65 ms);
+// L2 had no failures at 16, and 32 costs it 60 → 66 ms (the fuller epilogue lists), so L2 keeps 16.
+constexpr int kFlatRerankKIP = 32;
 // Flat BLAS-path (nq >= kBlasThreshold) q·x form (hipann_flat_set_form): exact fp32 MFMA products
 // (flat_gemm_topk2), or the fp32-level 3-term split-bf16 products on the bf16 matrix cores
 // (flat_gemm_topk_bf); kFlatSplit2 is the 2-term split (≈2^-16 relative, A/B only).  kFlatSplit2Exact

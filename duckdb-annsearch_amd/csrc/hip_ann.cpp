@@ -283,7 +283,7 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
     const bool exact = form == kFlatSplit2Exact && kout <= kRerankMaxK;
     if (form == kFlatSplit2Exact && !exact) form = kFlatSplit3;
     const int k_user = k;
-    if (exact) k = kRerankK;  // the scan keeps 16 per (split, query); the rerank returns kout
+    if (exact) k = metric == kIP ? kFlatRerankKIP : kRerankK;  // kept per (split, query); the rerank returns kout
     sh.part_d.ensure((size_t)nsplit * nq * k * sizeof(float), sh.device);
     sh.part_i.ensure((size_t)nsplit * nq * k * sizeof(int), sh.device);
     {

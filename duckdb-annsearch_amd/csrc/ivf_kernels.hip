@@ -995,6 +995,7 @@ namespace hipann {
 // rounding of the norms and of both sums, with margin).  A query whose kout-th exact distance is not
 // < K16 − E (or < −K16... for IP the same bound on −q·x) is flagged; the host re-runs the flagged
 // queries on the 3-term path.  With fewer than 16 merged candidates nothing was pruned.
+// The list length k (16; 32 for Flat IP, common.hpp) is the number of candidates reranked.
 // ---------------------------------------------------------------------------------------------
 template <bool IP>
 __global__ void __launch_bounds__(256)
@@ -1027,12 +1028,12 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
                 row = raw;
             }
         }
-        L.offer(key, row, kRerankK - 1);
+        L.offer(key, row, k - 1);
     }
     const int myrow = L.id[0];
-    const bool real = lane < kRerankK && myrow != IdTraits<int>::pad();
+    const bool real = lane < k && myrow != IdTraits<int>::pad();
     const int ncand = __popcll(__ballot(real));
-    const float k16 = readlane_f(L.d[0], kRerankK - 1);
+    const float k16 = readlane_f(L.d[0], k - 1);  // K_k: the k-th merged scan key
     // 2. exact direct-form distances of the candidates (4 rows in flight, wave reduction per row)
     const float *qp = Q + q * (int64_t)d;
     float qq = 0.f;
@@ -1076,7 +1077,7 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
     // 4. exactness check
     const float dk = readlane_f(R.d[0], kout - 1);
     const float E = 0x1p-12f * (qq + xmax2);
-    if (ncand == kRerankK && !(dk < k16 - E) && lane == 0) flagged[atomicAdd(nflag, 1)] = (int)q;
+    if (ncand == k && !(dk < k16 - E) && lane == 0) flagged[atomicAdd(nflag, 1)] = (int)q;
     const float pad_d = IP ? -__builtin_inff() : __builtin_inff();
     if (lane < kout) {
         const bool pad = R.id[0] == IdTraits<long long>::pad();
@@ -1117,7 +1118,7 @@ void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int 
                        int64_t label_offset, float xmax2, float *D, int64_t *I, int *nflag, int *flagged,
                        hipStream_t st) {
     if (nq <= 0) return;
-    HIPANN_REQUIRE(k == kRerankK && kout >= 1 && kout <= kRerankMaxK, "ivf rerank: k / kout out of range");
+    HIPANN_REQUIRE(k >= kRerankK && k <= 64 && kout >= 1 && kout <= kRerankMaxK, "ivf rerank: k / kout out of range");
     dim3 grid((unsigned)ceil_div(nq, 4)), block(256);
     if (metric == kIP)
         hipLaunchKernelGGL(ivf_rerank_topk<true>, grid, block, 0, st, pd, pi, slot_off, nprobe, nq, k, kout, Q, codes, d,
