@@ -350,7 +350,7 @@ def main():
             fdesc = (f"bf16 MFMA (v_mfma_f32_32x32x16_bf16) over a {3 if fform == 1 else 2}-term split: "
                      f"{terms} bf16 products per fp32 product")
             if fform == 3:
-                fdesc += ("; the scan keeps 16 per (split, query) as a filter, merge_ms = exact direct-form "
+                fdesc += ("; the scan keeps 16 (IP: 32) per (split, query) as a filter, merge_ms = exact direct-form "
                           "rerank of the 16 + bound check")
         achieved = terms * flops / (kern_ms * 1e-3) / 1e12 if kern_ms > 0 else 0.0
         roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",

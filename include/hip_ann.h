@@ -78,7 +78,7 @@ int hipann_flat_reconstruct(void *index, int64_t key, float *out, char *err_buf,
  * six products above 2^-26 relative on the bf16 matrix cores, fp32 accumulation — fp32-level products
  * at several times the fp32 rate.  HIPANN_FLAT_FORM_SPLIT2: two terms, three products (≈2^-16
  * relative per product; measurement only).  HIPANN_FLAT_FORM_SPLIT2_EXACT (default): the SPLIT2 scan
- * keeps the 16 best rows per database split and query only as a filter; every returned distance is
+ * keeps the 16 best rows (32 for IP) per database split and query only as a filter; every returned distance is
  * recomputed in FAISS's direct fp32 form (Σ(q−x)² / q·x) and a per-query bound (|scan key − exact| ≤
  * 2^-12·(‖q‖² + max‖x‖²)) proves no pruned row reaches the top-k — queries that fail it re-run on
  * SPLIT3 (k ≤ 12; larger k use SPLIT3).  Returns 0, or -1 for a bad handle / form. */
