@@ -321,6 +321,7 @@ void *hipann_ivf_create(int d, int metric, int nlist, int nprobe, const float *c
                 load[s] += list_offsets[l + 1] - list_offsets[l];
             }
         }
+        ix->owner = owner;
         for (int s = 0; s < ns; ++s) {
             auto sh = std::make_unique<IvfShard>();
             sh->device = devs[s];
@@ -375,6 +376,7 @@ void *hipann_ivf_create_device(int d, int metric, int nlist, int nprobe, const f
         ix->metric = metric;
         ix->nlist = nlist;
         ix->nprobe = nprobe;
+        ix->owner.assign(nlist, 0);
         auto sh = std::make_unique<IvfShard>();
         sh->device = device;
         sh->stream = make_stream(device);
@@ -483,6 +485,30 @@ int hipann_ivf_search(void *h, int64_t nq, const float *xq, int64_t k, float *D,
         auto *vx = static_cast<IvfIndex *>(ix);
         std::lock_guard<std::mutex> lk(vx->mu);
         return ivf_search_host(*vx, nq, xq, k, D, I);
+    });
+}
+
+int hipann_ivf_search_np(void *h, int nprobe, int64_t nq, const float *xq, int64_t k, float *D, int64_t *I, char *eb,
+                         int el) {
+    return guard_int(eb, el, [&]() -> int {
+        HIPANN_REQUIRE(h, "null index");
+        auto *ix = static_cast<IndexBase *>(h);
+        HIPANN_REQUIRE(ix->kind == Kind::IVF, "not an IVFFlat index");
+        auto *vx = static_cast<IvfIndex *>(ix);
+        std::lock_guard<std::mutex> lk(vx->mu);
+        if (nprobe <= 0) return ivf_search_host(*vx, nq, xq, k, D, I);
+        // the call's nprobe, read and restored under the handle's lock (concurrent connections with
+        // different SearchParametersIVF never see each other's value)
+        const int saved = vx->nprobe;
+        vx->nprobe = nprobe;
+        try {
+            const int rc = ivf_search_host(*vx, nq, xq, k, D, I);
+            vx->nprobe = saved;
+            return rc;
+        } catch (...) {
+            vx->nprobe = saved;
+            throw;
+        }
     });
 }
 

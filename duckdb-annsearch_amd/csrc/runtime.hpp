@@ -203,6 +203,7 @@ struct IvfShard {
 
 struct IvfIndex : IndexBase {
     int nlist = 0, nprobe = 1;
+    std::vector<int> owner;  // list → shard (size-balanced at create; appended rows follow their list)
     int form = kFormSplit2Exact;
     int64_t rerank_fallbacks = 0;  // queries re-run on the 3-term path by the exactness check
     std::vector<std::unique_ptr<IvfShard>> shards;

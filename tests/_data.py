@@ -40,43 +40,104 @@ def build_ivf_lists(xb: np.ndarray, centroids: np.ndarray, metric: int = 0):
     return off, order.astype(np.int64), np.ascontiguousarray(xb[order])
 
 
-def check_topk_parity(xb, xq, D, I, Do, Io, metric=0, tau=1e-5, dist_rtol=1e-5, dist_atol=None, min_exact=0.99):
-    """Parity rule: ids/order identical to the oracle except inside near-tie windows.
+# Parity rule: tau calibrated on the box (SURVEY §8c asks for 1e-6 "to be calibrated"); the observed
+# gaps are collected in PARITY_STATS and written to gpurun_out/parity_calibration.json (conftest.py).
+TAU = 1e-6
+# The 2-term split forms (Flat form 2, IVF form 4: measurement only) drop terms worth up to 2^-15·‖q‖‖x‖
+# per q·x (3·2^-16 plus the operands' 2^-17 remainders), i.e. ≤ 3.1e-5 of the L2 / IP scale.
+SPLIT2_TAU = 4e-5
+PARITY_STATS: list = []
+CURRENT_TEST = None
 
-    For every rank where the labels differ, the exact (fp64) distances of the two labels must lie
-    within ``tau * scale`` of each other (scale = |q|² + max |x|² for L2, |q|·max|x| for IP: the
-    rounding scale of the fp32 forms), the returned label list must hold distinct valid labels, and
-    at least ``min_exact`` of all slots must match exactly.  Reported distances must match the fp64
-    distance of the returned label within dist_rtol (relative) / dist_atol (absolute, default from
-    the scale).  Pads (-1) must coincide.
-    """
+
+def max_sqnorm(xb) -> float:
+    """max_i ‖x_i‖² in fp64, chunked (1M × 768 rows would need a 6 GB fp64 copy at once)."""
+    m = 0.0
+    for r0 in range(0, len(xb), 65536):
+        c = xb[r0:r0 + 65536].astype(np.float64)
+        m = max(m, float(np.max(np.einsum("ij,ij->i", c, c))))
+    return m
+
+
+def check_probe_parity(cen, xq, P, Po, metric=0, tau=TAU):
+    """IVF probe lists (coarse quantizer: a Flat search over the centroids) equal the oracle's, in order,
+    except where the differing centroids are near ties at the nprobe boundary (fp64 distances within
+    tau·scale).  Returns a bool mask of the queries whose probe lists are identical (the IVF results of
+    the others may legitimately differ and are excluded from the id parity check)."""
+    assert P.shape == Po.shape
+    same = np.all(P == Po, axis=1)
+    cmax = max_sqnorm(cen)
+    for qi in np.nonzero(~same)[0]:
+        q = xq[qi].astype(np.float64)
+        w = tau * _scale(q, cmax, metric)
+        lab_g, lab_o = P[qi], Po[qi]
+        eg = O.exact_dists(cen, xq[qi], lab_g, metric)
+        eo = O.exact_dists(cen, xq[qi], lab_o, metric)
+        diff = np.nonzero(lab_g != lab_o)[0]
+        assert np.all(np.abs(eg[diff] - eo[diff]) <= w + 1e-12), (
+            f"query {qi}: probe lists differ beyond the tie window at ranks {diff}: {lab_g[diff]} vs {lab_o[diff]}")
+    return same
+
+
+def _scale(q64, xmax, metric):
+    """Rounding scale of one query's fp32 distances: |q|² + max|x|² (L2) or |q|·max|x| (IP)."""
+    qn = float(np.dot(q64, q64))
+    return (qn + xmax) if metric == 0 else float(np.sqrt(qn * xmax))
+
+
+def check_topk_parity(xb, xq, D, I, Do, Io, metric=0, tau=TAU, dist_rtol=1e-5, dist_tau=8e-6, min_exact=None,
+                      name=None):
+    """Parity rule: ids and order identical to the oracle's except inside near-tie windows.
+
+    Per query, with w = tau·scale (scale = |q|² + max|x|² for L2, |q|·max|x| for IP — the rounding
+    scale of the fp32 forms) and fp64 distances e(label):
+      * at every rank where the labels differ, |e(gpu label) − e(oracle label)| ≤ w (a near tie);
+      * the label SETS agree outside the boundary window: every label (of either list) whose key is
+        below the oracle's k-th key − w is in both lists;
+      * the returned labels are distinct and valid, pads (−1) coincide;
+      * returned distances match the fp64 distance of the returned label within dist_rtol (relative)
+        plus dist_tau·scale (absolute), and are sorted.
+    The largest gap seen at a differing rank (in units of scale) is recorded in PARITY_STATS.
+    Returns a dict of the observed statistics."""
     nq, k = I.shape
     assert I.shape == Io.shape
     pads = Io < 0
     assert np.array_equal(I < 0, pads), "pad slots differ"
-    xmax = float(np.max(np.sum(xb.astype(np.float64) ** 2, 1))) if len(xb) else 0.0
-    exact = (I == Io).mean() if I.size else 1.0
-    assert exact >= min_exact, f"only {exact:.4f} of the slots match exactly"
+    xmax = max_sqnorm(xb)
+    exact = float((I == Io).mean()) if I.size else 1.0
+    if min_exact is not None:
+        assert exact >= min_exact, f"only {exact:.4f} of the slots match exactly"
+    sgn = 1.0 if metric == 0 else -1.0  # key = dist (L2) or -ip (IP): ascending
+    max_gap = 0.0
+    ndiff = 0
     for qi in range(nq):
         q = xq[qi]
-        qn = float(np.dot(q.astype(np.float64), q.astype(np.float64)))
-        scale = (qn + xmax) if metric == 0 else np.sqrt(qn * xmax) * np.sqrt(xb.shape[1])
-        atol = dist_atol if dist_atol is not None else 8e-6 * max(scale, 1e-30)
+        scale = _scale(q.astype(np.float64), xmax, metric)
+        w = tau * scale
+        atol = dist_tau * max(scale, 1e-30)
         valid = I[qi] >= 0
         labs = I[qi][valid]
         assert len(set(labs.tolist())) == len(labs), f"duplicate labels for query {qi}"
         if not len(labs):
             continue
-        ex = O.exact_dists(xb, q, labs, metric)
-        assert np.all(np.abs(D[qi][valid] - ex) <= atol + dist_rtol * np.abs(ex)), (
-            f"query {qi}: distances off: {D[qi][valid]} vs exact {ex}")
-        diff = np.nonzero(I[qi] != Io[qi])[0]
+        eg = O.exact_dists(xb, q, labs, metric)
+        assert np.all(np.abs(D[qi][valid] - eg) <= atol + dist_rtol * np.abs(eg)), (
+            f"query {qi}: distances off: {D[qi][valid]} vs exact {eg}")
+        olabs = Io[qi][valid]
+        eo = O.exact_dists(xb, q, olabs, metric)
+        diff = np.nonzero(labs != olabs)[0]
         if len(diff):
-            eo = O.exact_dists(xb, q, Io[qi][diff], metric)
-            eg = O.exact_dists(xb, q, I[qi][diff], metric)
-            assert np.all(np.abs(eo - eg) <= tau * scale + 1e-12), (
-                f"query {qi}: rank(s) {diff} differ beyond the tie window: {I[qi][diff]} vs {Io[qi][diff]}, "
-                f"exact {eg} vs {eo}")
+            ndiff += len(diff)
+            gap = np.abs(eo[diff] - eg[diff])
+            max_gap = max(max_gap, float(gap.max()) / max(scale, 1e-30))
+            assert np.all(gap <= w + 1e-12), (
+                f"query {qi}: rank(s) {diff} differ beyond the tie window (tau={tau}): {labs[diff]} vs "
+                f"{olabs[diff]}, exact {eg[diff]} vs {eo[diff]}, gap/scale {gap / scale}")
+            bound = sgn * eo[-1] - w
+            inner_g = set(labs[sgn * eg < bound].tolist())
+            inner_o = set(olabs[sgn * eo < bound].tolist())
+            assert inner_g <= set(olabs.tolist()) and inner_o <= set(labs.tolist()), (
+                f"query {qi}: label sets differ outside the boundary tie window")
     # sortedness of the returned distances
     Dv = np.where(pads, np.nan, D)
     for qi in range(nq):
@@ -85,3 +146,8 @@ def check_topk_parity(xb, xq, D, I, Do, Io, metric=0, tau=1e-5, dist_rtol=1e-5, 
             assert np.all(np.diff(v) >= 0), f"query {qi}: distances not ascending"
         else:
             assert np.all(np.diff(v) <= 0), f"query {qi}: distances not descending"
+    st = {"name": name or CURRENT_TEST, "nq": int(nq), "k": int(k), "d": int(xb.shape[1]) if xb.ndim == 2 else None,
+          "n": int(len(xb)), "metric": int(metric), "exact_fraction": exact, "differing_slots": int(ndiff),
+          "max_gap_over_scale": max_gap, "tau": tau}
+    PARITY_STATS.append(st)
+    return st

@@ -18,6 +18,42 @@ sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(Path(__file__).resolve().parent))
 
 
+@pytest.fixture(autouse=True)
+def _parity_test_name(request):
+    """Tag the parity statistics (tests/_data.py PARITY_STATS) with the running test's id."""
+    import _data
+
+    _data.CURRENT_TEST = request.node.nodeid
+    yield
+
+
+def pytest_sessionfinish(session, exitstatus):
+    """Tie-window calibration (tau "to be calibrated on the box"): the largest gap between
+    the fp64 distances of differing labels seen by check_topk_parity, per test and overall, written to
+    gpurun_out/parity_calibration.json when any GPU parity check ran."""
+    import json
+
+    import _data
+
+    st = _data.PARITY_STATS
+    if not st:
+        return
+    out = ROOT / "gpurun_out"
+    out.mkdir(exist_ok=True)
+    worst = max(st, key=lambda r: r["max_gap_over_scale"])
+    summary = {
+        "checks": len(st),
+        "tau": _data.TAU,
+        "max_gap_over_scale": worst["max_gap_over_scale"],
+        "max_gap_check": worst,
+        "checks_with_differing_slots": sum(1 for r in st if r["differing_slots"]),
+        "min_exact_fraction": min(r["exact_fraction"] for r in st),
+        "large": [r for r in st if r["n"] * (r["d"] or 0) >= 100_000_000],
+        "all": st,
+    }
+    (out / "parity_calibration.json").write_text(json.dumps(summary, indent=1) + "\n")
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: requires an MI355X GPU (HIP path through libhipann.so)")
 

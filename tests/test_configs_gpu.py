@@ -1,0 +1,203 @@
+"""GPU parity at the BASELINE configurations' shapes, against the oracle.
+
+The benchmark configurations themselves (10M rows) are far beyond what the oracle finishes in seconds, so
+each test runs the same code path at the largest shape the oracle checks quickly, with the same data
+model, the same build (GPU k-means / k-NN graph / SQ8 codec) and the same batch:
+
+* C2  Flat L2 1M × 768, nq = 1024, k = 10 (the full C2 shape): every form through the device API the
+      bench uses; the oracle (FAISS BLAS-path restatement) on a 256-query subset.
+* C3  IVFFlat nlist = 1024, nprobe = 32, d = 768, nq = 1024, k = 10 on 200k rows of the bench's
+      low-rank data, built by ivf_build (the bench's GPU k-means + assignment): probe lists equal the
+      oracle's (tie-tolerant) and ids follow the parity rule; forms 5 (default), 3 and 0.
+* C4  DiskANN resident traversal at d = 1536 SQ8, R = 64, L = 128 on a 32k-node graph built by
+      diskann_build (the bench's graph builder), plus the exact-tie integer variant (ids, distances,
+      evaluation and step counts identical to the oracle).
+
+Pattern: faiss-metal/tests/test_metal_ivfflat.mm:28-100 and test_metal_flat.mm:489-505 (GPU vs CPU FAISS
+on the same data, top-k compared).
+"""
+from __future__ import annotations
+
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from _data import TAU, check_probe_parity, check_topk_parity
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+
+def _dev_search(index, xq_t, k, torch):
+    nq = xq_t.shape[0]
+    D = torch.empty((nq, k), device=xq_t.device, dtype=torch.float32)
+    I = torch.empty((nq, k), device=xq_t.device, dtype=torch.int64)
+    index.search_device(nq, xq_t.data_ptr(), k, D.data_ptr(), I.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return D.cpu().numpy(), I.cpu().numpy()
+
+
+@pytest.fixture(scope="module")
+def c2_data(gpu):
+    import torch
+
+    import bench
+
+    dev = torch.device("cuda", 0)
+    n, d, nq = 1_000_000, 768, 1024
+    xb_t = torch.empty((n, d), device=dev, dtype=torch.float32)
+    bench.gen_uniform_rows(torch, xb_t, 0, 42)  # the bench's C2 rows (U(-1,1), chunk-seeded)
+    g = torch.Generator(device=dev).manual_seed(4242)
+    xq_t = (torch.rand((nq, d), generator=g, device=dev) * 2 - 1).contiguous()
+    torch.cuda.synchronize()
+    return xb_t, xq_t, xb_t.cpu().numpy(), xq_t.cpu().numpy()
+
+
+@pytest.fixture(scope="module")
+def c2_oracle(c2_data, oracle):
+    _, _, xb, xq = c2_data
+    return oracle.flat_search(xb, xq[:256], 10, 0)
+
+
+@pytest.mark.parametrize("form", [3, 1, 0])
+def test_c2_flat_1m_768_nq1024(gpu, c2_data, c2_oracle, form):
+    """C2: 1M × 768, nq = 1024, k = 10 through hipann_flat_search_device (the bench's call), every
+    fp32-level form; the oracle's BLAS-path top-k on 256 queries; all 1024 rows sorted and distinct."""
+    import torch
+
+    xb_t, xq_t, xb, xq = c2_data
+    ix = gpu.HipIndexFlatDevice(768, 0, xb_t.data_ptr(), xb_t.shape[0], 0, copy=False)
+    ix.form = form
+    D, I = _dev_search(ix, xq_t, 10, torch)
+    Do, Io = c2_oracle
+    st = check_topk_parity(xb, xq[:256], D[:256], I[:256], Do, Io, 0)
+    assert st["exact_fraction"] >= 0.995, st
+    assert np.all(np.diff(D, axis=1) >= 0) and np.all(I >= 0)
+    assert all(len(set(r)) == 10 for r in I.tolist())
+    ix.close()
+
+
+@pytest.fixture(scope="module")
+def c3_index(gpu):
+    import torch
+
+    import bench
+    from ivf_build import build_ivf_shard
+
+    dev = torch.device("cuda", 0)
+    n, d, nq, nlist, nprobe = 200_000, 768, 1024, 1024, 32
+    gc = torch.Generator(device=dev).manual_seed(7)
+    basis = bench.lowrank_basis(torch, 16, d, gc)  # the bench's C3 data model (intrinsic dim 16)
+    xb_t = torch.empty((n, d), device=dev, dtype=torch.float32)
+    bench.gen_lowrank_rows(torch, xb_t, 0, basis, 0.02, 42)
+    xq_t = torch.empty((nq, d), device=dev, dtype=torch.float32)
+    bench.gen_lowrank_rows(torch, xq_t, 0, basis, 0.02, 4242)
+    xb = xb_t.cpu().numpy()
+    index, info = build_ivf_shard(torch, gpu, xb_t, 0, n, nlist, nprobe, 0, 0, 1, centres_seed=1234)
+    del xb_t
+    cen_t, codes_t, ids_t = index._keep
+    lists = (cen_t.cpu().numpy(), index._offsets.copy(), ids_t.cpu().numpy(), codes_t.cpu().numpy())
+    return index, info, xb, xq_t, xq_t.cpu().numpy(), lists
+
+
+@pytest.fixture(scope="module")
+def c3_oracle(c3_index, oracle):
+    _, _, _, _, xq, (cen, off, ids, codes) = c3_index
+    return oracle.ivf_search(cen, off, ids, codes, xq, 10, 32, 0)
+
+
+@pytest.mark.parametrize("form", [5, 3, 0])
+def test_c3_ivf_nlist1024_nprobe32_d768_nq1024(gpu, c3_index, c3_oracle, form):
+    """C3 shape: nlist = 1024, nprobe = 32, d = 768, nq = 1024, k = 10 (200k rows of the bench's data,
+    lists from the bench's GPU build).  Probe lists equal the oracle's; ids follow the parity rule over
+    the scanned set on every query whose probe list is identical (tie-window differences excluded)."""
+    import torch
+
+    index, info, xb, xq_t, xq, (cen, off, ids, codes) = c3_index
+    assert info["nlist"] == 1024 and np.diff(off).sum() == len(xb)
+    index.form = form
+    D, I = _dev_search(index, xq_t, 10, torch)
+    P = index.last_probes(len(xq))
+    Do, Io, Po = c3_oracle
+    same = check_probe_parity(cen, xq, P, Po, 0)
+    assert same.mean() >= 0.99, same.mean()
+    st = check_topk_parity(xb, xq[same], D[same], I[same], Do[same], Io[same], 0)
+    assert st["exact_fraction"] >= 0.995, st
+    if form == 5:  # returned distances are the direct fp32 form, like the oracle's scanner
+        v = I[same] >= 0
+        assert np.allclose(D[same][v], Do[same][v], rtol=2e-6, atol=1e-6)
+    index.form = 5
+
+
+def _c4_graph(gpu, n, d, R, seed, integer=False):
+    import torch
+
+    import bench
+    import diskann_build as DB
+
+    dev = torch.device("cuda", 0)
+    gc = torch.Generator(device=dev).manual_seed(seed)
+    if integer:
+        g = torch.Generator(device=dev).manual_seed(seed)
+        base = torch.randint(0, 4, (n // 4, d), generator=g, device=dev).to(torch.float32)
+        x = base.repeat_interleave(4, 0)[torch.randperm(n, generator=g, device=dev)].contiguous()
+        x[0] = 0.0
+        x[1] = 255.0  # SQ8 min 0, scale 255: codes equal the values, distances exact in fp32
+        q = torch.randint(0, 4, (256, d), generator=g, device=dev).to(torch.float32)
+    else:
+        basis = bench.lowrank_basis(torch, 16, d, gc)  # the bench's C4 data model
+        x = torch.empty((n, d), device=dev, dtype=torch.float32)
+        bench.gen_lowrank_rows(torch, x, 0, basis, 0.02, 42)
+        q = torch.empty((512, d), device=dev, dtype=torch.float32)
+        bench.gen_lowrank_rows(torch, q, 0, basis, 0.02, 4242)
+    codes, mins, scale = DB.sq8_encode(torch, x)
+    adj_t, medoid = DB.knn_graph(torch, x, R=R, n_random=R // 4, seed=seed)
+    adj = DB.adjacency_u32(torch, adj_t)
+    torch.cuda.synchronize()
+    return (x.cpu().numpy(), q.cpu().numpy(), codes.cpu().numpy(), mins.cpu().numpy(), scale.cpu().numpy(), adj,
+            medoid)
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+def test_c4_resident_bfs_d1536_sq8_L128(gpu, oracle, metric):
+    """C4 shape: the resident traversal at d = 1536 SQ8, R = 64, L = 128 (the bench's template of
+    diskann_bfs) on a 32k-node graph from the bench's builder, vs DiskProvider::search_batch restated.
+    The device SQ8 encoder equals the oracle's codec; BFS ids ≥ 99% identical (summation order can
+    move a trajectory), distances within 1e-5, evaluation counts within 1%."""
+    x, q, codes, mins, scale, adj, medoid = _c4_graph(gpu, 32768, 1536, 64, 8)
+    m2, s2 = oracle.sq8_train(x)
+    assert np.array_equal(mins, m2) and np.array_equal(scale, s2)
+    assert np.array_equal(codes, oracle.sq8_encode(x, mins, scale))
+    db = gpu.DiskannDeviceDB(codes, 1, mins, scale)
+    db.register_graph(adj)
+    ids, dists, st = db.search_batch_resident([medoid], q, 10, 128, metric)
+    assert st["host_requeries"] == 0 and st["pops"] > 0
+    oi, od, ost = oracle.diskann_search_batch(adj, [medoid], q, 10, 128, metric, codes=codes, mins=mins,
+                                               scale=scale)
+    assert (ids == oi).mean() >= 0.99
+    same = ids == oi
+    assert np.allclose(dists[same], od[same], rtol=1e-5, atol=1e-4)
+    assert abs(st["evals"] - ost["evals"]) <= 0.01 * ost["evals"]
+    assert np.all(np.diff(dists, axis=1) >= 0)
+    # the host lock-step BFS over the id-gather kernel (the reference-shaped path) on the same graph
+    hi, hd, hst = db.search_batch(adj, [medoid], q[:128], 10, 128, metric)
+    assert (hi == oi[:128]).mean() >= 0.99
+
+
+def test_c4_resident_bfs_d1536_exact_ties(gpu, oracle):
+    """C4 shape on small-integer data (every distance exact in fp32, rows duplicated 4×: exact ties in the
+    result-list binary search, the boundary evictions and the spill list): ids, distances, evaluation
+    and step counts identical to the oracle."""
+    x, q, codes, mins, scale, adj, medoid = _c4_graph(gpu, 16384, 1536, 64, 9, integer=True)
+    assert np.all(mins == 0) and np.all(scale == 255)
+    db = gpu.DiskannDeviceDB(codes, 1, mins, scale)
+    db.register_graph(adj)
+    ids, dists, st = db.search_batch_resident([medoid, 7], q, 10, 128)
+    oi, od, ost = oracle.diskann_search_batch(adj, [medoid, 7], q, 10, 128, 0, codes=codes, mins=mins, scale=scale)
+    assert np.array_equal(ids, oi)
+    assert np.array_equal(dists, od)
+    assert st["evals"] == ost["evals"]
+    assert st["steps"] == ost["steps"]
