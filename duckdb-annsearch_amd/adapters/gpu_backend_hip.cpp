@@ -8,7 +8,9 @@
 // Behaviour mirrored:
 //   IsAvailable / DeviceInfo / BackendName     gpu_backend_metal.mm:33-45
 //   CpuToGpu: IndexIVFFlat first, then IndexFlat, else throw std::runtime_error   :45-60
-//   GpuToCpu: back to a CPU IndexFlat / IndexIVFFlat                             :62-75
+//   GpuToCpu: back to a CPU IndexIVFFlat / IndexFlat                             :62-75
+//             (index_metal_to_cpu_ivf, MetalIndexIVFFlat.mm:328-356: flat quantizer over the centroids,
+//             own_fields, is_trained, nprobe, invlists->add_entries per list, ntotal)
 //   search(): MetalIndexFlat::search contract (MetalIndexFlat.mm:294-369): k <= 0 throws,
 //             effective_k = min(k, ntotal), (+inf | -inf, -1) pads, int64 labels.
 //   Errors are std::runtime_error (faiss_index.cpp:122-124, :146-148 catch exactly that type).
@@ -22,6 +24,9 @@
 #include <faiss/IndexIVFFlat.h>
 #include <faiss/invlists/InvertedLists.h>
 
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -80,6 +85,7 @@ public:
         char err[512] = {0};
         check(hipann_flat_reconstruct(handle_->h, key, recons, err, sizeof err), err);
     }
+    void *handle() const { return handle_->h; }
 
 private:
     std::unique_ptr<Handle> handle_;
@@ -112,25 +118,33 @@ public:
         is_trained = true;
         nprobe_ = cpu.nprobe;
     }
-    void add(faiss::idx_t, const float *) override {
-        throw std::runtime_error("HipIndexIVFFlat::add: the GPU copy is invalidated on append (faiss_index.cpp:469)");
+    // IndexIVF::add / add_with_ids on the GPU copy: hipann_ivf_add assigns the rows with the GPU coarse
+    // quantizer and appends them to their lists (labels ntotal + i, or xids).
+    void add(faiss::idx_t n, const float *x) override { add_with_ids(n, x, nullptr); }
+    void add_with_ids(faiss::idx_t n, const float *x, const faiss::idx_t *xids) override {
+        char err[512] = {0};
+        check(hipann_ivf_add(handle_->h, n, x, reinterpret_cast<const int64_t *>(xids), err, sizeof err), err);
+        ntotal += n;
     }
     void search(faiss::idx_t n, const float *x, faiss::idx_t k, float *distances, faiss::idx_t *labels,
                 const faiss::SearchParameters *params = nullptr) const override {
         if (k <= 0) throw std::runtime_error("k must be > 0");
         // FaissIndex::Search sets nprobe on the CPU index before each search (faiss_index.cpp:720-726);
-        // honour IVF search parameters when given.
-        if (auto *ip = dynamic_cast<const faiss::SearchParametersIVF *>(params)) {
-            if (ip->nprobe > 0) hipann_ivf_set_nprobe(handle_->h, (int)ip->nprobe);
-        } else {
-            hipann_ivf_set_nprobe(handle_->h, (int)nprobe_);
-        }
+        // IVF search parameters override it per call.  The value travels with the call and is read under
+        // the handle's lock (hipann_ivf_search_np), so concurrent searches with different nprobe are safe.
+        int np = (int)nprobe_;
+        if (auto *ip = dynamic_cast<const faiss::SearchParametersIVF *>(params))
+            if (ip->nprobe > 0) np = (int)ip->nprobe;
         char err[512] = {0};
-        check(hipann_ivf_search(handle_->h, n, x, k, distances, reinterpret_cast<int64_t *>(labels), err, sizeof err),
+        check(hipann_ivf_search_np(handle_->h, np, n, x, k, distances, reinterpret_cast<int64_t *>(labels), err,
+                                   sizeof err),
               err);
     }
     void reset() override { throw std::runtime_error("HipIndexIVFFlat::reset: rebuild from the CPU index"); }
     void set_nprobe(size_t np) { nprobe_ = np; }
+    size_t nprobe() const { return nprobe_; }
+    size_t nlist() const { return nlist_; }
+    void *handle() const { return handle_->h; }
 
 private:
     std::unique_ptr<Handle> handle_;
@@ -154,16 +168,39 @@ public:
         throw std::runtime_error("HIP GPU supports IndexFlat and IndexIVFFlat. Got an unsupported index type.");
     }
     std::unique_ptr<faiss::Index> GpuToCpu(faiss::Index *gpu_index) override {
-        if (auto *f = dynamic_cast<HipIndexFlat *>(gpu_index)) {
-            auto cpu = std::make_unique<faiss::IndexFlat>(f->d, f->metric_type);
-            std::vector<float> row(f->d);
-            for (faiss::idx_t i = 0; i < f->ntotal; ++i) {
-                f->reconstruct(i, row.data());
-                cpu->add(1, row.data());
+        if (auto *v = dynamic_cast<HipIndexIVFFlat *>(gpu_index)) {
+            // index_metal_to_cpu_ivf (MetalIndexIVFFlat.mm:328-356) from the HBM lists
+            const int nlist = (int)v->nlist(), d = (int)v->d;
+            char err[512] = {0};
+            std::vector<int64_t> off(nlist + 1);
+            check(hipann_ivf_export(v->handle(), nullptr, off.data(), nullptr, nullptr, err, sizeof err), err);
+            std::vector<float> cen((size_t)nlist * d), codes((size_t)off[nlist] * d);
+            std::vector<int64_t> ids((size_t)off[nlist]);
+            check(hipann_ivf_export(v->handle(), cen.data(), off.data(), ids.data(), codes.data(), err, sizeof err), err);
+            auto *quantizer = new faiss::IndexFlat(d, v->metric_type);
+            quantizer->add(nlist, cen.data());
+            auto cpu = std::make_unique<faiss::IndexIVFFlat>(quantizer, d, nlist, v->metric_type);
+            cpu->own_fields = true;
+            cpu->is_trained = true;
+            cpu->nprobe = v->nprobe();
+            for (int l = 0; l < nlist; ++l) {
+                const size_t len = (size_t)(off[l + 1] - off[l]);
+                if (!len) continue;
+                cpu->invlists->add_entries(l, len, reinterpret_cast<const faiss::idx_t *>(ids.data() + off[l]),
+                                           reinterpret_cast<const uint8_t *>(codes.data() + (size_t)off[l] * d));
             }
+            cpu->ntotal = off[nlist];
             return cpu;
         }
-        throw std::runtime_error("Index is not a HIP Flat index -- keep the CPU index authoritative");
+        if (auto *f = dynamic_cast<HipIndexFlat *>(gpu_index)) {  // index_metal_to_cpu
+            auto cpu = std::make_unique<faiss::IndexFlat>(f->d, f->metric_type);
+            std::vector<float> xb((size_t)f->ntotal * f->d);
+            char err[512] = {0};
+            check(hipann_flat_reconstruct_n(f->handle(), 0, f->ntotal, xb.data(), err, sizeof err), err);
+            cpu->add(f->ntotal, xb.data());
+            return cpu;
+        }
+        throw std::runtime_error("Index is not a HIP index -- cannot convert to CPU");
     }
 };
 

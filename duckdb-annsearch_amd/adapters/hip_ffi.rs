@@ -1,7 +1,15 @@
 //! FFI bridge to MI355X batch distance computation — drop-in replacement of
-//! rust_lib/src/metal_ffi.rs (same public API, so disk_provider.rs / provider.rs only change their
-//! `use crate::metal_ffi` to `use crate::hip_ffi`, or keep metal_ffi.rs unchanged and link
-//! libhipann.so, which also exports the `diskann_metal_*` names).
+//! rust_lib/src/metal_ffi.rs.  The callers name the module by full path
+//! (`crate::metal_ffi::MIN_GPU_WORK`, `crate::metal_ffi::metal_batch_distances`,
+//! `crate::metal_ffi::metal_multi_batch_distances`: disk_provider.rs:417, :427, :590, :601;
+//! provider.rs:385, :396), so the swap is one line in rust_lib/src/lib.rs:6:
+//!
+//!     #[path = "hip_ffi.rs"] pub mod metal_ffi;
+//!
+//! and this module exports the reference names (`is_metal_available`, `metal_batch_distances`,
+//! `metal_multi_batch_distances`, `MIN_GPU_WORK`, `MIN_GPU_WORK_ONESHOT`) next to the `hip_*` ones.
+//! (Alternatively keep metal_ffi.rs unchanged and link libhipann.so, which also exports the
+//! `diskann_metal_*` C names.)
 //!
 //! The implementation lives in libhipann.so (duckdb-annsearch_amd/csrc/diskann.hip); its C ABI is
 //! include/hip_diskann_bridge.h.  Symbols are resolved at link time when the Rust static lib is
@@ -64,6 +72,12 @@ pub const MIN_GPU_WORK: usize = 131072;
 
 /// One-shot threshold for vector_distances() (ann_search.cpp:699).
 pub const MIN_GPU_WORK_ONESHOT: usize = 49152;
+
+/// Reference names (metal_ffi.rs:49, :67, :107): with `#[path = "hip_ffi.rs"] pub mod metal_ffi;` the
+/// callers in disk_provider.rs / provider.rs resolve unchanged.
+pub use self::hip_batch_distances as metal_batch_distances;
+pub use self::hip_multi_batch_distances as metal_multi_batch_distances;
+pub use self::is_hip_available as is_metal_available;
 
 pub fn is_hip_available() -> bool {
     let status = HIP_STATUS.load(Ordering::Relaxed);

@@ -870,7 +870,11 @@ merge_parts_topk(const float *__restrict__ pd, const InId *__restrict__ pi, int 
             const int64_t off = (p * nq + q) * k + i;
             const InId raw = pi[off];
             const float v = pd[off] * in_sign;
-            if (raw >= 0 && raw != (InId)0x7fffffff && !(v == __builtin_inff())) {
+            // int32 partials pad with 0x7fffffff; int64 (global label) partials only with negatives, so a
+            // real label 2^31 - 1 (arbitrary IVF ids, > 2^31 rows) is kept
+            bool pad_in = raw < 0;
+            if constexpr (sizeof(InId) == 4) pad_in = pad_in || raw == (InId)0x7fffffff;
+            if (!pad_in && !(v == __builtin_inff())) {
                 key = v;
                 lab = (long long)raw + label_offset;
             }

@@ -510,6 +510,27 @@ int hipann_flat_reconstruct(void *h, int64_t key, float *out, char *eb, int el) 
     });
 }
 
+int hipann_flat_reconstruct_n(void *h, int64_t i0, int64_t n, float *out, char *eb, int el) {
+    return guard_int(eb, el, [&]() -> int {
+        HIPANN_REQUIRE(h && (n == 0 || out), "null argument");
+        auto *ix = static_cast<IndexBase *>(h);
+        HIPANN_REQUIRE(ix->kind == Kind::Flat, "not a Flat index");
+        auto *fx = static_cast<FlatIndex *>(ix);
+        std::lock_guard<std::mutex> lk(fx->mu);
+        HIPANN_REQUIRE(i0 >= 0 && n >= 0 && i0 + n <= fx->ntotal(), "hipann: reconstruct_n range out of bounds");
+        for (auto &shp : fx->shards) {  // shards hold contiguous label ranges
+            FlatShard &sh = *shp;
+            const int64_t lo = std::max(i0, sh.label_offset), hi = std::min(i0 + n, sh.label_offset + sh.n);
+            if (lo >= hi) continue;
+            DeviceGuard g(sh.device);
+            HIPANN_CHECK(hipMemcpyAsync(out + (lo - i0) * fx->d, sh.xb + (lo - sh.label_offset) * fx->d,
+                                        sizeof(float) * (size_t)(hi - lo) * fx->d, hipMemcpyDeviceToHost, sh.stream));
+            HIPANN_CHECK(hipStreamSynchronize(sh.stream));
+        }
+        return 0;
+    });
+}
+
 void *hipann_flat_create_device(int d, int metric, const float *xb_dev, int64_t n, int device, int copy,
                                 int64_t label_offset, char *eb, int el) {
     return guard_ptr(eb, el, [&]() -> void * {

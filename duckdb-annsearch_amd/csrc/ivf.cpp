@@ -278,6 +278,105 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     HIPANN_CHECK(hipMemcpyAsync(sh.coarse_i.p, sh.coarse_save.p, pbytes, hipMemcpyDeviceToDevice, st));
 }
 
+
+// IndexIVF::add_with_ids (FAISS 1.13.2, external): rows are assigned to their nearest centroid by the
+// coarse quantizer (quantizer->assign, k = 1, in blocks of 65536 rows — so the Flat nq < 20 direct-form
+// rule applies per block) and appended to their lists in insertion order; labels are `ids` or
+// ntotal + i.  On the GPU copy this replaces the reference's invalidate-on-append
+// (faiss_index.cpp:469): the HBM lists are rebuilt per shard with the new rows in place.
+static void ivf_add_rows(IvfIndex &ix, int64_t n, const float *xb, const int64_t *ids) {
+    const int d = ix.d, nlist = ix.nlist;
+    IvfShard &s0 = *ix.shards[0];
+    DeviceGuard g0(s0.device);
+    hipStream_t st = s0.stream;
+    const int64_t base = ix.ntotal();
+    // 1. assignment on the GPU (shard 0's quantizer; every shard holds all centroids)
+    std::vector<int64_t> assign((size_t)n);
+    const int64_t bs = 65536;
+    DevBuf rows, dd, ii;
+    rows.ensure(sizeof(float) * (size_t)std::min(n, bs) * d, s0.device);
+    dd.ensure(sizeof(float) * (size_t)std::min(n, bs), s0.device);
+    ii.ensure(sizeof(int64_t) * (size_t)std::min(n, bs), s0.device);
+    for (int64_t r0 = 0; r0 < n; r0 += bs) {
+        const int64_t m = std::min(bs, n - r0);
+        HIPANN_CHECK(hipMemcpyAsync(rows.p, xb + r0 * d, sizeof(float) * (size_t)m * d, hipMemcpyHostToDevice, st));
+        flat_shard_search(*s0.quant, *s0.quant->shards[0], m, rows.get<float>(), 1, 1, dd.get<float>(),
+                          ii.get<int64_t>(), st);
+        HIPANN_CHECK(hipMemcpyAsync(assign.data() + r0, ii.p, sizeof(int64_t) * (size_t)m, hipMemcpyDeviceToHost, st));
+    }
+    HIPANN_CHECK(hipStreamSynchronize(st));
+    rows.release();
+    // 2. per list, the new rows in insertion order (stable counting sort)
+    std::vector<int64_t> cnt(nlist + 1, 0);
+    for (int64_t i = 0; i < n; ++i) {
+        HIPANN_REQUIRE(assign[i] >= 0 && assign[i] < nlist, "coarse assignment out of range");
+        ++cnt[assign[i] + 1];
+    }
+    std::vector<int64_t> noff(nlist + 1, 0);  // offsets of the new rows, grouped by list
+    for (int l = 0; l < nlist; ++l) noff[l + 1] = noff[l] + cnt[l + 1];
+    std::vector<int64_t> perm((size_t)n), cur(noff.begin(), noff.end() - 1);
+    for (int64_t i = 0; i < n; ++i) perm[cur[assign[i]]++] = i;
+    HostBuf hc, hi;
+    hc.ensure(sizeof(float) * (size_t)n * d);
+    hi.ensure(sizeof(int64_t) * (size_t)n);
+    for (int64_t j = 0; j < n; ++j) {
+        std::memcpy(hc.get<float>() + j * d, xb + perm[j] * d, sizeof(float) * d);
+        hi.get<int64_t>()[j] = ids ? ids[perm[j]] : base + perm[j];
+    }
+    // 3. rebuild each shard that owns a list with new rows
+    for (size_t s = 0; s < ix.shards.size(); ++s) {
+        IvfShard &sh = *ix.shards[s];
+        int64_t add_s = 0;
+        for (int l = 0; l < nlist; ++l)
+            if (ix.owner[l] == (int)s) add_s += cnt[l + 1];
+        if (!add_s) continue;
+        DeviceGuard g(sh.device);
+        std::vector<int64_t> off(nlist + 1, 0);
+        for (int l = 0; l < nlist; ++l)
+            off[l + 1] = off[l] + (sh.h_off[l + 1] - sh.h_off[l]) + (ix.owner[l] == (int)s ? cnt[l + 1] : 0);
+        const int64_t n_new = off[nlist];
+        DevBuf stage_c, stage_i, codes_nb, ids_nb;
+        stage_c.ensure(sizeof(float) * (size_t)n * d, sh.device);
+        stage_i.ensure(sizeof(int64_t) * (size_t)n, sh.device);
+        HIPANN_CHECK(hipMemcpyAsync(stage_c.p, hc.p, sizeof(float) * (size_t)n * d, hipMemcpyHostToDevice, sh.stream));
+        HIPANN_CHECK(hipMemcpyAsync(stage_i.p, hi.p, sizeof(int64_t) * (size_t)n, hipMemcpyHostToDevice, sh.stream));
+        codes_nb.ensure(sizeof(float) * (size_t)n_new * d, sh.device);
+        ids_nb.ensure(sizeof(int64_t) * (size_t)n_new, sh.device);
+        for (int l = 0; l < nlist; ++l) {
+            const int64_t old_len = sh.h_off[l + 1] - sh.h_off[l];
+            if (old_len) {
+                HIPANN_CHECK(hipMemcpyAsync(codes_nb.get<float>() + off[l] * d, sh.codes + sh.h_off[l] * d,
+                                            sizeof(float) * (size_t)old_len * d, hipMemcpyDeviceToDevice, sh.stream));
+                HIPANN_CHECK(hipMemcpyAsync(ids_nb.get<int64_t>() + off[l], sh.ids + sh.h_off[l],
+                                            sizeof(int64_t) * (size_t)old_len, hipMemcpyDeviceToDevice, sh.stream));
+            }
+            const int64_t add_l = ix.owner[l] == (int)s ? cnt[l + 1] : 0;
+            if (add_l) {
+                HIPANN_CHECK(hipMemcpyAsync(codes_nb.get<float>() + (off[l] + old_len) * d,
+                                            stage_c.get<float>() + noff[l] * d, sizeof(float) * (size_t)add_l * d,
+                                            hipMemcpyDeviceToDevice, sh.stream));
+                HIPANN_CHECK(hipMemcpyAsync(ids_nb.get<int64_t>() + off[l] + old_len, stage_i.get<int64_t>() + noff[l],
+                                            sizeof(int64_t) * (size_t)add_l, hipMemcpyDeviceToDevice, sh.stream));
+            }
+        }
+        HIPANN_CHECK(hipStreamSynchronize(sh.stream));
+        std::swap(sh.codes_buf.p, codes_nb.p);
+        std::swap(sh.codes_buf.bytes, codes_nb.bytes);
+        std::swap(sh.codes_buf.device, codes_nb.device);
+        std::swap(sh.ids_buf.p, ids_nb.p);
+        std::swap(sh.ids_buf.bytes, ids_nb.bytes);
+        std::swap(sh.ids_buf.device, ids_nb.device);
+        sh.codes = sh.codes_buf.get<float>();  // borrowed storage becomes owned here
+        sh.ids = sh.ids_buf.get<int64_t>();
+        sh.n = n_new;
+        upload_list_meta(sh, off, nlist);
+        compute_row_norms(sh, d, ix.metric);
+        sh.codes_t.release();  // the MFMA scan's tiled copy is rebuilt at the next search
+        sh.tpass_off.release();
+        sh.xmax2 = -1.f;
+    }
+}
+
 }  // namespace hipann
 
 extern "C" {
@@ -528,6 +627,72 @@ int hipann_ivf_search_device(void *h, int64_t nq, const float *xq_dev, int64_t k
         vx->last_np = std::min(vx->nprobe, vx->nlist);
         const int keff = (int)std::min<int64_t>(k, std::max<int64_t>(sh.n, 1));
         ivf_shard_search(*vx, sh, nq, xq_dev, keff, (int)k, D_dev, I_dev, st);
+        return 0;
+    });
+}
+
+int hipann_ivf_add(void *h, int64_t n, const float *xb, const int64_t *ids, char *eb, int el) {
+    return guard_int(eb, el, [&]() -> int {
+        HIPANN_REQUIRE(h, "null index");
+        auto *ix = static_cast<IndexBase *>(h);
+        HIPANN_REQUIRE(ix->kind == Kind::IVF, "not an IVFFlat index");
+        auto *vx = static_cast<IvfIndex *>(ix);
+        std::lock_guard<std::mutex> lk(vx->mu);
+        HIPANN_REQUIRE(n >= 0 && (n == 0 || xb), "invalid vectors");
+        if (n > 0) ivf_add_rows(*vx, n, xb, ids);
+        return 0;
+    });
+}
+
+int hipann_ivf_nlist(void *h) {
+    if (!h || static_cast<IndexBase *>(h)->kind != Kind::IVF) return -1;
+    return static_cast<IvfIndex *>(h)->nlist;
+}
+
+int hipann_ivf_get_nprobe(void *h) {
+    if (!h || static_cast<IndexBase *>(h)->kind != Kind::IVF) return -1;
+    auto *vx = static_cast<IvfIndex *>(h);
+    std::lock_guard<std::mutex> lk(vx->mu);
+    return vx->nprobe;
+}
+
+int hipann_ivf_export(void *h, float *centroids, int64_t *list_offsets, int64_t *ids, float *codes, char *eb, int el) {
+    return guard_int(eb, el, [&]() -> int {
+        HIPANN_REQUIRE(h, "null index");
+        auto *ix = static_cast<IndexBase *>(h);
+        HIPANN_REQUIRE(ix->kind == Kind::IVF, "not an IVFFlat index");
+        auto *vx = static_cast<IvfIndex *>(ix);
+        std::lock_guard<std::mutex> lk(vx->mu);
+        const int nlist = vx->nlist, d = vx->d;
+        std::vector<int64_t> off(nlist + 1, 0);
+        for (int l = 0; l < nlist; ++l) {
+            const IvfShard &sh = *vx->shards[vx->owner[l]];
+            off[l + 1] = off[l] + (sh.h_off[l + 1] - sh.h_off[l]);
+        }
+        if (list_offsets) std::memcpy(list_offsets, off.data(), sizeof(int64_t) * (nlist + 1));
+        IvfShard &s0 = *vx->shards[0];
+        if (centroids) {
+            DeviceGuard g(s0.device);
+            HIPANN_CHECK(hipMemcpyAsync(centroids, s0.centroids, sizeof(float) * (size_t)nlist * d, hipMemcpyDeviceToHost,
+                                        s0.stream));
+            HIPANN_CHECK(hipStreamSynchronize(s0.stream));
+        }
+        for (int l = 0; l < nlist && (ids || codes); ++l) {
+            IvfShard &sh = *vx->shards[vx->owner[l]];
+            const int64_t len = off[l + 1] - off[l];
+            if (!len) continue;
+            DeviceGuard g(sh.device);
+            if (codes)
+                HIPANN_CHECK(hipMemcpyAsync(codes + off[l] * d, sh.codes + sh.h_off[l] * d, sizeof(float) * (size_t)len * d,
+                                            hipMemcpyDeviceToHost, sh.stream));
+            if (ids)
+                HIPANN_CHECK(hipMemcpyAsync(ids + off[l], sh.ids + sh.h_off[l], sizeof(int64_t) * (size_t)len,
+                                            hipMemcpyDeviceToHost, sh.stream));
+        }
+        for (auto &shp : vx->shards) {
+            DeviceGuard g(shp->device);
+            HIPANN_CHECK(hipStreamSynchronize(shp->stream));
+        }
         return 0;
     });
 }

@@ -33,7 +33,8 @@ METRIC_L2 = 0
 METRIC_INNER_PRODUCT = 1
 MAX_K = 2048
 
-# rust_lib/src/metal_ffi.rs:41, :46 — gates for the DiskANN bridge, re-tuned for MI355X.
+# rust_lib/src/metal_ffi.rs:41, :46 — gates for the DiskANN bridge (the reference's Metal values until the
+# MI355X break-even measured by tools/bench_batch_distances.py replaces them).
 MIN_GPU_WORK = 131072
 MIN_GPU_WORK_ONESHOT = 49152
 
@@ -98,6 +99,12 @@ def lib() -> C.CDLL:
             "hipann_ivf_search_device": ([vp, i64, vp, i64, vp, vp, vp, cp, i32], i32),
             "hipann_ivf_last_probes": ([vp, i64p, i64, cp, i32], i32),
             "hipann_ivf_set_nprobe": ([vp, i32], i32),
+            "hipann_ivf_get_nprobe": ([vp], i32),
+            "hipann_ivf_nlist": ([vp], i32),
+            "hipann_ivf_search_np": ([vp, i32, i64, f, i64, f, i64p, cp, i32], i32),
+            "hipann_ivf_add": ([vp, i64, f, i64p, cp, i32], i32),
+            "hipann_ivf_export": ([vp, f, i64p, i64p, f, cp, i32], i32),
+            "hipann_flat_reconstruct_n": ([vp, i64, i64, f, cp, i32], i32),
             "hipann_ivf_set_form": ([vp, i32], i32),
             "hipann_ivf_get_form": ([vp], i32),
             "hipann_ivf_rerank_fallbacks": ([vp], i64),
@@ -271,6 +278,13 @@ class HipIndexFlat(_FlatForm, _Handle):
                                         eb, 1024), eb)
         return D, I
 
+    def reconstruct_n(self, i0: int, n: int) -> np.ndarray:
+        """faiss::Index::reconstruct_n: rows [i0, i0 + n) back to host in one call."""
+        out = np.empty((max(n, 0), self.d), np.float32)
+        eb = _err()
+        _check(lib().hipann_flat_reconstruct_n(self._h, i0, n, _ptr(out, C.c_float), eb, 1024), eb)
+        return out
+
     def reconstruct(self, key: int) -> np.ndarray:
         out = np.empty(self.d, np.float32)
         eb = _err()
@@ -374,15 +388,49 @@ class HipIndexIVFFlat(_Handle):
             raise HipAnnError("form must be 0 (decomposed), 1 (direct), 2 (decomposed, VALU), 3 or 4 (split bf16), "
                               "5 (split bf16 + exact rerank)")
 
-    def search(self, x, k: int) -> Tuple[np.ndarray, np.ndarray]:
+    def search(self, x, k: int, nprobe: Optional[int] = None) -> Tuple[np.ndarray, np.ndarray]:
+        """search(n, x, k) — with ``nprobe`` the per-call SearchParametersIVF value (hipann_ivf_search_np:
+        read under the handle's lock, the index's own nprobe is left unchanged)."""
         x = _f32_2d(x, self.d)
         n = x.shape[0]
         D = np.empty((n, max(k, 0)), np.float32)
         I = np.empty((n, max(k, 0)), np.int64)
         eb = _err()
-        _check(lib().hipann_ivf_search(self._h, n, _ptr(x, C.c_float), k, _ptr(D, C.c_float), _ptr(I, C.c_int64),
-                                       eb, 1024), eb)
+        if nprobe is None:
+            rc = lib().hipann_ivf_search(self._h, n, _ptr(x, C.c_float), k, _ptr(D, C.c_float), _ptr(I, C.c_int64),
+                                         eb, 1024)
+        else:
+            if int(nprobe) < 1:
+                raise HipAnnError("nprobe must be >= 1")
+            rc = lib().hipann_ivf_search_np(self._h, int(nprobe), n, _ptr(x, C.c_float), k, _ptr(D, C.c_float),
+                                            _ptr(I, C.c_int64), eb, 1024)
+        _check(rc, eb)
         return D, I
+
+    def add(self, x, ids=None) -> None:
+        """IndexIVFFlat::add / add_with_ids on the GPU copy (hipann_ivf_add): rows assigned by the GPU
+        coarse quantizer, appended to their lists in insertion order; labels ``ids`` or ntotal + i."""
+        x = _f32_2d(x, self.d)
+        idv = None if ids is None else np.ascontiguousarray(ids, np.int64)
+        if idv is not None and idv.shape != (x.shape[0],):
+            raise ValueError("ids must hold one label per row")
+        eb = _err()
+        _check(lib().hipann_ivf_add(self._h, x.shape[0], _ptr(x, C.c_float), _ptr(idv, C.c_int64), eb, 1024), eb)
+
+    def export(self) -> dict:
+        """The index in FAISS ArrayInvertedLists CSR form (hipann_ivf_export): centroids, list_offsets,
+        ids, codes, nprobe, metric — what GpuToCpu rebuilds a CPU IndexIVFFlat from."""
+        off = np.empty(self.nlist + 1, np.int64)
+        eb = _err()
+        _check(lib().hipann_ivf_export(self._h, None, _ptr(off, C.c_int64), None, None, eb, 1024), eb)
+        n = int(off[-1])
+        cen = np.empty((self.nlist, self.d), np.float32)
+        ids = np.empty(n, np.int64)
+        codes = np.empty((n, self.d), np.float32)
+        _check(lib().hipann_ivf_export(self._h, _ptr(cen, C.c_float), _ptr(off, C.c_int64), _ptr(ids, C.c_int64),
+                                       _ptr(codes, C.c_float), eb, 1024), eb)
+        return {"type": "IVFFlat", "centroids": cen, "list_offsets": off, "ids": ids, "codes": codes,
+                "nprobe": int(lib().hipann_ivf_get_nprobe(self._h)), "metric": self.metric_type}
 
     def search_device(self, nq: int, xq_ptr: int, k: int, d_ptr: int, i_ptr: int, stream: int = 0) -> None:
         eb = _err()
@@ -441,9 +489,10 @@ class GpuBackend:
 
     def gpu_to_cpu(self, gpu_index) -> dict:
         if isinstance(gpu_index, HipIndexFlat):
-            xb = np.stack([gpu_index.reconstruct(i) for i in range(gpu_index.ntotal)]) if gpu_index.ntotal else \
-                np.zeros((0, gpu_index.d), np.float32)
-            return {"type": "Flat", "d": gpu_index.d, "metric": gpu_index.metric_type, "xb": xb}
+            return {"type": "Flat", "d": gpu_index.d, "metric": gpu_index.metric_type,
+                    "xb": gpu_index.reconstruct_n(0, gpu_index.ntotal)}
+        if isinstance(gpu_index, HipIndexIVFFlat):  # gpu_backend_metal.mm:62-67 (index_metal_to_cpu_ivf)
+            return gpu_index.export()
         raise RuntimeError("Index is not a HIP index -- cannot convert to CPU")
 
 

@@ -72,6 +72,10 @@ int hipann_flat_search(void *index, int64_t nq, const float *xq, int64_t k, floa
 /* Copy vector `key` back to host (faiss::Index::reconstruct; MetalIndexFlat::reconstruct). */
 int hipann_flat_reconstruct(void *index, int64_t key, float *out, char *err_buf, int err_len);
 
+/* Copy rows [i0, i0+n) back to host (faiss::Index::reconstruct_n; GpuToCpu of a Flat index,
+ * gpu_backend_metal.mm:68-72 → index_metal_to_cpu). */
+int hipann_flat_reconstruct_n(void *index, int64_t i0, int64_t n, float *out, char *err_buf, int err_len);
+
 /* q·x form of the batched (nq >= 20, FAISS's BLAS threshold) distance path, ‖q‖² + ‖x‖² − 2·q·x.
  * HIPANN_FLAT_FORM_FP32: exact fp32 products on the fp32 matrix cores (v_mfma_f32_32x32x2_f32).
  * HIPANN_FLAT_FORM_SPLIT3: both operands split into three round-to-nearest bf16 terms, the
@@ -133,6 +137,12 @@ void *hipann_ivf_create_device(int d, int metric, int nlist, int nprobe, const f
 int hipann_ivf_search(void *index, int64_t nq, const float *xq, int64_t k, float *D, int64_t *I,
                       char *err_buf, int err_len);
 
+/* Search with a per-call nprobe (SearchParametersIVF::nprobe, faiss_index.cpp:720-726); nprobe <= 0 uses
+ * the index's.  The value is read under the handle's lock, so concurrent callers with different nprobe
+ * never see each other's (the race of a set_nprobe + search pair). */
+int hipann_ivf_search_np(void *index, int nprobe, int64_t nq, const float *xq, int64_t k, float *D, int64_t *I,
+                         char *err_buf, int err_len);
+
 int hipann_ivf_search_device(void *index, int64_t nq, const float *xq_dev, int64_t k, float *D_dev,
                              int64_t *I_dev, void *stream, char *err_buf, int err_len);
 
@@ -140,6 +150,22 @@ int hipann_ivf_search_device(void *index, int64_t nq, const float *xq_dev, int64
 int hipann_ivf_last_probes(void *index, int64_t *probes, int64_t cap, char *err_buf, int err_len);
 
 int hipann_ivf_set_nprobe(void *index, int nprobe);
+int hipann_ivf_get_nprobe(void *index);
+int hipann_ivf_nlist(void *index);
+
+/* IndexIVFFlat::add_with_ids on the GPU copy (FAISS 1.13.2 IndexIVF::add_with_ids / add_core): the n rows
+ * `xb` (host, n*d fp32) are assigned to their nearest centroid by the GPU coarse quantizer (k = 1, blocks
+ * of 65536 rows as FAISS assigns them) and appended to their lists in insertion order, labels `ids`
+ * (NULL: ntotal + i).  Replaces the reference's invalidate-on-append (faiss_index.cpp:469). */
+int hipann_ivf_add(void *index, int64_t n, const float *xb, const int64_t *ids, char *err_buf, int err_len);
+
+/* Copy the index back to host in FAISS's ArrayInvertedLists CSR form — the inverse of hipann_ivf_create
+ * (GpuBackend::GpuToCpu, gpu_backend_metal.mm:62-67 → index_metal_to_cpu_ivf, MetalIndexIVFFlat.mm:328-356):
+ * centroids (nlist*d), list_offsets (nlist+1), ids (ntotal) and codes (ntotal*d, raw fp32 rows), lists in
+ * order, rows in list order.  Any output may be NULL (skipped); size ids/codes from list_offsets[nlist]
+ * (call once with only list_offsets first). */
+int hipann_ivf_export(void *index, float *centroids, int64_t *list_offsets, int64_t *ids, float *codes,
+                      char *err_buf, int err_len);
 
 /* List-scan distance form.  HIPANN_IVF_FORM_DECOMPOSED: ‖q‖² + ‖x‖² − 2·q·x clamped ≥ 0
  * (IP: q·x), with ‖x‖² stored per row — the form faiss-metal's IVF path and FAISS's GPU IVFFlat use

@@ -283,3 +283,85 @@ def test_ivf_exact_form_fallback_on_ties(gpu, oracle):
     Do, Io, Po = oracle.ivf_search(cen, off, ids, codes, xq, 10, 4, 0)
     assert np.array_equal(ix.last_probes(40), Po)
     check_topk_parity(xb, xq, D, I, Do, Io, 0)
+
+
+@pytest.mark.parametrize("devices", [None, [0, 0]])
+def test_ivf_add_on_gpu_copy(gpu, oracle, devices):
+    """IndexIVFFlat::add_with_ids on the GPU copy (hipann_ivf_add): appended rows land in their nearest
+    centroid's list after the existing rows (insertion order), labels given or ntotal + i; the exported
+    lists equal the oracle's assignment of all rows, and search keeps parity."""
+    xb, xq = faiss_metal_case(9000, 30, 48)
+    cen = np.ascontiguousarray(xb[::300][:30])
+    n1 = 5000
+    off1, ids1, codes1 = build_ivf_lists(xb[:n1], cen)
+    ix = gpu.HipIndexIVFFlat(cen, off1, ids1, codes1, 6, devices=devices)
+    ix.search(xq, 10)  # builds the scan's tiled copy, which the add must invalidate
+    ix.add(xb[n1:8000])                      # labels ntotal + i
+    ix.add(xb[8000:8010])                    # < 20 rows: FAISS assigns with the direct form
+    ix.add(xb[8010:], ids=np.arange(8010, 9000, dtype=np.int64))
+    assert ix.ntotal == 9000
+    ex = ix.export()
+    off, ids, codes = build_ivf_lists(xb, cen)
+    assert np.array_equal(ex["list_offsets"], off)
+    assert np.array_equal(ex["ids"], ids) and np.array_equal(ex["codes"], codes)
+    assert np.array_equal(ex["centroids"], cen)
+    D, I = ix.search(xq, 10)
+    Do, Io, Po = oracle.ivf_search(cen, off, ids, codes, xq, 10, 6)
+    assert np.array_equal(ix.last_probes(30), Po)
+    check_topk_parity(xb, xq, D, I, Do, Io)
+
+
+def test_ivf_search_per_call_nprobe_threads(gpu, oracle):
+    """hipann_ivf_search_np: concurrent searches with different nprobe on one handle (two DuckDB
+    connections with different SearchParametersIVF) each get their own nprobe; the index's own nprobe
+    is unchanged."""
+    import threading
+    xb, xq = faiss_metal_case(8000, 40, 32)
+    ix, (cen, off, ids, codes) = _ivf(gpu, xb, 40, 2)
+    ref = {np_: oracle.ivf_search(cen, off, ids, codes, xq, 10, np_)[1] for np_ in (1, 3, 9, 40)}
+    errors = []
+
+    def run(np_):
+        for _ in range(5):
+            _, I = ix.search(xq, 10, nprobe=np_)
+            if not np.array_equal(I, ref[np_]):
+                errors.append(np_)
+
+    ts = [threading.Thread(target=run, args=(p,)) for p in (1, 3, 9, 40) for _ in range(2)]
+    [t.start() for t in ts]
+    [t.join() for t in ts]
+    assert not errors
+    assert ix.nprobe == 2 and gpu.lib().hipann_ivf_get_nprobe(ix._h) == 2
+
+
+def test_ivf_gpu_to_cpu_round_trip(gpu, oracle):
+    """GpuBackend::GpuToCpu for IVFFlat (gpu_backend_metal.mm:62-67): the exported CPU index equals the
+    one converted in, and converting it back searches identically."""
+    be = gpu.get_gpu_backend()
+    xb, xq = faiss_metal_case(6000, 25, 40)
+    cen = np.ascontiguousarray(xb[::200][:30])
+    off, ids, codes = build_ivf_lists(xb, cen)
+    cpu = {"type": "IVFFlat", "centroids": cen, "list_offsets": off, "ids": ids * 3 + 11, "codes": codes,
+           "nprobe": 5, "metric": 0}
+    g = be.cpu_to_gpu(cpu)
+    back = be.gpu_to_cpu(g)
+    for key in ("centroids", "list_offsets", "ids", "codes"):
+        assert np.array_equal(back[key], cpu[key]), key
+    assert back["nprobe"] == 5 and back["metric"] == 0 and back["type"] == "IVFFlat"
+    g2 = be.cpu_to_gpu(back)
+    assert all(np.array_equal(a, b) for a, b in zip(g.search(xq, 10), g2.search(xq, 10)))
+
+
+def test_ivf_label_int32_max_survives_multi_shard_merge(gpu, oracle):
+    """Labels around 2^31 − 1 through the multi-shard int64 merge (merge_parts_topk<long long>): the int32
+    partials' pad value must not drop a real int64 label 2147483647."""
+    xb, xq = faiss_metal_case(3000, 12, 32)
+    cen = np.ascontiguousarray(xb[::300][:10])
+    off, ids, codes = build_ivf_lists(xb, cen)
+    labels = ids + (2**31 - 1) - ids[np.argmin(np.abs(ids - 100))]  # some row carries exactly 2^31 - 1
+    ix = gpu.HipIndexIVFFlat(cen, off, labels, codes, 10, devices=[0, 0])
+    q = np.vstack([codes[np.nonzero(labels == 2**31 - 1)[0]], xq])
+    D, I = ix.search(q, 5)
+    Do, Io, _ = oracle.ivf_search(cen, off, labels, codes, q, 5, 10)
+    assert I[0, 0] == 2**31 - 1
+    assert np.array_equal(I, Io)
