@@ -3,16 +3,23 @@
 
 Metric (BASELINE.json): queries/s at recall@10 >= 0.95 on synthetic 10M x 768 fp32, batch = 1024
 queries, at 1/2/4/8 GPUs.  A "step" = one search of the 1024-query batch against the whole
-database (inputs already resident in HBM when the timed region starts).
+database (inputs already resident in HBM when the timed region starts; the PCIe-inclusive rate of
+the host-pointer API is reported beside it as ``with_h2d_d2h``, never as ``value``).
 
 Workloads (--workload):
-  flat  FAISS Flat L2 over 10M x 768 (exact: recall 1.0).  Rows are sharded contiguously over the
-        ranks (strong scaling: the 10M database is fixed, each GPU holds 10M/N rows), every rank
-        searches its shard (fp32 MFMA GEMM + fused top-k), the per-rank top-k (1024 x 10 x 12 B) is
-        all-gathered over RCCL and merged on every rank.
-  ivf   FAISS IVFFlat nlist=1024 nprobe=32 over the same 10M x 768 shape, clustered synthetic data
-        (the default workload: the fastest configuration meeting recall@10 >= 0.95); lists are
-        sharded over the ranks, same allgather + merge.
+  ivf   (default) FAISS IVFFlat nlist=1024 nprobe=32 over 10M x 768 (BASELINE configs[2], C3): the
+        fastest configuration meeting recall@10 >= 0.95.  N GPUs: whole lists dealt to ranks by size
+        (strong scaling), every rank scans the probed lists it owns, one packed all-gather of the
+        per-rank top-k over RCCL + merge.
+  flat  FAISS Flat L2 over 10M x 768 (exact: recall 1.0), rows sharded contiguously over the ranks.
+  diskann  DiskProvider batch path, 1M x 1536 SQ8, L_search=128 (C4); replicas (weak scaling).
+
+At N = 1 the default line also carries, from the same run, every other BASELINE configuration as a
+sub-object of ``configs`` (each with its own roofline and CPU baseline): C1 (Flat 10k x 128, the CPU
+path), C2 (Flat L2 1M x 768), Flat L2 10M x 768, C4 (DiskANN), the extension's real call shape
+(nq = 1 / 4 latency, Flat and IVF), the reference's published batch-distance microbenchmark shapes
+(README.md:140-147) with the MIN_GPU_WORK break-even, and the IVF recall/nprobe sweep at intrinsic
+ranks 16/24/32.  --no-suite skips them.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]  (N>1 under torch.distributed.run).
 """
@@ -34,6 +41,7 @@ sys.path.insert(0, str(ROOT))
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 FP32_MFMA_PEAK_TF = 157.3  # MI355X_MICROARCH.md: fp32 MFMA = fp32 vector peak
 BF16_MFMA_PEAK_TF = 16 * FP32_MFMA_PEAK_TF  # dense bf16 MFMA = 16x the fp32 matrix rate (~2.5 PF)
+METRIC = "queries/sec @ recall@10>=0.95, 10Mx768 fp32, batch=1024"
 
 
 def log(*a):
@@ -61,53 +69,57 @@ def parse():
     p.add_argument("--metric", choices=["l2", "ip"], default="l2")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-alt-forms", action="store_true", help="ivf/flat: skip timing the other distance forms")
-    p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU sample duration")
+    p.add_argument("--suite", dest="suite", action="store_true", default=None,
+                   help="N=1: add the other BASELINE configurations as sub-objects (default for --workload ivf)")
+    p.add_argument("--no-suite", dest="suite", action="store_false")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU sample duration (main line)")
     a = p.parse_args()
     if a.n is None:
         a.n = 1_000_000 if a.workload == "diskann" else 10_000_000
     if a.d is None:
         a.d = 1536 if a.workload == "diskann" else 768
+    if a.suite is None:
+        a.suite = a.workload == "ivf"
     return a
 
 
+# ------------------------------------------------------------------------------------------------
+# synthetic data (generated on the device, chunk-seeded so every sharding sees the same matrix)
+# ------------------------------------------------------------------------------------------------
 CHUNK = 125_000  # generation granularity (divides 10M / {1,2,4,8})
 
 
-def gen_uniform_rows(torch, out, row0, seed):
-    """Fill `out` (rows [row0, row0+len)) with U(-1,1) fp32, chunk-seeded so every sharding sees the
-    same global matrix."""
-    n = out.shape[0]
+def _chunks(n, row0):
     r = 0
     while r < n:
         g_row = row0 + r
         chunk = g_row // CHUNK
         off = g_row - chunk * CHUNK
         take = min(CHUNK - off, n - r)
+        yield r, chunk, off, take
+        r += take
+
+
+def gen_uniform_rows(torch, out, row0, seed):
+    """Fill `out` (rows [row0, row0+len)) with U(-1,1) fp32."""
+    for r, chunk, off, take in _chunks(out.shape[0], row0):
         gen = torch.Generator(device=out.device)
         gen.manual_seed(seed * 1_000_003 + chunk)
         blk = torch.rand((CHUNK, out.shape[1]), generator=gen, device=out.device, dtype=torch.float32)
         out[r:r + take].copy_(blk[off:off + take]).mul_(2.0).sub_(1.0)
-        r += take
     return out
 
 
 def gen_clustered_rows(torch, out, row0, centres, sigma, seed):
-    """Rows = centre[assign] + N(0, sigma^2), chunk-seeded (assignment and noise)."""
-    n = out.shape[0]
+    """Rows = centre[assign] + N(0, sigma^2)."""
     nc = centres.shape[0]
-    r = 0
-    while r < n:
-        g_row = row0 + r
-        chunk = g_row // CHUNK
-        off = g_row - chunk * CHUNK
-        take = min(CHUNK - off, n - r)
+    for r, chunk, off, take in _chunks(out.shape[0], row0):
         gen = torch.Generator(device=out.device)
         gen.manual_seed(seed * 1_000_003 + chunk)
         a = torch.randint(0, nc, (CHUNK,), generator=gen, device=out.device)
         noise = torch.randn((CHUNK, out.shape[1]), generator=gen, device=out.device, dtype=torch.float32)
         blk = centres[a].add_(noise.mul_(sigma))
         out[r:r + take].copy_(blk[off:off + take])
-        r += take
     return out
 
 
@@ -119,178 +131,373 @@ def lowrank_basis(torch, r_dim, d, gen):
 
 
 def gen_lowrank_rows(torch, out, row0, basis, eta, seed):
-    """Rows = z·B + eta·N(0, I_d), z ~ N(0, I_r): a low-intrinsic-dimension gaussian (chunk-seeded)."""
-    n = out.shape[0]
+    """Rows = z·B + eta·N(0, I_d), z ~ N(0, I_r): a low-intrinsic-dimension gaussian."""
     r_dim, d = basis.shape
-    r = 0
-    while r < n:
-        g_row = row0 + r
-        chunk = g_row // CHUNK
-        off = g_row - chunk * CHUNK
-        take = min(CHUNK - off, n - r)
+    for r, chunk, off, take in _chunks(out.shape[0], row0):
         gen = torch.Generator(device=out.device)
         gen.manual_seed(seed * 1_000_003 + chunk)
         z = torch.randn((CHUNK, r_dim), generator=gen, device=out.device, dtype=torch.float32)
         noise = torch.randn((CHUNK, d), generator=gen, device=out.device, dtype=torch.float32)
         blk = torch.addmm(noise.mul_(eta), z, basis)
         out[r:r + take].copy_(blk[off:off + take])
-        r += take
     return out
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
-    import hipann
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
-    if not hipann.is_available():
-        raise SystemExit("libhipann.so / HIP device not available")
-
-    n, d, nq, k = args.n, args.d, args.nq, args.k
-    metric = 0 if args.metric == "l2" else 1
-    if args.workload == "diskann":
-        run_diskann(args, torch, dist, hipann, rank, world, dev)
-        return
-    from sharded import shard_bounds
-    lo, hi = shard_bounds(n, rank, world)
-    n_local = hi - lo
-    stream = torch.cuda.current_stream().cuda_stream
-
-    # ---------------- data (generated on device; never touches the host) ----------------
-    t_setup = time.perf_counter()
+def uniform_queries(torch, nq, d, dev):
     gq = torch.Generator(device=dev)
     gq.manual_seed(4242)
-    extra = {}
-    if args.workload == "flat":
-        xb = torch.empty((n_local, d), device=dev, dtype=torch.float32)
-        gen_uniform_rows(torch, xb, lo, 42)
-        xq = (torch.rand((nq, d), generator=gq, device=dev, dtype=torch.float32) * 2 - 1).contiguous()
-        index = hipann.HipIndexFlatDevice(d, metric, xb.data_ptr(), n_local, local_rank, copy=False,
-                                          label_offset=lo)
-        # batched q·x form (hipann_flat_set_form): 3 = the library default (2-term split-bf16 scan as a
-        # filter + exact direct-form rerank); A/B: 0 exact fp32 MFMA, 1 three-term split, 2 two-term split
-        index.form = int(os.environ.get("HIPANN_FLAT_FORM", "3"))
-        search = index.search_device
-        workload = f"FAISS Flat {'L2' if metric == 0 else 'IP'}, {n // 1_000_000}Mx{d} fp32, batch={nq}, k={k}"
-    else:
-        from ivf_build import build_ivf_shard  # duckdb-annsearch_amd/ivf_build.py
-        gc = torch.Generator(device=dev)
-        gc.manual_seed(7)
-        data_model = os.environ.get("HIPANN_IVF_DATA", "lowrank")
-        xb = torch.empty((n_local, d), device=dev, dtype=torch.float32)
-        if data_model == "lowrank":
-            r_dim = int(os.environ.get("HIPANN_IVF_RANK", "16"))
-            eta = float(os.environ.get("HIPANN_IVF_NOISE", "0.02"))
-            basis = lowrank_basis(torch, r_dim, d, gc)
-            gen_lowrank_rows(torch, xb, lo, basis, eta, 42)
-            xq = torch.empty((nq, d), device=dev, dtype=torch.float32)
-            gen_lowrank_rows(torch, xq, 0, basis, eta, 4242)
-            data_desc = f"low-rank gaussian, intrinsic dim {r_dim}, noise {eta}"
-        else:
-            n_centres = int(os.environ.get("HIPANN_IVF_CENTRES", "4096"))
-            sigma = float(os.environ.get("HIPANN_IVF_SIGMA", "0.35"))
-            centres = (torch.rand((n_centres, d), generator=gc, device=dev) * 2 - 1)
-            gen_clustered_rows(torch, xb, lo, centres, sigma, 42)
-            a = torch.randint(0, n_centres, (nq,), generator=gq, device=dev)
-            xq = (centres[a] + torch.randn((nq, d), generator=gq, device=dev) * sigma).contiguous()
-            data_desc = f"{n_centres} gaussian centres, sigma={sigma}"
-        index, ivf_info = build_ivf_shard(torch, hipann, xb, lo, n, args.nlist, args.nprobe, metric, rank, world,
-                                          centres_seed=1234)
-        # list-scan form (hipann_ivf_set_form): 5 = the library default (2-term split-bf16 scan as a
-        # filter + exact fp32 direct-form rerank); A/B: 0 fp32 MFMA, 3/4 split scans, 1/2 VALU
-        index.form = int(os.environ.get("HIPANN_IVF_FORM", "5"))
-        del xb  # lists hold a list-ordered copy
-        torch.cuda.empty_cache()
-        search = index.search_device
-        extra.update(ivf_info)
-        workload = (f"FAISS IVFFlat nlist={args.nlist} nprobe={args.nprobe}, {n // 1_000_000}Mx{d} fp32 "
-                    f"({data_desc}), batch={nq}, k={k}")
-    torch.cuda.synchronize()
-    setup_s = time.perf_counter() - t_setup
+    return (torch.rand((nq, d), generator=gq, device=dev, dtype=torch.float32) * 2 - 1).contiguous()
 
-    from sharded import ShardedSearch, merge_topk_device_torch, shard_bounds
 
-    D_loc = torch.empty((nq, k), device=dev, dtype=torch.float32)
-    I_loc = torch.empty((nq, k), device=dev, dtype=torch.int64)
-
-    def local_search(q):
-        search(nq, q.data_ptr(), k, D_loc.data_ptr(), I_loc.data_ptr(), stream)
-        return D_loc, I_loc
-
-    sharded = ShardedSearch(local_search, merge_topk_device_torch(hipann, metric))
-
-    def step():
-        return sharded.search(xq)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if args.workload == "ivf":
-        from ivf_build import scan_bytes
-        probes = index.last_probes(nq)
-        extra["scan_bytes_per_batch_local"] = scan_bytes(index, probes, d)
-        extra["distinct_lists_probed"] = int(np.unique(probes[probes >= 0]).size)
-        from ivf_build import scan_pairs
-        extra["scanned_pairs_per_batch_local"] = scan_pairs(index, probes)
-        from ivf_build import scan_group_rows
-        extra["group_rows_per_batch_local"] = scan_group_rows(index, probes)
-        cnt = np.bincount(probes[probes >= 0].ravel(), minlength=args.nlist)
-        extra["probes_per_list_p50_p90_max"] = [int(np.percentile(cnt, 50)), int(np.percentile(cnt, 90)), int(cnt.max())]
-
-    # ---------------- timed region ----------------
-    index.set_kernel_timing(True)
+# ------------------------------------------------------------------------------------------------
+# timing helpers
+# ------------------------------------------------------------------------------------------------
+def timed_steps(torch, dist, world, fn, steps):
+    """Barrier + sync, `steps` calls, sync + barrier; max over ranks.  Returns seconds."""
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for _ in range(steps):
+        fn()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = index.kernel_ms(0)
-    merge_ms = index.kernel_ms(1)
-    index.set_kernel_timing(False)
+    el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([el], device=torch.device("cuda", torch.cuda.current_device()), dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    ms_per_step = elapsed * 1e3 / args.steps
-    qps = nq * args.steps / elapsed
+        el = float(t.item())
+    return el
 
-    # ---------------- recall (outside the timed region) ----------------
+
+def host_pointer_rate(torch, search_dev, xq, nq, k, steps):
+    """The same search with the queries starting in host memory and the results returned to host memory
+    (pinned buffers, H2D + search + D2H per step): the PCIe-inclusive rate of the host-pointer API."""
+    q_h = xq.cpu().pin_memory()
+    q_d = torch.empty_like(xq)
+    D_h = torch.empty((nq, k), dtype=torch.float32).pin_memory()
+    I_h = torch.empty((nq, k), dtype=torch.int64).pin_memory()
+
+    def step():
+        q_d.copy_(q_h, non_blocking=True)
+        D, I = search_dev(q_d)
+        D_h.copy_(D, non_blocking=True)
+        I_h.copy_(I, non_blocking=True)
+
+    step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"queries_per_s": round(nq * steps / el, 1), "ms_per_step": round(el * 1e3 / steps, 3),
+            "includes": "pinned H2D of the queries + search + D2H of D/I per step"}
+
+
+def recall_at(got, gt, k):
+    return float(np.mean([len(set(got[i][:k]) & set(gt[i][:k])) / k for i in range(len(gt))]))
+
+
+def pmc_traffic(key: str, kernel: str):
+    """HBM bytes per launch of `kernel` for workload `key` (e.g. "ivf_10000000x768") from the newest
+    committed FETCH_SIZE pass (profiles/rNN/pmc_<key>.json, written by tools/pmc_traffic.py from a
+    separate `rocprofv3 --pmc FETCH_SIZE` run of the same workload), or (None, None)."""
+    for f in sorted((ROOT / "profiles").glob(f"r*/pmc_{key}.json"), reverse=True):
+        try:
+            js = json.loads(f.read_text())
+        except Exception:
+            continue
+        if js.get("kernel") == kernel:
+            return js.get("hbm_bytes_per_launch"), str(f.relative_to(ROOT))
+    return None, None
+
+
+def attach_traffic(roof, key, algorithmic_bytes):
+    tb, tsrc = pmc_traffic(key, roof["kernel"])
+    roof["traffic_key"] = key
+    if tb is not None:
+        roof["traffic"] = round(tb / 1e9, 3)
+        roof["traffic_unit"] = "GB per launch (PMC FETCH_SIZE x1024 x2, gfx950 correction)"
+        roof["traffic_source"] = tsrc
+    roof["algorithmic_per_launch_gb"] = round(algorithmic_bytes / 1e9, 3)
+
+
+# ------------------------------------------------------------------------------------------------
+# Flat
+# ------------------------------------------------------------------------------------------------
+FLAT_FORMS = {0: ("flat_gemm_topk2", 1, FP32_MFMA_PEAK_TF, "fp32 MFMA (v_mfma_f32_32x32x2_f32)"),
+              1: ("flat_gemm_topk_bf", 6, BF16_MFMA_PEAK_TF,
+                  "bf16 MFMA (v_mfma_f32_32x32x16_bf16) over a 3-term split: 6 bf16 products per fp32 product"),
+              2: ("flat_gemm_topk_bf", 3, BF16_MFMA_PEAK_TF,
+                  "bf16 MFMA (v_mfma_f32_32x32x16_bf16) over a 2-term split: 3 bf16 products per fp32 product"),
+              3: ("flat_gemm_topk_bf", 3, BF16_MFMA_PEAK_TF,
+                  "bf16 MFMA (v_mfma_f32_32x32x16_bf16) over a 2-term split: 3 bf16 products per fp32 product; "
+                  "the scan keeps 16 (IP: 32) per (split, query) as a filter, merge_ms = exact direct-form rerank "
+                  "+ bound check")}
+
+
+def flat_config(args, torch, dist, hipann, rank, world, dev, n, d, nq, k, metric, steps, warmup, alt_forms=True,
+                cpu_seconds=0.0, oracle_queries=0, latency=False, host_rate=True):
+    from sharded import ShardedSearch, merge_packed_device_torch, shard_bounds
+
+    lo, hi = shard_bounds(n, rank, world)
+    n_local = hi - lo
+    stream = torch.cuda.current_stream().cuda_stream
+    t_setup = time.perf_counter()
+    xb = torch.empty((n_local, d), device=dev, dtype=torch.float32)
+    gen_uniform_rows(torch, xb, lo, 42)
+    xq = uniform_queries(torch, nq, d, dev)
+    index = hipann.HipIndexFlatDevice(d, metric, xb.data_ptr(), n_local, dev.index, copy=False, label_offset=lo)
+    index.form = int(os.environ.get("HIPANN_FLAT_FORM", "3"))
+    torch.cuda.synchronize()
+    setup_s = time.perf_counter() - t_setup
+
+    def local(q, D, I):
+        index.search_device(q.shape[0], q.data_ptr(), k, D.data_ptr(), I.data_ptr(), stream)
+
+    sharded = ShardedSearch(local, merge_packed_device_torch(hipann, metric), nq, k, dev)
+    step = lambda: sharded.search(xq)  # noqa: E731
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    index.set_kernel_timing(True)
+    el = timed_steps(torch, dist, world, step, steps)
+    kern_ms, merge_ms = index.kernel_ms(0), index.kernel_ms(1)
+    index.set_kernel_timing(False)
     Dr, Ir = step()
     torch.cuda.synchronize()
-    recall = None
-    if args.workload == "ivf":
-        from ivf_build import flat_ground_truth
-        gt = flat_ground_truth(torch, hipann, d, metric, xq, k, n, rank, world, ivf_info_tensor=index)
-        if rank == 0 and gt is not None:
-            got = Ir.cpu().numpy()
-            recall = float(np.mean([len(set(got[i]) & set(gt[i])) / k for i in range(nq)]))
-    else:
-        recall = 1.0  # exact search (parity tests: ids identical to the FAISS restatement)
-
-    # ---------------- the other fp32-level list-scan forms, same batch (IVF, 1 GPU) ----------------
-    alt = None
-    if args.workload == "ivf" and world == 1 and not args.no_alt_forms:
+    Ir = Ir.cpu().numpy().copy()
+    form = index.form
+    kname, terms, peak, fdesc = FLAT_FORMS[form]
+    flops = 2.0 * nq * n_local * d
+    achieved = terms * flops / (kern_ms * 1e-3) / 1e12 if kern_ms > 0 else 0.0
+    roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "traffic": None, "kernel": kname, "kernel_ms": round(kern_ms, 3),
+            "merge_ms": round(merge_ms, 3),
+            "algorithmic": f"{terms} x 2*nq*N_local*d = {terms * flops:.4g} MFMA FLOP per launch ({fdesc})",
+            "fp32_equivalent_tflops": round(flops / (kern_ms * 1e-3) / 1e12, 2) if kern_ms > 0 else None}
+    if world == 1:
+        attach_traffic(roof, f"flat_{n}x{d}{'' if metric == 0 else '_ip'}", 4.0 * n_local * d)
+    out = {"workload": f"FAISS Flat {'L2' if metric == 0 else 'IP'}, {n}x{d} fp32, batch={nq}, k={k}",
+           "value": round(nq * steps / el, 1), "unit": "queries/s", "ms_per_step": round(el * 1e3 / steps, 3),
+           "steps": steps, "recall_at_10": 1.0, "roofline": roof, "setup_s": round(setup_s, 1),
+           "rerank_fallbacks_total": index.rerank_fallbacks()}
+    if world > 1:
+        return out, index, xb
+    if host_rate:
+        out["with_h2d_d2h"] = host_pointer_rate(torch, lambda q: sharded.search(q), xq, nq, k, max(3, steps // 2))
+    # exactness: ids against the fp32 form (exact fp32 products, pinned by the C2 parity tests) on the whole
+    # batch, and against the CPU oracle (FAISS BLAS-path restatement) on a query subset
+    if alt_forms:
         alt = {}
-        base_form = index.form
-        names = {0: "fp32_mfma (exact fp32 products)", 3: "split3 (3-term bf16 split, 6 products)",
-                 5: "split2_exact (default)"}
+        for f in (0, 1):
+            if f == form:
+                continue
+            index.form = f
+            step()
+            torch.cuda.synchronize()
+            index.set_kernel_timing(True)
+            ta = time.perf_counter()
+            for _ in range(2):
+                step()
+            torch.cuda.synchronize()
+            ea = time.perf_counter() - ta
+            kms = index.kernel_ms(0)
+            index.set_kernel_timing(False)
+            _, Ia = step()
+            torch.cuda.synchronize()
+            alt[FLAT_FORMS[f][3]] = {"queries_per_s": round(nq * 2 / ea, 1), "kernel_ms": round(kms, 3),
+                                     "ids_equal_to_reported_form": round(float((Ia.cpu().numpy() == Ir).mean()), 6)}
+        index.form = form
+        out["other_forms"] = alt
+    if oracle_queries:
+        try:
+            from oracle import oracle as O
+            xb_h = xb.cpu().numpy()
+            xq_h = xq[:oracle_queries].cpu().numpy()
+            _, Io = O.flat_search(xb_h, xq_h, k, metric)
+            out["ids_equal_to_oracle"] = {"fraction": float((Io == Ir[:oracle_queries]).mean()),
+                                          "queries": oracle_queries,
+                                          "oracle": "FAISS IndexFlat BLAS-path restatement (oracle.c)"}
+            del xb_h
+        except Exception as e:  # report, never fail the line
+            out["ids_equal_to_oracle"] = {"error": repr(e)}
+    if latency:
+        out["latency"] = flat_latency(torch, hipann, index, xb, xq, n_local, d, k, metric)
+    if cpu_seconds > 0:
+        out["cpu_baseline"] = flat_cpu_baseline(torch, xq, n, d, k, metric, cpu_seconds)
+    return out, index, xb
+
+
+def flat_latency(torch, hipann, index, xb, xq, n, d, k, metric):
+    """The extension's call shape: FaissIndex::Search → search(1, …) (faiss_index.cpp:737), and a
+    4-query batch; the direct-form scan (flat_scan_topk, nq < 20) streams the whole table per call."""
+    stream = torch.cuda.current_stream().cuda_stream
+    res = {}
+    for nq in (1, 4):
+        q = xq[:nq].contiguous()
+        D = torch.empty((nq, k), device=xq.device)
+        I = torch.empty((nq, k), device=xq.device, dtype=torch.int64)
+        call = lambda: index.search_device(nq, q.data_ptr(), k, D.data_ptr(), I.data_ptr(), stream)  # noqa: E731
+        for _ in range(3):
+            call()
+        torch.cuda.synchronize()
+        index.set_kernel_timing(True)
+        it = 20
+        t0 = time.perf_counter()
+        for _ in range(it):
+            call()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        kms = index.kernel_ms(0)
+        index.set_kernel_timing(False)
+        bytes_ = 4.0 * n * d
+        gbs = bytes_ / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
+        res[f"nq{nq}"] = {"ms_per_call": round(el * 1e3 / it, 4), "kernel": "flat_scan_topk",
+                          "kernel_ms": round(kms, 4),
+                          "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                       "frac": round(gbs / HBM_PEAK_GBS, 4),
+                                       "algorithmic": f"N*d*4 = {bytes_ / 1e9:.3f} GB per call"}}
+    return res
+
+
+def flat_cpu_baseline(torch, xq, n, d, k, metric, cpu_seconds):
+    from oracle import cpu_baseline as CB
+
+    try:
+        xq_h = xq.cpu().numpy()
+        gen_rows = lambda rows: gen_uniform_rows(torch, torch.empty((rows, d), device=xq.device), 0,  # noqa: E731
+                                                 42).cpu().numpy()
+        probe = gen_rows(20_000)
+        _, dt0, _ = CB.flat_blas_qps(probe, xq_h, k, n, metric)
+        rows = int(min(n, 2_000_000, max(20_000, 20_000 * cpu_seconds / max(dt0, 1e-3))))
+        qps, dt, nth = CB.flat_blas_qps(gen_rows(rows), xq_h, k, n, metric)
+        return {"value": round(qps, 2), "unit": "queries/s", "cores": nth, "kind": "port",
+                "sample": f"all {xq_h.shape[0]} queries x first {rows} of {n} rows ({dt:.1f} s), FAISS BLAS-path "
+                          f"restatement (torch CPU sgemm 4096x1024 blocks + norms + top-k), extrapolated linearly to "
+                          f"{n} rows"}
+    except Exception as e:
+        return {"value": None, "error": repr(e)}
+
+
+# ------------------------------------------------------------------------------------------------
+# IVFFlat
+# ------------------------------------------------------------------------------------------------
+IVF_FORMS = {0: ("ivf_scan_mfma", "decomposed, fp32 MFMA"), 1: ("ivf_scan_topk", "direct, VALU"),
+             2: ("ivf_scan_dot", "decomposed, VALU"),
+             3: ("ivf_scan_mfma_bf", "decomposed, bf16 MFMA over a 3-term split (6 products)"),
+             4: ("ivf_scan_mfma_bf", "decomposed, bf16 MFMA over a 2-term split (3 products)"),
+             5: ("ivf_scan_mfma_bf", "bf16 MFMA 2-term split scan as a filter (16 per list) + exact fp32 "
+                                     "direct-form rerank, bound-checked (merge_ms includes the rerank)")}
+
+
+def build_ivf(args, torch, hipann, rank, world, dev, n, d, nlist, nprobe, metric, r_dim, eta):
+    """Low-intrinsic-dimension data (DESIGN.md §8) + the GPU IVF build.  N=1: one pass over the rows;
+    N>1: list sharding (sharded.assign_lists) unless HIPANN_IVF_SHARD=rows."""
+    from ivf_build import build_ivf_list_shard, build_ivf_shard
+    from sharded import shard_bounds
+
+    gc = torch.Generator(device=dev)
+    gc.manual_seed(7)
+    basis = lowrank_basis(torch, r_dim, d, gc)
+    xq = torch.empty((args.nq, d), device=dev, dtype=torch.float32)
+    gen_lowrank_rows(torch, xq, 0, basis, eta, 4242)
+    mode = os.environ.get("HIPANN_IVF_SHARD", "lists")
+    if world > 1 and mode == "lists":
+        gen = lambda out, row0: gen_lowrank_rows(torch, out, row0, basis, eta, 42)  # noqa: E731
+        index, info = build_ivf_list_shard(torch, hipann, gen, n, d, nlist, nprobe, metric, rank, world, dev)
+    else:
+        lo, hi = shard_bounds(n, rank, world)
+        xb = torch.empty((hi - lo, d), device=dev, dtype=torch.float32)
+        gen_lowrank_rows(torch, xb, lo, basis, eta, 42)
+        index, info = build_ivf_shard(torch, hipann, xb, lo, n, nlist, nprobe, metric, rank, world,
+                                      centres_seed=1234)
+        del xb
+    torch.cuda.empty_cache()
+    return index, info, xq, f"low-rank gaussian, intrinsic dim {r_dim}, noise {eta}"
+
+
+def ivf_scan_stats(index, probes, d, nlist):
+    from ivf_build import scan_bytes, scan_group_rows, scan_pairs
+
+    cnt = np.bincount(probes[probes >= 0].ravel(), minlength=nlist)
+    return {"scan_bytes_per_batch_local": scan_bytes(index, probes, d),
+            "distinct_lists_probed": int(np.unique(probes[probes >= 0]).size),
+            "scanned_pairs_per_batch_local": scan_pairs(index, probes),
+            "group_rows_per_batch_local": scan_group_rows(index, probes),
+            "probes_per_list_p50_p90_max": [int(np.percentile(cnt, 50)), int(np.percentile(cnt, 90)), int(cnt.max())]}
+
+
+def ivf_config(args, torch, dist, hipann, rank, world, dev, steps, warmup, suite_extras=False):
+    from ivf_build import flat_ground_truth
+    from sharded import ShardedSearch, merge_packed_device_torch
+
+    n, d, nq, k, nlist, nprobe = args.n, args.d, args.nq, args.k, args.nlist, args.nprobe
+    metric = 0 if args.metric == "l2" else 1
+    stream = torch.cuda.current_stream().cuda_stream
+    t_setup = time.perf_counter()
+    r_dim = int(os.environ.get("HIPANN_IVF_RANK", "16"))
+    eta = float(os.environ.get("HIPANN_IVF_NOISE", "0.02"))
+    index, info, xq, data_desc = build_ivf(args, torch, hipann, rank, world, dev, n, d, nlist, nprobe, metric,
+                                           r_dim, eta)
+    index.form = int(os.environ.get("HIPANN_IVF_FORM", "5"))
+    torch.cuda.synchronize()
+    setup_s = time.perf_counter() - t_setup
+
+    def local(q, D, I):
+        index.search_device(q.shape[0], q.data_ptr(), k, D.data_ptr(), I.data_ptr(), stream)
+
+    sharded = ShardedSearch(local, merge_packed_device_torch(hipann, metric), nq, k, dev)
+    step = lambda: sharded.search(xq)  # noqa: E731
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    probes = index.last_probes(nq)
+    info.update(ivf_scan_stats(index, probes, d, nlist))
+    index.set_kernel_timing(True)
+    el = timed_steps(torch, dist, world, step, steps)
+    kern_ms, merge_ms = index.kernel_ms(0), index.kernel_ms(1)
+    index.set_kernel_timing(False)
+    Dr, Ir = step()
+    torch.cuda.synchronize()
+    Ir = Ir.cpu().numpy().copy()
+    gt = flat_ground_truth(torch, hipann, d, metric, xq, k, n, rank, world, ivf_info_tensor=index)
+    recall = recall_at(Ir, gt, k) if rank == 0 and gt is not None else None
+    b_alg = info["scan_bytes_per_batch_local"]
+    if world > 1:  # per-rank scan bytes (list sharding balance)
+        t = torch.tensor([b_alg, kern_ms], device=dev, dtype=torch.float64)
+        allv = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(allv, t)
+        per = [float(v[0].item()) for v in allv]
+        info["per_rank_scan_gb"] = [round(x / 1e9, 3) for x in per]
+        info["per_rank_scan_kernel_ms"] = [round(float(v[1].item()), 3) for v in allv]
+        info["scan_balance_max_over_mean"] = round(max(per) / (sum(per) / world), 4)
+    form = index.form
+    kname, fname = IVF_FORMS[form]
+    fpp = 3.0 if form == 1 else 2.0  # flop per (query, row, dim): sub + fma vs fma
+    achieved = b_alg / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kname,
+            "kernel_ms": round(kern_ms, 3), "merge_ms": round(merge_ms, 3),
+            "algorithmic": "sum over distinct probed lists |l|*(4d+8) B per launch (this rank's lists)",
+            "form": fname,
+            "scan_tflops": round(fpp * d * info["scanned_pairs_per_batch_local"] / (kern_ms * 1e-3) / 1e12, 2)
+            if kern_ms > 0 else None}
+    if world == 1:
+        attach_traffic(roof, f"ivf_{n}x{d}", b_alg)
+    out = {"workload": f"FAISS IVFFlat nlist={nlist} nprobe={nprobe}, {n}x{d} fp32 ({data_desc}), batch={nq}, k={k}",
+           "value": round(nq * steps / el, 1), "ms_per_step": round(el * 1e3 / steps, 3), "recall_at_10": recall,
+           "roofline": roof, "setup_s": round(setup_s, 1),
+           "ivf": {kk: v for kk, v in info.items() if kk != "scan_bytes_per_batch_local"}}
+    if world > 1:
+        return out, index
+    out["with_h2d_d2h"] = host_pointer_rate(torch, lambda q: sharded.search(q), xq, nq, k, max(5, steps // 2))
+    if not args.no_alt_forms:
+        alt = {}
         for f in (3, 0):
-            if f == base_form:
+            if f == form:
                 continue
             index.form = f
             step()
@@ -300,155 +507,131 @@ def main():
             for _ in range(5):
                 step()
             torch.cuda.synchronize()
-            el = time.perf_counter() - ta
+            ea = time.perf_counter() - ta
             kms = index.kernel_ms(0)
             index.set_kernel_timing(False)
             _, Ia = step()
             torch.cuda.synchronize()
-            rec = None
-            if gt is not None:
-                got = Ia.cpu().numpy()
-                rec = float(np.mean([len(set(got[i]) & set(gt[i])) / k for i in range(nq)]))
-            alt[names[f]] = {"queries_per_s": round(nq * 5 / el, 1), "scan_kernel_ms": round(kms, 3),
-                             "recall_at_10": rec}
-        index.form = base_form
-        extra["rerank_fallbacks_total"] = index.rerank_fallbacks()
+            Ia = Ia.cpu().numpy()
+            alt[IVF_FORMS[f][1]] = {"queries_per_s": round(nq * 5 / ea, 1), "scan_kernel_ms": round(kms, 3),
+                                    "recall_at_10": recall_at(Ia, gt, k),
+                                    "ids_equal_to_reported_form": round(float((Ia == Ir).mean()), 6)}
+        index.form = form
+        out["other_forms"] = alt
+    out["ivf"]["rerank_fallbacks_total"] = index.rerank_fallbacks()
+    if suite_extras:
+        out["latency"] = ivf_latency(torch, index, xq, k, d)
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = ivf_cpu_baseline(index, xq, k, nprobe, metric, args.cpu_seconds)
+    return out, index
 
-    if args.workload == "flat" and world == 1 and not args.no_alt_forms:
-        alt = {}
-        base_form = index.form
-        for f, nm in ((0, "fp32_mfma (exact fp32 products)"), (1, "split3 (3-term bf16 split, 6 products)")):
-            if f == base_form:
-                continue
-            index.form = f
-            step()
+
+def ivf_latency(torch, index, xq, k, d):
+    """nq = 1 / 4 through the IVF path (the extension's per-query call, faiss_index.cpp:737)."""
+    stream = torch.cuda.current_stream().cuda_stream
+    res = {}
+    for nq in (1, 4):
+        q = xq[:nq].contiguous()
+        D = torch.empty((nq, k), device=xq.device)
+        I = torch.empty((nq, k), device=xq.device, dtype=torch.int64)
+        call = lambda: index.search_device(nq, q.data_ptr(), k, D.data_ptr(), I.data_ptr(), stream)  # noqa: E731
+        for _ in range(3):
+            call()
+        torch.cuda.synchronize()
+        probes = index.last_probes(nq)
+        from ivf_build import scan_bytes
+        b = scan_bytes(index, probes, d)
+        index.set_kernel_timing(True)
+        it = 20
+        t0 = time.perf_counter()
+        for _ in range(it):
+            call()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        kms = index.kernel_ms(0)
+        index.set_kernel_timing(False)
+        gbs = b / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
+        res[f"nq{nq}"] = {"ms_per_call": round(el * 1e3 / it, 4), "scan_kernel_ms": round(kms, 4),
+                          "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                       "frac": round(gbs / HBM_PEAK_GBS, 4),
+                                       "algorithmic": f"probed lists |l|*(4d+8) = {b / 1e9:.4f} GB per call"}}
+    return res
+
+
+def ivf_cpu_baseline(index, xq, k, nprobe, metric, cpu_seconds):
+    from oracle import cpu_baseline as CB
+
+    try:
+        cen, codes, ids = index._keep
+        cen_h, codes_h, ids_h = cen.cpu().numpy(), codes.cpu().numpy(), ids.cpu().numpy()
+        off = index._offsets
+        xq_h = xq.cpu().numpy()
+        s0 = min(16, xq_h.shape[0])
+        _, dt0, _ = CB.ivf_qps(cen_h, off, ids_h, codes_h, xq_h[:s0], k, nprobe, metric)
+        s = int(min(xq_h.shape[0], max(s0, s0 * cpu_seconds / max(dt0, 1e-3))))
+        qps, dt, nth = CB.ivf_qps(cen_h, off, ids_h, codes_h, xq_h[:s], k, nprobe, metric)
+        return {"value": round(qps, 2), "unit": "queries/s", "cores": nth, "kind": "port",
+                "sample": f"first {s} of {xq_h.shape[0]} queries ({dt:.1f} s) through the C oracle's FAISS "
+                          f"IndexIVFFlat::search restatement (coarse quantizer + direct SIMD distances + heaps, "
+                          f"OpenMP over queries) on the same centroids and lists"}
+    except Exception as e:
+        return {"value": None, "error": repr(e)}
+
+
+def ivf_robustness(args, torch, dist, hipann, dev):
+    """Recall@10 and QPS against nprobe at intrinsic ranks 16 / 24 / 32 (same 10M x 768 shape, same build):
+    the smallest nprobe reaching recall@10 >= 0.95 and its QPS, per rank."""
+    from ivf_build import flat_ground_truth
+
+    k, nq, d, n = args.k, args.nq, args.d, args.n
+    stream = torch.cuda.current_stream().cuda_stream
+    res = {}
+    for r_dim in (16, 24, 32):
+        index, info, xq, _ = build_ivf(args, torch, hipann, 0, 1, dev, n, d, args.nlist, args.nprobe, 0, r_dim, 0.02)
+        gt = flat_ground_truth(torch, hipann, d, 0, xq, k, n, 0, 1, ivf_info_tensor=index)
+        D = torch.empty((nq, k), device=dev)
+        I = torch.empty((nq, k), device=dev, dtype=torch.int64)
+        sweep = []
+        best = None
+        for nprobe in (16, 32, 48, 64, 96, 128, 192, 256):
+            index.nprobe = nprobe
+            call = lambda: index.search_device(nq, xq.data_ptr(), k, D.data_ptr(), I.data_ptr(), stream)  # noqa
+            call()
             torch.cuda.synchronize()
-            index.set_kernel_timing(True)
-            ta = time.perf_counter()
+            t0 = time.perf_counter()
             for _ in range(3):
-                step()
+                call()
             torch.cuda.synchronize()
-            el = time.perf_counter() - ta
-            kms = index.kernel_ms(0)
-            index.set_kernel_timing(False)
-            _, Ia = step()
-            torch.cuda.synchronize()
-            same = float((Ia == Ir).float().mean().item())
-            alt[nm] = {"queries_per_s": round(nq * 3 / el, 1), "kernel_ms": round(kms, 3),
-                       "ids_equal_to_reported_form": round(same, 5)}
-        index.form = base_form
-
-    # ---------------- roofline of the dominant kernel ----------------
-    if args.workload == "flat":
-        flops = 2.0 * nq * n_local * d
-        fform = index.form
-        if fform == 0:
-            kname, terms, peak, fdesc = "flat_gemm_topk2", 1, FP32_MFMA_PEAK_TF, "fp32 MFMA (v_mfma_f32_32x32x2_f32)"
-        else:
-            terms = 6 if fform == 1 else 3
-            kname, peak = "flat_gemm_topk_bf", BF16_MFMA_PEAK_TF
-            fdesc = (f"bf16 MFMA (v_mfma_f32_32x32x16_bf16) over a {3 if fform == 1 else 2}-term split: "
-                     f"{terms} bf16 products per fp32 product")
-            if fform == 3:
-                fdesc += ("; the scan keeps 16 (IP: 32) per (split, query) as a filter, merge_ms = exact direct-form "
-                          "rerank of the 16 + bound check")
-        achieved = terms * flops / (kern_ms * 1e-3) / 1e12 if kern_ms > 0 else 0.0
-        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4), "traffic": None,
-                "kernel": kname, "kernel_ms": round(kern_ms, 3), "merge_ms": round(merge_ms, 3),
-                "algorithmic": f"{terms} x 2*nq*N_local*d = {terms * flops:.4g} MFMA FLOP per launch",
-                "form": fdesc,
-                "fp32_equivalent_tflops": round(flops / (kern_ms * 1e-3) / 1e12, 2) if kern_ms > 0 else None}
-    else:
-        b_alg = extra.get("scan_bytes_per_batch_local", 0.0)
-        form = index.form
-        kname, fname = {0: ("ivf_scan_mfma", "decomposed, fp32 MFMA"), 1: ("ivf_scan_topk", "direct, VALU"),
-                        2: ("ivf_scan_dot", "decomposed, VALU"),
-                        3: ("ivf_scan_mfma_bf", "decomposed, bf16 MFMA over a 3-term split (6 products)"),
-                        4: ("ivf_scan_mfma_bf", "decomposed, bf16 MFMA over a 2-term split (3 products)"),
-                        5: ("ivf_scan_mfma_bf", "bf16 MFMA 2-term split scan as a filter (16 per list) + exact fp32 "
-                            "direct-form rerank, bound-checked (merge_ms includes the rerank)")}[form]
-        fpp = 3.0 if form == 1 else 2.0  # flop per (query, row, dim): sub + fma vs fma
-        achieved = b_alg / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kname,
-                "kernel_ms": round(kern_ms, 3), "merge_ms": round(merge_ms, 3),
-                "algorithmic": "sum over distinct probed lists |l|*(4d+8) B per launch",
-                "form": fname,
-                "scan_tflops": round(fpp * d * extra.get("scanned_pairs_per_batch_local", 0) / (kern_ms * 1e-3) / 1e12, 2)
-                if kern_ms > 0 else None}
-
-    tb, tsrc = pmc_traffic(args.workload, roof["kernel"])
-    if tb is not None and world == 1:
-        roof["traffic"] = round(tb / 1e9, 3)
-        roof["traffic_unit"] = "GB per launch (PMC FETCH_SIZE x1024 x2, gfx950 correction)"
-        roof["traffic_source"] = tsrc
-        roof["algorithmic_per_launch"] = round((b_alg if args.workload == "ivf" else 4.0 * n_local * d) / 1e9, 3)
-
-    # ---------------- CPU baseline (rank 0, N=1 only) ----------------
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        try:
-            cpu = cpu_baseline(args, torch, xq, index, extra, n, d, k, metric)
-        except Exception as e:  # report, never fail the bench line
-            log(f"[bench] cpu baseline failed: {e!r}")
-            cpu = {"value": None, "error": repr(e)}
-
-    if rank == 0:
-        line = {
-            "metric": "queries/sec @ recall@10>=0.95, 10Mx768 fp32, batch=1024",
-            "value": round(qps, 1),
-            "unit": "queries/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 3),
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic (generated on device: U(-1,1) rows for flat; low-intrinsic-dimension gaussian rows for ivf)",
-            "config": {"workload": workload, "global_batch": nq, "n": n, "d": d, "k": k,
-                       "parallelism": f"shard{world}"},
-            "recall_at_10": recall,
-            "roofline": roof,
-            "cpu_baseline": cpu,
-            "setup_s": round(setup_s, 1),
-        }
-        if extra:
-            line["ivf"] = {kk: v for kk, v in extra.items() if kk != "scan_bytes_per_batch_local"}
-        if alt:
-            line["ivf_other_forms" if args.workload == "ivf" else "flat_other_forms"] = alt
-        if args.workload == "flat" and index.form == 3:
-            line["precision"] = ("returned distances are fp32 direct-form Σ(q−x)² of the returned rows; the bf16 2-term "
-                                 "split scan only prunes, and a per-query bound (|scan key − exact| ≤ "
-                                 "2^-12·(|q|²+max|x|²)) proves no pruned row reaches the top-k (failures re-run on the "
-                                 "3-term path)")
-            line["flat"] = {"rerank_fallbacks_total": index.rerank_fallbacks()}
-        if args.workload == "ivf" and index.form == 5:
-            line["precision"] = ("returned distances are fp32 direct-form Σ(q−x)² (FAISS CPU IVFFlatScanner arithmetic); "
-                                 "the bf16 2-term split scan only prunes, and a per-query bound "
-                                 "(|scan key − exact| ≤ 2^-12·(|q|²+max|x|²)) proves no pruned row reaches the top-k "
-                                 "(failures re-run on the 3-term path)")
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+            el = time.perf_counter() - t0
+            rec = recall_at(I.cpu().numpy(), gt, k)
+            sweep.append({"nprobe": nprobe, "queries_per_s": round(nq * 3 / el, 1), "recall_at_10": round(rec, 4)})
+            if rec >= 0.95 and best is None:
+                best = sweep[-1]
+            if rec >= 0.99:
+                break
+        res[f"intrinsic_dim_{r_dim}"] = {"smallest_nprobe_at_recall_0.95": best, "sweep": sweep,
+                                         "list_size_min_max": [info["list_size_min"], info["list_size_max"]]}
+        index.close()
+        del index, call, xq
+        torch.cuda.empty_cache()
+    return res
 
 
-def run_diskann(args, torch, dist, hipann, rank, world, dev):
-    """C4 (SURVEY §8d): DiskProvider::search_batch over 1M x 1536 SQ8, L_search=128, R=64, nq=1024.
+# ------------------------------------------------------------------------------------------------
+# DiskANN (C4)
+# ------------------------------------------------------------------------------------------------
+def diskann_config(args, torch, dist, hipann, rank, world, dev, n, d, nq, k, L, R, steps, warmup, cpu=True,
+                   resident=True):
+    """C4 (SURVEY §8d): DiskProvider::search_batch over n x d SQ8, L_search, R, nq queries.
 
     Graph traversal does not shard, so N GPUs run N replicas (each holds the whole SQ8 DB and answers
-    its own 1024-query batch; weak scaling, no collective).  A step = one BFS batch of nq queries:
-      * default: diskann_hip_search_batch_resident_device — the traversal on the GPU (one wavefront per
-        query, DB + adjacency + visited bitmaps in HBM); roofline of that kernel, algorithmic bytes =
-        distances x d (SQ8 code rows) + expansions x 4R (adjacency rows);
-      * --diskann-host-bfs: diskann_hip_search_batch — the reference's structure (host lock-step BFS,
-        one id-gather launch per step); roofline of the id-gather kernel, d + 12 B per distance
-        (code row + id + query_map + out)."""
+    its own batch; weak scaling, no collective).  A step = one BFS batch of nq queries:
+      * default: diskann_hip_search_batch_resident_device — the traversal on the GPU; roofline of that
+        kernel, algorithmic bytes = distances x d (SQ8 code rows) + expansions x 4R (adjacency rows);
+      * resident=False: diskann_hip_search_batch — the reference's structure (host lock-step BFS, one
+        id-gather launch per step); roofline of the id-gather kernel, d + 12 B per distance."""
     import diskann_build as DB
 
-    n, d, nq, k, L, R = args.n, args.d, args.nq, args.k, args.l_search, args.degree
     metric = 0 if args.metric == "l2" else 1
     t_setup = time.perf_counter()
     gc = torch.Generator(device=dev)
@@ -472,7 +655,6 @@ def run_diskann(args, torch, dist, hipann, rank, world, dev):
     torch.cuda.empty_cache()
     xq_h = xq.cpu().numpy()
     eps = np.array([medoid], np.uint32)
-    resident = not args.diskann_host_bfs
     stream = torch.cuda.current_stream().cuda_stream
     if resident:
         db.register_graph(adj)
@@ -487,7 +669,7 @@ def run_diskann(args, torch, dist, hipann, rank, world, dev):
             return None, None, st
         return db.search_batch(adj, eps, xq_h, k, L, metric)
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     db.set_kernel_timing(True)
     if world > 1:
@@ -496,7 +678,7 @@ def run_diskann(args, torch, dist, hipann, rank, world, dev):
     t0 = time.perf_counter()
     evals = pops = requeries = 0
     bfs_steps = []
-    for _ in range(args.steps):
+    for _ in range(steps):
         ids, dd, st = step()
         evals += st["evals"]
         pops += st.get("pops", 0)
@@ -512,141 +694,265 @@ def run_diskann(args, torch, dist, hipann, rank, world, dev):
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    qps = world * nq * args.steps / elapsed
+    qps = world * nq * steps / elapsed
     if resident:
         ids = I_dev.cpu().numpy()
-
     gt = DB.exact_topk(torch, xb, xq, k, metric).cpu().numpy()
-    recall = float(np.mean([len(set(ids[i]) & set(gt[i])) / k for i in range(nq)]))
+    recall = recall_at(ids, gt, k)
     if resident:
-        # per distance: the SQ8 code row (d B); per expansion: the adjacency row (4R B)
         b_alg = evals * d + pops * 4 * R
-        achieved = b_alg / (kern_total_ms * 1e-3) / 1e9 if kern_total_ms > 0 else 0.0
         kname = "diskann_bfs"
         alg = (f"distances x d B (SQ8 code rows) + expansions x 4R B (adjacency rows) = "
-               f"{b_alg / args.steps / 1e9:.3f} GB per batch (one launch per batch)")
+               f"{b_alg / steps / 1e9:.3f} GB per batch (one launch per batch)")
     else:
         b_alg = evals * (d + 12)
-        achieved = b_alg / (kern_total_ms * 1e-3) / 1e9 if kern_total_ms > 0 else 0.0
         kname = "dist_ids_sq8"
         alg = (f"distances x (d + 12) B = {d + 12} B per distance (SQ8 code row + id + query_map + out), summed "
                f"over the timed launches")
+    achieved = b_alg / (kern_total_ms * 1e-3) / 1e9 if kern_total_ms > 0 else 0.0
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kname,
             "kernel_ms_per_launch": round(kern_total_ms / max(launches, 1), 4),
-            "kernel_ms_per_batch": round(kern_total_ms / args.steps, 3),
-            "launches_per_batch": launches / args.steps,
-            "distances_per_batch": evals // args.steps,
-            "expansions_per_batch": pops // args.steps if resident else None,
+            "kernel_ms_per_batch": round(kern_total_ms / steps, 3), "launches_per_batch": launches / steps,
+            "distances_per_batch": evals // steps, "expansions_per_batch": pops // steps if resident else None,
             "algorithmic": alg}
-    tb, tsrc = pmc_traffic("diskann", kname)
-    if tb is not None and world == 1:
-        roof["traffic"] = round(tb / 1e9, 4)
-        roof["traffic_unit"] = "GB per launch (PMC FETCH_SIZE)"
-        roof["traffic_source"] = tsrc
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if world == 1:
+        attach_traffic(roof, f"diskann_{n}x{d}", b_alg / max(launches, 1))
+    out = {"workload": f"DISKANN DiskProvider batch-distance, {n}x{d} sq8, L_search={L}, R={R}, batch={nq}, k={k}",
+           "value": round(qps, 1), "unit": "queries/s", "ms_per_step": round(elapsed * 1e3 / steps, 3),
+           "steps": steps, "recall_at_10": recall, "roofline": roof, "setup_s": round(setup_s, 1),
+           "data": f"low-rank gaussian rows, intrinsic dim {r_dim}, noise {eta}; SQ8-encoded; graph = {R - R // 4} "
+                   f"exact cell-local nearest neighbours + {R // 4} random edges, medoid entry point",
+           "diskann": {"graph_build_s": round(t_graph, 1), "bfs_steps_per_batch": int(np.mean(bfs_steps)),
+                       "traversal": "GPU-resident (one 2-wavefront workgroup per query)" if resident else
+                                    f"host lock-step BFS ({os.environ.get('HIPANN_BFS_THREADS', '16')} threads) + "
+                                    f"per-step id-gather launches",
+                       "host_requeries": requeries}}
+    if cpu and rank == 0 and world == 1:
         try:
             from oracle import oracle as O
-            c_h = codes_h
             m_h, s_h = mins.cpu().numpy(), scale.cpu().numpy()
             s0 = 16
             t1 = time.perf_counter()
-            O.diskann_search_batch(adj, eps, xq_h[:s0], k, L, metric, codes=c_h, mins=m_h, scale=s_h)
+            O.diskann_search_batch(adj, eps, xq_h[:s0], k, L, metric, codes=codes_h, mins=m_h, scale=s_h)
             dt0 = time.perf_counter() - t1
-            s1 = int(min(nq, max(s0, s0 * args.cpu_seconds / max(dt0, 1e-3))))
+            s1 = int(min(nq, max(s0, s0 * 5.0 / max(dt0, 1e-3))))
             t1 = time.perf_counter()
-            O.diskann_search_batch(adj, eps, xq_h[:s1], k, L, metric, codes=c_h, mins=m_h, scale=s_h)
+            oi, _, _ = O.diskann_search_batch(adj, eps, xq_h[:s1], k, L, metric, codes=codes_h, mins=m_h, scale=s_h)
             dt = time.perf_counter() - t1
-            cpu = {"value": round(s1 / dt, 2), "unit": "queries/s", "cores": O.num_threads(), "kind": "port",
-                   "sample": f"first {s1} of {nq} queries ({dt:.1f} s) through the C oracle's "
-                             f"DiskProvider::search_batch restatement (lock-step BFS on the host, SQ8 "
-                             f"distances OpenMP over each step's candidates) on the same graph and codes"}
+            out["cpu_baseline"] = {
+                "value": round(s1 / dt, 2), "unit": "queries/s", "cores": O.num_threads(), "kind": "port",
+                "sample": f"first {s1} of {nq} queries ({dt:.1f} s) through the C oracle's DiskProvider::search_batch "
+                          f"restatement (lock-step BFS on the host, SQ8 distances OpenMP over each step's candidates) "
+                          f"on the same graph and codes"}
+            out["ids_equal_to_oracle_bfs"] = round(float((oi == ids[:s1]).mean()), 5)
         except Exception as e:
-            log(f"[bench] cpu baseline failed: {e!r}")
-            cpu = {"value": None, "error": repr(e)}
+            out["cpu_baseline"] = {"value": None, "error": repr(e)}
+    db.close()
+    del xb, xq
+    torch.cuda.empty_cache()
+    return out
 
+
+# ------------------------------------------------------------------------------------------------
+# C1 and the reference's published microbenchmark
+# ------------------------------------------------------------------------------------------------
+def c1_config(torch, hipann, dev):
+    """C1: FAISS Flat L2 10k x 128, k = 10, gpu=false — the CPU path (the oracle restates FAISS's CPU
+    IndexFlatL2::search), timed at nq = 1000 (BLAS form) and per query (nq = 1, the extension's call),
+    next to the GPU path through the host-pointer C ABI (hipann_flat_search, PCIe included), which
+    EnsureGpuIndex's AUTO gates (ntotal >= 256, d >= 128, faiss_index.cpp:128-143) would select."""
+    from oracle import oracle as O
+
+    sys.path.insert(0, str(ROOT / "tests"))
+    from _data import faiss_metal_case
+
+    xb, xq = faiss_metal_case(10_000, 1000, 128)
+    res = {"workload": "FAISS Flat L2, 10k x 128 fp32, k=10 (mt19937(42) U(-1,1), faiss-metal test inputs)"}
+    t0 = time.perf_counter()
+    Do, Io = O.flat_search(xb, xq, 10)
+    dt = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    for i in range(200):
+        O.flat_search(xb, xq[i:i + 1], 10)
+    dt1 = time.perf_counter() - t0
+    res["cpu_path"] = {"kind": "port", "cores": O.num_threads(), "batch1000_queries_per_s": round(1000 / dt, 1),
+                       "nq1_ms_per_query": round(dt1 * 1e3 / 200, 4),
+                       "note": "C oracle (FAISS IndexFlatL2::search restatement): BLAS form at nq >= 20 (OpenMP over "
+                               "queries), direct fvec_L2sqr per query at nq = 1"}
+    ix = hipann.HipIndexFlat(128, 0, xb)
+    D, I = ix.search(xq, 10)
+    res["gpu_ids_equal_to_cpu_path"] = float((I == Io).mean())
+    for _ in range(3):
+        ix.search(xq, 10)
+    t0 = time.perf_counter()
+    for _ in range(10):
+        ix.search(xq, 10)
+    dtg = time.perf_counter() - t0
+    for i in range(5):
+        ix.search(xq[i:i + 1], 10)
+    t0 = time.perf_counter()
+    for i in range(200):
+        ix.search(xq[i:i + 1], 10)
+    dtg1 = time.perf_counter() - t0
+    res["gpu_path_host_pointers"] = {"batch1000_queries_per_s": round(10_000 / dtg, 1),
+                                     "nq1_ms_per_query": round(dtg1 * 1e3 / 200, 4)}
+    ix.close()
+    return res
+
+
+README_SHAPES = [(64, 128, 4, 448), (64, 768, 53, 453), (128, 1536, 210, 495), (256, 1536, 424, 415),
+                 (512, 1536, 870, 380), (1024, 768, 784, 532)]  # (n, d, M1 Pro CPU us, Metal us), README.md:140-145
+
+
+def batch_distance_microbench(hipann):
+    """The reference's only published hot-path numbers (README.md:140-147): one query vs n candidates,
+    L2, through the host-pointer bridge (diskann_hip_batch_distances: H2D of the candidates, kernel, D2H),
+    next to the CPU (ComputeDistancesCPU restatement, one thread, as the Rust caller runs per query); and
+    the break-even n·d that sets MIN_GPU_WORK (metal_ffi.rs:36-46)."""
+    from oracle import oracle as O
+
+    rng = np.random.default_rng(1)
+
+    def time_pair(n, d, it):
+        q = rng.uniform(-1, 1, d).astype(np.float32)
+        c = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+        out = np.empty(n, np.float32)
+        for _ in range(5):
+            hipann.diskann_hip_batch_distances(q, c, n, d, 0, out)
+        t0 = time.perf_counter()
+        for _ in range(it):
+            hipann.diskann_hip_batch_distances(q, c, n, d, 0, out)
+        g = (time.perf_counter() - t0) / it * 1e6
+        lib = O.lib()
+        fp = lambda a: a.ctypes.data_as(__import__("ctypes").POINTER(__import__("ctypes").c_float))  # noqa: E731
+        ref = np.empty(n, np.float32)
+        lib.oracle_batch_distances(fp(q), fp(c), n, d, 0, fp(ref))
+        t0 = time.perf_counter()
+        for _ in range(it):
+            lib.oracle_batch_distances(fp(q), fp(c), n, d, 0, fp(ref))
+        cpu = (time.perf_counter() - t0) / it * 1e6
+        return g, cpu
+
+    rows = []
+    for n, d, m1_cpu, metal in README_SHAPES:
+        g, cpu = time_pair(n, d, 200)
+        rows.append({"n": n, "d": d, "gpu_us": round(g, 1), "cpu_us": round(cpu, 1), "speedup": round(cpu / g, 3),
+                     "reference_m1pro_cpu_us": m1_cpu, "reference_metal_us": metal,
+                     "reference_speedup": round(m1_cpu / metal, 2)})
+    sweep = []
+    even = None
+    for nd_log in range(12, 22):
+        nd = 1 << nd_log
+        d = 768
+        n = max(1, nd // d)
+        g, cpu = time_pair(n, d, 100)
+        sweep.append({"n_times_d": n * d, "gpu_us": round(g, 1), "cpu_us": round(cpu, 1)})
+        if even is None and g < cpu:
+            even = n * d
+    return {"shapes": rows, "break_even_sweep_d768": sweep, "break_even_n_times_d": even,
+            "cpu": "oracle_batch_distances (ComputeDistancesCPU restatement, sequential fp32 sum, 1 thread)",
+            "gpu": "diskann_hip_batch_distances (host pointers: candidates H2D + kernel + D2H, synchronous)",
+            "current_gates": {"MIN_GPU_WORK": hipann.MIN_GPU_WORK, "MIN_GPU_WORK_ONESHOT": hipann.MIN_GPU_WORK_ONESHOT}}
+
+
+def run_suite(args, torch, dist, hipann, dev):
+    """Every other BASELINE configuration, N = 1, same run."""
+    cfg = {}
+
+    def guarded(name, fn):
+        t0 = time.perf_counter()
+        try:
+            cfg[name] = fn()
+        except Exception as e:  # a sub-configuration never kills the headline line
+            log(f"[bench] {name} failed: {e!r}")
+            cfg[name] = {"error": repr(e)}
+        cfg[name]["wall_s"] = round(time.perf_counter() - t0, 1)
+        torch.cuda.empty_cache()
+
+    def flat(n, metric=0, oracle_queries=0, latency=False, steps=10):
+        out, index, xb = flat_config(args, torch, dist, hipann, 0, 1, dev, n, 768, 1024, args.k, metric, steps, 2,
+                                     cpu_seconds=5.0, oracle_queries=oracle_queries, latency=latency)
+        index.close()
+        del index, xb
+        return out
+
+    guarded("C1_flat_10k_128_cpu_path", lambda: c1_config(torch, hipann, dev))
+    guarded("C2_flat_l2_1m_768", lambda: flat(1_000_000, oracle_queries=32))
+    guarded("flat_l2_10m_768", lambda: flat(10_000_000, latency=True, steps=5))
+    guarded("C4_diskann_1m_1536_sq8", lambda: diskann_config(args, torch, dist, hipann, 0, 1, dev, 1_000_000, 1536,
+                                                             1024, args.k, 128, 64, 10, 2))
+    guarded("reference_readme_batch_distances", lambda: batch_distance_microbench(hipann))
+    guarded("ivf_recall_vs_nprobe", lambda: ivf_robustness(args, torch, dist, hipann, dev))
+    return cfg
+
+
+# ------------------------------------------------------------------------------------------------
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import hipann
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    if not hipann.is_available():
+        raise SystemExit("libhipann.so / HIP device not available")
+    metric = 0 if args.metric == "l2" else 1
+
+    if args.workload == "diskann":
+        sub = diskann_config(args, torch, dist, hipann, rank, world, dev, args.n, args.d, args.nq, args.k,
+                             args.l_search, args.degree, args.steps, args.warmup, cpu=not args.no_cpu_baseline,
+                             resident=not args.diskann_host_bfs)
+        line = {"metric": "queries/sec @ recall@10>=0.95 (DiskANN DiskProvider batch path, 1Mx1536 sq8, L_search=128)",
+                "value": sub.pop("value"), "unit": "queries/s", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": sub.pop("ms_per_step"), "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "u8 codes, f32 accumulate",
+                "data": "synthetic (generated on device: " + sub.pop("data") + ")",
+                "config": {"workload": sub.pop("workload"), "global_batch": args.nq * world, "n": args.n, "d": args.d,
+                           "k": args.k, "parallelism": f"replicas{world}"}}
+        line.update(sub)
+    else:
+        if args.workload == "flat":
+            sub, index, xb_keep = flat_config(args, torch, dist, hipann, rank, world, dev, args.n, args.d, args.nq, args.k,
+                                        metric, args.steps, args.warmup, alt_forms=not args.no_alt_forms,
+                                        cpu_seconds=0.0 if args.no_cpu_baseline else args.cpu_seconds)
+            dtype, data = "f32 (bf16-split MFMA filter + fp32 rerank)", "U(-1,1) rows"
+        else:
+            sub, index = ivf_config(args, torch, dist, hipann, rank, world, dev, args.steps, args.warmup,
+                                    suite_extras=args.suite and world == 1)
+            dtype, data = "f32", "low-intrinsic-dimension gaussian rows (DESIGN.md §8)"
+        line = {"metric": METRIC, "value": sub.pop("value"), "unit": "queries/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": sub.pop("ms_per_step"),
+                "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": dtype,
+                "data": f"synthetic (generated on device: {data})",
+                "config": {"workload": sub.pop("workload"), "global_batch": args.nq, "n": args.n, "d": args.d,
+                           "k": args.k, "parallelism": f"shard{world}" + (
+                               f" ({os.environ.get('HIPANN_IVF_SHARD', 'lists')})" if args.workload == "ivf" and
+                               world > 1 else "")}}
+        sub.pop("unit", None)
+        line.update(sub)
+        if args.workload == "ivf" and index.form == 5:
+            line["precision"] = ("returned distances are fp32 direct-form Σ(q−x)² (FAISS CPU IVFFlatScanner "
+                                 "arithmetic); the bf16 2-term split scan only prunes, and a per-query bound "
+                                 "(|scan key − exact| ≤ 2^-12·(|q|²+max|x|²)) proves no pruned row reaches the top-k "
+                                 "(failures re-run on the 3-term path)")
+        if args.suite and world == 1:
+            index.close()
+            del index
+            torch.cuda.empty_cache()
+            line["configs"] = run_suite(args, torch, dist, hipann, dev)
     if rank == 0:
-        line = {
-            "metric": "queries/sec @ recall@10>=0.95 (DiskANN DiskProvider batch path, 1Mx1536 sq8, L_search=128)",
-            "value": round(qps, 1),
-            "unit": "queries/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8 codes, f32 accumulate",
-            "data": f"synthetic (generated on device: low-rank gaussian rows, intrinsic dim {r_dim}, noise {eta}; "
-                    f"SQ8-encoded; graph = {R - R // 4} exact cell-local nearest neighbours + {R // 4} random "
-                    f"edges, medoid entry point)",
-            "config": {"workload": f"DISKANN DiskProvider batch-distance, {n // 1_000_000}Mx{d} sq8, "
-                                   f"L_search={L}, R={R}, batch={nq}, k={k}",
-                       "global_batch": nq * world, "n": n, "d": d, "k": k,
-                       "parallelism": f"replicas{world}"},
-            "recall_at_10": recall,
-            "roofline": roof,
-            "cpu_baseline": cpu,
-            "setup_s": round(setup_s, 1),
-            "diskann": {"graph_build_s": round(t_graph, 1), "bfs_steps_per_batch": int(np.mean(bfs_steps)),
-                        "traversal": "GPU-resident (one 2-wavefront workgroup per query)" if resident else
-                                     f"host lock-step BFS ({os.environ.get('HIPANN_BFS_THREADS', '16')} threads) + "
-                                     f"per-step id-gather launches",
-                        "host_requeries": requeries},
-        }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
-
-
-def pmc_traffic(workload: str, kernel: str):
-    """HBM bytes per launch of `kernel` from the newest committed FETCH_SIZE pass
-    (profiles/rNN/pmc_<workload>.json, written by tools/pmc_traffic.py from a separate
-    `rocprofv3 --pmc FETCH_SIZE` run of this same command), or None."""
-    for f in sorted((ROOT / "profiles").glob(f"r*/pmc_{workload}.json"), reverse=True):
-        try:
-            js = json.loads(f.read_text())
-        except Exception:
-            continue
-        if js.get("kernel") == kernel:
-            return js.get("hbm_bytes_per_launch"), str(f.relative_to(ROOT))
-    return None, None
-
-
-def cpu_baseline(args, torch, xq, index, extra, n, d, k, metric):
-    from oracle import cpu_baseline as CB
-
-    if args.workload == "flat":
-        # calibrate on a small slice, then size the sample to ~cpu_seconds (bounded)
-        xq_h = xq.cpu().numpy()
-        gen_rows = lambda rows: gen_uniform_rows(torch, torch.empty((rows, d), device=xq.device), 0, 42).cpu().numpy()
-        probe = gen_rows(20_000)
-        q0, dt0, nth = CB.flat_blas_qps(probe, xq_h, k, n, metric)
-        rows = int(min(2_000_000, max(20_000, 20_000 * args.cpu_seconds / max(dt0, 1e-3))))
-        sample = gen_rows(rows)
-        qps, dt, nth = CB.flat_blas_qps(sample, xq_h, k, n, metric)
-        return {"value": round(qps, 2), "unit": "queries/s", "cores": nth, "kind": "port",
-                "sample": f"all {xq_h.shape[0]} queries x first {rows} of {n} rows ({dt:.1f} s), FAISS "
-                          f"BLAS-path restatement (torch CPU sgemm 4096x1024 blocks + norms + top-k), "
-                          f"extrapolated linearly to {n} rows"}
-    # IVF: the C oracle's IndexIVFFlat::search (OpenMP over queries) on a bounded query subset
-    cen, codes, ids = index._keep
-    cen_h = cen.cpu().numpy()
-    codes_h = codes.cpu().numpy()
-    ids_h = ids.cpu().numpy()
-    off = index._offsets
-    xq_h = xq.cpu().numpy()
-    s0 = min(16, xq_h.shape[0])
-    _, dt0, nth = CB.ivf_qps(cen_h, off, ids_h, codes_h, xq_h[:s0], k, args.nprobe, metric)
-    s = int(min(xq_h.shape[0], max(s0, s0 * args.cpu_seconds / max(dt0, 1e-3))))
-    qps, dt, nth = CB.ivf_qps(cen_h, off, ids_h, codes_h, xq_h[:s], k, args.nprobe, metric)
-    return {"value": round(qps, 2), "unit": "queries/s", "cores": nth, "kind": "port",
-            "sample": f"first {s} of {xq_h.shape[0]} queries ({dt:.1f} s) through the C oracle's FAISS "
-                      f"IndexIVFFlat::search restatement (coarse quantizer + direct SIMD distances + heaps, "
-                      f"OpenMP over queries) on the same centroids and lists"}
 
 
 if __name__ == "__main__":

@@ -854,7 +854,7 @@ template <int S, typename InId>
 __global__ void __launch_bounds__(256)
 merge_parts_topk(const float *__restrict__ pd, const InId *__restrict__ pi, int nparts, int64_t nq, int k,
                  int kout, int64_t label_offset, float in_sign, float out_sign, float *__restrict__ D,
-                 int64_t *__restrict__ I) {
+                 int64_t *__restrict__ I, int64_t pstride_d, int64_t pstride_i) {
     const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (q >= nq) return;
     const int lane = threadIdx.x & 63;
@@ -867,9 +867,8 @@ merge_parts_topk(const float *__restrict__ pd, const InId *__restrict__ pi, int 
         long long lab = IdTraits<long long>::pad();
         if (c < total) {
             const int64_t p = c / k, i = c - p * k;
-            const int64_t off = (p * nq + q) * k + i;
-            const InId raw = pi[off];
-            const float v = pd[off] * in_sign;
+            const InId raw = pi[p * pstride_i + q * k + i];
+            const float v = pd[p * pstride_d + q * k + i] * in_sign;
             // int32 partials pad with 0x7fffffff; int64 (global label) partials only with negatives, so a
             // real label 2^31 - 1 (arbitrary IVF ids, > 2^31 rows) is kept
             bool pad_in = raw < 0;
@@ -1142,14 +1141,17 @@ void launch_flat_scan_topk(const float *Q, int nq, const float *X, int64_t N, in
 
 template <typename InId>
 void launch_merge_parts(const float *pd, const InId *pi, int nparts, int64_t nq, int k, int kout,
-                        int64_t label_offset, float in_sign, float out_sign, float *D, int64_t *I, hipStream_t st) {
+                        int64_t label_offset, float in_sign, float out_sign, float *D, int64_t *I, hipStream_t st,
+                        int64_t pstride_d, int64_t pstride_i) {
     if (nq <= 0) return;
+    if (pstride_d < 0) pstride_d = nq * k;  // default layout [part][nq][k]
+    if (pstride_i < 0) pstride_i = nq * k;
     dim3 grid((unsigned)ceil_div(nq, 4)), block(256);
     const int S = (kout + 63) / 64;
 #define HIPANN_MERGE_CASE(s)                                                                                  \
     if (S <= s) {                                                                                             \
         hipLaunchKernelGGL((merge_parts_topk<s, InId>), grid, block, 0, st, pd, pi, nparts, nq, k, kout, \
-                           label_offset, in_sign, out_sign, D, I);                                                          \
+                           label_offset, in_sign, out_sign, D, I, pstride_d, pstride_i);                                    \
         HIPANN_CHECK(hipGetLastError());                                                                      \
         return;                                                                                               \
     }
@@ -1160,8 +1162,8 @@ void launch_merge_parts(const float *pd, const InId *pi, int nparts, int64_t nq,
 }
 
 template void launch_merge_parts<int>(const float *, const int *, int, int64_t, int, int, int64_t, float, float,
-                                      float *, int64_t *, hipStream_t);
+                                      float *, int64_t *, hipStream_t, int64_t, int64_t);
 template void launch_merge_parts<long long>(const float *, const long long *, int, int64_t, int, int, int64_t, float,
-                                            float, float *, int64_t *, hipStream_t);
+                                            float, float *, int64_t *, hipStream_t, int64_t, int64_t);
 
 }  // namespace hipann

@@ -600,6 +600,24 @@ int hipann_merge_topk_device(int metric, int nparts, int64_t nq, int64_t k, cons
     });
 }
 
+int hipann_merge_topk_packed_device(int metric, int nparts, int64_t nq, int64_t k, const void *parts,
+                                    int64_t part_bytes, float *D_out, int64_t *I_out, void *stream, char *eb, int el) {
+    return guard_int(eb, el, [&]() -> int {
+        require_device();
+        HIPANN_REQUIRE(metric == kL2 || metric == kIP, "bad metric");
+        HIPANN_REQUIRE(k > 0 && k <= HIPANN_MAX_K && nparts >= 0, "bad arguments");
+        HIPANN_REQUIRE(part_bytes % 8 == 0 && part_bytes >= nq * k * 12, "part_bytes too small / misaligned");
+        const float sign = metric == kIP ? -1.f : 1.f;
+        const char *base = static_cast<const char *>(parts);
+        // part p: [labels int64 nq*k][distances fp32 nq*k] at base + p * part_bytes
+        launch_merge_parts<long long>(reinterpret_cast<const float *>(base + nq * k * 8),
+                                      reinterpret_cast<const long long *>(base), nparts, nq, (int)k, (int)k, 0, sign,
+                                      sign, D_out, I_out, static_cast<hipStream_t>(stream), part_bytes / 4,
+                                      part_bytes / 8);
+        return 0;
+    });
+}
+
 int64_t hipann_ntotal(void *h) { return h ? static_cast<IndexBase *>(h)->ntotal() : -1; }
 int hipann_dim(void *h) { return h ? static_cast<IndexBase *>(h)->d : -1; }
 int hipann_metric(void *h) { return h ? static_cast<IndexBase *>(h)->metric : -1; }

@@ -291,6 +291,7 @@ void launch_ivf_merge(const float *pd, const int *pi, const int64_t *ids, int64_
                       int k, int kout, float out_sign, float *D, int64_t *I, hipStream_t st);
 template <typename InId>
 void launch_merge_parts(const float *pd, const InId *pi, int nparts, int64_t nq, int k, int kout,
-                        int64_t label_offset, float in_sign, float out_sign, float *D, int64_t *I, hipStream_t st);
+                        int64_t label_offset, float in_sign, float out_sign, float *D, int64_t *I, hipStream_t st,
+                        int64_t pstride_d = -1, int64_t pstride_i = -1);  // part strides (elements); -1: nq*k
 
 }  // namespace hipann

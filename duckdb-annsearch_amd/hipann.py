@@ -93,6 +93,7 @@ def lib() -> C.CDLL:
             "hipann_flat_get_form": ([vp], i32),
             "hipann_flat_rerank_fallbacks": ([vp], i64),
             "hipann_merge_topk_device": ([i32, i32, i64, i64, vp, vp, vp, vp, vp, cp, i32], i32),
+            "hipann_merge_topk_packed_device": ([i32, i32, i64, i64, vp, i64, vp, vp, vp, cp, i32], i32),
             "hipann_ivf_create": ([i32, i32, i32, i32, f, i64p, i64p, f, C.POINTER(C.c_int), i32, cp, i32], vp),
             "hipann_ivf_create_device": ([i32, i32, i32, i32, vp, i64p, vp, vp, i32, i32, cp, i32], vp),
             "hipann_ivf_search": ([vp, i64, f, i64, f, i64p, cp, i32], i32),
@@ -318,6 +319,16 @@ def merge_topk_device(metric: int, nparts: int, nq: int, k: int, d_parts: int, i
     _check(lib().hipann_merge_topk_device(metric, nparts, nq, k, C.c_void_p(d_parts), C.c_void_p(i_parts),
                                           C.c_void_p(d_out), C.c_void_p(i_out), C.c_void_p(stream or None), eb, 1024),
            eb)
+
+
+def merge_topk_packed_device(metric: int, nparts: int, nq: int, k: int, parts: int, part_bytes: int, d_out: int,
+                             i_out: int, stream: int = 0) -> None:
+    """hipann_merge_topk_packed_device: merge of the all-gathered packed parts ([labels int64 nq·k]
+    [distances fp32 nq·k] per part, part_bytes apart) — sharded.py's single-collective layout."""
+    eb = _err()
+    _check(lib().hipann_merge_topk_packed_device(metric, nparts, nq, k, C.c_void_p(parts), part_bytes,
+                                                 C.c_void_p(d_out), C.c_void_p(i_out), C.c_void_p(stream or None), eb,
+                                                 1024), eb)
 
 
 class HipIndexIVFFlat(_Handle):

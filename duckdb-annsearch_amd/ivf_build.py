@@ -7,9 +7,16 @@ MetalIndexIVFFlat.mm:283-326).  FAISS is absent here, so this module does the sa
 25 iterations, seeded init from the sample), assignment of every row with the Flat kernels (k = 1),
 a stable counting sort into list-contiguous storage, and hipann_ivf_create_device on the result.
 
-Multi-GPU: rank 0 trains and broadcasts the centroids; every rank assigns and stores only its own
-rows (its lists' rows come from its shard of the database), so list l is split across ranks by row
-range — equivalent to sharding the lists' contents, and every rank scans only its local rows.
+Training sample: the first 256·nlist rows of the database (identical for every world size, so the
+1/2/4/8-GPU runs search the same lists).
+
+Multi-GPU: rank 0 trains and broadcasts the centroids, then
+  * ``build_ivf_list_shard`` (the default): whole lists are dealt to ranks by size
+    (sharded.assign_lists — the list sizes come from each rank counting its row range, summed by one
+    all-reduce at build time); every rank regenerates the database chunk by chunk (the generators are
+    chunk-seeded, so no rows travel between GPUs), assigns it, and keeps the rows of the lists it owns;
+  * ``build_ivf_shard`` with world > 1: every rank assigns and stores only its own row range, so list l
+    is split across ranks by row range (kept for comparison: perfectly balanced bytes, shorter lists).
 """
 from __future__ import annotations
 
@@ -73,51 +80,114 @@ def build_ivf_shard(torch, hipann, xb, row0: int, n_total: int, nlist: int, npro
 
     dev = xb.device
     n_local, d = xb.shape
-    # ---- train (rank 0) ----
+    # ---- train (rank 0, on the first 256·nlist rows; rank 0 holds them in both layouts) ----
     if rank == 0:
         m = min(n_local, train_points_per_list * nlist)
-        stride = max(1, n_local // m)
-        sample = xb[::stride][:m].contiguous()
-        cen = kmeans(torch, hipann, sample, nlist, seed=centres_seed)
-        del sample
+        cen = kmeans(torch, hipann, xb[:m].contiguous(), nlist, seed=centres_seed)
     else:
         cen = torch.empty((nlist, d), device=dev, dtype=torch.float32)
     if world > 1:
         dist.broadcast(cen, 0)
     cen = cen.contiguous()
-    # ---- assign (Flat kernels, k = 1, chunks of 1M rows) ----
-    stream = torch.cuda.current_stream().cuda_stream
-    assign = torch.empty((n_local,), device=dev, dtype=torch.int64)
-    qidx = hipann.HipIndexFlatDevice(d, metric, cen.data_ptr(), nlist, dev.index, copy=False)
-    chunk = 1_000_000
-    Dc = torch.empty((chunk, 1), device=dev, dtype=torch.float32)
-    Ic = torch.empty((chunk, 1), device=dev, dtype=torch.int64)
-    for s in range(0, n_local, chunk):
-        e = min(n_local, s + chunk)
-        qidx.search_device(e - s, xb[s:e].data_ptr(), 1, Dc.data_ptr(), Ic.data_ptr(), stream)
-        assign[s:e].copy_(Ic[:e - s, 0])
-    torch.cuda.synchronize()
-    qidx.close()
-    del Dc, Ic
+    assign = assign_rows(torch, hipann, cen, xb, metric)
     # ---- list-contiguous storage (stable counting sort) ----
     order = torch.sort(assign, stable=True).indices
     counts = torch.bincount(assign, minlength=nlist)
-    offsets = np.zeros(nlist + 1, np.int64)
-    offsets[1:] = np.cumsum(counts.cpu().numpy())
     codes = torch.empty_like(xb)
-    for s in range(0, n_local, chunk):
-        e = min(n_local, s + chunk)
+    for s in range(0, n_local, ASSIGN_CHUNK):
+        e = min(n_local, s + ASSIGN_CHUNK)
         codes[s:e] = xb[order[s:e]]
     ids = (order + row0).contiguous()
     del order, assign
+    info = {"shard": "rows" if world > 1 else "single"}
+    return _make_index(torch, hipann, d, metric, nlist, nprobe, cen, counts, codes, ids, dev, info)
+
+
+ASSIGN_CHUNK = 1_000_000
+
+
+def assign_rows(torch, hipann, cen, x, metric: int):
+    """Nearest centroid of every row of x (Flat kernels, k = 1, chunks of 1M rows) → int64 CUDA tensor."""
+    n, d = x.shape
+    dev = x.device
+    stream = torch.cuda.current_stream().cuda_stream
+    assign = torch.empty((n,), device=dev, dtype=torch.int64)
+    qidx = hipann.HipIndexFlatDevice(d, metric, cen.data_ptr(), cen.shape[0], dev.index, copy=False)
+    m = min(n, ASSIGN_CHUNK)
+    Dc = torch.empty((m, 1), device=dev, dtype=torch.float32)
+    Ic = torch.empty((m, 1), device=dev, dtype=torch.int64)
+    for s in range(0, n, ASSIGN_CHUNK):
+        e = min(n, s + ASSIGN_CHUNK)
+        qidx.search_device(e - s, x[s:e].data_ptr(), 1, Dc.data_ptr(), Ic.data_ptr(), stream)
+        assign[s:e].copy_(Ic[:e - s, 0])
+    torch.cuda.synchronize()
+    qidx.close()
+    return assign
+
+
+def _make_index(torch, hipann, d, metric, nlist, nprobe, cen, counts, codes, ids, dev, info):
+    offsets = np.zeros(nlist + 1, np.int64)
+    offsets[1:] = np.cumsum(counts.cpu().numpy())
     index = hipann.HipIndexIVFFlat.from_device(d, metric, nlist, nprobe, cen.data_ptr(), offsets, ids.data_ptr(),
                                                codes.data_ptr(), dev.index, copy=False)
     index._keep = (cen, codes, ids)  # borrowed by the library
     index._offsets = offsets
     sizes = np.diff(offsets)
-    info = {"nlist": nlist, "nprobe": nprobe, "list_size_min": int(sizes.min()), "list_size_max": int(sizes.max()),
-            "list_size_mean": float(sizes.mean())}
+    info.update({"nlist": nlist, "nprobe": nprobe, "list_size_min": int(sizes.min()),
+                 "list_size_max": int(sizes.max()), "list_size_mean": float(sizes.mean()),
+                 "rows_local": int(offsets[-1])})
     return index, info
+
+
+def build_ivf_list_shard(torch, hipann, gen_rows, n_total: int, d: int, nlist: int, nprobe: int, metric: int,
+                         rank: int, world: int, dev, centres_seed: int = 1234, train_points_per_list: int = 256):
+    """List-sharded IVF shard of rank `rank`.  ``gen_rows(out, row0)`` fills `out` with
+    global rows [row0, row0 + len(out)) (deterministic, chunk-seeded).  Returns (index over the owned
+    lists, info)."""
+    import torch.distributed as dist
+
+    from sharded import assign_lists, collective_tensor, shard_bounds
+
+    m = min(n_total, train_points_per_list * nlist)
+    if rank == 0:
+        sample = gen_rows(torch.empty((m, d), device=dev, dtype=torch.float32), 0)
+        cen = kmeans(torch, hipann, sample, nlist, seed=centres_seed)
+        del sample
+    else:
+        cen = torch.empty((nlist, d), device=dev, dtype=torch.float32)
+    if world > 1:
+        collective_tensor(cen, lambda t: dist.broadcast(t, 0))
+    cen = cen.contiguous()
+    buf = torch.empty((min(ASSIGN_CHUNK, n_total), d), device=dev, dtype=torch.float32)
+    # list sizes: each rank counts its own row range, one all-reduce sums them (build time only)
+    lo, hi = shard_bounds(n_total, rank, world)
+    counts = torch.zeros(nlist, device=dev, dtype=torch.int64)
+    for s in range(lo, hi, ASSIGN_CHUNK):
+        e = min(hi, s + ASSIGN_CHUNK)
+        x = gen_rows(buf[:e - s], s)
+        counts += torch.bincount(assign_rows(torch, hipann, cen, x, metric), minlength=nlist)
+    if world > 1:
+        collective_tensor(counts, dist.all_reduce)
+    owner = assign_lists(counts.cpu().numpy(), world)
+    mine = torch.from_numpy(owner == rank).to(dev)
+    keep_x, keep_i, keep_a = [], [], []
+    for s in range(0, n_total, ASSIGN_CHUNK):
+        e = min(n_total, s + ASSIGN_CHUNK)
+        x = gen_rows(buf[:e - s], s)
+        a = assign_rows(torch, hipann, cen, x, metric)
+        sel = torch.nonzero(mine[a]).squeeze(1)
+        keep_x.append(x[sel])
+        keep_i.append(sel + s)
+        keep_a.append(a[sel])
+    del buf
+    a = torch.cat(keep_a)
+    order = torch.sort(a, stable=True).indices  # rows of a list stay in ascending global id (insertion order)
+    codes = torch.cat(keep_x)[order].contiguous()
+    ids = torch.cat(keep_i)[order].contiguous()
+    del keep_x, keep_i, keep_a
+    local_counts = torch.bincount(a, minlength=nlist)
+    info = {"shard": "lists", "lists_owned": int(mine.sum())}
+    return _make_index(torch, hipann, d, metric, nlist, nprobe, cen, local_counts, codes, ids, dev, info)
 
 
 def scan_bytes(index, probes: np.ndarray, d: int) -> float:

@@ -1,15 +1,25 @@
-"""sharded — one-process-per-GPU sharded search with a single all-gather of per-shard top-k.
+"""sharded — one-process-per-GPU sharded search with ONE all-gather of per-shard top-k.
 
 The reference has no multi-device code (SURVEY §2a "Parallelism and communication"); this is the
-MI355X-native addition of SURVEY §8e: database rows (Flat) or the rows of every IVF list are split
-into contiguous ranges, one per rank; every rank searches only its range on its own GPU; the per-rank
-top-k (nq × k × (4 + 8) bytes — 123 KB at nq = 1024, k = 10) is all-gathered over RCCL (xGMI) and
-merged on every rank with the same (distance, label) order the single-GPU path uses.  There is no
-other data-path collective: the queries are replicated, the database never moves.
+MI355X-native addition of SURVEY §8e:
+
+* Flat: database rows split into contiguous ranges, one per rank (``shard_bounds``);
+* IVFFlat: whole inverted lists dealt to ranks by size-balanced greedy assignment, largest first onto
+  the least-loaded rank (``assign_lists``) — every rank replicates the 3 MB coarse quantizer and scans
+  only the probed lists it owns.
+
+Every rank searches only its shard on its own GPU, with labels already global.  Its top-k is packed
+into one buffer per rank — ``[labels int64 nq·k][distances fp32 nq·k]``, 12·nq·k bytes (123 KB at
+nq = 1024, k = 10) — and moved by a single ``all_gather_into_tensor`` over RCCL (xGMI), then merged on
+every rank with the same (distance, label) order the single-GPU path uses
+(``hipann_merge_topk_packed_device``).  There is no other data-path collective: queries are
+replicated, the database never moves.
 """
 from __future__ import annotations
 
-from typing import Callable, Tuple
+from typing import Callable, Sequence, Tuple
+
+import numpy as np
 
 
 def shard_bounds(n: int, rank: int, world: int) -> Tuple[int, int]:
@@ -19,55 +29,112 @@ def shard_bounds(n: int, rank: int, world: int) -> Tuple[int, int]:
     return rank * n // world, (rank + 1) * n // world
 
 
-class ShardedSearch:
-    """Glue between a per-rank search and the all-gather + merge.
+def assign_lists(list_sizes: Sequence[int], world: int) -> np.ndarray:
+    """Size-balanced list → rank map: lists sorted by size (largest first, stable), each dealt to the
+    currently least-loaded rank (ties → lowest rank).  The same rule hipann_ivf_create uses for the
+    in-process multi-device index (ivf.cpp)."""
+    sizes = np.asarray(list_sizes, np.int64)
+    owner = np.zeros(len(sizes), np.int64)
+    if world <= 1:
+        return owner
+    load = np.zeros(world, np.int64)
+    for l in np.argsort(-sizes, kind="stable"):
+        r = int(np.argmin(load))
+        owner[l] = r
+        load[r] += sizes[l]
+    return owner
 
-    ``local_search(xq) -> (D, I)``: this rank's top-k, I holding GLOBAL labels (−1 pads).
-    ``merge(D_all, I_all) -> (D, I)``: merge of [world][nq][k] partials (the GPU path passes
-    hipann.merge_topk_device; tests may pass a host implementation of the same order).
+
+def part_bytes(nq: int, k: int) -> int:
+    """Bytes of one rank's packed top-k: int64 labels then fp32 distances, padded to 8 B."""
+    b = nq * k * 12
+    return (b + 7) // 8 * 8
+
+
+def unpack_parts(gathered, nq: int, k: int):
+    """[world][part_bytes] uint8 → (D [world][nq][k] fp32, I [world][nq][k] int64) (host merges, tests)."""
+    world = gathered.shape[0]
+    import torch
+
+    lab = gathered[:, : nq * k * 8].contiguous().view(torch.int64).reshape(world, nq, k)
+    dis = gathered[:, nq * k * 8: nq * k * 12].contiguous().view(torch.float32).reshape(world, nq, k)
+    return dis, lab
+
+
+class ShardedSearch:
+    """Glue between a per-rank search and the single all-gather + merge.
+
+    ``local_search(xq, D, I)``: writes this rank's top-k into the (nq, k) views D (fp32) and I (int64,
+    GLOBAL labels, −1 pads) — views into the packed buffer the collective sends.
+    ``merge(gathered, nq, k) -> (D, I)``: merge of the [world][part_bytes] uint8 buffer (the GPU path
+    passes ``merge_packed_device_torch``; CPU tests a host restatement via ``unpack_parts``).
     Works with any torch.distributed backend (nccl = RCCL on ROCm; gloo for CPU tests).
     """
 
-    def __init__(self, local_search: Callable, merge: Callable, group=None):
+    def __init__(self, local_search: Callable, merge: Callable, nq: int, k: int, device, group=None):
+        import torch
         import torch.distributed as dist
 
         self.local_search = local_search
         self.merge = merge
         self.group = group
+        self.nq, self.k = nq, k
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.pb = part_bytes(nq, k)
+        self.packed = torch.zeros(self.pb, dtype=torch.uint8, device=device)
+        self.I = self.packed[: nq * k * 8].view(torch.int64).view(nq, k)
+        self.D = self.packed[nq * k * 8: nq * k * 12].view(torch.float32).view(nq, k)
+        self.gathered = torch.empty((self.world, self.pb), dtype=torch.uint8, device=device) if self.world > 1 \
+            else None
 
     def search(self, xq):
-        import torch
         import torch.distributed as dist
 
-        D, I = self.local_search(xq)
+        self.local_search(xq, self.D, self.I)
         if self.world == 1:
-            return D, I
-        if D.is_cuda:  # RCCL: gather straight into the [world][nq][k] buffers the merge reads
-            if getattr(self, "_bufs", None) is None or self._bufs[0].shape[1:] != D.shape:
-                self._bufs = (torch.empty((self.world, *D.shape), device=D.device, dtype=D.dtype),
-                              torch.empty((self.world, *I.shape), device=I.device, dtype=I.dtype))
-            Da, Ia = self._bufs
-            dist.all_gather_into_tensor(Da, D.contiguous(), group=self.group)
-            dist.all_gather_into_tensor(Ia, I.contiguous(), group=self.group)
-            return self.merge(Da, Ia)
-        Dl = [torch.empty_like(D) for _ in range(self.world)]
-        Il = [torch.empty_like(I) for _ in range(self.world)]
-        dist.all_gather(Dl, D.contiguous(), group=self.group)
-        dist.all_gather(Il, I.contiguous(), group=self.group)
-        return self.merge(torch.stack(Dl), torch.stack(Il))
+            return self.D, self.I
+        if self.packed.is_cuda and dist.get_backend(self.group) == "nccl":
+            # RCCL: one collective straight into the buffer the merge reads
+            dist.all_gather_into_tensor(self.gathered.view(-1), self.packed, group=self.group)
+        else:  # gloo (CPU tests; GPU tests with several ranks on one device): the same bytes via host memory
+            host = self.packed.cpu()
+            parts = [torch_empty_like_cpu(host) for _ in range(self.world)]
+            dist.all_gather(parts, host, group=self.group)
+            for r, p in enumerate(parts):
+                self.gathered[r].copy_(p)
+        return self.merge(self.gathered, self.nq, self.k)
 
 
-def merge_topk_device_torch(hipann, metric: int):
-    """The GPU merge as a ``merge`` callable for ShardedSearch (torch CUDA tensors in / out)."""
+def torch_empty_like_cpu(t):
     import torch
 
-    def merge(D_all, I_all):
-        world, nq, k = D_all.shape
-        D = torch.empty((nq, k), device=D_all.device, dtype=torch.float32)
-        I = torch.empty((nq, k), device=D_all.device, dtype=torch.int64)
-        hipann.merge_topk_device(metric, world, nq, k, D_all.data_ptr(), I_all.data_ptr(), D.data_ptr(),
-                                 I.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    return torch.empty_like(t, device="cpu")
+
+
+def collective_tensor(t, op, group=None):
+    """Run an in-place collective (``op(tensor)``: broadcast / all_reduce) on `t`, through host memory when
+    the backend is not RCCL (gloo cannot reduce device tensors in every build)."""
+    import torch.distributed as dist
+
+    if not t.is_cuda or dist.get_backend(group) == "nccl":
+        op(t)
+        return t
+    h = t.cpu()
+    op(h)
+    t.copy_(h)
+    return t
+
+
+def merge_packed_device_torch(hipann, metric: int):
+    """The GPU merge of packed parts as a ``merge`` callable for ShardedSearch."""
+    import torch
+
+    def merge(gathered, nq, k):
+        world, pb = gathered.shape
+        D = torch.empty((nq, k), device=gathered.device, dtype=torch.float32)
+        I = torch.empty((nq, k), device=gathered.device, dtype=torch.int64)
+        hipann.merge_topk_packed_device(metric, world, nq, k, gathered.data_ptr(), pb, D.data_ptr(), I.data_ptr(),
+                                        torch.cuda.current_stream().cuda_stream)
         return D, I
 
     return merge

@@ -117,6 +117,13 @@ int hipann_merge_topk_device(int metric, int nparts, int64_t nq, int64_t k, cons
                              const int64_t *I_parts, float *D_out, int64_t *I_out, void *stream,
                              char *err_buf, int err_len);
 
+/* The same merge over packed parts, the layout of ONE all-gather (sharded.py): part p sits at
+ * parts + p*part_bytes and holds [labels int64 nq*k][distances fp32 nq*k] (part_bytes >= 12*nq*k, a
+ * multiple of 8).  One collective moves each rank's distances and labels together. */
+int hipann_merge_topk_packed_device(int metric, int nparts, int64_t nq, int64_t k, const void *parts,
+                                    int64_t part_bytes, float *D_out, int64_t *I_out, void *stream,
+                                    char *err_buf, int err_len);
+
 /* ---------------------------------------------------------------------------------------------
  * IVFFlat — replaces index_cpu_to_metal_ivf + MetalIndexIVFFlat (MetalIndexIVFFlat.mm:283-326,
  * :122-256).  Lists are given in CSR form exactly as FAISS's ArrayInvertedLists hold them:

@@ -1,10 +1,15 @@
-"""World-size-2 gloo test of the sharded (multi-GPU) search orchestration on the CPU.
+"""World-size-2 tests of the sharded (multi-GPU) search orchestration.
 
-Each rank searches its contiguous row range (the oracle stands in for the per-GPU shard search: it is
-the same semantic contract the GPU parity tests check), the per-rank top-k is all-gathered through
-ShardedSearch (the class bench.py uses over RCCL), and merged with a host restatement of
-merge_parts_topk's (distance, label) order.  The result must equal the single-process search over the
-whole database.
+CPU (gloo): each rank searches its shard — contiguous rows (Flat) or the whole lists it owns by the
+size-balanced assignment (IVF) — with the oracle standing in for the per-GPU search (the same semantic
+contract the GPU parity tests check); the per-rank top-k travels as ONE packed buffer through
+ShardedSearch (the class bench.py uses over RCCL) and is merged with a host restatement of
+merge_parts_topk's (distance, label) order.  The result must equal the single-process search.
+
+GPU (gloo transport, both ranks on device 0 — RCCL needs one device per rank and the box has one):
+the real per-rank HIP searches (HipIndexFlatDevice with label_offset; build_ivf_list_shard's
+list-sharded IVF) and the device merge (hipann_merge_topk_packed_device), against the oracle over
+the whole database.
 """
 from __future__ import annotations
 
@@ -27,46 +32,54 @@ def _free_port():
     return p
 
 
-def host_merge(D_all, I_all, metric):
-    """Host restatement of merge_parts_topk: k best of the union by (key, label), key = D (L2) or −D (IP)."""
+def host_merge(gathered, nq, k, metric):
+    """Host restatement of merge_parts_topk over the packed parts: k best of the union by (key, label),
+    key = D (L2) or −D (IP)."""
     import torch
+    from sharded import unpack_parts
 
-    world, nq, k = D_all.shape
+    D_all, I_all = unpack_parts(gathered.cpu(), nq, k)
+    world = D_all.shape[0]
     D = np.asarray(D_all.permute(1, 0, 2).reshape(nq, world * k))
     I = np.asarray(I_all.permute(1, 0, 2).reshape(nq, world * k))
     key = D if metric == 0 else -D
     outD = np.full((nq, k), np.inf if metric == 0 else -np.inf, np.float32)
     outI = np.full((nq, k), -1, np.int64)
     for q in range(nq):
-        cand = [(key[q, j], I[q, j]) for j in range(world * k) if I[q, j] >= 0]
-        cand.sort()
+        cand = sorted((key[q, j], I[q, j]) for j in range(world * k) if I[q, j] >= 0)
         for j, (kv, lab) in enumerate(cand[:k]):
             outD[q, j] = kv if metric == 0 else -kv
             outI[q, j] = lab
     return torch.from_numpy(outD), torch.from_numpy(outI)
 
 
-def _worker(rank, world, port, metric, result_path):
+def _setup(rank, world, port):
     sys.path.insert(0, str(ROOT))
     sys.path.insert(0, str(ROOT / "duckdb-annsearch_amd"))
     sys.path.insert(0, str(ROOT / "tests"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    import torch
     import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    return dist
+
+
+def _worker_flat(rank, world, port, metric, result_path):
+    dist = _setup(rank, world, port)
+    import torch
     from oracle import oracle as O
     from sharded import ShardedSearch, shard_bounds
     from _data import faiss_metal_case
 
-    dist.init_process_group("gloo", rank=rank, world_size=world)
     xb, xq = faiss_metal_case(3001, 25, 48)
     lo, hi = shard_bounds(len(xb), rank, world)
 
-    def local(q):
-        D, I = O.flat_search(xb[lo:hi], q.numpy(), 12, metric, label_offset=lo)
-        I = np.where(I >= 0, I, -1)
-        return torch.from_numpy(D), torch.from_numpy(I)
+    def local(q, D, I):
+        Dl, Il = O.flat_search(xb[lo:hi], q.numpy(), 12, metric, label_offset=lo)
+        D.copy_(torch.from_numpy(Dl))
+        I.copy_(torch.from_numpy(np.where(Il >= 0, Il, -1)))
 
-    s = ShardedSearch(local, lambda Da, Ia: host_merge(Da, Ia, metric))
+    s = ShardedSearch(local, lambda g, nq, k: host_merge(g, nq, k, metric), 25, 12, "cpu")
     D, I = s.search(torch.from_numpy(xq))
     if rank == 0:
         np.savez(result_path, D=D.numpy(), I=I.numpy())
@@ -75,18 +88,95 @@ def _worker(rank, world, port, metric, result_path):
 
 
 @pytest.mark.parametrize("metric", [0, 1])
-def test_sharded_search_gloo_world2(tmp_path, metric):
+def test_sharded_flat_gloo_world2(tmp_path, metric):
     import torch.multiprocessing as mp
     from oracle import oracle as O
     from _data import faiss_metal_case
 
     out = tmp_path / "res.npz"
-    mp.spawn(_worker, args=(2, _free_port(), metric, str(out)), nprocs=2, join=True)
+    mp.spawn(_worker_flat, args=(2, _free_port(), metric, str(out)), nprocs=2, join=True)
     r = np.load(out)
     xb, xq = faiss_metal_case(3001, 25, 48)
     Do, Io = O.flat_search(xb, xq, 12, metric)
     assert np.array_equal(r["I"], Io)
     assert np.allclose(r["D"], Do, rtol=1e-6)
+
+
+def _worker_ivf_lists(rank, world, port, result_path):
+    dist = _setup(rank, world, port)
+    import torch
+    from oracle import oracle as O
+    from sharded import ShardedSearch, assign_lists
+    from _data import build_ivf_lists, faiss_metal_case
+
+    xb, xq = faiss_metal_case(6000, 30, 40)
+    cen = np.ascontiguousarray(xb[::200][:30])
+    off, ids, codes = build_ivf_lists(xb, cen)
+    owner = assign_lists(np.diff(off), world)
+    # this rank's lists only (the others empty), every centroid kept: the coarse step is replicated
+    keep = np.concatenate([np.arange(off[l], off[l + 1]) for l in range(len(cen)) if owner[l] == rank])
+    loff = np.zeros(len(cen) + 1, np.int64)
+    loff[1:] = np.cumsum(np.where(owner == rank, np.diff(off), 0))
+
+    def local(q, D, I):
+        Dl, Il, _ = O.ivf_search(cen, loff, ids[keep], codes[keep], q.numpy(), 10, 7)
+        D.copy_(torch.from_numpy(Dl))
+        I.copy_(torch.from_numpy(np.where(Il >= 0, Il, -1)))
+
+    s = ShardedSearch(local, lambda g, nq, k: host_merge(g, nq, k, 0), 30, 10, "cpu")
+    D, I = s.search(torch.from_numpy(xq))
+    if rank == 0:
+        np.savez(result_path, D=D.numpy(), I=I.numpy(), owner=owner)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_ivf_list_ownership_gloo_world2(tmp_path):
+    """IVF list sharding (north_star: "IVF lists shard across the GPUs"): every rank owns whole lists by
+    size, scans the probed lists it owns; the merged result equals the single-index IVF search."""
+    import torch.multiprocessing as mp
+    from oracle import oracle as O
+    from _data import build_ivf_lists, faiss_metal_case
+
+    out = tmp_path / "res.npz"
+    mp.spawn(_worker_ivf_lists, args=(2, _free_port(), str(out)), nprocs=2, join=True)
+    r = np.load(out)
+    xb, xq = faiss_metal_case(6000, 30, 40)
+    cen = np.ascontiguousarray(xb[::200][:30])
+    off, ids, codes = build_ivf_lists(xb, cen)
+    Do, Io, _ = O.ivf_search(cen, off, ids, codes, xq, 10, 7)
+    assert np.array_equal(r["I"], Io)
+    assert np.allclose(r["D"], Do, rtol=1e-6)
+    assert set(np.unique(r["owner"]).tolist()) == {0, 1}
+
+
+def test_assign_lists_balances_sizes():
+    sys.path.insert(0, str(ROOT / "duckdb-annsearch_amd"))
+    from sharded import assign_lists
+    rng = np.random.default_rng(3)
+    sizes = rng.integers(7000, 12000, 1024)
+    for w in (1, 2, 4, 8):
+        owner = assign_lists(sizes, w)
+        load = np.bincount(owner, weights=sizes, minlength=w)
+        assert owner.min() == 0 and owner.max() == w - 1 if w > 1 else owner.max() == 0
+        assert load.max() / load.mean() < 1.002
+
+
+def test_packed_parts_layout():
+    """One rank's packed top-k: int64 labels then fp32 distances, 8-B aligned; unpack restores both."""
+    import torch
+    sys.path.insert(0, str(ROOT / "duckdb-annsearch_amd"))
+    from sharded import part_bytes, unpack_parts
+    for nq, k in ((1, 1), (3, 5), (1024, 10)):
+        pb = part_bytes(nq, k)
+        assert pb % 8 == 0 and pb >= 12 * nq * k
+        g = torch.zeros((2, pb), dtype=torch.uint8)
+        for r in range(2):
+            g[r, : nq * k * 8].view(torch.int64).copy_(torch.arange(nq * k) + 100 * r)
+            g[r, nq * k * 8: nq * k * 12].view(torch.float32).copy_(torch.arange(nq * k, dtype=torch.float32) / 2 + r)
+        D, I = unpack_parts(g, nq, k)
+        assert D.shape == (2, nq, k) and I.shape == (2, nq, k)
+        assert int(I[1, 0, 0]) == 100 and float(D[1, 0, 0]) == 1.0
 
 
 def test_shard_bounds_cover_rows():
@@ -97,3 +187,87 @@ def test_shard_bounds_cover_rows():
             b = [shard_bounds(n, r, w) for r in range(w)]
             assert b[0][0] == 0 and b[-1][1] == n
             assert all(b[i][1] == b[i + 1][0] for i in range(w - 1))
+
+
+# ------------------------------------------------------------------------------------------------
+# GPU: the real per-rank HIP searches + device merge, two ranks on device 0 (gloo transport)
+# ------------------------------------------------------------------------------------------------
+def _worker_gpu(rank, world, port, workload, result_path):
+    dist = _setup(rank, world, port)
+    import torch
+    import hipann
+    import bench
+    from sharded import ShardedSearch, merge_packed_device_torch, shard_bounds
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    n, d, nq, k = 60_000, 96, 200, 10
+    stream = torch.cuda.current_stream().cuda_stream
+    xq = bench.uniform_queries(torch, nq, d, dev)
+    if workload == "flat":
+        lo, hi = shard_bounds(n, rank, world)
+        xb = torch.empty((hi - lo, d), device=dev)
+        bench.gen_uniform_rows(torch, xb, lo, 42)
+        index = hipann.HipIndexFlatDevice(d, 0, xb.data_ptr(), hi - lo, 0, copy=False, label_offset=lo)
+        extra = {}
+    else:
+        from ivf_build import build_ivf_list_shard
+        gen = lambda out, row0: bench.gen_uniform_rows(torch, out, row0, 42)  # noqa: E731
+        index, info = build_ivf_list_shard(torch, hipann, gen, n, d, 64, 8, 0, rank, world, dev)
+        cen, codes, ids = index._keep
+        extra = {f"cen{rank}": cen.cpu().numpy(), f"ids{rank}": ids.cpu().numpy(), f"off{rank}": index._offsets,
+                 f"codes{rank}": codes.cpu().numpy()}
+
+    def local(q, D, I):
+        index.search_device(nq, q.data_ptr(), k, D.data_ptr(), I.data_ptr(), stream)
+
+    s = ShardedSearch(local, merge_packed_device_torch(hipann, 0), nq, k, dev)
+    D, I = s.search(xq)
+    torch.cuda.synchronize()
+    np.savez(f"{result_path}.{rank}.npz", D=D.cpu().numpy(), I=I.cpu().numpy(), xq=xq.cpu().numpy(), **extra)
+    dist.barrier()
+    index.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("workload", ["flat", "ivf_lists"])
+def test_sharded_hip_world2_on_one_device(gpu, oracle, tmp_path, workload):
+    """two processes, each running the real HIP shard search (Flat row shards with
+    label_offset / list-sharded IVF from build_ivf_list_shard), one packed all-gather, the device merge
+    kernel; the merged top-k equals the oracle's over the whole database (IVF: the lists the two ranks
+    own partition the single index's lists, and the probe lists are the replicated coarse step's)."""
+    import torch
+    import torch.multiprocessing as mp
+    import bench
+    from _data import check_topk_parity
+
+    res = str(tmp_path / "res")
+    mp.spawn(_worker_gpu, args=(2, _free_port(), workload, res), nprocs=2, join=True)
+    r0, r1 = np.load(res + ".0.npz"), np.load(res + ".1.npz")
+    assert np.array_equal(r0["I"], r1["I"]) and np.array_equal(r0["D"], r1["D"])  # every rank merges the same
+    n, d = 60_000, 96
+    xb = bench.gen_uniform_rows(torch, torch.empty((n, d), device="cuda"), 0, 42).cpu().numpy()
+    xq = r0["xq"]
+    if workload == "flat":
+        Do, Io = oracle.flat_search(xb, xq, 10)
+    else:
+        cen = r0["cen0"]
+        assert np.array_equal(cen, r1["cen1"])
+        len0, len1 = np.diff(r0["off0"]), np.diff(r1["off1"])
+        assert not np.any((len0 > 0) & (len1 > 0))            # every list lives on one rank
+        assert len0.sum() + len1.sum() == n and min(len0.sum(), len1.sum()) > 0.4 * n
+        # the single index those two shards partition: list l from its owner, rows in ascending id
+        parts = [(r0["off0"], r0["ids0"], r0["codes0"]), (r1["off1"], r1["ids1"], r1["codes1"])]
+        off = np.zeros(len(cen) + 1, np.int64)
+        off[1:] = np.cumsum(len0 + len1)
+        ids = np.concatenate([p[1][p[0][l]:p[0][l + 1]] for l in range(len(cen)) for p in parts])
+        codes = np.concatenate([p[2][p[0][l]:p[0][l + 1]] for l in range(len(cen)) for p in parts])
+        assert np.array_equal(np.sort(ids), np.arange(n)) and np.array_equal(codes, xb[ids])
+        assert all(np.all(np.diff(ids[off[l]:off[l + 1]]) > 0) for l in range(len(cen)))
+        # the GPU assignment is the nearest centroid (up to fp32 near-ties) — the oracle's, mostly
+        _, a = oracle.flat_search(cen, xb[ids], 1)
+        lab = np.repeat(np.arange(len(cen)), np.diff(off))
+        assert (a[:, 0] == lab).mean() > 0.999
+        Do, Io, _ = oracle.ivf_search(cen, off, ids, codes, xq, 10, 8)
+    check_topk_parity(xb, xq, r0["D"], r0["I"], Do, Io, 0)
