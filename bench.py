@@ -227,7 +227,11 @@ def attach_traffic(roof, key, algorithmic_bytes):
 # ------------------------------------------------------------------------------------------------
 # Flat
 # ------------------------------------------------------------------------------------------------
-FLAT_FORMS = {0: ("flat_gemm_topk2", 1, FP32_MFMA_PEAK_TF, "fp32 MFMA (v_mfma_f32_32x32x2_f32)"),
+FLAT_FORMS = {4: ("flat_bf16_topk", 1, BF16_MFMA_PEAK_TF,
+                  "bf16 MFMA (v_mfma_f32_32x32x16_bf16), one bf16 product per fp32 product over a tiled bf16 image of the "
+                  "rows; the scan keeps 16 (IP: 32) per (split, query) as a filter, merge_ms = exact fp32 direct-form "
+                  "rerank + bound check (E = 2^-7·(|q|²+max|x|²))"),
+              0: ("flat_gemm_topk2", 1, FP32_MFMA_PEAK_TF, "fp32 MFMA (v_mfma_f32_32x32x2_f32)"),
               1: ("flat_gemm_topk_bf", 6, BF16_MFMA_PEAK_TF,
                   "bf16 MFMA (v_mfma_f32_32x32x16_bf16) over a 3-term split: 6 bf16 products per fp32 product"),
               2: ("flat_gemm_topk_bf", 3, BF16_MFMA_PEAK_TF,
@@ -250,7 +254,8 @@ def flat_config(args, torch, dist, hipann, rank, world, dev, n, d, nq, k, metric
     gen_uniform_rows(torch, xb, lo, 42)
     xq = uniform_queries(torch, nq, d, dev)
     index = hipann.HipIndexFlatDevice(d, metric, xb.data_ptr(), n_local, dev.index, copy=False, label_offset=lo)
-    index.form = int(os.environ.get("HIPANN_FLAT_FORM", "3"))
+    if os.environ.get("HIPANN_FLAT_FORM"):  # A/B; the library default is form 4 (bf16 filter + exact rerank)
+        index.form = int(os.environ["HIPANN_FLAT_FORM"])
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t_setup
 
@@ -292,7 +297,7 @@ def flat_config(args, torch, dist, hipann, rank, world, dev, n, d, nq, k, metric
     # batch, and against the CPU oracle (FAISS BLAS-path restatement) on a query subset
     if alt_forms:
         alt = {}
-        for f in (0, 1):
+        for f in (0, 1, 3):
             if f == form:
                 continue
             index.form = f

@@ -56,7 +56,12 @@ constexpr int kFlatRerankKIP = 32;
 // (default): the 2-term scan keeps kRerankK rows per database split and query as a filter, every
 // returned distance is recomputed exactly in the direct form with the IVF exact form's bound check
 // (ivf_rerank_topk), failures re-run on kFlatSplit3; kout <= kRerankMaxK (else kFlatSplit3).
-enum FlatForm : int { kFlatFp32 = 0, kFlatSplit3 = 1, kFlatSplit2 = 2, kFlatSplit2Exact = 3 };
+// kFlatBf16Exact (default): the same filter + rerank on ONE plain bf16 product per element (flat_bf16.hip:
+// a tiled bf16 image of the database built once; 32 kept per (split, query); the rerank's bound is the
+// Cauchy-Schwarz bound of the actual bf16 rounding residuals), failures re-run on kFlatSplit3.
+enum FlatForm : int { kFlatFp32 = 0, kFlatSplit3 = 1, kFlatSplit2 = 2, kFlatSplit2Exact = 3, kFlatBf16Exact = 4 };
+// rerank bound E = eps·(‖q‖² + max‖x‖²) of the 2-term split scans' filters
+constexpr float kSplit2Eps = 0x1p-12f;
 __host__ __device__ inline bool ivf_form_split(int f) { return f == kFormSplit3 || f == kFormSplit2; }
 __host__ __device__ inline int ivf_form_terms(int f) { return f == kFormSplit3 ? 3 : 2; }
 

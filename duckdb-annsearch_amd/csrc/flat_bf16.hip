@@ -1,0 +1,327 @@
+// flat_bf16.hip — Flat exact form on the plain bf16 matrix cores (form kFlatBf16Exact, the default).
+//
+// Replaces the GEMM + select half of MetalIndexFlat::search (faiss-metal/src/MetalIndexFlat.mm:294-369;
+// MetalDistance.mm:107-288 simdgroup_gemm_l2_fused, MetalSelect.mm:31-74 warp/block select) for
+// nq >= 20 (FAISS's BLAS path).  One q·x product per element instead of the split forms' three:
+//
+//   * the database is converted ONCE (at the first search after an add) into a tiled bf16 image, and
+//     every batch's queries into the same layout: tile of R rows, chunk of 32 dims = R·4 units of 16 B,
+//     unit b16_slot(c, row) = dims 8c..8c+7 of the row, XOR-swizzled so that the 16-B fragment reads of
+//     v_mfma_f32_32x32x16_bf16 (16-lane groups of 16 distinct rows) and the linear staging writes are
+//     bank-conflict free.  A chunk of a tile is 16 KB of consecutive HBM: the block copies it with one
+//     coalesced 16-B load per thread per unit, no conversion in the loop;
+//   * block = W waves, tile = 32W queries × 256 database rows; A (queries) and B (rows) chunks
+//     double-buffered in LDS, one barrier per chunk; wave w owns queries [32w, 32w+32) × all 256 rows
+//     (8 accumulators of 32×32), so a query's candidates never leave its wave;
+//   * the epilogue (once per tile) filters keys straight from the accumulators: 2·ip − ‖x‖² ≥
+//     ‖q‖² − thr is one fma + one compare per element (key = ‖q‖² + ‖x‖² − 2·ip, thr = the query's
+//     k-th kept key; IP: 2·ip ≥ −2·thr); a ballot per accumulator row sends the rare passing rows to
+//     the WaveList insert (exact keys, (key, row) order).  The filter's rounding (a few ulps of the
+//     key magnitudes) is covered by the rerank bound's margin (below);
+//   * output: the k best (key, row) per (database split, query), query-major, for ivf_rerank_topk.
+//
+// Exactness (ivf_rerank_topk, shared with the IVF exact form): the 32 best scan keys per (split, query)
+// are merged to 32, recomputed in the fp32 direct form and ordered by (distance, label).  The scan key of
+// any row differs from its fp32 distance by at most the Cauchy-Schwarz bound of the bf16 rounding,
+// |q̂·x̂ − q·x| ≤ ‖q‖·‖x̂−x‖ + ‖q̂−q‖·‖x̂‖, with ‖x̂−x‖ ≤ rxmax (the largest row residual, measured when the
+// image is built) and this query's own residual, plus the fp32 accumulation and rounding terms (the
+// kernel's comment).  For U(−1,1) rows at d = 768 that is ≈1.3 against a ≈5 gap between the 10th and 32nd
+// distances of 10M rows; a query whose k-th exact distance is not below K₃₂ − E re-runs on the 3-term
+// split form.
+#include "runtime.hpp"
+#include "wave_topk.hpp"
+
+namespace hipann {
+
+typedef __bf16 b16x8 __attribute__((ext_vector_type(8)));
+typedef float b16_f32x8 __attribute__((ext_vector_type(8)));
+typedef float b16_f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned b16_u32x4 __attribute__((ext_vector_type(4)));  // 16-B unit (native vector: stays in VGPRs)
+
+constexpr int B16_TN = 256;  // database rows per tile
+constexpr int B16_KC = 32;   // dims per chunk
+
+__host__ __device__ inline int b16_nk(int d) { return (d + B16_KC - 1) / B16_KC; }
+// 16-B unit of (group c, row) in a chunk image of R rows
+__device__ __forceinline__ int b16_slot(int c, int row, int R) { return c * R + (row ^ (c << 1)); }
+
+// Tiled bf16 image of an n × d fp32 matrix, tiles of R rows: unit u = ((t·nk + kc)·4 + c)·R + (row ^ 2c)
+// holds RNE bf16 of dims kc·32 + 8c .. +7 of row t·R + row (zero past n / d).  One thread per unit.
+__global__ void __launch_bounds__(256) b16_tile_rows(const float *__restrict__ X, int64_t n, int d, int R, int nk,
+                                                     int64_t total, uint4 *__restrict__ out) {
+    const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (u >= total) return;
+    const int rr = (int)(u % R);
+    int64_t rest = u / R;
+    const int c = (int)(rest & 3);
+    rest >>= 2;
+    const int kc = (int)(rest % nk);
+    const int64_t t = rest / nk;
+    const int row = rr ^ (c << 1);
+    const int64_t grow = t * R + row;
+    const int dim0 = kc * B16_KC + 8 * c;
+    b16_f32x8 v;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = (grow < n && dim0 + i < d) ? X[grow * (int64_t)d + dim0 + i] : 0.f;
+    const b16x8 b = __builtin_convertvector(v, b16x8);
+    out[u] = __builtin_bit_cast(uint4, b);
+}
+
+// ‖bf16(x) − x‖² per row (one wave per row): the largest is the rerank bound's row term.
+__global__ void __launch_bounds__(256) b16_row_residual2(const float *__restrict__ X, int64_t n, int d,
+                                                         float *__restrict__ out) {
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= n) return;
+    const int lane = threadIdx.x & 63;
+    const float *x = X + row * (int64_t)d;
+    float s = 0.f;
+    for (int e = lane; e < d; e += 64) {
+        const float r = x[e] - (float)(__bf16)x[e];
+        s = fmaf(r, r, s);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) out[row] = s;
+}
+
+// Epilogue of one tile: acc[j] = q·x of query rows (r&3) + 8(r>>2) + 4h (+ 32·wave) and database row
+// x0 + 32j + (lane & 31).  cth[r] = ‖q‖² − thr (L2) or −2·thr (IP); xnv[j] = ‖x‖² (L2) or 0, +inf past N.
+template <bool L2M>
+__device__ __forceinline__ void b16_epilogue(const b16_f32x16 (&acc)[8], float (&cth)[16], const float (&qnv)[16],
+                                             const float (&xnv)[8], int64_t x0, int64_t N, float *__restrict__ Ld,
+                                             int *__restrict__ Li, int k, int wave, int lane) {
+    const int l31 = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) any |= fmaf(2.f, acc[j][r], -xnv[j]) >= cth[r];
+        const unsigned long long m = __ballot(any);
+        if (m == 0ull) continue;
+        // slow path (rare after the first tiles): each half of the wave is one query
+        float key[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float kv;
+            if (L2M) {
+                kv = fmaf(-2.f, acc[j][r], qnv[r] + xnv[j]);
+                kv = kv < 0.f ? 0.f : kv;
+            } else {
+                kv = -acc[j][r];
+            }
+            key[j] = x0 + 32 * j + l31 < N ? kv : __builtin_inff();
+        }
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            if (((m >> (32 * hh)) & 0xffffffffull) == 0ull) continue;
+            const int ql = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            const int src = 32 * hh + l31;
+            WaveList<1, int> L;
+            L.d[0] = lane < k ? Ld[ql * k + lane] : __builtin_inff();
+            L.id[0] = lane < k ? Li[ql * k + lane] : 0x7fffffff;
+#pragma unroll
+            for (int o = 0; o < 4; ++o) {
+                const float c0 = __shfl(key[2 * o], src), c1 = __shfl(key[2 * o + 1], src);
+                const float v = lane < 32 ? c0 : c1;
+                const int64_t col = x0 + 32 * (2 * o + h) + l31;
+                L.offer(v, col < N ? (int)col : 0x7fffffff, k - 1);
+            }
+            if (lane < k) {
+                Ld[ql * k + lane] = L.d[0];
+                Li[ql * k + lane] = L.id[0];
+            }
+            const float nt = readlane_f(L.d[0], k - 1);
+            if (h == hh) cth[r] = L2M ? qnv[r] - nt : -2.f * nt;
+        }
+    }
+}
+
+typedef __attribute__((address_space(3))) void b16_lds_void;
+
+template <int N>
+__device__ __forceinline__ void b16_wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <bool L2M, int W>
+__global__ void __launch_bounds__(64 * W, 1)
+flat_bf16_topk(const b16_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm, int64_t nq,
+               const b16_u32x4 *__restrict__ Xt,
+               const float *__restrict__ xnorm, int64_t N, int nk, int k, int nqt, int nsplit,
+               int64_t tiles_per_split, float *__restrict__ part_d, int *__restrict__ part_i) {
+    constexpr int QM = 32 * W;
+    constexpr int AU = QM * 4, BU = B16_TN * 4;  // 16-B units per chunk image
+    constexpr int SU = AU + BU;                  // units per LDS stage
+    constexpr int NB = 3;                        // stages: chunk g+2 in flight while chunk g is read
+    constexpr int IA = AU / 64 / W, IB = BU / 64 / W;  // global_load_lds (1 KiB each) per wave per chunk
+    constexpr int NI = IA + IB;
+    static_assert(IA * 64 * W == AU && IB * 64 * W == BU, "chunk images must split evenly over the waves");
+    extern __shared__ __attribute__((aligned(16))) b16_u32x4 smem_b16[];
+    float *Ld = reinterpret_cast<float *>(smem_b16 + NB * SU);  // [QM][k]
+    int *Li = reinterpret_cast<int *>(Ld + QM * k);
+
+    const int nblocks = nqt * nsplit;
+    const int lb = xcd_remap(blockIdx.x, nblocks);
+    const int qt = lb % nqt;
+    const int split = lb / nqt;
+    const int64_t q0 = (int64_t)qt * QM;
+    const int64_t ntiles = ceil_div(N, B16_TN);
+    const int64_t t0 = (int64_t)split * tiles_per_split;
+    const int64_t t1 = t0 + tiles_per_split < ntiles ? t0 + tiles_per_split : ntiles;
+    const int64_t G = t1 > t0 ? (t1 - t0) * nk : 0;
+
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int l31 = lane & 31, h = lane >> 5;
+
+    for (int e = tid; e < QM * k; e += 64 * W) {
+        Ld[e] = __builtin_inff();
+        Li[e] = 0x7fffffff;
+    }
+    float cth[16], qnv[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int64_t q = q0 + 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * h;
+        qnv[r] = (L2M && q < nq) ? qnorm[q] : 0.f;
+        cth[r] = q < nq ? -__builtin_inff() : __builtin_inff();  // thr = +inf (admit) / −inf (rows past nq)
+    }
+
+    // chunk g = (t − t0)·nk + kc: query chunk kc and database chunk t·nk + kc (a split's database chunks are
+    // consecutive in the image).  LDS-DMA (global_load_lds_dwordx4): each wave copies its share of the two
+    // images, 1 KiB per instruction, into stage g % NB — lane-linear, the swizzle is in the images themselves.
+    const b16_u32x4 *Qb = Qt + (int64_t)qt * nk * AU + lane;
+    const b16_u32x4 *Xb = Xt + t0 * nk * BU + lane;
+    int kc_issue = 0;
+    auto issue = [&](int64_t g, int stage) {
+        b16_u32x4 *dst = smem_b16 + stage * SU;
+#pragma unroll
+        for (int i = 0; i < IA; ++i) {
+            const int inst = wave * IA + i;
+            __builtin_amdgcn_global_load_lds((const void *)(Qb + (int64_t)kc_issue * AU + inst * 64),
+                                             (b16_lds_void *)(dst + inst * 64), 16, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < IB; ++i) {
+            const int inst = wave * IB + i;
+            __builtin_amdgcn_global_load_lds((const void *)(Xb + g * BU + inst * 64),
+                                             (b16_lds_void *)(dst + AU + inst * 64), 16, 0, 0);
+        }
+        kc_issue = kc_issue + 1 < nk ? kc_issue + 1 : 0;
+    };
+
+    b16_f32x16 acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    __syncthreads();  // list initialisation
+    if (G > 0) issue(0, 0);
+    if (G > 1) issue(1, 1);
+
+    int kc = 0, stage = 0;
+    int64_t t = t0;
+    for (int64_t g = 0; g < G; ++g) {
+        // retire this wave's copies of chunk g (chunk g+1's stay in flight), finish this wave's reads of the
+        // stage about to be refilled, then one barrier: every wave's chunk-g copies have landed and nobody
+        // still reads stage (g+2) % NB = (g−1) % NB
+        if (g + 1 < G) b16_wait_vm<NI>();
+        else b16_wait_vm<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (g + 2 < G) issue(g + 2, stage == 0 ? 2 : stage - 1);
+        const b16_u32x4 *Ab = smem_b16 + stage * SU;
+        const b16_u32x4 *Bb = Ab + AU;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int c = 2 * s + h;
+            const b16x8 a = __builtin_bit_cast(b16x8, Ab[b16_slot(c, 32 * wave + l31, QM)]);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const b16x8 b = __builtin_bit_cast(b16x8, Bb[b16_slot(c, 32 * j + l31, B16_TN)]);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[j], 0, 0, 0);
+            }
+        }
+        stage = stage + 1 < NB ? stage + 1 : 0;
+        if (++kc == nk) {
+            kc = 0;
+            const int64_t x0 = t * B16_TN;
+            float xnv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int64_t x = x0 + 32 * j + l31;
+                xnv[j] = x < N ? (L2M ? xnorm[x] : 0.f) : __builtin_inff();
+            }
+            b16_epilogue<L2M>(acc, cth, qnv, xnv, x0, N, Ld, Li, k, wave, lane);
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+            ++t;
+        }
+    }
+    // per-(split, query) lists, query-major (ivf_rerank_topk reads a query's lists contiguously)
+    for (int r = 0; r < 32; ++r) {
+        const int ql = 32 * wave + r;
+        const int64_t q = q0 + ql;
+        if (q < nq && lane < k) {
+            const int64_t off = (q * nsplit + split) * k;
+            part_d[off + lane] = Ld[ql * k + lane];
+            part_i[off + lane] = Li[ql * k + lane];
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+int flat_bf16_waves(int64_t nq) { return nq >= 256 ? 8 : nq >= 128 ? 4 : 2; }
+int flat_bf16_tile_rows() { return B16_TN; }
+
+size_t flat_bf16_img_bytes(int64_t n, int d, int R) {
+    return (size_t)ceil_div(std::max<int64_t>(n, 1), R) * b16_nk(d) * R * 4 * 16;
+}
+
+void launch_b16_tile_rows(const float *X, int64_t n, int d, int R, void *out, hipStream_t st) {
+    const int nk = b16_nk(d);
+    const int64_t total = ceil_div(std::max<int64_t>(n, 1), R) * nk * R * 4;
+    hipLaunchKernelGGL(b16_tile_rows, dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, st, X, n, d, R, nk, total,
+                       static_cast<uint4 *>(out));
+    HIPANN_CHECK(hipGetLastError());
+}
+
+void launch_b16_row_residual2(const float *X, int64_t n, int d, float *out, hipStream_t st) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(b16_row_residual2, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, st, X, n, d, out);
+    HIPANN_CHECK(hipGetLastError());
+}
+
+void launch_flat_bf16_topk(const float *Q, const float *qn, int64_t nq, void *qimg, const void *ximg, const float *xn,
+                           int64_t N, int d, int metric, int k, int nsplit, int64_t tiles_per_split, float *pd, int *pi,
+                           hipStream_t st) {
+    const int W = flat_bf16_waves(nq);
+    const int QM = 32 * W;
+    const int nk = b16_nk(d);
+    launch_b16_tile_rows(Q, nq, d, QM, qimg, st);
+    const int nqt = (int)ceil_div(nq, QM);
+    const size_t smem = (size_t)3 * (QM * 4 + B16_TN * 4) * 16 + (size_t)QM * k * 8;
+    HIPANN_REQUIRE(smem <= 160 * 1024, "k too large for the bf16 Flat kernel");
+    HIPANN_REQUIRE((int64_t)nqt * nsplit < 0x7fffffff, "grid too large");
+    dim3 grid((unsigned)(nqt * nsplit)), block(64 * W);
+    const b16_u32x4 *qa = static_cast<const b16_u32x4 *>(qimg);
+    const b16_u32x4 *xa = static_cast<const b16_u32x4 *>(ximg);
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, grid, block, smem, st, qa, qn, nq, xa, xn, N, nk, k, nqt, nsplit, tiles_per_split, pd,
+                           pi);
+    };
+    if (metric == kL2) {
+        if (W == 8) go(flat_bf16_topk<true, 8>);
+        else if (W == 4) go(flat_bf16_topk<true, 4>);
+        else go(flat_bf16_topk<true, 2>);
+    } else {
+        if (W == 8) go(flat_bf16_topk<false, 8>);
+        else if (W == 4) go(flat_bf16_topk<false, 4>);
+        else go(flat_bf16_topk<false, 2>);
+    }
+    HIPANN_CHECK(hipGetLastError());
+}
+
+}  // namespace hipann

@@ -10,6 +10,7 @@
 #include "ivf.hpp"
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <string>
 
@@ -119,6 +120,8 @@ void shard_append(FlatShard &sh, int d, int metric, const float *x_host, const f
     HIPANN_CHECK(hipStreamSynchronize(sh.stream));
     sh.n = need;
     sh.xmax2 = -1.f;  // new rows: the exact form's bound is recomputed
+    sh.xb16_ok = false;  // and the bf16 image rebuilt
+    sh.xb16.release();
 }
 
 }  // namespace
@@ -269,24 +272,61 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
         launch_row_norms(xq, nq, d, sh.qn.get<float>(), st);
         qn = sh.qn.get<float>();
     }
-    const int64_t nqt = ceil_div(nq, 128);
-    const int64_t ntiles = ceil_div(sh.n, 128);
-    // ≈2048 blocks; small tables (an IVF coarse quantizer: 1024 centroids = 8 tiles) go down to one
-    // column tile per block rather than leaving CUs idle
-    int64_t nsplit = std::max<int64_t>(1, ceil_div(2048, nqt));
-    nsplit = std::min<int64_t>(nsplit, ntiles);
-    if (nsplit >= 8) nsplit = nsplit / 8 * 8;
-    const int64_t tps = ceil_div(ntiles, nsplit);
-    nsplit = ceil_div(ntiles, tps);
-    HIPANN_REQUIRE(nqt * nsplit < (int64_t)0x7fffffff, "grid too large");
     int form = form_override >= 0 ? form_override : ix.form;
-    const bool exact = form == kFlatSplit2Exact && kout <= kRerankMaxK;
-    if (form == kFlatSplit2Exact && !exact) form = kFlatSplit3;
+    const bool exact = (form == kFlatSplit2Exact || form == kFlatBf16Exact) && kout <= kRerankMaxK;
+    if ((form == kFlatSplit2Exact || form == kFlatBf16Exact) && !exact) form = kFlatSplit3;
     const int k_user = k;
-    if (exact) k = metric == kIP ? kFlatRerankKIP : kRerankK;  // kept per (split, query); the rerank returns kout
-    sh.part_d.ensure((size_t)nsplit * nq * k * sizeof(float), sh.device);
-    sh.part_i.ensure((size_t)nsplit * nq * k * sizeof(int), sh.device);
-    {
+    // kept per (split, query); the rerank returns kout.  The bf16 filter keeps 32: at 10M × 768 the 10th and
+    // 16th distances are ≈2 apart, inside its rounding bound (≈1.3), the 10th and 32nd ≈5
+    if (exact) k = metric == kIP || form == kFlatBf16Exact ? kFlatRerankKIP : kRerankK;
+    int64_t nsplit;
+    if (form == kFlatBf16Exact) {
+        // one plain bf16 product per element over the tiled bf16 image (flat_bf16.hip), built once
+        if (!sh.xb16_ok) {
+            sh.xb16.ensure(flat_bf16_img_bytes(sh.n, d, flat_bf16_tile_rows()), sh.device);
+            launch_b16_tile_rows(sh.xb, sh.n, d, flat_bf16_tile_rows(), sh.xb16.p, st);
+            // the rows' largest bf16 rounding residual ‖x̂ − x‖ (the rerank's bound)
+            sh.tmpnorm.ensure(sizeof(float) * (size_t)sh.n, sh.device);
+            launch_b16_row_residual2(sh.xb, sh.n, d, sh.tmpnorm.get<float>(), st);
+            sh.nflag.ensure(sizeof(int), sh.device);
+            launch_ivf_max_norm(sh.tmpnorm.get<float>(), sh.n, sh.nflag.get<unsigned>(), st);
+            unsigned bits = 0;
+            HIPANN_CHECK(hipMemcpyAsync(&bits, sh.nflag.p, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+            HIPANN_CHECK(hipStreamSynchronize(st));  // later searches may run on other streams
+            sh.tmpnorm.release();
+            float r2;
+            std::memcpy(&r2, &bits, sizeof(r2));
+            sh.bf16_rxmax = std::sqrt(r2) * 1.0001f;
+            sh.xb16_ok = true;
+        }
+        const int W = flat_bf16_waves(nq);
+        const int64_t nqt = ceil_div(nq, 32 * W);
+        const int64_t ntiles = ceil_div(sh.n, flat_bf16_tile_rows());
+        // ≈ two rounds of resident blocks (W = 8: one block per CU; W ≤ 4: two to three per CU)
+        nsplit = std::max<int64_t>(1, ceil_div(W == 8 ? 512 : 1024, nqt));
+        nsplit = std::min<int64_t>(nsplit, ntiles);
+        const int64_t tps = ceil_div(ntiles, nsplit);
+        nsplit = ceil_div(ntiles, tps);
+        HIPANN_REQUIRE(nqt * nsplit < (int64_t)0x7fffffff, "grid too large");
+        sh.part_d.ensure((size_t)nsplit * nq * k * sizeof(float), sh.device);
+        sh.part_i.ensure((size_t)nsplit * nq * k * sizeof(int), sh.device);
+        sh.qimg.ensure(flat_bf16_img_bytes(nq, d, 32 * W), sh.device);
+        ScopedTiming t(ix.timer_main, st);
+        launch_flat_bf16_topk(xq, qn, nq, sh.qimg.p, sh.xb16.p, sh.xn.get<float>(), sh.n, d, metric, k, (int)nsplit,
+                              tps, sh.part_d.get<float>(), sh.part_i.get<int>(), st);
+    } else {
+        const int64_t nqt = ceil_div(nq, 128);
+        const int64_t ntiles = ceil_div(sh.n, 128);
+        // ≈2048 blocks; small tables (an IVF coarse quantizer: 1024 centroids = 8 tiles) go down to one
+        // column tile per block rather than leaving CUs idle
+        nsplit = std::max<int64_t>(1, ceil_div(2048, nqt));
+        nsplit = std::min<int64_t>(nsplit, ntiles);
+        if (nsplit >= 8) nsplit = nsplit / 8 * 8;
+        const int64_t tps = ceil_div(ntiles, nsplit);
+        nsplit = ceil_div(ntiles, tps);
+        HIPANN_REQUIRE(nqt * nsplit < (int64_t)0x7fffffff, "grid too large");
+        sh.part_d.ensure((size_t)nsplit * nq * k * sizeof(float), sh.device);
+        sh.part_i.ensure((size_t)nsplit * nq * k * sizeof(int), sh.device);
         ScopedTiming t(ix.timer_main, st);
         if (form == kFlatFp32) {
             launch_flat_gemm_topk(xq, qn, nq, sh.xb, sh.xn.get<float>(), sh.n, d, metric, k, (int)nsplit, tps,
@@ -315,7 +355,7 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
         ScopedTiming t(ix.timer_merge, st);
         launch_ivf_rerank(sh.part_d.get<float>(), sh.part_i.get<int>(), nullptr, (int)nsplit, nq, k, kout, metric, xq,
                           sh.xb, d, nullptr, sh.n, sh.label_offset, xmax2, D, I, sh.nflag.get<int>(),
-                          sh.flagged.get<int>(), st);
+                          sh.flagged.get<int>(), st, kSplit2Eps, form == kFlatBf16Exact ? sh.bf16_rxmax : -1.f);
     }
     int nf = 0;
     HIPANN_CHECK(hipMemcpyAsync(&nf, sh.nflag.p, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -624,7 +664,7 @@ int hipann_metric(void *h) { return h ? static_cast<IndexBase *>(h)->metric : -1
 int64_t hipann_memory_bytes(void *h) { return h ? static_cast<IndexBase *>(h)->memory_bytes() : -1; }
 
 int hipann_flat_set_form(void *h, int form) {
-    if (!h || form < kFlatFp32 || form > kFlatSplit2Exact) return -1;
+    if (!h || form < kFlatFp32 || form > kFlatBf16Exact) return -1;
     auto *ix = static_cast<IndexBase *>(h);
     if (ix->kind != Kind::Flat) return -1;
     auto *fx = static_cast<FlatIndex *>(ix);

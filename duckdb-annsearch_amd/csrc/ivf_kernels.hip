@@ -996,6 +996,11 @@ namespace hipann {
 // < K16 − E (or < −K16... for IP the same bound on −q·x) is flagged; the host re-runs the flagged
 // queries on the 3-term path.  With fewer than 16 merged candidates nothing was pruned.
 // The list length k (16; 32 for Flat IP, common.hpp) is the number of candidates reranked.
+// rxmax >= 0 (Flat form kFlatBf16Exact: one plain bf16 product per element): the bound is the
+// Cauchy-Schwarz bound of the bf16 rounding instead, from this query's own rounding residual and the
+// largest row residual: |q̂·x̂ − q·x| ≤ ‖q‖·‖x̂−x‖ + ‖q̂−q‖·‖x̂‖ ≤ ‖q‖·rxmax + ‖q̂−q‖·(max‖x‖ + rxmax),
+// plus the fp32 accumulation of d exact products (≤ d·2⁻²⁴·‖q̂‖‖x̂‖), doubled for L2, plus the fp32
+// rounding of the key and of the reranked direct distance (≤ (d + 8)·2⁻²⁴·2(‖q‖² + max‖x‖²)), all ×1.01.
 // ---------------------------------------------------------------------------------------------
 template <bool IP>
 __global__ void __launch_bounds__(256)
@@ -1003,7 +1008,7 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
                 int nprobe, int64_t nq, int k, int kout, const float *__restrict__ Q,
                 const float *__restrict__ codes, int d, const int64_t *__restrict__ ids, int64_t nrows,
                 int64_t label_offset, float xmax2, float *__restrict__ D, int64_t *__restrict__ I,
-                int *__restrict__ nflag, int *__restrict__ flagged) {
+                int *__restrict__ nflag, int *__restrict__ flagged, float eps, float rxmax) {
     const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (q >= nq) return;
     const int lane = threadIdx.x & 63;
@@ -1036,10 +1041,17 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
     const float k16 = readlane_f(L.d[0], k - 1);  // K_k: the k-th merged scan key
     // 2. exact direct-form distances of the candidates (4 rows in flight, wave reduction per row)
     const float *qp = Q + q * (int64_t)d;
-    float qq = 0.f;
-    for (int e = lane; e < d; e += 64) qq = fmaf(qp[e], qp[e], qq);
+    float qq = 0.f, rq2 = 0.f;
+    for (int e = lane; e < d; e += 64) {
+        qq = fmaf(qp[e], qp[e], qq);
+        const float r = qp[e] - (float)(__bf16)qp[e];  // RNE, as the bf16 image of the queries
+        rq2 = fmaf(r, r, rq2);
+    }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) qq += __shfl_xor(qq, o);
+    for (int o = 32; o > 0; o >>= 1) {
+        qq += __shfl_xor(qq, o);
+        rq2 += __shfl_xor(rq2, o);
+    }
     float mine = __builtin_inff();
     for (int r0 = 0; r0 < ncand; r0 += 4) {
         float acc[4] = {0.f, 0.f, 0.f, 0.f};
@@ -1076,7 +1088,15 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
     R.offer(real ? mine : __builtin_inff(), lab, kout - 1);
     // 4. exactness check
     const float dk = readlane_f(R.d[0], kout - 1);
-    const float E = 0x1p-12f * (qq + xmax2);
+    float E;
+    if (rxmax >= 0.f) {
+        const float qn = sqrtf(qq), rq = sqrtf(rq2), xh = sqrtf(xmax2) + rxmax;
+        const float g = (float)d * 0x1p-24f;
+        const float eip = qn * rxmax + rq * xh + g * (qn + rq) * xh;
+        E = 1.01f * ((IP ? 1.f : 2.f) * eip + (float)(d + 8) * 0x1p-24f * 2.f * (qq + xmax2));
+    } else {
+        E = eps * (qq + xmax2);
+    }
     if (ncand == k && !(dk < k16 - E) && lane == 0) flagged[atomicAdd(nflag, 1)] = (int)q;
     const float pad_d = IP ? -__builtin_inff() : __builtin_inff();
     if (lane < kout) {
@@ -1116,16 +1136,16 @@ __global__ void __launch_bounds__(256) ivf_scatter_results(const float *__restri
 void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int nprobe, int64_t nq, int k, int kout,
                        int metric, const float *Q, const float *codes, int d, const int64_t *ids, int64_t nrows,
                        int64_t label_offset, float xmax2, float *D, int64_t *I, int *nflag, int *flagged,
-                       hipStream_t st) {
+                       hipStream_t st, float eps, float rxmax) {
     if (nq <= 0) return;
     HIPANN_REQUIRE(k >= kRerankK && k <= 64 && kout >= 1 && kout <= kRerankMaxK, "ivf rerank: k / kout out of range");
     dim3 grid((unsigned)ceil_div(nq, 4)), block(256);
     if (metric == kIP)
         hipLaunchKernelGGL(ivf_rerank_topk<true>, grid, block, 0, st, pd, pi, slot_off, nprobe, nq, k, kout, Q, codes, d,
-                           ids, nrows, label_offset, xmax2, D, I, nflag, flagged);
+                           ids, nrows, label_offset, xmax2, D, I, nflag, flagged, eps, rxmax);
     else
         hipLaunchKernelGGL(ivf_rerank_topk<false>, grid, block, 0, st, pd, pi, slot_off, nprobe, nq, k, kout, Q, codes,
-                           d, ids, nrows, label_offset, xmax2, D, I, nflag, flagged);
+                           d, ids, nrows, label_offset, xmax2, D, I, nflag, flagged, eps, rxmax);
     HIPANN_CHECK(hipGetLastError());
 }
 

@@ -138,6 +138,11 @@ struct FlatShard {
     // flagged queries of the last batch and the re-run's buffers
     float xmax2 = -1.f;
     DevBuf nflag, flagged, fq, fD, fI, tmpnorm;
+    // kFlatBf16Exact: tiled bf16 image of the rows (built at the first search after an add) and the
+    // batch's query image
+    DevBuf xb16, qimg;
+    bool xb16_ok = false;
+    float bf16_rxmax = 0.f;  // max over rows of ‖bf16(x) − x‖ (the rerank's bound)
 };
 
 struct IndexBase {
@@ -154,7 +159,7 @@ struct IndexBase {
 
 struct FlatIndex : IndexBase {
     std::vector<std::unique_ptr<FlatShard>> shards;
-    int form = kFlatSplit2Exact;  // BLAS-path q·x form (FlatForm)
+    int form = kFlatBf16Exact;  // BLAS-path q·x form (FlatForm)
     int64_t rerank_fallbacks = 0;  // queries re-run on the 3-term path by the exact form's bound check
     HostBuf h_q, h_d, h_i;
     DevBuf gather_d, gather_i, merged_d, merged_i;  // multi-device merge on shards[0]'s device
@@ -167,7 +172,7 @@ struct FlatIndex : IndexBase {
     }
     int64_t memory_bytes() const override {
         int64_t b = 0;
-        for (auto &s : shards) b += s->n * (int64_t)d * 4 + (metric == kL2 ? s->n * 4 : 0);
+        for (auto &s : shards) b += s->n * (int64_t)d * 4 + (metric == kL2 ? s->n * 4 : 0) + (int64_t)s->xb16.bytes;
         return b;
     }
 };
@@ -256,7 +261,16 @@ int64_t ivf_mfma_bf_qsplit_bytes(int64_t nq, int d, int np);
 void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int nprobe, int64_t nq, int k, int kout,
                        int metric, const float *Q, const float *codes, int d, const int64_t *ids, int64_t nrows,
                        int64_t label_offset, float xmax2, float *D, int64_t *I, int *nflag, int *flagged,
-                       hipStream_t st);
+                       hipStream_t st, float eps = kSplit2Eps, float rxmax = -1.f);
+// flat_bf16.hip
+int flat_bf16_waves(int64_t nq);
+int flat_bf16_tile_rows();
+size_t flat_bf16_img_bytes(int64_t n, int d, int R);
+void launch_b16_tile_rows(const float *X, int64_t n, int d, int R, void *out, hipStream_t st);
+void launch_b16_row_residual2(const float *X, int64_t n, int d, float *out, hipStream_t st);
+void launch_flat_bf16_topk(const float *Q, const float *qn, int64_t nq, void *qimg, const void *ximg, const float *xn,
+                           int64_t N, int d, int metric, int k, int nsplit, int64_t tiles_per_split, float *pd, int *pi,
+                           hipStream_t st);
 void launch_ivf_max_norm(const float *xn, int64_t n, unsigned *out, hipStream_t st);
 void launch_ivf_gather_queries(const float *Q, const int *idx, int nf, int d, float *out, hipStream_t st);
 void launch_ivf_scatter_results(const float *Df, const int64_t *If, const int *idx, int nf, int kout, float *D,

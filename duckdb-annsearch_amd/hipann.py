@@ -234,7 +234,8 @@ class _FlatForm:
     FORM_FP32 = 0          # exact fp32 products on the fp32 matrix cores
     FORM_SPLIT3 = 1        # 3-term split-bf16 products (fp32-level) on the bf16 matrix cores
     FORM_SPLIT2 = 2        # 2-term split (~2^-16 relative per product; measurement only)
-    FORM_SPLIT2_EXACT = 3  # default: the 2-term scan as a filter + exact direct-form rerank with a bound check
+    FORM_SPLIT2_EXACT = 3  # the 2-term scan as a filter + exact direct-form rerank with a bound check
+    FORM_BF16_EXACT = 4    # default: one bf16 product per element (tiled bf16 image) as the filter, same rerank
 
     @property
     def form(self) -> int:
@@ -243,8 +244,8 @@ class _FlatForm:
     @form.setter
     def form(self, v: int) -> None:
         if lib().hipann_flat_set_form(self._h, int(v)) != 0:
-            raise HipAnnError("form must be 0 (fp32), 1 (split bf16, 3 terms), 2 (split bf16, 2 terms) or "
-                              "3 (split bf16 + exact rerank)")
+            raise HipAnnError("form must be 0 (fp32), 1 (split bf16, 3 terms), 2 (split bf16, 2 terms), "
+                              "3 (split bf16 + exact rerank) or 4 (bf16 + exact rerank)")
 
     def rerank_fallbacks(self) -> int:
         """Queries the exact form's bound check re-ran on the 3-term path since creation."""

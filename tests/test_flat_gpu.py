@@ -242,16 +242,16 @@ def test_flat_large_properties(gpu, oracle):
     check_topk_parity(xb, xq[:64], D[:64], I[:64], Do, Io)
 
 
-@pytest.mark.parametrize("form", [0, 1, 2, 3])
+@pytest.mark.parametrize("form", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("metric", [0, 1])
-@pytest.mark.parametrize("nq,d", [(20, 64), (129, 33), (300, 768), (64, 5)])
+@pytest.mark.parametrize("nq,d", [(20, 64), (129, 33), (300, 768), (64, 5), (257, 100), (600, 96)])
 def test_flat_forms_blas_path(gpu, oracle, form, metric, nq, d):
     """hipann_flat_set_form: the fp32 (0), 3-term split-bf16 (1) and exact (3, default: 2-term filter +
     direct-form rerank) forms of the batched path meet the fp32 parity rule; the 2-term split (2,
     measurement only) keeps ≈2^-16 relative products, so only its recall is checked."""
     xb, xq = faiss_metal_case(20000, nq, d)  # > 16384 rows: the fused path (smaller tables select from keys)
     ix = gpu.HipIndexFlat(d, metric, xb)
-    assert ix.form == ix.FORM_SPLIT2_EXACT
+    assert ix.form == ix.FORM_BF16_EXACT
     ix.form = form
     assert ix.form == form
     D, I = ix.search(xq, 10)
@@ -262,7 +262,7 @@ def test_flat_forms_blas_path(gpu, oracle, form, metric, nq, d):
         hit = np.mean([len(set(a) & set(b)) / 10 for a, b in zip(I.tolist(), Io.tolist())])
         assert hit >= 0.97, hit
     with pytest.raises(gpu.HipAnnError):
-        ix.form = 4
+        ix.form = 5
 
 
 def test_flat_exact_form_ties_fall_back(gpu, oracle):
@@ -286,7 +286,8 @@ def test_flat_exact_form_large_k_uses_split3(gpu, oracle):
     assert ix.rerank_fallbacks() == 0
 
 
-def test_flat_exact_form_matches_fp32_form_at_scale(gpu):
+@pytest.mark.parametrize("form", [3, 4])
+def test_flat_exact_form_matches_fp32_form_at_scale(gpu, form):
     """Large-size property: the exact form (2-term split filter + direct-form rerank) returns the fp32
     form's lists except inside near-tie windows (distances within the fp32 rounding scale), on
     200k × 128 with 512 queries."""
@@ -296,7 +297,7 @@ def test_flat_exact_form_matches_fp32_form_at_scale(gpu):
     ix = gpu.HipIndexFlat(128, 0, xb)
     ix.form = ix.FORM_FP32
     D0, I0 = ix.search(xq, 10)
-    ix.form = ix.FORM_SPLIT2_EXACT
+    ix.form = form
     D1, I1 = ix.search(xq, 10)
     scale = np.sum(xq.astype(np.float64) ** 2, 1)[:, None] + np.max(np.sum(xb.astype(np.float64) ** 2, 1))
     assert (np.abs(D1 - D0) <= 1e-5 * scale).all()
