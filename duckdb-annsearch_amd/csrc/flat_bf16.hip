@@ -148,7 +148,8 @@ __global__ void __launch_bounds__(64 * W, 1)
 flat_bf16_topk(const b16_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm, int64_t nq,
                const b16_u32x4 *__restrict__ Xt,
                const float *__restrict__ xnorm, int64_t N, int nk, int k, int nqt, int nsplit,
-               int64_t tiles_per_split, float *__restrict__ part_d, int *__restrict__ part_i) {
+               int64_t tiles_per_split, float *__restrict__ part_d, int *__restrict__ part_i,
+               const float *__restrict__ seed) {
     constexpr int QM = 32 * W;
     constexpr int AU = QM * 4, BU = B16_TN * 4;  // 16-B units per chunk image
     constexpr int SU = AU + BU;                  // units per LDS stage
@@ -174,8 +175,12 @@ flat_bf16_topk(const b16_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm
     const int wave = tid >> 6, lane = tid & 63;
     const int l31 = lane & 31, h = lane >> 5;
 
+    // seed (optional): per query an upper bound T_q of its k-th best scan key (the k-th best over a sample of
+    // rows, flat_bf16_seed).  The list starts as k copies of (T_q, pad): only keys ≤ T_q are admitted, and
+    // the pads never reach the rerank (their row id is out of range)
     for (int e = tid; e < QM * k; e += 64 * W) {
-        Ld[e] = __builtin_inff();
+        const int64_t q = q0 + e / k;
+        Ld[e] = seed && q < nq ? seed[q] : __builtin_inff();
         Li[e] = 0x7fffffff;
     }
     float cth[16], qnv[16];
@@ -183,7 +188,8 @@ flat_bf16_topk(const b16_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm
     for (int r = 0; r < 16; ++r) {
         const int64_t q = q0 + 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * h;
         qnv[r] = (L2M && q < nq) ? qnorm[q] : 0.f;
-        cth[r] = q < nq ? -__builtin_inff() : __builtin_inff();  // thr = +inf (admit) / −inf (rows past nq)
+        const float thr = q < nq ? (seed ? seed[q] : __builtin_inff()) : -__builtin_inff();  // −inf: rows past nq
+        cth[r] = L2M ? qnv[r] - thr : -2.f * thr;
     }
 
     // chunk g = (t − t0)·nk + kc: query chunk kc and database chunk t·nk + kc (a split's database chunks are
@@ -272,6 +278,28 @@ flat_bf16_topk(const b16_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm
     }
 }
 
+// Seed thresholds: per query the k-th smallest key of its nsplit partial lists (query-major [q][split][k]),
+// raised by a few ulps (the main pass recomputes those sample rows' keys bit-identically; the margin only
+// guards the ≥ k rows with key ≤ T_q that make the rerank's K_k ≤ T_q).  One wave per query.
+__global__ void __launch_bounds__(256) flat_bf16_seed(const float *__restrict__ pd, int nsplit, int64_t nq, int k,
+                                                      float *__restrict__ seed) {
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq) return;
+    const int lane = threadIdx.x & 63;
+    WaveList<1, int> L;
+    L.init();
+    const int64_t total = (int64_t)nsplit * k;
+    for (int64_t c0 = 0; c0 < total; c0 += 64) {
+        const int64_t c = c0 + lane;
+        const float v = c < total ? pd[q * total + c] : __builtin_inff();
+        L.offer(v, (int)lane, k - 1);
+    }
+    if (lane == 0) {
+        const float t = readlane_f(L.d[0], k - 1);
+        seed[q] = t == __builtin_inff() ? t : fmaxf(t * (1.f + 0x1p-20f), t + 0x1p-100f);
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 int flat_bf16_waves(int64_t nq) { return nq >= 256 ? 8 : nq >= 128 ? 4 : 2; }
 int flat_bf16_tile_rows() { return B16_TN; }
@@ -294,13 +322,19 @@ void launch_b16_row_residual2(const float *X, int64_t n, int d, float *out, hipS
     HIPANN_CHECK(hipGetLastError());
 }
 
+void launch_flat_bf16_seed(const float *pd, int nsplit, int64_t nq, int k, float *seed, hipStream_t st) {
+    if (nq <= 0) return;
+    hipLaunchKernelGGL(flat_bf16_seed, dim3((unsigned)ceil_div(nq, 4)), dim3(256), 0, st, pd, nsplit, nq, k, seed);
+    HIPANN_CHECK(hipGetLastError());
+}
+
 void launch_flat_bf16_topk(const float *Q, const float *qn, int64_t nq, void *qimg, const void *ximg, const float *xn,
                            int64_t N, int d, int metric, int k, int nsplit, int64_t tiles_per_split, float *pd, int *pi,
-                           hipStream_t st) {
+                           const float *seed, bool image_ready, hipStream_t st) {
     const int W = flat_bf16_waves(nq);
     const int QM = 32 * W;
     const int nk = b16_nk(d);
-    launch_b16_tile_rows(Q, nq, d, QM, qimg, st);
+    if (!image_ready) launch_b16_tile_rows(Q, nq, d, QM, qimg, st);
     const int nqt = (int)ceil_div(nq, QM);
     const size_t smem = (size_t)3 * (QM * 4 + B16_TN * 4) * 16 + (size_t)QM * k * 8;
     HIPANN_REQUIRE(smem <= 160 * 1024, "k too large for the bf16 Flat kernel");
@@ -310,7 +344,7 @@ void launch_flat_bf16_topk(const float *Q, const float *qn, int64_t nq, void *qi
     const b16_u32x4 *xa = static_cast<const b16_u32x4 *>(ximg);
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, grid, block, smem, st, qa, qn, nq, xa, xn, N, nk, k, nqt, nsplit, tiles_per_split, pd,
-                           pi);
+                           pi, seed);
     };
     if (metric == kL2) {
         if (W == 8) go(flat_bf16_topk<true, 8>);

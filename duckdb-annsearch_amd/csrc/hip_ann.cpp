@@ -10,6 +10,7 @@
 #include "ivf.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -302,8 +303,13 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
         const int W = flat_bf16_waves(nq);
         const int64_t nqt = ceil_div(nq, 32 * W);
         const int64_t ntiles = ceil_div(sh.n, flat_bf16_tile_rows());
-        // ≈ two rounds of resident blocks (W = 8: one block per CU; W ≤ 4: two to three per CU)
-        nsplit = std::max<int64_t>(1, ceil_div(W == 8 ? 512 : 1024, nqt));
+        static const int64_t blocks_env = [] {
+            const char *e = std::getenv("HIPANN_FLAT_BF16_BLOCKS");  // A/B: target grid size
+            return e ? (int64_t)std::atoll(e) : (int64_t)0;
+        }();
+        // one round of resident blocks (W = 8 / 4: one block per CU; W = 2: two) — fewer, longer splits admit
+        // fewer candidates into the per-split lists (≈ k·ln(rows / k) per list), the epilogue's slow path
+        nsplit = std::max<int64_t>(1, ceil_div(blocks_env > 0 ? blocks_env : (W == 2 ? 512 : 256), nqt));
         nsplit = std::min<int64_t>(nsplit, ntiles);
         const int64_t tps = ceil_div(ntiles, nsplit);
         nsplit = ceil_div(ntiles, tps);
@@ -311,9 +317,26 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
         sh.part_d.ensure((size_t)nsplit * nq * k * sizeof(float), sh.device);
         sh.part_i.ensure((size_t)nsplit * nq * k * sizeof(int), sh.device);
         sh.qimg.ensure(flat_bf16_img_bytes(nq, d, 32 * W), sh.device);
+        // seed thresholds (large tables): the k-th best key of each query over the first 64K rows, from the same
+        // kernel on those rows (bit-identical keys); the main pass then admits only keys ≤ that bound
+        static const bool seed_env = [] { const char *e = std::getenv("HIPANN_FLAT_BF16_SEED"); return !e || std::atoi(e); }();
+        const int64_t seed_rows = 65536;
+        const bool seeded = seed_env && sh.n >= 8 * seed_rows;
         ScopedTiming t(ix.timer_main, st);
+        if (seeded) {
+            const int64_t stiles = seed_rows / flat_bf16_tile_rows();
+            const int64_t snsplit = std::min<int64_t>(stiles, std::max<int64_t>(1, ceil_div(256, nqt)));
+            const int64_t stps = ceil_div(stiles, snsplit);
+            sh.seed.ensure(sizeof(float) * ((size_t)snsplit * nq * k * 2 + (size_t)nq), sh.device);
+            float *spd = sh.seed.get<float>() + nq;
+            int *spi = reinterpret_cast<int *>(spd + (size_t)snsplit * nq * k);
+            launch_flat_bf16_topk(xq, qn, nq, sh.qimg.p, sh.xb16.p, sh.xn.get<float>(), seed_rows, d, metric, k,
+                                  (int)ceil_div(stiles, stps), stps, spd, spi, nullptr, false, st);
+            launch_flat_bf16_seed(spd, (int)ceil_div(stiles, stps), nq, k, sh.seed.get<float>(), st);
+        }
         launch_flat_bf16_topk(xq, qn, nq, sh.qimg.p, sh.xb16.p, sh.xn.get<float>(), sh.n, d, metric, k, (int)nsplit,
-                              tps, sh.part_d.get<float>(), sh.part_i.get<int>(), st);
+                              tps, sh.part_d.get<float>(), sh.part_i.get<int>(), seeded ? sh.seed.get<float>() : nullptr,
+                              seeded, st);
     } else {
         const int64_t nqt = ceil_div(nq, 128);
         const int64_t ntiles = ceil_div(sh.n, 128);

@@ -140,7 +140,7 @@ struct FlatShard {
     DevBuf nflag, flagged, fq, fD, fI, tmpnorm;
     // kFlatBf16Exact: tiled bf16 image of the rows (built at the first search after an add) and the
     // batch's query image
-    DevBuf xb16, qimg;
+    DevBuf xb16, qimg, seed;
     bool xb16_ok = false;
     float bf16_rxmax = 0.f;  // max over rows of ‖bf16(x) − x‖ (the rerank's bound)
 };
@@ -270,7 +270,8 @@ void launch_b16_tile_rows(const float *X, int64_t n, int d, int R, void *out, hi
 void launch_b16_row_residual2(const float *X, int64_t n, int d, float *out, hipStream_t st);
 void launch_flat_bf16_topk(const float *Q, const float *qn, int64_t nq, void *qimg, const void *ximg, const float *xn,
                            int64_t N, int d, int metric, int k, int nsplit, int64_t tiles_per_split, float *pd, int *pi,
-                           hipStream_t st);
+                           const float *seed, bool image_ready, hipStream_t st);
+void launch_flat_bf16_seed(const float *pd, int nsplit, int64_t nq, int k, float *seed, hipStream_t st);
 void launch_ivf_max_norm(const float *xn, int64_t n, unsigned *out, hipStream_t st);
 void launch_ivf_gather_queries(const float *Q, const int *idx, int nf, int d, float *out, hipStream_t st);
 void launch_ivf_scatter_results(const float *Df, const int64_t *If, const int *idx, int nf, int kout, float *D,
