@@ -15,4 +15,4 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/
     python3 "$root/bench.py" --workload "$wl" --no-cpu-baseline --no-suite "$@" > "$out/stats.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$kern" --output-format csv -d "$out/pmc" -o run -- \
     python3 "$root/bench.py" --workload "$wl" --no-cpu-baseline --no-suite "$@" > "$out/pmc.log" 2>&1
-python3 "$root/tools/pmc_traffic.py" "$out/pmc" "$kern" --skip 3 --out "$root/gpurun_out/pmc_$key.json"
+python3 "$root/tools/pmc_traffic.py" "$out/pmc" "$kern" --skip 3 --per-step "${PER_STEP:-1}" --out "$root/gpurun_out/pmc_$key.json"

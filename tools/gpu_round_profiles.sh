@@ -1,16 +1,24 @@
 #!/usr/bin/env bash
-# The round's GPU evidence in one call: the whole -m gpu suite, then rocprofv3 kernel-trace/stats and a
-# separate FETCH_SIZE PMC pass (tools/gpu_profile.sh) for the IVF (default bench), DiskANN and Flat workloads.
-#   tools/gpu_round_profiles.sh   → gpurun_out/pytest_gpu.log, gpurun_out/prof_{ivf,diskann,flat}/, gpurun_out/pmc_*.json
+# The round's GPU evidence in one call: the whole -m gpu suite, the default bench line, then per
+# configuration a rocprofv3 kernel-trace/stats pass and a separate FETCH_SIZE PMC pass (tools/gpu_profile.sh)
+# for IVF 10M (default bench), Flat 10M and 1M (L2), and DiskANN C4.
+#   tools/gpu_round_profiles.sh [--no-tests]  → gpurun_out/pytest_gpu.log, gpurun_out/bench_default.json,
+#                                               gpurun_out/prof_<key>/, gpurun_out/pmc_<key>.json
 set -uo pipefail
 root="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$root"
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
-    > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
-tail -1 gpurun_out/pytest_gpu.log
-bash tools/gpu_profile.sh ivf ivf_scan_mfma_bf --no-alt-forms || exit 1
-bash tools/gpu_profile.sh diskann diskann_bfs || exit 1
-bash tools/gpu_profile.sh flat flat_gemm_topk_bf --no-alt-forms || exit 1
-ls gpurun_out/prof_ivf/stats gpurun_out/prof_diskann/stats gpurun_out/prof_flat/stats
-cat gpurun_out/pmc_ivf.json gpurun_out/pmc_diskann.json gpurun_out/pmc_flat.json
+if [ "${1:-}" != "--no-tests" ]; then
+    timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+        > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+    tail -1 gpurun_out/pytest_gpu.log
+fi
+timeout -k 10 600 python -u bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err \
+    || { tail -20 gpurun_out/bench_default.err; exit 1; }
+bash tools/gpu_profile.sh ivf ivf_scan_mfma_bf ivf_10000000x768 --no-alt-forms --steps 10 || exit 1
+PER_STEP=2 bash tools/gpu_profile.sh flat flat_bf16_topk flat_10000000x768 --no-alt-forms --steps 5 || exit 1
+PER_STEP=2 bash tools/gpu_profile.sh flat flat_bf16_topk flat_1000000x768 --no-alt-forms --n 1000000 --steps 10 || exit 1
+bash tools/gpu_profile.sh diskann diskann_bfs diskann_1000000x1536 --steps 10 || exit 1
+for key in ivf_10000000x768 flat_10000000x768 flat_1000000x768 diskann_1000000x1536; do
+    echo "== $key"; cat gpurun_out/pmc_$key.json
+done
