@@ -395,7 +395,21 @@ IVF_FORMS = {0: ("ivf_scan_mfma", "decomposed, fp32 MFMA"), 1: ("ivf_scan_topk",
              3: ("ivf_scan_mfma_bf", "decomposed, bf16 MFMA over a 3-term split (6 products)"),
              4: ("ivf_scan_mfma_bf", "decomposed, bf16 MFMA over a 2-term split (3 products)"),
              5: ("ivf_scan_mfma_bf", "bf16 MFMA 2-term split scan as a filter (16 per list) + exact fp32 "
-                                     "direct-form rerank, bound-checked (merge_ms includes the rerank)")}
+                                     "direct-form rerank, bound-checked (merge_ms includes the rerank)"),
+             6: ("ivf_scan_mfma_h", "fp16 MFMA scan over a tiled fp16 image of the rows (2 B per element, "
+                                    "2-term fp16 queries) as a filter (16 per list) + exact fp32 direct-form "
+                                    "rerank, bound-checked with the measured fp16 residuals (merge_ms includes "
+                                    "the rerank)")}
+
+
+def ivf_row_bytes(form, d, metric):
+    """HBM bytes one scanned row costs the form's list-scan kernel: the fp16 image (2d) + the row norm
+    (L2) for form 6; SURVEY §8d's fp32 codes + label (4d + 8) for the fp32-row forms."""
+    return 2 * d + (4 if metric == 0 else 0) if form == 6 else 4 * d + 8
+
+
+def ivf_row_bytes_desc(form):
+    return "|l|*(2d+4) (fp16 image + L2 row norm)" if form == 6 else "|l|*(4d+8)"
 
 
 def build_ivf(args, torch, hipann, rank, world, dev, n, d, nlist, nprobe, metric, r_dim, eta):
@@ -424,11 +438,12 @@ def build_ivf(args, torch, hipann, rank, world, dev, n, d, nlist, nprobe, metric
     return index, info, xq, f"low-rank gaussian, intrinsic dim {r_dim}, noise {eta}"
 
 
-def ivf_scan_stats(index, probes, d, nlist):
+def ivf_scan_stats(index, probes, d, nlist, row_bytes=None):
     from ivf_build import scan_bytes, scan_group_rows, scan_pairs
 
     cnt = np.bincount(probes[probes >= 0].ravel(), minlength=nlist)
-    return {"scan_bytes_per_batch_local": scan_bytes(index, probes, d),
+    return {"scan_bytes_per_batch_local": scan_bytes(index, probes, d, row_bytes),
+            "fp32_rows_bytes_per_batch_local": scan_bytes(index, probes, d),
             "distinct_lists_probed": int(np.unique(probes[probes >= 0]).size),
             "scanned_pairs_per_batch_local": scan_pairs(index, probes),
             "group_rows_per_batch_local": scan_group_rows(index, probes),
@@ -447,7 +462,7 @@ def ivf_config(args, torch, dist, hipann, rank, world, dev, steps, warmup, suite
     eta = float(os.environ.get("HIPANN_IVF_NOISE", "0.02"))
     index, info, xq, data_desc = build_ivf(args, torch, hipann, rank, world, dev, n, d, nlist, nprobe, metric,
                                            r_dim, eta)
-    index.form = int(os.environ.get("HIPANN_IVF_FORM", "5"))
+    index.form = int(os.environ.get("HIPANN_IVF_FORM", "6"))
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t_setup
 
@@ -460,7 +475,7 @@ def ivf_config(args, torch, dist, hipann, rank, world, dev, steps, warmup, suite
         step()
     torch.cuda.synchronize()
     probes = index.last_probes(nq)
-    info.update(ivf_scan_stats(index, probes, d, nlist))
+    info.update(ivf_scan_stats(index, probes, d, nlist, ivf_row_bytes(index.form, d, metric)))
     index.set_kernel_timing(True)
     el = timed_steps(torch, dist, world, step, steps)
     kern_ms, merge_ms = index.kernel_ms(0), index.kernel_ms(1)
@@ -486,7 +501,7 @@ def ivf_config(args, torch, dist, hipann, rank, world, dev, steps, warmup, suite
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "kernel": kname,
             "kernel_ms": round(kern_ms, 3), "merge_ms": round(merge_ms, 3),
-            "algorithmic": "sum over distinct probed lists |l|*(4d+8) B per launch (this rank's lists)",
+            "algorithmic": f"sum over distinct probed lists {ivf_row_bytes_desc(form)} B per launch (this rank's lists)",
             "form": fname,
             "scan_tflops": round(fpp * d * info["scanned_pairs_per_batch_local"] / (kern_ms * 1e-3) / 1e12, 2)
             if kern_ms > 0 else None}
@@ -501,7 +516,7 @@ def ivf_config(args, torch, dist, hipann, rank, world, dev, steps, warmup, suite
     out["with_h2d_d2h"] = host_pointer_rate(torch, lambda q: sharded.search(q), xq, nq, k, max(5, steps // 2))
     if not args.no_alt_forms:
         alt = {}
-        for f in (3, 0):
+        for f in (5, 3, 0):
             if f == form:
                 continue
             index.form = f
@@ -525,13 +540,13 @@ def ivf_config(args, torch, dist, hipann, rank, world, dev, steps, warmup, suite
         out["other_forms"] = alt
     out["ivf"]["rerank_fallbacks_total"] = index.rerank_fallbacks()
     if suite_extras:
-        out["latency"] = ivf_latency(torch, index, xq, k, d)
+        out["latency"] = ivf_latency(torch, index, xq, k, d, metric)
     if not args.no_cpu_baseline:
         out["cpu_baseline"] = ivf_cpu_baseline(index, xq, k, nprobe, metric, args.cpu_seconds)
     return out, index
 
 
-def ivf_latency(torch, index, xq, k, d):
+def ivf_latency(torch, index, xq, k, d, metric=0):
     """nq = 1 / 4 through the IVF path (the extension's per-query call, faiss_index.cpp:737)."""
     stream = torch.cuda.current_stream().cuda_stream
     res = {}
@@ -545,7 +560,7 @@ def ivf_latency(torch, index, xq, k, d):
         torch.cuda.synchronize()
         probes = index.last_probes(nq)
         from ivf_build import scan_bytes
-        b = scan_bytes(index, probes, d)
+        b = scan_bytes(index, probes, d, ivf_row_bytes(index.form, d, metric))
         index.set_kernel_timing(True)
         it = 20
         t0 = time.perf_counter()
@@ -559,7 +574,7 @@ def ivf_latency(torch, index, xq, k, d):
         res[f"nq{nq}"] = {"ms_per_call": round(el * 1e3 / it, 4), "scan_kernel_ms": round(kms, 4),
                           "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                        "frac": round(gbs / HBM_PEAK_GBS, 4),
-                                       "algorithmic": f"probed lists |l|*(4d+8) = {b / 1e9:.4f} GB per call"}}
+                                       "algorithmic": f"probed lists {ivf_row_bytes_desc(index.form)} = {b / 1e9:.4f} GB per call"}}
     return res
 
 
@@ -944,7 +959,12 @@ def main():
                                world > 1 else "")}}
         sub.pop("unit", None)
         line.update(sub)
-        if args.workload == "ivf" and index.form == 5:
+        if args.workload == "ivf" and index.form == 6:
+            line["precision"] = ("returned distances are fp32 direct-form Σ(q−x)² (FAISS CPU IVFFlatScanner "
+                                 "arithmetic); the fp16-image scan only prunes, and a per-query bound "
+                                 "(|scan key − exact| ≤ 2(|q|·max‖x−x̂‖ + ‖q−q̂‖·max‖x̂‖) + fp32 accumulation) "
+                                 "proves no pruned row reaches the top-k (failures re-run on the 3-term path)")
+        elif args.workload == "ivf" and index.form == 5:
             line["precision"] = ("returned distances are fp32 direct-form Σ(q−x)² (FAISS CPU IVFFlatScanner "
                                  "arithmetic); the bf16 2-term split scan only prunes, and a per-query bound "
                                  "(|scan key − exact| ≤ 2^-12·(|q|²+max|x|²)) proves no pruned row reaches the top-k "

@@ -37,13 +37,16 @@ enum Metric : int { kL2 = 0, kIP = 1 };
 // products) / 2-term bf16 split of both operands (ivf_mfma.hip, split-bf16 variant).
 // kFormSplit2Exact: the 2-term scan keeps the kRerankK best per list and every returned distance is
 // recomputed exactly in the direct form, with a per-query bound check (ivf_rerank_topk); k <= kRerankMaxK.
+// kFormHalfExact (default): the same filter + rerank, the scan over a tiled fp16 image of the rows (half
+// the bytes of the fp32 forms) with 2-term fp16 queries; the bound uses the measured fp16 residuals.
 enum IvfForm : int {
     kFormDecomposed = 0,
     kFormDirect = 1,
     kFormDecomposedValu = 2,
     kFormSplit3 = 3,
     kFormSplit2 = 4,
-    kFormSplit2Exact = 5
+    kFormSplit2Exact = 5,
+    kFormHalfExact = 6
 };
 constexpr int kRerankK = 16, kRerankMaxK = 12;
 // Flat exact form, IP: 32 candidates per (split, query).  At 10M × 768 (U(-1,1) rows) 16 left ≈0.2% of

@@ -96,18 +96,63 @@ void upload_list_meta(IvfShard &sh, const std::vector<int64_t> &off, int nlist) 
     HIPANN_CHECK(hipStreamSynchronize(sh.stream));
 }
 
+// 32-row pass offsets of every list (the tiled copies' layout); returns the total pass count.
+int64_t ensure_tpass(IvfShard &sh, int nlist, hipStream_t st) {
+    std::vector<int64_t> tp(nlist + 1, 0);
+    for (int l = 0; l < nlist; ++l) tp[l + 1] = tp[l] + ceil_div(sh.h_off[l + 1] - sh.h_off[l], 32);
+    if (!sh.tpass_off.p) {
+        sh.tpass_off.ensure(sizeof(int64_t) * (nlist + 1), sh.device);
+        HIPANN_CHECK(hipMemcpyAsync(sh.tpass_off.p, tp.data(), sizeof(int64_t) * (nlist + 1), hipMemcpyHostToDevice, st));
+        HIPANN_CHECK(hipStreamSynchronize(st));  // tp (host) is released on return
+    }
+    return tp[nlist];
+}
+
 // The MFMA scan's tiled copy of the codes (built once, at the first search that uses it).
 void ensure_tiled_codes(IvfShard &sh, int d, int nlist, hipStream_t st) {
     if (sh.codes_t.p || sh.n == 0) return;
-    std::vector<int64_t> tp(nlist + 1, 0);
-    for (int l = 0; l < nlist; ++l) tp[l + 1] = tp[l] + ceil_div(sh.h_off[l + 1] - sh.h_off[l], 32);
+    const int64_t np = ensure_tpass(sh, nlist, st);
     const int64_t pf = ivf_mfma_pass_floats(d);
-    sh.codes_t.ensure(sizeof(float) * (size_t)std::max<int64_t>(tp[nlist], 1) * pf, sh.device);
-    sh.tpass_off.ensure(sizeof(int64_t) * (nlist + 1), sh.device);
-    HIPANN_CHECK(hipMemcpyAsync(sh.tpass_off.p, tp.data(), sizeof(int64_t) * (nlist + 1), hipMemcpyHostToDevice, st));
-    launch_ivf_tile_codes(sh.codes, sh.list_off.get<int64_t>(), sh.tpass_off.get<int64_t>(), nlist, tp[nlist], d,
+    sh.codes_t.ensure(sizeof(float) * (size_t)std::max<int64_t>(np, 1) * pf, sh.device);
+    launch_ivf_tile_codes(sh.codes, sh.list_off.get<int64_t>(), sh.tpass_off.get<int64_t>(), nlist, np, d,
                           sh.codes_t.get<float>(), st);
-    HIPANN_CHECK(hipStreamSynchronize(st));  // tp (host) is released on return
+    HIPANN_CHECK(hipStreamSynchronize(st));
+}
+
+// kFormHalfExact: the tiled fp16 image of x·s, s = 2^half_es with max|x| = f·2^e, f ∈ [½, 1), half_es =
+// 14 − e (every scaled element < 2^14), and the largest row residual ‖x − x̂/s‖ (built once).  Codes
+// with a non-finite entry or a scale outside 2^±100 leave the form unsupported (the search then takes
+// kFormSplit2Exact).  Returns whether the image is usable.
+bool ensure_half_codes(IvfShard &sh, int d, int nlist, hipStream_t st) {
+    if (sh.half_state != 0) return sh.half_state > 0;
+    if (sh.n == 0) return false;  // nothing to scan (and nothing to measure); retried after an add
+    sh.nflag.ensure(sizeof(int), sh.device);
+    unsigned bits = 0;
+    launch_ivf_max_abs(sh.codes, sh.n * (int64_t)d, sh.nflag.get<unsigned>(), st);
+    HIPANN_CHECK(hipMemcpyAsync(&bits, sh.nflag.p, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    HIPANN_CHECK(hipStreamSynchronize(st));
+    float mx;
+    std::memcpy(&mx, &bits, sizeof(mx));
+    int e = 0;
+    if (bits != 0 && bits < 0x7f800000u) (void)std::frexp(mx, &e);
+    if (bits >= 0x7f800000u || e < -100 || e > 100) {
+        sh.half_state = -1;
+        return false;
+    }
+    sh.half_es = 14 - e;
+    const float scale = std::ldexp(1.f, sh.half_es);
+    const int64_t np = ensure_tpass(sh, nlist, st);
+    sh.codes_h.ensure((size_t)std::max<int64_t>(np, 1) * (size_t)ivf_half_pass_bytes(d), sh.device);
+    launch_ivf_tile_half(sh.codes, sh.list_off.get<int64_t>(), sh.tpass_off.get<int64_t>(), nlist, np, d, scale,
+                         sh.codes_h.p, st);
+    launch_ivf_half_residual(sh.codes, sh.n, d, scale, sh.nflag.get<unsigned>(), st);
+    HIPANN_CHECK(hipMemcpyAsync(&bits, sh.nflag.p, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    HIPANN_CHECK(hipStreamSynchronize(st));
+    float r2;
+    std::memcpy(&r2, &bits, sizeof(r2));
+    sh.half_rxmax = std::sqrt(r2) * 1.0001f;  // fp32 sum of d exact squares: relative error ≪ 1e-4
+    sh.half_state = 1;
+    return true;
 }
 
 // ‖x‖² of every stored row (L2 only): the decomposed scan form reads it with the codes
@@ -179,6 +224,12 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     // the decomposed forms need float4 rows (else the direct kernel, also on the GPU); the MFMA kernel
     // keeps 16-lane lists (k <= 16) and the item's queries in LDS (else the VALU decomposed kernel)
     int req = form_override >= 0 ? form_override : ix.form;
+    // kFormHalfExact: the fp16-image scan as the filter of the same rerank (else kFormSplit2Exact)
+    bool half = false;
+    if (req == kFormHalfExact) {
+        half = kout <= kRerankMaxK && !bigk && ivf_mfma_h_supported(d, kRerankK) && ensure_half_codes(sh, d, nlist, st);
+        req = kFormSplit2Exact;
+    }
     // kFormSplit2Exact: the 2-term scan keeps kRerankK per list, the rerank makes the results exact
     // (k > kRerankMaxK leaves too little margin: the 3-term scan instead)
     const bool want_exact = req == kFormSplit2Exact;
@@ -186,12 +237,14 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     const int k_user = k;
     const int kscan = want_exact && req == kFormSplit2 ? kRerankK : k;
     int form = req != kFormDirect && !bigk && ivf_dot_supported(xq, d, sh.codes) ? req : kFormDirect;
-    if (ivf_form_split(form) && !ivf_mfma_bf_supported(xq, d, sh.codes, kscan, ivf_form_terms(form))) form = kFormDecomposed;
+    if (half) form = kFormSplit2;  // any d: the fp16 image is zero-padded to whole super-steps
+    if (!half && ivf_form_split(form) && !ivf_mfma_bf_supported(xq, d, sh.codes, kscan, ivf_form_terms(form)))
+        form = kFormDecomposed;
     if (form == kFormDecomposed && !ivf_mfma_supported(xq, d, sh.codes, kscan)) form = kFormDecomposedValu;
     const bool exact = want_exact && form == kFormSplit2;
     k = kscan;  // per-list k of the scan (the output keeps kout)
     const bool tiled = form == kFormDecomposed || ivf_form_split(form);  // the matrix-core scans
-    const int group = ivf_group_size(form, d);
+    const int group = half ? ivf_mfma_h_group(d) : ivf_group_size(form, d);
     launch_ivf_plan(sh.coarse_i.get<int64_t>(), nq, np, sh.list_len.get<int>(), nlist, group, sh.cnt.get<int>(),
                     sh.bucket_off.get<int>(), sh.item_off.get<int>(), sh.cursor.get<int>(), sh.bucket.get<int>(),
                     sh.slot_off.get<int>(), st);
@@ -213,12 +266,23 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
         qbound = sh.qbound.get<unsigned>();
         HIPANN_CHECK(hipMemsetD32Async((hipDeviceptr_t)qbound, 0xff800000, (size_t)nq, st));
     }
-    if (tiled) ensure_tiled_codes(sh, d, nlist, st);
-    if (ivf_form_split(form))
+    if (tiled && !half) ensure_tiled_codes(sh, d, nlist, st);
+    if (half) {
+        sh.hsplit.ensure((size_t)ivf_half_qsplit_bytes(nq, d), sh.device);
+        sh.hits.ensure(sizeof(float) * (size_t)nq, sh.device);
+        sh.hres.ensure(sizeof(float) * (size_t)nq, sh.device);
+    } else if (ivf_form_split(form)) {
         sh.qsplit.ensure((size_t)ivf_mfma_bf_qsplit_bytes(nq, d, ivf_form_terms(form)), sh.device);
+    }
     {
         ScopedTiming t(ix.timer_main, st);
-        if (bigk)
+        if (half)
+            launch_ivf_scan_mfma_h(xq, nq, sh.hsplit.p, sh.hits.get<float>(), sh.hres.get<float>(), sh.half_es, qn, d,
+                                   metric, sh.codes_h.p, sh.tpass_off.get<int64_t>(), sh.xnorm.get<float>(),
+                                   sh.list_off.get<int64_t>(), sh.cnt.get<int>(), sh.bucket_off.get<int>(),
+                                   sh.item_off.get<int>(), sh.bucket.get<int>(), sh.slot_off.get<int>(), nlist, np, k,
+                                   max_items, qbound, sh.part_d.get<float>(), sh.part_i.get<int>(), st);
+        else if (bigk)
             launch_ivf_scan_bigk(xq, d, metric, sh.codes, sh.list_off.get<int64_t>(), sh.coarse_i.get<int64_t>(),
                                  nq * np, np, sh.slot_off.get<int>(), nq * np * std::max(sh.max_nch, 1), k,
                                  sh.part_d.get<float>(), sh.part_i.get<int>(), st);
@@ -254,7 +318,8 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     {
         ScopedTiming t(ix.timer_merge, st);
         launch_ivf_rerank(sh.part_d.get<float>(), sh.part_i.get<int>(), sh.slot_off.get<int>(), np, nq, k, kout, metric,
-                          xq, sh.codes, d, sh.ids, sh.n, 0, xmax2, D, I, sh.nflag.get<int>(), sh.flagged.get<int>(), st);
+                          xq, sh.codes, d, sh.ids, sh.n, 0, xmax2, D, I, sh.nflag.get<int>(), sh.flagged.get<int>(), st,
+                          kSplit2Eps, half ? sh.half_rxmax : -1.f, half ? sh.hres.get<float>() : nullptr);
     }
     int nf = 0;
     HIPANN_CHECK(hipMemcpyAsync(&nf, sh.nflag.p, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -371,8 +436,10 @@ static void ivf_add_rows(IvfIndex &ix, int64_t n, const float *xb, const int64_t
         sh.n = n_new;
         upload_list_meta(sh, off, nlist);
         compute_row_norms(sh, d, ix.metric);
-        sh.codes_t.release();  // the MFMA scan's tiled copy is rebuilt at the next search
+        sh.codes_t.release();  // the MFMA scans' tiled copies are rebuilt at the next search
         sh.tpass_off.release();
+        sh.codes_h.release();
+        sh.half_state = 0;
         sh.xmax2 = -1.f;
     }
 }
@@ -727,7 +794,7 @@ int hipann_ivf_set_nprobe(void *h, int nprobe) {
 }
 
 int hipann_ivf_set_form(void *h, int form) {
-    if (!h || form < kFormDecomposed || form > kFormSplit2Exact) return -1;
+    if (!h || form < kFormDecomposed || form > kFormHalfExact) return -1;
     auto *ix = static_cast<IndexBase *>(h);
     if (ix->kind != Kind::IVF) return -1;
     auto *vx = static_cast<IvfIndex *>(ix);

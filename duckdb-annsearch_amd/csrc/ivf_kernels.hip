@@ -1008,7 +1008,8 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
                 int nprobe, int64_t nq, int k, int kout, const float *__restrict__ Q,
                 const float *__restrict__ codes, int d, const int64_t *__restrict__ ids, int64_t nrows,
                 int64_t label_offset, float xmax2, float *__restrict__ D, int64_t *__restrict__ I,
-                int *__restrict__ nflag, int *__restrict__ flagged, float eps, float rxmax) {
+                int *__restrict__ nflag, int *__restrict__ flagged, float eps, float rxmax,
+                const float *__restrict__ qres) {
     const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (q >= nq) return;
     const int lane = threadIdx.x & 63;
@@ -1090,14 +1091,16 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
     const float dk = readlane_f(R.d[0], kout - 1);
     float E;
     if (rxmax >= 0.f) {
-        const float qn = sqrtf(qq), rq = sqrtf(rq2), xh = sqrtf(xmax2) + rxmax;
-        const float g = (float)d * 0x1p-24f;
+        // qres (IVF fp16 form): the query's own split residual, and 2d products per accumulator chain
+        const float qn = sqrtf(qq), rq = qres ? qres[q] : sqrtf(rq2), xh = sqrtf(xmax2) + rxmax;
+        const float g = (float)(qres ? 2 * d : d) * 0x1p-24f;
         const float eip = qn * rxmax + rq * xh + g * (qn + rq) * xh;
         E = 1.01f * ((IP ? 1.f : 2.f) * eip + (float)(d + 8) * 0x1p-24f * 2.f * (qq + xmax2));
     } else {
         E = eps * (qq + xmax2);
     }
-    if (ncand == k && !(dk < k16 - E) && lane == 0) flagged[atomicAdd(nflag, 1)] = (int)q;
+    // a non-finite bound (a query outside the fp16 form's safe scale range) is always re-run
+    if ((!(E <= 3.4e38f) || (ncand == k && !(dk < k16 - E))) && lane == 0) flagged[atomicAdd(nflag, 1)] = (int)q;
     const float pad_d = IP ? -__builtin_inff() : __builtin_inff();
     if (lane < kout) {
         const bool pad = R.id[0] == IdTraits<long long>::pad();
@@ -1136,16 +1139,16 @@ __global__ void __launch_bounds__(256) ivf_scatter_results(const float *__restri
 void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int nprobe, int64_t nq, int k, int kout,
                        int metric, const float *Q, const float *codes, int d, const int64_t *ids, int64_t nrows,
                        int64_t label_offset, float xmax2, float *D, int64_t *I, int *nflag, int *flagged,
-                       hipStream_t st, float eps, float rxmax) {
+                       hipStream_t st, float eps, float rxmax, const float *qres) {
     if (nq <= 0) return;
     HIPANN_REQUIRE(k >= kRerankK && k <= 64 && kout >= 1 && kout <= kRerankMaxK, "ivf rerank: k / kout out of range");
     dim3 grid((unsigned)ceil_div(nq, 4)), block(256);
     if (metric == kIP)
         hipLaunchKernelGGL(ivf_rerank_topk<true>, grid, block, 0, st, pd, pi, slot_off, nprobe, nq, k, kout, Q, codes, d,
-                           ids, nrows, label_offset, xmax2, D, I, nflag, flagged, eps, rxmax);
+                           ids, nrows, label_offset, xmax2, D, I, nflag, flagged, eps, rxmax, qres);
     else
         hipLaunchKernelGGL(ivf_rerank_topk<false>, grid, block, 0, st, pd, pi, slot_off, nprobe, nq, k, kout, Q, codes,
-                           d, ids, nrows, label_offset, xmax2, D, I, nflag, flagged, eps, rxmax);
+                           d, ids, nrows, label_offset, xmax2, D, I, nflag, flagged, eps, rxmax, qres);
     HIPANN_CHECK(hipGetLastError());
 }
 

@@ -914,4 +914,451 @@ void launch_ivf_scan_mfma_bf(int np, const float *Q, int64_t nq, void *qsplit, c
     HIPANN_CHECK(hipGetLastError());
 }
 
+
+// ================================================================================================
+// fp16-image variant (form kFormHalfExact): the list scan reads HALF the bytes of the fp32 forms.
+// The rows are stored once as a tiled fp16 image of x·s (s = 2^(14 − e), max|x| = f·2^e, f ∈ [½, 1):
+// every scaled element ≤ 2^14, far inside fp16's range), round to nearest even, subnormal results
+// flushed to zero; each query is scaled the same way (t = 2^(14 − e_q)) and split into two fp16 terms
+// q·t = h + l (+ ≤ 2⁻²² relative), so q·x ≈ (h + l)·x̂ / (t·s) on v_mfma_f32_16x16x32_f16 (fp16 × fp16
+// products are exact in fp32, fp32 accumulation).  The only non-negligible error is the rows' own
+// fp16 rounding, |q·(x − x̂/s)| ≤ ‖q‖·‖x − x̂/s‖, and the scan is a FILTER: it keeps the 16 best per
+// (query, list, chunk) like form 5, ivf_rerank_topk recomputes them in FAISS's direct fp32 form and
+// proves with the measured residuals (largest row residual, this query's split residual) that no
+// pruned row reaches the top-k; failing queries re-run on the 3-term path.
+// Image layout (per list, 32-row passes as codes_t): [pass][32-dim super-step S][row tile r][lane (g, m)]
+// [8 halves] = row 16r + m, dims 32S + 4g + j and 32S + 16 + 4g + j (j < 4) — the k-slot order of the
+// split-bf16 variant, so a wave load is 1 KiB contiguous and a pass of d = 768 is 48 KiB.
+typedef _Float16 mh_f16x8 __attribute__((ext_vector_type(8)));
+constexpr int MH_P = 6;  // super-steps in flight per wave: 6 × 2 row tiles × 16 B = 192 B per lane
+__host__ __device__ inline int mh_nsup(int d) { return (int)ceil_div(ceil_div(d, 32), MH_P) * MH_P; }
+// LDS dwords per query: 2 terms × super-steps × 4 groups × 4 dwords, + 8 (≡ 8 mod 64: conflict-free)
+__host__ __device__ inline int mh_stride(int d) { return 2 * mh_nsup(d) * 16 + 8; }
+inline int mh_group(int d) {
+    const int g = (int)(MF_LDS_MAX / ((size_t)mh_stride(d) * 4)) / 16 * 16;
+    return g < 16 * MF_QTMAX ? g : 16 * MF_QTMAX;
+}
+
+// fp32 → fp16 round to nearest even; subnormal results flushed to zero (the MFMA sees only normal
+// values or zero whatever its denormal mode, and the residuals are measured against exactly this)
+__device__ __forceinline__ unsigned short mh_half_bits(float v) {
+    const _Float16 h = (_Float16)v;
+    return __builtin_fabsf((float)h) < 0x1p-14f ? (unsigned short)0 : __builtin_bit_cast(unsigned short, h);
+}
+__device__ __forceinline__ float mh_val(unsigned short b) { return (float)__builtin_bit_cast(_Float16, b); }
+__device__ __forceinline__ unsigned mh_pack(float a, float b) {
+    return (unsigned)mh_half_bits(a) | ((unsigned)mh_half_bits(b) << 16);
+}
+
+__device__ __forceinline__ mf_f32x4 mh_mfma(const uint4 &a, const uint4 &b, const mf_f32x4 &c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(mh_f16x8, a), __builtin_bit_cast(mh_f16x8, b), c,
+                                                  0, 0, 0);
+}
+
+// max |x| over cnt floats as the bits of the magnitude (unsigned order = magnitude order; any NaN
+// compares above +inf, so a non-finite table is detected by bits >= 0x7f800000)
+__global__ void __launch_bounds__(256) ivf_max_abs(const float *__restrict__ x, int64_t cnt, unsigned *__restrict__ out) {
+    unsigned m = 0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * 256)
+        m = max(m, __float_as_uint(x[i]) & 0x7fffffffu);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o));
+    if ((threadIdx.x & 63) == 0) atomicMax(out, m);
+}
+
+// one block per 32-row pass (list found by binary search over the pass offsets); zero past the
+// list's end and past d
+__global__ void __launch_bounds__(256)
+ivf_tile_half(const float *__restrict__ codes, const int64_t *__restrict__ list_off, const int64_t *__restrict__ tpass_off,
+              int nlist, int d, int nsup, float scale, uint4 *__restrict__ dst) {
+    const int64_t pass = blockIdx.x;
+    int lo = 0, hi = nlist - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (tpass_off[mid] <= pass) lo = mid; else hi = mid - 1;
+    }
+    const int64_t len = list_off[lo + 1] - list_off[lo];
+    const int64_t prow = (pass - tpass_off[lo]) * MF_PASS;
+    const int nt = nsup * MF_RT * 64;
+    for (int t = threadIdx.x; t < nt; t += 256) {
+        const int S = t / (MF_RT * 64), rem = t - S * (MF_RT * 64);
+        const int r = rem >> 6, lane = rem & 63, g = lane >> 4, m = lane & 15;
+        const int64_t row = prow + 16 * r + m;
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = 0.f;
+        if (row < len) {
+            const float *src = codes + (list_off[lo] + row) * (int64_t)d;
+            const int d0 = 32 * S + 4 * g, d1 = d0 + 16;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (d0 + j < d) v[j] = src[d0 + j] * scale;
+                if (d1 + j < d) v[4 + j] = src[d1 + j] * scale;
+            }
+        }
+        dst[pass * nt + t] = make_uint4(mh_pack(v[0], v[1]), mh_pack(v[2], v[3]), mh_pack(v[4], v[5]), mh_pack(v[6], v[7]));
+    }
+}
+
+// max over rows of ‖x − x̂/s‖² (one wave per row), as float bits
+__global__ void __launch_bounds__(256) ivf_half_residual(const float *__restrict__ codes, int64_t n, int d, float scale,
+                                                         float inv_scale, unsigned *__restrict__ out) {
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    float s = 0.f;
+    if (row < n) {
+        const float *src = codes + row * (int64_t)d;
+        for (int e = lane; e < d; e += 64) {
+            const float x = src[e];
+            const float r = x - mh_val(mh_half_bits(x * scale)) * inv_scale;  // exact (Sterbenz / flushed: r = x)
+            s = fmaf(r, r, s);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0 && row < n) atomicMax(out, __float_as_uint(s));
+}
+
+// The batch's queries, one wave per query: t = 2^(14 − e_q), q·t split into two fp16 terms in the
+// image's k-slot order, qsplit [query][term][super-step][g][8 halves]; its[q] = 1/(t·s) (a power of
+// two) and qres[q] = ‖q − (h + l)/t‖ (×1.0001 for the fp32 sum).  A query whose scale leaves the safe
+// range (non-finite entries, |e_q| > 100, 1/(t·s) not a normal float) gets zero terms and qres = +inf:
+// the rerank flags it and it re-runs on the 3-term path.
+__global__ void __launch_bounds__(256) ivf_split_queries_h(const float *__restrict__ Q, int64_t nq, int d, int nsup,
+                                                           int es, uint4 *__restrict__ out, float *__restrict__ its,
+                                                           float *__restrict__ qres) {
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq) return;
+    const int lane = threadIdx.x & 63;
+    const float *src = Q + q * (int64_t)d;
+    unsigned mb = 0;
+    for (int e = lane; e < d; e += 64) mb = max(mb, __float_as_uint(src[e]) & 0x7fffffffu);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mb = max(mb, (unsigned)__shfl_xor((int)mb, o));
+    int eq = 0;
+    if (mb != 0 && mb < 0x7f800000u) (void)frexpf(__uint_as_float(mb), &eq);
+    const int et = 14 - eq;
+    const int eits = -(et + es);
+    const bool ok = mb < 0x7f800000u && eq >= -100 && eq <= 100 && eits >= -120 && eits <= 120;
+    const float t = ldexpf(1.f, ok ? et : 0), inv_t = ldexpf(1.f, ok ? -et : 0);
+    float r2 = 0.f;
+    for (int w = lane; w < nsup * 4; w += 64) {
+        const int S = w >> 2, gg = w & 3;
+        const int d0 = 32 * S + 4 * gg, d1 = d0 + 16;
+        float a[8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            a[j] = ok && d0 + j < d ? src[d0 + j] * t : 0.f;
+            a[4 + j] = ok && d1 + j < d ? src[d1 + j] * t : 0.f;
+        }
+        unsigned hw[4], lw[4];
+#pragma unroll
+        for (int pr = 0; pr < 4; ++pr) {
+            const float x0 = a[2 * pr], x1 = a[2 * pr + 1];
+            hw[pr] = mh_pack(x0, x1);
+            const float m0 = x0 - mh_val((unsigned short)(hw[pr] & 0xffffu)), m1 = x1 - mh_val((unsigned short)(hw[pr] >> 16));
+            lw[pr] = mh_pack(m0, m1);
+            const float e0 = (m0 - mh_val((unsigned short)(lw[pr] & 0xffffu))) * inv_t;
+            const float e1 = (m1 - mh_val((unsigned short)(lw[pr] >> 16))) * inv_t;
+            r2 = fmaf(e0, e0, r2);
+            r2 = fmaf(e1, e1, r2);
+        }
+        out[((q * 2 + 0) * nsup + S) * 4 + gg] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+        out[((q * 2 + 1) * nsup + S) * 4 + gg] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) r2 += __shfl_xor(r2, o);
+    if (lane == 0) {
+        its[q] = ldexpf(1.f, ok ? eits : 0);
+        qres[q] = ok ? sqrtf(r2) * 1.0001f : __builtin_inff();
+    }
+}
+
+template <int QT, bool IP>
+__device__ __forceinline__ void mh_item(int d, const uint4 *__restrict__ codes_h, int64_t tp0,
+                                        const float *__restrict__ xn, int64_t r0, int64_t r1, int nqi,
+                                        const unsigned *__restrict__ qs, int stride, const float (&qn)[QT][4],
+                                        const float (&qits)[QT][4], const unsigned (&qb)[QT][4],
+                                        const int *__restrict__ bucket, int boff, int nprobe,
+                                        const int *__restrict__ slot_off, int chunk, int k, float *smem,
+                                        unsigned *__restrict__ qbound, float *__restrict__ part_d,
+                                        int *__restrict__ part_i) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int m = lane & 15, g = lane >> 4;
+    const int nsup = mh_nsup(d);
+    const int npass_all = (int)ceil_div(r1 - r0, MF_PASS);
+    const int npass = npass_all > wave ? (npass_all - wave + MF_WAVES - 1) / MF_WAVES : 0;
+
+    bool qv[QT][4];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) qv[qt][v] = qt * 16 + 4 * g + v < nqi;
+    uint64_t lst[QT][4], thr[QT][4];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const uint64_t b = ((uint64_t)qb[qt][v] << 32) | MF_PAD_ID;
+            lst[qt][v] = m < k ? b : MF_EMPTY;
+            thr[qt][v] = b;
+        }
+
+    auto row_of = [&](int i, int r) -> int64_t {
+        const int64_t row = r0 + (int64_t)(wave + MF_WAVES * i) * MF_PASS + 16 * r + m;
+        return row < r1 ? row : r1 - 1;
+    };
+    const int ilast = npass > 0 ? npass - 1 : 0;
+    const uint4 *rp;
+    int ld_i = 0, ld_s = 0;  // stream position (super-steps), wave-uniform
+    auto set_pass = [&](int i) { rp = codes_h + ((tp0 + wave + MF_WAVES * i) * nsup) * (MF_RT * 64) + lane; };
+    // unconditional loads (past the wave's last step they re-read it): see mf_item
+    auto next_load = [&](uint4 (&dst)[MF_RT]) {
+        const int s = ld_i <= ilast ? ld_s : nsup - 1;
+#pragma unroll
+        for (int r = 0; r < MF_RT; ++r) dst[r] = rp[(int64_t)s * (MF_RT * 64) + r * 64];
+        if (++ld_s == nsup) {
+            ld_s = 0;
+            ++ld_i;
+            set_pass(ld_i <= ilast ? ld_i : ilast);
+        }
+    };
+
+    uint4 ring[MH_P][MF_RT];
+    float xnr[MF_RT] = {0.f, 0.f};
+    if (npass > 0) {
+        set_pass(0);
+#pragma unroll
+        for (int p = 0; p < MH_P; ++p) next_load(ring[p]);
+        if (!IP) {
+#pragma unroll
+            for (int r = 0; r < MF_RT; ++r) xnr[r] = xn[row_of(0, r)];
+        }
+    }
+    const unsigned *qrow[QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) qrow[qt] = qs + (qt * 16 + m) * stride + 4 * g;
+
+    mf_f32x4 acc[QT][MF_RT];
+    for (int i = 0; i < npass; ++i) {
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+            for (int r = 0; r < MF_RT; ++r) acc[qt][r] = mf_f32x4{0.f, 0.f, 0.f, 0.f};
+        float xnr_next[MF_RT] = {0.f, 0.f};
+        if (!IP) {
+#pragma unroll
+            for (int r = 0; r < MF_RT; ++r) xnr_next[r] = xn[row_of(i + 1 <= ilast ? i + 1 : ilast, r)];
+        }
+        for (int S0 = 0; S0 < nsup; S0 += MH_P) {
+#pragma unroll
+            for (int p = 0; p < MH_P; ++p) {
+                const int S = S0 + p;
+                uint4 qa[QT][2];
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j) qa[qt][j] = *reinterpret_cast<const uint4 *>(qrow[qt] + (j * nsup + S) * 16);
+                // the small query term first in every accumulator chain
+#pragma unroll
+                for (int j = 1; j >= 0; --j)
+#pragma unroll
+                    for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                        for (int r = 0; r < MF_RT; ++r) acc[qt][r] = mh_mfma(qa[qt][j], ring[p][r], acc[qt][r]);
+                next_load(ring[p]);
+            }
+        }
+        const int64_t prow0 = r0 + (int64_t)(wave + MF_WAVES * i) * MF_PASS;
+#pragma unroll
+        for (int r = 0; r < MF_RT; ++r) {
+            const int64_t row = prow0 + 16 * r + m;
+            const bool rok = row < r1;
+            const unsigned rid = rok ? (unsigned)row : MF_PAD_ID;
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    float key;
+                    if (IP) {
+                        key = -acc[qt][r][v] * qits[qt][v];
+                    } else {
+                        key = fmaf(-2.f * qits[qt][v], acc[qt][r][v], qn[qt][v] + xnr[r]);
+                        key = key < 0.f ? 0.f : key;
+                    }
+                    const bool ok = rok && qv[qt][v];
+                    uint64_t cp = ok ? (((uint64_t)mf_sortable(key) << 32) | rid) : MF_EMPTY;
+                    if (__ballot(cp < thr[qt][v])) {
+                        row_sort16(cp, m);
+                        row_merge16(lst[qt][v], cp, m);
+                        thr[qt][v] = row_kth(lst[qt][v], k - 1, g);
+                    }
+                }
+        }
+#pragma unroll
+        for (int r = 0; r < MF_RT; ++r) xnr[r] = xnr_next[r];
+    }
+
+    uint64_t *scratch = reinterpret_cast<uint64_t *>(smem);
+#pragma unroll 1
+    for (int half = MF_WAVES / 2; half > 0; half >>= 1) {
+        __syncthreads();
+        if (wave >= half && wave < 2 * half) {
+            uint64_t *dst = scratch + (size_t)(wave - half) * QT * 4 * 64;
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) dst[(qt * 4 + v) * 64 + lane] = lst[qt][v];
+        }
+        __syncthreads();
+        if (wave < half) {
+            const uint64_t *src = scratch + (size_t)wave * QT * 4 * 64;
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) row_merge16(lst[qt][v], src[(qt * 4 + v) * 64 + lane], m);
+        }
+    }
+    if (wave == 0 && m < k) {
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const int q = qt * 16 + 4 * g + v;
+                if (q < nqi) {
+                    const int pr = bucket[boff + q];
+                    const int64_t off = (int64_t)(slot_off[pr] + chunk) * k + m;
+                    const uint64_t e = lst[qt][v];
+                    const unsigned id = (unsigned)e;
+                    const bool real = e != MF_EMPTY && id != MF_PAD_ID;
+                    part_d[off] = real ? mf_unsortable((unsigned)(e >> 32)) : __builtin_inff();
+                    part_i[off] = real ? (int)id : (int)MF_PAD_ID;
+                    if (m == k - 1 && real) atomicMin(qbound + pr / nprobe, (unsigned)(e >> 32));
+                }
+            }
+    }
+}
+
+template <bool IP>
+__global__ void __launch_bounds__(MF_THREADS, MF_WAVES / 4)
+ivf_scan_mfma_h(const uint4 *__restrict__ qsplit, const float *__restrict__ qnorm, const float *__restrict__ its, int d,
+                const uint4 *__restrict__ codes_h, const int64_t *__restrict__ tpass_off, const float *__restrict__ xn,
+                const int64_t *__restrict__ list_off, const int *__restrict__ cnt, const int *__restrict__ bucket_off,
+                const int *__restrict__ item_off, const int *__restrict__ bucket, const int *__restrict__ slot_off,
+                int nlist, int nprobe, int group, int k, unsigned *__restrict__ qbound, float *__restrict__ part_d,
+                int *__restrict__ part_i) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int total = item_off[nlist];
+    if ((int)blockIdx.x >= total) return;
+    const int item = xcd_remap((int)blockIdx.x, total);
+    int lo = 0, hi = nlist - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (item_off[mid] <= item) lo = mid; else hi = mid - 1;
+    }
+    const int l = lo;
+    const int64_t lr0 = list_off[l], lr1 = list_off[l + 1];
+    const int c = cnt[l];
+    const int ng = (c + group - 1) / group;
+    const int rem = item - item_off[l];
+    const int chunk = rem / ng, grp = rem - chunk * ng;
+    const int q_begin = (int)((int64_t)grp * c / ng), q_end = (int)((int64_t)(grp + 1) * c / ng);
+    const int nqi = q_end - q_begin;
+    const int64_t r0 = lr0 + (int64_t)chunk * MF_CH;
+    const int64_t r1 = r0 + MF_CH < lr1 ? r0 + MF_CH : lr1;
+    const int boff = bucket_off[l] + q_begin;
+    const int nqt = (nqi + 15) >> 4;
+
+    unsigned *qs = reinterpret_cast<unsigned *>(smem);
+    const int stride = mh_stride(d);
+    mb_fill<2, 1>(qs, qsplit, mh_nsup(d), stride, 0, nqi, bucket, boff, nprobe);
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, g = lane >> 4;
+    const int64_t tp0 = tpass_off[l] + (int64_t)chunk * (MF_CH / MF_PASS);
+#define MH_ARGS d, codes_h, tp0, xn, r0, r1, nqi, qs, stride, qn, qi_s, qb, bucket, boff, nprobe, slot_off, chunk, k, smem, \
+                qbound, part_d, part_i
+#define MH_QN(QTV)                                                                                          \
+    float qn[QTV][4], qi_s[QTV][4];                                                                         \
+    unsigned qb[QTV][4];                                                                                    \
+    _Pragma("unroll") for (int qt = 0; qt < QTV; ++qt) _Pragma("unroll") for (int v = 0; v < 4; ++v) {      \
+        const int q = qt * 16 + 4 * g + v;                                                                  \
+        const int qi = q < nqi ? bucket[boff + q] / nprobe : 0;                                             \
+        qn[qt][v] = (!IP && q < nqi) ? qnorm[qi] : 0.f;                                                     \
+        qi_s[qt][v] = q < nqi ? its[qi] : 0.f;                                                              \
+        qb[qt][v] = q < nqi ? __atomic_load_n(qbound + qi, __ATOMIC_RELAXED) : 0xffffffffu;                 \
+    }
+    if (nqt <= 1) {
+        MH_QN(1)
+        mh_item<1, IP>(MH_ARGS);
+    } else if (nqt == 2) {
+        MH_QN(2)
+        mh_item<2, IP>(MH_ARGS);
+    } else {
+        MH_QN(3)
+        mh_item<3, IP>(MH_ARGS);
+    }
+#undef MH_QN
+#undef MH_ARGS
+}
+
+int ivf_mfma_h_group(int d) { return mh_group(d); }
+int64_t ivf_half_pass_bytes(int d) { return (int64_t)mh_nsup(d) * MF_RT * 64 * 16; }
+int64_t ivf_half_qsplit_bytes(int64_t nq, int d) { return nq * 2 * mh_nsup(d) * 64; }
+bool ivf_mfma_h_supported(int d, int k) { return d >= 1 && k >= 1 && k <= MF_KMAX && mh_group(d) >= 16; }
+
+void launch_ivf_max_abs(const float *x, int64_t cnt, unsigned *out, hipStream_t st) {
+    HIPANN_CHECK(hipMemsetAsync(out, 0, sizeof(unsigned), st));
+    if (cnt <= 0) return;
+    const unsigned blocks = (unsigned)std::min<int64_t>(4096, ceil_div(cnt, 256));
+    hipLaunchKernelGGL(ivf_max_abs, dim3(blocks), dim3(256), 0, st, x, cnt, out);
+    HIPANN_CHECK(hipGetLastError());
+}
+
+void launch_ivf_tile_half(const float *codes, const int64_t *list_off, const int64_t *tpass_off, int nlist,
+                          int64_t total_pass, int d, float scale, void *dst, hipStream_t st) {
+    if (total_pass <= 0) return;
+    HIPANN_REQUIRE(total_pass < (int64_t)0x7fffffff, "too many passes");
+    hipLaunchKernelGGL(ivf_tile_half, dim3((unsigned)total_pass), dim3(256), 0, st, codes, list_off, tpass_off, nlist, d,
+                       mh_nsup(d), scale, static_cast<uint4 *>(dst));
+    HIPANN_CHECK(hipGetLastError());
+}
+
+void launch_ivf_half_residual(const float *codes, int64_t n, int d, float scale, unsigned *out, hipStream_t st) {
+    HIPANN_CHECK(hipMemsetAsync(out, 0, sizeof(unsigned), st));
+    if (n <= 0) return;
+    HIPANN_REQUIRE(ceil_div(n, 4) < (int64_t)0x7fffffff, "too many rows");
+    hipLaunchKernelGGL(ivf_half_residual, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, st, codes, n, d, scale,
+                       1.f / scale, out);
+    HIPANN_CHECK(hipGetLastError());
+}
+
+void launch_ivf_scan_mfma_h(const float *Q, int64_t nq, void *qsplit, float *its, float *qres, int es, const float *qn,
+                            int d, int metric, const void *codes_h, const int64_t *tpass_off, const float *xn,
+                            const int64_t *list_off, const int *cnt, const int *bucket_off, const int *item_off,
+                            const int *bucket, const int *slot_off, int nlist, int nprobe, int k, int64_t max_items,
+                            unsigned *qbound, float *pd, int *pi, hipStream_t st) {
+    if (max_items <= 0 || nq <= 0) return;
+    HIPANN_REQUIRE(max_items < (int64_t)0x7fffffff, "too many IVF work items");
+    HIPANN_REQUIRE(qsplit && its && qres && codes_h, "fp16 IVF scan: missing buffers");
+    HIPANN_REQUIRE(ivf_mfma_h_supported(d, k), "fp16 IVF scan needs k <= 16");
+    HIPANN_REQUIRE(metric == kIP || (qn && xn), "decomposed L2 scan needs query and row norms");
+    const int nsup = mh_nsup(d);
+    uint4 *qs = static_cast<uint4 *>(qsplit);
+    hipLaunchKernelGGL(ivf_split_queries_h, dim3((unsigned)ceil_div(nq, 4)), dim3(256), 0, st, Q, nq, d, nsup, es, qs,
+                       its, qres);
+    const int group = mh_group(d);
+    const size_t merge = (size_t)(MF_WAVES / 2) * MF_QTMAX * 4 * 64 * sizeof(float2);
+    const size_t smem = std::max((size_t)group * mh_stride(d) * 4, merge);
+    dim3 grid((unsigned)max_items), block(MF_THREADS);
+    const uint4 *ch = static_cast<const uint4 *>(codes_h);
+#define MH_LAUNCH_ARGS qs, qn, its, d, ch, tpass_off, xn, list_off, cnt, bucket_off, item_off, bucket, slot_off, nlist, nprobe, \
+                       group, k, qbound, pd, pi
+    if (metric == kIP) hipLaunchKernelGGL((ivf_scan_mfma_h<true>), grid, block, smem, st, MH_LAUNCH_ARGS);
+    else hipLaunchKernelGGL((ivf_scan_mfma_h<false>), grid, block, smem, st, MH_LAUNCH_ARGS);
+#undef MH_LAUNCH_ARGS
+    HIPANN_CHECK(hipGetLastError());
+}
+
 }  // namespace hipann

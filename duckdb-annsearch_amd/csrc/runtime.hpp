@@ -203,13 +203,19 @@ struct IvfShard {
     // [16-dim step][2 row tiles][64 lanes][float4] (ivf_mfma.hip), zero-padded rows / dims
     std::vector<int64_t> h_off;    // host copy of list_off
     DevBuf codes_t, tpass_off;     // tiled codes; int64 nlist+1 pass offsets
+    // kFormHalfExact: tiled fp16 image of x·2^half_es (same passes as codes_t), its largest row
+    // residual ‖x − x̂·2^−half_es‖ and the batch's query terms / 1/(t·s) / split residuals.
+    // half_state: 0 not built, 1 built, −1 unsupported (non-finite or out-of-range codes)
+    int half_state = 0, half_es = 0;
+    float half_rxmax = 0.f;
+    DevBuf codes_h, hsplit, hits, hres;
     int max_nch = 1;  // largest list's row-chunk count
 };
 
 struct IvfIndex : IndexBase {
     int nlist = 0, nprobe = 1;
     std::vector<int> owner;  // list → shard (size-balanced at create; appended rows follow their list)
-    int form = kFormSplit2Exact;
+    int form = kFormHalfExact;
     int64_t rerank_fallbacks = 0;  // queries re-run on the 3-term path by the exactness check
     std::vector<std::unique_ptr<IvfShard>> shards;
     int64_t last_nq = 0;
@@ -261,7 +267,21 @@ int64_t ivf_mfma_bf_qsplit_bytes(int64_t nq, int d, int np);
 void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int nprobe, int64_t nq, int k, int kout,
                        int metric, const float *Q, const float *codes, int d, const int64_t *ids, int64_t nrows,
                        int64_t label_offset, float xmax2, float *D, int64_t *I, int *nflag, int *flagged,
-                       hipStream_t st, float eps = kSplit2Eps, float rxmax = -1.f);
+                       hipStream_t st, float eps = kSplit2Eps, float rxmax = -1.f, const float *qres = nullptr);
+// ivf_mfma.hip, fp16-image scan (kFormHalfExact)
+int ivf_mfma_h_group(int d);
+int64_t ivf_half_pass_bytes(int d);
+int64_t ivf_half_qsplit_bytes(int64_t nq, int d);
+bool ivf_mfma_h_supported(int d, int k);
+void launch_ivf_max_abs(const float *x, int64_t cnt, unsigned *out, hipStream_t st);
+void launch_ivf_tile_half(const float *codes, const int64_t *list_off, const int64_t *tpass_off, int nlist,
+                          int64_t total_pass, int d, float scale, void *dst, hipStream_t st);
+void launch_ivf_half_residual(const float *codes, int64_t n, int d, float scale, unsigned *out, hipStream_t st);
+void launch_ivf_scan_mfma_h(const float *Q, int64_t nq, void *qsplit, float *its, float *qres, int es, const float *qn,
+                            int d, int metric, const void *codes_h, const int64_t *tpass_off, const float *xn,
+                            const int64_t *list_off, const int *cnt, const int *bucket_off, const int *item_off,
+                            const int *bucket, const int *slot_off, int nlist, int nprobe, int k, int64_t max_items,
+                            unsigned *qbound, float *pd, int *pi, hipStream_t st);
 // flat_bf16.hip
 int flat_bf16_waves(int64_t nq);
 int flat_bf16_tile_rows();

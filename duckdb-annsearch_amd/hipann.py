@@ -388,7 +388,8 @@ class HipIndexIVFFlat(_Handle):
     FORM_DECOMPOSED_VALU = 2  # the decomposed form on the VALU kernel (A/B measurement)
     FORM_SPLIT3 = 3           # decomposed, q·x on the bf16 matrix cores over a 3-term bf16 split (6 products)
     FORM_SPLIT2 = 4           # decomposed, 2-term bf16 split (3 products, ~2^-16 relative per product)
-    FORM_SPLIT2_EXACT = 5     # default: the SPLIT2 scan as a filter + exact direct-form rerank with a bound check
+    FORM_SPLIT2_EXACT = 5     # the SPLIT2 scan as a filter + exact direct-form rerank with a bound check
+    FORM_HALF_EXACT = 6       # default: the same rerank, the filter scan over a tiled fp16 image (half the bytes)
 
     @property
     def form(self) -> int:
@@ -398,7 +399,7 @@ class HipIndexIVFFlat(_Handle):
     def form(self, v: int) -> None:
         if lib().hipann_ivf_set_form(self._h, int(v)) != 0:
             raise HipAnnError("form must be 0 (decomposed), 1 (direct), 2 (decomposed, VALU), 3 or 4 (split bf16), "
-                              "5 (split bf16 + exact rerank)")
+                              "5 (split bf16 + exact rerank), 6 (fp16 image + exact rerank)")
 
     def search(self, x, k: int, nprobe: Optional[int] = None) -> Tuple[np.ndarray, np.ndarray]:
         """search(n, x, k) — with ``nprobe`` the per-call SearchParametersIVF value (hipann_ivf_search_np:

@@ -190,12 +190,12 @@ def build_ivf_list_shard(torch, hipann, gen_rows, n_total: int, d: int, nlist: i
     return _make_index(torch, hipann, d, metric, nlist, nprobe, cen, local_counts, codes, ids, dev, info)
 
 
-def scan_bytes(index, probes: np.ndarray, d: int) -> float:
+def scan_bytes(index, probes: np.ndarray, d: int, row_bytes: float = None) -> float:
     """Algorithmic HBM bytes of one batch's list scan on this shard: every distinct probed list read
-    once, |l|·(4d + 8) bytes (codes + label)."""
+    once, |l|·row_bytes — by default SURVEY §8d's |l|·(4d + 8) (fp32 codes + label)."""
     sizes = np.diff(index._offsets)
     distinct = np.unique(probes[probes >= 0])
-    return float(sizes[distinct].sum()) * (4 * d + 8)
+    return float(sizes[distinct].sum()) * (4 * d + 8 if row_bytes is None else row_bytes)
 
 
 def scan_pairs(index, probes: np.ndarray) -> int:

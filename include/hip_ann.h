@@ -190,12 +190,18 @@ int hipann_ivf_export(void *index, float *centroids, int64_t *list_offsets, int6
  * HIPANN_IVF_FORM_SPLIT2: a 2-term split (three products, ≈2^-16 relative per product). */
 #define HIPANN_IVF_FORM_SPLIT3 3
 #define HIPANN_IVF_FORM_SPLIT2 4
-/* HIPANN_IVF_FORM_SPLIT2_EXACT (default): the SPLIT2 scan keeps the 16 best rows per list only as a
+/* HIPANN_IVF_FORM_SPLIT2_EXACT: the SPLIT2 scan keeps the 16 best rows per list only as a
  * filter; every returned distance is recomputed in the direct form Σ(q−x)² (IP: q·x) in fp32, ordered by
  * (distance, label), and a per-query bound (|scan key − exact| ≤ 2^-12·(‖q‖² + max‖x‖²)) proves that no
  * pruned row could enter the top-k — queries that fail it are re-run on SPLIT3.  k ≤ 12 (larger k: SPLIT3).
  * The search call then synchronises its stream once (the flag count). */
 #define HIPANN_IVF_FORM_SPLIT2_EXACT 5
+/* HIPANN_IVF_FORM_HALF_EXACT (default): the same filter + exact rerank, the scan reading a tiled fp16
+ * image of the rows (built once: x·2^s, round to nearest even, half the bytes of the fp32 forms) against
+ * 2-term fp16 queries on the fp16 matrix cores; the bound is the Cauchy-Schwarz bound of the measured
+ * residuals (largest row ‖x − x̂‖, the query's split residual) plus fp32 accumulation.  Codes with a
+ * non-finite entry take SPLIT2_EXACT; k ≤ 12 (larger k: SPLIT3).  Results equal SPLIT2_EXACT's. */
+#define HIPANN_IVF_FORM_HALF_EXACT 6
 int hipann_ivf_set_form(void *index, int form);
 int hipann_ivf_get_form(void *index);
 /* Queries re-run on HIPANN_IVF_FORM_SPLIT3 by the exact form's bound check since the index was created. */

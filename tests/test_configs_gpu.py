@@ -109,7 +109,7 @@ def c3_oracle(c3_index, oracle):
     return oracle.ivf_search(cen, off, ids, codes, xq, 10, 32, 0)
 
 
-@pytest.mark.parametrize("form", [5, 3, 0])
+@pytest.mark.parametrize("form", [6, 5, 3, 0])
 def test_c3_ivf_nlist1024_nprobe32_d768_nq1024(gpu, c3_index, c3_oracle, form):
     """C3 shape: nlist = 1024, nprobe = 32, d = 768, nq = 1024, k = 10 (200k rows of the bench's data,
     lists from the bench's GPU build).  Probe lists equal the oracle's; ids follow the parity rule over
@@ -126,10 +126,10 @@ def test_c3_ivf_nlist1024_nprobe32_d768_nq1024(gpu, c3_index, c3_oracle, form):
     assert same.mean() >= 0.99, same.mean()
     st = check_topk_parity(xb, xq[same], D[same], I[same], Do[same], Io[same], 0)
     assert st["exact_fraction"] >= 0.995, st
-    if form == 5:  # returned distances are the direct fp32 form, like the oracle's scanner
+    if form in (5, 6):  # returned distances are the direct fp32 form, like the oracle's scanner
         v = I[same] >= 0
         assert np.allclose(D[same][v], Do[same][v], rtol=2e-6, atol=1e-6)
-    index.form = 5
+    index.form = 6
 
 
 def _c4_graph(gpu, n, d, R, seed, integer=False):

@@ -47,7 +47,7 @@ def test_ivf_faiss_metal_shapes(gpu, oracle, nv, d, nlist, nprobe, nq, k, metric
 
 @pytest.mark.parametrize("nq", [1, 7, 19, 20, 64, 333])
 @pytest.mark.parametrize("metric", [0, 1])
-@pytest.mark.parametrize("form", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("form", [0, 1, 2, 3, 4, 5, 6])
 def test_ivf_vs_oracle_probe_sets(gpu, oracle, nq, metric, form):
     xb, xq = faiss_metal_case(20000, nq, 96)
     ix, (cen, off, ids, codes) = _ivf(gpu, xb, 64, 8, metric)
@@ -61,7 +61,7 @@ def test_ivf_vs_oracle_probe_sets(gpu, oracle, nq, metric, form):
 
 @pytest.mark.parametrize("d", [4, 8, 12, 20, 44, 77, 132, 768])
 @pytest.mark.parametrize("metric", [0, 1])
-@pytest.mark.parametrize("form", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("form", [0, 1, 2, 3, 4, 5, 6])
 def test_ivf_dims(gpu, oracle, d, metric, form):
     """Dimensions around the scans' LDS chunks (32 dims MFMA, 32 VALU-decomposed, 24 direct: partial
     last chunk, d < one chunk) and d % 4 != 0 (the decomposed forms fall back to the direct kernel)."""
@@ -75,7 +75,7 @@ def test_ivf_dims(gpu, oracle, d, metric, form):
 
 
 @pytest.mark.parametrize("nq", [5, 70])
-@pytest.mark.parametrize("form", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("form", [0, 1, 2, 3, 4, 5, 6])
 def test_ivf_long_lists(gpu, oracle, nq, form):
     """Lists longer than one work item's row chunk (2048 rows) and ragged 256-row tiles; with nq = 70 a
     list's probing queries split over several query groups."""
@@ -91,7 +91,7 @@ def test_ivf_long_lists(gpu, oracle, nq, form):
 
 @pytest.mark.parametrize("nq", [1, 15, 16, 17, 31, 33, 47, 48, 49, 64, 65, 130])
 @pytest.mark.parametrize("d,metric", [(96, 0), (100, 0), (96, 1)])
-@pytest.mark.parametrize("form", [0, 3, 4, 5])
+@pytest.mark.parametrize("form", [0, 3, 4, 5, 6])
 def test_ivf_mfma_query_tiles(gpu, oracle, nq, d, metric, form):
     """One list probed by every query: items of 1-4 16-query tiles (every wave → work mapping of the
     MFMA scan, incl. the idle wave at 3 tiles and the list merges at 1-2 tiles), several query groups
@@ -255,14 +255,16 @@ def test_ivf_large_nprobe(gpu, oracle, nprobe, k):
         check_topk_parity(xb, xq, D, I, Df, If_)
 
 
+@pytest.mark.parametrize("form", [5, 6])
 @pytest.mark.parametrize("metric", [0, 1])
-def test_ivf_exact_form_distances_are_direct(gpu, oracle, metric):
-    """Form 5 (default): the returned distances are the direct-form fp32 distances of the returned rows
-    (FAISS CPU IVFFlatScanner arithmetic; only the summation order differs), and the ids follow the
+def test_ivf_exact_form_distances_are_direct(gpu, oracle, metric, form):
+    """Forms 5 and 6 (default): the returned distances are the direct-form fp32 distances of the returned
+    rows (FAISS CPU IVFFlatScanner arithmetic; only the summation order differs), and the ids follow the
     oracle's (distance, label) order."""
     xb, xq = faiss_metal_case(20000, 64, 96)
     ix, (cen, off, ids, codes) = _ivf(gpu, xb, 64, 8, metric)
-    assert ix.form == 5  # the library default
+    assert ix.form == 6  # the library default
+    ix.form = form
     D, I = ix.search(xq, 10)
     Do, Io, Po = oracle.ivf_search(cen, off, ids, codes, xq, 10, 8, metric)
     check_topk_parity(xb, xq, D, I, Do, Io, metric)
@@ -270,13 +272,15 @@ def test_ivf_exact_form_distances_are_direct(gpu, oracle, metric):
     assert np.allclose(D[valid], Do[valid], rtol=2e-6, atol=1e-6)
 
 
-def test_ivf_exact_form_fallback_on_ties(gpu, oracle):
+@pytest.mark.parametrize("form", [5, 6])
+def test_ivf_exact_form_fallback_on_ties(gpu, oracle, form):
     """Every vector stored 24 times: the 16 rerank candidates tie, the bound check cannot prove the top-k,
     and the flagged queries are re-run on the 3-term path — results still follow the oracle's (distance,
     label) order."""
     base, xq = faiss_metal_case(600, 40, 64)
     xb = np.ascontiguousarray(np.repeat(base, 24, axis=0))
     ix, (cen, off, ids, codes) = _ivf(gpu, xb, 16, 4, 0)
+    ix.form = form
     before = ix.rerank_fallbacks()
     D, I = ix.search(xq, 10)
     assert ix.rerank_fallbacks() > before
@@ -365,3 +369,35 @@ def test_ivf_label_int32_max_survives_multi_shard_merge(gpu, oracle):
     Do, Io, _ = oracle.ivf_search(cen, off, labels, codes, q, 5, 10)
     assert I[0, 0] == 2**31 - 1
     assert np.array_equal(I, Io)
+
+
+@pytest.mark.parametrize("scale,metric", [(1e6, 0), (1e-6, 0), (2.0 ** -112, 1), (2.0 ** 40, 1)])
+def test_ivf_half_form_scaled_data(gpu, oracle, scale, metric):
+    """Form 6 scales the rows by a power of two into fp16's range (x·2^(14-e)), so the fp16 image keeps
+    its relative precision at any magnitude; codes whose scale leaves 2^±100 take form 5 instead.  Either
+    way the results follow the oracle on the same (scaled) data."""
+    xb, xq = faiss_metal_case(6000, 24, 64)
+    xb = np.ascontiguousarray((xb.astype(np.float64) * scale).astype(np.float32))
+    xq = np.ascontiguousarray((xq.astype(np.float64) * (scale if metric == 0 else 1.0)).astype(np.float32))
+    ix, (cen, off, ids, codes) = _ivf(gpu, xb, 24, 6, metric)
+    assert ix.form == 6
+    D, I = ix.search(xq, 10)
+    Do, Io, Po = oracle.ivf_search(cen, off, ids, codes, xq, 10, 6, metric)
+    assert np.array_equal(ix.last_probes(len(xq)), Po)
+    check_topk_parity(xb, xq, D, I, Do, Io, metric)
+    v = I >= 0
+    assert np.allclose(D[v], Do[v], rtol=2e-6, atol=0)
+
+
+def test_ivf_half_form_query_out_of_range(gpu, oracle):
+    """A query whose own scale leaves the fp16 form's safe range (here |q| ~ 2^110, IP) gets a non-finite
+    bound: the rerank flags it and it is re-run on the 3-term path; the other queries are unaffected."""
+    xb, xq = faiss_metal_case(6000, 24, 64)
+    xq = xq.copy()
+    xq[3] *= np.float32(2.0 ** 110)
+    ix, (cen, off, ids, codes) = _ivf(gpu, xb, 24, 6, 1)
+    before = ix.rerank_fallbacks()
+    D, I = ix.search(xq, 10)
+    assert ix.rerank_fallbacks() - before >= 1
+    Do, Io, Po = oracle.ivf_search(cen, off, ids, codes, xq, 10, 6, 1)
+    check_topk_parity(xb, xq, D, I, Do, Io, 1)
