@@ -19,7 +19,8 @@ sub-object of ``configs`` (each with its own roofline and CPU baseline): C1 (Fla
 path), C2 (Flat L2 1M x 768), Flat L2 10M x 768, C4 (DiskANN), the extension's real call shape
 (nq = 1 / 4 latency, Flat and IVF), the reference's published batch-distance microbenchmark shapes
 (README.md:140-147) with the MIN_GPU_WORK break-even, and the IVF recall/nprobe sweep at intrinsic
-ranks 16/24/32.  --no-suite skips them.
+ranks 16/24/32.  --no-suite skips them.  At every N the IVF line also carries C5 (Flat IP, 12.5M rows
+per GPU, sharded: exactly C5's 100M x 768 at N = 8); --no-c5 skips it.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]  (N>1 under torch.distributed.run).
 """
@@ -72,6 +73,7 @@ def parse():
     p.add_argument("--suite", dest="suite", action="store_true", default=None,
                    help="N=1: add the other BASELINE configurations as sub-objects (default for --workload ivf)")
     p.add_argument("--no-suite", dest="suite", action="store_false")
+    p.add_argument("--no-c5", action="store_true", help="skip the C5 sub-line (Flat IP, 12.5M rows per GPU)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU sample duration (main line)")
     a = p.parse_args()
     if a.n is None:
@@ -852,26 +854,38 @@ def batch_distance_microbench(hipann):
         for _ in range(it):
             lib.oracle_batch_distances(fp(q), fp(c), n, d, 0, fp(ref))
         cpu = (time.perf_counter() - t0) / it * 1e6
-        return g, cpu
+        lib.oracle_batch_distances_simd(fp(q), fp(c), n, d, 0, fp(ref))
+        t0 = time.perf_counter()
+        for _ in range(it):
+            lib.oracle_batch_distances_simd(fp(q), fp(c), n, d, 0, fp(ref))
+        simd = (time.perf_counter() - t0) / it * 1e6
+        return g, cpu, simd
 
     rows = []
     for n, d, m1_cpu, metal in README_SHAPES:
-        g, cpu = time_pair(n, d, 200)
+        g, cpu, simd = time_pair(n, d, 200)
         rows.append({"n": n, "d": d, "gpu_us": round(g, 1), "cpu_us": round(cpu, 1), "speedup": round(cpu / g, 3),
+                     "cpu_simd_us": round(simd, 1),
                      "reference_m1pro_cpu_us": m1_cpu, "reference_metal_us": metal,
                      "reference_speedup": round(m1_cpu / metal, 2)})
     sweep = []
-    even = None
-    for nd_log in range(12, 22):
+    even = even_simd = None
+    for nd_log in range(12, 23):
         nd = 1 << nd_log
         d = 768
         n = max(1, nd // d)
-        g, cpu = time_pair(n, d, 100)
-        sweep.append({"n_times_d": n * d, "gpu_us": round(g, 1), "cpu_us": round(cpu, 1)})
+        g, cpu, simd = time_pair(n, d, 100)
+        sweep.append({"n_times_d": n * d, "gpu_us": round(g, 1), "cpu_us": round(cpu, 1), "cpu_simd_us": round(simd, 1)})
         if even is None and g < cpu:
             even = n * d
+        if even_simd is None and g < simd:
+            even_simd = n * d
     return {"shapes": rows, "break_even_sweep_d768": sweep, "break_even_n_times_d": even,
-            "cpu": "oracle_batch_distances (ComputeDistancesCPU restatement, sequential fp32 sum, 1 thread)",
+            "break_even_n_times_d_simd_cpu": even_simd,
+            "gates_from": "MIN_GPU_WORK_ONESHOT (ann_search.cpp:696-699, scalar ComputeDistancesCPU) <- break_even_n_times_d; "
+                          "MIN_GPU_WORK (metal_ffi.rs:41, Rust SIMD distances) <- break_even_n_times_d_simd_cpu",
+            "cpu": "oracle_batch_distances (ComputeDistancesCPU restatement, sequential fp32 sum, 1 thread); "
+                   "cpu_simd: 16-accumulator AVX2 loop (timing model of diskann-vector's SIMD kernel, 1 thread)",
             "gpu": "diskann_hip_batch_distances (host pointers: candidates H2D + kernel + D2H, synchronous)",
             "current_gates": {"MIN_GPU_WORK": hipann.MIN_GPU_WORK, "MIN_GPU_WORK_ONESHOT": hipann.MIN_GPU_WORK_ONESHOT}}
 
@@ -905,6 +919,33 @@ def run_suite(args, torch, dist, hipann, dev):
     guarded("reference_readme_batch_distances", lambda: batch_distance_microbench(hipann))
     guarded("ivf_recall_vs_nprobe", lambda: ivf_robustness(args, torch, dist, hipann, dev))
     return cfg
+
+
+C5_ROWS_PER_GPU = 12_500_000  # BASELINE configs[4]: 100M x 768 over 8 GPUs
+
+
+def c5_config(args, torch, dist, hipann, rank, world, dev):
+    """BASELINE configs[4]: Flat IP over 100M x 768 fp32 sharded across 8 GPUs — per-GPU
+    partial top-k over a contiguous 12.5M-row shard (labels offset to global rows), one packed RCCL
+    all-gather + merge on every rank.  Each rank holds 12.5M rows whatever N is, so N = 8 is exactly C5
+    (100M rows) and N < 8 runs the same per-GPU shard over 12.5M·N rows (weak scaling)."""
+    n = C5_ROWS_PER_GPU * world
+    steps = max(3, min(args.steps, 10))
+    out, index, xb = flat_config(args, torch, dist, hipann, rank, world, dev, n, 768, 1024, args.k, 1, steps, 2,
+                                 alt_forms=world == 1 and not args.no_alt_forms, host_rate=False)
+    index.close()
+    del index, xb
+    torch.cuda.empty_cache()
+    out["scaling"] = "weak"
+    out["rows_per_gpu"] = C5_ROWS_PER_GPU
+    out["note"] = (f"{world} GPU(s) x 12.5M rows = {n / 1e6:g}M rows; at 8 GPUs this is C5's 100M x 768 "
+                   "(per-GPU shard, one packed all-gather of nq x k (dist, label) per rank over RCCL, merge on "
+                   "every rank)")
+    if world == 1 and not args.no_cpu_baseline:
+        xq = uniform_queries(torch, 1024, 768, dev)
+        out["cpu_baseline"] = flat_cpu_baseline(torch, xq, 100_000_000, 768, args.k, 1, 5.0)
+        out["cpu_baseline"]["note"] = "the whole 100M-row job on this host's cores (SURVEY §8d C5: a slice, extrapolated)"
+    return out
 
 
 # ------------------------------------------------------------------------------------------------
@@ -969,11 +1010,20 @@ def main():
                                  "arithmetic); the bf16 2-term split scan only prunes, and a per-query bound "
                                  "(|scan key − exact| ≤ 2^-12·(|q|²+max|x|²)) proves no pruned row reaches the top-k "
                                  "(failures re-run on the 3-term path)")
-        if args.suite and world == 1:
+        if (args.suite and world == 1) or not args.no_c5:
             index.close()
             del index
             torch.cuda.empty_cache()
+        if args.suite and world == 1:
             line["configs"] = run_suite(args, torch, dist, hipann, dev)
+        if not args.no_c5 and args.workload == "ivf":
+            t0 = time.perf_counter()
+            try:
+                c5 = c5_config(args, torch, dist, hipann, rank, world, dev)
+            except Exception as e:  # report, never lose the main line
+                c5 = {"error": repr(e)}
+            c5["wall_s"] = round(time.perf_counter() - t0, 1)
+            line.setdefault("configs", {})["C5_flat_ip_100m_768_sharded"] = c5
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

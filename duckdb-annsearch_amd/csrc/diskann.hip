@@ -34,8 +34,9 @@
 namespace hipann {
 
 bool diskann_bfs_supported(int d, int fmt, int R, int n_ep, int L, uint32_t N);
+void launch_diskann_dup_rows(const uint32_t *adj, int R, int64_t n, uint32_t *dupw, hipStream_t st);
 void launch_diskann_bfs(const float *Q, int nq, int d, int fmt, const void *data, const float2 *ab,
-                        const uint32_t *adj, int R, uint32_t N, const uint32_t *eps, int n_ep, int k, int L,
+                        const uint32_t *adj, const uint32_t *dupw, int R, uint32_t N, const uint32_t *eps, int n_ep, int k, int L,
                         int metric, uint32_t *visited, int64_t vwords, int64_t *out_ids, float *out_d, int *flags,
                         unsigned long long *stats, hipStream_t st);
 
@@ -220,6 +221,8 @@ struct ThreadCtx {
 };
 
 thread_local ThreadCtx t_ctx;
+// host-pointer calls with at most this many candidate bytes run zero-copy from pinned staging
+constexpr size_t kZeroCopyMax = (size_t)1 << 20;
 
 void launch_rows(const float *q, const float *c, const unsigned *m, int total_n, int d, int metric, float *out,
                  hipStream_t st) {
@@ -249,7 +252,7 @@ struct DiskDB {
     KernelTimer timer;
     // resident graph + BFS scratch (diskann_hip_register_graph / _search_batch_resident)
     int R = 0;
-    DevBuf adj_dev, visited, flags, bstats, eps_dev;
+    DevBuf adj_dev, dupw, visited, flags, bstats, eps_dev;
     std::vector<uint32_t> adj_host;
     ~DiskDB() {
         if (stream) { DeviceGuard g(device); (void)hipStreamDestroy(stream); }
@@ -644,6 +647,25 @@ int diskann_hip_batch_distances(const float *query, const float *candidates, int
         ThreadCtx &t = t_ctx;
         t.init();
         const size_t qb = (size_t)dim * 4, cb = (size_t)n * dim * 4, ob = (size_t)n * 4;
+        if (cb <= kZeroCopyMax) {
+            // small calls (the per-step shapes of metal_ffi.rs): stage into this thread's pinned buffers
+            // and let the kernel read / write them over PCIe — no DMA round trips (the reference's
+            // zero-copy wrap of page-aligned buffers, metal_diskann_bridge.mm:182-222)
+            t.hq.ensure(qb);
+            t.hc.ensure(cb);
+            t.hout.ensure(ob);
+            std::memcpy(t.hq.p, query, qb);
+            std::memcpy(t.hc.p, candidates, cb);
+            void *dq = nullptr, *dc = nullptr, *dout = nullptr;
+            HIPANN_CHECK(hipHostGetDevicePointer(&dq, t.hq.p, 0));
+            HIPANN_CHECK(hipHostGetDevicePointer(&dc, t.hc.p, 0));
+            HIPANN_CHECK(hipHostGetDevicePointer(&dout, t.hout.p, 0));
+            launch_rows(static_cast<const float *>(dq), static_cast<const float *>(dc), nullptr, n, dim, metric,
+                        static_cast<float *>(dout), t.stream);
+            HIPANN_CHECK(hipStreamSynchronize(t.stream));
+            std::memcpy(out_distances, t.hout.p, ob);
+            return 0;
+        }
         t.q.ensure(qb, t.device);
         t.c.ensure(cb, t.device);
         t.out.ensure(ob, t.device);
@@ -844,6 +866,13 @@ int diskann_hip_register_graph(void *h, const uint32_t *adj, int R) {
         db->adj_host.assign(adj, adj + cnt);
         db->adj_dev.ensure(cnt * 4 + 16, db->device);
         if (cnt) HIPANN_CHECK(hipMemcpyAsync(db->adj_dev.p, adj, cnt * 4, hipMemcpyHostToDevice, db->stream));
+        // rows with a repeated id (the traversal's first-occurrence dedupe runs only on those)
+        if (R <= 64) {  // (wider graphs run on the host BFS)
+            db->dupw.ensure((size_t)((db->n + 31) / 32) * 4 + 16, db->device);
+            launch_diskann_dup_rows(db->adj_dev.get<uint32_t>(), R, db->n, db->dupw.get<uint32_t>(), db->stream);
+        } else {
+            db->dupw.release();
+        }
         HIPANN_CHECK(hipStreamSynchronize(db->stream));
         db->R = R;
         return 0;
@@ -890,7 +919,7 @@ int diskann_hip_search_batch_resident_device(void *h, const uint32_t *eps, int n
                 HIPANN_CHECK(hipMemsetAsync(db->visited.p, 0, (size_t)qn * vwords * 4, st));
                 ScopedTiming tm(db->timer, st);
                 launch_diskann_bfs(queries_dev + q0 * db->dim, (int)qn, db->dim, db->fmt, db->data.p,
-                                   db->ab.get<float2>(), db->adj_dev.get<uint32_t>(), db->R, N,
+                                   db->ab.get<float2>(), db->adj_dev.get<uint32_t>(), db->dupw.get<uint32_t>(), db->R, N,
                                    db->eps_dev.get<uint32_t>(), n_ep, kk, L, metric, db->visited.get<uint32_t>(),
                                    vwords, out_ids_dev + q0 * kk, out_d_dev + q0 * kk, db->flags.get<int>() + q0,
                                    db->bstats.get<unsigned long long>(), st);

@@ -31,6 +31,7 @@
 
 #include <cfloat>
 #include <cstdint>
+#include <type_traits>
 
 namespace hipann {
 namespace {
@@ -92,10 +93,13 @@ __device__ __forceinline__ unsigned up1_u(unsigned v, int) {
 
 // Row chunks: 8 SQ8 codes (8 B; 1536 codes = 3 chunks per lane exactly) or 4 floats (16 B); lane `l`,
 // chunk t covers chunk index l + 64t.
+#ifndef HIPANN_BFS_SQ8_CHUNK
+#define HIPANN_BFS_SQ8_CHUNK 8  // bytes of SQ8 codes per lane-load (8: global_load_dwordx2, 16: dwordx4)
+#endif
 template <bool SQ8> struct Fmt;
 template <> struct Fmt<true> {
-    static constexpr int kDims = 8;
-    using Chunk = uint2;
+    static constexpr int kDims = HIPANN_BFS_SQ8_CHUNK;
+    using Chunk = typename std::conditional<HIPANN_BFS_SQ8_CHUNK == 16, uint4, uint2>::type;
 };
 template <> struct Fmt<false> {
     static constexpr int kDims = 4;
@@ -224,8 +228,8 @@ __device__ __forceinline__ float reduce_rows(float (&v)[P], int lane) {
 template <int S, int T, int W, bool SQ8, bool IP>
 __global__ void __launch_bounds__(64 * W)
 diskann_bfs(const float *__restrict__ Qs, int nq, int d, const uint8_t *__restrict__ data,
-            const float2 *__restrict__ ab, const uint32_t *__restrict__ adj, int R, uint32_t N,
-            const uint32_t *__restrict__ eps, int n_ep, int k, int L, uint32_t *__restrict__ visited,
+            const float2 *__restrict__ ab, const uint32_t *__restrict__ adj, const uint32_t *__restrict__ dupw,
+            int R, uint32_t N, const uint32_t *__restrict__ eps, int n_ep, int k, int L, uint32_t *__restrict__ visited,
             int64_t vwords, int64_t *__restrict__ out_ids, float *__restrict__ out_d, int *__restrict__ flags,
             unsigned long long *__restrict__ stats) {
     constexpr int DC = Fmt<SQ8>::kDims;
@@ -295,9 +299,10 @@ diskann_bfs(const float *__restrict__ Qs, int nq, int d, const uint8_t *__restri
 #pragma unroll
         for (int t = 0; t < T; ++t) {
             if constexpr (SQ8) {
-                const unsigned w[2] = {v[t].x, v[t].y};
+                unsigned w[4];
+                __builtin_memcpy(w, &v[t], sizeof(Chunk));
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
+                for (int e = 0; e < DC / 2; ++e) {
                     const unsigned ww = w[e >> 1] >> (16 * (e & 1));
                     const f32x2 c = {(float)(ww & 0xffu), (float)((ww >> 8) & 0xffu)};
                     if (IP) acc = __builtin_elementwise_fma(qp[t][e], c, acc);
@@ -471,15 +476,19 @@ diskann_bfs(const float *__restrict__ Qs, int nq, int d, const uint8_t *__restri
         BFS_T(0);
         // expand: neighbours up to the first sentinel, ids < N, visited insert in order
         const uint32_t nb = lane < R ? adj[(size_t)cid * R + lane] : kNone;
+        // rows flagged at registration as holding a repeated id before their first sentinel (none in
+        // a Vamana graph) take the dedupe below; every other row skips it
+        const bool maydup = dupw == nullptr || ((dupw[cid >> 5] >> (cid & 31)) & 1u);
         const uint64_t sent = __ballot(lane < R && nb == kNone);
         BFS_T(1);
         const int first = sent ? __ffsll((unsigned long long)sent) - 1 : R;
         const bool valid = lane < first && nb < N;
+        bool dup = false;
+        if (maydup) {
         // first occurrence wins: compare with every earlier lane's id through LDS broadcast reads
         // (invalid lanes hold 0x80000000 | lane, which no id < N ≤ 2^31 − 1 equals)
         s_nb[lane] = valid ? nb : (0x80000000u | (unsigned)lane);
         __builtin_amdgcn_wave_barrier();
-        bool dup = false;
 #pragma unroll 4
         for (int i = 0; i < 64; i += 4) {  // 4 broadcast reads in flight per iteration (lanes ≥ first hold sentinels)
             const uint4 w = *reinterpret_cast<const uint4 *>(s_nb + i);
@@ -488,6 +497,7 @@ diskann_bfs(const float *__restrict__ Qs, int nq, int d, const uint8_t *__restri
         }
         dup = dup && valid;
         __builtin_amdgcn_wave_barrier();
+        }
         BFS_T(2);
         bool fresh = false;
         if (valid && !dup) {
@@ -576,29 +586,51 @@ diskann_bfs(const float *__restrict__ Qs, int nq, int d, const uint8_t *__restri
     }
 }
 
+// dupw bit r = adjacency row r holds some id twice before its first u32::MAX (one wave per row)
+__global__ void __launch_bounds__(256) diskann_dup_rows(const uint32_t *__restrict__ adj, int R, int64_t n,
+                                                        uint32_t *__restrict__ dupw) {
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= n) return;
+    const uint32_t v = lane < R ? adj[row * R + lane] : kNone;
+    const uint64_t sent = __ballot(lane < R && v == kNone);
+    const int first = sent ? __ffsll((unsigned long long)sent) - 1 : R;
+    bool dup = false;
+    for (int i = 0; i < first; ++i) dup |= lane > i && lane < first && v == rl_u(v, i);
+    if (__ballot(dup) && lane == 0) atomicOr(dupw + (row >> 5), 1u << (row & 31));
+}
+
 }  // namespace
+
+void launch_diskann_dup_rows(const uint32_t *adj, int R, int64_t n, uint32_t *dupw, hipStream_t st) {
+    HIPANN_CHECK(hipMemsetAsync(dupw, 0, (size_t)((n + 31) / 32) * 4, st));
+    if (n <= 0) return;
+    HIPANN_REQUIRE(R > 0 && R <= 64 && (n + 3) / 4 < (int64_t)0x7fffffff, "diskann_dup_rows: bad shape");
+    hipLaunchKernelGGL(diskann_dup_rows, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, adj, R, n, dupw);
+    HIPANN_CHECK(hipGetLastError());
+}
 
 // S: result slots per lane (L ≤ 64·S); T: row chunks per lane (8 codes or 4 floats each)
 bool diskann_bfs_supported(int d, int fmt, int R, int n_ep, int L, uint32_t N) {
-    const int dc = fmt == 1 ? 8 : 4;
+    const int dc = fmt == 1 ? HIPANN_BFS_SQ8_CHUNK : 4;
     return d > 0 && d % dc == 0 && d <= 64 * dc * (fmt == 1 ? 4 : 8) && R > 0 && R <= 64 && n_ep >= 0 &&
            n_ep <= 64 && L >= 1 && L <= 256 && N <= 0x7fffffffu;
 }
 
 void launch_diskann_bfs(const float *Q, int nq, int d, int fmt, const void *data, const float2 *ab,
-                        const uint32_t *adj, int R, uint32_t N, const uint32_t *eps, int n_ep, int k, int L,
+                        const uint32_t *adj, const uint32_t *dupw, int R, uint32_t N, const uint32_t *eps, int n_ep, int k, int L,
                         int metric, uint32_t *visited, int64_t vwords, int64_t *out_ids, float *out_d, int *flags,
                         unsigned long long *stats, hipStream_t st) {
     if (nq <= 0) return;
     HIPANN_REQUIRE(diskann_bfs_supported(d, fmt, R, n_ep, L, N), "diskann_bfs: unsupported shape");
-    const int dc = fmt == 1 ? 8 : 4;
+    const int dc = fmt == 1 ? HIPANN_BFS_SQ8_CHUNK : 4;
     const int chunks = (d / dc + 63) / 64;  // row chunks per lane
     const bool s2 = L <= 128;
     const uint8_t *x = static_cast<const uint8_t *>(data);
     constexpr int W = HIPANN_BFS_W;
     dim3 grid((unsigned)nq), block(64 * W);
 #define HIPANN_BFS(S_, T_, SQ_, IP_)                                                                              \
-    hipLaunchKernelGGL((diskann_bfs<S_, T_, W, SQ_, IP_>), grid, block, 0, st, Q, nq, d, x, ab, adj, R, N, eps, n_ep, \
+    hipLaunchKernelGGL((diskann_bfs<S_, T_, W, SQ_, IP_>), grid, block, 0, st, Q, nq, d, x, ab, adj, dupw, R, N, eps, n_ep, \
                        k, L, visited, vwords, out_ids, out_d, flags, stats)
 #define HIPANN_BFS_S(T_, SQ_, IP_) \
     do { if (s2) HIPANN_BFS(2, T_, SQ_, IP_); else HIPANN_BFS(4, T_, SQ_, IP_); } while (0)

@@ -289,6 +289,27 @@ void oracle_batch_distances(const float *query, const float *cands, int n, int d
     for (int i = 0; i < n; ++i) out[i] = diskann_dist(query, cands + (int64_t)i * d, d, metric);
 }
 
+/* Timing model of the Rust caller's CPU distances (distance.rs:15-24 → diskann-vector 0.45's SIMD
+ * SquaredL2 / InnerProduct, external): 16 independent fp32 accumulators (two 8-wide AVX2 vectors),
+ * summed at the end.  Used only by bench.py to place MIN_GPU_WORK (metal_ffi.rs:36-46) against a
+ * SIMD CPU; its rounding differs from the sequential sum, so no parity test uses it. */
+void oracle_batch_distances_simd(const float *query, const float *cands, int n, int d, int metric, float *out) {
+    for (int i = 0; i < n; ++i) {
+        const float *c = cands + (int64_t)i * d;
+        float acc[16] = {0};
+        int j = 0;
+        for (; j + 16 <= d; j += 16)
+            for (int l = 0; l < 16; ++l) {
+                const float t = metric == 1 ? query[j + l] * c[j + l] : (query[j + l] - c[j + l]) * (query[j + l] - c[j + l]);
+                acc[l] += t;
+            }
+        float s = 0.f;
+        for (int l = 0; l < 16; ++l) s += acc[l];
+        for (; j < d; ++j) s += metric == 1 ? query[j] * c[j] : (query[j] - c[j]) * (query[j] - c[j]);
+        out[i] = metric == 1 ? -s : s;
+    }
+}
+
 void oracle_multi_batch_distances(const float *queries, const float *cands, const uint32_t *qmap, int total_n,
                                   int d, int metric, float *out) {
 #pragma omp parallel for schedule(static)

@@ -38,6 +38,7 @@ def lib():
         _lib.oracle_ivf_search.argtypes = [f, i32, i64, i64, f, i32, f, C.c_int64, i32, i32, i32, f, i64, i64]
         _lib.oracle_exact_dists.argtypes = [f, i32, f, i64, C.c_int64, i32, d64]
         _lib.oracle_batch_distances.argtypes = [f, f, i32, i32, i32, f]
+        _lib.oracle_batch_distances_simd.argtypes = [f, f, i32, i32, i32, f]
         _lib.oracle_multi_batch_distances.argtypes = [f, f, u32, i32, i32, i32, f]
         _lib.oracle_sq8_train.argtypes = [f, C.c_int64, i32, f, f]
         _lib.oracle_sq8_encode.argtypes = [f, C.c_int64, i32, f, f, u8]

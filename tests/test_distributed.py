@@ -201,14 +201,14 @@ def _worker_gpu(rank, world, port, workload, result_path):
 
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
-    n, d, nq, k = 60_000, 96, 200, 10
+    n, d, nq, k, metric = GPU_SHAPES[workload]
     stream = torch.cuda.current_stream().cuda_stream
     xq = bench.uniform_queries(torch, nq, d, dev)
-    if workload == "flat":
+    if workload.startswith("flat"):
         lo, hi = shard_bounds(n, rank, world)
         xb = torch.empty((hi - lo, d), device=dev)
         bench.gen_uniform_rows(torch, xb, lo, 42)
-        index = hipann.HipIndexFlatDevice(d, 0, xb.data_ptr(), hi - lo, 0, copy=False, label_offset=lo)
+        index = hipann.HipIndexFlatDevice(d, metric, xb.data_ptr(), hi - lo, 0, copy=False, label_offset=lo)
         extra = {}
     else:
         from ivf_build import build_ivf_list_shard
@@ -221,7 +221,7 @@ def _worker_gpu(rank, world, port, workload, result_path):
     def local(q, D, I):
         index.search_device(nq, q.data_ptr(), k, D.data_ptr(), I.data_ptr(), stream)
 
-    s = ShardedSearch(local, merge_packed_device_torch(hipann, 0), nq, k, dev)
+    s = ShardedSearch(local, merge_packed_device_torch(hipann, metric), nq, k, dev)
     D, I = s.search(xq)
     torch.cuda.synchronize()
     np.savez(f"{result_path}.{rank}.npz", D=D.cpu().numpy(), I=I.cpu().numpy(), xq=xq.cpu().numpy(), **extra)
@@ -230,13 +230,21 @@ def _worker_gpu(rank, world, port, workload, result_path):
     dist.destroy_process_group()
 
 
+# (rows, d, nq, k, metric); flat_ip_c5: C5's per-GPU path (Flat IP, d = 768, the 1024-query batch) on
+# 2 × 200k rows — the 100M × 768 / 8-GPU configuration's shard search, label offsets, all-gather and merge
+GPU_SHAPES = {"flat": (60_000, 96, 200, 10, 0), "ivf_lists": (60_000, 96, 200, 10, 0),
+              "flat_ip_c5": (400_000, 768, 1024, 10, 1)}
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("workload", ["flat", "ivf_lists"])
+@pytest.mark.parametrize("workload", ["flat", "ivf_lists", "flat_ip_c5"])
 def test_sharded_hip_world2_on_one_device(gpu, oracle, tmp_path, workload):
     """two processes, each running the real HIP shard search (Flat row shards with
     label_offset / list-sharded IVF from build_ivf_list_shard), one packed all-gather, the device merge
     kernel; the merged top-k equals the oracle's over the whole database (IVF: the lists the two ranks
-    own partition the single index's lists, and the probe lists are the replicated coarse step's)."""
+    own partition the single index's lists, and the probe lists are the replicated coarse step's).
+    flat_ip_c5 is C5's path (BASELINE configs[4]) at 400k rows: Flat IP, d 768, nq 1024, checked against
+    the oracle on 128 of the queries."""
     import torch
     import torch.multiprocessing as mp
     import bench
@@ -246,9 +254,15 @@ def test_sharded_hip_world2_on_one_device(gpu, oracle, tmp_path, workload):
     mp.spawn(_worker_gpu, args=(2, _free_port(), workload, res), nprocs=2, join=True)
     r0, r1 = np.load(res + ".0.npz"), np.load(res + ".1.npz")
     assert np.array_equal(r0["I"], r1["I"]) and np.array_equal(r0["D"], r1["D"])  # every rank merges the same
-    n, d = 60_000, 96
+    n, d, nq, k, metric = GPU_SHAPES[workload]
     xb = bench.gen_uniform_rows(torch, torch.empty((n, d), device="cuda"), 0, 42).cpu().numpy()
     xq = r0["xq"]
+    if workload == "flat_ip_c5":
+        sub = slice(0, 128)
+        Do, Io = oracle.flat_search(xb, xq[sub], k, metric)
+        check_topk_parity(xb, xq[sub], r0["D"][sub], r0["I"][sub], Do, Io, metric)
+        assert np.all(np.diff(r0["D"], axis=1) <= 0)  # IP: descending on every query
+        return
     if workload == "flat":
         Do, Io = oracle.flat_search(xb, xq, 10)
     else:
