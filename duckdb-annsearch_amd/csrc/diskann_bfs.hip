@@ -50,6 +50,10 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 constexpr unsigned kNone = 0xffffffffu;
 constexpr unsigned kExpanded = 0x80000000u;
+#ifndef HIPANN_BFS_BULK
+#define HIPANN_BFS_BULK 6  // admitted candidates from which a step merges them at once (65: never)
+#endif
+constexpr int kBulkMin = HIPANN_BFS_BULK;
 
 __device__ __forceinline__ unsigned ford(float f) {
     const unsigned u = __float_as_uint(f);
@@ -241,6 +245,9 @@ diskann_bfs(const float *__restrict__ Qs, int nq, int d, const uint8_t *__restri
     __shared__ float s_dist[64];    // their distances
     __shared__ int s_cnt;           // how many; −1 = the query is done
     __shared__ __attribute__((aligned(16))) uint32_t s_nb[64];  // wave 0: the expansion's neighbour ids
+    // wave 0, bulk insert: the result list, the sorted admitted candidates, the merged list
+    __shared__ float s_ld[64 * S], s_md[64 * S], s_cd[64];
+    __shared__ uint32_t s_mi[64 * S];
     const int qi = blockIdx.x;
     if (qi >= nq) return;
     const int lane = threadIdx.x & 63;
@@ -355,6 +362,71 @@ diskann_bfs(const float *__restrict__ Qs, int nq, int d, const uint8_t *__restri
 #pragma unroll
     for (int s = 0; s < S; ++s) { res.d[s] = __builtin_inff(); res.id[s] = kNone; }
     int len = 0;
+
+    // Bulk insert (wave 0): returns false, with the list untouched, when any admitted distance is
+    // non-finite or equals another admitted or listed distance, or two listed distances are equal —
+    // the sequential Rust-order inserts then run as before.
+    auto bulk_insert = [&](uint64_t am, float dd, unsigned nbr) -> bool {
+        const bool adm = (am >> lane) & 1ull;
+        const int nA = __popcll(am);
+        if (__ballot(adm && !(__builtin_fabsf(dd) < __builtin_inff()))) return false;
+        // admitted candidates sorted ascending (ties only among the non-admitted +inf keys)
+        float key = adm ? dd : __builtin_inff();
+        int src = lane;
+#pragma unroll
+        for (int size = 2; size <= 64; size <<= 1)
+#pragma unroll
+            for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                const float ok2 = __shfl_xor(key, stride);
+                const int os = __shfl_xor(src, stride);
+                const bool keep_min = ((lane & stride) == 0) == ((lane & size) == 0);
+                const bool o_less = ok2 < key || (ok2 == key && os < src);
+                if (keep_min == o_less) { key = ok2; src = os; }
+            }
+        const unsigned cid = (unsigned)__shfl((int)nbr, src);
+        __builtin_amdgcn_wave_barrier();
+        s_cd[lane] = key;
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+            if (s * 64 + lane < len) s_ld[s * 64 + lane] = res.d[s];
+        __builtin_amdgcn_wave_barrier();
+        bool bad = lane + 1 < nA && s_cd[lane + 1] == key;  // equal admitted distances
+        // list elements: new position e + #(candidates < d_e); a candidate equal to d_e is a tie
+        int np_l[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const int e = s * 64 + lane;
+            const float de = res.d[s];
+            int c = 0;
+#pragma unroll
+            for (int b = 64; b > 0; b >>= 1)
+                if (c + b <= nA && s_cd[c + b - 1] < de) c += b;
+            np_l[s] = e + c;
+            if (e < len) bad |= (c < nA && s_cd[c] == de) || !(de == de) || (e + 1 < len && s_ld[e + 1] == de);
+        }
+        // candidates: new position i + #(list elements < key)
+        int cl = 0;
+#pragma unroll
+        for (int b = 128 * (S > 2 ? 2 : 1); b > 0; b >>= 1)
+            if (cl + b <= len && s_ld[cl + b - 1] < key) cl += b;
+        const int np_c = lane + cl;
+        if (__ballot(bad)) return false;
+        const int nlen = len + nA < L ? len + nA : L;
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+            if (s * 64 + lane < len && np_l[s] < nlen) { s_md[np_l[s]] = res.d[s]; s_mi[np_l[s]] = res.id[s]; }
+        if (lane < nA && np_c < nlen) { s_md[np_c] = key; s_mi[np_c] = cid; }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const int e = s * 64 + lane;
+            res.d[s] = e < nlen ? s_md[e] : __builtin_inff();
+            res.id[s] = e < nlen ? s_mi[e] : kNone;
+        }
+        len = nlen;
+        return true;
+    };
     uint64_t spill = ~0ull;  // lane < nspill: a heap entry evicted from result on a boundary tie
     int nspill = 0;
     int flag = 0;
@@ -529,6 +601,11 @@ diskann_bfs(const float *__restrict__ Qs, int nq, int d, const uint8_t *__restri
         const bool full = len >= L;
         const float thr0 = full ? res.get_d(len - 1) : 0.f;
         uint64_t am = __ballot(lane < cnt && (!full || dd < thr0));
+        // Many admitted candidates and no equal / non-finite distance anywhere: the inserts in neighbour
+        // order end in exactly the first L of the sorted union (each binary search lands on the unique
+        // insertion point; a candidate rejected at its turn already had L smaller entries ahead of it;
+        // with no equal values no eviction is a boundary tie, so nothing spills) — one merge instead.
+        if (__popcll(am) >= kBulkMin && bulk_insert(am, dd, nbr)) am = 0;
         while (am) {
             const int j = __ffsll((unsigned long long)am) - 1;
             am &= am - 1;
