@@ -116,6 +116,17 @@ constexpr int rows_in_flight(int vg) {
     while (p < 32 && 2 * p * vg <= HIPANN_BFS_RV) p *= 2;
     return p;
 }
+// Groups of pg rows in flight at once: HIPANN_BFS_RVG VGPRs of row data (0: one group).  At
+// 1M × 1536 SQ8 a step has ≈46 fresh neighbours, 23 per wave: 3 groups of 8 (144 VGPRs) load them in
+// one round where one group of 16 needed two.
+#ifndef HIPANN_BFS_RVG
+#define HIPANN_BFS_RVG 0
+#endif
+constexpr int groups_in_flight(int vg, int pg) {
+    int g = 1;
+    while ((g + 1) * pg * vg <= HIPANN_BFS_RVG) ++g;
+    return g;
+}
 
 template <int S>
 struct ResultList {
@@ -239,8 +250,11 @@ diskann_bfs(const float *__restrict__ Qs, int nq, int d, const uint8_t *__restri
     constexpr int DC = Fmt<SQ8>::kDims;
     using Chunk = typename Fmt<SQ8>::Chunk;
     constexpr int CB = (int)sizeof(Chunk);
-    constexpr int P = rows_in_flight(T * CB / 4);  // rows in flight per wave
-    constexpr int LP = P >= 32 ? 5 : P >= 16 ? 4 : P >= 8 ? 3 : P >= 4 ? 2 : P >= 2 ? 1 : 0;
+    // rows in flight per wave: P = NG groups of PG (a power of two, one reduce-scatter per group)
+    constexpr int PG = rows_in_flight(T * CB / 4);
+    constexpr int NG = groups_in_flight(T * CB / 4, PG);
+    constexpr int P = PG * NG;
+    constexpr int LP = PG >= 32 ? 5 : PG >= 16 ? 4 : PG >= 8 ? 3 : PG >= 4 ? 2 : PG >= 2 ? 1 : 0;
     __shared__ uint32_t s_ids[64];  // this step's fresh neighbours, in neighbour order
     __shared__ float s_dist[64];    // their distances
     __shared__ int s_cnt;           // how many; −1 = the query is done
@@ -349,12 +363,16 @@ diskann_bfs(const float *__restrict__ Qs, int nq, int d, const uint8_t *__restri
                 const int r = r0 + p < r_end ? r0 + p : r_end - 1;
                 load_row((uint32_t)__builtin_amdgcn_readfirstlane((int)s_ids[r]), v[p]);
             }
-            float part[P];
 #pragma unroll
-            for (int p = 0; p < P; ++p) part[p] = row_part(v[p]);
-            const float tot = reduce_rows<P>(part, lane);
-            const int r = r0 + (lane >> (6 - LP));
-            if ((lane & ((64 >> LP) - 1)) == 0 && r < r_end) s_dist[r] = IP ? -(tot + cq) : tot;
+            for (int g = 0; g < NG; ++g) {
+                if (NG > 1 && r0 + g * PG >= r_end) break;  // wave-uniform
+                float part[PG];
+#pragma unroll
+                for (int p = 0; p < PG; ++p) part[p] = row_part(v[g * PG + p]);
+                const float tot = reduce_rows<PG>(part, lane);
+                const int r = r0 + g * PG + (lane >> (6 - LP));
+                if ((lane & ((64 >> LP) - 1)) == 0 && r < r_end) s_dist[r] = IP ? -(tot + cq) : tot;
+            }
         }
     };
 
