@@ -64,14 +64,16 @@ extern "C" {
 /// Cached availability: -1 = unchecked, 0 = unavailable, 1 = available (metal_ffi.rs:33-34).
 static HIP_STATUS: AtomicI32 = AtomicI32::new(-1);
 
-/// Minimum n*dim to dispatch the reference-ABI (host candidate copy) path.  On MI355X the launch +
-/// PCIe round trip is ~15-30 us (vs ~100-200 us Metal dispatch, metal_ffi.rs:36-38), so the
-/// break-even is lower than the Metal value; kept at the reference value until DESIGN.md's
-/// measured break-even replaces it.
-pub const MIN_GPU_WORK: usize = 131072;
+/// Minimum n*dim to dispatch the reference-ABI (host candidate copy) path, measured on MI355X
+/// (bench.py `reference_readme_batch_distances`, d = 768 sweep, profiles/r02/): the host-pointer call
+/// costs ~21 us + ~0.15 us per 1000 floats (zero-copy from pinned staging up to 1 MiB), against a
+/// 16-accumulator AVX2 CPU loop (the timing model of diskann-vector's SIMD distances this caller
+/// falls back to) — break-even between n*d = 524K (GPU 103 us, CPU 90) and 1.05M (151 vs 176).
+pub const MIN_GPU_WORK: usize = 786432;
 
-/// One-shot threshold for vector_distances() (ann_search.cpp:699).
-pub const MIN_GPU_WORK_ONESHOT: usize = 49152;
+/// One-shot threshold for vector_distances() (ann_search.cpp:699): its CPU side is the scalar
+/// ComputeDistancesCPU loop, break-even measured at n*d = 65K (GPU 26.7 us, CPU 28.5).
+pub const MIN_GPU_WORK_ONESHOT: usize = 65536;
 
 /// Reference names (metal_ffi.rs:49, :67, :107): with `#[path = "hip_ffi.rs"] pub mod metal_ffi;` the
 /// callers in disk_provider.rs / provider.rs resolve unchanged.

@@ -33,10 +33,11 @@ METRIC_L2 = 0
 METRIC_INNER_PRODUCT = 1
 MAX_K = 2048
 
-# rust_lib/src/metal_ffi.rs:41, :46 — gates for the DiskANN bridge (the reference's Metal values until the
-# MI355X break-even measured by tools/bench_batch_distances.py replaces them).
-MIN_GPU_WORK = 131072
-MIN_GPU_WORK_ONESHOT = 49152
+# rust_lib/src/metal_ffi.rs:41, :46 — gates for the DiskANN bridge, from the MI355X break-even measured by
+# bench.py (reference_readme_batch_distances, profiles/r02/): against the SIMD CPU distances of the Rust
+# caller (n*d ~0.7M) and against the scalar ComputeDistancesCPU of vector_distances (n*d ~65K).
+MIN_GPU_WORK = 786432
+MIN_GPU_WORK_ONESHOT = 65536
 
 
 class HipAnnError(RuntimeError):

@@ -88,7 +88,7 @@ def test_argument_validation_precedes_device(hipann_mod):
 
 def test_min_gpu_work_gate(hipann_mod):
     """metal_ffi.rs:78 — the single-query wrapper declines work below MIN_GPU_WORK (CPU computes it)."""
-    n, d = 64, 128  # 8192 < 131072
+    n, d = 64, 128  # 8192 < MIN_GPU_WORK (786432)
     assert not hipann_mod.hip_batch_distances(np.zeros(d, np.float32), np.zeros((n, d), np.float32), n, d, 0,
                                               np.zeros(n, np.float32))
 

@@ -79,9 +79,10 @@ def test_wrappers_gate_and_succeed(gpu, oracle):
     q = rng.uniform(-1, 1, d).astype(np.float32)
     small = rng.uniform(-1, 1, (8, d)).astype(np.float32)   # 12288 < MIN_GPU_WORK → declined
     assert not gpu.hip_batch_distances(q, small, 8, d, 0, np.empty(8, np.float32))
-    big = rng.uniform(-1, 1, (128, d)).astype(np.float32)   # 196608 ≥ MIN_GPU_WORK
-    out = np.empty(128, np.float32)
-    assert gpu.hip_batch_distances(q, big, 128, d, 0, out)
+    assert gpu.MIN_GPU_WORK == 786432
+    big = rng.uniform(-1, 1, (600, d)).astype(np.float32)   # 921600 ≥ MIN_GPU_WORK (DMA path: > 1 MiB)
+    out = np.empty(600, np.float32)
+    assert gpu.hip_batch_distances(q, big, 600, d, 0, out)
     assert close(out, oracle.batch_distances(q, big, 0), q[None], big, 0)
 
 
