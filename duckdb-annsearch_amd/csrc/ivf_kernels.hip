@@ -1002,17 +1002,21 @@ namespace hipann {
 // plus the fp32 accumulation of d exact products (≤ d·2⁻²⁴·‖q̂‖‖x̂‖), doubled for L2, plus the fp32
 // rounding of the key and of the reranked direct distance (≤ (d + 8)·2⁻²⁴·2(‖q‖² + max‖x‖²)), all ×1.01.
 // ---------------------------------------------------------------------------------------------
-template <bool IP>
-__global__ void __launch_bounds__(256)
+// WV = 1: one wave per query, four queries per block (large batches).  WV > 1 (small batches, the
+// extension's nq = 1 call): one block of WV waves per query — the waves merge disjoint parts of the
+// partial lists and compute a share of the candidates' distances, wave 0 finishes.
+template <bool IP, int WV>
+__global__ void __launch_bounds__(WV == 1 ? 256 : 64 * WV)
 ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const int *__restrict__ slot_off,
                 int nprobe, int64_t nq, int k, int kout, const float *__restrict__ Q,
                 const float *__restrict__ codes, int d, const int64_t *__restrict__ ids, int64_t nrows,
                 int64_t label_offset, float xmax2, float *__restrict__ D, int64_t *__restrict__ I,
                 int *__restrict__ nflag, int *__restrict__ flagged, float eps, float rxmax,
                 const float *__restrict__ qres) {
-    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t q = WV == 1 ? (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6) : (int64_t)blockIdx.x;
     if (q >= nq) return;
     const int lane = threadIdx.x & 63;
+    const int wv = WV == 1 ? 0 : (int)(threadIdx.x >> 6);
     // 1. the kRerankK best (scan key, row) of the query's partial lists
     WaveList<1, int> L;
     L.init();
@@ -1021,7 +1025,7 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
     const int64_t s0 = slot_off ? slot_off[q * nprobe] : q * nprobe;
     const int64_t s1 = slot_off ? slot_off[(q + 1) * nprobe] : (q + 1) * nprobe;
     const int64_t total = (s1 - s0) * k;
-    for (int64_t c0 = 0; c0 < total; c0 += 64) {
+    for (int64_t c0 = (int64_t)wv * 64; c0 < total; c0 += 64 * WV) {
         const int64_t c = c0 + lane;
         float key = __builtin_inff();
         int row = IdTraits<int>::pad();
@@ -1036,12 +1040,68 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
         }
         L.offer(key, row, k - 1);
     }
-    const int myrow = L.id[0];
-    const bool real = lane < k && myrow != IdTraits<int>::pad();
-    const int ncand = __popcll(__ballot(real));
-    const float k16 = readlane_f(L.d[0], k - 1);  // K_k: the k-th merged scan key
-    // 2. exact direct-form distances of the candidates (4 rows in flight, wave reduction per row)
     const float *qp = Q + q * (int64_t)d;
+    float mine = __builtin_inff();
+    int myrow, ncand;
+    float k16;
+    if constexpr (WV > 1) {
+        __shared__ float sd[WV * 64], sdist[64];
+        __shared__ int si[WV * 64], srow[64];
+        sd[wv * 64 + lane] = lane < k ? L.d[0] : __builtin_inff();
+        si[wv * 64 + lane] = lane < k ? L.id[0] : IdTraits<int>::pad();
+        __syncthreads();
+        if (wv == 0) {
+            L.init();
+#pragma unroll
+            for (int w = 0; w < WV; ++w) L.offer(sd[w * 64 + lane], si[w * 64 + lane], k - 1);
+            srow[lane] = lane < k ? L.id[0] : IdTraits<int>::pad();
+        }
+        __syncthreads();
+        // every wave: its share of the candidates' direct-form distances (4 rows in flight)
+        for (int r0 = wv * 4; r0 < k; r0 += 4 * WV) {
+            float acc[4] = {0.f, 0.f, 0.f, 0.f};
+            const float *xr[4];
+            bool ok[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int r = r0 + u < k ? r0 + u : k - 1;
+                const int row = srow[r];
+                ok[u] = r0 + u < k && row != IdTraits<int>::pad();
+                xr[u] = codes + (int64_t)(ok[u] ? row : 0) * d;
+            }
+            for (int e = lane; e < d; e += 64) {
+                const float qv = qp[e];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const float xv = xr[u][e];
+                    if (IP) acc[u] = fmaf(qv, xv, acc[u]);
+                    else {
+                        const float t = qv - xv;
+                        acc[u] = fmaf(t, t, acc[u]);
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                float a = acc[u];
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+                if (lane == 0 && ok[u]) sdist[r0 + u] = IP ? -a : a;
+            }
+        }
+        __syncthreads();
+        if (wv != 0) return;
+        myrow = L.id[0];
+        ncand = __popcll(__ballot(lane < k && myrow != IdTraits<int>::pad()));
+        k16 = readlane_f(L.d[0], k - 1);
+        if (lane < ncand) mine = sdist[lane];
+    } else {
+        myrow = L.id[0];
+        ncand = __popcll(__ballot(lane < k && myrow != IdTraits<int>::pad()));
+        k16 = readlane_f(L.d[0], k - 1);  // K_k: the k-th merged scan key
+    }
+    const bool real = lane < k && myrow != IdTraits<int>::pad();
+    // 2. exact direct-form distances of the candidates (4 rows in flight, wave reduction per row)
     float qq = 0.f, rq2 = 0.f;
     for (int e = lane; e < d; e += 64) {
         qq = fmaf(qp[e], qp[e], qq);
@@ -1053,7 +1113,7 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
         qq += __shfl_xor(qq, o);
         rq2 += __shfl_xor(rq2, o);
     }
-    float mine = __builtin_inff();
+    if constexpr (WV == 1) {
     for (int r0 = 0; r0 < ncand; r0 += 4) {
         float acc[4] = {0.f, 0.f, 0.f, 0.f};
         const float *xr[4];
@@ -1081,6 +1141,7 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
             for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
             if (lane == r0 + u) mine = IP ? -a : a;
         }
+    }
     }
     // 3. (distance, label) order, first kout
     WaveList<1, long long> R;
@@ -1142,13 +1203,19 @@ void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int 
                        hipStream_t st, float eps, float rxmax, const float *qres) {
     if (nq <= 0) return;
     HIPANN_REQUIRE(k >= kRerankK && k <= 64 && kout >= 1 && kout <= kRerankMaxK, "ivf rerank: k / kout out of range");
-    dim3 grid((unsigned)ceil_div(nq, 4)), block(256);
-    if (metric == kIP)
-        hipLaunchKernelGGL(ivf_rerank_topk<true>, grid, block, 0, st, pd, pi, slot_off, nprobe, nq, k, kout, Q, codes, d,
-                           ids, nrows, label_offset, xmax2, D, I, nflag, flagged, eps, rxmax, qres);
-    else
-        hipLaunchKernelGGL(ivf_rerank_topk<false>, grid, block, 0, st, pd, pi, slot_off, nprobe, nq, k, kout, Q, codes,
-                           d, ids, nrows, label_offset, xmax2, D, I, nflag, flagged, eps, rxmax, qres);
+    // small batches: one 4-wave block per query (fills more of the chip, shorter per-query chain)
+    const bool wide = nq < 512;
+    dim3 grid((unsigned)(wide ? nq : ceil_div(nq, 4))), block(256);
+#define RR_ARGS pd, pi, slot_off, nprobe, nq, k, kout, Q, codes, d, ids, nrows, label_offset, xmax2, D, I, nflag, flagged, \
+                eps, rxmax, qres
+    if (metric == kIP) {
+        if (wide) hipLaunchKernelGGL((ivf_rerank_topk<true, 4>), grid, block, 0, st, RR_ARGS);
+        else hipLaunchKernelGGL((ivf_rerank_topk<true, 1>), grid, block, 0, st, RR_ARGS);
+    } else {
+        if (wide) hipLaunchKernelGGL((ivf_rerank_topk<false, 4>), grid, block, 0, st, RR_ARGS);
+        else hipLaunchKernelGGL((ivf_rerank_topk<false, 1>), grid, block, 0, st, RR_ARGS);
+    }
+#undef RR_ARGS
     HIPANN_CHECK(hipGetLastError());
 }
 
