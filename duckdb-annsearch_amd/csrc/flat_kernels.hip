@@ -1028,6 +1028,101 @@ void launch_flat_gemm_topk_bf(int np, const float *Q, const float *qn, int64_t n
     else launch_flat_gemm_topk_bf_t<3>(Q, qn, nq, qsplit, X, xn, N, d, metric, k, nsplit, tiles_per_split, pd, pi, qmajor, st);
 }
 
+// Key matrix of a small problem (the IVF coarse quantizer: 1024 queries × 1024 centroids gives the 128 × 128
+// tiles of flat_gemm_topk only 64 blocks): 64 × 64 tiles, one 32 × 32 sub-tile per wave, the same fp32 MFMA
+// in the same k order as flat_gemm_topk<WRITE> (bit-identical keys), 4× the blocks.
+constexpr int SBM = 64;
+template <bool VEC4>
+__device__ __forceinline__ void small_stage_load(const float *__restrict__ base, int64_t row0, int64_t nrows, int d,
+                                                 int k0, float4 (&r)[2]) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const int f = threadIdx.x + 256 * p;  // float4 index within the 64×32 tile
+        const int row = f >> 3, c4 = f & 7;
+        const int64_t grow = row0 + row;
+        const int kk = k0 + 4 * c4;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (grow < nrows) {
+            const float *src = base + grow * (int64_t)d + kk;
+            if (VEC4) {
+                if (kk < d) v = *reinterpret_cast<const float4 *>(src);
+            } else {
+                if (kk + 0 < d) v.x = src[0];
+                if (kk + 1 < d) v.y = src[1];
+                if (kk + 2 < d) v.z = src[2];
+                if (kk + 3 < d) v.w = src[3];
+            }
+        }
+        r[p] = v;
+    }
+}
+__device__ __forceinline__ void small_stage_store(float *__restrict__ lds, const float4 (&r)[2]) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const int f = threadIdx.x + 256 * p;
+        *reinterpret_cast<float4 *>(lds + (f >> 3) * GLD + 4 * (f & 7)) = r[p];
+    }
+}
+
+template <bool VEC4>
+__global__ void __launch_bounds__(256)
+flat_keys_small(const float *__restrict__ Q, const float *__restrict__ qnorm, int64_t nq, const float *__restrict__ X,
+                const float *__restrict__ xnorm, int64_t N, int d, int metric, int nqt, float *__restrict__ keys_out,
+                int64_t ldk) {
+    __shared__ __attribute__((aligned(16))) float As[2][SBM * GLD], Bs[2][SBM * GLD];
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int qt = lb % nqt;
+    const int64_t q0 = (int64_t)qt * SBM, x0 = (int64_t)(lb / nqt) * SBM;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int l31 = lane & 31, h = lane >> 5;
+    const int nk = (d + GBK - 1) / GBK;
+    float4 sa[2], sb[2];
+    small_stage_load<VEC4>(Q, q0, nq, d, 0, sa);
+    small_stage_load<VEC4>(X, x0, N, d, 0, sb);
+    small_stage_store(As[0], sa);
+    small_stage_store(Bs[0], sb);
+    __syncthreads();
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    for (int kc = 0; kc < nk; ++kc) {
+        const float *Ab = As[kc & 1], *Bb = Bs[kc & 1];
+        if (kc + 1 < nk) {
+            small_stage_load<VEC4>(Q, q0, nq, d, (kc + 1) * GBK, sa);
+            small_stage_load<VEC4>(X, x0, N, d, (kc + 1) * GBK, sb);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const f32x4 a4 = *reinterpret_cast<const f32x4 *>(Ab + (32 * wr + l31) * GLD + 16 * h + 4 * u);
+            const f32x4 b4 = *reinterpret_cast<const f32x4 *>(Bb + (32 * wc + l31) * GLD + 16 * h + 4 * u);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[e], b4[e], acc, 0, 0, 0);
+        }
+        if (kc + 1 < nk) {
+            small_stage_store(As[(kc + 1) & 1], sa);
+            small_stage_store(Bs[(kc + 1) & 1], sb);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int64_t q = q0 + 32 * wr + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int64_t x = x0 + 32 * wc + l31;
+        if (q < nq && x < N) {
+            const float ip = acc[r];
+            float key;
+            if (metric == kL2) {
+                key = fmaf(-2.f, ip, qnorm[q] + xnorm[x]);
+                key = key < 0.f ? 0.f : key;
+            } else {
+                key = -ip;
+            }
+            keys_out[q * ldk + x] = key;
+        }
+    }
+}
+
 size_t scan_smem_bytes(int nq, int d);
 
 void launch_flat_gemm_keys(const float *Q, const float *qn, int64_t nq, const float *X, const float *xn, int64_t N,
@@ -1035,6 +1130,15 @@ void launch_flat_gemm_keys(const float *Q, const float *qn, int64_t nq, const fl
     const int nqt = (int)ceil_div(nq, GBM);
     const int64_t ntiles = ceil_div(N, GBN);
     const bool vec4 = (d % 4 == 0) && ((uintptr_t)Q % 16 == 0) && ((uintptr_t)X % 16 == 0);
+    if ((int64_t)nqt * ntiles < 512) {  // too few 128 × 128 tiles to fill the chip: 64 × 64
+        const int sq = (int)ceil_div(nq, SBM);
+        const int64_t blocks = (int64_t)sq * ceil_div(N, SBM);
+        dim3 g((unsigned)blocks), b(256);
+        if (vec4) hipLaunchKernelGGL(flat_keys_small<true>, g, b, 0, st, Q, qn, nq, X, xn, N, d, metric, sq, keys, ldk);
+        else hipLaunchKernelGGL(flat_keys_small<false>, g, b, 0, st, Q, qn, nq, X, xn, N, d, metric, sq, keys, ldk);
+        HIPANN_CHECK(hipGetLastError());
+        return;
+    }
     const size_t smem = gemm_smem_bytes();
     dim3 grid((unsigned)(nqt * ntiles)), block(256);
     if (vec4)
