@@ -890,6 +890,43 @@ def batch_distance_microbench(hipann):
             "current_gates": {"MIN_GPU_WORK": hipann.MIN_GPU_WORK, "MIN_GPU_WORK_ONESHOT": hipann.MIN_GPU_WORK_ONESHOT}}
 
 
+def flat_auto_gate(hipann):
+    """EnsureGpuIndex's AUTO gates (ntotal >= 256, d >= 128, faiss_index.cpp:128-143) are Metal numbers.  The
+    extension searches one query per call (faiss_index.cpp:737), so the MI355X break-even is the table size
+    from which the host-pointer nq = 1 call (hipann_flat_search: query in, scan, top-k out) beats the CPU
+    path's per-query search (the oracle's FAISS IndexFlat direct-form restatement, one thread at nq = 1)."""
+    from oracle import oracle as O
+
+    rng = np.random.default_rng(3)
+    out = {}
+    for d, sizes in ((128, (1024, 4096, 16384, 65536, 262144, 1048576)), (768, (1024, 4096, 16384, 65536, 262144))):
+        rows, even = [], None
+        for n in sizes:
+            xb = rng.random((n, d), dtype=np.float32)
+            xq = rng.random((24, d), dtype=np.float32)
+            ix = hipann.HipIndexFlat(d, 0, xb)
+            for i in range(4):
+                ix.search(xq[i:i + 1], 10)
+            t0 = time.perf_counter()
+            for i in range(4, 24):
+                ix.search(xq[i:i + 1], 10)
+            g = (time.perf_counter() - t0) / 20 * 1e6
+            ix.close()
+            O.flat_search(xb, xq[:1], 10)
+            t0 = time.perf_counter()
+            for i in range(4, 24):
+                O.flat_search(xb, xq[i:i + 1], 10)
+            c = (time.perf_counter() - t0) / 20 * 1e6
+            rows.append({"ntotal": n, "gpu_us": round(g, 1), "cpu_us": round(c, 1)})
+            if even is None and g < c:
+                even = n
+        out[f"d{d}"] = {"sweep": rows, "break_even_ntotal": even}
+    out["reference_gate"] = "AUTO: ntotal >= 256 and d >= 128 (faiss_index.cpp:128-143)"
+    out["cpu"] = "oracle flat_search, nq = 1 (direct fvec_L2sqr form, one thread)"
+    out["gpu"] = "hipann_flat_search, nq = 1, host pointers (pinned staging, copy kernels, scan, top-k)"
+    return out
+
+
 def run_suite(args, torch, dist, hipann, dev):
     """Every other BASELINE configuration, N = 1, same run."""
     cfg = {}
@@ -917,6 +954,7 @@ def run_suite(args, torch, dist, hipann, dev):
     guarded("C4_diskann_1m_1536_sq8", lambda: diskann_config(args, torch, dist, hipann, 0, 1, dev, 1_000_000, 1536,
                                                              1024, args.k, 128, 64, 10, 2))
     guarded("reference_readme_batch_distances", lambda: batch_distance_microbench(hipann))
+    guarded("flat_auto_gate_nq1", lambda: flat_auto_gate(hipann))
     guarded("ivf_recall_vs_nprobe", lambda: ivf_robustness(args, torch, dist, hipann, dev))
     return cfg
 

@@ -1123,6 +1123,28 @@ flat_keys_small(const float *__restrict__ Q, const float *__restrict__ qnorm, in
     }
 }
 
+// Word copy between device memory and the device mapping of pinned host buffers (small host-pointer
+// calls: no DMA-engine round trips for the query upload and the result download).
+__global__ void __launch_bounds__(256) copy_words(const unsigned *__restrict__ src, unsigned *__restrict__ dst,
+                                                  int64_t words) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < words; i += (int64_t)gridDim.x * 256) dst[i] = src[i];
+}
+
+void launch_copy_words(const void *src, void *dst, size_t bytes, hipStream_t st) {
+    HIPANN_REQUIRE(bytes % 4 == 0, "copy_words: bytes must be a multiple of 4");
+    const int64_t words = (int64_t)(bytes / 4);
+    if (words == 0) return;
+    hipLaunchKernelGGL(copy_words, dim3((unsigned)std::min<int64_t>(64, ceil_div(words, 256))), dim3(256), 0, st,
+                       static_cast<const unsigned *>(src), static_cast<unsigned *>(dst), words);
+    HIPANN_CHECK(hipGetLastError());
+}
+
+void *host_device_ptr(void *pinned) {
+    void *p = nullptr;
+    HIPANN_CHECK(hipHostGetDevicePointer(&p, pinned, 0));
+    return p;
+}
+
 size_t scan_smem_bytes(int nq, int d);
 
 void launch_flat_gemm_keys(const float *Q, const float *qn, int64_t nq, const float *X, const float *xn, int64_t N,

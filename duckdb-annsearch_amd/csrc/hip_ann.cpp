@@ -503,7 +503,8 @@ static int flat_search_host(FlatIndex &ix, int64_t nq, const float *xq, int64_t 
         sh.q.ensure(qbytes, sh.device);
         sh.out_d.ensure(ob * sizeof(float), sh.device);
         sh.out_i.ensure(ob * sizeof(int64_t), sh.device);
-        HIPANN_CHECK(hipMemcpyAsync(sh.q.p, ix.h_q.p, qbytes, hipMemcpyHostToDevice, sh.stream));
+        if (qbytes <= kKernelCopyMax) launch_copy_words(host_device_ptr(ix.h_q.p), sh.q.p, qbytes, sh.stream);
+        else HIPANN_CHECK(hipMemcpyAsync(sh.q.p, ix.h_q.p, qbytes, hipMemcpyHostToDevice, sh.stream));
         flat_shard_search(ix, sh, nq, sh.q.get<float>(), keff, kout, sh.out_d.get<float>(), sh.out_i.get<int64_t>(),
                           sh.stream);
     }
@@ -512,8 +513,13 @@ static int flat_search_host(FlatIndex &ix, int64_t nq, const float *xq, int64_t 
     FlatShard &s0 = *ix.shards[0];
     if (ix.shards.size() == 1) {
         DeviceGuard g(s0.device);
-        HIPANN_CHECK(hipMemcpyAsync(ix.h_d.p, s0.out_d.p, ob * sizeof(float), hipMemcpyDeviceToHost, s0.stream));
-        HIPANN_CHECK(hipMemcpyAsync(ix.h_i.p, s0.out_i.p, ob * sizeof(int64_t), hipMemcpyDeviceToHost, s0.stream));
+        if (ob * sizeof(int64_t) <= kKernelCopyMax) {
+            launch_copy_words(s0.out_d.p, host_device_ptr(ix.h_d.p), ob * sizeof(float), s0.stream);
+            launch_copy_words(s0.out_i.p, host_device_ptr(ix.h_i.p), ob * sizeof(int64_t), s0.stream);
+        } else {
+            HIPANN_CHECK(hipMemcpyAsync(ix.h_d.p, s0.out_d.p, ob * sizeof(float), hipMemcpyDeviceToHost, s0.stream));
+            HIPANN_CHECK(hipMemcpyAsync(ix.h_i.p, s0.out_i.p, ob * sizeof(int64_t), hipMemcpyDeviceToHost, s0.stream));
+        }
         HIPANN_CHECK(hipStreamSynchronize(s0.stream));
     } else {
         // gather per-device partial top-k onto shard 0's device, then one device merge

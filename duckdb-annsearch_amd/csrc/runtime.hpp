@@ -237,6 +237,11 @@ struct IvfIndex : IndexBase {
 };
 
 // ---- kernel launchers (flat_kernels.hip, ivf_kernels.hip, ivf_mfma.hip) ----
+// host-pointer calls up to this many bytes each way move queries / results with a copy kernel through
+// the pinned buffers' device mapping instead of DMA round trips
+constexpr size_t kKernelCopyMax = (size_t)64 << 10;
+void launch_copy_words(const void *src, void *dst, size_t bytes, hipStream_t st);
+void *host_device_ptr(void *pinned);
 void launch_row_norms(const float *x, int64_t n, int d, float *out, hipStream_t st);
 size_t gemm_smem_bytes();
 void launch_flat_gemm_topk(const float *Q, const float *qn, int64_t nq, const float *X, const float *xn, int64_t N,

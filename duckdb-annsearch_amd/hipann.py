@@ -38,6 +38,8 @@ MAX_K = 2048
 # caller (n*d ~0.7M) and against the scalar ComputeDistancesCPU of vector_distances (n*d ~65K).
 MIN_GPU_WORK = 786432
 MIN_GPU_WORK_ONESHOT = 65536
+# hip_ann.h HIPANN_AUTO_MIN_WORK: EnsureGpuIndex's AUTO gate on MI355X, ntotal * d (bench.py flat_auto_gate)
+AUTO_MIN_WORK = 1048576
 
 
 class HipAnnError(RuntimeError):
@@ -485,6 +487,14 @@ class GpuBackend:
 
     def backend_name(self) -> str:
         return "hip"
+
+    def auto_upload(self, ntotal: int, d: int, index_type: str = "Flat") -> bool:
+        """FaissIndex::EnsureGpuIndex's AUTO branch (faiss_index.cpp:128-149) with the MI355X gate: no backend or
+        HNSW → CPU; otherwise upload when ntotal * d >= AUTO_MIN_WORK (the Metal gates ntotal >= 256, d >= 128
+        upload tables whose per-query GPU call is slower than the CPU scan on this part)."""
+        if not self.is_available() or index_type.lower() == "hnsw":
+            return False
+        return int(ntotal) * int(d) >= AUTO_MIN_WORK
 
     def cpu_to_gpu(self, cpu_index: dict):
         if not self.is_available():

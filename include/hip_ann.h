@@ -39,6 +39,11 @@ extern "C" {
 
 /* Largest k the GPU path serves (faiss-metal's block select tops out at 2048, MetalSelect.mm:53-57). */
 #define HIPANN_MAX_K 2048
+/* EnsureGpuIndex's AUTO gate on MI355X (replaces ntotal >= 256 && d >= 128, faiss_index.cpp:128-143): upload
+ * when ntotal * d >= HIPANN_AUTO_MIN_WORK.  Measured (bench.py flat_auto_gate): the host-pointer nq = 1 call
+ * (the extension's per-query search, faiss_index.cpp:737) beats the CPU path's per-query scan from
+ * ntotal * d ~ 0.6-1.5M floats at d = 128 and 768. */
+#define HIPANN_AUTO_MIN_WORK 1048576
 
 /* 1 when at least one gfx950 HIP device is usable, else 0.  Replaces
  * MetalGpuBackend::IsAvailable (gpu_backend_metal.mm:20-31, :33-35). */

@@ -98,3 +98,22 @@ def test_free_null_is_noop(hipann_mod):
     L.hipann_free(None)
     L.diskann_hip_release_db(None)
     assert L.hipann_ntotal(None) == -1
+
+
+def test_auto_gate_mirror(hipann_mod):
+    """EnsureGpuIndex's AUTO branch (faiss_index.cpp:128-149) with the MI355X gate HIPANN_AUTO_MIN_WORK
+    (hip_ann.h): no backend → CPU; HNSW → CPU; else upload from ntotal * d >= 2^20."""
+    import re
+    hdr = (Path(__file__).resolve().parents[1] / "include" / "hip_ann.h").read_text()
+    assert int(re.search(r"#define HIPANN_AUTO_MIN_WORK (\d+)", hdr).group(1)) == hipann_mod.AUTO_MIN_WORK
+
+    class Avail(hipann_mod.GpuBackend):
+        def is_available(self):
+            return True
+
+    b = Avail()
+    assert not b.auto_upload(8191, 128) and b.auto_upload(8192, 128)
+    assert b.auto_upload(1366, 768) and not b.auto_upload(1365, 768)
+    assert not b.auto_upload(10 ** 7, 768, "HNSW")
+    if not hipann_mod.is_available():
+        assert not hipann_mod.GpuBackend().auto_upload(10 ** 7, 768)
