@@ -11,8 +11,9 @@
 //                    the lock-step BFS, disk_provider.rs:556-577).
 //   dist_ids_f32   — HBM-resident fp32 database, candidate = row id (gather).  One wave per row.
 //   dist_ids_sq8   — HBM-resident SQ8 codes (provider.rs:161-210), half a wave per row, 16 codes per
-//                    lane-load; dequantised as v = code·(scale/255) + min (one fma; within 1 ulp of the
-//                    reference's (code/255)·scale + min).
+//                    lane-load; dequantised bit-identically to the reference, (code/255)·scale + min
+//                    (sq8_value).  The resident traversal (diskann_bfs.hip) keeps the fused
+//                    (q − min) − code·(scale/255) form, within 1 ulp per element.
 //
 // Host side: per-thread stream + staging (thread-safe, unlike the Metal bridge's shared ring,
 // metal_diskann_bridge.mm:52-53), a registry of HBM databases, and diskann_hip_search_batch — the
@@ -120,8 +121,19 @@ __global__ void __launch_bounds__(256) dist_ids_f32(const float *__restrict__ qu
     if (lane == 0) out[w] = IP ? -s : s;
 }
 
+// SQ8 decode exactly as provider.rs:140-146: (code as f32 / 255.0) * scale + min, two roundings (no fma).
+// code/255 is the correctly rounded quotient: q0 = code·fl(1/255), one fma residual step (checked for all
+// 256 codes against IEEE division, tests/test_oracle.py).
+__device__ __forceinline__ float sq8_value(float code, float scale, float mn) {
+    constexpr float r = 1.0f / 255.0f;
+    const float q0 = code * r;
+    const float a = fmaf(fmaf(-q0, 255.0f, code), r, q0);
+    const float b = a * scale;
+    return b + mn;
+}
+
 // SQ8: half-wave (32 lanes) per candidate, 16 codes (one uint4) per lane per step.  `ab` holds
-// per-dimension (scale/255, min) pairs in LDS.  Requires d % 16 == 0 (host checks; otherwise the
+// per-dimension (scale, min) pairs in LDS.  Requires d % 16 == 0 (host checks; otherwise the
 // scalar path below).
 template <bool IP>
 __global__ void __launch_bounds__(256) dist_ids_sq8(const float *__restrict__ queries, const uint8_t *__restrict__ codes,
@@ -150,7 +162,7 @@ __global__ void __launch_bounds__(256) dist_ids_sq8(const float *__restrict__ qu
                 for (int b = 0; b < 4; ++b) {
                     const float code = (float)((wv[e] >> (8 * b)) & 0xffu);
                     const float2 p = ab[j0 + 4 * e + b];
-                    const float v = fmaf(code, p.x, p.y);
+                    const float v = sq8_value(code, p.x, p.y);
                     if (IP) s = fmaf(qa[b], v, s);
                     else { const float t = qa[b] - v; s = fmaf(t, t, s); }
                 }
@@ -178,7 +190,7 @@ __global__ void __launch_bounds__(256) dist_ids_sq8_scalar(const float *__restri
     float s = 0.f;
     for (int j = lane; j < d; j += 64) {
         const float2 p = ab[j];
-        const float v = fmaf((float)row[j], p.x, p.y);
+        const float v = sq8_value((float)row[j], p.x, p.y);
         if (IP) s = fmaf(q[j], v, s);
         else { const float t = q[j] - v; s = fmaf(t, t, s); }
     }
@@ -244,7 +256,8 @@ struct DiskDB {
     int dim = 0;
     int fmt = DISKANN_HIP_FMT_F32;
     DevBuf data;  // fp32 rows or u8 codes
-    DevBuf ab;    // float2 per dim (SQ8)
+    DevBuf ab;    // float2 per dim (SQ8): (scale/255, min), the traversal's fused decode
+    DevBuf ab_raw;  // float2 per dim (SQ8): (scale, min), the id-gather kernels' exact decode
     hipStream_t stream = nullptr;
     std::mutex mu;
     DevBuf q, ids, m, out;
@@ -276,7 +289,7 @@ void launch_ids(DiskDB &db, const float *q, const unsigned *ids, const unsigned 
         }
     } else {
         const uint8_t *x = db.data.get<uint8_t>();
-        const float2 *ab = db.ab.get<float2>();
+        const float2 *ab = db.ab_raw.get<float2>();
         if (d % 16 == 0 && (uintptr_t)q % 16 == 0 && d * sizeof(float2) <= 64 * 1024) {
             dim3 grid((unsigned)ceil_div(total_n, 8)), block(256);
             const size_t smem = (size_t)d * sizeof(float2);
@@ -735,13 +748,19 @@ void *diskann_hip_register_db(const void *data, int64_t n, int dim, int fmt, con
         db->data.ensure(bytes + 16, db->device);
         if (bytes) HIPANN_CHECK(hipMemcpyAsync(db->data.p, data, bytes, hipMemcpyHostToDevice, db->stream));
         if (fmt == DISKANN_HIP_FMT_SQ8) {
-            std::vector<float> ab((size_t)dim * 2);
+            // ab: (scale/255, min) for the traversal's fused form; ab_raw: (scale, min) for the id-gather
+            // kernels' exact decode
+            std::vector<float> ab((size_t)dim * 2), abr((size_t)dim * 2);
             for (int j = 0; j < dim; ++j) {
                 ab[2 * j] = sq8_scale[j] / 255.0f;
                 ab[2 * j + 1] = sq8_min[j];
+                abr[2 * j] = sq8_scale[j];
+                abr[2 * j + 1] = sq8_min[j];
             }
             db->ab.ensure(ab.size() * 4, db->device);
+            db->ab_raw.ensure(abr.size() * 4, db->device);
             HIPANN_CHECK(hipMemcpyAsync(db->ab.p, ab.data(), ab.size() * 4, hipMemcpyHostToDevice, db->stream));
+            HIPANN_CHECK(hipMemcpyAsync(db->ab_raw.p, abr.data(), abr.size() * 4, hipMemcpyHostToDevice, db->stream));
         }
         HIPANN_CHECK(hipStreamSynchronize(db->stream));
         return db.release();

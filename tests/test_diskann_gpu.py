@@ -132,6 +132,29 @@ def test_ids_gather_f32_and_sq8(gpu, oracle, fmt, metric, d):
         db.distances_ids(qs, np.array([N], np.uint32), np.array([0], np.uint32), metric)
 
 
+@pytest.mark.parametrize("d", [1536, 100])
+def test_sq8_decode_bit_identical(gpu, oracle, d):
+    """The id-gather kernels dequantise exactly as provider.rs:140-146, (code as f32 / 255.0) * scale + min:
+    with one-hot IP queries the distance of row r to e_j is exactly −v[r, j], compared bitwise with the
+    oracle's decode (the same expression in C, -ffp-contract=off)."""
+    rng = np.random.default_rng(d)
+    N = 2000
+    x = (rng.standard_normal((N, d)) * rng.uniform(0.1, 30, d)).astype(np.float32)
+    mins, scale = oracle.sq8_train(x)
+    codes = oracle.sq8_encode(x, mins, scale)
+    db = gpu.DiskannDeviceDB(codes, 1, mins, scale)
+    dims = np.arange(0, d, 7)
+    qs = np.zeros((len(dims), d), np.float32)
+    qs[np.arange(len(dims)), dims] = 1.0
+    rows = rng.integers(0, N, 300).astype(np.uint32)
+    ids = np.tile(rows, len(dims)).astype(np.uint32)
+    qm = np.repeat(np.arange(len(dims)), len(rows)).astype(np.uint32)
+    out = db.distances_ids(qs, ids, qm, 1)
+    dec = oracle.sq8_decode(codes[rows], mins, scale)  # (rows, d)
+    want = -dec[:, dims].T.reshape(-1)
+    assert np.array_equal(out.view(np.uint32), want.astype(np.float32).view(np.uint32))
+
+
 def test_bfs_matches_oracle_trace(gpu, oracle):
     """Lock-step BFS (DiskProvider::search_batch) through the GPU id-gather path reproduces the oracle
     trace on the committed 2,000-node graph (fp32 and SQ8)."""

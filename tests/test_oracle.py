@@ -243,3 +243,27 @@ def test_cpu_baseline_leg_runs():
     off, ids, codes = build_ivf_lists(xb, cen)
     qps, dt, nth = CB.ivf_qps(cen, off, ids, codes, xq, 10, 4)
     assert qps > 0
+
+
+def test_sq8_code_div255_fma_step_is_ieee():
+    """diskann.hip sq8_value: code/255 as q0 = code·fl(1/255) and one fma residual step equals the IEEE
+    fp32 quotient (Rust's `code as f32 / 255.0`, provider.rs:140-146) for every code 0..255 (fmas
+    evaluated exactly with Fractions, then rounded once to fp32)."""
+    from fractions import Fraction
+
+    def rnd32(fr):
+        c = np.float32(float(fr))  # nearest double, then nearest float: check the two neighbours exactly
+        best = None
+        for cand in (np.nextafter(c, np.float32(-np.inf)), c, np.nextafter(c, np.float32(np.inf))):
+            err = abs(Fraction(float(cand)) - fr)
+            even = (np.float32(cand).view(np.uint32) & 1) == 0
+            if best is None or err < best[0] or (err == best[0] and even):
+                best = (err, np.float32(cand))
+        return best[1]
+
+    r = np.float32(1.0) / np.float32(255.0)
+    for code in range(256):
+        q0 = np.float32(np.float32(code) * r)
+        e = rnd32(Fraction(float(code)) - Fraction(float(q0)) * 255)
+        a = rnd32(Fraction(float(e)) * Fraction(float(r)) + Fraction(float(q0)))
+        assert a == np.float32(code) / np.float32(255.0), code
