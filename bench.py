@@ -954,7 +954,7 @@ def run_suite(args, torch, dist, hipann, dev):
 
     guarded("C1_flat_10k_128_cpu_path", lambda: c1_config(torch, hipann, dev))
     guarded("C2_flat_l2_1m_768", lambda: flat(1_000_000, oracle_queries=32))
-    guarded("flat_l2_10m_768", lambda: flat(10_000_000, latency=True, steps=5))
+    guarded("flat_l2_10m_768", lambda: flat(10_000_000, oracle_queries=20, latency=True, steps=5))
     guarded("C4_diskann_1m_1536_sq8", lambda: diskann_config(args, torch, dist, hipann, 0, 1, dev, 1_000_000, 1536,
                                                              1024, args.k, 128, 64, 10, 2))
     guarded("reference_readme_batch_distances", lambda: batch_distance_microbench(hipann))
