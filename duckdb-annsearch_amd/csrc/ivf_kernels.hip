@@ -1197,6 +1197,10 @@ __global__ void __launch_bounds__(256) ivf_scatter_results(const float *__restri
     I[(int64_t)idx[j] * kout + e] = If[t];
 }
 
+#ifndef HIPANN_RR_WIDE
+#define HIPANN_RR_WIDE (1 << 30)  // below this many queries: one 4-wave block per query (nq 1024: 80 -> 65 us)
+#endif
+
 void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int nprobe, int64_t nq, int k, int kout,
                        int metric, const float *Q, const float *codes, int d, const int64_t *ids, int64_t nrows,
                        int64_t label_offset, float xmax2, float *D, int64_t *I, int *nflag, int *flagged,
@@ -1204,7 +1208,7 @@ void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int 
     if (nq <= 0) return;
     HIPANN_REQUIRE(k >= kRerankK && k <= 64 && kout >= 1 && kout <= kRerankMaxK, "ivf rerank: k / kout out of range");
     // small batches: one 4-wave block per query (fills more of the chip, shorter per-query chain)
-    const bool wide = nq < 512;
+    const bool wide = nq < HIPANN_RR_WIDE;
     dim3 grid((unsigned)(wide ? nq : ceil_div(nq, 4))), block(256);
 #define RR_ARGS pd, pi, slot_off, nprobe, nq, k, kout, Q, codes, d, ids, nrows, label_offset, xmax2, D, I, nflag, flagged, \
                 eps, rxmax, qres
