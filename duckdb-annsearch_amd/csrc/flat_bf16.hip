@@ -86,8 +86,11 @@ __global__ void __launch_bounds__(256) b16_row_residual2(const float *__restrict
 
 // Epilogue of one tile: acc[j] = q·x of query rows (r&3) + 8(r>>2) + 4h (+ 32·wave) and database row
 // x0 + 32j + (lane & 31).  cth[r] = ‖q‖² − thr (L2) or −2·thr (IP); xnv[j] = ‖x‖² (L2) or 0, +inf past N.
+// ‖q‖² of the lane's query row r is read from qnorm (L2-resident) on the slow path only, which keeps the
+// main loop's registers for deeper LDS fragment prefetch.
 template <bool L2M>
-__device__ __forceinline__ void b16_epilogue(const b16_f32x16 (&acc)[8], float (&cth)[16], const float (&qnv)[16],
+__device__ __forceinline__ void b16_epilogue(const b16_f32x16 (&acc)[8], float (&cth)[16],
+                                             const float *__restrict__ qnorm, int64_t qrow0, int64_t nq,
                                              const float (&xnv)[8], int64_t x0, int64_t N, float *__restrict__ Ld,
                                              int *__restrict__ Li, int k, int wave, int lane) {
     const int l31 = lane & 31, h = lane >> 5;
@@ -99,12 +102,14 @@ __device__ __forceinline__ void b16_epilogue(const b16_f32x16 (&acc)[8], float (
         const unsigned long long m = __ballot(any);
         if (m == 0ull) continue;
         // slow path (rare after the first tiles): each half of the wave is one query
+        const int64_t qr = qrow0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float qnr = (L2M && qr < nq) ? qnorm[qr] : 0.f;
         float key[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             float kv;
             if (L2M) {
-                kv = fmaf(-2.f, acc[j][r], qnv[r] + xnv[j]);
+                kv = fmaf(-2.f, acc[j][r], qnr + xnv[j]);
                 kv = kv < 0.f ? 0.f : kv;
             } else {
                 kv = -acc[j][r];
@@ -131,7 +136,7 @@ __device__ __forceinline__ void b16_epilogue(const b16_f32x16 (&acc)[8], float (
                 Li[ql * k + lane] = L.id[0];
             }
             const float nt = readlane_f(L.d[0], k - 1);
-            if (h == hh) cth[r] = L2M ? qnv[r] - nt : -2.f * nt;
+            if (h == hh) cth[r] = L2M ? qnr - nt : -2.f * nt;
         }
     }
 }
@@ -183,13 +188,13 @@ flat_bf16_topk(const b16_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm
         Ld[e] = seed && q < nq ? seed[q] : __builtin_inff();
         Li[e] = 0x7fffffff;
     }
-    float cth[16], qnv[16];
+    float cth[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int64_t q = q0 + 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * h;
-        qnv[r] = (L2M && q < nq) ? qnorm[q] : 0.f;
+        const float qn = (L2M && q < nq) ? qnorm[q] : 0.f;
         const float thr = q < nq ? (seed ? seed[q] : __builtin_inff()) : -__builtin_inff();  // −inf: rows past nq
-        cth[r] = L2M ? qnv[r] - thr : -2.f * thr;
+        cth[r] = L2M ? qn - thr : -2.f * thr;
     }
 
     // chunk g = (t − t0)·nk + kc: query chunk kc and database chunk t·nk + kc (a split's database chunks are
@@ -241,12 +246,27 @@ flat_bf16_topk(const b16_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             const int c = 2 * s + h;
-            const b16x8 a = __builtin_bit_cast(b16x8, Ab[b16_slot(c, 32 * wave + l31, QM)]);
+            // every fragment of this k-step read before its MFMAs: one LDS wait per 8 MFMAs instead of
+            // one per MFMA
+            // b16_slot(c, 32·j + l31, R) = c·R + 32·j + (l31 ^ 2c) (the swizzle stays inside the low 5 bits):
+            // one base per c, the j offsets are immediates
+            const int lx = l31 ^ (c << 1);
+            const b16x8 a = __builtin_bit_cast(b16x8, Ab[c * QM + 32 * wave + lx]);
+            const b16_u32x4 *Bc = Bb + c * B16_TN + lx;
+            b16x8 bf[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const b16x8 b = __builtin_bit_cast(b16x8, Bb[b16_slot(c, 32 * j + l31, B16_TN)]);
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[j], 0, 0, 0);
+            for (int j = 0; j < 8; ++j) bf[j] = __builtin_bit_cast(b16x8, Bc[32 * j]);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bf[j], acc[j], 0, 0, 0);
+            // schedule: three LDS reads ahead, then one MFMA per read — each fragment is read two MFMAs
+            // (≥ 64 cycles) before its use instead of waiting on a read issued just before
+            __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
             }
+            __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
         }
         stage = stage + 1 < NB ? stage + 1 : 0;
         if (++kc == nk) {
@@ -258,7 +278,7 @@ flat_bf16_topk(const b16_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm
                 const int64_t x = x0 + 32 * j + l31;
                 xnv[j] = x < N ? (L2M ? xnorm[x] : 0.f) : __builtin_inff();
             }
-            b16_epilogue<L2M>(acc, cth, qnv, xnv, x0, N, Ld, Li, k, wave, lane);
+            b16_epilogue<L2M>(acc, cth, qnorm, q0 + 32 * wave, nq, xnv, x0, N, Ld, Li, k, wave, lane);
 #pragma unroll
             for (int j = 0; j < 8; ++j)
 #pragma unroll
