@@ -286,15 +286,16 @@ def flat_config(args, torch, dist, hipann, rank, world, dev, n, d, nq, k, metric
             "algorithmic": f"{terms} x 2*nq*N_local*d = {terms * flops:.4g} MFMA FLOP per launch ({fdesc})",
             "fp32_equivalent_tflops": round(flops / (kern_ms * 1e-3) / 1e12, 2) if kern_ms > 0 else None}
     if form == 4 and kern_ms > 0:
-        # what bounds the bf16 scan: every 256-query x 256-row tile streams (256 + 256) x 32 dims x 2 B into LDS
-        # per 32-dim chunk (LDS-DMA) for 4.2 MFLOP — 128 FLOP/B, so the fill rate, not the MFMA pipe, sets the pace
+        # LDS-DMA fill of the bf16 scan: per 32-dim chunk the 256-row database tile (16 KB) — plus the query tile
+        # when the queries are not loaded straight into registers (RA, 256-query blocks)
         qm = 256 if nq >= 256 else 128 if nq >= 128 else 64
-        fill = -(-nq // qm) * -(-n_local // 256) * -(-d // 32) * (qm + 256) * 64.0
+        a_rows = 0 if qm == 256 and os.environ.get("HIPANN_B16_RA", "1") != "0" else qm  # RA: queries via VGPRs
+        fill = -(-nq // qm) * -(-n_local // 256) * -(-d // 32) * (a_rows + 256) * 64.0
         roof["lds_fill"] = {"bytes_per_launch_gb": round(fill / 1e9, 2),
                             "achieved_tbps": round(fill / (kern_ms * 1e-3) / 1e12, 2),
                             "ceiling_note": "MI355X_MICROARCH.md: LDS-DMA streams measured at 6.4-6.8 TB/s chip-wide "
                                             "(ldsdma-fill), an all-LDS-DMA prologue at 12-13 B/cycle/CU",
-                            "flop_per_byte": 128}
+                            "flop_per_byte": round(2.0 * nq * n_local * d / fill, 1)}
     if world == 1:
         attach_traffic(roof, f"flat_{n}x{d}{'' if metric == 0 else '_ip'}", 4.0 * n_local * d)
     out = {"workload": f"FAISS Flat {'L2' if metric == 0 else 'IP'}, {n}x{d} fp32, batch={nq}, k={k}",

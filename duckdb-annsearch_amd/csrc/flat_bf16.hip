@@ -31,6 +31,9 @@
 #include "runtime.hpp"
 #include "wave_topk.hpp"
 
+#include <cstdlib>
+#include <type_traits>
+
 namespace hipann {
 
 typedef __bf16 b16x8 __attribute__((ext_vector_type(8)));
@@ -148,7 +151,11 @@ __device__ __forceinline__ void b16_wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <bool L2M, int W>
+// RA (register A): each wave's query fragments (2 × 16 B per lane per chunk — no other wave reads them) come
+// straight from the L2-resident query image into a 3-deep register ring instead of through LDS, so the
+// LDS-DMA fill carries only the shared database tile: 16 KB per 32-dim chunk instead of 32 KB (the fill
+// rate, ≈6 TB/s chip-wide, is what bounds this kernel at 128 FLOP/B).
+template <bool L2M, int W, bool RA>
 __global__ void __launch_bounds__(64 * W, 1)
 flat_bf16_topk(const b16_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm, int64_t nq,
                const b16_u32x4 *__restrict__ Xt,
@@ -157,10 +164,10 @@ flat_bf16_topk(const b16_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm
                const float *__restrict__ seed) {
     constexpr int QM = 32 * W;
     constexpr int AU = QM * 4, BU = B16_TN * 4;  // 16-B units per chunk image
-    constexpr int SU = AU + BU;                  // units per LDS stage
+    constexpr int SU = RA ? BU : AU + BU;        // units per LDS stage
     constexpr int NB = 3;                        // stages: chunk g+2 in flight while chunk g is read
     constexpr int IA = AU / 64 / W, IB = BU / 64 / W;  // global_load_lds (1 KiB each) per wave per chunk
-    constexpr int NI = IA + IB;
+    constexpr int NI = RA ? IB + 2 : IA + IB;   // vector-memory ops per wave per chunk
     static_assert(IA * 64 * W == AU && IB * 64 * W == BU, "chunk images must split evenly over the waves");
     extern __shared__ __attribute__((aligned(16))) b16_u32x4 smem_b16[];
     float *Ld = reinterpret_cast<float *>(smem_b16 + NB * SU);  // [QM][k]
@@ -203,19 +210,31 @@ flat_bf16_topk(const b16_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm
     const b16_u32x4 *Qb = Qt + (int64_t)qt * nk * AU + lane;
     const b16_u32x4 *Xb = Xt + t0 * nk * BU + lane;
     int kc_issue = 0;
-    auto issue = [&](int64_t g, int stage) {
+    // RA: this lane's fragment of query chunk kc, k-step s (c = 2s + h), read from the image directly
+    const b16_u32x4 *Qw = Qt + (int64_t)qt * nk * AU + 32 * wave;
+    b16_u32x4 ar[NB][2];  // RA register ring (slot = chunk % NB, compile-time after unrolling)
+    auto issue = [&](int64_t g, int stage, auto slot_c) {
+        constexpr int SL = decltype(slot_c)::value;
         b16_u32x4 *dst = smem_b16 + stage * SU;
+        if constexpr (RA) {
 #pragma unroll
-        for (int i = 0; i < IA; ++i) {
-            const int inst = wave * IA + i;
-            __builtin_amdgcn_global_load_lds((const void *)(Qb + (int64_t)kc_issue * AU + inst * 64),
-                                             (b16_lds_void *)(dst + inst * 64), 16, 0, 0);
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const int c = 2 * s2 + h;
+                ar[SL][s2] = Qw[(int64_t)kc_issue * AU + c * QM + (l31 ^ (c << 1))];
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < IA; ++i) {
+                const int inst = wave * IA + i;
+                __builtin_amdgcn_global_load_lds((const void *)(Qb + (int64_t)kc_issue * AU + inst * 64),
+                                                 (b16_lds_void *)(dst + inst * 64), 16, 0, 0);
+            }
         }
 #pragma unroll
         for (int i = 0; i < IB; ++i) {
             const int inst = wave * IB + i;
             __builtin_amdgcn_global_load_lds((const void *)(Xb + g * BU + inst * 64),
-                                             (b16_lds_void *)(dst + AU + inst * 64), 16, 0, 0);
+                                             (b16_lds_void *)(dst + (RA ? 0 : AU) + inst * 64), 16, 0, 0);
         }
         kc_issue = kc_issue + 1 < nk ? kc_issue + 1 : 0;
     };
@@ -226,23 +245,36 @@ flat_bf16_topk(const b16_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
     __syncthreads();  // list initialisation
-    if (G > 0) issue(0, 0);
-    if (G > 1) issue(1, 1);
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    if (RA && G > 0) {  // the ring starts full (past the end: the last chunk again)
+        issue(0, 0, I0{});
+        issue(G > 1 ? 1 : 0, 1, I1{});
+    } else {
+        if (G > 0) issue(0, 0, I0{});
+        if (G > 1) issue(1, 1, I1{});
+    }
 
     int kc = 0, stage = 0;
     int64_t t = t0;
-    for (int64_t g = 0; g < G; ++g) {
+    // one chunk; SL = g % NB (RA's register slot; the loop below is unrolled by NB)
+    auto body = [&](int64_t g, auto slot_c) {
+        constexpr int SL = decltype(slot_c)::value;
         // retire this wave's copies of chunk g (chunk g+1's stay in flight), finish this wave's reads of the
         // stage about to be refilled, then one barrier: every wave's chunk-g copies have landed and nobody
         // still reads stage (g+2) % NB = (g−1) % NB
-        if (g + 1 < G) b16_wait_vm<NI>();
+        // RA: the issue is unconditional (past the end it re-reads the last chunk into a free stage), so every
+        // iteration has the same count of vector-memory ops and the compiler's own waits stay exact
+        if (RA || g + 1 < G) b16_wait_vm<NI>();
         else b16_wait_vm<0>();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (g + 2 < G) issue(g + 2, stage == 0 ? 2 : stage - 1);
+        if (RA) issue(g + 2 < G ? g + 2 : G - 1, stage == 0 ? 2 : stage - 1, std::integral_constant<int, (SL + 2) % NB>{});
+        else if (g + 2 < G) issue(g + 2, stage == 0 ? 2 : stage - 1, std::integral_constant<int, (SL + 2) % NB>{});
         const b16_u32x4 *Ab = smem_b16 + stage * SU;
-        const b16_u32x4 *Bb = Ab + AU;
+        const b16_u32x4 *Bb = Ab + (RA ? 0 : AU);
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             const int c = 2 * s + h;
@@ -251,7 +283,8 @@ flat_bf16_topk(const b16_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm
             // b16_slot(c, 32·j + l31, R) = c·R + 32·j + (l31 ^ 2c) (the swizzle stays inside the low 5 bits):
             // one base per c, the j offsets are immediates
             const int lx = l31 ^ (c << 1);
-            const b16x8 a = __builtin_bit_cast(b16x8, Ab[c * QM + 32 * wave + lx]);
+            const b16x8 a = RA ? __builtin_bit_cast(b16x8, ar[SL][s])
+                               : __builtin_bit_cast(b16x8, Ab[c * QM + 32 * wave + lx]);
             const b16_u32x4 *Bc = Bb + c * B16_TN + lx;
             b16x8 bf[8];
 #pragma unroll
@@ -285,6 +318,16 @@ flat_bf16_topk(const b16_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm
                 for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
             ++t;
         }
+    };
+    if constexpr (RA) {
+        for (int64_t g = 0; g < G; g += NB) {
+            body(g, I0{});
+            if (g + 1 < G) body(g + 1, I1{});
+            if (g + 2 < G) body(g + 2, I2{});
+        }
+        b16_wait_vm<0>();  // no LDS-DMA copy may land after the block's LDS is handed to the next block
+    } else {
+        for (int64_t g = 0; g < G; ++g) body(g, I0{});
     }
     // per-(split, query) lists, query-major (ivf_rerank_topk reads a query's lists contiguously)
     for (int r = 0; r < 32; ++r) {
@@ -366,14 +409,21 @@ void launch_flat_bf16_topk(const float *Q, const float *qn, int64_t nq, void *qi
         hipLaunchKernelGGL(kern, grid, block, smem, st, qa, qn, nq, xa, xn, N, nk, k, nqt, nsplit, tiles_per_split, pd,
                            pi, seed);
     };
-    if (metric == kL2) {
-        if (W == 8) go(flat_bf16_topk<true, 8>);
-        else if (W == 4) go(flat_bf16_topk<true, 4>);
-        else go(flat_bf16_topk<true, 2>);
+    static const bool ra = [] { const char *e = std::getenv("HIPANN_B16_RA"); return !e || std::atoi(e); }();
+    const size_t smem_ra = (size_t)3 * (B16_TN * 4) * 16 + (size_t)QM * k * 8;
+    if (ra && W == 8) {
+        if (metric == kL2) hipLaunchKernelGGL((flat_bf16_topk<true, 8, true>), grid, block, smem_ra, st, qa, qn, nq, xa, xn, N,
+                                              nk, k, nqt, nsplit, tiles_per_split, pd, pi, seed);
+        else hipLaunchKernelGGL((flat_bf16_topk<false, 8, true>), grid, block, smem_ra, st, qa, qn, nq, xa, xn, N, nk, k,
+                                nqt, nsplit, tiles_per_split, pd, pi, seed);
+    } else if (metric == kL2) {
+        if (W == 8) go(flat_bf16_topk<true, 8, false>);
+        else if (W == 4) go(flat_bf16_topk<true, 4, false>);
+        else go(flat_bf16_topk<true, 2, false>);
     } else {
-        if (W == 8) go(flat_bf16_topk<false, 8>);
-        else if (W == 4) go(flat_bf16_topk<false, 4>);
-        else go(flat_bf16_topk<false, 2>);
+        if (W == 8) go(flat_bf16_topk<false, 8, false>);
+        else if (W == 4) go(flat_bf16_topk<false, 4, false>);
+        else go(flat_bf16_topk<false, 2, false>);
     }
     HIPANN_CHECK(hipGetLastError());
 }
