@@ -917,6 +917,123 @@ rows_topk(const float *__restrict__ keys, int64_t ldk, int64_t ncols, int64_t nq
     L.store(part_d + off, part_i + off, k);
 }
 
+// rows_select_out — a whole key row per wave straight to the output (one-chunk tables: the IVF coarse
+// quantizer's nq × nlist keys).  The lexicographic (key, column) top-k of the row, written as
+// merge_parts_topk writes it (D = key·out_sign, I = label_offset + column; +inf keys and empty slots
+// become (±inf, −1)) — identical to rows_topk over segments + merge_parts_topk, in one launch with
+// every key load of the row in flight at once.
+template <int S>
+__global__ void __launch_bounds__(256)
+rows_select_out(const float *__restrict__ keys, int64_t ldk, int64_t ncols, int64_t nq, int k, int kout,
+                int64_t label_offset, float out_sign, float *__restrict__ D, int64_t *__restrict__ I) {
+    constexpr int U = 8;  // 64-column chunks loaded ahead of their offers
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq) return;
+    const int lane = threadIdx.x & 63;
+    const float *row = keys + q * ldk;
+    WaveList<S, int> L;
+    L.init();
+    for (int64_t c0 = 0; c0 < ncols; c0 += 64 * U) {
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t c = c0 + 64 * u + lane;
+            v[u] = c < ncols ? row[c] : __builtin_inff();
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t c = c0 + 64 * u + lane;
+            L.offer(v[u], c < ncols ? (int)c : 0x7fffffff, k - 1);
+        }
+    }
+    const float pad_d = out_sign > 0.f ? __builtin_inff() : -__builtin_inff();
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const int e = s * 64 + lane;
+        if (e < kout) {
+            const bool pad = e >= k || L.id[s] == 0x7fffffff || L.d[s] == __builtin_inff();
+            D[q * kout + e] = pad ? pad_d : L.d[s] * out_sign;
+            I[q * kout + e] = pad ? -1 : (int64_t)L.id[s] + label_offset;
+        }
+    }
+}
+
+// rows_select_small — the same output for rows of ≤ 64·J columns and k ≤ 64, without serial inserts:
+// the row sits in registers (J keys per lane, column 64j + lane) as order-preserving u32 (±0 merged, NaN
+// never selected — as lex_less never admits it); the k-th smallest value T comes from a 32-step bitwise
+// search (each step: J ballots + popcounts), the keys < T and then the first (by column) keys == T are
+// compacted through LDS, and one bitonic wave sort orders them by (key, column).  ≈ 1.5K instructions
+// per row against the ≈ 20 latency-bound serial inserts per row of the list path (1024 × 1024, k 32:
+// 41 µs with the list path).
+template <int J>
+__global__ void __launch_bounds__(256)
+rows_select_small(const float *__restrict__ keys, int64_t ldk, int ncols, int64_t nq, int k, int kout,
+                  int64_t label_offset, float out_sign, float *__restrict__ D, int64_t *__restrict__ I) {
+    __shared__ float sk[4][64];
+    __shared__ int sc[4][64];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t q = (int64_t)blockIdx.x * 4 + wv;
+    const bool live = q < nq;  // wave-uniform; every wave reaches the barrier
+    const float *row = keys + (live ? q : 0) * ldk;
+    float v[J];
+    unsigned u[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int c = 64 * j + lane;
+        v[j] = live && c < ncols ? row[c] : __builtin_nanf("");
+    }
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const float f = v[j] == 0.f ? 0.f : v[j];
+        const unsigned b = __float_as_uint(f);
+        u[j] = v[j] == v[j] ? ((b >> 31) ? ~b : (b | 0x80000000u)) : 0xffffffffu;
+    }
+    unsigned T = 0;
+    for (int bit = 31; bit >= 0; --bit) {
+        const unsigned cand = T | (1u << bit);
+        int cnt = 0;
+#pragma unroll
+        for (int j = 0; j < J; ++j) cnt += __popcll(__ballot(u[j] < cand));
+        if (cnt < k) T = cand;
+    }
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    int base = 0;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const bool s = u[j] < T;
+        const unsigned long long m = __ballot(s);
+        if (s) {
+            const int pos = base + __popcll(m & lt);
+            sk[wv][pos] = v[j];
+            sc[wv][pos] = 64 * j + lane;
+        }
+        base += __popcll(m);
+    }
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const bool s = u[j] == T && u[j] != 0xffffffffu;
+        const unsigned long long m = __ballot(s);
+        if (s) {
+            const int pos = base + __popcll(m & lt);
+            if (pos < k) {
+                sk[wv][pos] = v[j];
+                sc[wv][pos] = 64 * j + lane;
+            }
+        }
+        base += __popcll(m);
+    }
+    const int nsel = base < k ? base : k;
+    __syncthreads();
+    float kk = lane < nsel ? sk[wv][lane] : __builtin_inff();
+    int cc = lane < nsel ? sc[wv][lane] : 0x7fffffff;
+    wave_sort(kk, cc);
+    if (live && lane < kout) {
+        const bool pad = lane >= nsel || kk == __builtin_inff();
+        D[q * kout + lane] = pad ? (out_sign > 0.f ? __builtin_inff() : -__builtin_inff()) : kk * out_sign;
+        I[q * kout + lane] = pad ? -1 : (int64_t)cc + label_offset;
+    }
+}
+
 // Raw merge: nparts partial [part][nq][k] (keys, int ids) → one [nq][k] partial (keys, int ids).
 template <int S>
 __global__ void __launch_bounds__(256)
@@ -1218,6 +1335,34 @@ void launch_rows_topk(const float *keys, int64_t ldk, int64_t ncols, int64_t nq,
     HIPANN_ROWS_CASE(32)
 #undef HIPANN_ROWS_CASE
     throw HipError("rows_topk: k too large");
+}
+
+bool launch_rows_select_out(const float *keys, int64_t ldk, int64_t ncols, int64_t nq, int k, int kout,
+                            int64_t label_offset, float out_sign, float *D, int64_t *I, hipStream_t st) {
+    const int S = (kout + 63) / 64;
+    if (S > 4 || ncols > 0x7ffffffe || k > kout) return false;  // the segment path + merge instead
+    dim3 grid((unsigned)ceil_div(nq, 4)), block(256);
+    static const bool lists = [] { const char *e = std::getenv("HIPANN_ROWSEL_LIST"); return e && std::atoi(e); }();
+    if (kout <= 64 && ncols <= 1024 && !lists) {  // rows of ≤ 1024 keys: the bitwise select
+        if (ncols <= 256)
+            hipLaunchKernelGGL(rows_select_small<4>, grid, block, 0, st, keys, ldk, (int)ncols, nq, k, kout,
+                               label_offset, out_sign, D, I);
+        else
+            hipLaunchKernelGGL(rows_select_small<16>, grid, block, 0, st, keys, ldk, (int)ncols, nq, k, kout,
+                               label_offset, out_sign, D, I);
+        HIPANN_CHECK(hipGetLastError());
+        return true;
+    }
+#define HIPANN_RSEL_CASE(s)                                                                                      \
+    if (S <= s) {                                                                                                \
+        hipLaunchKernelGGL(rows_select_out<s>, grid, block, 0, st, keys, ldk, ncols, nq, k, kout, label_offset, \
+                           out_sign, D, I);                                                                      \
+        HIPANN_CHECK(hipGetLastError());                                                                         \
+        return true;                                                                                             \
+    }
+    HIPANN_RSEL_CASE(1) HIPANN_RSEL_CASE(2) HIPANN_RSEL_CASE(4)
+#undef HIPANN_RSEL_CASE
+    return false;
 }
 
 void launch_merge_raw(const float *pd, const int *pi, int nparts, int64_t nq, int k, float *od, int *oi,

@@ -159,6 +159,12 @@ static void flat_shard_search_bigk(FlatIndex &ix, FlatShard &sh, int64_t nq, con
                 launch_flat_gemm_keys(xq, qn, nq, sh.xb, sh.xn.get<float>(), sh.n, d, metric, sh.keys.get<float>(), C,
                                       st);
         }
+        {  // kout ≤ 256: one wave selects the whole row and writes the output (no segment lists, no merge)
+            ScopedTiming t(ix.timer_merge, st);
+            if (launch_rows_select_out(sh.keys.get<float>(), C, sh.n, nq, k, kout, sh.label_offset, out_sign, D, I,
+                                       st))
+                return;
+        }
         // short rows: 256-column segments, so a 1024-centroid row is selected by 4 waves, not 1
         const int64_t sl = sh.n <= seg_len && k <= 64 ? 256 : seg_len;
         const int ns = (int)ceil_div(sh.n, sl);
@@ -228,6 +234,7 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
     const int d = ix.d, metric = ix.metric;
     const float out_sign = metric == kIP ? -1.f : 1.f;
     HIPANN_REQUIRE(k <= HIPANN_MAX_K, "k larger than HIPANN_MAX_K");
+    sh.qn_of = nullptr;  // set below when this call computes ‖q‖² into sh.qn
     if (nq <= 0) return;
     if (sh.n == 0) {  // no rows: pads only
         launch_merge_parts<int>(nullptr, nullptr, 0, nq, k, kout, sh.label_offset, 1.f, out_sign, D, I, st);
@@ -243,6 +250,8 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
             sh.qn.ensure((size_t)nq * sizeof(float), sh.device);
             launch_row_norms(xq, nq, d, sh.qn.get<float>(), st);
             qn = sh.qn.get<float>();
+            sh.qn_of = xq;
+            sh.qn_nq = nq;
         }
         flat_shard_search_bigk(ix, sh, nq, xq, qn, k, kout, D, I, st);
         return;
@@ -275,6 +284,8 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
         sh.qn.ensure((size_t)nq * sizeof(float), sh.device);
         launch_row_norms(xq, nq, d, sh.qn.get<float>(), st);
         qn = sh.qn.get<float>();
+        sh.qn_of = xq;
+        sh.qn_nq = nq;
     }
     int form = form_override >= 0 ? form_override : ix.form;
     const bool exact = (form == kFlatSplit2Exact || form == kFlatBf16Exact) && kout <= kRerankMaxK;

@@ -9,6 +9,7 @@
 #include "ivf.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 
@@ -176,6 +177,13 @@ IvfIndex::~IvfIndex() {
     }
 }
 
+// HIPANN_IVF_HOST_FALLBACK=1: the flagged queries of the exact forms are re-run from the host on the 3-term
+// path after a readback of the flag count (the r01/r02 scheme; A/B only).  Default: on the device.
+static bool host_fallback() {
+    static const bool v = [] { const char *e = std::getenv("HIPANN_IVF_HOST_FALLBACK"); return e && std::atoi(e) != 0; }();
+    return v;
+}
+
 // One shard: queries on the shard's device → D/I (nq × kout) on the same device, async on `st`.
 // max‖x‖² of the shard (once): the rerank's error bound
 float shard_xmax2(IvfShard &sh, int d, hipStream_t st) {
@@ -245,9 +253,26 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     k = kscan;  // per-list k of the scan (the output keeps kout)
     const bool tiled = form == kFormDecomposed || ivf_form_split(form);  // the matrix-core scans
     const int group = half ? ivf_mfma_h_group(d) : ivf_group_size(form, d);
+    float xmax2 = 0.f;
+    if (exact) {  // max‖x‖² (once per row set; nflag is its scratch, so before the plan resets the flag count)
+        xmax2 = shard_xmax2(sh, d, st);
+        sh.nflag.ensure(sizeof(int), sh.device);
+        sh.flagged.ensure(sizeof(int) * (size_t)nq, sh.device);
+    }
+    unsigned *qbound = nullptr;
+    if (tiled) {  // every query's bound starts at +inf (order-preserving bits 0xff800000), set by the plan
+        sh.qbound.ensure(sizeof(unsigned) * (size_t)nq, sh.device);
+        qbound = sh.qbound.get<unsigned>();
+    }
+    if (!sh.ccnt.p) {  // zeroed once; ivf_plan_q leaves it zero after every batch
+        sh.ccnt.ensure(sizeof(int) * (size_t)nlist, sh.device);
+        HIPANN_CHECK(hipMemsetAsync(sh.ccnt.p, 0, sizeof(int) * (size_t)nlist, st));
+    }
+    sh.qtot.ensure(sizeof(int) * (size_t)nq, sh.device);
     launch_ivf_plan(sh.coarse_i.get<int64_t>(), nq, np, sh.list_len.get<int>(), nlist, group, sh.cnt.get<int>(),
                     sh.bucket_off.get<int>(), sh.item_off.get<int>(), sh.cursor.get<int>(), sh.bucket.get<int>(),
-                    sh.slot_off.get<int>(), st);
+                    sh.slot_off.get<int>(), st, exact ? sh.nflag.get<int>() : nullptr, qbound, sh.ccnt.get<int>(),
+                    sh.qtot.get<int>());
     // 3. scan: one k-list per (query, probe, row chunk) slot — every slot is written by exactly one item
     const size_t parts = (size_t)np * nq * sh.max_nch * k;
     HIPANN_REQUIRE((int64_t)np * nq * sh.max_nch < (int64_t)0x7fffffff, "too many partial lists");
@@ -256,15 +281,14 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     const int64_t max_items = ivf_max_items(nq, np, nlist, sh.max_nch, sh.n, group);
     const float *qn = nullptr;
     if (form != kFormDirect && metric == kL2) {
-        sh.qn.ensure(sizeof(float) * (size_t)nq, sh.device);
-        launch_row_norms(xq, nq, d, sh.qn.get<float>(), st);
-        qn = sh.qn.get<float>();
-    }
-    unsigned *qbound = nullptr;
-    if (tiled) {  // every query's bound starts at +inf (order-preserving bits 0xff800000)
-        sh.qbound.ensure(sizeof(unsigned) * (size_t)nq, sh.device);
-        qbound = sh.qbound.get<unsigned>();
-        HIPANN_CHECK(hipMemsetD32Async((hipDeviceptr_t)qbound, 0xff800000, (size_t)nq, st));
+        const FlatShard &qs = *sh.quant->shards[0];
+        if (qs.qn_of == xq && qs.qn_nq == nq) {
+            qn = qs.qn.get<float>();  // the coarse quantizer's ‖q‖² of the same queries
+        } else {
+            sh.qn.ensure(sizeof(float) * (size_t)nq, sh.device);
+            launch_row_norms(xq, nq, d, sh.qn.get<float>(), st);
+            qn = sh.qn.get<float>();
+        }
     }
     if (tiled && !half) ensure_tiled_codes(sh, d, nlist, st);
     if (half) {
@@ -311,15 +335,26 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
                          kout, out_sign, D, I, st);
         return;
     }
-    const float xmax2 = shard_xmax2(sh, d, st);
-    sh.nflag.ensure(sizeof(int), sh.device);
-    sh.flagged.ensure(sizeof(int) * (size_t)nq, sh.device);
-    HIPANN_CHECK(hipMemsetAsync(sh.nflag.p, 0, sizeof(int), st));
     {
         ScopedTiming t(ix.timer_merge, st);
         launch_ivf_rerank(sh.part_d.get<float>(), sh.part_i.get<int>(), sh.slot_off.get<int>(), np, nq, k, kout, metric,
                           xq, sh.codes, d, sh.ids, sh.n, 0, xmax2, D, I, sh.nflag.get<int>(), sh.flagged.get<int>(), st,
                           kSplit2Eps, half ? sh.half_rxmax : -1.f, half ? sh.hres.get<float>() : nullptr);
+    }
+    if (!host_fallback()) {
+        // flagged queries re-run on the device in the direct form (ivf_fallback_scan/_merge): no host
+        // readback, the next batch queues behind this one
+        if (!sh.fb_total.p) {
+            sh.fb_total.ensure(sizeof(unsigned long long), sh.device);
+            HIPANN_CHECK(hipMemsetAsync(sh.fb_total.p, 0, sizeof(unsigned long long), st));
+        }
+        sh.fpd.ensure(sizeof(float) * (size_t)nq * np * kout, sh.device);
+        sh.fpi.ensure(sizeof(long long) * (size_t)nq * np * kout, sh.device);
+        launch_ivf_fallback(sh.nflag.get<int>(), sh.flagged.get<int>(), nq, sh.coarse_i.get<int64_t>(), np, metric, xq,
+                            sh.codes, d, sh.list_off.get<int64_t>(), sh.list_len.get<int>(), nlist, sh.ids, 0, kout,
+                            sh.fpd.get<float>(), sh.fpi.get<long long>(), D, I, sh.fb_total.get<unsigned long long>(),
+                            st);
+        return;
     }
     int nf = 0;
     HIPANN_CHECK(hipMemcpyAsync(&nf, sh.nflag.p, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -813,7 +848,18 @@ int64_t hipann_ivf_rerank_fallbacks(void *h) {
     if (!h) return -1;
     auto *ix = static_cast<IndexBase *>(h);
     if (ix->kind != Kind::IVF) return -1;
-    return static_cast<IvfIndex *>(ix)->rerank_fallbacks;
+    auto *vx = static_cast<IvfIndex *>(ix);
+    std::lock_guard<std::mutex> lk(vx->mu);
+    int64_t t = vx->rerank_fallbacks;  // host re-runs (HIPANN_IVF_HOST_FALLBACK)
+    for (auto &sh : vx->shards) {       // + the device re-runs' running count
+        if (!sh->fb_total.p) continue;
+        DeviceGuard g(sh->device);
+        unsigned long long v = 0;
+        if (hipDeviceSynchronize() != hipSuccess) return -1;
+        if (hipMemcpy(&v, sh->fb_total.p, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+        t += (int64_t)v;
+    }
+    return t;
 }
 
 int hipann_ivf_get_form(void *h) {

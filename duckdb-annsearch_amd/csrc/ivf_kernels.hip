@@ -20,6 +20,7 @@
 #include "wave_topk.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <utility>
 
 namespace hipann {
@@ -96,16 +97,15 @@ __global__ void ivf_fill(const int64_t *__restrict__ probes, int64_t npairs, con
 // Single block: partial-list slots.  Pair i (= q·nprobe + p, probing list l) owns nch(l) consecutive
 // slots (one per row chunk of l; 0 if l is empty or not on this shard): slot_off = exclusive scan.
 // The slots of one query are therefore the contiguous range [slot_off[q·np], slot_off[(q+1)·np]).
-__global__ void __launch_bounds__(1024) ivf_slot_scan(const int64_t *__restrict__ probes, int64_t npairs,
-                                                      const int *__restrict__ list_len, int nlist,
-                                                      int *__restrict__ slot_off) {
+__device__ __forceinline__ void slot_scan_block(const int64_t *__restrict__ probes, int64_t npairs,
+                                                const int *__restrict__ list_len, int nlist, int *__restrict__ slot_off,
+                                                int *wsum) {
     // Per round, wave w owns the contiguous pairs base + [1024w, 1024w + 1024) as 16 chunks of 64: lane
     // i of chunk j is pair 64j + i, so the 16 probe loads and the 16 list-length gathers of a lane are
     // coalesced across the wave and all independent (two memory latencies per round); each chunk is
     // then scanned with shuffles and the 16 wave totals are combined in LDS.  (The first version gave
     // each thread 32 consecutive pairs — strided loads — and a 10-step block scan: 43 µs at 32K pairs.)
     constexpr int J = 16;  // (32 spilled at 1024 threads per block)
-    __shared__ int wsum[16];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int carry = 0;
     for (int64_t base = 0; base < npairs; base += 16 * 64 * J) {
@@ -150,6 +150,133 @@ __global__ void __launch_bounds__(1024) ivf_slot_scan(const int64_t *__restrict_
         __syncthreads();
     }
     if (threadIdx.x == 0) slot_off[npairs] = carry;
+}
+
+__global__ void __launch_bounds__(1024) ivf_slot_scan(const int64_t *__restrict__ probes, int64_t npairs,
+                                                      const int *__restrict__ list_len, int nlist,
+                                                      int *__restrict__ slot_off) {
+    __shared__ int wsum[16];
+    slot_scan_block(probes, npairs, list_len, nlist, slot_off, wsum);
+}
+
+// Query-major plan (default): three launches, two of them wide.
+//   ivf_count_q  — one wave per query: its pairs' list counts into ccnt (global atomics), the exclusive
+//                  prefix of their slot counts within the query into slot_off, the query's total to qtot
+//   ivf_plan_q   — one block: the list scans of ivf_plan (from ccnt, which it zeroes again for the next
+//                  batch), the exclusive scan of qtot (query slot bases), slot_off[npairs], and the batch's
+//                  other per-query state (the rerank's flag count, the scans' running bounds = +inf)
+//   ivf_fill_q   — one wave per query: slot_off += the query's base, bucket fill
+// (the list-major count / plan / slot scan / fill sequence kept a 1024-pair single block on one CU for
+// the slot scan: ≈ 55 µs of a 1024-query batch)
+__global__ void __launch_bounds__(256) ivf_count_q(const int64_t *__restrict__ probes, int64_t nq, int nprobe,
+                                                   const int *__restrict__ list_len, int nlist, int *__restrict__ ccnt,
+                                                   int *__restrict__ slot_off, int *__restrict__ qtot) {
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq) return;
+    const int lane = threadIdx.x & 63;
+    int carry = 0;
+    for (int p0 = 0; p0 < nprobe; p0 += 64) {
+        const int p = p0 + lane;
+        const int64_t i = q * nprobe + p;
+        const int64_t l = p < nprobe ? probes[i] : -1;
+        const bool ok = l >= 0 && l < nlist;
+        const int len = ok ? list_len[l] : 0;
+        if (len > 0) atomicAdd(ccnt + l, 1);
+        const int v = len > 0 ? ivf_nch(len) : 0;
+        int x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(x, o);
+            if (lane >= o) x += t;
+        }
+        if (p < nprobe) slot_off[i] = carry + x - v;
+        carry += __shfl(x, 63);
+    }
+    if (lane == 0) qtot[q] = carry;
+}
+
+__global__ void __launch_bounds__(1024) ivf_plan_q(int *__restrict__ ccnt, const int *__restrict__ list_len, int nlist,
+                                                   int group, int *__restrict__ cnt, int *__restrict__ bucket_off,
+                                                   int *__restrict__ item_off, int *__restrict__ cursor,
+                                                   int *__restrict__ qtot, int64_t nq, int64_t npairs,
+                                                   int *__restrict__ slot_off, int *__restrict__ nflag_reset,
+                                                   unsigned *__restrict__ qbound) {
+    __shared__ int sb[1024], si[1024];
+    __shared__ int carry_b, carry_i;
+    const int tid = threadIdx.x;
+    if (tid == 0) { carry_b = 0; carry_i = 0; }
+    if (nflag_reset && tid == 0) *nflag_reset = 0;
+    if (qbound)
+        for (int64_t q = tid; q < nq; q += 1024) qbound[q] = 0xff800000u;
+    __syncthreads();
+    for (int base = 0; base < nlist; base += 1024) {
+        const int l = base + tid;
+        const int c = l < nlist ? ccnt[l] : 0;
+        const int items = l < nlist ? ((c + group - 1) / group) * ivf_nch(list_len[l]) : 0;
+        sb[tid] = c;
+        si[tid] = items;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
+            int vb = 0, vi = 0;
+            if (tid >= o) { vb = sb[tid - o]; vi = si[tid - o]; }
+            __syncthreads();
+            sb[tid] += vb;
+            si[tid] += vi;
+            __syncthreads();
+        }
+        if (l < nlist) {
+            cnt[l] = c;
+            ccnt[l] = 0;
+            bucket_off[l] = carry_b + sb[tid] - c;
+            item_off[l] = carry_i + si[tid] - items;
+            cursor[l] = 0;
+        }
+        __syncthreads();
+        if (tid == 1023) { carry_b += sb[1023]; carry_i += si[1023]; }
+        __syncthreads();
+    }
+    if (tid == 0) { bucket_off[nlist] = carry_b; item_off[nlist] = carry_i; }
+    // query slot bases: exclusive scan of qtot, in place
+    __syncthreads();
+    if (tid == 0) carry_b = 0;
+    __syncthreads();
+    for (int64_t base = 0; base < nq; base += 1024) {
+        const int64_t q = base + tid;
+        const int t = q < nq ? qtot[q] : 0;
+        sb[tid] = t;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {
+            int v = 0;
+            if (tid >= o) v = sb[tid - o];
+            __syncthreads();
+            sb[tid] += v;
+            __syncthreads();
+        }
+        if (q < nq) qtot[q] = carry_b + sb[tid] - t;
+        __syncthreads();
+        if (tid == 1023) carry_b += sb[1023];
+        __syncthreads();
+    }
+    if (tid == 0) slot_off[npairs] = carry_b;
+}
+
+__global__ void __launch_bounds__(256) ivf_fill_q(const int64_t *__restrict__ probes, int64_t nq, int nprobe,
+                                                  const int *__restrict__ list_len, int nlist,
+                                                  const int *__restrict__ qbase, const int *__restrict__ bucket_off,
+                                                  int *__restrict__ cursor, int *__restrict__ bucket,
+                                                  int *__restrict__ slot_off) {
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq) return;
+    const int lane = threadIdx.x & 63;
+    const int b = qbase[q];
+    for (int p = lane; p < nprobe; p += 64) {
+        const int64_t i = q * nprobe + p;
+        slot_off[i] += b;
+        const int64_t l = probes[i];
+        if (l < 0 || l >= nlist || list_len[l] <= 0) continue;
+        const int pos = atomicAdd(cursor + l, 1);
+        bucket[bucket_off[l] + pos] = (int)i;
+    }
 }
 
 // Row staging: IVF_TR rows × IVF_BK dims = IVF_TR·IVF_BK/4 float4, IVF_SP per thread.
@@ -889,8 +1016,24 @@ void launch_ivf_scan_bigk(const float *Q, int d, int metric, const float *codes,
 // ---------------------------------------------------------------------------------------------
 void launch_ivf_plan(const int64_t *probes, int64_t nq, int nprobe, const int *list_len, int nlist, int group,
                      int *cnt, int *bucket_off, int *item_off, int *cursor, int *bucket, int *slot_off,
-                     hipStream_t st) {
+                     hipStream_t st, int *nflag_reset, unsigned *qbound, int *ccnt, int *qtot) {
     const int64_t npairs = nq * nprobe;
+    static const bool split = [] { const char *e = std::getenv("HIPANN_IVF_PLAN_SPLIT"); return e && std::atoi(e); }();
+    if (!split && ccnt && qtot) {
+        const unsigned gq = (unsigned)std::max<int64_t>(1, ceil_div(nq, (int64_t)4));
+        if (nq > 0)
+            hipLaunchKernelGGL(ivf_count_q, dim3(gq), dim3(256), 0, st, probes, nq, nprobe, list_len, nlist, ccnt,
+                               slot_off, qtot);
+        hipLaunchKernelGGL(ivf_plan_q, dim3(1), dim3(1024), 0, st, ccnt, list_len, nlist, group, cnt, bucket_off,
+                           item_off, cursor, qtot, nq, npairs, slot_off, nflag_reset, qbound);
+        if (nq > 0)
+            hipLaunchKernelGGL(ivf_fill_q, dim3(gq), dim3(256), 0, st, probes, nq, nprobe, list_len, nlist, qtot,
+                               bucket_off, cursor, bucket, slot_off);
+        HIPANN_CHECK(hipGetLastError());
+        return;
+    }
+    if (nflag_reset) HIPANN_CHECK(hipMemsetAsync(nflag_reset, 0, sizeof(int), st));
+    if (qbound) HIPANN_CHECK(hipMemsetD32Async((hipDeviceptr_t)qbound, 0xff800000, (size_t)nq, st));
     HIPANN_CHECK(hipMemsetAsync(cnt, 0, sizeof(int) * (size_t)nlist, st));
     if (npairs > 0)
         hipLaunchKernelGGL(ivf_count, dim3((unsigned)ceil_div(npairs, 256)), dim3(256), 0, st, probes, npairs, list_len,
@@ -1195,6 +1338,135 @@ __global__ void __launch_bounds__(256) ivf_scatter_results(const float *__restri
     const int j = (int)(t / kout), e = (int)(t - (int64_t)j * kout);
     D[(int64_t)idx[j] * kout + e] = Df[t];
     I[(int64_t)idx[j] * kout + e] = If[t];
+}
+
+// ---------------------------------------------------------------------------------------------
+// Device-side re-run of the queries ivf_rerank_topk flagged (no host round trip per batch).
+// ivf_fallback_scan: work item (f, p), f < *nflag — query flagged[f] against its p-th probed list; the
+// block's 4 waves take 64-row groups of the list, each row's distance in the rerank's direct form (the
+// same lane-strided fmaf chain and xor butterfly: the rerank's values bit for bit), a (distance,
+// label) list of kout per wave, merged through LDS into the item's partial list fpd/fpi[f][p][kout].
+// ivf_fallback_merge: per flagged query, the (distance, label) top-kout of its nprobe partials into
+// D/I (+inf distances and empty slots are pads, as FAISS's heaps leave them); adds the batch's flag
+// count to the shard's running total.  Both grids are persistent loops bounded by *nflag, so a batch
+// with nothing flagged costs two near-empty launches.
+// ---------------------------------------------------------------------------------------------
+template <bool IP>
+__global__ void __launch_bounds__(256)
+ivf_fallback_scan(const int *__restrict__ nflag, const int *__restrict__ flagged, const int64_t *__restrict__ probes,
+                  int nprobe, const float *__restrict__ Q, const float *__restrict__ codes, int d,
+                  const int64_t *__restrict__ list_off, const int *__restrict__ list_len, int nlist,
+                  const int64_t *__restrict__ ids, int64_t label_offset, int kout, float *__restrict__ fpd,
+                  long long *__restrict__ fpi) {
+    __shared__ float sd[4 * 64];
+    __shared__ long long si[4 * 64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t items = (int64_t)(*nflag) * nprobe;
+    for (int64_t w = blockIdx.x; w < items; w += gridDim.x) {
+        const int64_t f = w / nprobe, p = w - f * nprobe;
+        const int64_t q = flagged[f];
+        const int64_t l = probes[q * nprobe + p];
+        const float *qp = Q + q * (int64_t)d;
+        WaveList<1, long long> L;
+        L.init();
+        if (l >= 0 && l < nlist && list_len[l] > 0) {
+            const int64_t r0 = list_off[l], len = list_len[l];
+            for (int64_t g = (int64_t)wv * 64; g < len; g += 256) {
+                const int nr = (int)(len - g < 64 ? len - g : 64);
+                float mine = __builtin_inff();
+                for (int r = 0; r < nr; r += 4) {
+                    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+                    const float *xr[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) xr[u] = codes + (r0 + g + (r + u < nr ? r + u : nr - 1)) * d;
+                    for (int e = lane; e < d; e += 64) {
+                        const float qv = qp[e];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const float xv = xr[u][e];
+                            if (IP) acc[u] = fmaf(qv, xv, acc[u]);
+                            else {
+                                const float t = qv - xv;
+                                acc[u] = fmaf(t, t, acc[u]);
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        float a = acc[u];
+#pragma unroll
+                        for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+                        if (lane == r + u) mine = IP ? -a : a;
+                    }
+                }
+                const int64_t row = r0 + g + lane;
+                const bool ok = lane < nr && !(mine == __builtin_inff());
+                const long long lab = ok ? (long long)(ids ? ids[row] : label_offset + row) : IdTraits<long long>::pad();
+                L.offer(ok ? mine : __builtin_inff(), lab, kout - 1);
+            }
+        }
+        sd[wv * 64 + lane] = L.d[0];
+        si[wv * 64 + lane] = L.id[0];
+        __syncthreads();
+        if (wv == 0) {
+            L.init();
+#pragma unroll
+            for (int w2 = 0; w2 < 4; ++w2) L.offer(sd[w2 * 64 + lane], si[w2 * 64 + lane], kout - 1);
+            if (lane < kout) {
+                fpd[w * kout + lane] = L.d[0];
+                fpi[w * kout + lane] = L.id[0];
+            }
+        }
+        __syncthreads();
+    }
+}
+
+template <bool IP>
+__global__ void __launch_bounds__(256)
+ivf_fallback_merge(const int *__restrict__ nflag, const int *__restrict__ flagged, int nprobe, int kout,
+                   const float *__restrict__ fpd, const long long *__restrict__ fpi, float *__restrict__ D,
+                   int64_t *__restrict__ I, unsigned long long *__restrict__ total) {
+    const int nf = *nflag;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && nf > 0) atomicAdd(total, (unsigned long long)nf);
+    const int lane = threadIdx.x & 63;
+    const float pad_d = IP ? -__builtin_inff() : __builtin_inff();
+    for (int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); f < nf; f += (int64_t)gridDim.x * 4) {
+        WaveList<1, long long> L;
+        L.init();
+        const int64_t n = (int64_t)nprobe * kout;
+        for (int64_t c = lane; c - lane < n; c += 64) {
+            const bool v = c < n;
+            L.offer(v ? fpd[f * n + c] : __builtin_inff(), v ? fpi[f * n + c] : IdTraits<long long>::pad(), kout - 1);
+        }
+        const int64_t q = flagged[f];
+        if (lane < kout) {
+            const bool pad = L.id[0] == IdTraits<long long>::pad() || L.d[0] == __builtin_inff();
+            D[q * kout + lane] = pad ? pad_d : (IP ? -L.d[0] : L.d[0]);
+            I[q * kout + lane] = pad ? -1 : (int64_t)L.id[0];
+        }
+    }
+}
+
+void launch_ivf_fallback(const int *nflag, const int *flagged, int64_t nq, const int64_t *probes, int nprobe, int metric,
+                         const float *Q, const float *codes, int d, const int64_t *list_off, const int *list_len,
+                         int nlist, const int64_t *ids, int64_t label_offset, int kout, float *fpd, long long *fpi,
+                         float *D, int64_t *I, unsigned long long *total, hipStream_t st) {
+    if (nq <= 0) return;
+    HIPANN_REQUIRE(kout >= 1 && kout <= 64, "ivf fallback: kout out of range");
+    const unsigned gs = (unsigned)std::min<int64_t>(512, nq * nprobe);
+    const unsigned gm = (unsigned)std::min<int64_t>(256, ceil_div(nq, (int64_t)4));
+    if (metric == kIP) {
+        hipLaunchKernelGGL(ivf_fallback_scan<true>, dim3(gs), dim3(256), 0, st, nflag, flagged, probes, nprobe, Q, codes,
+                           d, list_off, list_len, nlist, ids, label_offset, kout, fpd, fpi);
+        hipLaunchKernelGGL(ivf_fallback_merge<true>, dim3(gm), dim3(256), 0, st, nflag, flagged, nprobe, kout, fpd, fpi,
+                           D, I, total);
+    } else {
+        hipLaunchKernelGGL(ivf_fallback_scan<false>, dim3(gs), dim3(256), 0, st, nflag, flagged, probes, nprobe, Q,
+                           codes, d, list_off, list_len, nlist, ids, label_offset, kout, fpd, fpi);
+        hipLaunchKernelGGL(ivf_fallback_merge<false>, dim3(gm), dim3(256), 0, st, nflag, flagged, nprobe, kout, fpd,
+                           fpi, D, I, total);
+    }
+    HIPANN_CHECK(hipGetLastError());
 }
 
 #ifndef HIPANN_RR_WIDE

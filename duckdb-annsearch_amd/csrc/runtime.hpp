@@ -132,6 +132,8 @@ struct FlatShard {
     hipStream_t stream = nullptr;
     // scratch
     DevBuf q, qn, part_d, part_i, out_d, out_i;
+    const float *qn_of = nullptr;  // sh.qn holds ‖q‖² of these queries (the last search's, nq of them)
+    int64_t qn_nq = 0;
     DevBuf keys, run_d, run_i, run2_d, run2_i;  // k > 64 path
     DevBuf qsplit;                              // split-bf16 form: the batch's queries as bf16 terms
     // kFlatSplit2Exact: max row ‖x‖² (the rerank's error bound; −1 until computed / after an add), the
@@ -199,6 +201,9 @@ struct IvfShard {
     // queries of the last batch and the re-run's buffers
     float xmax2 = -1.f;
     DevBuf nflag, flagged, fq, fD, fI, coarse_save, tmpnorm;
+    DevBuf ccnt, qtot;             // query-major plan: per-list running counts (kept zero between batches), per-query slot totals
+    DevBuf fpd, fpi;               // device fallback: per (flagged query, probe) partial lists
+    DevBuf fb_total;               // u64 running count of flagged queries (device side)
     // MFMA scan copy of the codes, built at the first search that uses it: per list, 32-row passes of
     // [16-dim step][2 row tiles][64 lanes][float4] (ivf_mfma.hip), zero-padded rows / dims
     std::vector<int64_t> h_off;    // host copy of list_off
@@ -258,13 +263,16 @@ void launch_flat_scan_keys(const float *Q, int nq, const float *X, int64_t N, in
                            int64_t ldk, hipStream_t st);
 void launch_rows_topk(const float *keys, int64_t ldk, int64_t ncols, int64_t nq, int64_t seg_len, int nseg, int k,
                       int id0, float *pd, int *pi, hipStream_t st);
+bool launch_rows_select_out(const float *keys, int64_t ldk, int64_t ncols, int64_t nq, int k, int kout,
+                            int64_t label_offset, float out_sign, float *D, int64_t *I, hipStream_t st);
 void launch_merge_raw(const float *pd, const int *pi, int nparts, int64_t nq, int k, float *od, int *oi,
                       hipStream_t st);
 void launch_flat_scan_topk(const float *Q, int nq, const float *X, int64_t N, int d, int metric, int k, int nwaves,
                            int64_t rows_per_wave, float *pd, int *pi, hipStream_t st);
 void launch_ivf_plan(const int64_t *probes, int64_t nq, int nprobe, const int *list_len, int nlist, int group,
                      int *cnt, int *bucket_off, int *item_off, int *cursor, int *bucket, int *slot_off,
-                     hipStream_t st);
+                     hipStream_t st, int *nflag_reset = nullptr, unsigned *qbound = nullptr, int *ccnt = nullptr,
+                     int *qtot = nullptr);
 int64_t ivf_max_items(int64_t nq, int nprobe, int nlist, int max_nch, int64_t nrows, int group);
 int ivf_mfma_bf_group(int d, int np);
 bool ivf_mfma_bf_supported(const float *Q, int d, const float *codes, int k, int np);
@@ -298,6 +306,10 @@ void launch_flat_bf16_topk(const float *Q, const float *qn, int64_t nq, void *qi
                            const float *seed, bool image_ready, hipStream_t st);
 void launch_flat_bf16_seed(const float *pd, int nsplit, int64_t nq, int k, float *seed, hipStream_t st);
 void launch_ivf_max_norm(const float *xn, int64_t n, unsigned *out, hipStream_t st);
+void launch_ivf_fallback(const int *nflag, const int *flagged, int64_t nq, const int64_t *probes, int nprobe, int metric,
+                         const float *Q, const float *codes, int d, const int64_t *list_off, const int *list_len,
+                         int nlist, const int64_t *ids, int64_t label_offset, int kout, float *fpd, long long *fpi,
+                         float *D, int64_t *I, unsigned long long *total, hipStream_t st);
 void launch_ivf_gather_queries(const float *Q, const int *idx, int nf, int d, float *out, hipStream_t st);
 void launch_ivf_scatter_results(const float *Df, const int64_t *If, const int *idx, int nf, int kout, float *D,
                                 int64_t *I, hipStream_t st);
