@@ -302,3 +302,23 @@ def test_flat_exact_form_matches_fp32_form_at_scale(gpu, form):
     scale = np.sum(xq.astype(np.float64) ** 2, 1)[:, None] + np.max(np.sum(xb.astype(np.float64) ** 2, 1))
     assert (np.abs(D1 - D0) <= 1e-5 * scale).all()
     assert (I1 == I0).mean() >= 0.995
+
+
+@pytest.mark.parametrize("n", [200, 1000, 3000])
+@pytest.mark.parametrize("metric", [0, 1])
+@pytest.mark.parametrize("k", [1, 7, 32, 64])
+def test_flat_small_table_select_exact_ties(gpu, oracle, n, metric, k):
+    """Small tables at nq >= 20 (the IVF coarse quantizer's shape): GEMM keys + one select per key row
+    (the bitwise select for <= 1024 columns, the list path beyond).  Small-integer data makes every
+    product exact, so keys tie exactly and the (distance, label) order alone decides: ids and distances
+    must equal the oracle's bit for bit, including an all-zero query (IP keys +-0 for every row)."""
+    rng = np.random.default_rng(n * 10 + k + metric)
+    d = 24
+    xb = rng.integers(-2, 3, size=(n, d)).astype(np.float32)
+    xq = rng.integers(-2, 3, size=(40, d)).astype(np.float32)
+    xq[5] = 0.0
+    ix = gpu.HipIndexFlat(d, metric, xb)
+    D, I = ix.search(xq, k)
+    Do, Io = oracle.flat_search(xb, xq, k, metric)
+    assert np.array_equal(I, Io)
+    assert np.array_equal(D, Do)

@@ -401,3 +401,27 @@ def test_ivf_half_form_query_out_of_range(gpu, oracle):
     assert ix.rerank_fallbacks() - before >= 1
     Do, Io, Po = oracle.ivf_search(cen, off, ids, codes, xq, 10, 6, 1)
     check_topk_parity(xb, xq, D, I, Do, Io, 1)
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+def test_ivf_device_fallback_labels_and_batch(gpu, oracle, metric):
+    """The device-side re-run of flagged queries (ivf_fallback_scan/_merge): every vector stored 20 times
+    under scattered int64 labels, so most of a 300-query batch is flagged; the re-run's (distance, label)
+    lists follow the oracle (labels, not row numbers, break the exact ties), and the flag count reaches
+    rerank_fallbacks() without a host readback per batch."""
+    base, xq = faiss_metal_case(500, 300, 48)
+    xb = np.ascontiguousarray(np.repeat(base, 20, axis=0))
+    cen = np.ascontiguousarray(xb[::500][:20])
+    off, ids, codes = build_ivf_lists(xb, cen, metric)
+    labels = np.ascontiguousarray((ids * 7919) % 100003 + 5, dtype=np.int64)
+    ix = gpu.HipIndexIVFFlat(cen, off, labels, codes, 5, metric)
+    before = ix.rerank_fallbacks()
+    D, I = ix.search(xq, 10)
+    assert ix.rerank_fallbacks() - before >= 100
+    Do, Io, Po = oracle.ivf_search(cen, off, labels, codes, xq, 10, 5, metric)
+    assert np.array_equal(ix.last_probes(len(xq)), Po)
+    by_label = np.zeros((int(labels.max()) + 1, xb.shape[1]), np.float32)  # the parity rule indexes rows by label
+    by_label[labels] = codes
+    check_topk_parity(by_label, xq, D, I, Do, Io, metric)
+    v = I >= 0
+    assert np.allclose(D[v], Do[v], rtol=2e-6, atol=1e-6)
