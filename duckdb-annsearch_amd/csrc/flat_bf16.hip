@@ -33,6 +33,7 @@
 
 #include <cstdlib>
 #include <type_traits>
+#include <utility>
 
 namespace hipann {
 
@@ -155,7 +156,7 @@ __device__ __forceinline__ void b16_wait_vm() {
 // straight from the L2-resident query image into a 3-deep register ring instead of through LDS, so the
 // LDS-DMA fill carries only the shared database tile: 16 KB per 32-dim chunk instead of 32 KB (the fill
 // rate, ≈6 TB/s chip-wide, is what bounds this kernel at 128 FLOP/B).
-template <bool L2M, int W, bool RA>
+template <bool L2M, int W, bool RA, int NB = 3>
 __global__ void __launch_bounds__(64 * W, 1)
 flat_bf16_topk(const b16_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm, int64_t nq,
                const b16_u32x4 *__restrict__ Xt,
@@ -165,7 +166,9 @@ flat_bf16_topk(const b16_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm
     constexpr int QM = 32 * W;
     constexpr int AU = QM * 4, BU = B16_TN * 4;  // 16-B units per chunk image
     constexpr int SU = RA ? BU : AU + BU;        // units per LDS stage
-    constexpr int NB = 3;                        // stages: chunk g+2 in flight while chunk g is read
+    // NB stages: chunks g+1 .. g+NB−1 in flight while chunk g is read (NB − 1 chunk times to cover the
+    // LDS-DMA issue → landed latency, ≈1.1 µs)
+    static_assert(NB >= 3 && NB <= 6, "stages");
     constexpr int IA = AU / 64 / W, IB = BU / 64 / W;  // global_load_lds (1 KiB each) per wave per chunk
     constexpr int NI = RA ? IB + 2 : IA + IB;   // vector-memory ops per wave per chunk
     static_assert(IA * 64 * W == AU && IB * 64 * W == BU, "chunk images must split evenly over the waves");
@@ -246,14 +249,14 @@ flat_bf16_topk(const b16_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm
         for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
     __syncthreads();  // list initialisation
     using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, 1>;
-    using I2 = std::integral_constant<int, 2>;
     if (RA && G > 0) {  // the ring starts full (past the end: the last chunk again)
-        issue(0, 0, I0{});
-        issue(G > 1 ? 1 : 0, 1, I1{});
+        [&]<int... P>(std::integer_sequence<int, P...>) {
+            (issue(P < G ? P : G - 1, P, std::integral_constant<int, P>{}), ...);
+        }(std::make_integer_sequence<int, NB - 1>{});
     } else {
-        if (G > 0) issue(0, 0, I0{});
-        if (G > 1) issue(1, 1, I1{});
+        [&]<int... P>(std::integer_sequence<int, P...>) {
+            ((P < G ? issue(P, P, std::integral_constant<int, P>{}) : void()), ...);
+        }(std::make_integer_sequence<int, NB - 1>{});
     }
 
     int kc = 0, stage = 0;
@@ -266,13 +269,15 @@ flat_bf16_topk(const b16_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm
         // still reads stage (g+2) % NB = (g−1) % NB
         // RA: the issue is unconditional (past the end it re-reads the last chunk into a free stage), so every
         // iteration has the same count of vector-memory ops and the compiler's own waits stay exact
-        if (RA || g + 1 < G) b16_wait_vm<NI>();
+        if (RA) b16_wait_vm<NI * (NB - 2)>();
+        else if (g + NB - 2 < G) b16_wait_vm<NI * (NB - 2)>();
         else b16_wait_vm<0>();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        if (RA) issue(g + 2 < G ? g + 2 : G - 1, stage == 0 ? 2 : stage - 1, std::integral_constant<int, (SL + 2) % NB>{});
-        else if (g + 2 < G) issue(g + 2, stage == 0 ? 2 : stage - 1, std::integral_constant<int, (SL + 2) % NB>{});
+        const int st_next = stage == 0 ? NB - 1 : stage - 1;  // (stage + NB − 1) % NB: chunk g−1's, now free
+        if (RA) issue(g + NB - 1 < G ? g + NB - 1 : G - 1, st_next, std::integral_constant<int, (SL + NB - 1) % NB>{});
+        else if (g + NB - 1 < G) issue(g + NB - 1, st_next, std::integral_constant<int, (SL + NB - 1) % NB>{});
         const b16_u32x4 *Ab = smem_b16 + stage * SU;
         const b16_u32x4 *Bb = Ab + (RA ? 0 : AU);
 #pragma unroll
@@ -321,9 +326,9 @@ flat_bf16_topk(const b16_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm
     };
     if constexpr (RA) {
         for (int64_t g = 0; g < G; g += NB) {
-            body(g, I0{});
-            if (g + 1 < G) body(g + 1, I1{});
-            if (g + 2 < G) body(g + 2, I2{});
+            [&]<int... P>(std::integer_sequence<int, P...>) {
+                ((g + P < G ? body(g + P, std::integral_constant<int, P>{}) : void()), ...);
+            }(std::make_integer_sequence<int, NB>{});
         }
         b16_wait_vm<0>();  // no LDS-DMA copy may land after the block's LDS is handed to the next block
     } else {
@@ -364,6 +369,7 @@ __global__ void __launch_bounds__(256) flat_bf16_seed(const float *__restrict__ 
 }
 
 // ------------------------------------------------------------------------------------------------
+constexpr int kB16StagesDefault = 4;  // 10M x 768: 19.16 (3) / 18.68 (4) / 19.06 (5) ms
 int flat_bf16_waves(int64_t nq) { return nq >= 256 ? 8 : nq >= 128 ? 4 : 2; }
 int flat_bf16_tile_rows() { return B16_TN; }
 
@@ -410,12 +416,24 @@ void launch_flat_bf16_topk(const float *Q, const float *qn, int64_t nq, void *qi
                            pi, seed);
     };
     static const bool ra = [] { const char *e = std::getenv("HIPANN_B16_RA"); return !e || std::atoi(e); }();
-    const size_t smem_ra = (size_t)3 * (B16_TN * 4) * 16 + (size_t)QM * k * 8;
-    if (ra && W == 8) {
-        if (metric == kL2) hipLaunchKernelGGL((flat_bf16_topk<true, 8, true>), grid, block, smem_ra, st, qa, qn, nq, xa, xn, N,
-                                              nk, k, nqt, nsplit, tiles_per_split, pd, pi, seed);
-        else hipLaunchKernelGGL((flat_bf16_topk<false, 8, true>), grid, block, smem_ra, st, qa, qn, nq, xa, xn, N, nk, k,
-                                nqt, nsplit, tiles_per_split, pd, pi, seed);
+    // RA stages (HIPANN_B16_NB = 3..5, A/B): LDS-DMA chunks in flight = NB − 1
+    static const int nb = [] { const char *e = std::getenv("HIPANN_B16_NB"); const int v = e ? std::atoi(e) : 0;
+                               return v >= 3 && v <= 5 ? v : kB16StagesDefault; }();
+    const size_t smem_ra = (size_t)nb * (B16_TN * 4) * 16 + (size_t)QM * k * 8;
+    if (ra && W == 8 && smem_ra <= 160 * 1024) {
+        auto go_ra = [&](auto kern) {
+            hipLaunchKernelGGL(kern, grid, block, smem_ra, st, qa, qn, nq, xa, xn, N, nk, k, nqt, nsplit, tiles_per_split,
+                               pd, pi, seed);
+        };
+        if (metric == kL2) {
+            if (nb == 3) go_ra(flat_bf16_topk<true, 8, true, 3>);
+            else if (nb == 4) go_ra(flat_bf16_topk<true, 8, true, 4>);
+            else go_ra(flat_bf16_topk<true, 8, true, 5>);
+        } else {
+            if (nb == 3) go_ra(flat_bf16_topk<false, 8, true, 3>);
+            else if (nb == 4) go_ra(flat_bf16_topk<false, 8, true, 4>);
+            else go_ra(flat_bf16_topk<false, 8, true, 5>);
+        }
     } else if (metric == kL2) {
         if (W == 8) go(flat_bf16_topk<true, 8, false>);
         else if (W == 4) go(flat_bf16_topk<true, 4, false>);

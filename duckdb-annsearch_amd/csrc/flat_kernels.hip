@@ -1209,13 +1209,17 @@ flat_keys_small(const float *__restrict__ Q, const float *__restrict__ qnorm, in
             small_stage_load<VEC4>(Q, q0, nq, d, (kc + 1) * GBK, sa);
             small_stage_load<VEC4>(X, x0, N, d, (kc + 1) * GBK, sb);
         }
+        // the chunk's 8 fragment reads first, then its 16 MFMAs (one LDS wait per chunk; same k order)
+        f32x4 a4[4], b4[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const f32x4 a4 = *reinterpret_cast<const f32x4 *>(Ab + (32 * wr + l31) * GLD + 16 * h + 4 * u);
-            const f32x4 b4 = *reinterpret_cast<const f32x4 *>(Bb + (32 * wc + l31) * GLD + 16 * h + 4 * u);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[e], b4[e], acc, 0, 0, 0);
+            a4[u] = *reinterpret_cast<const f32x4 *>(Ab + (32 * wr + l31) * GLD + 16 * h + 4 * u);
+            b4[u] = *reinterpret_cast<const f32x4 *>(Bb + (32 * wc + l31) * GLD + 16 * h + 4 * u);
         }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[u][e], b4[u][e], acc, 0, 0, 0);
         if (kc + 1 < nk) {
             small_stage_store(As[(kc + 1) & 1], sa);
             small_stage_store(Bs[(kc + 1) & 1], sb);
@@ -1304,7 +1308,9 @@ void launch_flat_scan_keys(const float *Q, int nq, const float *X, int64_t N, in
                            int64_t ldk, hipStream_t st) {
     const bool vec4 = (d % 4 == 0) && ((uintptr_t)X % 16 == 0);
     const size_t smem = scan_smem_bytes(nq, d);
-    int64_t nwaves = std::min<int64_t>(8192, std::max<int64_t>(1, ceil_div(N, 512)));
+    // ≥ 512 rows per wave on large tables, small ones spread over waves of ≥ 16 rows (as the fused scan)
+    int64_t nwaves = std::min<int64_t>(8192, std::max<int64_t>(std::min<int64_t>(256, ceil_div(N, 16)),
+                                                               ceil_div(N, 512)));
     const int64_t rpw = ceil_div(N, nwaves);
     nwaves = ceil_div(N, rpw);
     dim3 grid((unsigned)ceil_div(nwaves, 4));

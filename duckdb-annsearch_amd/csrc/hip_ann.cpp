@@ -244,7 +244,11 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
     // Large k, or a small table (an IVF coarse quantizer: nq x nlist keys are a few MB): the GEMM writes
     // the key matrix and one wave per query selects — the fused epilogue would spend its time
     // filling empty lists, one query tile per CU.
-    if (k > kFusedMaxK || (nq >= kBlasThreshold && sh.n <= kSmallTable)) {
+    // nq < 20 on a table of ≤ 1024 rows (the coarse quantizer of the extension's nq = 1 call): direct-form
+    // keys over ≥ 16-row waves + one bitwise select per query row (the fused scan's nparts × k partial
+    // lists took one wave 47 µs to merge at nlist 1024)
+    if (k > kFusedMaxK || (nq >= kBlasThreshold && sh.n <= kSmallTable) ||
+        (nq < kBlasThreshold && sh.n <= 1024 && kout <= 64 && scan_smem_bytes((int)nq, d) <= 64 * 1024)) {
         const float *qn = nullptr;
         if (nq >= kBlasThreshold && metric == kL2) {
             sh.qn.ensure((size_t)nq * sizeof(float), sh.device);
