@@ -17,6 +17,7 @@
 #include "wave_topk.hpp"
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 namespace hipann {
@@ -1194,21 +1195,29 @@ flat_keys_small(const float *__restrict__ Q, const float *__restrict__ qnorm, in
     const int wr = wave >> 1, wc = wave & 1;
     const int l31 = lane & 31, h = lane >> 5;
     const int nk = (d + GBK - 1) / GBK;
-    float4 sa[2], sb[2];
-    small_stage_load<VEC4>(Q, q0, nq, d, 0, sa);
-    small_stage_load<VEC4>(X, x0, N, d, 0, sb);
-    small_stage_store(As[0], sa);
-    small_stage_store(Bs[0], sb);
+    // chunks kc+1 and kc+2 in flight in two register sets (set = chunk & 1) while chunk kc is multiplied:
+    // the Q / centroid rows come from the Infinity Cache, ≈1 µs away — one chunk of lookahead (≈0.4 µs of
+    // MFMAs) left every chunk waiting on its loads (32 µs for 1024 × 1024 × 768)
+    float4 sa[2][2], sb[2][2];
+    small_stage_load<VEC4>(Q, q0, nq, d, 0, sa[0]);
+    small_stage_load<VEC4>(X, x0, N, d, 0, sb[0]);
+    small_stage_store(As[0], sa[0]);
+    small_stage_store(Bs[0], sb[0]);
+    if (nk > 1) {
+        small_stage_load<VEC4>(Q, q0, nq, d, GBK, sa[1]);
+        small_stage_load<VEC4>(X, x0, N, d, GBK, sb[1]);
+    }
+    if (nk > 2) {
+        small_stage_load<VEC4>(Q, q0, nq, d, 2 * GBK, sa[0]);
+        small_stage_load<VEC4>(X, x0, N, d, 2 * GBK, sb[0]);
+    }
     __syncthreads();
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    for (int kc = 0; kc < nk; ++kc) {
-        const float *Ab = As[kc & 1], *Bb = Bs[kc & 1];
-        if (kc + 1 < nk) {
-            small_stage_load<VEC4>(Q, q0, nq, d, (kc + 1) * GBK, sa);
-            small_stage_load<VEC4>(X, x0, N, d, (kc + 1) * GBK, sb);
-        }
+    auto step = [&](int kc, auto par_c) {
+        constexpr int P = decltype(par_c)::value;  // kc & 1
+        const float *Ab = As[P], *Bb = Bs[P];
         // the chunk's 8 fragment reads first, then its 16 MFMAs (one LDS wait per chunk; same k order)
         f32x4 a4[4], b4[4];
 #pragma unroll
@@ -1220,11 +1229,19 @@ flat_keys_small(const float *__restrict__ Q, const float *__restrict__ qnorm, in
         for (int u = 0; u < 4; ++u)
 #pragma unroll
             for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[u][e], b4[u][e], acc, 0, 0, 0);
-        if (kc + 1 < nk) {
-            small_stage_store(As[(kc + 1) & 1], sa);
-            small_stage_store(Bs[(kc + 1) & 1], sb);
+        if (kc + 1 < nk) {  // chunk kc+1 (register set 1−P) → LDS buffer 1−P, last read at kc−1
+            small_stage_store(As[1 - P], sa[1 - P]);
+            small_stage_store(Bs[1 - P], sb[1 - P]);
+            if (kc + 3 < nk) {
+                small_stage_load<VEC4>(Q, q0, nq, d, (kc + 3) * GBK, sa[1 - P]);
+                small_stage_load<VEC4>(X, x0, N, d, (kc + 3) * GBK, sb[1 - P]);
+            }
         }
         __syncthreads();
+    };
+    for (int kc = 0; kc < nk; kc += 2) {
+        step(kc, std::integral_constant<int, 0>{});
+        if (kc + 1 < nk) step(kc + 1, std::integral_constant<int, 1>{});
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
