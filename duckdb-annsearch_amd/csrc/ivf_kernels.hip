@@ -1166,6 +1166,100 @@ __device__ __forceinline__ void rerank_rows4(const float *__restrict__ qp, const
     }
 }
 
+// HIPANN_RERANK_LISTS=1: the rerank merges with per-wave lists only (A/B of rerank_block_select).
+__device__ __forceinline__ bool rerank_lists() {
+#ifdef HIPANN_RERANK_LISTS
+    return true;
+#else
+    return false;
+#endif
+}
+
+// The k best scan keys of a query's ≤ 64·WV·J candidates (pd/pi: keys and row ids, contiguous) by one
+// bitwise select over the whole block: candidate c = (j·WV + wave)·64 + lane sits in register j as an
+// order-preserving u32 (pads, rows out of range, +inf and NaN keys excluded — the entries the list merge
+// never admits); 32 steps find the k-th smallest value T (per step J ballots + popcounts per wave and
+// one barrier for the block sum), the keys < T and then the first keys == T (in (wave, j, lane) order)
+// are compacted into LDS, and wave 0 sorts them into L (lanes < k: ascending (key, row); pads past the
+// candidates).  A tie at T may pick different rows than the (key, row) lists would — harmless: every
+// row left out still has scan key ≥ K_k, which is all the bound check assumes.
+template <int WV, int J>
+__device__ __forceinline__ void rerank_block_select(const float *__restrict__ pd, const int *__restrict__ pi,
+                                                    int64_t total, int k, int64_t nrows, float *sd, int *si,
+                                                    int (*scnt)[WV], WaveList<1, int> &L) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    float v[J];
+    int r[J];
+    unsigned u[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int64_t c = ((int64_t)j * WV + wv) * 64 + lane;
+        v[j] = c < total ? pd[c] : __builtin_inff();
+        r[j] = c < total ? pi[c] : -1;
+    }
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const bool ok = r[j] >= 0 && r[j] < nrows && v[j] == v[j] && !(v[j] == __builtin_inff());
+        const float f = v[j] == 0.f ? 0.f : v[j];
+        const unsigned b = __float_as_uint(f);
+        u[j] = ok ? ((b >> 31) ? ~b : (b | 0x80000000u)) : 0xffffffffu;
+    }
+    unsigned T = 0;
+    for (int bit = 31; bit >= 0; --bit) {
+        const unsigned cand = T | (1u << bit);
+        int cnt = 0;
+#pragma unroll
+        for (int j = 0; j < J; ++j) cnt += __popcll(__ballot(u[j] < cand));
+        const int par = bit & 1;
+        if (lane == 0) scnt[par][wv] = cnt;
+        __syncthreads();
+        int tot = 0;
+#pragma unroll
+        for (int w = 0; w < WV; ++w) tot += scnt[par][w];
+        if (tot < k) T = cand;
+    }
+    // compaction: this wave's counts below / at T, the waves' offsets through LDS
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    int nlt = 0, neq = 0;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        nlt += __popcll(__ballot(u[j] < T));
+        neq += __popcll(__ballot(u[j] == T && u[j] != 0xffffffffu));
+    }
+    __syncthreads();  // every wave has read the last search step's counts
+    if (lane == 0) { scnt[0][wv] = nlt; scnt[1][wv] = neq; }
+    __syncthreads();
+    int olt = 0, oeq = 0, tlt = 0;
+#pragma unroll
+    for (int w = 0; w < WV; ++w) {
+        olt += w < wv ? scnt[0][w] : 0;
+        oeq += w < wv ? scnt[1][w] : 0;
+        tlt += scnt[0][w];
+    }
+    int plt = olt, peq = tlt + oeq;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const bool a = u[j] < T, b = u[j] == T && u[j] != 0xffffffffu;
+        const unsigned long long ma = __ballot(a), mb = __ballot(b);
+        if (a) { const int p = plt + __popcll(ma & lt); sd[p] = v[j]; si[p] = r[j]; }
+        if (b) { const int p = peq + __popcll(mb & lt); if (p < k) { sd[p] = v[j]; si[p] = r[j]; } }
+        plt += __popcll(ma);
+        peq += __popcll(mb);
+    }
+    int tot_eq = 0;
+#pragma unroll
+    for (int w = 0; w < WV; ++w) tot_eq += scnt[1][w];
+    const int nsel = tlt + tot_eq < k ? tlt + tot_eq : k;
+    __syncthreads();
+    if (wv == 0) {
+        float kk = lane < nsel ? sd[lane] : __builtin_inff();
+        int cc = lane < nsel ? si[lane] : IdTraits<int>::pad();
+        wave_sort(kk, cc);
+        L.d[0] = kk;
+        L.id[0] = cc;
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // ivf_rerank_topk — form kFormSplit2Exact.  The 2-term split-bf16 scan (≈2⁻¹⁶ relative per product)
 // only prunes; the results are exact.  Per query (one wave): merge the partial lists to the
@@ -1208,8 +1302,12 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
     const int64_t s0 = slot_off ? slot_off[q * nprobe] : q * nprobe;
     const int64_t s1 = slot_off ? slot_off[(q + 1) * nprobe] : (q + 1) * nprobe;
     const int64_t total = (s1 - s0) * k;
+    // WV > 1 and ≤ 64·WV·RS_J candidates (block-uniform): the block's bitwise select (rerank_block_select)
+    // instead of per-wave lists and serial inserts
+    constexpr int RS_J = 16;
+    const bool bsel = WV > 1 && total <= (int64_t)64 * WV * RS_J && !rerank_lists();
     constexpr int MU = 4;  // candidate chunks loaded ahead of their offers
-    for (int64_t cb = (int64_t)wv * 64; cb < total; cb += 64 * WV * MU) {
+    for (int64_t cb = (int64_t)wv * 64; !bsel && cb < total; cb += 64 * WV * MU) {
         float vv[MU];
         int rr[MU];
 #pragma unroll
@@ -1231,14 +1329,20 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
     if constexpr (WV > 1) {
         __shared__ float sd[WV * 64], sdist[64];
         __shared__ int si[WV * 64], srow[64];
-        sd[wv * 64 + lane] = lane < k ? L.d[0] : __builtin_inff();
-        si[wv * 64 + lane] = lane < k ? L.id[0] : IdTraits<int>::pad();
-        __syncthreads();
-        if (wv == 0) {
-            L.init();
+        __shared__ int scnt[2][WV];
+        if (bsel) {
+            rerank_block_select<WV, RS_J>(pd + s0 * k, pi + s0 * k, total, k, nrows, sd, si, scnt, L);
+            if (wv == 0) srow[lane] = lane < k ? L.id[0] : IdTraits<int>::pad();
+        } else {
+            sd[wv * 64 + lane] = lane < k ? L.d[0] : __builtin_inff();
+            si[wv * 64 + lane] = lane < k ? L.id[0] : IdTraits<int>::pad();
+            __syncthreads();
+            if (wv == 0) {
+                L.init();
 #pragma unroll
-            for (int w = 0; w < WV; ++w) L.offer(sd[w * 64 + lane], si[w * 64 + lane], k - 1);
-            srow[lane] = lane < k ? L.id[0] : IdTraits<int>::pad();
+                for (int w = 0; w < WV; ++w) L.offer(sd[w * 64 + lane], si[w * 64 + lane], k - 1);
+                srow[lane] = lane < k ? L.id[0] : IdTraits<int>::pad();
+            }
         }
         __syncthreads();
         // every wave: its share of the candidates' direct-form distances (4 rows in flight)
