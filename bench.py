@@ -1057,12 +1057,12 @@ def main():
             line["precision"] = ("returned distances are fp32 direct-form Σ(q−x)² (FAISS CPU IVFFlatScanner "
                                  "arithmetic); the fp16-image scan only prunes, and a per-query bound "
                                  "(|scan key − exact| ≤ 2(|q|·max‖x−x̂‖ + ‖q−q̂‖·max‖x̂‖) + fp32 accumulation) "
-                                 "proves no pruned row reaches the top-k (failures re-run on the 3-term path)")
+                                 "proves no pruned row reaches the top-k (failures re-run on the device in the direct form)")
         elif args.workload == "ivf" and index.form == 5:
             line["precision"] = ("returned distances are fp32 direct-form Σ(q−x)² (FAISS CPU IVFFlatScanner "
                                  "arithmetic); the bf16 2-term split scan only prunes, and a per-query bound "
                                  "(|scan key − exact| ≤ 2^-12·(|q|²+max|x|²)) proves no pruned row reaches the top-k "
-                                 "(failures re-run on the 3-term path)")
+                                 "(failures re-run on the device in the direct form)")
         if (args.suite and world == 1) or not args.no_c5:
             index.close()
             del index

@@ -1271,7 +1271,8 @@ __device__ __forceinline__ void rerank_block_select(const float *__restrict__ pd
 // E = 2⁻¹²·(‖q‖² + max‖x‖²) (the dropped split terms, ≤ 3·2⁻¹⁶·‖q‖‖x‖ per q·x, doubled, plus fp32
 // rounding of the norms and of both sums, with margin).  A query whose kout-th exact distance is not
 // < K16 − E (or < −K16... for IP the same bound on −q·x) is flagged; the host re-runs the flagged
-// queries on the 3-term path.  With fewer than 16 merged candidates nothing was pruned.
+// queries on the device in the direct form (ivf_fallback_scan/_merge; the Flat form: on the host, 3-term
+// path).  With fewer than 16 merged candidates nothing was pruned.
 // The list length k (16; 32 for Flat IP, common.hpp) is the number of candidates reranked.
 // rxmax >= 0 (Flat form kFlatBf16Exact: one plain bf16 product per element): the bound is the
 // Cauchy-Schwarz bound of the bf16 rounding instead, from this query's own rounding residual and the

@@ -925,7 +925,7 @@ void launch_ivf_scan_mfma_bf(int np, const float *Q, int64_t nq, void *qsplit, c
 // fp16 rounding, |q·(x − x̂/s)| ≤ ‖q‖·‖x − x̂/s‖, and the scan is a FILTER: it keeps the 16 best per
 // (query, list, chunk) like form 5, ivf_rerank_topk recomputes them in FAISS's direct fp32 form and
 // proves with the measured residuals (largest row residual, this query's split residual) that no
-// pruned row reaches the top-k; failing queries re-run on the 3-term path.
+// pruned row reaches the top-k; failing queries re-run on the device in the direct form.
 // Image layout (per list, 32-row passes as codes_t): [pass][32-dim super-step S][row tile r][lane (g, m)]
 // [8 halves] = row 16r + m, dims 32S + 4g + j and 32S + 16 + 4g + j (j < 4) — the k-slot order of the
 // split-bf16 variant, so a wave load is 1 KiB contiguous and a pass of d = 768 is 48 KiB.
@@ -1029,7 +1029,7 @@ __global__ void __launch_bounds__(256) ivf_half_residual(const float *__restrict
 // image's k-slot order, qsplit [query][term][super-step][g][8 halves]; its[q] = 1/(t·s) (a power of
 // two) and qres[q] = ‖q − (h + l)/t‖ (×1.0001 for the fp32 sum).  A query whose scale leaves the safe
 // range (non-finite entries, |e_q| > 100, 1/(t·s) not a normal float) gets zero terms and qres = +inf:
-// the rerank flags it and it re-runs on the 3-term path.
+// the rerank flags it and it re-runs on the device in the direct form.
 __global__ void __launch_bounds__(256) ivf_split_queries_h(const float *__restrict__ Q, int64_t nq, int d, int nsup,
                                                            int es, uint4 *__restrict__ out, float *__restrict__ its,
                                                            float *__restrict__ qres) {

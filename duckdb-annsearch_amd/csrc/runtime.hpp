@@ -221,7 +221,7 @@ struct IvfIndex : IndexBase {
     int nlist = 0, nprobe = 1;
     std::vector<int> owner;  // list → shard (size-balanced at create; appended rows follow their list)
     int form = kFormHalfExact;
-    int64_t rerank_fallbacks = 0;  // queries re-run on the 3-term path by the exactness check
+    int64_t rerank_fallbacks = 0;  // queries re-run from the host (HIPANN_IVF_HOST_FALLBACK); device re-runs: fb_total
     std::vector<std::unique_ptr<IvfShard>> shards;
     int64_t last_nq = 0;
     int last_np = 0;

@@ -454,7 +454,7 @@ class HipIndexIVFFlat(_Handle):
                                               C.c_void_p(i_ptr), C.c_void_p(stream or None), eb, 1024), eb)
 
     def rerank_fallbacks(self) -> int:
-        """Queries the exact form's bound check re-ran on the 3-term path since creation."""
+        """Queries the exact form's bound check flagged since creation (re-run on the device in the direct form)."""
         return int(lib().hipann_ivf_rerank_fallbacks(self._h))
 
     def last_probes(self, nq: int) -> np.ndarray:

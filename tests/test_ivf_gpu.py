@@ -275,7 +275,7 @@ def test_ivf_exact_form_distances_are_direct(gpu, oracle, metric, form):
 @pytest.mark.parametrize("form", [5, 6])
 def test_ivf_exact_form_fallback_on_ties(gpu, oracle, form):
     """Every vector stored 24 times: the 16 rerank candidates tie, the bound check cannot prove the top-k,
-    and the flagged queries are re-run on the 3-term path — results still follow the oracle's (distance,
+    and the flagged queries are re-run on the device in the direct form — results still follow the oracle's (distance,
     label) order."""
     base, xq = faiss_metal_case(600, 40, 64)
     xb = np.ascontiguousarray(np.repeat(base, 24, axis=0))
@@ -391,7 +391,7 @@ def test_ivf_half_form_scaled_data(gpu, oracle, scale, metric):
 
 def test_ivf_half_form_query_out_of_range(gpu, oracle):
     """A query whose own scale leaves the fp16 form's safe range (here |q| ~ 2^110, IP) gets a non-finite
-    bound: the rerank flags it and it is re-run on the 3-term path; the other queries are unaffected."""
+    bound: the rerank flags it and it is re-run on the device (direct form); the other queries are unaffected."""
     xb, xq = faiss_metal_case(6000, 24, 64)
     xq = xq.copy()
     xq[3] *= np.float32(2.0 ** 110)
