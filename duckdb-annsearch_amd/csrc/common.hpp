@@ -8,6 +8,15 @@
 
 namespace hipann {
 
+// The IVF plan's per-query count step, handed to the coarse quantizer's probe select (runtime.hpp
+// FlatShard::plan_hook, rows_select_small): list counts into ccnt, per-query slot prefixes and totals.
+struct IvfPlanHook {
+    const int *list_len;
+    int nlist, chunk_rows;
+    int *ccnt, *slot_off, *qtot;
+    bool done;
+};
+
 struct HipError : std::runtime_error {
     using std::runtime_error::runtime_error;
 };

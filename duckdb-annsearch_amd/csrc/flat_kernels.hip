@@ -969,7 +969,9 @@ rows_select_out(const float *__restrict__ keys, int64_t ldk, int64_t ncols, int6
 template <int J>
 __global__ void __launch_bounds__(256)
 rows_select_small(const float *__restrict__ keys, int64_t ldk, int ncols, int64_t nq, int k, int kout,
-                  int64_t label_offset, float out_sign, float *__restrict__ D, int64_t *__restrict__ I) {
+                  int64_t label_offset, float out_sign, float *__restrict__ D, int64_t *__restrict__ I,
+                  const int *__restrict__ list_len, int nlist, int chunk_rows, int *__restrict__ ccnt,
+                  int *__restrict__ slot_off, int *__restrict__ qtot) {
     __shared__ float sk[4][64];
     __shared__ int sc[4][64];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1028,10 +1030,24 @@ rows_select_small(const float *__restrict__ keys, int64_t ldk, int ncols, int64_
     float kk = lane < nsel ? sk[wv][lane] : __builtin_inff();
     int cc = lane < nsel ? sc[wv][lane] : 0x7fffffff;
     wave_sort(kk, cc);
+    const bool pad = lane >= nsel || kk == __builtin_inff();
     if (live && lane < kout) {
-        const bool pad = lane >= nsel || kk == __builtin_inff();
         D[q * kout + lane] = pad ? (out_sign > 0.f ? __builtin_inff() : -__builtin_inff()) : kk * out_sign;
         I[q * kout + lane] = pad ? -1 : (int64_t)cc + label_offset;
+    }
+    if (ccnt && live) {  // the IVF plan's per-query step (ivf_count_q) on the probes just selected (kout ≤ 64)
+        const int64_t l = lane < kout && !pad ? (int64_t)cc + label_offset : -1;
+        const int len = l >= 0 && l < nlist ? list_len[l] : 0;
+        if (len > 0) atomicAdd(ccnt + l, 1);
+        const int v = len > 0 ? (len + chunk_rows - 1) / chunk_rows : 0;
+        int x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(x, o);
+            if (lane >= o) x += t;
+        }
+        if (lane < kout) slot_off[q * kout + lane] = x - v;
+        if (lane == 63) qtot[q] = x;
     }
 }
 
@@ -1361,19 +1377,25 @@ void launch_rows_topk(const float *keys, int64_t ldk, int64_t ncols, int64_t nq,
 }
 
 bool launch_rows_select_out(const float *keys, int64_t ldk, int64_t ncols, int64_t nq, int k, int kout,
-                            int64_t label_offset, float out_sign, float *D, int64_t *I, hipStream_t st) {
+                            int64_t label_offset, float out_sign, float *D, int64_t *I, hipStream_t st,
+                            IvfPlanHook *hook) {
     const int S = (kout + 63) / 64;
     if (S > 4 || ncols > 0x7ffffffe || k > kout) return false;  // the segment path + merge instead
     dim3 grid((unsigned)ceil_div(nq, 4)), block(256);
     static const bool lists = [] { const char *e = std::getenv("HIPANN_ROWSEL_LIST"); return e && std::atoi(e); }();
     if (kout <= 64 && ncols <= 1024 && !lists) {  // rows of ≤ 1024 keys: the bitwise select
+        const bool h = hook != nullptr;
+        const int *ll = h ? hook->list_len : nullptr;
+        const int nl = h ? hook->nlist : 0, cr = h ? hook->chunk_rows : 1;
+        int *cc = h ? hook->ccnt : nullptr, *so = h ? hook->slot_off : nullptr, *qt = h ? hook->qtot : nullptr;
         if (ncols <= 256)
             hipLaunchKernelGGL(rows_select_small<4>, grid, block, 0, st, keys, ldk, (int)ncols, nq, k, kout,
-                               label_offset, out_sign, D, I);
+                               label_offset, out_sign, D, I, ll, nl, cr, cc, so, qt);
         else
             hipLaunchKernelGGL(rows_select_small<16>, grid, block, 0, st, keys, ldk, (int)ncols, nq, k, kout,
-                               label_offset, out_sign, D, I);
+                               label_offset, out_sign, D, I, ll, nl, cr, cc, so, qt);
         HIPANN_CHECK(hipGetLastError());
+        if (h) hook->done = true;
         return true;
     }
 #define HIPANN_RSEL_CASE(s)                                                                                      \

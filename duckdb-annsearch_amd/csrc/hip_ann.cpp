@@ -162,7 +162,7 @@ static void flat_shard_search_bigk(FlatIndex &ix, FlatShard &sh, int64_t nq, con
         {  // kout ≤ 256: one wave selects the whole row and writes the output (no segment lists, no merge)
             ScopedTiming t(ix.timer_merge, st);
             if (launch_rows_select_out(sh.keys.get<float>(), C, sh.n, nq, k, kout, sh.label_offset, out_sign, D, I,
-                                       st))
+                                       st, sh.plan_hook))
                 return;
         }
         // short rows: 256-column segments, so a 1024-centroid row is selected by 4 waves, not 1

@@ -218,8 +218,25 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     // 1. coarse quantizer (FAISS: quantizer->search(n, x, nprobe) — Flat rules incl. nq < 20)
     sh.coarse_d.ensure((size_t)nq * np * sizeof(float), sh.device);
     sh.coarse_i.ensure((size_t)nq * np * sizeof(int64_t), sh.device);
-    flat_shard_search(*sh.quant, *sh.quant->shards[0], nq, xq, np, np, sh.coarse_d.get<float>(),
-                      sh.coarse_i.get<int64_t>(), st);
+    HIPANN_REQUIRE((int64_t)nq * np < (int64_t)0x7fffffff, "nq * nprobe too large");
+    sh.slot_off.ensure(sizeof(int) * ((size_t)nq * np + 1), sh.device);
+    if (!sh.ccnt.p) {  // zeroed once; ivf_plan_q leaves it zero after every batch
+        sh.ccnt.ensure(sizeof(int) * (size_t)nlist, sh.device);
+        HIPANN_CHECK(hipMemsetAsync(sh.ccnt.p, 0, sizeof(int) * (size_t)nlist, st));
+    }
+    sh.qtot.ensure(sizeof(int) * (size_t)nq, sh.device);
+    // the plan's per-query count step rides on the coarse probe select when that path is taken
+    IvfPlanHook hook{sh.list_len.get<int>(), nlist, ivf_chunk_rows(), sh.ccnt.get<int>(), sh.slot_off.get<int>(),
+                     sh.qtot.get<int>(), false};
+    FlatShard &qsh = *sh.quant->shards[0];
+    qsh.plan_hook = ivf_plan_query_major() ? &hook : nullptr;
+    try {
+        flat_shard_search(*sh.quant, qsh, nq, xq, np, np, sh.coarse_d.get<float>(), sh.coarse_i.get<int64_t>(), st);
+    } catch (...) {
+        qsh.plan_hook = nullptr;
+        throw;
+    }
+    qsh.plan_hook = nullptr;
     // 2. list-major work plan
     sh.cnt.ensure(sizeof(int) * (nlist + 1), sh.device);
     sh.bucket_off.ensure(sizeof(int) * (nlist + 1), sh.device);
@@ -264,15 +281,10 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
         sh.qbound.ensure(sizeof(unsigned) * (size_t)nq, sh.device);
         qbound = sh.qbound.get<unsigned>();
     }
-    if (!sh.ccnt.p) {  // zeroed once; ivf_plan_q leaves it zero after every batch
-        sh.ccnt.ensure(sizeof(int) * (size_t)nlist, sh.device);
-        HIPANN_CHECK(hipMemsetAsync(sh.ccnt.p, 0, sizeof(int) * (size_t)nlist, st));
-    }
-    sh.qtot.ensure(sizeof(int) * (size_t)nq, sh.device);
     launch_ivf_plan(sh.coarse_i.get<int64_t>(), nq, np, sh.list_len.get<int>(), nlist, group, sh.cnt.get<int>(),
                     sh.bucket_off.get<int>(), sh.item_off.get<int>(), sh.cursor.get<int>(), sh.bucket.get<int>(),
                     sh.slot_off.get<int>(), st, exact ? sh.nflag.get<int>() : nullptr, qbound, sh.ccnt.get<int>(),
-                    sh.qtot.get<int>());
+                    sh.qtot.get<int>(), hook.done);
     // 3. scan: one k-list per (query, probe, row chunk) slot — every slot is written by exactly one item
     const size_t parts = (size_t)np * nq * sh.max_nch * k;
     HIPANN_REQUIRE((int64_t)np * nq * sh.max_nch < (int64_t)0x7fffffff, "too many partial lists");

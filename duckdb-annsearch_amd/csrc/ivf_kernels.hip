@@ -1014,14 +1014,19 @@ void launch_ivf_scan_bigk(const float *Q, int d, int metric, const float *codes,
 }
 
 // ---------------------------------------------------------------------------------------------
+// HIPANN_IVF_PLAN_SPLIT=1: the list-major count / plan / slot scan / fill sequence (A/B)
+bool ivf_plan_query_major() {
+    static const bool split = [] { const char *e = std::getenv("HIPANN_IVF_PLAN_SPLIT"); return e && std::atoi(e); }();
+    return !split;
+}
+
 void launch_ivf_plan(const int64_t *probes, int64_t nq, int nprobe, const int *list_len, int nlist, int group,
                      int *cnt, int *bucket_off, int *item_off, int *cursor, int *bucket, int *slot_off,
-                     hipStream_t st, int *nflag_reset, unsigned *qbound, int *ccnt, int *qtot) {
+                     hipStream_t st, int *nflag_reset, unsigned *qbound, int *ccnt, int *qtot, bool counted) {
     const int64_t npairs = nq * nprobe;
-    static const bool split = [] { const char *e = std::getenv("HIPANN_IVF_PLAN_SPLIT"); return e && std::atoi(e); }();
-    if (!split && ccnt && qtot) {
+    if (ivf_plan_query_major() && ccnt && qtot) {
         const unsigned gq = (unsigned)std::max<int64_t>(1, ceil_div(nq, (int64_t)4));
-        if (nq > 0)
+        if (nq > 0 && !counted)  // counted: the coarse probe select already did this step (IvfPlanHook)
             hipLaunchKernelGGL(ivf_count_q, dim3(gq), dim3(256), 0, st, probes, nq, nprobe, list_len, nlist, ccnt,
                                slot_off, qtot);
         hipLaunchKernelGGL(ivf_plan_q, dim3(1), dim3(1024), 0, st, ccnt, list_len, nlist, group, cnt, bucket_off,

@@ -132,6 +132,9 @@ struct FlatShard {
     hipStream_t stream = nullptr;
     // scratch
     DevBuf q, qn, part_d, part_i, out_d, out_i;
+    // IVF coarse quantizer only: the plan's per-query count step fused into the probe select (set by
+    // ivf_shard_search around its coarse call; done = the select consumed it)
+    struct IvfPlanHook *plan_hook = nullptr;
     const float *qn_of = nullptr;  // sh.qn holds ‖q‖² of these queries (the last search's, nq of them)
     int64_t qn_nq = 0;
     DevBuf keys, run_d, run_i, run2_d, run2_i;  // k > 64 path
@@ -264,7 +267,8 @@ void launch_flat_scan_keys(const float *Q, int nq, const float *X, int64_t N, in
 void launch_rows_topk(const float *keys, int64_t ldk, int64_t ncols, int64_t nq, int64_t seg_len, int nseg, int k,
                       int id0, float *pd, int *pi, hipStream_t st);
 bool launch_rows_select_out(const float *keys, int64_t ldk, int64_t ncols, int64_t nq, int k, int kout,
-                            int64_t label_offset, float out_sign, float *D, int64_t *I, hipStream_t st);
+                            int64_t label_offset, float out_sign, float *D, int64_t *I, hipStream_t st,
+                            IvfPlanHook *hook = nullptr);
 void launch_merge_raw(const float *pd, const int *pi, int nparts, int64_t nq, int k, float *od, int *oi,
                       hipStream_t st);
 void launch_flat_scan_topk(const float *Q, int nq, const float *X, int64_t N, int d, int metric, int k, int nwaves,
@@ -272,7 +276,7 @@ void launch_flat_scan_topk(const float *Q, int nq, const float *X, int64_t N, in
 void launch_ivf_plan(const int64_t *probes, int64_t nq, int nprobe, const int *list_len, int nlist, int group,
                      int *cnt, int *bucket_off, int *item_off, int *cursor, int *bucket, int *slot_off,
                      hipStream_t st, int *nflag_reset = nullptr, unsigned *qbound = nullptr, int *ccnt = nullptr,
-                     int *qtot = nullptr);
+                     int *qtot = nullptr, bool counted = false);
 int64_t ivf_max_items(int64_t nq, int nprobe, int nlist, int max_nch, int64_t nrows, int group);
 int ivf_mfma_bf_group(int d, int np);
 bool ivf_mfma_bf_supported(const float *Q, int d, const float *codes, int k, int np);
@@ -320,6 +324,7 @@ void launch_ivf_scan_mfma_bf(int np, const float *Q, int64_t nq, void *qsplit, c
                              float *pd, int *pi, hipStream_t st);
 int ivf_group_size(int form, int d);  // queries per work item of the form's scan kernel
 int ivf_chunk_rows();
+bool ivf_plan_query_major();
 void launch_ivf_scan_bigk(const float *Q, int d, int metric, const float *codes, const int64_t *list_off,
                           const int64_t *probes, int64_t npairs, int nprobe, const int *slot_off, int64_t nslots,
                           int k, float *pd, int *pi, hipStream_t st);
