@@ -1051,6 +1051,104 @@ rows_select_small(const float *__restrict__ keys, int64_t ldk, int ncols, int64_
     }
 }
 
+// rows_select_block — rows of 257..1024 keys: rows_select_small's select with the row spread over a
+// block of 4 waves (column c = 256·wave + 64·j + lane, J = 4 registers per lane); each search step sums
+// the waves' ballot counts through LDS (one barrier), the compaction runs in (wave, j, lane) = column
+// order, and wave 0 sorts and writes the output (and the IVF plan's count step).  A quarter of the
+// per-wave ballot chain of the one-wave version (16 µs for 1024 × 1024 keys).
+__global__ void __launch_bounds__(256)
+rows_select_block(const float *__restrict__ keys, int64_t ldk, int ncols, int64_t nq, int k, int kout,
+                  int64_t label_offset, float out_sign, float *__restrict__ D, int64_t *__restrict__ I,
+                  const int *__restrict__ list_len, int nlist, int chunk_rows, int *__restrict__ ccnt,
+                  int *__restrict__ slot_off, int *__restrict__ qtot) {
+    constexpr int J = 4, WV = 4;
+    __shared__ float sk[64];
+    __shared__ int sc[64];
+    __shared__ int scnt[2][WV];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t q = blockIdx.x;
+    const float *row = keys + q * ldk;
+    float v[J];
+    unsigned u[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int c = 256 * wv + 64 * j + lane;
+        v[j] = c < ncols ? row[c] : __builtin_nanf("");
+    }
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const float f = v[j] == 0.f ? 0.f : v[j];
+        const unsigned b = __float_as_uint(f);
+        u[j] = v[j] == v[j] ? ((b >> 31) ? ~b : (b | 0x80000000u)) : 0xffffffffu;
+    }
+    unsigned T = 0;
+    for (int bit = 31; bit >= 0; --bit) {
+        const unsigned cand = T | (1u << bit);
+        int cnt = 0;
+#pragma unroll
+        for (int j = 0; j < J; ++j) cnt += __popcll(__ballot(u[j] < cand));
+        const int par = bit & 1;
+        if (lane == 0) scnt[par][wv] = cnt;
+        __syncthreads();
+        const int tot = scnt[par][0] + scnt[par][1] + scnt[par][2] + scnt[par][3];
+        if (tot < k) T = cand;
+    }
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    int nlt = 0, neq = 0;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        nlt += __popcll(__ballot(u[j] < T));
+        neq += __popcll(__ballot(u[j] == T && u[j] != 0xffffffffu));
+    }
+    __syncthreads();  // every wave has read the last search step's counts
+    if (lane == 0) { scnt[0][wv] = nlt; scnt[1][wv] = neq; }
+    __syncthreads();
+    int olt = 0, oeq = 0, tlt = 0, teq = 0;
+#pragma unroll
+    for (int w = 0; w < WV; ++w) {
+        olt += w < wv ? scnt[0][w] : 0;
+        oeq += w < wv ? scnt[1][w] : 0;
+        tlt += scnt[0][w];
+        teq += scnt[1][w];
+    }
+    int plt = olt, peq = tlt + oeq;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const bool a = u[j] < T, b = u[j] == T && u[j] != 0xffffffffu;
+        const unsigned long long ma = __ballot(a), mb = __ballot(b);
+        const int c = 256 * wv + 64 * j + lane;
+        if (a) { const int p = plt + __popcll(ma & lt); sk[p] = v[j]; sc[p] = c; }
+        if (b) { const int p = peq + __popcll(mb & lt); if (p < k) { sk[p] = v[j]; sc[p] = c; } }
+        plt += __popcll(ma);
+        peq += __popcll(mb);
+    }
+    const int nsel = tlt + teq < k ? tlt + teq : k;
+    __syncthreads();
+    if (wv != 0) return;
+    float kk = lane < nsel ? sk[lane] : __builtin_inff();
+    int cc = lane < nsel ? sc[lane] : 0x7fffffff;
+    wave_sort(kk, cc);
+    const bool pad = lane >= nsel || kk == __builtin_inff();
+    if (lane < kout) {
+        D[q * kout + lane] = pad ? (out_sign > 0.f ? __builtin_inff() : -__builtin_inff()) : kk * out_sign;
+        I[q * kout + lane] = pad ? -1 : (int64_t)cc + label_offset;
+    }
+    if (ccnt) {  // the IVF plan's per-query step (ivf_count_q) on the probes just selected (kout ≤ 64)
+        const int64_t l = lane < kout && !pad ? (int64_t)cc + label_offset : -1;
+        const int len = l >= 0 && l < nlist ? list_len[l] : 0;
+        if (len > 0) atomicAdd(ccnt + l, 1);
+        const int vv = len > 0 ? (len + chunk_rows - 1) / chunk_rows : 0;
+        int x = vv;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(x, o);
+            if (lane >= o) x += t;
+        }
+        if (lane < kout) slot_off[q * kout + lane] = x - vv;
+        if (lane == 63) qtot[q] = x;
+    }
+}
+
 // Raw merge: nparts partial [part][nq][k] (keys, int ids) → one [nq][k] partial (keys, int ids).
 template <int S>
 __global__ void __launch_bounds__(256)
@@ -1376,6 +1474,12 @@ void launch_rows_topk(const float *keys, int64_t ldk, int64_t ncols, int64_t nq,
     throw HipError("rows_topk: k too large");
 }
 
+// HIPANN_ROWSEL_WAVE=1: rows of 257..1024 keys on one wave (rows_select_small<16>) instead of a block (A/B)
+static bool one_wave_rows() {
+    static const bool v = [] { const char *e = std::getenv("HIPANN_ROWSEL_WAVE"); return e && std::atoi(e); }();
+    return v;
+}
+
 bool launch_rows_select_out(const float *keys, int64_t ldk, int64_t ncols, int64_t nq, int k, int kout,
                             int64_t label_offset, float out_sign, float *D, int64_t *I, hipStream_t st,
                             IvfPlanHook *hook) {
@@ -1390,6 +1494,9 @@ bool launch_rows_select_out(const float *keys, int64_t ldk, int64_t ncols, int64
         int *cc = h ? hook->ccnt : nullptr, *so = h ? hook->slot_off : nullptr, *qt = h ? hook->qtot : nullptr;
         if (ncols <= 256)
             hipLaunchKernelGGL(rows_select_small<4>, grid, block, 0, st, keys, ldk, (int)ncols, nq, k, kout,
+                               label_offset, out_sign, D, I, ll, nl, cr, cc, so, qt);
+        else if (!one_wave_rows())
+            hipLaunchKernelGGL(rows_select_block, dim3((unsigned)nq), block, 0, st, keys, ldk, (int)ncols, nq, k, kout,
                                label_offset, out_sign, D, I, ll, nl, cr, cc, so, qt);
         else
             hipLaunchKernelGGL(rows_select_small<16>, grid, block, 0, st, keys, ldk, (int)ncols, nq, k, kout,
