@@ -22,7 +22,11 @@ path), C2 (Flat L2 1M x 768), Flat L2 10M x 768, C4 (DiskANN), the extension's r
 ranks 16/24/32.  --no-suite skips them.  At every N the IVF line also carries C5 (Flat IP, 12.5M rows
 per GPU, sharded: exactly C5's 100M x 768 at N = 8); --no-c5 skips it.
 
-Launch: python bench.py [--gpus N --steps K --warmup W]  (N>1 under torch.distributed.run).
+Launch: python bench.py [--gpus N --steps K --warmup W].  N > 1 runs one process per GPU over RCCL: under
+torch.distributed.run (the driver's launch) the ranks read RANK / WORLD_SIZE; started directly, bench.py
+starts the N ranks itself (a torch.distributed.run child process — the parent never touches the GPU and never
+re-execs) and exits with their status.  ``--workload selftest`` checks that launcher on the CPU (gloo): N
+ranks rendezvous, all-gather their ranks and run the timed-region barrier / max-over-ranks protocol.
 """
 from __future__ import annotations
 
@@ -54,7 +58,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", choices=["flat", "ivf", "diskann"],
+    p.add_argument("--workload", choices=["flat", "ivf", "diskann", "selftest"],
                    default=os.environ.get("HIPANN_BENCH_WORKLOAD", "ivf"))
     p.add_argument("--n", type=int, default=None, help="rows (10M; 1M for diskann)")
     p.add_argument("--d", type=int, default=None, help="dimension (768; 1536 for diskann)")
@@ -154,20 +158,23 @@ def uniform_queries(torch, nq, d, dev):
 # ------------------------------------------------------------------------------------------------
 # timing helpers
 # ------------------------------------------------------------------------------------------------
-def timed_steps(torch, dist, world, fn, steps):
-    """Barrier + sync, `steps` calls, sync + barrier; max over ranks.  Returns seconds."""
+def timed_steps(torch, dist, world, fn, steps, gpu=True):
+    """Barrier + sync, `steps` calls, sync + barrier; max over ranks.  Returns seconds.  gpu=False: the CPU
+    self-test (gloo, no device synchronisation)."""
+    sync = torch.cuda.synchronize if gpu else (lambda: None)
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(steps):
         fn()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], device=torch.device("cuda", torch.cuda.current_device()), dtype=torch.float64)
+        dev = torch.device("cuda", torch.cuda.current_device()) if gpu else torch.device("cpu")
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     return el
@@ -285,6 +292,11 @@ def flat_config(args, torch, dist, hipann, rank, world, dev, n, d, nq, k, metric
             "merge_ms": round(merge_ms, 3),
             "algorithmic": f"{terms} x 2*nq*N_local*d = {terms * flops:.4g} MFMA FLOP per launch ({fdesc})",
             "fp32_equivalent_tflops": round(flops / (kern_ms * 1e-3) / 1e12, 2) if kern_ms > 0 else None}
+    if kern_ms > 0:
+        # SURVEY §8d prices Flat against the fp32 matrix-core peak (2·nq·N·d fp32 products); the default form
+        # computes each product once in bf16 as a certified filter (exact fp32 rerank), so it can pass that peak
+        roof["frac_vs_fp32_peak"] = round(flops / (kern_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TF, 4)
+        roof["fp32_peak"] = FP32_MFMA_PEAK_TF
     if form == 4 and kern_ms > 0:
         # LDS-DMA fill of the bf16 scan: per 32-dim chunk the 256-row database tile (16 KB) — plus the query tile
         # when the queries are not loaded straight into registers (RA, 256-query blocks)
@@ -522,6 +534,13 @@ def ivf_config(args, torch, dist, hipann, rank, world, dev, steps, warmup, suite
             "form": fname,
             "scan_tflops": round(fpp * d * info["scanned_pairs_per_batch_local"] / (kern_ms * 1e-3) / 1e12, 2)
             if kern_ms > 0 else None}
+    if kern_ms > 0:
+        # SURVEY §8d's B_alg = Σ|ℓ|·(4d + 8) (the fp32 rows + labels) over the same kernel time.  The default
+        # form reads the fp16 image (2d + 4 B per row) and certifies with an exact fp32 rerank, so this fraction
+        # can exceed 1: it is the speed-up over an fp32-row stream at the HBM roofline, not a bandwidth.
+        b_survey = info["fp32_rows_bytes_per_batch_local"]
+        roof["frac_vs_survey_bytes"] = round(b_survey / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        roof["survey_bytes_per_launch_gb"] = round(b_survey / 1e9, 3)
     if world == 1:
         attach_traffic(roof, f"ivf_{n}x{d}", b_alg)
     out = {"workload": f"FAISS IVFFlat nlist={nlist} nprobe={nprobe}, {n}x{d} fp32 ({data_desc}), batch={nq}, k={k}",
@@ -550,9 +569,17 @@ def ivf_config(args, torch, dist, hipann, rank, world, dev, steps, warmup, suite
             _, Ia = step()
             torch.cuda.synchronize()
             Ia = Ia.cpu().numpy()
-            alt[IVF_FORMS[f][1]] = {"queries_per_s": round(nq * 5 / ea, 1), "scan_kernel_ms": round(kms, 3),
+            b_f = info["fp32_rows_bytes_per_batch_local"]
+            alt[IVF_FORMS[f][1]] = {"form": f, "queries_per_s": round(nq * 5 / ea, 1), "scan_kernel_ms": round(kms, 3),
                                     "recall_at_10": recall_at(Ia, gt, k),
-                                    "ids_equal_to_reported_form": round(float((Ia == Ir).mean()), 6)}
+                                    "ids_equal_to_reported_form": round(float((Ia == Ir).mean()), 6),
+                                    "roofline": {"bound": "hbm", "kernel": IVF_FORMS[f][0],
+                                                 "achieved": round(b_f / (kms * 1e-3) / 1e9, 1) if kms > 0 else None,
+                                                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                                 "frac": round(b_f / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                                                 if kms > 0 else None,
+                                                 "algorithmic": "SURVEY §8d: Σ distinct probed lists |ℓ|·(4d+8) "
+                                                                "(this form streams the fp32 rows)"}}
         index.form = form
         out["other_forms"] = alt
     out["ivf"]["rerank_fallbacks_total"] = index.rerank_fallbacks()
@@ -851,29 +878,31 @@ def batch_distance_microbench(hipann):
 
     rng = np.random.default_rng(1)
 
+    import ctypes
+
+    lib = O.lib()
+    fp = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_float))  # noqa: E731
+
     def time_pair(n, d, it):
+        """Median per-call time of the three calls, sampled interleaved (GPU, scalar CPU, SIMD CPU, GPU, …) so
+        that clock or load drift during the run hits all three alike."""
         q = rng.uniform(-1, 1, d).astype(np.float32)
         c = rng.uniform(-1, 1, (n, d)).astype(np.float32)
         out = np.empty(n, np.float32)
-        for _ in range(5):
-            hipann.diskann_hip_batch_distances(q, c, n, d, 0, out)
-        t0 = time.perf_counter()
-        for _ in range(it):
-            hipann.diskann_hip_batch_distances(q, c, n, d, 0, out)
-        g = (time.perf_counter() - t0) / it * 1e6
-        lib = O.lib()
-        fp = lambda a: a.ctypes.data_as(__import__("ctypes").POINTER(__import__("ctypes").c_float))  # noqa: E731
         ref = np.empty(n, np.float32)
-        lib.oracle_batch_distances(fp(q), fp(c), n, d, 0, fp(ref))
-        t0 = time.perf_counter()
+        calls = (lambda: hipann.diskann_hip_batch_distances(q, c, n, d, 0, out),
+                 lambda: lib.oracle_batch_distances(fp(q), fp(c), n, d, 0, fp(ref)),
+                 lambda: lib.oracle_batch_distances_simd(fp(q), fp(c), n, d, 0, fp(ref)))
+        for f in calls:
+            for _ in range(5):
+                f()
+        ts = [[], [], []]
         for _ in range(it):
-            lib.oracle_batch_distances(fp(q), fp(c), n, d, 0, fp(ref))
-        cpu = (time.perf_counter() - t0) / it * 1e6
-        lib.oracle_batch_distances_simd(fp(q), fp(c), n, d, 0, fp(ref))
-        t0 = time.perf_counter()
-        for _ in range(it):
-            lib.oracle_batch_distances_simd(fp(q), fp(c), n, d, 0, fp(ref))
-        simd = (time.perf_counter() - t0) / it * 1e6
+            for j, f in enumerate(calls):
+                t0 = time.perf_counter()
+                f()
+                ts[j].append(time.perf_counter() - t0)
+        g, cpu, simd = (float(np.median(t)) * 1e6 for t in ts)
         return g, cpu, simd
 
     rows = []
@@ -897,6 +926,9 @@ def batch_distance_microbench(hipann):
             even_simd = n * d
     return {"shapes": rows, "break_even_sweep_d768": sweep, "break_even_n_times_d": even,
             "break_even_n_times_d_simd_cpu": even_simd,
+            "gates_this_run_supports": {"MIN_GPU_WORK": even_simd, "MIN_GPU_WORK_ONESHOT": even,
+                                        "rule": "smallest swept n*d (powers of two, d = 768) whose median GPU call "
+                                                "beats the median CPU call, samples interleaved"},
             "gates_from": "MIN_GPU_WORK_ONESHOT (ann_search.cpp:696-699, scalar ComputeDistancesCPU) <- break_even_n_times_d; "
                           "MIN_GPU_WORK (metal_ffi.rs:41, Rust SIMD distances) <- break_even_n_times_d_simd_cpu",
             "cpu": "oracle_batch_distances (ComputeDistancesCPU restatement, sequential fp32 sum, 1 thread); "
@@ -968,6 +1000,12 @@ def run_suite(args, torch, dist, hipann, dev):
     guarded("flat_l2_10m_768", lambda: flat(10_000_000, oracle_queries=20, latency=True, steps=5))
     guarded("C4_diskann_1m_1536_sq8", lambda: diskann_config(args, torch, dist, hipann, 0, 1, dev, 1_000_000, 1536,
                                                              1024, args.k, 128, 64, 10, 2))
+    # C4 through the path hip_ffi.rs's fallback takes when the graph is not registered: DiskProvider::search_batch's
+    # own structure (host lock-step BFS, disk_provider.rs:539-638) with each step's distances from the id-gather
+    # kernel (dist_ids_sq8: d + 12 B per distance) — the kernel SURVEY §8d's C4 row prices
+    guarded("C4_diskann_1m_1536_sq8_host_bfs", lambda: diskann_config(args, torch, dist, hipann, 0, 1, dev, 1_000_000,
+                                                                      1536, 1024, args.k, 128, 64, 3, 1,
+                                                                      resident=False))
     guarded("reference_readme_batch_distances", lambda: batch_distance_microbench(hipann))
     guarded("flat_auto_gate_nq1", lambda: flat_auto_gate(hipann))
     guarded("ivf_recall_vs_nprobe", lambda: ivf_robustness(args, torch, dist, hipann, dev))
@@ -1002,23 +1040,88 @@ def c5_config(args, torch, dist, hipann, rank, world, dev):
 
 
 # ------------------------------------------------------------------------------------------------
+def spawn_ranks(args) -> int:
+    """--gpus N > 1 started without a launcher: run the N ranks as torch.distributed.run's children (one process
+    per GPU, rendezvous on 127.0.0.1) and return their exit status.  This parent process never initialises a GPU
+    (only argument parsing happened) and is not replaced: the ranks are child processes; rank 0 prints the
+    line to the inherited stdout."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve())] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on these hosts (RCCL)
+    log(f"[bench] starting {args.gpus} ranks: {' '.join(cmd)}")
+    return subprocess.call(cmd, env=env)
+
+
+def selftest(args, torch, dist, world, rank):
+    """CPU check of the launcher and the timing protocol (gloo): every rank joins, the ranks all-gather their
+    RANK, and `steps` timed all-gathers run between the barriers with the max-over-ranks elapsed time."""
+    if world > 1:
+        dist.init_process_group("gloo")
+    mine = torch.tensor([rank], dtype=torch.int64)
+    seen = [torch.empty_like(mine) for _ in range(world)]
+    step = (lambda: dist.all_gather(seen, mine)) if world > 1 else (lambda: seen[0].copy_(mine))  # noqa: E731
+    for _ in range(args.warmup):
+        step()
+    el = timed_steps(torch, dist, world, step, args.steps, gpu=False)
+    ranks_seen = sorted(int(t.item()) for t in seen)
+    if ranks_seen != list(range(world)):
+        raise SystemExit(f"launcher self-test: ranks seen {ranks_seen} != 0..{world - 1}")
+    line = {"metric": "launcher self-test (all-gathers/s)", "value": round(args.steps / el, 1), "unit": "all-gathers/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el * 1e3 / args.steps, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64", "data": "synthetic",
+            "config": {"workload": "selftest", "parallelism": f"ranks{world}"},
+            "world_check": {"backend": dist.get_backend() if world > 1 else None, "ranks_seen": ranks_seen}}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def world_check(torch, dist, world, rank, dev):
+    """Every rank's RANK all-gathered over the data-path backend (RCCL at N > 1): the line states the ranks the
+    collective saw, and the run stops if it is not 0..N-1."""
+    if world == 1:
+        return {"backend": None, "ranks_seen": [0]}
+    mine = torch.tensor([rank], dtype=torch.int64, device=dev)
+    allr = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(allr, mine)
+    seen = sorted(allr.cpu().tolist())
+    if seen != list(range(world)):
+        raise SystemExit(f"RCCL saw ranks {seen}, expected 0..{world - 1}")
+    return {"backend": dist.get_backend(), "ranks_seen": seen}
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
     import torch
     import torch.distributed as dist
-    import hipann
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    if args.workload == "selftest":
+        return selftest(args, torch, dist, world, rank)
+    import hipann
+
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
     if not hipann.is_available():
         raise SystemExit("libhipann.so / HIP device not available")
+    wcheck = world_check(torch, dist, world, rank, dev)
     metric = 0 if args.metric == "l2" else 1
 
     if args.workload == "diskann":
@@ -1055,9 +1158,13 @@ def main():
         line.update(sub)
         if args.workload == "ivf" and index.form == 6:
             line["precision"] = ("returned distances are fp32 direct-form Σ(q−x)² (FAISS CPU IVFFlatScanner "
-                                 "arithmetic); the fp16-image scan only prunes, and a per-query bound "
-                                 "(|scan key − exact| ≤ 2(|q|·max‖x−x̂‖ + ‖q−q̂‖·max‖x̂‖) + fp32 accumulation) "
-                                 "proves no pruned row reaches the top-k (failures re-run on the device in the direct form)")
+                                 "arithmetic); the scan is a certified filter, not an fp32 stream: it reads an fp16 "
+                                 "image of the rows (2d+4 B per row, half of SURVEY §8d's 4d+8) and only prunes, and a "
+                                 "per-query bound (|scan key − exact| ≤ 2(|q|·max‖x−x̂‖ + ‖q−q̂‖·max‖x̂‖) + fp32 "
+                                 "accumulation) proves no pruned row reaches the top-k (failures re-run on the device "
+                                 "in the direct form).  roofline.frac counts the image bytes the kernel streams; "
+                                 "roofline.frac_vs_survey_bytes counts SURVEY's fp32-row bytes; the fp32-row stream "
+                                 "itself is other_forms' form 5 line with its own roofline")
         elif args.workload == "ivf" and index.form == 5:
             line["precision"] = ("returned distances are fp32 direct-form Σ(q−x)² (FAISS CPU IVFFlatScanner "
                                  "arithmetic); the bf16 2-term split scan only prunes, and a per-query bound "
@@ -1077,6 +1184,7 @@ def main():
                 c5 = {"error": repr(e)}
             c5["wall_s"] = round(time.perf_counter() - t0, 1)
             line.setdefault("configs", {})["C5_flat_ip_100m_768_sharded"] = c5
+    line["world_check"] = wcheck
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -59,6 +59,39 @@ extern "C" {
         out_distances: *mut f32,
     ) -> i32;
     fn diskann_hip_release_db(db: *mut core::ffi::c_void);
+    fn diskann_hip_register_graph(db: *mut core::ffi::c_void, adjacency: *const u32, r: i32) -> i32;
+    fn diskann_hip_search_batch_resident(
+        db: *mut core::ffi::c_void,
+        entry_points: *const u32,
+        n_ep: i32,
+        queries: *const f32,
+        nq: i32,
+        k: i32,
+        l_search: i32,
+        metric: i32,
+        out_ids: *mut i64,
+        out_dists: *mut f32,
+        stats: *mut i64,
+        err_buf: *mut core::ffi::c_char,
+        err_len: i32,
+    ) -> i32;
+    fn diskann_hip_search_batch(
+        db: *mut core::ffi::c_void,
+        adjacency: *const u32,
+        r: i32,
+        entry_points: *const u32,
+        n_ep: i32,
+        queries: *const f32,
+        nq: i32,
+        k: i32,
+        l_search: i32,
+        metric: i32,
+        out_ids: *mut i64,
+        out_dists: *mut f32,
+        stats: *mut i64,
+        err_buf: *mut core::ffi::c_char,
+        err_len: i32,
+    ) -> i32;
 }
 
 /// Cached availability: -1 = unchecked, 0 = unavailable, 1 = available (metal_ffi.rs:33-34).
@@ -191,6 +224,121 @@ impl HipDiskDb {
             )
         };
         ret == 0
+    }
+}
+
+/// (nq × k) C-ABI outputs → DiskProvider::search_batch's return shape: per query the first k
+/// (id, dist) pairs, stopping at the first −1 label (the slots past a short result, ffi.rs:759-762).
+fn collect_results(ids: &[i64], dists: &[f32], nq: usize, k: usize) -> Vec<Vec<(u64, f32)>> {
+    (0..nq)
+        .map(|q| {
+            ids[q * k..(q + 1) * k]
+                .iter()
+                .zip(&dists[q * k..(q + 1) * k])
+                .take_while(|(id, _)| **id >= 0)
+                .map(|(id, d)| (*id as u64, *d))
+                .collect()
+        })
+        .collect()
+}
+
+impl HipDiskDb {
+    /// Upload the graph (the .diskann adjacency segment: n × R u32, u32::MAX padding, file_format.rs:3-18)
+    /// next to the registered vectors, once at DiskProvider::open.  After this, search_batch_resident runs
+    /// the whole lock-step BFS of DiskProvider::search_batch (disk_provider.rs:470-652) on the GPU.
+    pub fn register_graph(&self, adjacency: &[u32], max_degree: usize) -> bool {
+        if max_degree == 0 || adjacency.len() % max_degree != 0 {
+            return false;
+        }
+        unsafe { diskann_hip_register_graph(self.0, adjacency.as_ptr(), max_degree as i32) == 0 }
+    }
+
+    /// DiskProvider::search_batch with the traversal on the GPU (one workgroup per query runs the reference's
+    /// state machine: pop / stop rule / visited set / insert_result, disk_provider.rs:539-678).  `queries_flat`
+    /// is nq × dim.  None ⇒ the caller runs its own lock-step loop (host BFS + id-gather, or the CPU).
+    pub fn search_batch_resident(
+        &self,
+        entry_points: &[u32],
+        queries_flat: &[f32],
+        nq: usize,
+        k: usize,
+        l_search: usize,
+        metric: u8,
+    ) -> Option<Vec<Vec<(u64, f32)>>> {
+        if nq == 0 || k == 0 {
+            return Some(vec![Vec::new(); nq]);
+        }
+        let mut ids = vec![-1i64; nq * k];
+        let mut dists = vec![f32::MAX; nq * k];
+        let mut stats = [0i64; 4];
+        let mut err = [0 as core::ffi::c_char; 256];
+        let ret = unsafe {
+            diskann_hip_search_batch_resident(
+                self.0,
+                entry_points.as_ptr(),
+                entry_points.len() as i32,
+                queries_flat.as_ptr(),
+                nq as i32,
+                k as i32,
+                l_search as i32,
+                metric as i32,
+                ids.as_mut_ptr(),
+                dists.as_mut_ptr(),
+                stats.as_mut_ptr(),
+                err.as_mut_ptr(),
+                err.len() as i32,
+            )
+        };
+        if ret != 0 {
+            return None;
+        }
+        Some(collect_results(&ids, &dists, nq, k))
+    }
+
+    /// The same search with the BFS on the host (native C++ lock-step loop in libhipann) and every step's
+    /// distances from the id-gather kernel over this HBM-resident DB — the reference's structure with the
+    /// candidate copy replaced by ids.  Used when the graph was not registered.
+    pub fn search_batch_host_bfs(
+        &self,
+        adjacency: &[u32],
+        max_degree: usize,
+        entry_points: &[u32],
+        queries_flat: &[f32],
+        nq: usize,
+        k: usize,
+        l_search: usize,
+        metric: u8,
+    ) -> Option<Vec<Vec<(u64, f32)>>> {
+        if nq == 0 || k == 0 {
+            return Some(vec![Vec::new(); nq]);
+        }
+        let mut ids = vec![-1i64; nq * k];
+        let mut dists = vec![f32::MAX; nq * k];
+        let mut stats = [0i64; 4];
+        let mut err = [0 as core::ffi::c_char; 256];
+        let ret = unsafe {
+            diskann_hip_search_batch(
+                self.0,
+                adjacency.as_ptr(),
+                max_degree as i32,
+                entry_points.as_ptr(),
+                entry_points.len() as i32,
+                queries_flat.as_ptr(),
+                nq as i32,
+                k as i32,
+                l_search as i32,
+                metric as i32,
+                ids.as_mut_ptr(),
+                dists.as_mut_ptr(),
+                stats.as_mut_ptr(),
+                err.as_mut_ptr(),
+                err.len() as i32,
+            )
+        };
+        if ret != 0 {
+            return None;
+        }
+        Some(collect_results(&ids, &dists, nq, k))
     }
 }
 

@@ -85,6 +85,7 @@ constexpr int64_t kSmallTable = 16384;  // rows: below this, GEMM keys + per-que
 void shard_append(FlatShard &sh, int d, int metric, const float *x_host, const float *x_dev, int64_t n) {
     if (n <= 0) return;
     DeviceGuard g(sh.device);
+    FenceScope fs(sh.fence, sh.stream, sh.device);  // searches still running on other streams read sh.xb
     const int64_t need = sh.n + n;
     if (need > sh.cap || !sh.owns) {
         int64_t cap = std::max<int64_t>(need, std::max<int64_t>(1024, sh.cap * 2));
@@ -161,8 +162,9 @@ static void flat_shard_search_bigk(FlatIndex &ix, FlatShard &sh, int64_t nq, con
         }
         {  // kout ≤ 256: one wave selects the whole row and writes the output (no segment lists, no merge)
             ScopedTiming t(ix.timer_merge, st);
-            if (launch_rows_select_out(sh.keys.get<float>(), C, sh.n, nq, k, kout, sh.label_offset, out_sign, D, I,
-                                       st, sh.plan_hook))
+            // (short rows only: a long row would be one wave's serial inserts — the segment path spreads it)
+            if (sh.n <= kSmallTable && launch_rows_select_out(sh.keys.get<float>(), C, sh.n, nq, k, kout,
+                                                              sh.label_offset, out_sign, D, I, st, sh.plan_hook))
                 return;
         }
         // short rows: 256-column segments, so a 1024-centroid row is selected by 4 waves, not 1
@@ -518,6 +520,7 @@ static int flat_search_host(FlatIndex &ix, int64_t nq, const float *xq, int64_t 
         sh.q.ensure(qbytes, sh.device);
         sh.out_d.ensure(ob * sizeof(float), sh.device);
         sh.out_i.ensure(ob * sizeof(int64_t), sh.device);
+        FenceScope fs(sh.fence, sh.stream, sh.device);
         if (qbytes <= kKernelCopyMax) launch_copy_words(host_device_ptr(ix.h_q.p), sh.q.p, qbytes, sh.stream);
         else HIPANN_CHECK(hipMemcpyAsync(sh.q.p, ix.h_q.p, qbytes, hipMemcpyHostToDevice, sh.stream));
         flat_shard_search(ix, sh, nq, sh.q.get<float>(), keff, kout, sh.out_d.get<float>(), sh.out_i.get<int64_t>(),
@@ -669,6 +672,7 @@ int hipann_flat_search_device(void *h, int64_t nq, const float *xq_dev, int64_t 
         FlatShard &sh = *fx->shards[0];
         hipStream_t st = static_cast<hipStream_t>(stream);  // NULL = the default (null) stream
         const int keff = (int)std::min<int64_t>(k, std::max<int64_t>(sh.n, 1));
+        FenceScope fs(sh.fence, st, sh.device);  // the previous call's kernels may still use this shard's scratch
         flat_shard_search(*fx, sh, nq, xq_dev, keff, (int)k, D_dev, I_dev, st);
         return 0;
     });

@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <numeric>
 
 using namespace hipann;
@@ -225,6 +226,19 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
         HIPANN_CHECK(hipMemsetAsync(sh.ccnt.p, 0, sizeof(int) * (size_t)nlist, st));
     }
     sh.qtot.ensure(sizeof(int) * (size_t)nq, sh.device);
+    // ccnt must be zero between batches (ivf_plan_q clears it after use); the coarse select's count step and
+    // the plan add to it, so if anything throws before the plan has consumed this batch's counts, zero it
+    // again on the way out.
+    struct CcntReset {
+        IvfShard &sh;
+        int nlist;
+        hipStream_t st;
+        bool armed;
+        ~CcntReset() {
+            if (armed && std::uncaught_exceptions() > 0)
+                (void)hipMemsetAsync(sh.ccnt.p, 0, sizeof(int) * (size_t)nlist, st);
+        }
+    } ccnt_reset{sh, nlist, st, true};
     // the plan's per-query count step rides on the coarse probe select when that path is taken
     IvfPlanHook hook{sh.list_len.get<int>(), nlist, ivf_chunk_rows(), sh.ccnt.get<int>(), sh.slot_off.get<int>(),
                      sh.qtot.get<int>(), false};
@@ -285,6 +299,7 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
                     sh.bucket_off.get<int>(), sh.item_off.get<int>(), sh.cursor.get<int>(), sh.bucket.get<int>(),
                     sh.slot_off.get<int>(), st, exact ? sh.nflag.get<int>() : nullptr, qbound, sh.ccnt.get<int>(),
                     sh.qtot.get<int>(), hook.done);
+    ccnt_reset.armed = false;
     // 3. scan: one k-list per (query, probe, row chunk) slot — every slot is written by exactly one item
     const size_t parts = (size_t)np * nq * sh.max_nch * k;
     HIPANN_REQUIRE((int64_t)np * nq * sh.max_nch < (int64_t)0x7fffffff, "too many partial lists");
@@ -351,7 +366,8 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
         ScopedTiming t(ix.timer_merge, st);
         launch_ivf_rerank(sh.part_d.get<float>(), sh.part_i.get<int>(), sh.slot_off.get<int>(), np, nq, k, kout, metric,
                           xq, sh.codes, d, sh.ids, sh.n, 0, xmax2, D, I, sh.nflag.get<int>(), sh.flagged.get<int>(), st,
-                          kSplit2Eps, half ? sh.half_rxmax : -1.f, half ? sh.hres.get<float>() : nullptr);
+                          kSplit2Eps, half ? sh.half_rxmax : -1.f, half ? sh.hres.get<float>() : nullptr,
+                          sh.coarse_i.get<int64_t>(), sh.list_off.get<int64_t>(), nlist);
     }
     if (!host_fallback()) {
         // flagged queries re-run on the device in the direct form (ivf_fallback_scan/_merge): no host
@@ -401,6 +417,9 @@ static void ivf_add_rows(IvfIndex &ix, int64_t n, const float *xb, const int64_t
     IvfShard &s0 = *ix.shards[0];
     DeviceGuard g0(s0.device);
     hipStream_t st = s0.stream;
+    // every shard's pending searches (possibly on other streams) finish before its buffers are rebuilt
+    std::vector<std::unique_ptr<FenceScope>> fences;
+    for (auto &shp : ix.shards) fences.push_back(std::make_unique<FenceScope>(shp->fence, shp->stream, shp->device));
     const int64_t base = ix.ntotal();
     // 1. assignment on the GPU (shard 0's quantizer; every shard holds all centroids)
     std::vector<int64_t> assign((size_t)n);
@@ -650,6 +669,7 @@ static int ivf_search_host(IvfIndex &ix, int64_t nq, const float *xq, int64_t k,
         sh.q.ensure(qbytes, sh.device);
         sh.out_d.ensure(ob * sizeof(float), sh.device);
         sh.out_i.ensure(ob * sizeof(int64_t), sh.device);
+        FenceScope fs(sh.fence, sh.stream, sh.device);
         if (qbytes <= kKernelCopyMax) launch_copy_words(host_device_ptr(ix.h_q.p), sh.q.p, qbytes, sh.stream);
         else HIPANN_CHECK(hipMemcpyAsync(sh.q.p, ix.h_q.p, qbytes, hipMemcpyHostToDevice, sh.stream));
         ivf_shard_search(ix, sh, nq, sh.q.get<float>(), keff, kout, sh.out_d.get<float>(), sh.out_i.get<int64_t>(),
@@ -746,6 +766,7 @@ int hipann_ivf_search_device(void *h, int64_t nq, const float *xq_dev, int64_t k
         vx->last_nq = nq;
         vx->last_np = std::min(vx->nprobe, vx->nlist);
         const int keff = (int)std::min<int64_t>(k, std::max<int64_t>(sh.n, 1));
+        FenceScope fs(sh.fence, st, sh.device);  // the previous call's kernels may still use this shard's scratch
         ivf_shard_search(*vx, sh, nq, xq_dev, keff, (int)k, D_dev, I_dev, st);
         return 0;
     });

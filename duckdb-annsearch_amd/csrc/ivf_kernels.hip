@@ -1265,6 +1265,91 @@ __device__ __forceinline__ void rerank_block_select(const float *__restrict__ pd
     }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// FAISS IndexIVFFlat's exact-tie membership.  Its scanner admits a candidate only when it is strictly
+// better than the heap top (IVFFlatScanner: C::cmp(simi[0], dis)) and evicts the heap's worst by (key,
+// label) (heap_replace_top's cmp2), scanning the probed lists in probe order and each list in row order.
+// With T the k-th smallest key, that leaves exactly:
+//   * every candidate with key < T (n_lt of them, n_lt < k), and
+//   * of the candidates with key == T, those among the FIRST k candidates with key <= T in scan order
+//     (the point where the heap top first reaches T; later T-keys are never admitted), of which the
+//     k - n_lt smallest labels (each later admission evicted the largest-label T entry).
+// Flat scans in label order, so there the rule is the plain (key, label) order; IVF lists are not
+// label-ordered (duplicates stored under scattered ids, edge_cases.test:75-83).  ivf_scan_order_topk
+// applies the rule to a candidate stream gen(c) -> (key, pos, label), c < n, pos = (probe rank << 32) |
+// CSR row (scan order), keys +inf = no candidate, which must hold every candidate with key <= T (or
+// the k - n_lt earliest T-keys per list: each list's candidates in row order): four passes of wave
+// lists, the result in R as (key, label) ascending.
+// ---------------------------------------------------------------------------------------------
+struct ScanCand {
+    float key;
+    long long pos, label;
+};
+
+template <typename Gen>
+__device__ __forceinline__ void ivf_scan_order_topk(int64_t n, int kout, Gen gen, WaveList<1, long long> &R) {
+    const int lane = threadIdx.x & 63;
+    const long long PAD = IdTraits<long long>::pad();
+    // 1. the kout best by (key, scan position): T and n_lt
+    WaveList<1, long long> A;
+    A.init();
+    for (int64_t c0 = 0; c0 < n; c0 += 64) {
+        const ScanCand x = c0 + lane < n ? gen(c0 + lane) : ScanCand{__builtin_inff(), PAD, PAD};
+        const bool ok = !(x.key == __builtin_inff());
+        A.offer(ok ? x.key : __builtin_inff(), ok ? x.pos : PAD, kout - 1);
+    }
+    const float T = readlane_f(A.d[0], kout - 1);
+    const bool full = !(T == __builtin_inff());
+    const int n_lt = __popcll(__ballot(lane < kout && A.d[0] < T));
+    // 2. the kout-th earliest scan position among keys <= T: the end of FAISS's admission window for T
+    long long PM = PAD;
+    if (full) {
+        WaveList<1, long long> B;
+        B.init();
+        for (int64_t c0 = 0; c0 < n; c0 += 64) {
+            const ScanCand x = c0 + lane < n ? gen(c0 + lane) : ScanCand{__builtin_inff(), PAD, PAD};
+            const bool ok = x.key <= T;
+            B.offer(ok ? 0.f : __builtin_inff(), ok ? x.pos : PAD, kout - 1);
+        }
+        PM = readlane_i(B.id[0], kout - 1);
+    }
+    // 3. the T-keys inside that window: their kout - n_lt smallest labels
+    WaveList<1, long long> C;
+    C.init();
+    const int nt = kout - n_lt;
+    if (full) {
+        for (int64_t c0 = 0; c0 < n; c0 += 64) {
+            const ScanCand x = c0 + lane < n ? gen(c0 + lane) : ScanCand{__builtin_inff(), PAD, PAD};
+            const bool ok = x.key == T && x.pos <= PM;
+            C.offer(ok ? 0.f : __builtin_inff(), ok ? x.label : PAD, nt - 1);
+        }
+    }
+    // 4. the result: every key < T (all keys when fewer than kout), then the chosen T-keys; (key, label) order
+    R.init();
+    for (int64_t c0 = 0; c0 < n; c0 += 64) {
+        const ScanCand x = c0 + lane < n ? gen(c0 + lane) : ScanCand{__builtin_inff(), PAD, PAD};
+        const bool ok = !(x.key == __builtin_inff()) && (!full || x.key < T);
+        R.offer(ok ? x.key : __builtin_inff(), ok ? x.label : PAD, kout - 1);
+    }
+    if (full) R.offer(lane < nt && C.id[0] != PAD ? T : __builtin_inff(), lane < nt ? C.id[0] : PAD, kout - 1);
+}
+
+// Probe rank of CSR row `row` for query q: its list (binary search of list_off) and that list's index among
+// the query's nprobe probes (-1 if none).
+__device__ __forceinline__ int ivf_probe_rank_of_row(int64_t row, const int64_t *__restrict__ list_off, int nlist,
+                                                     const int64_t *__restrict__ qprobes, int nprobe) {
+    int lo = 0, hi = nlist;  // list_off[lo] <= row < list_off[hi]
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (list_off[mid] <= row) lo = mid;
+        else hi = mid;
+    }
+    for (int p = 0; p < nprobe; ++p)
+        if (qprobes[p] == lo) return p;
+    return -1;
+}
+
 // ---------------------------------------------------------------------------------------------
 // ivf_rerank_topk — form kFormSplit2Exact.  The 2-term split-bf16 scan (≈2⁻¹⁶ relative per product)
 // only prunes; the results are exact.  Per query (one wave): merge the partial lists to the
@@ -1295,7 +1380,8 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
                 const float *__restrict__ codes, int d, const int64_t *__restrict__ ids, int64_t nrows,
                 int64_t label_offset, float xmax2, float *__restrict__ D, int64_t *__restrict__ I,
                 int *__restrict__ nflag, int *__restrict__ flagged, float eps, float rxmax,
-                const float *__restrict__ qres) {
+                const float *__restrict__ qres, const int64_t *__restrict__ probes,
+                const int64_t *__restrict__ list_off, int nlist) {
     const int64_t q = WV == 1 ? (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6) : (int64_t)blockIdx.x;
     if (q >= nq) return;
     const int lane = threadIdx.x & 63;
@@ -1434,6 +1520,21 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
     R.init();
     const long long lab = real ? (long long)(ids ? ids[myrow] : label_offset + myrow) : IdTraits<long long>::pad();
     R.offer(real ? mine : __builtin_inff(), lab, kout - 1);
+    // 3b. exact ties at the kout-th distance with more tied rows than slots left: FAISS's scan-order
+    // admission decides which tied labels stay (ivf_scan_order_topk).  Every row with distance <= the
+    // kout-th is among the candidates whenever the bound check below passes (they all have scan key
+    // <= dk + E < K16); a flagged query is redone by the fallback, which applies the same rule.
+    if (probes) {
+        const float T = readlane_f(R.d[0], kout - 1);
+        const int n_le = __popcll(__ballot(real && mine <= T));
+        if (!(T == __builtin_inff()) && n_le > kout) {
+            const int64_t pr = real && mine <= T
+                                   ? ivf_probe_rank_of_row(myrow, list_off, nlist, probes + q * nprobe, nprobe) : -1;
+            const long long pos = pr >= 0 ? ((long long)pr << 32) | (long long)myrow : IdTraits<long long>::pad();
+            const float mk = real ? mine : __builtin_inff();
+            ivf_scan_order_topk(64, kout, [&](int64_t) { return ScanCand{mk, pos, lab}; }, R);
+        }
+    }
     // 4. exactness check
     const float dk = readlane_f(R.d[0], kout - 1);
     float E;
@@ -1542,10 +1643,11 @@ ivf_fallback_scan(const int *__restrict__ nflag, const int *__restrict__ flagged
                         if (lane == r + u) mine = IP ? -a : a;
                     }
                 }
+                // (distance, CSR row): within a list the row is the scan position, so this list holds every
+                // distance below its kout-th and the EARLIEST rows at ties — what FAISS's admission keeps
                 const int64_t row = r0 + g + lane;
                 const bool ok = lane < nr && !(mine == __builtin_inff());
-                const long long lab = ok ? (long long)(ids ? ids[row] : label_offset + row) : IdTraits<long long>::pad();
-                L.offer(ok ? mine : __builtin_inff(), lab, kout - 1);
+                L.offer(ok ? mine : __builtin_inff(), ok ? (long long)row : IdTraits<long long>::pad(), kout - 1);
             }
         }
         sd[wv * 64 + lane] = L.d[0];
@@ -1567,20 +1669,25 @@ ivf_fallback_scan(const int *__restrict__ nflag, const int *__restrict__ flagged
 template <bool IP>
 __global__ void __launch_bounds__(256)
 ivf_fallback_merge(const int *__restrict__ nflag, const int *__restrict__ flagged, int nprobe, int kout,
-                   const float *__restrict__ fpd, const long long *__restrict__ fpi, float *__restrict__ D,
-                   int64_t *__restrict__ I, unsigned long long *__restrict__ total) {
+                   const float *__restrict__ fpd, const long long *__restrict__ fpi, const int64_t *__restrict__ ids,
+                   int64_t label_offset, float *__restrict__ D, int64_t *__restrict__ I,
+                   unsigned long long *__restrict__ total) {
     const int nf = *nflag;
     if (blockIdx.x == 0 && threadIdx.x == 0 && nf > 0) atomicAdd(total, (unsigned long long)nf);
     const int lane = threadIdx.x & 63;
     const float pad_d = IP ? -__builtin_inff() : __builtin_inff();
     for (int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); f < nf; f += (int64_t)gridDim.x * 4) {
+        // per-probe (distance, row) partials in probe order → FAISS's scan-order result (ivf_scan_order_topk)
         WaveList<1, long long> L;
-        L.init();
         const int64_t n = (int64_t)nprobe * kout;
-        for (int64_t c = lane; c - lane < n; c += 64) {
-            const bool v = c < n;
-            L.offer(v ? fpd[f * n + c] : __builtin_inff(), v ? fpi[f * n + c] : IdTraits<long long>::pad(), kout - 1);
-        }
+        ivf_scan_order_topk(n, kout, [&](int64_t c) {
+            const float key = fpd[f * n + c];
+            const long long row = fpi[f * n + c];
+            const bool ok = !(key == __builtin_inff()) && row != IdTraits<long long>::pad();
+            const long long p = c / kout;
+            return ScanCand{ok ? key : __builtin_inff(), ok ? (p << 32) | row : IdTraits<long long>::pad(),
+                            ok ? (long long)(ids ? ids[row] : label_offset + row) : IdTraits<long long>::pad()};
+        }, L);
         const int64_t q = flagged[f];
         if (lane < kout) {
             const bool pad = L.id[0] == IdTraits<long long>::pad() || L.d[0] == __builtin_inff();
@@ -1602,12 +1709,12 @@ void launch_ivf_fallback(const int *nflag, const int *flagged, int64_t nq, const
         hipLaunchKernelGGL(ivf_fallback_scan<true>, dim3(gs), dim3(256), 0, st, nflag, flagged, probes, nprobe, Q, codes,
                            d, list_off, list_len, nlist, ids, label_offset, kout, fpd, fpi);
         hipLaunchKernelGGL(ivf_fallback_merge<true>, dim3(gm), dim3(256), 0, st, nflag, flagged, nprobe, kout, fpd, fpi,
-                           D, I, total);
+                           ids, label_offset, D, I, total);
     } else {
         hipLaunchKernelGGL(ivf_fallback_scan<false>, dim3(gs), dim3(256), 0, st, nflag, flagged, probes, nprobe, Q,
                            codes, d, list_off, list_len, nlist, ids, label_offset, kout, fpd, fpi);
         hipLaunchKernelGGL(ivf_fallback_merge<false>, dim3(gm), dim3(256), 0, st, nflag, flagged, nprobe, kout, fpd,
-                           fpi, D, I, total);
+                           fpi, ids, label_offset, D, I, total);
     }
     HIPANN_CHECK(hipGetLastError());
 }
@@ -1619,14 +1726,15 @@ void launch_ivf_fallback(const int *nflag, const int *flagged, int64_t nq, const
 void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int nprobe, int64_t nq, int k, int kout,
                        int metric, const float *Q, const float *codes, int d, const int64_t *ids, int64_t nrows,
                        int64_t label_offset, float xmax2, float *D, int64_t *I, int *nflag, int *flagged,
-                       hipStream_t st, float eps, float rxmax, const float *qres) {
+                       hipStream_t st, float eps, float rxmax, const float *qres, const int64_t *probes,
+                       const int64_t *list_off, int nlist) {
     if (nq <= 0) return;
     HIPANN_REQUIRE(k >= kRerankK && k <= 64 && kout >= 1 && kout <= kRerankMaxK, "ivf rerank: k / kout out of range");
     // small batches: one 4-wave block per query (fills more of the chip, shorter per-query chain)
     const bool wide = nq < HIPANN_RR_WIDE;
     dim3 grid((unsigned)(wide ? nq : ceil_div(nq, 4))), block(256);
 #define RR_ARGS pd, pi, slot_off, nprobe, nq, k, kout, Q, codes, d, ids, nrows, label_offset, xmax2, D, I, nflag, flagged, \
-                eps, rxmax, qres
+                eps, rxmax, qres, probes, list_off, nlist
     if (metric == kIP) {
         if (wide) hipLaunchKernelGGL((ivf_rerank_topk<true, 4>), grid, block, 0, st, RR_ARGS);
         else hipLaunchKernelGGL((ivf_rerank_topk<true, 1>), grid, block, 0, st, RR_ARGS);

@@ -118,6 +118,47 @@ struct TimerPause {
     ~TimerPause() { t.on = was; }
 };
 
+// Orders a handle's calls across streams.  Every search / add of a shard runs its kernels on the caller's
+// stream (device API) or the shard's own (host API) and reuses the shard's scratch (plan counts, partial
+// lists, flags).  The handle mutex only covers enqueueing, so a call on another stream must not start
+// before the previous call's kernels are done with that scratch: each call waits for the event the
+// previous call recorded (when the streams differ) and records its own at the end.
+struct StreamFence {
+    hipEvent_t ev = nullptr;
+    hipStream_t last = nullptr;
+    bool armed = false;
+    int device = 0;
+    StreamFence() = default;
+    StreamFence(const StreamFence &) = delete;
+    StreamFence &operator=(const StreamFence &) = delete;
+    ~StreamFence() { if (ev) { DeviceGuard g(device); (void)hipEventDestroy(ev); } }
+    void enter(hipStream_t st) {
+        if (armed && st != last) HIPANN_CHECK(hipStreamWaitEvent(st, ev, 0));
+    }
+    void leave(hipStream_t st, int dev) {
+        if (!ev) {
+            DeviceGuard g(dev);
+            HIPANN_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            device = dev;
+        }
+        HIPANN_CHECK(hipEventRecord(ev, st));
+        last = st;
+        armed = true;
+    }
+};
+
+// enter() at construction, leave() when the scope ends (normally or by an exception: whatever was
+// enqueued before the throw is fenced too).
+struct FenceScope {
+    StreamFence &f;
+    hipStream_t st;
+    int dev;
+    FenceScope(StreamFence &ff, hipStream_t s, int d) : f(ff), st(s), dev(d) { f.enter(st); }
+    ~FenceScope() {
+        try { f.leave(st, dev); } catch (...) {}
+    }
+};
+
 enum class Kind { Flat = 1, IVF = 2 };
 
 // One contiguous row range of a Flat index resident on one device.
@@ -148,6 +189,7 @@ struct FlatShard {
     DevBuf xb16, qimg, seed;
     bool xb16_ok = false;
     float bf16_rxmax = 0.f;  // max over rows of ‖bf16(x) − x‖ (the rerank's bound)
+    StreamFence fence;       // cross-stream ordering of this shard's calls
 };
 
 struct IndexBase {
@@ -218,6 +260,7 @@ struct IvfShard {
     float half_rxmax = 0.f;
     DevBuf codes_h, hsplit, hits, hres;
     int max_nch = 1;  // largest list's row-chunk count
+    StreamFence fence;  // cross-stream ordering of this shard's calls (its coarse quantizer's scratch included)
 };
 
 struct IvfIndex : IndexBase {
@@ -284,7 +327,8 @@ int64_t ivf_mfma_bf_qsplit_bytes(int64_t nq, int d, int np);
 void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int nprobe, int64_t nq, int k, int kout,
                        int metric, const float *Q, const float *codes, int d, const int64_t *ids, int64_t nrows,
                        int64_t label_offset, float xmax2, float *D, int64_t *I, int *nflag, int *flagged,
-                       hipStream_t st, float eps = kSplit2Eps, float rxmax = -1.f, const float *qres = nullptr);
+                       hipStream_t st, float eps = kSplit2Eps, float rxmax = -1.f, const float *qres = nullptr,
+                       const int64_t *probes = nullptr, const int64_t *list_off = nullptr, int nlist = 0);
 // ivf_mfma.hip, fp16-image scan (kFormHalfExact)
 int ivf_mfma_h_group(int d);
 int64_t ivf_half_pass_bytes(int d);

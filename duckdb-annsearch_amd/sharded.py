@@ -69,9 +69,12 @@ class ShardedSearch:
     ``merge(gathered, nq, k) -> (D, I)``: merge of the [world][part_bytes] uint8 buffer (the GPU path
     passes ``merge_packed_device_torch``; CPU tests a host restatement via ``unpack_parts``).
     Works with any torch.distributed backend (nccl = RCCL on ROCm; gloo for CPU tests).
+    ``gather_at_world1``: run the collective + merge even with one rank (the RCCL path's own test on a
+    one-GPU box; a single rank otherwise returns its local top-k directly).
     """
 
-    def __init__(self, local_search: Callable, merge: Callable, nq: int, k: int, device, group=None):
+    def __init__(self, local_search: Callable, merge: Callable, nq: int, k: int, device, group=None,
+                 gather_at_world1: bool = False):
         import torch
         import torch.distributed as dist
 
@@ -84,15 +87,16 @@ class ShardedSearch:
         self.packed = torch.zeros(self.pb, dtype=torch.uint8, device=device)
         self.I = self.packed[: nq * k * 8].view(torch.int64).view(nq, k)
         self.D = self.packed[nq * k * 8: nq * k * 12].view(torch.float32).view(nq, k)
-        self.gathered = torch.empty((self.world, self.pb), dtype=torch.uint8, device=device) if self.world > 1 \
+        self.collective = self.world > 1 or (gather_at_world1 and dist.is_initialized())
+        self.gathered = torch.empty((self.world, self.pb), dtype=torch.uint8, device=device) if self.collective \
             else None
 
     def search(self, xq):
         import torch.distributed as dist
 
         self.local_search(xq, self.D, self.I)
-        if self.world == 1:
-            return self.D, self.I
+        if not self.collective:  # fresh tensors, as the merge returns (the packed buffer is reused)
+            return self.D.clone(), self.I.clone()
         if self.packed.is_cuda and dist.get_backend(self.group) == "nccl":
             # RCCL: one collective straight into the buffer the merge reads
             dist.all_gather_into_tensor(self.gathered.view(-1), self.packed, group=self.group)

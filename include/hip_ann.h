@@ -86,25 +86,35 @@ int hipann_flat_reconstruct_n(void *index, int64_t i0, int64_t n, float *out, ch
  * HIPANN_FLAT_FORM_SPLIT3: both operands split into three round-to-nearest bf16 terms, the
  * six products above 2^-26 relative on the bf16 matrix cores, fp32 accumulation — fp32-level products
  * at several times the fp32 rate.  HIPANN_FLAT_FORM_SPLIT2: two terms, three products (≈2^-16
- * relative per product; measurement only).  HIPANN_FLAT_FORM_SPLIT2_EXACT (default): the SPLIT2 scan
- * keeps the 16 best rows (32 for IP) per database split and query only as a filter; every returned distance is
+ * relative per product; measurement only).  HIPANN_FLAT_FORM_SPLIT2_EXACT: the SPLIT2 scan keeps the
+ * 16 best rows (32 for IP) per database split and query only as a filter; every returned distance is
  * recomputed in FAISS's direct fp32 form (Σ(q−x)² / q·x) and a per-query bound (|scan key − exact| ≤
  * 2^-12·(‖q‖² + max‖x‖²)) proves no pruned row reaches the top-k — queries that fail it re-run on
- * SPLIT3 (k ≤ 12; larger k use SPLIT3).  Returns 0, or -1 for a bad handle / form. */
+ * SPLIT3 (k ≤ 12; larger k use SPLIT3).  HIPANN_FLAT_FORM_BF16_EXACT (default): the same filter +
+ * rerank, the scan computing ONE bf16 product per element over a tiled bf16 image of the rows (built
+ * once); the bound is the Cauchy-Schwarz bound of the measured bf16 residuals.  Returns 0, or -1 for a
+ * bad handle / form. */
 #define HIPANN_FLAT_FORM_FP32 0
 #define HIPANN_FLAT_FORM_SPLIT3 1
 #define HIPANN_FLAT_FORM_SPLIT2 2
 #define HIPANN_FLAT_FORM_SPLIT2_EXACT 3
+#define HIPANN_FLAT_FORM_BF16_EXACT 4
 int hipann_flat_set_form(void *index, int form);
 int hipann_flat_get_form(void *index);
-/* Queries re-run on HIPANN_FLAT_FORM_SPLIT3 by the exact form's bound check since the index was created. */
+/* Queries the exact forms' bound check flagged since the index was created (each re-run on
+ * HIPANN_FLAT_FORM_SPLIT3; the exact results replace the flagged ones). */
 int64_t hipann_flat_rerank_fallbacks(void *index);
 
 /* ---------------------------------------------------------------------------------------------
  * Device-resident variants (inputs and outputs already in HBM).  Used by the multi-GPU sharded
  * search (one process per GPU, partial top-k gathered over RCCL) and by bench.py, whose timed
  * region starts with the inputs resident.  `stream` is a hipStream_t (NULL = the default/null
- * stream, HIP's convention and PyTorch's default stream); the call is asynchronous on that stream.
+ * stream, HIP's convention and PyTorch's default stream); the call is asynchronous on that stream:
+ * it returns with its kernels still queued (no host synchronisation, the exact forms' flagged queries
+ * included — they are re-run on the device).  Calls on one handle may use different streams: each call
+ * makes its stream wait for an event recorded at the end of the handle's previous call (the per-handle
+ * scratch is reused), so they execute in the order they were issued.  The caller still orders its own
+ * buffers (queries written / results read on other streams) with its own events.
  * ------------------------------------------------------------------------------------------- */
 
 /* Wrap (copy=0: borrow, caller keeps it alive) or copy (copy=1) an HBM matrix of n*d fp32 on
@@ -198,8 +208,9 @@ int hipann_ivf_export(void *index, float *centroids, int64_t *list_offsets, int6
 /* HIPANN_IVF_FORM_SPLIT2_EXACT: the SPLIT2 scan keeps the 16 best rows per list only as a
  * filter; every returned distance is recomputed in the direct form Σ(q−x)² (IP: q·x) in fp32, ordered by
  * (distance, label), and a per-query bound (|scan key − exact| ≤ 2^-12·(‖q‖² + max‖x‖²)) proves that no
- * pruned row could enter the top-k — queries that fail it are re-run on SPLIT3.  k ≤ 12 (larger k: SPLIT3).
- * The search call then synchronises its stream once (the flag count). */
+ * pruned row could enter the top-k — queries that fail it are re-run ON THE DEVICE over their probe lists
+ * in the direct form (ivf_fallback_scan / _merge: grids bounded by the device flag count, no host
+ * readback), so the call stays asynchronous.  k ≤ 12 (larger k: SPLIT3). */
 #define HIPANN_IVF_FORM_SPLIT2_EXACT 5
 /* HIPANN_IVF_FORM_HALF_EXACT (default): the same filter + exact rerank, the scan reading a tiled fp16
  * image of the rows (built once: x·2^s, round to nearest even, half the bytes of the fp32 forms) against
@@ -209,7 +220,8 @@ int hipann_ivf_export(void *index, float *centroids, int64_t *list_offsets, int6
 #define HIPANN_IVF_FORM_HALF_EXACT 6
 int hipann_ivf_set_form(void *index, int form);
 int hipann_ivf_get_form(void *index);
-/* Queries re-run on HIPANN_IVF_FORM_SPLIT3 by the exact form's bound check since the index was created. */
+/* Queries the exact forms' bound check flagged since the index was created (each re-run on the device in
+ * the direct form; reading the device-side count synchronises the device). */
 int64_t hipann_ivf_rerank_fallbacks(void *index);
 
 /* ---------------------------------------------------------------------------------------------

@@ -4,6 +4,9 @@ The benchmark configurations themselves (10M rows) are far beyond what the oracl
 each test runs the same code path at the largest shape the oracle checks quickly, with the same data
 model, the same build (GPU k-means / k-NN graph / SQ8 codec) and the same batch:
 
+* C1  Flat L2 10k × 128, k = 10 (the full C1 shape, the faiss-metal test inputs): the host-pointer C ABI
+      (hipann_flat_search, the call the extension's FaissIndex::Search makes) at nq = 1 and nq = 1000;
+      ids bit-identical to the oracle's CPU path (FAISS IndexFlatL2::search restatement).
 * C2  Flat L2 1M × 768, nq = 1024, k = 10 (the full C2 shape): every form through the device API the
       bench uses; the oracle (FAISS BLAS-path restatement) on a 256-query subset.
 * C3  IVFFlat nlist = 1024, nprobe = 32, d = 768, nq = 1024, k = 10 on 200k rows of the bench's
@@ -38,6 +41,41 @@ def _dev_search(index, xq_t, k, torch):
     index.search_device(nq, xq_t.data_ptr(), k, D.data_ptr(), I.data_ptr(), torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     return D.cpu().numpy(), I.cpu().numpy()
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+def test_c1_flat_10k_128(gpu, oracle, metric):
+    """C1 (BASELINE configs[0]): 10k × 128, k = 10, at the extension's real call shape — FaissIndex::Search
+    calls search(1, …) (src/faiss_index.cpp:737) — and as one 1000-query batch (SearchBatch, SURVEY §8f
+    rank 1).  The CPU path the GPU must reproduce is FAISS's IndexFlatL2::search: the direct form at nq = 1,
+    the BLAS form at nq = 1000.  nq = 1: ids identical to the oracle's, bit for bit (both direct form).
+    nq = 1000: the BLAS form's dot products depend on the BLAS library's summation order (the oracle's
+    restatement has its own, OpenBLAS another), so ids are identical except where two rows' fp64 distances
+    lie within the parity rule's tie window (IP on this data: 1 query of 1000 at r03)."""
+    from _data import faiss_metal_case
+
+    xb, xq = faiss_metal_case(10_000, 1000, 128)
+    ix = gpu.HipIndexFlat(128, metric, xb)
+    # nq = 1: one call per query, as the per-query loops of ann_search.cpp:320-333 / :610-621 issue them
+    D1 = np.empty((100, 10), np.float32)
+    I1 = np.empty((100, 10), np.int64)
+    for i in range(100):
+        D1[i:i + 1], I1[i:i + 1] = ix.search(xq[i:i + 1], 10)
+    Io1 = np.empty_like(I1)
+    Do1 = np.empty_like(D1)
+    for i in range(100):  # the oracle at nq = 1 (direct fvec_L2sqr / inner product form)
+        Do1[i:i + 1], Io1[i:i + 1] = oracle.flat_search(xb, xq[i:i + 1], 10, metric)
+    assert np.array_equal(I1, Io1), f"nq=1 ids differ on {(I1 != Io1).any(axis=1).sum()} queries"
+    assert np.allclose(D1, Do1, rtol=2e-6, atol=1e-6)
+    # nq = 1000: the BLAS-form path (FAISS: nq >= distance_compute_blas_threshold)
+    D, I = ix.search(xq, 10)
+    Do, Io = oracle.flat_search(xb, xq, 10, metric)
+    st = check_topk_parity(xb, xq, D, I, Do, Io, metric)
+    assert st["exact_fraction"] >= 0.999, st
+    # a batch equals the loop of single-query calls (SearchBatch vs Search, SURVEY §8f rank 1), up to the same
+    # tie window (direct vs BLAS form)
+    check_topk_parity(xb, xq[:100], D[:100], I[:100], D1, I1, metric)
+    ix.close()
 
 
 @pytest.fixture(scope="module")
@@ -130,6 +168,39 @@ def test_c3_ivf_nlist1024_nprobe32_d768_nq1024(gpu, c3_index, c3_oracle, form):
         v = I[same] >= 0
         assert np.allclose(D[same][v], Do[same][v], rtol=2e-6, atol=1e-6)
     index.form = 6
+
+
+@pytest.mark.parametrize("form", [6, 5])
+def test_c3_duplicate_rows_faiss_tie_order(gpu, c3_index, oracle, form):
+    """C3 shape with exact ties: every stored row of the C3 lists appears twice more in its list (the copies
+    in reversed row order) under scattered labels — 600k rows, nlist 1024, nprobe 32, d 768, nq 1024.  FAISS's
+    IVF scanner keeps, among rows tied at the 10th distance, the smallest labels among the earliest tied rows
+    in scan order; the GPU (rerank, or the device fallback for flagged queries) must equal the oracle slot for
+    slot on every query whose probe list is the oracle's (reference edge case: duplicates,
+    test/sql/edge_cases.test:75-83)."""
+    import torch
+
+    index0, info, xb, xq_t, xq, (cen, off0, ids0, codes0) = c3_index
+    nlist = len(cen)
+    off = off0 * 3
+    parts = []
+    for l in range(nlist):
+        c = codes0[off0[l]:off0[l + 1]]
+        parts += [c, c[::-1], c]
+    codes = np.ascontiguousarray(np.concatenate(parts))
+    rng = np.random.default_rng(11)
+    labels = (rng.permutation(len(codes)).astype(np.int64) * 5 + 3)
+    ix = gpu.HipIndexIVFFlat(cen, off, labels, codes, 32, 0)
+    ix.form = form
+    D, I = ix.search(xq, 10)
+    Do, Io, Po = oracle.ivf_search(cen, off, labels, codes, xq, 10, 32, 0)
+    same = check_probe_parity(cen, xq, ix.last_probes(len(xq)), Po, 0)
+    assert same.mean() >= 0.99, same.mean()
+    exact = float((I[same] == Io[same]).mean())
+    assert exact == 1.0, f"{(I[same] != Io[same]).any(axis=1).sum()} queries differ"
+    v = I[same] >= 0
+    assert np.allclose(D[same][v], Do[same][v], rtol=2e-6, atol=1e-6)
+    ix.close()
 
 
 def _c4_graph(gpu, n, d, R, seed, integer=False):

@@ -285,3 +285,95 @@ def test_sharded_hip_world2_on_one_device(gpu, oracle, tmp_path, workload):
         assert (a[:, 0] == lab).mean() > 0.999
         Do, Io, _ = oracle.ivf_search(cen, off, ids, codes, xq, 10, 8)
     check_topk_parity(xb, xq, r0["D"], r0["I"], Do, Io, 0)
+
+
+# ------------------------------------------------------------------------------------------------
+# RCCL: the all_gather_into_tensor branch of ShardedSearch (one rank: the box has one GPU)
+# ------------------------------------------------------------------------------------------------
+def _worker_rccl(rank, world, port, result_path):
+    sys.path.insert(0, str(ROOT))
+    sys.path.insert(0, str(ROOT / "duckdb-annsearch_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    import hipann
+    import bench
+    from sharded import ShardedSearch, merge_packed_device_torch
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    assert dist.get_backend() == "nccl"
+    n, d, nq, k = 50_000, 128, 64, 10
+    xb = torch.empty((n, d), device=dev)
+    bench.gen_uniform_rows(torch, xb, 0, 42)
+    xq = bench.uniform_queries(torch, nq, d, dev)
+    index = hipann.HipIndexFlatDevice(d, 0, xb.data_ptr(), n, 0, copy=False)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def local(q, D, I):
+        index.search_device(nq, q.data_ptr(), k, D.data_ptr(), I.data_ptr(), stream)
+
+    s = ShardedSearch(local, merge_packed_device_torch(hipann, 0), nq, k, dev, gather_at_world1=True)
+    assert s.collective and s.gathered.shape[0] == world
+    D, I = s.search(xq)
+    # the same search without the collective
+    Dl = torch.empty((nq, k), device=dev)
+    Il = torch.empty((nq, k), device=dev, dtype=torch.int64)
+    local(xq, Dl, Il)
+    torch.cuda.synchronize()
+    np.savez(result_path, D=D.cpu().numpy(), I=I.cpu().numpy(), Dl=Dl.cpu().numpy(), Il=Il.cpu().numpy(),
+             gathered=s.gathered.cpu().numpy(), packed=s.packed.cpu().numpy())
+    index.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_rccl_all_gather_world1(gpu, tmp_path):
+    """the RCCL branch of ShardedSearch.search (all_gather_into_tensor over the nccl backend,
+    sharded.py) executes on the box — one rank on its one GPU, the packed top-k gathered by RCCL and merged by
+    hipann_merge_topk_packed_device; the result equals the rank's own search, byte for byte."""
+    import torch.multiprocessing as mp
+
+    out = tmp_path / "rccl.npz"
+    mp.spawn(_worker_rccl, args=(1, _free_port(), str(out)), nprocs=1, join=True)
+    r = np.load(out)
+    assert np.array_equal(r["gathered"][0], r["packed"])  # RCCL moved the packed buffer unchanged
+    assert np.array_equal(r["I"], r["Il"]) and np.array_equal(r["D"], r["Dl"])
+
+
+def test_bench_spawner_gloo_world2():
+    """`bench.py --gpus 2` without a launcher starts the two ranks itself (torch.distributed.run
+    child, no re-exec) — here the CPU self-test workload over gloo: both ranks rendezvous, all-gather their ranks
+    and run the barrier / max-over-ranks timing; rank 0 prints one JSON line."""
+    import json
+    import subprocess
+
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    env.pop("LOCAL_RANK", None)
+    env["OMP_NUM_THREADS"] = "1"
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--workload", "selftest", "--steps",
+                        "5", "--warmup", "1"], capture_output=True, text=True, timeout=300, env=env, cwd=str(ROOT))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    js = json.loads(lines[0])
+    assert js["n_gpus"] == 2 and js["world_check"]["ranks_seen"] == [0, 1]
+    assert js["world_check"]["backend"] == "gloo" and js["steps"] == 5
+
+
+def test_bench_selftest_world1():
+    """--gpus 1 stays one process (no spawner): the self-test line at N = 1."""
+    import json
+    import subprocess
+
+    env = dict(os.environ)
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(v, None)
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "1", "--workload", "selftest", "--steps",
+                        "3", "--warmup", "1"], capture_output=True, text=True, timeout=300, env=env, cwd=str(ROOT))
+    assert r.returncode == 0, r.stderr[-3000:]
+    js = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert js["n_gpus"] == 1 and js["world_check"]["ranks_seen"] == [0]
