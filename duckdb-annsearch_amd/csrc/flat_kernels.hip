@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <type_traits>
 #include <cstdlib>
+#include <utility>
 
 namespace hipann {
 
@@ -862,24 +863,31 @@ merge_parts_topk(const float *__restrict__ pd, const InId *__restrict__ pi, int 
     WaveList<S, long long> L;
     L.init();
     const int64_t total = (int64_t)nparts * k;
-    for (int64_t c0 = 0; c0 < total; c0 += 64) {
-        const int64_t c = c0 + lane;
-        float key = __builtin_inff();
-        long long lab = IdTraits<long long>::pad();
-        if (c < total) {
-            const int64_t p = c / k, i = c - p * k;
-            const InId raw = pi[p * pstride_i + q * k + i];
-            const float v = pd[p * pstride_d + q * k + i] * in_sign;
-            // int32 partials pad with 0x7fffffff; int64 (global label) partials only with negatives, so a
-            // real label 2^31 - 1 (arbitrary IVF ids, > 2^31 rows) is kept
-            bool pad_in = raw < 0;
-            if constexpr (sizeof(InId) == 4) pad_in = pad_in || raw == (InId)0x7fffffff;
-            if (!pad_in && !(v == __builtin_inff())) {
-                key = v;
-                lab = (long long)raw + label_offset;
+    constexpr int MU = 4;  // 64-candidate chunks loaded ahead of their offers
+    for (int64_t c0 = 0; c0 < total; c0 += 64 * MU) {
+        float key[MU];
+        long long lab[MU];
+#pragma unroll
+        for (int u = 0; u < MU; ++u) {
+            const int64_t c = c0 + 64 * u + lane;
+            key[u] = __builtin_inff();
+            lab[u] = IdTraits<long long>::pad();
+            if (c < total) {
+                const int64_t p = c / k, i = c - p * k;
+                const InId raw = pi[p * pstride_i + q * k + i];
+                const float v = pd[p * pstride_d + q * k + i] * in_sign;
+                // int32 partials pad with 0x7fffffff; int64 (global label) partials only with negatives, so a
+                // real label 2^31 - 1 (arbitrary IVF ids, > 2^31 rows) is kept
+                bool pad_in = raw < 0;
+                if constexpr (sizeof(InId) == 4) pad_in = pad_in || raw == (InId)0x7fffffff;
+                if (!pad_in && !(v == __builtin_inff())) {
+                    key[u] = v;
+                    lab[u] = (long long)raw + label_offset;
+                }
             }
         }
-        L.offer(key, lab, kout - 1);
+#pragma unroll
+        for (int u = 0; u < MU; ++u) L.offer(key[u], lab[u], kout - 1);
     }
     const float pad_d = out_sign > 0.f ? __builtin_inff() : -__builtin_inff();
 #pragma unroll
@@ -890,6 +898,104 @@ merge_parts_topk(const float *__restrict__ pd, const InId *__restrict__ pi, int 
             D[q * kout + e] = pad ? pad_d : L.d[s] * out_sign;
             I[q * kout + e] = pad ? -1 : (int64_t)L.id[s];
         }
+    }
+}
+
+// merge_parts_stage1 — the first level of a two-level merge (many parts, few queries: the direct scan's
+// 8192 per-wave lists at nq = 1 kept ONE wave busy for ~1 ms).  Wave (g, q) merges parts
+// [g·ppg, (g+1)·ppg) of query q into one (key, label) list of kout written to [g][q][kout] (labels global,
+// pads (+inf, −1)); merge_parts_topk then merges the G group lists.  Lexicographic top-k is associative,
+// so the result equals the one-level merge.
+template <typename InId>
+__global__ void __launch_bounds__(256)
+merge_parts_stage1(const float *__restrict__ pd, const InId *__restrict__ pi, int nparts, int64_t nq, int k, int kout,
+                   int64_t label_offset, float in_sign, int ppg, int ngroups, float *__restrict__ md,
+                   long long *__restrict__ mi) {
+    const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= (int64_t)ngroups * nq) return;
+    const int64_t q = w % nq, g = w / nq;
+    const int lane = threadIdx.x & 63;
+    const int p0 = (int)g * ppg, p1 = p0 + ppg < nparts ? p0 + ppg : nparts;
+    const int64_t total = (int64_t)(p1 - p0) * k;
+    WaveList<1, long long> L;
+    L.init();
+    constexpr int MU = 4;
+    for (int64_t c0 = 0; c0 < total; c0 += 64 * MU) {
+        float key[MU];
+        long long lab[MU];
+#pragma unroll
+        for (int u = 0; u < MU; ++u) {
+            const int64_t c = c0 + 64 * u + lane;
+            key[u] = __builtin_inff();
+            lab[u] = IdTraits<long long>::pad();
+            if (c < total) {
+                const int64_t p = p0 + c / k, i = c % k;
+                const InId raw = pi[(p * nq + q) * k + i];
+                const float v = pd[(p * nq + q) * k + i] * in_sign;
+                bool pad_in = raw < 0;
+                if constexpr (sizeof(InId) == 4) pad_in = pad_in || raw == (InId)0x7fffffff;
+                if (!pad_in && !(v == __builtin_inff())) {
+                    key[u] = v;
+                    lab[u] = (long long)raw + label_offset;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < MU; ++u) L.offer(key[u], lab[u], kout - 1);
+    }
+    if (lane < kout) {
+        const bool pad = L.id[0] == IdTraits<long long>::pad();
+        md[w * kout + lane] = pad ? __builtin_inff() : L.d[0];
+        mi[w * kout + lane] = pad ? -1 : L.id[0];
+    }
+}
+
+// merge_groups_block — the second level: one 4-wave block per query, each wave merging a quarter of the
+// ngroups group lists ([g][q][kout], global labels, −1 pads), wave 0 merging the four wave lists through LDS.
+__global__ void __launch_bounds__(256)
+merge_groups_block(const float *__restrict__ md, const long long *__restrict__ mi, int ngroups, int64_t nq, int kout,
+                   float out_sign, float *__restrict__ D, int64_t *__restrict__ I) {
+    __shared__ float sd[4 * 64];
+    __shared__ long long si[4 * 64];
+    const int64_t q = blockIdx.x;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int g0 = (int)((int64_t)ngroups * wv / 4), g1 = (int)((int64_t)ngroups * (wv + 1) / 4);
+    const int64_t total = (int64_t)(g1 - g0) * kout;
+    WaveList<1, long long> L;
+    L.init();
+    constexpr int MU = 4;
+    for (int64_t c0 = 0; c0 < total; c0 += 64 * MU) {
+        float key[MU];
+        long long lab[MU];
+#pragma unroll
+        for (int u = 0; u < MU; ++u) {
+            const int64_t c = c0 + 64 * u + lane;
+            key[u] = __builtin_inff();
+            lab[u] = IdTraits<long long>::pad();
+            if (c < total) {
+                const int64_t g = g0 + c / kout, i = c % kout;
+                const long long raw = mi[(g * nq + q) * kout + i];
+                const float v = md[(g * nq + q) * kout + i];
+                if (raw >= 0 && !(v == __builtin_inff())) {
+                    key[u] = v;
+                    lab[u] = raw;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < MU; ++u) L.offer(key[u], lab[u], kout - 1);
+    }
+    sd[wv * 64 + lane] = L.d[0];
+    si[wv * 64 + lane] = L.id[0];
+    __syncthreads();
+    if (wv != 0) return;
+    L.init();
+#pragma unroll
+    for (int w = 0; w < 4; ++w) L.offer(sd[w * 64 + lane], si[w * 64 + lane], kout - 1);
+    if (lane < kout) {
+        const bool pad = L.id[0] == IdTraits<long long>::pad();
+        D[q * kout + lane] = pad ? (out_sign > 0.f ? __builtin_inff() : -__builtin_inff()) : L.d[0] * out_sign;
+        I[q * kout + lane] = pad ? -1 : (int64_t)L.id[0];
     }
 }
 
@@ -1375,6 +1481,92 @@ flat_keys_small(const float *__restrict__ Q, const float *__restrict__ qnorm, in
     }
 }
 
+// flat_keys_direct — the same 64 × 64 tiles, MFMAs and k order as flat_keys_small (bit-identical keys), but every
+// wave loads its own A / B fragments straight from memory into a 3-chunk register ring: no LDS staging, no
+// per-chunk barrier.  The inputs are small and cache-resident (the coarse quantizer's queries and centroids),
+// so the doubled L2 reads cost little, while the 4 waves — one per SIMD — no longer wait on each other
+// (flat_keys_small: 32 µs for 1024 × 1024 × 768, ≈ 3× its MFMA time).
+template <bool VEC4>
+__device__ __forceinline__ void keys_frag_load(const float *__restrict__ base, int64_t row, int d, int k0,
+                                               float4 (&r)[4]) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int kk = k0 + 4 * u;
+        const float *src = base + row * (int64_t)d + kk;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (VEC4) {
+            if (kk < d) v = *reinterpret_cast<const float4 *>(src);
+        } else {
+            if (kk + 0 < d) v.x = src[0];
+            if (kk + 1 < d) v.y = src[1];
+            if (kk + 2 < d) v.z = src[2];
+            if (kk + 3 < d) v.w = src[3];
+        }
+        r[u] = v;
+    }
+}
+
+template <bool VEC4, int KR>
+__global__ void __launch_bounds__(256)
+flat_keys_direct(const float *__restrict__ Q, const float *__restrict__ qnorm, int64_t nq, const float *__restrict__ X,
+                 const float *__restrict__ xnorm, int64_t N, int d, int metric, int nqt, float *__restrict__ keys_out,
+                 int64_t ldk) {
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int qt = lb % nqt;
+    const int64_t q0 = (int64_t)qt * SBM, x0 = (int64_t)(lb / nqt) * SBM;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wr = wave >> 1, wc = wave & 1;
+    const int l31 = lane & 31, h = lane >> 5;
+    const int nk = (d + GBK - 1) / GBK;
+    // this lane's fragment rows (rows past the end re-read the last row; their keys are never written)
+    int64_t qa = q0 + 32 * wr + l31, xb = x0 + 32 * wc + l31;
+    qa = qa < nq ? qa : nq - 1;
+    xb = xb < N ? xb : N - 1;
+    constexpr int R = KR;
+    float4 ra[R][4], rb[R][4];
+#pragma unroll
+    for (int s = 0; s < R; ++s)
+        if (s < nk) {
+            keys_frag_load<VEC4>(Q, qa, d, s * GBK + 16 * h, ra[s]);
+            keys_frag_load<VEC4>(X, xb, d, s * GBK + 16 * h, rb[s]);
+        }
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    auto step = [&](int kc, auto slot_c) {
+        constexpr int S = decltype(slot_c)::value;  // kc % R
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[S][u][e], rb[S][u][e], acc, 0, 0, 0);
+        if (kc + R < nk) {
+            keys_frag_load<VEC4>(Q, qa, d, (kc + R) * GBK + 16 * h, ra[S]);
+            keys_frag_load<VEC4>(X, xb, d, (kc + R) * GBK + 16 * h, rb[S]);
+        }
+    };
+    for (int kc = 0; kc < nk; kc += R) {
+        [&]<int... P>(std::integer_sequence<int, P...>) {
+            ((kc + P < nk ? step(kc + P, std::integral_constant<int, P>{}) : void()), ...);
+        }(std::make_integer_sequence<int, R>{});
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int64_t q = q0 + 32 * wr + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int64_t x = x0 + 32 * wc + l31;
+        if (q < nq && x < N) {
+            const float ip = acc[r];
+            float key;
+            if (metric == kL2) {
+                key = fmaf(-2.f, ip, qnorm[q] + xnorm[x]);
+                key = key < 0.f ? 0.f : key;
+            } else {
+                key = -ip;
+            }
+            keys_out[q * ldk + x] = key;
+        }
+    }
+}
+
 // Word copy between device memory and the device mapping of pinned host buffers (small host-pointer
 // calls: no DMA-engine round trips for the query upload and the result download).
 __global__ void __launch_bounds__(256) copy_words(const unsigned *__restrict__ src, unsigned *__restrict__ dst,
@@ -1408,8 +1600,19 @@ void launch_flat_gemm_keys(const float *Q, const float *qn, int64_t nq, const fl
         const int sq = (int)ceil_div(nq, SBM);
         const int64_t blocks = (int64_t)sq * ceil_div(N, SBM);
         dim3 g((unsigned)blocks), b(256);
-        if (vec4) hipLaunchKernelGGL(flat_keys_small<true>, g, b, 0, st, Q, qn, nq, X, xn, N, d, metric, sq, keys, ldk);
-        else hipLaunchKernelGGL(flat_keys_small<false>, g, b, 0, st, Q, qn, nq, X, xn, N, d, metric, sq, keys, ldk);
+        // HIPANN_KEYS = 0 (default): LDS-staged (flat_keys_small, 29.7 µs for 1024 × 1024 × 768); 3 / 6: the
+        // register-ring flat_keys_direct with that many chunks in flight (A/B: 34.0 / 35.7 µs)
+        static const int mode = [] { const char *e = std::getenv("HIPANN_KEYS"); return e ? std::atoi(e) : 0; }();
+        if (mode == 3) {
+            if (vec4) hipLaunchKernelGGL((flat_keys_direct<true, 3>), g, b, 0, st, Q, qn, nq, X, xn, N, d, metric, sq, keys, ldk);
+            else hipLaunchKernelGGL((flat_keys_direct<false, 3>), g, b, 0, st, Q, qn, nq, X, xn, N, d, metric, sq, keys, ldk);
+        } else if (mode == 6) {
+            if (vec4) hipLaunchKernelGGL((flat_keys_direct<true, 6>), g, b, 0, st, Q, qn, nq, X, xn, N, d, metric, sq, keys, ldk);
+            else hipLaunchKernelGGL((flat_keys_direct<false, 6>), g, b, 0, st, Q, qn, nq, X, xn, N, d, metric, sq, keys, ldk);
+        } else {
+            if (vec4) hipLaunchKernelGGL(flat_keys_small<true>, g, b, 0, st, Q, qn, nq, X, xn, N, d, metric, sq, keys, ldk);
+            else hipLaunchKernelGGL(flat_keys_small<false>, g, b, 0, st, Q, qn, nq, X, xn, N, d, metric, sq, keys, ldk);
+        }
         HIPANN_CHECK(hipGetLastError());
         return;
     }
@@ -1583,6 +1786,25 @@ void launch_merge_parts(const float *pd, const InId *pi, int nparts, int64_t nq,
 #undef HIPANN_MERGE_CASE
     throw HipError("merge: k too large");
 }
+
+template <typename InId>
+void launch_merge_parts_2level(const float *pd, const InId *pi, int nparts, int64_t nq, int k, int kout,
+                               int64_t label_offset, float in_sign, float out_sign, float *D, int64_t *I, float *md,
+                               long long *mi, int ngroups, hipStream_t st) {
+    if (nq <= 0) return;
+    HIPANN_REQUIRE(kout <= 64 && ngroups >= 1, "2-level merge: kout <= 64");
+    const int ppg = (int)ceil_div(nparts, ngroups);
+    ngroups = (int)ceil_div(nparts, ppg);
+    hipLaunchKernelGGL((merge_parts_stage1<InId>), dim3((unsigned)ceil_div((int64_t)ngroups * nq, 4)), dim3(256), 0,
+                       st, pd, pi, nparts, nq, k, kout, label_offset, in_sign, ppg, ngroups, md, mi);
+    HIPANN_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(merge_groups_block, dim3((unsigned)nq), dim3(256), 0, st, md, mi, ngroups, nq, kout, out_sign, D,
+                       I);
+    HIPANN_CHECK(hipGetLastError());
+}
+
+template void launch_merge_parts_2level<int>(const float *, const int *, int, int64_t, int, int, int64_t, float, float,
+                                             float *, int64_t *, float *, long long *, int, hipStream_t);
 
 template void launch_merge_parts<int>(const float *, const int *, int, int64_t, int, int, int64_t, float, float,
                                       float *, int64_t *, hipStream_t, int64_t, int64_t);

@@ -236,7 +236,9 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
     const int d = ix.d, metric = ix.metric;
     const float out_sign = metric == kIP ? -1.f : 1.f;
     HIPANN_REQUIRE(k <= HIPANN_MAX_K, "k larger than HIPANN_MAX_K");
-    sh.qn_of = nullptr;  // set below when this call computes ‖q‖² into sh.qn
+    // set below when this call computes ‖q‖² into sh.qn (or already: the caller prepared it, qn_given)
+    sh.qn_of = sh.qn_given == xq && sh.qn_given_nq == nq ? xq : nullptr;
+    sh.qn_nq = nq;
     if (nq <= 0) return;
     if (sh.n == 0) {  // no rows: pads only
         launch_merge_parts<int>(nullptr, nullptr, 0, nq, k, kout, sh.label_offset, 1.f, out_sign, D, I, st);
@@ -253,8 +255,10 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
         (nq < kBlasThreshold && sh.n <= 1024 && kout <= 64 && scan_smem_bytes((int)nq, d) <= 64 * 1024)) {
         const float *qn = nullptr;
         if (nq >= kBlasThreshold && metric == kL2) {
-            sh.qn.ensure((size_t)nq * sizeof(float), sh.device);
-            launch_row_norms(xq, nq, d, sh.qn.get<float>(), st);
+            if (!(sh.qn_given == xq && sh.qn_given_nq == nq)) {
+                sh.qn.ensure((size_t)nq * sizeof(float), sh.device);
+                launch_row_norms(xq, nq, d, sh.qn.get<float>(), st);
+            }
             qn = sh.qn.get<float>();
             sh.qn_of = xq;
             sh.qn_nq = nq;
@@ -280,6 +284,17 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
                                   sh.part_i.get<int>(), st);
         }
         ScopedTiming t(ix.timer_merge, st);
+        if (nw_alloc > 256) {
+            // thousands of per-wave lists: groups of ~32 merged by one wave each, then the group lists by one
+            // 4-wave block per query (one wave per query took ~1 ms for 8192 lists at 10M rows, nq = 1)
+            const int groups = (int)std::min<int64_t>(256, ceil_div(nw_alloc, 32));
+            sh.mid_d.ensure(sizeof(float) * (size_t)groups * nq * kout, sh.device);
+            sh.mid_i.ensure(sizeof(long long) * (size_t)groups * nq * kout, sh.device);
+            launch_merge_parts_2level<int>(sh.part_d.get<float>(), sh.part_i.get<int>(), (int)nw_alloc, nq, k, kout,
+                                           sh.label_offset, 1.f, out_sign, D, I, sh.mid_d.get<float>(),
+                                           sh.mid_i.get<long long>(), groups, st);
+            return;
+        }
         launch_merge_parts<int>(sh.part_d.get<float>(), sh.part_i.get<int>(), (int)nw_alloc, nq, k, kout,
                                 sh.label_offset, 1.f, out_sign, D, I, st);
         return;
@@ -287,8 +302,10 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
     // BLAS form: ‖q‖² + ‖x‖² − 2 q·x on fp32 MFMA
     const float *qn = nullptr;
     if (metric == kL2) {
-        sh.qn.ensure((size_t)nq * sizeof(float), sh.device);
-        launch_row_norms(xq, nq, d, sh.qn.get<float>(), st);
+        if (!(sh.qn_given == xq && sh.qn_given_nq == nq)) {
+            sh.qn.ensure((size_t)nq * sizeof(float), sh.device);
+            launch_row_norms(xq, nq, d, sh.qn.get<float>(), st);
+        }
         qn = sh.qn.get<float>();
         sh.qn_of = xq;
         sh.qn_nq = nq;

@@ -239,26 +239,6 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
                 (void)hipMemsetAsync(sh.ccnt.p, 0, sizeof(int) * (size_t)nlist, st);
         }
     } ccnt_reset{sh, nlist, st, true};
-    // the plan's per-query count step rides on the coarse probe select when that path is taken
-    IvfPlanHook hook{sh.list_len.get<int>(), nlist, ivf_chunk_rows(), sh.ccnt.get<int>(), sh.slot_off.get<int>(),
-                     sh.qtot.get<int>(), false};
-    FlatShard &qsh = *sh.quant->shards[0];
-    qsh.plan_hook = ivf_plan_query_major() ? &hook : nullptr;
-    try {
-        flat_shard_search(*sh.quant, qsh, nq, xq, np, np, sh.coarse_d.get<float>(), sh.coarse_i.get<int64_t>(), st);
-    } catch (...) {
-        qsh.plan_hook = nullptr;
-        throw;
-    }
-    qsh.plan_hook = nullptr;
-    // 2. list-major work plan
-    sh.cnt.ensure(sizeof(int) * (nlist + 1), sh.device);
-    sh.bucket_off.ensure(sizeof(int) * (nlist + 1), sh.device);
-    sh.item_off.ensure(sizeof(int) * (nlist + 1), sh.device);
-    sh.cursor.ensure(sizeof(int) * (nlist + 1), sh.device);
-    sh.bucket.ensure(sizeof(int) * (size_t)nq * np, sh.device);
-    HIPANN_REQUIRE((int64_t)nq * np < (int64_t)0x7fffffff, "nq * nprobe too large");
-    sh.slot_off.ensure(sizeof(int) * ((size_t)nq * np + 1), sh.device);
     // the decomposed form needs float4 rows; other shapes take the direct kernel (also on the GPU)
     // the decomposed forms need float4 rows (else the direct kernel, also on the GPU); the MFMA kernel
     // keeps 16-lane lists (k <= 16) and the item's queries in LDS (else the VALU decomposed kernel)
@@ -295,6 +275,45 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
         sh.qbound.ensure(sizeof(unsigned) * (size_t)nq, sh.device);
         qbound = sh.qbound.get<unsigned>();
     }
+    // the batch's query preparation, one launch before the coarse step (fp16 form): the fp16 query terms, 1/(t·s),
+    // the split residuals and ‖q‖² (row_norms_f32's bits) for the coarse quantizer and the scan
+    FlatShard &qsh0 = *sh.quant->shards[0];
+    if (half) {
+        sh.hsplit.ensure((size_t)ivf_half_qsplit_bytes(nq, d), sh.device);
+        sh.hits.ensure(sizeof(float) * (size_t)nq, sh.device);
+        sh.hres.ensure(sizeof(float) * (size_t)nq, sh.device);
+        float *qn_out = nullptr;
+        if (metric == kL2) {  // the quantizer's BLAS-form paths (nq >= 20) and the scan's L2 keys read ‖q‖²
+            qsh0.qn.ensure(sizeof(float) * (size_t)nq, sh.device);
+            qn_out = qsh0.qn.get<float>();
+        }
+        launch_ivf_split_queries_h(xq, nq, d, sh.half_es, sh.hsplit.p, sh.hits.get<float>(), sh.hres.get<float>(), qn_out,
+                                   st);
+        qsh0.qn_given = qn_out ? xq : nullptr;
+        qsh0.qn_given_nq = nq;
+    }
+    // the plan's per-query count step rides on the coarse probe select when that path is taken
+    IvfPlanHook hook{sh.list_len.get<int>(), nlist, ivf_chunk_rows(), sh.ccnt.get<int>(), sh.slot_off.get<int>(),
+                     sh.qtot.get<int>(), false};
+    FlatShard &qsh = *sh.quant->shards[0];
+    qsh.plan_hook = ivf_plan_query_major() ? &hook : nullptr;
+    try {
+        flat_shard_search(*sh.quant, qsh, nq, xq, np, np, sh.coarse_d.get<float>(), sh.coarse_i.get<int64_t>(), st);
+    } catch (...) {
+        qsh.plan_hook = nullptr;
+        qsh.qn_given = nullptr;
+        throw;
+    }
+    qsh.plan_hook = nullptr;
+    qsh.qn_given = nullptr;
+    // 2. list-major work plan
+    sh.cnt.ensure(sizeof(int) * (nlist + 1), sh.device);
+    sh.bucket_off.ensure(sizeof(int) * (nlist + 1), sh.device);
+    sh.item_off.ensure(sizeof(int) * (nlist + 1), sh.device);
+    sh.cursor.ensure(sizeof(int) * (nlist + 1), sh.device);
+    sh.bucket.ensure(sizeof(int) * (size_t)nq * np, sh.device);
+    HIPANN_REQUIRE((int64_t)nq * np < (int64_t)0x7fffffff, "nq * nprobe too large");
+    sh.slot_off.ensure(sizeof(int) * ((size_t)nq * np + 1), sh.device);
     launch_ivf_plan(sh.coarse_i.get<int64_t>(), nq, np, sh.list_len.get<int>(), nlist, group, sh.cnt.get<int>(),
                     sh.bucket_off.get<int>(), sh.item_off.get<int>(), sh.cursor.get<int>(), sh.bucket.get<int>(),
                     sh.slot_off.get<int>(), st, exact ? sh.nflag.get<int>() : nullptr, qbound, sh.ccnt.get<int>(),
@@ -319,9 +338,7 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     }
     if (tiled && !half) ensure_tiled_codes(sh, d, nlist, st);
     if (half) {
-        sh.hsplit.ensure((size_t)ivf_half_qsplit_bytes(nq, d), sh.device);
-        sh.hits.ensure(sizeof(float) * (size_t)nq, sh.device);
-        sh.hres.ensure(sizeof(float) * (size_t)nq, sh.device);
+        // query terms prepared before the coarse step
     } else if (ivf_form_split(form)) {
         sh.qsplit.ensure((size_t)ivf_mfma_bf_qsplit_bytes(nq, d, ivf_form_terms(form)), sh.device);
     }
@@ -332,7 +349,7 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
                                    metric, sh.codes_h.p, sh.tpass_off.get<int64_t>(), sh.xnorm.get<float>(),
                                    sh.list_off.get<int64_t>(), sh.cnt.get<int>(), sh.bucket_off.get<int>(),
                                    sh.item_off.get<int>(), sh.bucket.get<int>(), sh.slot_off.get<int>(), nlist, np, k,
-                                   max_items, qbound, sh.part_d.get<float>(), sh.part_i.get<int>(), st);
+                                   max_items, qbound, sh.part_d.get<float>(), sh.part_i.get<int>(), st, true);
         else if (bigk)
             launch_ivf_scan_bigk(xq, d, metric, sh.codes, sh.list_off.get<int64_t>(), sh.coarse_i.get<int64_t>(),
                                  nq * np, np, sh.slot_off.get<int>(), nq * np * std::max(sh.max_nch, 1), k,
@@ -367,11 +384,12 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
         launch_ivf_rerank(sh.part_d.get<float>(), sh.part_i.get<int>(), sh.slot_off.get<int>(), np, nq, k, kout, metric,
                           xq, sh.codes, d, sh.ids, sh.n, 0, xmax2, D, I, sh.nflag.get<int>(), sh.flagged.get<int>(), st,
                           kSplit2Eps, half ? sh.half_rxmax : -1.f, half ? sh.hres.get<float>() : nullptr,
-                          sh.coarse_i.get<int64_t>(), sh.list_off.get<int64_t>(), nlist);
+                          sh.coarse_i.get<int64_t>(), sh.list_off.get<int64_t>(), nlist, qbound,
+                          half && metric == kL2 ? qn : nullptr);
     }
     if (!host_fallback()) {
-        // flagged queries re-run on the device in the direct form (ivf_fallback_scan/_merge): no host
-        // readback, the next batch queues behind this one
+        // flagged queries re-run on the device in the direct form (ivf_fallback_query, one block per flagged
+        // query, bounded by the device flag count): no host readback, the next batch queues behind this one
         if (!sh.fb_total.p) {
             sh.fb_total.ensure(sizeof(unsigned long long), sh.device);
             HIPANN_CHECK(hipMemsetAsync(sh.fb_total.p, 0, sizeof(unsigned long long), st));

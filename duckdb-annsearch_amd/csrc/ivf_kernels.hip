@@ -1188,10 +1188,15 @@ __device__ __forceinline__ bool rerank_lists() {
 // are compacted into LDS, and wave 0 sorts them into L (lanes < k: ascending (key, row); pads past the
 // candidates).  A tie at T may pick different rows than the (key, row) lists would — harmless: every
 // row left out still has scan key ≥ K_k, which is all the bound check assumes.
+// bound (the scan's final per-query bound, an upper bound of the k-th smallest key): when at most 64 candidates
+// have key <= bound — the usual case: the lists' early entries were admitted under looser running bounds —
+// they are compacted and sorted directly (the k smallest (key, row) among them are the k smallest overall), no
+// 32-step search.
 template <int WV, int J>
 __device__ __forceinline__ void rerank_block_select(const float *__restrict__ pd, const int *__restrict__ pi,
                                                     int64_t total, int k, int64_t nrows, float *sd, int *si,
-                                                    int (*scnt)[WV], WaveList<1, int> &L) {
+                                                    int (*scnt)[WV], WaveList<1, int> &L,
+                                                    float bound = __builtin_inff()) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     float v[J];
     int r[J];
@@ -1208,6 +1213,39 @@ __device__ __forceinline__ void rerank_block_select(const float *__restrict__ pd
         const float f = v[j] == 0.f ? 0.f : v[j];
         const unsigned b = __float_as_uint(f);
         u[j] = ok ? ((b >> 31) ? ~b : (b | 0x80000000u)) : 0xffffffffu;
+    }
+    if (bound < __builtin_inff()) {
+        const unsigned long long lt = (1ull << lane) - 1ull;
+        int nb = 0;
+#pragma unroll
+        for (int j = 0; j < J; ++j) nb += __popcll(__ballot(u[j] != 0xffffffffu && v[j] <= bound));
+        if (lane == 0) scnt[0][wv] = nb;
+        __syncthreads();
+        int tot = 0, off = 0;
+#pragma unroll
+        for (int w = 0; w < WV; ++w) {
+            tot += scnt[0][w];
+            off += w < wv ? scnt[0][w] : 0;
+        }
+        if (tot <= 64) {  // block-uniform
+#pragma unroll
+            for (int j = 0; j < J; ++j) {
+                const bool a = u[j] != 0xffffffffu && v[j] <= bound;
+                const unsigned long long ma = __ballot(a);
+                if (a) { const int p = off + __popcll(ma & lt); sd[p] = v[j]; si[p] = r[j]; }
+                off += __popcll(ma);
+            }
+            __syncthreads();
+            if (wv == 0) {
+                float kk = lane < tot ? sd[lane] : __builtin_inff();
+                int cc = lane < tot ? si[lane] : IdTraits<int>::pad();
+                wave_sort(kk, cc);
+                L.d[0] = lane < k ? kk : __builtin_inff();
+                L.id[0] = lane < k ? cc : IdTraits<int>::pad();
+            }
+            return;
+        }
+        __syncthreads();  // every wave has read scnt before the search reuses it
     }
     unsigned T = 0;
     for (int bit = 31; bit >= 0; --bit) {
@@ -1350,6 +1388,101 @@ __device__ __forceinline__ int ivf_probe_rank_of_row(int64_t row, const int64_t 
     return -1;
 }
 
+
+// Re-run of one flagged query by one block (all WV waves): each probed list in probe order,
+// every row's distance in the direct form (the same lane-strided fmaf chain and xor butterfly as
+// rerank_rows4: the rerank's values bit for bit), a (distance, CSR row) list of kout per
+// list into fpd/fpi[q][p][kout], then wave 0 applies FAISS's scan-order rule (ivf_scan_order_topk) and
+// writes D/I.  ivf_fallback_query runs it for every flagged query (persistent grid bounded by the device flag
+// count): one launch per batch instead of the scan + merge pair.
+template <bool IP, int WV>
+__device__ __forceinline__ void ivf_block_fallback(int64_t q, int nprobe, int kout, const float *__restrict__ Q,
+                                                const float *__restrict__ codes, int d, const int64_t *__restrict__ ids,
+                                                int64_t label_offset, const int64_t *__restrict__ probes,
+                                                const int64_t *__restrict__ list_off, const int *__restrict__ list_len,
+                                                int nlist, float *__restrict__ fpd, long long *__restrict__ fpi,
+                                                float *__restrict__ D, int64_t *__restrict__ I,
+                                                unsigned long long *__restrict__ total, float *sd2, long long *si2) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const float *qp = Q + q * (int64_t)d;
+    for (int p = 0; p < nprobe; ++p) {
+        const int64_t l = probes[q * nprobe + p];
+        WaveList<1, long long> L;
+        L.init();
+        if (l >= 0 && l < nlist && list_len[l] > 0) {
+            const int64_t r0 = list_off[l], len = list_len[l];
+            for (int64_t g = (int64_t)wv * 64; g < len; g += 64 * WV) {
+                const int nr = (int)(len - g < 64 ? len - g : 64);
+                float mine = __builtin_inff();
+                for (int r = 0; r < nr; r += 4) {
+                    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+                    const float *xr[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) xr[u] = codes + (r0 + g + (r + u < nr ? r + u : nr - 1)) * d;
+                    for (int e = lane; e < d; e += 64) {
+                        const float qv = qp[e];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const float xv = xr[u][e];
+                            if (IP) acc[u] = fmaf(qv, xv, acc[u]);
+                            else {
+                                const float t = qv - xv;
+                                acc[u] = fmaf(t, t, acc[u]);
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        float a = acc[u];
+#pragma unroll
+                        for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+                        if (lane == r + u) mine = IP ? -a : a;
+                    }
+                }
+                const bool ok = lane < nr && !(mine == __builtin_inff());
+                L.offer(ok ? mine : __builtin_inff(), ok ? (long long)(r0 + g + lane) : IdTraits<long long>::pad(),
+                        kout - 1);
+            }
+        }
+        sd2[wv * 64 + lane] = L.d[0];
+        si2[wv * 64 + lane] = L.id[0];
+        __syncthreads();
+        if (wv == 0) {
+            L.init();
+#pragma unroll
+            for (int w = 0; w < WV; ++w) L.offer(sd2[w * 64 + lane], si2[w * 64 + lane], kout - 1);
+            if (lane < kout) {
+                fpd[(q * nprobe + p) * kout + lane] = L.d[0];
+                fpi[(q * nprobe + p) * kout + lane] = L.id[0];
+            }
+        }
+        __syncthreads();
+    }
+    if (wv != 0) return;
+    WaveList<1, long long> R;
+    const int64_t n = (int64_t)nprobe * kout;
+    const float *pd = fpd + q * n;
+    const long long *pr = fpi + q * n;
+    ivf_scan_order_topk(n, kout, [&](int64_t c) {
+        const float key = pd[c];
+        const long long row = pr[c];
+        const bool ok = !(key == __builtin_inff()) && row != IdTraits<long long>::pad();
+        const long long pp = c / kout;
+        return ScanCand{ok ? key : __builtin_inff(), ok ? (pp << 32) | row : IdTraits<long long>::pad(),
+                        ok ? (long long)(ids ? ids[row] : label_offset + row) : IdTraits<long long>::pad()};
+    }, R);
+    const float pad_d = IP ? -__builtin_inff() : __builtin_inff();
+    if (lane < kout) {
+        const bool pad = R.id[0] == IdTraits<long long>::pad() || R.d[0] == __builtin_inff();
+        D[q * kout + lane] = pad ? pad_d : (IP ? -R.d[0] : R.d[0]);
+        I[q * kout + lane] = pad ? -1 : (int64_t)R.id[0];
+    }
+    if (lane == 0) atomicAdd(total, 1ull);
+}
+
+#ifndef HIPANN_RR_MINB
+#define HIPANN_RR_MINB 4  // 4-wave blocks resident per CU: ≤ 128 VGPRs, one round for a 1024-query batch
+#endif
 // ---------------------------------------------------------------------------------------------
 // ivf_rerank_topk — form kFormSplit2Exact.  The 2-term split-bf16 scan (≈2⁻¹⁶ relative per product)
 // only prunes; the results are exact.  Per query (one wave): merge the partial lists to the
@@ -1361,7 +1494,7 @@ __device__ __forceinline__ int ivf_probe_rank_of_row(int64_t row, const int64_t 
 // E = 2⁻¹²·(‖q‖² + max‖x‖²) (the dropped split terms, ≤ 3·2⁻¹⁶·‖q‖‖x‖ per q·x, doubled, plus fp32
 // rounding of the norms and of both sums, with margin).  A query whose kout-th exact distance is not
 // < K16 − E (or < −K16... for IP the same bound on −q·x) is flagged; the host re-runs the flagged
-// queries on the device in the direct form (ivf_fallback_scan/_merge; the Flat form: on the host, 3-term
+// queries on the device in the direct form (ivf_fallback_query; the Flat form: on the host, 3-term
 // path).  With fewer than 16 merged candidates nothing was pruned.
 // The list length k (16; 32 for Flat IP, common.hpp) is the number of candidates reranked.
 // rxmax >= 0 (Flat form kFlatBf16Exact: one plain bf16 product per element): the bound is the
@@ -1374,14 +1507,15 @@ __device__ __forceinline__ int ivf_probe_rank_of_row(int64_t row, const int64_t 
 // extension's nq = 1 call): one block of WV waves per query — the waves merge disjoint parts of the
 // partial lists and compute a share of the candidates' distances, wave 0 finishes.
 template <bool IP, int WV>
-__global__ void __launch_bounds__(WV == 1 ? 256 : 64 * WV)
+__global__ void __launch_bounds__(WV == 1 ? 256 : 64 * WV, WV == 4 ? HIPANN_RR_MINB : 1)
 ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const int *__restrict__ slot_off,
                 int nprobe, int64_t nq, int k, int kout, const float *__restrict__ Q,
                 const float *__restrict__ codes, int d, const int64_t *__restrict__ ids, int64_t nrows,
                 int64_t label_offset, float xmax2, float *__restrict__ D, int64_t *__restrict__ I,
                 int *__restrict__ nflag, int *__restrict__ flagged, float eps, float rxmax,
                 const float *__restrict__ qres, const int64_t *__restrict__ probes,
-                const int64_t *__restrict__ list_off, int nlist) {
+                const int64_t *__restrict__ list_off, int nlist, const unsigned *__restrict__ qbound,
+                const float *__restrict__ qnorm) {
     const int64_t q = WV == 1 ? (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6) : (int64_t)blockIdx.x;
     if (q >= nq) return;
     const int lane = threadIdx.x & 63;
@@ -1423,7 +1557,11 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
         __shared__ int si[WV * 64], srow[64];
         __shared__ int scnt[2][WV];
         if (bsel) {
-            rerank_block_select<WV, RS_J>(pd + s0 * k, pi + s0 * k, total, k, nrows, sd, si, scnt, L);
+            // the scan's final bound (order-preserving bits of a full slot list's k-th key, atomicMin'ed): >= the
+            // k-th smallest key of the query's candidates
+            const unsigned qb = qbound ? qbound[q] : 0xffffffffu;
+            const float bound = (qb & 0x80000000u) ? __uint_as_float(qb & 0x7fffffffu) : __builtin_inff();
+            rerank_block_select<WV, RS_J>(pd + s0 * k, pi + s0 * k, total, k, nrows, sd, si, scnt, L, bound);
             if (wv == 0) srow[lane] = lane < k ? L.id[0] : IdTraits<int>::pad();
         } else {
             sd[wv * 64 + lane] = lane < k ? L.d[0] : __builtin_inff();
@@ -1472,7 +1610,9 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
     const bool real = lane < k && myrow != IdTraits<int>::pad();
     // 2. exact direct-form distances of the candidates (4 rows in flight, wave reduction per row)
     float qq = 0.f, rq2 = 0.f;
-    {
+    if (qres && qnorm) {
+        qq = qnorm[q];  // the IVF fp16 form: ‖q‖² prepared with the query terms, its own split residual in qres
+    } else {
         int e = lane;
         for (; e + 192 < d; e += 256) {  // 4 strides of loads in flight, sums in e order
             float qv[4];
@@ -1491,10 +1631,12 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
             rq2 = fmaf(r, r, rq2);
         }
     }
+    if (!(qres && qnorm)) {
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        qq += __shfl_xor(qq, o);
-        rq2 += __shfl_xor(rq2, o);
+        for (int o = 32; o > 0; o >>= 1) {
+            qq += __shfl_xor(qq, o);
+            rq2 += __shfl_xor(rq2, o);
+        }
     }
     if constexpr (WV == 1) {
     for (int r0 = 0; r0 < ncand; r0 += 4) {
@@ -1548,7 +1690,8 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
         E = eps * (qq + xmax2);
     }
     // a non-finite bound (a query outside the fp16 form's safe scale range) is always re-run
-    if ((!(E <= 3.4e38f) || (ncand == k && !(dk < k16 - E))) && lane == 0) flagged[atomicAdd(nflag, 1)] = (int)q;
+    const bool flag = !(E <= 3.4e38f) || (ncand == k && !(dk < k16 - E));
+    if (flag && lane == 0) flagged[atomicAdd(nflag, 1)] = (int)q;
     const float pad_d = IP ? -__builtin_inff() : __builtin_inff();
     if (lane < kout) {
         const bool pad = R.id[0] == IdTraits<long long>::pad();
@@ -1585,116 +1728,24 @@ __global__ void __launch_bounds__(256) ivf_scatter_results(const float *__restri
 }
 
 // ---------------------------------------------------------------------------------------------
-// Device-side re-run of the queries ivf_rerank_topk flagged (no host round trip per batch).
-// ivf_fallback_scan: work item (f, p), f < *nflag — query flagged[f] against its p-th probed list; the
-// block's 4 waves take 64-row groups of the list, each row's distance in the rerank's direct form (the
-// same lane-strided fmaf chain and xor butterfly: the rerank's values bit for bit), a (distance,
-// label) list of kout per wave, merged through LDS into the item's partial list fpd/fpi[f][p][kout].
-// ivf_fallback_merge: per flagged query, the (distance, label) top-kout of its nprobe partials into
-// D/I (+inf distances and empty slots are pads, as FAISS's heaps leave them); adds the batch's flag
-// count to the shard's running total.  Both grids are persistent loops bounded by *nflag, so a batch
-// with nothing flagged costs two near-empty launches.
+// Device-side re-run of the queries ivf_rerank_topk flagged (no host round trip per batch): one block per
+// flagged query (ivf_block_fallback), a persistent grid bounded by the device flag count, so a batch with
+// nothing flagged costs one near-empty launch.
 // ---------------------------------------------------------------------------------------------
 template <bool IP>
 __global__ void __launch_bounds__(256)
-ivf_fallback_scan(const int *__restrict__ nflag, const int *__restrict__ flagged, const int64_t *__restrict__ probes,
-                  int nprobe, const float *__restrict__ Q, const float *__restrict__ codes, int d,
-                  const int64_t *__restrict__ list_off, const int *__restrict__ list_len, int nlist,
-                  const int64_t *__restrict__ ids, int64_t label_offset, int kout, float *__restrict__ fpd,
-                  long long *__restrict__ fpi) {
-    __shared__ float sd[4 * 64];
-    __shared__ long long si[4 * 64];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int64_t items = (int64_t)(*nflag) * nprobe;
-    for (int64_t w = blockIdx.x; w < items; w += gridDim.x) {
-        const int64_t f = w / nprobe, p = w - f * nprobe;
-        const int64_t q = flagged[f];
-        const int64_t l = probes[q * nprobe + p];
-        const float *qp = Q + q * (int64_t)d;
-        WaveList<1, long long> L;
-        L.init();
-        if (l >= 0 && l < nlist && list_len[l] > 0) {
-            const int64_t r0 = list_off[l], len = list_len[l];
-            for (int64_t g = (int64_t)wv * 64; g < len; g += 256) {
-                const int nr = (int)(len - g < 64 ? len - g : 64);
-                float mine = __builtin_inff();
-                for (int r = 0; r < nr; r += 4) {
-                    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-                    const float *xr[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) xr[u] = codes + (r0 + g + (r + u < nr ? r + u : nr - 1)) * d;
-                    for (int e = lane; e < d; e += 64) {
-                        const float qv = qp[e];
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            const float xv = xr[u][e];
-                            if (IP) acc[u] = fmaf(qv, xv, acc[u]);
-                            else {
-                                const float t = qv - xv;
-                                acc[u] = fmaf(t, t, acc[u]);
-                            }
-                        }
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        float a = acc[u];
-#pragma unroll
-                        for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
-                        if (lane == r + u) mine = IP ? -a : a;
-                    }
-                }
-                // (distance, CSR row): within a list the row is the scan position, so this list holds every
-                // distance below its kout-th and the EARLIEST rows at ties — what FAISS's admission keeps
-                const int64_t row = r0 + g + lane;
-                const bool ok = lane < nr && !(mine == __builtin_inff());
-                L.offer(ok ? mine : __builtin_inff(), ok ? (long long)row : IdTraits<long long>::pad(), kout - 1);
-            }
-        }
-        sd[wv * 64 + lane] = L.d[0];
-        si[wv * 64 + lane] = L.id[0];
-        __syncthreads();
-        if (wv == 0) {
-            L.init();
-#pragma unroll
-            for (int w2 = 0; w2 < 4; ++w2) L.offer(sd[w2 * 64 + lane], si[w2 * 64 + lane], kout - 1);
-            if (lane < kout) {
-                fpd[w * kout + lane] = L.d[0];
-                fpi[w * kout + lane] = L.id[0];
-            }
-        }
-        __syncthreads();
-    }
-}
-
-template <bool IP>
-__global__ void __launch_bounds__(256)
-ivf_fallback_merge(const int *__restrict__ nflag, const int *__restrict__ flagged, int nprobe, int kout,
-                   const float *__restrict__ fpd, const long long *__restrict__ fpi, const int64_t *__restrict__ ids,
-                   int64_t label_offset, float *__restrict__ D, int64_t *__restrict__ I,
+ivf_fallback_query(const int *__restrict__ nflag, const int *__restrict__ flagged, const int64_t *__restrict__ probes,
+                   int nprobe, const float *__restrict__ Q, const float *__restrict__ codes, int d,
+                   const int64_t *__restrict__ list_off, const int *__restrict__ list_len, int nlist,
+                   const int64_t *__restrict__ ids, int64_t label_offset, int kout, float *__restrict__ fpd,
+                   long long *__restrict__ fpi, float *__restrict__ D, int64_t *__restrict__ I,
                    unsigned long long *__restrict__ total) {
+    __shared__ float sd2[4 * 64];
+    __shared__ long long si2[4 * 64];
     const int nf = *nflag;
-    if (blockIdx.x == 0 && threadIdx.x == 0 && nf > 0) atomicAdd(total, (unsigned long long)nf);
-    const int lane = threadIdx.x & 63;
-    const float pad_d = IP ? -__builtin_inff() : __builtin_inff();
-    for (int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); f < nf; f += (int64_t)gridDim.x * 4) {
-        // per-probe (distance, row) partials in probe order → FAISS's scan-order result (ivf_scan_order_topk)
-        WaveList<1, long long> L;
-        const int64_t n = (int64_t)nprobe * kout;
-        ivf_scan_order_topk(n, kout, [&](int64_t c) {
-            const float key = fpd[f * n + c];
-            const long long row = fpi[f * n + c];
-            const bool ok = !(key == __builtin_inff()) && row != IdTraits<long long>::pad();
-            const long long p = c / kout;
-            return ScanCand{ok ? key : __builtin_inff(), ok ? (p << 32) | row : IdTraits<long long>::pad(),
-                            ok ? (long long)(ids ? ids[row] : label_offset + row) : IdTraits<long long>::pad()};
-        }, L);
-        const int64_t q = flagged[f];
-        if (lane < kout) {
-            const bool pad = L.id[0] == IdTraits<long long>::pad() || L.d[0] == __builtin_inff();
-            D[q * kout + lane] = pad ? pad_d : (IP ? -L.d[0] : L.d[0]);
-            I[q * kout + lane] = pad ? -1 : (int64_t)L.id[0];
-        }
-    }
+    for (int f = blockIdx.x; f < nf; f += gridDim.x)
+        ivf_block_fallback<IP, 4>(flagged[f], nprobe, kout, Q, codes, d, ids, label_offset, probes, list_off, list_len,
+                                  nlist, fpd, fpi, D, I, total, sd2, si2);
 }
 
 void launch_ivf_fallback(const int *nflag, const int *flagged, int64_t nq, const int64_t *probes, int nprobe, int metric,
@@ -1703,19 +1754,14 @@ void launch_ivf_fallback(const int *nflag, const int *flagged, int64_t nq, const
                          float *D, int64_t *I, unsigned long long *total, hipStream_t st) {
     if (nq <= 0) return;
     HIPANN_REQUIRE(kout >= 1 && kout <= 64, "ivf fallback: kout out of range");
-    const unsigned gs = (unsigned)std::min<int64_t>(512, nq * nprobe);
-    const unsigned gm = (unsigned)std::min<int64_t>(256, ceil_div(nq, (int64_t)4));
-    if (metric == kIP) {
-        hipLaunchKernelGGL(ivf_fallback_scan<true>, dim3(gs), dim3(256), 0, st, nflag, flagged, probes, nprobe, Q, codes,
-                           d, list_off, list_len, nlist, ids, label_offset, kout, fpd, fpi);
-        hipLaunchKernelGGL(ivf_fallback_merge<true>, dim3(gm), dim3(256), 0, st, nflag, flagged, nprobe, kout, fpd, fpi,
-                           ids, label_offset, D, I, total);
-    } else {
-        hipLaunchKernelGGL(ivf_fallback_scan<false>, dim3(gs), dim3(256), 0, st, nflag, flagged, probes, nprobe, Q,
-                           codes, d, list_off, list_len, nlist, ids, label_offset, kout, fpd, fpi);
-        hipLaunchKernelGGL(ivf_fallback_merge<false>, dim3(gm), dim3(256), 0, st, nflag, flagged, nprobe, kout, fpd,
-                           fpi, ids, label_offset, D, I, total);
-    }
+    // one block per flagged query (persistent grid bounded by the device flag count); fpd/fpi: [q][p][kout]
+    const unsigned g = (unsigned)std::min<int64_t>(512, nq);
+    if (metric == kIP)
+        hipLaunchKernelGGL(ivf_fallback_query<true>, dim3(g), dim3(256), 0, st, nflag, flagged, probes, nprobe, Q, codes,
+                           d, list_off, list_len, nlist, ids, label_offset, kout, fpd, fpi, D, I, total);
+    else
+        hipLaunchKernelGGL(ivf_fallback_query<false>, dim3(g), dim3(256), 0, st, nflag, flagged, probes, nprobe, Q, codes,
+                           d, list_off, list_len, nlist, ids, label_offset, kout, fpd, fpi, D, I, total);
     HIPANN_CHECK(hipGetLastError());
 }
 
@@ -1727,14 +1773,14 @@ void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int 
                        int metric, const float *Q, const float *codes, int d, const int64_t *ids, int64_t nrows,
                        int64_t label_offset, float xmax2, float *D, int64_t *I, int *nflag, int *flagged,
                        hipStream_t st, float eps, float rxmax, const float *qres, const int64_t *probes,
-                       const int64_t *list_off, int nlist) {
+                       const int64_t *list_off, int nlist, const unsigned *qbound, const float *qnorm) {
     if (nq <= 0) return;
     HIPANN_REQUIRE(k >= kRerankK && k <= 64 && kout >= 1 && kout <= kRerankMaxK, "ivf rerank: k / kout out of range");
     // small batches: one 4-wave block per query (fills more of the chip, shorter per-query chain)
     const bool wide = nq < HIPANN_RR_WIDE;
     dim3 grid((unsigned)(wide ? nq : ceil_div(nq, 4))), block(256);
 #define RR_ARGS pd, pi, slot_off, nprobe, nq, k, kout, Q, codes, d, ids, nrows, label_offset, xmax2, D, I, nflag, flagged, \
-                eps, rxmax, qres, probes, list_off, nlist
+                eps, rxmax, qres, probes, list_off, nlist, qbound, qnorm
     if (metric == kIP) {
         if (wide) hipLaunchKernelGGL((ivf_rerank_topk<true, 4>), grid, block, 0, st, RR_ARGS);
         else hipLaunchKernelGGL((ivf_rerank_topk<true, 1>), grid, block, 0, st, RR_ARGS);

@@ -1030,13 +1030,31 @@ __global__ void __launch_bounds__(256) ivf_half_residual(const float *__restrict
 // two) and qres[q] = ‖q − (h + l)/t‖ (×1.0001 for the fp32 sum).  A query whose scale leaves the safe
 // range (non-finite entries, |e_q| > 100, 1/(t·s) not a normal float) gets zero terms and qres = +inf:
 // the rerank flags it and it re-runs on the device in the direct form.
+// qn (optional): also ‖q‖², in exactly row_norms_f32's order (vec4: float4 j = lane, lane + 64, …, four fmas
+// each; else element-strided), so the coarse quantizer and the scan read the same bits they read before — the
+// batch's query preparation in one launch.
 __global__ void __launch_bounds__(256) ivf_split_queries_h(const float *__restrict__ Q, int64_t nq, int d, int nsup,
                                                            int es, uint4 *__restrict__ out, float *__restrict__ its,
-                                                           float *__restrict__ qres) {
+                                                           float *__restrict__ qres, float *__restrict__ qn, int vec4) {
     const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (q >= nq) return;
     const int lane = threadIdx.x & 63;
     const float *src = Q + q * (int64_t)d;
+    if (qn) {
+        float s = 0.f;
+        if (vec4) {
+            const float4 *p4 = reinterpret_cast<const float4 *>(src);
+            for (int j = lane; j < (d >> 2); j += 64) {
+                const float4 v = p4[j];
+                s = fmaf(v.x, v.x, s); s = fmaf(v.y, v.y, s); s = fmaf(v.z, v.z, s); s = fmaf(v.w, v.w, s);
+            }
+        } else {
+            for (int j = lane; j < d; j += 64) s = fmaf(src[j], src[j], s);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+        if (lane == 0) qn[q] = s;
+    }
     unsigned mb = 0;
     for (int e = lane; e < d; e += 64) mb = max(mb, __float_as_uint(src[e]) & 0x7fffffffu);
 #pragma unroll
@@ -1347,11 +1365,20 @@ void launch_ivf_half_residual(const float *codes, int64_t n, int d, float scale,
     HIPANN_CHECK(hipGetLastError());
 }
 
+void launch_ivf_split_queries_h(const float *Q, int64_t nq, int d, int es, void *qsplit, float *its, float *qres,
+                                float *qn, hipStream_t st) {
+    if (nq <= 0) return;
+    const int vec4 = (d % 4 == 0) && ((uintptr_t)Q % 16 == 0);  // launch_row_norms' rule
+    hipLaunchKernelGGL(ivf_split_queries_h, dim3((unsigned)ceil_div(nq, 4)), dim3(256), 0, st, Q, nq, d, mh_nsup(d), es,
+                       static_cast<uint4 *>(qsplit), its, qres, qn, vec4);
+    HIPANN_CHECK(hipGetLastError());
+}
+
 void launch_ivf_scan_mfma_h(const float *Q, int64_t nq, void *qsplit, float *its, float *qres, int es, const float *qn,
                             int d, int metric, const void *codes_h, const int64_t *tpass_off, const float *xn,
                             const int64_t *list_off, const int *cnt, const int *bucket_off, const int *item_off,
                             const int *bucket, const int *slot_off, int nlist, int nprobe, int k, int64_t max_items,
-                            unsigned *qbound, float *pd, int *pi, hipStream_t st) {
+                            unsigned *qbound, float *pd, int *pi, hipStream_t st, bool split_done) {
     if (max_items <= 0 || nq <= 0) return;
     HIPANN_REQUIRE(max_items < (int64_t)0x7fffffff, "too many IVF work items");
     HIPANN_REQUIRE(qsplit && its && qres && codes_h, "fp16 IVF scan: missing buffers");
@@ -1359,8 +1386,9 @@ void launch_ivf_scan_mfma_h(const float *Q, int64_t nq, void *qsplit, float *its
     HIPANN_REQUIRE(metric == kIP || (qn && xn), "decomposed L2 scan needs query and row norms");
     const int nsup = mh_nsup(d);
     uint4 *qs = static_cast<uint4 *>(qsplit);
-    hipLaunchKernelGGL(ivf_split_queries_h, dim3((unsigned)ceil_div(nq, 4)), dim3(256), 0, st, Q, nq, d, nsup, es, qs,
-                       its, qres);
+    if (!split_done)
+        hipLaunchKernelGGL(ivf_split_queries_h, dim3((unsigned)ceil_div(nq, 4)), dim3(256), 0, st, Q, nq, d, nsup, es, qs,
+                           its, qres, nullptr, 0);
     const int group = mh_group(d);
     const size_t merge = (size_t)(MF_WAVES / 2) * MF_QTMAX * 4 * 64 * sizeof(float2);
     const size_t smem = std::max((size_t)group * mh_stride(d) * 4, merge);

@@ -178,7 +178,12 @@ struct FlatShard {
     struct IvfPlanHook *plan_hook = nullptr;
     const float *qn_of = nullptr;  // sh.qn holds ‖q‖² of these queries (the last search's, nq of them)
     int64_t qn_nq = 0;
+    // set by the caller before a search: sh.qn already holds ‖q‖² of these queries (the IVF query preparation
+    // computed it), so the search does not launch row_norms again
+    const float *qn_given = nullptr;
+    int64_t qn_given_nq = 0;
     DevBuf keys, run_d, run_i, run2_d, run2_i;  // k > 64 path
+    DevBuf mid_d, mid_i;                        // two-level merge of the direct scan's per-wave lists
     DevBuf qsplit;                              // split-bf16 form: the batch's queries as bf16 terms
     // kFlatSplit2Exact: max row ‖x‖² (the rerank's error bound; −1 until computed / after an add), the
     // flagged queries of the last batch and the re-run's buffers
@@ -328,7 +333,8 @@ void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int 
                        int metric, const float *Q, const float *codes, int d, const int64_t *ids, int64_t nrows,
                        int64_t label_offset, float xmax2, float *D, int64_t *I, int *nflag, int *flagged,
                        hipStream_t st, float eps = kSplit2Eps, float rxmax = -1.f, const float *qres = nullptr,
-                       const int64_t *probes = nullptr, const int64_t *list_off = nullptr, int nlist = 0);
+                       const int64_t *probes = nullptr, const int64_t *list_off = nullptr, int nlist = 0,
+                       const unsigned *qbound = nullptr, const float *qnorm = nullptr);
 // ivf_mfma.hip, fp16-image scan (kFormHalfExact)
 int ivf_mfma_h_group(int d);
 int64_t ivf_half_pass_bytes(int d);
@@ -342,7 +348,10 @@ void launch_ivf_scan_mfma_h(const float *Q, int64_t nq, void *qsplit, float *its
                             int d, int metric, const void *codes_h, const int64_t *tpass_off, const float *xn,
                             const int64_t *list_off, const int *cnt, const int *bucket_off, const int *item_off,
                             const int *bucket, const int *slot_off, int nlist, int nprobe, int k, int64_t max_items,
-                            unsigned *qbound, float *pd, int *pi, hipStream_t st);
+                            unsigned *qbound, float *pd, int *pi, hipStream_t st, bool split_done = false);
+// the batch's fp16 query terms (+ 1/(t·s), split residuals) and, when qn != nullptr, ‖q‖² (row_norms_f32's bits)
+void launch_ivf_split_queries_h(const float *Q, int64_t nq, int d, int es, void *qsplit, float *its, float *qres,
+                                float *qn, hipStream_t st);
 // flat_bf16.hip
 int flat_bf16_waves(int64_t nq);
 int flat_bf16_tile_rows();
@@ -394,5 +403,11 @@ template <typename InId>
 void launch_merge_parts(const float *pd, const InId *pi, int nparts, int64_t nq, int k, int kout,
                         int64_t label_offset, float in_sign, float out_sign, float *D, int64_t *I, hipStream_t st,
                         int64_t pstride_d = -1, int64_t pstride_i = -1);  // part strides (elements); -1: nq*k
+// Many parts, few queries: groups of parts merged by ngroups·nq waves into md/mi ([g][nq][kout]), then the
+// group lists by launch_merge_parts (kout <= 64).
+template <typename InId>
+void launch_merge_parts_2level(const float *pd, const InId *pi, int nparts, int64_t nq, int k, int kout,
+                               int64_t label_offset, float in_sign, float out_sign, float *D, int64_t *I, float *md,
+                               long long *mi, int ngroups, hipStream_t st);
 
 }  // namespace hipann

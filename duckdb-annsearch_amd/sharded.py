@@ -94,9 +94,14 @@ class ShardedSearch:
     def search(self, xq):
         import torch.distributed as dist
 
+        if not self.collective:  # one rank: the search writes fresh tensors (no packed buffer, no copy)
+            import torch
+
+            D = torch.empty((self.nq, self.k), dtype=torch.float32, device=self.packed.device)
+            I = torch.empty((self.nq, self.k), dtype=torch.int64, device=self.packed.device)
+            self.local_search(xq, D, I)
+            return D, I
         self.local_search(xq, self.D, self.I)
-        if not self.collective:  # fresh tensors, as the merge returns (the packed buffer is reused)
-            return self.D.clone(), self.I.clone()
         if self.packed.is_cuda and dist.get_backend(self.group) == "nccl":
             # RCCL: one collective straight into the buffer the merge reads
             dist.all_gather_into_tensor(self.gathered.view(-1), self.packed, group=self.group)

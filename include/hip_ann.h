@@ -209,7 +209,7 @@ int hipann_ivf_export(void *index, float *centroids, int64_t *list_offsets, int6
  * filter; every returned distance is recomputed in the direct form Σ(q−x)² (IP: q·x) in fp32, ordered by
  * (distance, label), and a per-query bound (|scan key − exact| ≤ 2^-12·(‖q‖² + max‖x‖²)) proves that no
  * pruned row could enter the top-k — queries that fail it are re-run ON THE DEVICE over their probe lists
- * in the direct form (ivf_fallback_scan / _merge: grids bounded by the device flag count, no host
+ * in the direct form (ivf_fallback_query: one block per flagged query, grid bounded by the device flag count, no host
  * readback), so the call stays asynchronous.  k ≤ 12 (larger k: SPLIT3). */
 #define HIPANN_IVF_FORM_SPLIT2_EXACT 5
 /* HIPANN_IVF_FORM_HALF_EXACT (default): the same filter + exact rerank, the scan reading a tiled fp16
