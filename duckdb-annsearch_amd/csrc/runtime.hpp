@@ -362,6 +362,10 @@ void launch_flat_bf16_topk(const float *Q, const float *qn, int64_t nq, void *qi
                            int64_t N, int d, int metric, int k, int nsplit, int64_t tiles_per_split, float *pd, int *pi,
                            const float *seed, bool image_ready, hipStream_t st);
 void launch_flat_bf16_seed(const float *pd, int nsplit, int64_t nq, int k, float *seed, hipStream_t st);
+bool flat_bf16_k64_supported(int nk, int k);
+void launch_flat_bf16_k64(const void *qimg, const float *qn, int64_t nq, const void *ximg, const float *xn, int64_t N,
+                          int nk, int metric, int k, int nqt, int nsplit, int64_t tiles_per_split, float *pd, int *pi,
+                          const float *seed, hipStream_t st);
 void launch_ivf_max_norm(const float *xn, int64_t n, unsigned *out, hipStream_t st);
 void launch_ivf_fallback(const int *nflag, const int *flagged, int64_t nq, const int64_t *probes, int nprobe, int metric,
                          const float *Q, const float *codes, int d, const int64_t *list_off, const int *list_len,
