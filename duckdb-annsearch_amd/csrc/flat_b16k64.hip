@@ -1,21 +1,24 @@
-// flat_b16k64.hip — the Flat bf16 filter scan (form kFlatBf16Exact) with 64-dim K-steps on
-// v_mfma_f32_16x16x32_bf16.
+// flat_b16k64.hip — the Flat bf16 filter scan (form kFlatBf16Exact) of a bounded pass: 64-dim K-steps on
+// v_mfma_f32_16x16x32_bf16, a 2-K-step-deep memory pipeline, and the passing rows appended to per-(query,
+// split) candidate buffers in global memory instead of per-query top-k lists in LDS.
 //
-// Same job, images and output as flat_bf16_topk (flat_bf16.hip: MetalIndexFlat::search's GEMM + select for
-// nq >= 20, faiss-metal/src/MetalIndexFlat.mm:294-369): per (database split, query) the k best scan keys
-// of one bf16 product per element, as the filter of the exact fp32 rerank (ivf_rerank_topk).  What
-// changes is the main loop, after the 256² GEMM recipe of cdna_hip_programming.md §5:
-//   * K-step = 64 dims (two 32-dim image chunks, consecutive in the tiled image): one barrier and one
-//     counted vmcnt per 64 MFMAs per wave instead of per 16 — BK 32 → 64 is the first lever of that recipe;
-//   * v_mfma_f32_16x16x32_bf16 (16-cycle issue; the chip holds a higher clock on it than on the 32×32×16
-//     shape under load, MI355X_MICROARCH.md 'DVFS give-back' item 7): wave w owns queries [32w, 32w+32) ×
-//     all 256 rows of the tile = 2 × 16 accumulators of 16 × 16;
-//   * the database tile streams by LDS-DMA into 3 stages of 32 KB (K-steps g+1 and g+2 in flight), the
-//     query fragments straight into a 2-deep register ring (each wave reads only its own queries); the
-//     per-query top-k lists stay in LDS: 3 × 32 KB + 256 × k × 8 B = 160 KiB at k = 32.
-// Keys, lists and the epilogue's filter (2·ip − ‖x‖² ≥ ‖q‖² − thr) are those of flat_bf16_topk; only the
-// fp32 accumulation order of the bf16 products differs, which the rerank bound covers (any order of d
-// exact products: the (d + 8)·2⁻²⁴ term).
+// Same keys and images as flat_bf16_topk (flat_bf16.hip: MetalIndexFlat::search's GEMM + select for nq >= 20,
+// faiss-metal/src/MetalIndexFlat.mm:294-369): key = ‖q‖² + ‖x‖² − 2·q̂·x̂ (L2, clamped at 0) or −q̂·x̂ (IP) from
+// one bf16 product per element, as the filter of the exact fp32 rerank (ivf_rerank_topk).  A pass runs under a
+// per-query bound T (flat_bf16_seed on a sample, then flat_cand_bound on the previous pass's candidates): every
+// row with key ≤ T is appended to its (query, split) buffer; flat_cand_select then keeps each query's k best.
+//   * tile = 256 queries × 256 database rows, K-step = 64 dims (two 32-dim image chunks, consecutive in the
+//     tiled image); wave w owns queries [32w, 32w+32) × all 256 rows = 2 × 16 accumulators of 16 × 16 (the
+//     256² recipe of cdna_hip_programming.md §5 with the query operand in registers);
+//   * memory: the database tile streams by LDS-DMA into 5 stages of 32 KB three K-steps ahead, the query
+//     fragments into a 2-slot register ring one K-step ahead; loads retire in issue order under vmcnt, so each
+//     K-step issues A(g+1) before B(g+3) and one counted vmcnt(4) keeps B(g+2), B(g+3) in flight.  Measured on
+//     10M × 768 with 3 stages and one K-step in flight for both (timing ablations):
+//     the compute + LDS structure alone runs at 0.74 of dense bf16; with one K-step in flight the tile DMA and
+//     the fragment loads added 3.5 and 2.4 ms to its 8.5 ms;
+//   * the lists left LDS (5 stages need all 160 KiB): with a bound from a sample the passing rows are few
+//     (≈12 per query and split at 10M rows), so the epilogue appends them (one scattered store each, the count
+//     in a register) — no LDS round trips, no sorting in the scan.
 #include "runtime.hpp"
 #include "wave_topk.hpp"
 
@@ -33,100 +36,86 @@ typedef __attribute__((address_space(3))) void k64_lds_void;
 constexpr int K64_TN = 256;               // database rows per tile
 constexpr int K64_QM = 256;               // queries per block (8 waves × 32)
 constexpr int K64_W = 8;
-constexpr int K64_NB = 3;                 // LDS stages (K-steps g+1, g+2 in flight while g is read)
+constexpr int K64_NB = 5;                 // LDS stages: g read, g+1 .. g+3 landing / in flight
 constexpr int K64_BU = K64_TN * 4;        // 16-B units of one 32-dim chunk of a database tile
 constexpr int K64_SU = 2 * K64_BU;        // units per stage (one 64-dim K-step): 32 KB
 constexpr int K64_PIECES = K64_SU / 64 / K64_W;  // 1-KiB LDS-DMA pieces per wave per K-step
+constexpr size_t K64_LDS = (size_t)K64_NB * K64_SU * 16;
 static_assert(K64_PIECES * 64 * K64_W == K64_SU, "pieces split evenly");
+static_assert(K64_LDS <= 160 * 1024, "LDS");
 
-template <int N>
-__device__ __forceinline__ void k64_wait_vm() {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// Epilogue of one tile.  On entry acc[mb][jb][i] = s = 2·q·x − ‖x‖² (L2; 2·q·x for IP, −inf past N) of query
-// 32·wave + 16·mb + 4·(lane >> 4) + i and database row x0 + 16·jb + (lane & 15); a row passes the query's
-// bound when s ≥ cth = ‖q‖² − thr (L2) or −2·thr (IP) — cth[mb][i] is the lane's own query's (its 16-lane
-// group).  Rare passing rows go through the query's LDS list (one WaveList of k per query, offered 64
-// candidates per round) with key = ‖q‖² − s (L2, clamped at 0) or −s/2 = −q·x (IP): +inf past N.
+// Epilogue of one tile for accumulator row (MB, I).  On entry acc[mb][jb][i] = s = 2·q·x − ‖x‖² (L2; 2·q·x
+// for IP; −inf past N) of query 32·wave + 16·mb + 4·(lane >> 4) + i and database row x0 + 16·jb + (lane & 15);
+// a row passes its query's bound when s ≥ cth = ‖q‖² − T (L2) or −2·T (IP) — cth[mb][i] is the lane's own
+// query's (its 16-lane group).  Passing rows (rare) are appended to the query's buffer with key = ‖q‖² − s
+// (L2, clamped at 0) or −s/2 = −q·x (IP); cntv lane j holds the count of the wave's query j (it keeps
+// counting past cap: flat_cand_select flags an overflowed query for the exact fallback).
 template <bool L2M, int MB, int I>
-__device__ __forceinline__ void k64_epilogue_row(const k64_f32x4 (&acc)[2][16], float (&cth)[2][4],
-                                                 const float *__restrict__ qnorm, int64_t q0wave, int64_t nq,
-                                                 int64_t x0, int64_t N, float *__restrict__ Ld,
-                                                 int *__restrict__ Li, int k, int wave, int lane) {
-    const int m16 = lane & 15, g4 = lane >> 4;
+__device__ __forceinline__ void k64_epilogue_row(const k64_f32x4 (&acc)[2][16], const float (&cth)[2][4], float qnl,
+                                                 int &cntv, int64_t x0, float *__restrict__ cand_d,
+                                                 int *__restrict__ cand_i, int64_t cbase, int64_t cq, int cap,
+                                                 int lane) {
     bool any = false;
 #pragma unroll
     for (int jb = 0; jb < 16; ++jb) any |= acc[MB][jb][I] >= cth[MB][I];
     const unsigned long long m = __ballot(any);
     if (m == 0ull) return;
+    // the lane's passing columns (bit jb)
+    unsigned pm = 0;
+#pragma unroll
+    for (int jb = 0; jb < 16; ++jb) pm |= acc[MB][jb][I] >= cth[MB][I] ? 1u << jb : 0u;
 #pragma unroll 1
     for (int fq = 0; fq < 4; ++fq) {
-        if (((m >> (16 * fq)) & 0xffffull) == 0ull) continue;
-        const int ql = 32 * wave + 16 * MB + 4 * fq + I;
-        const int64_t qr = q0wave + 16 * MB + 4 * fq + I;  // wave-uniform
-        const float qnr = (L2M && qr < nq) ? qnorm[qr] : 0.f;
-        WaveList<1, int> L;
-        L.d[0] = lane < k ? Ld[ql * k + lane] : __builtin_inff();
-        L.id[0] = lane < k ? Li[ql * k + lane] : 0x7fffffff;
-        const int src = 16 * fq + m16;  // the lanes of query fq hold its 256 scores (16 per lane)
+        unsigned grp = (unsigned)(m >> (16 * fq)) & 0xffffu;  // lanes of query fq holding a passing row
+        if (grp == 0u) continue;
+        const int qw = 16 * MB + 4 * fq + I;  // the query's index in the wave
+        const float qnr = L2M ? readlane_f(qnl, qw) : 0.f;
+        int c = readlane_i(cntv, qw);
+        float *cd = cand_d + cbase + (int64_t)qw * cq;
+        int *ci = cand_i + cbase + (int64_t)qw * cq;
+        while (grp) {
+            const int l = __ffs(grp) - 1;
+            grp &= grp - 1;
+            const int src = 16 * fq + l;
+            unsigned pml = (unsigned)__builtin_amdgcn_readlane((int)pm, src);
+            while (pml) {
+                const int jb = __ffs(pml) - 1;
+                pml &= pml - 1;
+                float sv = acc[MB][0][I];
 #pragma unroll
-        for (int o = 0; o < 4; ++o) {
-            const float c0 = __shfl(acc[MB][4 * o + 0][I], src), c1 = __shfl(acc[MB][4 * o + 1][I], src);
-            const float c2 = __shfl(acc[MB][4 * o + 2][I], src), c3 = __shfl(acc[MB][4 * o + 3][I], src);
-            const float sv = g4 == 0 ? c0 : g4 == 1 ? c1 : g4 == 2 ? c2 : c3;
-            float key;
-            if (L2M) {
-                key = qnr - sv;
-                key = key < 0.f ? 0.f : key;
-            } else {
-                key = -0.5f * sv;
+                for (int j = 1; j < 16; ++j) sv = jb == j ? acc[MB][j][I] : sv;
+                sv = readlane_f(sv, src);
+                float key;
+                if (L2M) {
+                    key = qnr - sv;
+                    key = key < 0.f ? 0.f : key;
+                } else {
+                    key = -0.5f * sv;
+                }
+                if (lane == 0 && c < cap) {
+                    cd[c] = key;
+                    ci[c] = (int)(x0 + 16 * jb + l);
+                }
+                ++c;
             }
-            const int64_t col = x0 + 16 * (4 * o + g4) + m16;
-            L.offer(key, col < N ? (int)col : 0x7fffffff, k - 1);
         }
-        if (lane < k) {
-            Ld[ql * k + lane] = L.d[0];
-            Li[ql * k + lane] = L.id[0];
-        }
-        const float nt = readlane_f(L.d[0], k - 1);
-        if (g4 == fq) cth[MB][I] = L2M ? qnr - nt : -2.f * nt;
+        cntv = lane == qw ? c : cntv;
     }
 }
 
-template <bool L2M>
-__device__ __forceinline__ void k64_epilogue(k64_f32x4 (&acc)[2][16], float (&cth)[2][4],
-                                             const float *__restrict__ qnorm, int64_t q0wave, int64_t nq,
-                                             const float *__restrict__ xnorm, int64_t x0, int64_t N,
-                                             float *__restrict__ Ld, int *__restrict__ Li, int k, int wave,
-                                             int lane) {
-    const int m16 = lane & 15;
-    // s = 2·q·x − ‖x‖² in place (the filter's left side; the key follows from it with one more rounding,
-    // inside the rerank bound's (d + 8)·2⁻²⁴ term): no ‖x‖² registers live through the list updates
-#pragma unroll
-    for (int jb = 0; jb < 16; ++jb) {
-        const int64_t x = x0 + 16 * jb + m16;
-        const float xv = x < N ? (L2M ? xnorm[x] : 0.f) : __builtin_inff();
-#pragma unroll
-        for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) acc[mb][jb][i] = fmaf(2.f, acc[mb][jb][i], -xv);
-    }
-    [&]<int... P>(std::integer_sequence<int, P...>) {
-        (k64_epilogue_row<L2M, P / 4, P % 4>(acc, cth, qnorm, q0wave, nq, x0, N, Ld, Li, k, wave, lane), ...);
-    }(std::make_integer_sequence<int, 8>{});
-}
-
+// One bounded pass of a split: tiles [tile_begin, tile_end) of split `split` for the block's 256 queries.
+// Candidate buffers: cand_[dn]{[(q·nsplit + split)·cap + j]}, counts cand_n[q·nsplit + split] (resume: the
+// previous pass's count is continued).  bound[q]: the pass's T (k-th best key of a sample / previous pass,
+// with margin, flat_bf16_seed / flat_cand_bound).
 template <bool L2M>
 __global__ void __launch_bounds__(64 * K64_W, 1)
 flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm, int64_t nq,
-              const k64_u32x4 *__restrict__ Xt, const float *__restrict__ xnorm, int64_t N, int nk, int k, int nqt,
-              int nsplit, int64_t tiles_per_split, float *__restrict__ part_d, int *__restrict__ part_i,
-              const float *__restrict__ seed) {
+              const k64_u32x4 *__restrict__ Xt, const float *xnorm, int64_t N, int nk, int nqt, int nsplit,
+              int64_t tiles_per_split, int64_t tile_begin, int64_t tile_end, const float *__restrict__ bound,
+              float *__restrict__ cand_d, int *__restrict__ cand_i, int *__restrict__ cand_n, int cap,
+              int resume) {
     constexpr int NB = K64_NB;
     extern __shared__ __attribute__((aligned(16))) k64_u32x4 smem_k64[];
-    float *Ld = reinterpret_cast<float *>(smem_k64 + NB * K64_SU);  // [QM][k]
-    int *Li = reinterpret_cast<int *>(Ld + K64_QM * k);
 
     const int nblocks = nqt * nsplit;
     const int lb = xcd_remap(blockIdx.x, nblocks);
@@ -134,8 +123,10 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
     const int split = lb / nqt;
     const int64_t q0 = (int64_t)qt * K64_QM;
     const int64_t ntiles = ceil_div(N, K64_TN);
-    const int64_t t0 = (int64_t)split * tiles_per_split;
-    const int64_t t1 = t0 + tiles_per_split < ntiles ? t0 + tiles_per_split : ntiles;
+    const int64_t ts = (int64_t)split * tiles_per_split;
+    const int64_t t0 = ts + tile_begin;
+    const int64_t te = ts + (tile_end < tiles_per_split ? tile_end : tiles_per_split);
+    const int64_t t1 = te < ntiles ? te : ntiles;
     const int ns = nk >> 1;  // K-steps per tile (nk even)
     const int64_t G = t1 > t0 ? (t1 - t0) * ns : 0;
 
@@ -143,14 +134,13 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
     const int wave = tid >> 6, lane = tid & 63;
     const int m16 = lane & 15, g4 = lane >> 4;
     const int64_t q0w = q0 + 32 * wave + 4 * g4;  // + 16·mb + i: the lane's accumulator query rows
-    const int64_t q0wave = q0 + 32 * __builtin_amdgcn_readfirstlane(wave);
 
-    // seed (optional, as flat_bf16_topk): lists start at k copies of (T_q, pad)
-    for (int e = tid; e < K64_QM * k; e += 64 * K64_W) {
-        const int64_t q = q0 + e / k;
-        Ld[e] = seed && q < nq ? seed[q] : __builtin_inff();
-        Li[e] = 0x7fffffff;
-    }
+    // per-lane state of the wave's 32 queries (lane j: query 32·wave + j): ‖q‖², candidate count
+    const int64_t qlane = q0 + 32 * wave + (lane & 31);
+    float qnl = 0.f;
+    if (L2M) qnl = qlane < nq ? qnorm[qlane] : 0.f;
+    int cntv = 0;
+    if (resume && lane < 32 && qlane < nq) cntv = cand_n[qlane * nsplit + split];
     float cth[2][4];
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb)
@@ -158,17 +148,19 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
         for (int i = 0; i < 4; ++i) {
             const int64_t q = q0w + 16 * mb + i;
             const float qn = (L2M && q < nq) ? qnorm[q] : 0.f;
-            const float thr = q < nq ? (seed ? seed[q] : __builtin_inff()) : -__builtin_inff();
+            const float thr = q < nq ? bound[q] : -__builtin_inff();  // −inf: rows past nq pass nothing
             cth[mb][i] = L2M ? qn - thr : -2.f * thr;
         }
+    const int64_t cq = (int64_t)nsplit * cap;  // buffer stride between consecutive queries
+    const int64_t cbase = ((q0 + 32 * wave) * nsplit + split) * (int64_t)cap;
 
     // K-step g = (t − t0)·ns + s covers image chunks 2s, 2s + 1 of tile t: 2·K64_BU consecutive units
     const k64_u32x4 *Xb = Xt + t0 * nk * K64_BU + lane;
     // the lane's query fragments: rows 32·wave + 16·mb + m16, unit c = g4 of each 32-dim chunk
     const k64_u32x4 *Qw = Qt + (int64_t)qt * nk * (K64_QM * 4) + g4 * K64_QM;
     const int qrow0 = (32 * wave + m16) ^ (g4 << 1), qrow1 = (32 * wave + 16 + m16) ^ (g4 << 1);
-    // query fragments: a 2-deep register ring, K-step g+1's issued (before K-step g+2's tile pieces) while g
-    // is computed, so at the top of K-step g only g+1's pieces may stay in flight
+    // query fragments: a 2-slot register ring (K-step g+1's loaded while g is computed); the loop is unrolled by
+    // two so the slot is a compile-time index
     int ks_a = 0;
     k64_u32x4 ar[2][2][2];  // [ring slot][chunk of the K-step][mb]
     auto issue_a = [&](auto slot_c) {
@@ -196,28 +188,52 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
     for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
         for (int jb = 0; jb < 16; ++jb) acc[mb][jb] = (k64_f32x4){0.f, 0.f, 0.f, 0.f};
-    __syncthreads();  // list initialisation
-    if (G > 0) {  // A(0), B(0), B(1) (past the end: the last K-step again, never read)
-        issue_a(std::integral_constant<int, 0>{});
+    // ‖x‖² of tile tt, row 64·j + lane in xr[j] (0 for IP)
+    float xr[4] = {0.f, 0.f, 0.f, 0.f};
+    auto load_xn = [&](int64_t tt) {
+        if constexpr (!L2M) return;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t x = tt * K64_TN + 64 * j + lane;
+            xr[j] = xnorm[x < N ? x : N - 1];  // rows past N: +inf at the use (G > 0: N > 0)
+        }
+    };
+    // Per K-step g the vector-memory ops go out as ‖x‖²(g) (L2), A(g+1), B(g+3); at its end A(g+1) and B(g+1)
+    // must have landed and only B(g+3) is younger than A(g+1): vmcnt(4).  Loads retire
+    // in issue order, so the tile pieces lead by three K-steps (HBM misses) and the query fragments by one (L2
+    // hits) without either wait covering the other.  The waits are the builtin (s_waitcnt vmcnt(4) expcnt(7)
+    // lgkmcnt(15)), not inline asm: the compiler's wait pass must see them.
+    constexpr unsigned kWaitStep = 0xF70u | K64_PIECES;
+    auto clampg = [&](int64_t g) { return g < G ? g : G - 1; };  // past the end: the last K-step again, never read
+    if (G > 0) {
+        // the steady state's order: B(0), B(1), A(0), B(2)
         issue_b(0, 0);
-        issue_b(G > 1 ? 1 : 0, 1);
+        issue_b(clampg(1), 1);
+        issue_a(std::integral_constant<int, 0>{});
+        issue_b(clampg(2), 2);
     }
+    __builtin_amdgcn_s_waitcnt(kWaitStep);  // B(0), B(1), A(0) landed (B(2) in flight)
 
     int ks = 0, stage = 0;
     int64_t t = t0;
     auto body = [&](int64_t g, auto slot_c) {
         constexpr int SL = decltype(slot_c)::value;
-        // K-step g landed (this wave's ops; B(g+1) stays in flight), every wave done reading the stage about
-        // to be refilled (g−1's), one barrier; the issues are unconditional so the compiler's waits stay exact
-        k64_wait_vm<K64_PIECES>();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        // K-step g landed (the wait at the end of the previous K-step), every wave done reading the stage about to
+        // be refilled (g−2's): one barrier
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        issue_a(std::integral_constant<int, 1 - SL>{});
-        issue_b(g + 2 < G ? g + 2 : G - 1, stage == 0 ? NB - 1 : stage - 1);
+        // the tile's ‖x‖² for the epilogue (xnorm is deliberately not __restrict__: a read-only noalias argument's
+        // loads get sunk into the epilogue's block, where the wait for them is a vmcnt(0))
+        load_xn(t);
+        __builtin_amdgcn_sched_barrier(0);
         const k64_u32x4 *Bb = smem_k64 + stage * K64_SU;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
+            // A(g+1) spread over chunk 0's MFMAs, B(g+3) over chunk 1's last eight, after the K-step's last LDS
+            // read (the compiler keeps LDS reads behind an LDS-DMA in program order).  Issued together after the
+            // barrier instead, the eight vector-memory ops of all eight waves queue at once and hold back the
+            // MFMAs (17.4 vs 16.6 ms with one K-step in flight).
+            if (h == 0) issue_a(std::integral_constant<int, 1 - SL>{});
             // B fragment of rows 16·jb + m16, unit c = g4: slot c·256 + 16·jb + (m16 ^ 2c)
             const k64_u32x4 *Bc = Bb + h * K64_BU + g4 * K64_TN + (m16 ^ (g4 << 1));
             const k64_b16x8 a0 = __builtin_bit_cast(k64_b16x8, ar[SL][h][0]);
@@ -230,20 +246,41 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
                 acc[0][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[jb], acc[0][jb], 0, 0, 0);
                 acc[1][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf[jb], acc[1][jb], 0, 0, 0);
             }
-            // schedule (same region): four LDS reads ahead, then one read per MFMA pair
+            if (h == 1) issue_b(clampg(g + 3), stage < 2 ? stage + 3 : stage - 2);
+            // schedule (same region): four LDS reads ahead, then one read per MFMA pair, one vector-memory op per
+            // eight MFMAs
             __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
 #pragma unroll
-            for (int jb = 0; jb < 12; ++jb) {
+            for (int p = 0; p < 16; ++p) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                if (p < 12) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                if (h == 0 ? p % 4 == 1 : p >= 12) __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
             }
-            __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+            // chunk fence: A(g+1) stays in chunk 0, B(g+3) at the end of chunk 1 (their order is what the counted
+            // wait assumes)
+            __builtin_amdgcn_sched_barrier(0);
         }
+        // A(g+1), B(g+1) landed; B(g+2), B(g+3) stay in flight
+        __builtin_amdgcn_s_waitcnt(kWaitStep);
         stage = stage + 1 < NB ? stage + 1 : 0;
         if (++ks == ns) {
             ks = 0;
             const int64_t x0 = t * K64_TN;
-            k64_epilogue<L2M>(acc, cth, qnorm, q0wave, nq, xnorm, x0, N, Ld, Li, k, wave, lane);
+            // s = 2·q·x − ‖x‖² in place (the filter's left side; the key follows from it with one more rounding,
+            // inside the rerank bound's (d + 8)·2⁻²⁴ term); xr: row 64·j + l in lane l's xr[j]
+#pragma unroll
+            for (int jb = 0; jb < 16; ++jb) {
+                const float xs = __shfl(xr[jb >> 2], 16 * (jb & 3) + m16);
+                const float xv = x0 + 16 * jb + m16 < N ? xs : __builtin_inff();
+#pragma unroll
+                for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) acc[mb][jb][i] = fmaf(2.f, acc[mb][jb][i], -xv);
+            }
+            [&]<int... P>(std::integer_sequence<int, P...>) {
+                (k64_epilogue_row<L2M, P / 4, P % 4>(acc, cth, qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane),
+                 ...);
+            }(std::make_integer_sequence<int, 8>{});
 #pragma unroll
             for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
@@ -255,40 +292,103 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
         body(g, std::integral_constant<int, 0>{});
         if (g + 1 < G) body(g + 1, std::integral_constant<int, 1>{});
     }
-    k64_wait_vm<0>();  // no LDS-DMA copy may land after the block's LDS is handed to the next block
-    __syncthreads();
-    // per-(split, query) lists, query-major (ivf_rerank_topk reads a query's lists contiguously)
-    for (int r = 0; r < 32; ++r) {
-        const int ql = 32 * wave + r;
-        const int64_t q = q0 + ql;
-        if (q < nq && lane < k) {
-            const int64_t off = (q * nsplit + split) * k;
-            part_d[off + lane] = Ld[ql * k + lane];
-            part_i[off + lane] = Li[ql * k + lane];
+    // no LDS-DMA copy may land after the block's LDS is handed to the next block
+    __builtin_amdgcn_s_waitcnt(0xF70u);
+    if (lane < 32 && qlane < nq) cand_n[qlane * nsplit + split] = cntv;
+}
+
+// The k-th smallest candidate key of each query over all splits (its bound for the next pass), with the
+// margin of flat_bf16_seed, never above the current bound.  One wave per query.
+__global__ void __launch_bounds__(256) flat_cand_bound(const float *__restrict__ cand_d, const int *__restrict__ cand_n,
+                                                       int nsplit, int cap, int64_t nq, int k,
+                                                       float *__restrict__ bound) {
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq) return;
+    const int lane = threadIdx.x & 63;
+    WaveList<1, int> L;
+    L.init();
+    for (int s = 0; s < nsplit; ++s) {
+        const int n = min(cand_n[q * nsplit + s], cap);
+        const float *cd = cand_d + (q * nsplit + s) * (int64_t)cap;
+        for (int c0 = 0; c0 < n; c0 += 64) {
+            const int c = c0 + lane;
+            L.offer(c < n ? cd[c] : __builtin_inff(), lane, k - 1);
         }
+    }
+    if (lane == 0) {
+        const float t = readlane_f(L.d[0], k - 1);
+        const float tm = t == __builtin_inff() ? t : fmaxf(t * (1.f + 0x1p-20f), t + 0x1p-100f);
+        bound[q] = fminf(bound[q], tm);
     }
 }
 
-// The K-step-64 kernel applies to 256-query blocks over an image with an even chunk count; the caller
-// (launch_flat_bf16_topk) falls back to flat_bf16_topk otherwise.
-bool flat_bf16_k64_supported(int nk, int k) {
-    return nk % 2 == 0 && (size_t)K64_NB * K64_SU * 16 + (size_t)K64_QM * k * 8 <= 160 * 1024;
+// Each query's k best candidates (key, row) over all splits, ascending, into out_[di][q·k + j] — the list the
+// rerank merges (nsplit = 1).  A query whose buffer overflowed in some split is appended to flagged (the exact
+// fallback re-runs it).  One wave per query.
+__global__ void __launch_bounds__(256) flat_cand_select(const float *__restrict__ cand_d, const int *__restrict__ cand_i,
+                                                        const int *__restrict__ cand_n, int nsplit, int cap, int64_t nq,
+                                                        int k, float *__restrict__ out_d, int *__restrict__ out_i,
+                                                        int *__restrict__ nflag, int *__restrict__ flagged) {
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq) return;
+    const int lane = threadIdx.x & 63;
+    WaveList<1, int> L;
+    L.init();
+    bool over = false;
+    for (int s = 0; s < nsplit; ++s) {
+        const int nr = cand_n[q * nsplit + s];
+        over |= nr > cap;
+        const int n = min(nr, cap);
+        const int64_t base = (q * nsplit + s) * (int64_t)cap;
+        for (int c0 = 0; c0 < n; c0 += 64) {
+            const int c = c0 + lane;
+            L.offer(c < n ? cand_d[base + c] : __builtin_inff(), c < n ? cand_i[base + c] : 0x7fffffff, k - 1);
+        }
+    }
+    // an overflowed query gets an all-pad list: the rerank then finds no candidate and does not flag it a second
+    // time (flagged holds nq entries)
+    if (lane < k) {
+        out_d[q * k + lane] = over ? __builtin_inff() : L.d[0];
+        out_i[q * k + lane] = over ? 0x7fffffff : L.id[0];
+    }
+    if (over && lane == 0) flagged[atomicAdd(nflag, 1)] = (int)q;
 }
 
+bool flat_bf16_k64_supported(int nk, int k) { return nk % 2 == 0 && k <= 64; }
+
+size_t flat_bf16_k64_cap() { return 64; }
+
 void launch_flat_bf16_k64(const void *qimg, const float *qn, int64_t nq, const void *ximg, const float *xn, int64_t N,
-                          int nk, int metric, int k, int nqt, int nsplit, int64_t tiles_per_split, float *pd, int *pi,
-                          const float *seed, hipStream_t st) {
-    HIPANN_REQUIRE(flat_bf16_k64_supported(nk, k), "flat_bf16_k64: unsupported shape");
-    const size_t smem = (size_t)K64_NB * K64_SU * 16 + (size_t)K64_QM * k * 8;
+                          int nk, int metric, int nqt, int nsplit, int64_t tiles_per_split, int64_t tile_begin,
+                          int64_t tile_end, const float *bound, float *cand_d, int *cand_i, int *cand_n, int cap,
+                          bool resume, hipStream_t st) {
+    HIPANN_REQUIRE(nk % 2 == 0 && bound && cand_d && cand_i && cand_n && cap > 0, "flat_bf16_k64: bad arguments");
+    HIPANN_REQUIRE((int64_t)nqt * nsplit < 0x7fffffff, "grid too large");
     dim3 grid((unsigned)(nqt * nsplit)), block(64 * K64_W);
     const k64_u32x4 *qa = static_cast<const k64_u32x4 *>(qimg);
     const k64_u32x4 *xa = static_cast<const k64_u32x4 *>(ximg);
-    if (metric == kL2)
-        hipLaunchKernelGGL(flat_bf16_k64<true>, grid, block, smem, st, qa, qn, nq, xa, xn, N, nk, k, nqt, nsplit,
-                           tiles_per_split, pd, pi, seed);
-    else
-        hipLaunchKernelGGL(flat_bf16_k64<false>, grid, block, smem, st, qa, qn, nq, xa, xn, N, nk, k, nqt, nsplit,
-                           tiles_per_split, pd, pi, seed);
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, grid, block, K64_LDS, st, qa, qn, nq, xa, xn, N, nk, nqt, nsplit, tiles_per_split,
+                           tile_begin, tile_end, bound, cand_d, cand_i, cand_n, cap, resume ? 1 : 0);
+    };
+    if (metric == kL2) go(flat_bf16_k64<true>);
+    else go(flat_bf16_k64<false>);
+    HIPANN_CHECK(hipGetLastError());
+}
+
+void launch_flat_cand_bound(const float *cand_d, const int *cand_n, int nsplit, int cap, int64_t nq, int k,
+                            float *bound, hipStream_t st) {
+    if (nq <= 0) return;
+    hipLaunchKernelGGL(flat_cand_bound, dim3((unsigned)ceil_div(nq, 4)), dim3(256), 0, st, cand_d, cand_n, nsplit, cap,
+                       nq, k, bound);
+    HIPANN_CHECK(hipGetLastError());
+}
+
+void launch_flat_cand_select(const float *cand_d, const int *cand_i, const int *cand_n, int nsplit, int cap, int64_t nq,
+                             int k, float *out_d, int *out_i, int *nflag, int *flagged, hipStream_t st) {
+    if (nq <= 0) return;
+    hipLaunchKernelGGL(flat_cand_select, dim3((unsigned)ceil_div(nq, 4)), dim3(256), 0, st, cand_d, cand_i, cand_n,
+                       nsplit, cap, nq, k, out_d, out_i, nflag, flagged);
     HIPANN_CHECK(hipGetLastError());
 }
 

@@ -397,6 +397,13 @@ void launch_flat_bf16_seed(const float *pd, int nsplit, int64_t nq, int k, float
     HIPANN_CHECK(hipGetLastError());
 }
 
+// the bounded passes of flat_b16k64.hip apply to 256-query blocks over an even chunk count (HIPANN_B16_K64=0:
+// one pass of the 32-dim list kernel below, A/B)
+bool flat_bf16_resumable(int64_t nq, int d, int k) {
+    static const bool k64 = [] { const char *e = std::getenv("HIPANN_B16_K64"); return !e || std::atoi(e); }();
+    return k64 && flat_bf16_waves(nq) == 8 && flat_bf16_k64_supported(b16_nk(d), k);
+}
+
 void launch_flat_bf16_topk(const float *Q, const float *qn, int64_t nq, void *qimg, const void *ximg, const float *xn,
                            int64_t N, int d, int metric, int k, int nsplit, int64_t tiles_per_split, float *pd, int *pi,
                            const float *seed, bool image_ready, hipStream_t st) {
@@ -415,13 +422,6 @@ void launch_flat_bf16_topk(const float *Q, const float *qn, int64_t nq, void *qi
         hipLaunchKernelGGL(kern, grid, block, smem, st, qa, qn, nq, xa, xn, N, nk, k, nqt, nsplit, tiles_per_split, pd,
                            pi, seed);
     };
-    // 64-dim K-steps on 16×16×32 MFMA (flat_b16k64.hip) for 256-query blocks; HIPANN_B16_K64=0 keeps the
-    // 32-dim kernels below (A/B)
-    static const bool k64 = [] { const char *e = std::getenv("HIPANN_B16_K64"); return !e || std::atoi(e); }();
-    if (k64 && W == 8 && flat_bf16_k64_supported(nk, k)) {
-        launch_flat_bf16_k64(qimg, qn, nq, ximg, xn, N, nk, metric, k, nqt, nsplit, tiles_per_split, pd, pi, seed, st);
-        return;
-    }
     static const bool ra = [] { const char *e = std::getenv("HIPANN_B16_RA"); return !e || std::atoi(e); }();
     // RA stages (HIPANN_B16_NB = 3..5, A/B): LDS-DMA chunks in flight = NB − 1
     static const int nb = [] { const char *e = std::getenv("HIPANN_B16_NB"); const int v = e ? std::atoi(e) : 0;

@@ -10,6 +10,7 @@
 #include "ivf.hpp"
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
@@ -318,6 +319,9 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
     // 16th distances are ≈2 apart, inside its rounding bound (≈1.3), the 10th and 32nd ≈5
     if (exact) k = metric == kIP || form == kFlatBf16Exact ? kFlatRerankKIP : kRerankK;
     int64_t nsplit;
+    bool flags_ready = false;  // the bounded passes' select already reset nflag and flagged overflows
+    // the exact forms' max ‖x‖² (cached; its first computation uses sh.nflag as scratch, so before any flags)
+    const float xmax2 = exact ? flat_xmax2(sh, d, st) : 0.f;
     if (form == kFlatBf16Exact) {
         // one plain bf16 product per element over the tiled bf16 image (flat_bf16.hip), built once
         if (!sh.xb16_ok) {
@@ -371,9 +375,62 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
                                   (int)ceil_div(stiles, stps), stps, spd, spi, nullptr, false, st);
             launch_flat_bf16_seed(spd, (int)ceil_div(stiles, stps), nq, k, sh.seed.get<float>(), st);
         }
-        launch_flat_bf16_topk(xq, qn, nq, sh.qimg.p, sh.xb16.p, sh.xn.get<float>(), sh.n, d, metric, k, (int)nsplit,
-                              tps, sh.part_d.get<float>(), sh.part_i.get<int>(), seeded ? sh.seed.get<float>() : nullptr,
-                              seeded, st);
+        // bounded passes (64-dim K-step kernel, flat_b16k64.hip): every row with key ≤ the bound goes to a
+        // per-(query, split) candidate buffer.  Pass A covers the first ≈1/10 of every split under the 64K-row
+        // seed bound; the bound is then re-merged from its candidates (the k-th best key over ≈N/10 rows) and
+        // pass B covers the rest — ≈12 candidates per query and split at 10M rows instead of ≈76 under the
+        // seed alone, no row scanned twice.  flat_cand_select keeps each query's k best for the rerank.
+        static const int64_t pass_div = [] {
+            const char *e = std::getenv("HIPANN_FLAT_PASS_A");  // A/B: 1/x of each split in pass A; 0 = one pass
+            return e ? (int64_t)std::atoll(e) : (int64_t)10;
+        }();
+        if (seeded && flat_bf16_resumable(nq, d, k)) {
+            const int64_t tps_a = pass_div > 1 ? tps / pass_div : 0;
+            // per-(query, split) capacity: ≈12 expected at 10M rows with two passes, ≈76 under the seed alone
+            const int cap = (int)flat_bf16_k64_cap() * (tps_a >= 1 ? 1 : 3);
+            const size_t ncell = (size_t)nq * nsplit;
+            static const bool dbg = std::getenv("HIPANN_FLAT_CAND_DEBUG") != nullptr;
+            if (dbg) std::fprintf(stderr, "hipann flat cand: nq %lld nsplit %lld cap %d bytes %zu\n", (long long)nq,
+                                  (long long)nsplit, cap, ncell * ((size_t)cap * 8 + 4));
+            sh.cand.ensure(ncell * ((size_t)cap * 8 + 4), sh.device);
+            float *cd = sh.cand.get<float>();
+            int *ci = reinterpret_cast<int *>(cd + ncell * cap);
+            int *cn = ci + ncell * cap;
+            const int nk = (int)ceil_div(d, 32);
+            float *bound = sh.seed.get<float>();
+            if (tps_a >= 1) {
+                launch_flat_bf16_k64(sh.qimg.p, qn, nq, sh.xb16.p, sh.xn.get<float>(), sh.n, nk, metric, (int)nqt,
+                                     (int)nsplit, tps, 0, tps_a, bound, cd, ci, cn, cap, false, st);
+                launch_flat_cand_bound(cd, cn, (int)nsplit, cap, nq, k, bound, st);
+            }
+            launch_flat_bf16_k64(sh.qimg.p, qn, nq, sh.xb16.p, sh.xn.get<float>(), sh.n, nk, metric, (int)nqt,
+                                 (int)nsplit, tps, tps_a, tps, bound, cd, ci, cn, cap, tps_a >= 1, st);
+            sh.nflag.ensure(sizeof(int), sh.device);
+            sh.flagged.ensure(sizeof(int) * (size_t)nq, sh.device);
+            HIPANN_CHECK(hipMemsetAsync(sh.nflag.p, 0, sizeof(int), st));
+            // overflowed queries are flagged here, ahead of the rerank's own flags (the fallback re-runs both)
+            launch_flat_cand_select(cd, ci, cn, (int)nsplit, cap, nq, k, sh.part_d.get<float>(), sh.part_i.get<int>(),
+                                    sh.nflag.get<int>(), sh.flagged.get<int>(), st);
+            if (dbg) {
+                std::vector<int> hn(ncell);
+                std::vector<float> hb((size_t)nq);
+                HIPANN_CHECK(hipMemcpyAsync(hn.data(), cn, sizeof(int) * ncell, hipMemcpyDeviceToHost, st));
+                HIPANN_CHECK(hipMemcpyAsync(hb.data(), bound, sizeof(float) * nq, hipMemcpyDeviceToHost, st));
+                HIPANN_CHECK(hipStreamSynchronize(st));
+                long long tot = 0;
+                int mx = 0;
+                for (int v : hn) { tot += v; mx = std::max(mx, v); }
+                std::fprintf(stderr, "hipann flat cand: nsplit %lld tps %lld tps_a %lld mean %.2f max %d bound[0] %g\n",
+                             (long long)nsplit, (long long)tps, (long long)tps_a, (double)tot / (double)ncell, mx,
+                             (double)hb[0]);
+            }
+            nsplit = 1;
+            flags_ready = true;
+        } else {
+            launch_flat_bf16_topk(xq, qn, nq, sh.qimg.p, sh.xb16.p, sh.xn.get<float>(), sh.n, d, metric, k,
+                                  (int)nsplit, tps, sh.part_d.get<float>(), sh.part_i.get<int>(),
+                                  seeded ? sh.seed.get<float>() : nullptr, seeded, st);
+        }
     } else {
         const int64_t nqt = ceil_div(nq, 128);
         const int64_t ntiles = ceil_div(sh.n, 128);
@@ -407,10 +464,11 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
     }
     // exact form: merge each query's nsplit lists to the 16 best scan keys, recompute those rows in the
     // direct form, bound-check (ivf_rerank_topk, slot lists query-major); flagged queries re-run on split3
-    const float xmax2 = flat_xmax2(sh, d, st);
-    sh.nflag.ensure(sizeof(int), sh.device);
-    sh.flagged.ensure(sizeof(int) * (size_t)nq, sh.device);
-    HIPANN_CHECK(hipMemsetAsync(sh.nflag.p, 0, sizeof(int), st));
+    if (!flags_ready) {
+        sh.nflag.ensure(sizeof(int), sh.device);
+        sh.flagged.ensure(sizeof(int) * (size_t)nq, sh.device);
+        HIPANN_CHECK(hipMemsetAsync(sh.nflag.p, 0, sizeof(int), st));
+    }
     {
         ScopedTiming t(ix.timer_merge, st);
         launch_ivf_rerank(sh.part_d.get<float>(), sh.part_i.get<int>(), nullptr, (int)nsplit, nq, k, kout, metric, xq,

@@ -192,6 +192,7 @@ struct FlatShard {
     // kFlatBf16Exact: tiled bf16 image of the rows (built at the first search after an add) and the
     // batch's query image
     DevBuf xb16, qimg, seed;
+    DevBuf cand;  // bounded passes: per-(query, split) candidate buffers and counts
     bool xb16_ok = false;
     float bf16_rxmax = 0.f;  // max over rows of ‖bf16(x) − x‖ (the rerank's bound)
     StreamFence fence;       // cross-stream ordering of this shard's calls
@@ -361,11 +362,19 @@ void launch_b16_row_residual2(const float *X, int64_t n, int d, float *out, hipS
 void launch_flat_bf16_topk(const float *Q, const float *qn, int64_t nq, void *qimg, const void *ximg, const float *xn,
                            int64_t N, int d, int metric, int k, int nsplit, int64_t tiles_per_split, float *pd, int *pi,
                            const float *seed, bool image_ready, hipStream_t st);
+// bounded passes of the 64-dim K-step kernel (flat_b16k64.hip): candidate buffers, their bound and select
+bool flat_bf16_resumable(int64_t nq, int d, int k);
+size_t flat_bf16_k64_cap();
+void launch_flat_bf16_k64(const void *qimg, const float *qn, int64_t nq, const void *ximg, const float *xn, int64_t N,
+                          int nk, int metric, int nqt, int nsplit, int64_t tiles_per_split, int64_t tile_begin,
+                          int64_t tile_end, const float *bound, float *cand_d, int *cand_i, int *cand_n, int cap,
+                          bool resume, hipStream_t st);
+void launch_flat_cand_bound(const float *cand_d, const int *cand_n, int nsplit, int cap, int64_t nq, int k,
+                            float *bound, hipStream_t st);
+void launch_flat_cand_select(const float *cand_d, const int *cand_i, const int *cand_n, int nsplit, int cap, int64_t nq,
+                             int k, float *out_d, int *out_i, int *nflag, int *flagged, hipStream_t st);
 void launch_flat_bf16_seed(const float *pd, int nsplit, int64_t nq, int k, float *seed, hipStream_t st);
 bool flat_bf16_k64_supported(int nk, int k);
-void launch_flat_bf16_k64(const void *qimg, const float *qn, int64_t nq, const void *ximg, const float *xn, int64_t N,
-                          int nk, int metric, int k, int nqt, int nsplit, int64_t tiles_per_split, float *pd, int *pi,
-                          const float *seed, hipStream_t st);
 void launch_ivf_max_norm(const float *xn, int64_t n, unsigned *out, hipStream_t st);
 void launch_ivf_fallback(const int *nflag, const int *flagged, int64_t nq, const int64_t *probes, int nprobe, int metric,
                          const float *Q, const float *codes, int d, const int64_t *list_off, const int *list_len,

@@ -304,6 +304,28 @@ def test_flat_exact_form_matches_fp32_form_at_scale(gpu, form):
     assert (I1 == I0).mean() >= 0.995
 
 
+@pytest.mark.parametrize("metric", [0, 1])
+def test_flat_bf16_two_pass_resume(gpu, oracle, metric):
+    """The bf16 filter's two-pass schedule (1M rows, 64 splits of 61 tiles, nq = 512: pass A over the first
+    6 tiles of every split under the 64K-row seed bound, the bound re-merged, pass B resumed from pass A's
+    lists): the fp32 form's lists except inside near-tie windows, and the oracle's parity rule on a
+    query subset."""
+    rng = np.random.default_rng(11)
+    n, d, nq = 1_000_000, 64, 512
+    xb = rng.standard_normal((n, d), dtype=np.float32)
+    xq = rng.standard_normal((nq, d), dtype=np.float32)
+    ix = gpu.HipIndexFlat(d, metric, xb)
+    ix.form = ix.FORM_FP32
+    D0, I0 = ix.search(xq, 10)
+    ix.form = ix.FORM_BF16_EXACT
+    D1, I1 = ix.search(xq, 10)
+    scale = np.sum(xq.astype(np.float64) ** 2, 1)[:, None] + np.max(np.sum(xb.astype(np.float64) ** 2, 1))
+    assert (np.abs(D1 - D0) <= 1e-5 * scale).all()
+    assert (I1 == I0).mean() >= 0.995
+    Do, Io = oracle.flat_search(xb, xq[:48], 10, metric)
+    check_topk_parity(xb, xq[:48], D1[:48], I1[:48], Do, Io, metric)
+
+
 @pytest.mark.parametrize("n", [200, 1000, 3000])
 @pytest.mark.parametrize("metric", [0, 1])
 @pytest.mark.parametrize("k", [1, 7, 32, 64])
