@@ -106,8 +106,10 @@ __device__ __forceinline__ void k64_epilogue_row(const k64_f32x4 (&acc)[2][16], 
 // One bounded pass of a split: tiles [tile_begin, tile_end) of split `split` for the block's 256 queries.
 // Candidate buffers: cand_[dn]{[(q·nsplit + split)·cap + j]}, counts cand_n[q·nsplit + split] (resume: the
 // previous pass's count is continued).  bound[q]: the pass's T (k-th best key of a sample / previous pass,
-// with margin, flat_bf16_seed / flat_cand_bound).
-template <bool L2M>
+// with margin, flat_keys_kth / flat_cand_bound).
+// KEYS (the sample pass that seeds the bound): no filter, every key of the block's tiles goes to
+// cand_d[q·N + row] (a dense nq × N key matrix over the N sample rows; bound, cand_i, cand_n unused).
+template <bool L2M, bool KEYS>
 __global__ void __launch_bounds__(64 * K64_W, 1)
 flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm, int64_t nq,
               const k64_u32x4 *__restrict__ Xt, const float *xnorm, int64_t N, int nk, int nqt, int nsplit,
@@ -140,7 +142,7 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
     float qnl = 0.f;
     if (L2M) qnl = qlane < nq ? qnorm[qlane] : 0.f;
     int cntv = 0;
-    if (resume && lane < 32 && qlane < nq) cntv = cand_n[qlane * nsplit + split];
+    if (!KEYS && resume && lane < 32 && qlane < nq) cntv = cand_n[qlane * nsplit + split];
     float cth[2][4];
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb)
@@ -148,8 +150,12 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
         for (int i = 0; i < 4; ++i) {
             const int64_t q = q0w + 16 * mb + i;
             const float qn = (L2M && q < nq) ? qnorm[q] : 0.f;
-            const float thr = q < nq ? bound[q] : -__builtin_inff();  // −inf: rows past nq pass nothing
-            cth[mb][i] = L2M ? qn - thr : -2.f * thr;
+            if constexpr (KEYS) {
+                cth[mb][i] = qn;  // the keys pass keeps ‖q‖² of the lane's rows here
+            } else {
+                const float thr = q < nq ? bound[q] : -__builtin_inff();  // −inf: rows past nq pass nothing
+                cth[mb][i] = L2M ? qn - thr : -2.f * thr;
+            }
         }
     const int64_t cq = (int64_t)nsplit * cap;  // buffer stride between consecutive queries
     const int64_t cbase = ((q0 + 32 * wave) * nsplit + split) * (int64_t)cap;
@@ -277,10 +283,32 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
 #pragma unroll
                     for (int i = 0; i < 4; ++i) acc[mb][jb][i] = fmaf(2.f, acc[mb][jb][i], -xv);
             }
-            [&]<int... P>(std::integer_sequence<int, P...>) {
-                (k64_epilogue_row<L2M, P / 4, P % 4>(acc, cth, qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane),
-                 ...);
-            }(std::make_integer_sequence<int, 8>{});
+            if constexpr (KEYS) {
+                // every key (L2: ‖q‖² − s clamped at 0; IP: −s/2) into the dense key matrix
+#pragma unroll
+                for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int64_t q = q0w + 16 * mb + i;
+#pragma unroll
+                        for (int jb = 0; jb < 16; ++jb) {
+                            const int64_t x = x0 + 16 * jb + m16;
+                            float key;
+                            if (L2M) {
+                                key = cth[mb][i] - acc[mb][jb][i];
+                                key = key < 0.f ? 0.f : key;
+                            } else {
+                                key = -0.5f * acc[mb][jb][i];
+                            }
+                            if (q < nq && x < N) cand_d[q * N + x] = key;
+                        }
+                    }
+            } else {
+                [&]<int... P>(std::integer_sequence<int, P...>) {
+                    (k64_epilogue_row<L2M, P / 4, P % 4>(acc, cth, qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane),
+                     ...);
+                }(std::make_integer_sequence<int, 8>{});
+            }
 #pragma unroll
             for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
@@ -294,7 +322,41 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
     }
     // no LDS-DMA copy may land after the block's LDS is handed to the next block
     __builtin_amdgcn_s_waitcnt(0xF70u);
-    if (lane < 32 && qlane < nq) cand_n[qlane * nsplit + split] = cntv;
+    if (!KEYS && lane < 32 && qlane < nq) cand_n[qlane * nsplit + split] = cntv;
+}
+
+// Candidates of query q, one split per lane: round j offers entry j of splits s0 + lane (64 splits at a time),
+// the round's loads issued together ahead of its offers (a query holds ≈10-30 per split: ≈max-count rounds).
+template <bool WITH_IDS, typename F>
+__device__ __forceinline__ bool cand_offer_all(const float *__restrict__ cand_d, const int *__restrict__ cand_i,
+                                               const int *__restrict__ cand_n, int nsplit, int cap, int64_t q,
+                                               int lane, F offer) {
+    bool over = false;
+    for (int s0 = 0; s0 < nsplit; s0 += 64) {
+        const int s = s0 + lane;
+        const int nr = s < nsplit ? cand_n[q * nsplit + s] : 0;
+        over |= nr > cap;
+        const int n = nr < cap ? nr : cap;
+        int mx = n;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+        const int64_t base = (q * nsplit + s) * (int64_t)cap;
+        constexpr int U = 8;  // entries per lane loaded ahead of their offers
+        for (int j0 = 0; j0 < mx; j0 += U) {
+            float v[U];
+            int id[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const bool ok = j0 + u < n;
+                v[u] = ok ? cand_d[base + j0 + u] : __builtin_inff();
+                id[u] = WITH_IDS && ok ? cand_i[base + j0 + u] : 0x7fffffff;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (j0 + u < mx) offer(v[u], WITH_IDS ? id[u] : lane);
+        }
+    }
+    return __ballot(over) != 0ull;
 }
 
 // The k-th smallest candidate key of each query over all splits (its bound for the next pass), with the
@@ -307,14 +369,8 @@ __global__ void __launch_bounds__(256) flat_cand_bound(const float *__restrict__
     const int lane = threadIdx.x & 63;
     WaveList<1, int> L;
     L.init();
-    for (int s = 0; s < nsplit; ++s) {
-        const int n = min(cand_n[q * nsplit + s], cap);
-        const float *cd = cand_d + (q * nsplit + s) * (int64_t)cap;
-        for (int c0 = 0; c0 < n; c0 += 64) {
-            const int c = c0 + lane;
-            L.offer(c < n ? cd[c] : __builtin_inff(), lane, k - 1);
-        }
-    }
+    cand_offer_all<false>(cand_d, nullptr, cand_n, nsplit, cap, q, lane,
+                          [&](float v, int id) { L.offer(v, id, k - 1); });
     if (lane == 0) {
         const float t = readlane_f(L.d[0], k - 1);
         const float tm = t == __builtin_inff() ? t : fmaxf(t * (1.f + 0x1p-20f), t + 0x1p-100f);
@@ -334,17 +390,8 @@ __global__ void __launch_bounds__(256) flat_cand_select(const float *__restrict_
     const int lane = threadIdx.x & 63;
     WaveList<1, int> L;
     L.init();
-    bool over = false;
-    for (int s = 0; s < nsplit; ++s) {
-        const int nr = cand_n[q * nsplit + s];
-        over |= nr > cap;
-        const int n = min(nr, cap);
-        const int64_t base = (q * nsplit + s) * (int64_t)cap;
-        for (int c0 = 0; c0 < n; c0 += 64) {
-            const int c = c0 + lane;
-            L.offer(c < n ? cand_d[base + c] : __builtin_inff(), c < n ? cand_i[base + c] : 0x7fffffff, k - 1);
-        }
-    }
+    const bool over = cand_offer_all<true>(cand_d, cand_i, cand_n, nsplit, cap, q, lane,
+                                           [&](float v, int id) { L.offer(v, id, k - 1); });
     // an overflowed query gets an all-pad list: the rerank then finds no candidate and does not flag it a second
     // time (flagged holds nq entries)
     if (lane < k) {
@@ -354,6 +401,53 @@ __global__ void __launch_bounds__(256) flat_cand_select(const float *__restrict_
     if (over && lane == 0) flagged[atomicAdd(nflag, 1)] = (int)q;
 }
 
+// The k-th smallest of each query's S sample keys (keys[q·S + j]), with the margin of flat_bf16_seed: the seed
+// bound of the bounded passes.  One 256-thread block per query, the keys in registers (S ≤ 256·KPT), the k-th
+// order statistic by bisection on order-preserving bits (32 rounds of count-and-reduce).
+constexpr int KTH_KPT = 64;
+__global__ void __launch_bounds__(256) flat_keys_kth(const float *__restrict__ keys, int S, int64_t nq, int k,
+                                                     float *__restrict__ bound) {
+    const int64_t q = blockIdx.x;
+    if (q >= nq) return;
+    __shared__ int part[4];
+    unsigned u[KTH_KPT];
+#pragma unroll
+    for (int j = 0; j < KTH_KPT; ++j) {
+        const int c = j * 256 + (int)threadIdx.x;
+        const unsigned b = c < S ? __float_as_uint(keys[q * S + c]) : 0x7f800000u;  // +inf past S
+        u[j] = (b & 0x80000000u) ? ~b : (b | 0x80000000u);                        // order-preserving
+    }
+    unsigned lo = 0u, hi = 0xffffffffu;  // smallest t with #{u ≤ t} ≥ k
+    while (lo < hi) {
+        const unsigned mid = lo + (hi - lo) / 2u;
+        int c = 0;
+#pragma unroll
+        for (int j = 0; j < KTH_KPT; ++j) c += u[j] <= mid ? 1 : 0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+        __syncthreads();
+        if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+        __syncthreads();
+        const int tot = part[0] + part[1] + part[2] + part[3];
+        if (tot >= k) hi = mid;
+        else lo = mid + 1u;
+    }
+    if (threadIdx.x == 0) {
+        const unsigned b = (lo & 0x80000000u) ? (lo & 0x7fffffffu) : ~lo;
+        const float t = __uint_as_float(b);
+        bound[q] = t == __builtin_inff() ? t : fmaxf(t * (1.f + 0x1p-20f), t + 0x1p-100f);
+    }
+}
+
+int flat_keys_kth_max() { return 256 * KTH_KPT; }
+
+void launch_flat_keys_kth(const float *keys, int S, int64_t nq, int k, float *bound, hipStream_t st) {
+    if (nq <= 0) return;
+    HIPANN_REQUIRE(S >= k && S <= 256 * KTH_KPT, "flat_keys_kth: sample size");
+    hipLaunchKernelGGL(flat_keys_kth, dim3((unsigned)nq), dim3(256), 0, st, keys, S, nq, k, bound);
+    HIPANN_CHECK(hipGetLastError());
+}
+
 bool flat_bf16_k64_supported(int nk, int k) { return nk % 2 == 0 && k <= 64; }
 
 size_t flat_bf16_k64_cap() { return 64; }
@@ -361,8 +455,9 @@ size_t flat_bf16_k64_cap() { return 64; }
 void launch_flat_bf16_k64(const void *qimg, const float *qn, int64_t nq, const void *ximg, const float *xn, int64_t N,
                           int nk, int metric, int nqt, int nsplit, int64_t tiles_per_split, int64_t tile_begin,
                           int64_t tile_end, const float *bound, float *cand_d, int *cand_i, int *cand_n, int cap,
-                          bool resume, hipStream_t st) {
-    HIPANN_REQUIRE(nk % 2 == 0 && bound && cand_d && cand_i && cand_n && cap > 0, "flat_bf16_k64: bad arguments");
+                          bool resume, bool keys, hipStream_t st) {
+    HIPANN_REQUIRE(nk % 2 == 0 && cand_d && (keys || (bound && cand_i && cand_n && cap > 0)),
+                   "flat_bf16_k64: bad arguments");
     HIPANN_REQUIRE((int64_t)nqt * nsplit < 0x7fffffff, "grid too large");
     dim3 grid((unsigned)(nqt * nsplit)), block(64 * K64_W);
     const k64_u32x4 *qa = static_cast<const k64_u32x4 *>(qimg);
@@ -371,8 +466,13 @@ void launch_flat_bf16_k64(const void *qimg, const float *qn, int64_t nq, const v
         hipLaunchKernelGGL(kern, grid, block, K64_LDS, st, qa, qn, nq, xa, xn, N, nk, nqt, nsplit, tiles_per_split,
                            tile_begin, tile_end, bound, cand_d, cand_i, cand_n, cap, resume ? 1 : 0);
     };
-    if (metric == kL2) go(flat_bf16_k64<true>);
-    else go(flat_bf16_k64<false>);
+    if (keys) {
+        if (metric == kL2) go(flat_bf16_k64<true, true>);
+        else go(flat_bf16_k64<false, true>);
+    } else {
+        if (metric == kL2) go(flat_bf16_k64<true, false>);
+        else go(flat_bf16_k64<false, false>);
+    }
     HIPANN_CHECK(hipGetLastError());
 }
 

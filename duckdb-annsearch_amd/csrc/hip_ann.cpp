@@ -358,13 +358,35 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
         sh.part_d.ensure((size_t)nsplit * nq * k * sizeof(float), sh.device);
         sh.part_i.ensure((size_t)nsplit * nq * k * sizeof(int), sh.device);
         sh.qimg.ensure(flat_bf16_img_bytes(nq, d, 32 * W), sh.device);
-        // seed thresholds (large tables): the k-th best key of each query over the first 64K rows, from the same
-        // kernel on those rows (bit-identical keys); the main pass then admits only keys ≤ that bound
+        // seed bound (large tables): the k-th best key of each query over a sample of the first rows.  Bounded
+        // passes (below): the sample's keys from the same kernel in its keys mode (a dense nq × S matrix, one
+        // tile per block) and their k-th order statistic (flat_keys_kth); otherwise the 32-dim list kernel over
+        // 64K rows and flat_bf16_seed (its lists start empty: every row an insert, ≈1 ms at 1024 queries — what
+        // the keys mode replaces).  The main passes then admit only keys ≤ that bound.
         static const bool seed_env = [] { const char *e = std::getenv("HIPANN_FLAT_BF16_SEED"); return !e || std::atoi(e); }();
-        const int64_t seed_rows = 65536;
-        const bool seeded = seed_env && sh.n >= 8 * seed_rows;
+        const bool bounded = flat_bf16_resumable(nq, d, k);
+        const bool seeded = seed_env && sh.n >= 8 * 65536;
+        static const int64_t pass_div = [] {
+            const char *e = std::getenv("HIPANN_FLAT_PASS_A");  // A/B: 1/x of each split in pass A; 0 = one pass
+            return e ? (int64_t)std::atoll(e) : (int64_t)20;
+        }();
+        const int64_t tps_a = pass_div > 1 ? tps / pass_div : 0;
+        // per-(query, split) candidate capacity: ≈26 expected at 10M rows with two passes (tail ≈45); one pass
+        // under the seed alone: 32·N/16K/nsplit (≈300 at 10M) — a larger cap
+        const int cap = (int)flat_bf16_k64_cap() * (tps_a >= 1 ? 1 : 8);
+        const size_t ncell = (size_t)nq * nsplit;
+        const int64_t sample = std::min<int64_t>(16384, flat_keys_kth_max());
         ScopedTiming t(ix.timer_main, st);
-        if (seeded) {
+        if (seeded && bounded) {
+            sh.seed.ensure(sizeof(float) * (size_t)nq, sh.device);
+            sh.cand.ensure(std::max(ncell * ((size_t)cap * 8 + 4), (size_t)nq * sample * sizeof(float)), sh.device);
+            launch_b16_tile_rows(xq, nq, d, 32 * W, sh.qimg.p, st);
+            launch_flat_bf16_k64(sh.qimg.p, qn, nq, sh.xb16.p, sh.xn.get<float>(), sample, (int)ceil_div(d, 32), metric,
+                                 (int)nqt, (int)(sample / flat_bf16_tile_rows()), 1, 0, 1, nullptr, sh.cand.get<float>(),
+                                 nullptr, nullptr, 0, false, true, st);
+            launch_flat_keys_kth(sh.cand.get<float>(), (int)sample, nq, k, sh.seed.get<float>(), st);
+        } else if (seeded) {
+            const int64_t seed_rows = 65536;
             const int64_t stiles = seed_rows / flat_bf16_tile_rows();
             const int64_t snsplit = std::min<int64_t>(stiles, std::max<int64_t>(1, ceil_div(256, nqt)));
             const int64_t stps = ceil_div(stiles, snsplit);
@@ -376,23 +398,12 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
             launch_flat_bf16_seed(spd, (int)ceil_div(stiles, stps), nq, k, sh.seed.get<float>(), st);
         }
         // bounded passes (64-dim K-step kernel, flat_b16k64.hip): every row with key ≤ the bound goes to a
-        // per-(query, split) candidate buffer.  Pass A covers the first ≈1/10 of every split under the 64K-row
-        // seed bound; the bound is then re-merged from its candidates (the k-th best key over ≈N/10 rows) and
-        // pass B covers the rest — ≈12 candidates per query and split at 10M rows instead of ≈76 under the
-        // seed alone, no row scanned twice.  flat_cand_select keeps each query's k best for the rerank.
-        static const int64_t pass_div = [] {
-            const char *e = std::getenv("HIPANN_FLAT_PASS_A");  // A/B: 1/x of each split in pass A; 0 = one pass
-            return e ? (int64_t)std::atoll(e) : (int64_t)10;
-        }();
-        if (seeded && flat_bf16_resumable(nq, d, k)) {
-            const int64_t tps_a = pass_div > 1 ? tps / pass_div : 0;
-            // per-(query, split) capacity: ≈12 expected at 10M rows with two passes, ≈76 under the seed alone
-            const int cap = (int)flat_bf16_k64_cap() * (tps_a >= 1 ? 1 : 3);
-            const size_t ncell = (size_t)nq * nsplit;
+        // per-(query, split) candidate buffer.  Pass A covers the first ≈1/20 of every split under the 16K-row
+        // seed bound; the bound is then re-merged from its candidates (the k-th best key over ≈N/20 rows) and
+        // pass B covers the rest — ≈16 + 10 candidates per query and split at 10M rows (expected 32·rows/sample
+        // per query), no row scanned twice.  flat_cand_select keeps each query's k best for the rerank.
+        if (seeded && bounded) {
             static const bool dbg = std::getenv("HIPANN_FLAT_CAND_DEBUG") != nullptr;
-            if (dbg) std::fprintf(stderr, "hipann flat cand: nq %lld nsplit %lld cap %d bytes %zu\n", (long long)nq,
-                                  (long long)nsplit, cap, ncell * ((size_t)cap * 8 + 4));
-            sh.cand.ensure(ncell * ((size_t)cap * 8 + 4), sh.device);
             float *cd = sh.cand.get<float>();
             int *ci = reinterpret_cast<int *>(cd + ncell * cap);
             int *cn = ci + ncell * cap;
@@ -400,11 +411,11 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
             float *bound = sh.seed.get<float>();
             if (tps_a >= 1) {
                 launch_flat_bf16_k64(sh.qimg.p, qn, nq, sh.xb16.p, sh.xn.get<float>(), sh.n, nk, metric, (int)nqt,
-                                     (int)nsplit, tps, 0, tps_a, bound, cd, ci, cn, cap, false, st);
+                                     (int)nsplit, tps, 0, tps_a, bound, cd, ci, cn, cap, false, false, st);
                 launch_flat_cand_bound(cd, cn, (int)nsplit, cap, nq, k, bound, st);
             }
             launch_flat_bf16_k64(sh.qimg.p, qn, nq, sh.xb16.p, sh.xn.get<float>(), sh.n, nk, metric, (int)nqt,
-                                 (int)nsplit, tps, tps_a, tps, bound, cd, ci, cn, cap, tps_a >= 1, st);
+                                 (int)nsplit, tps, tps_a, tps, bound, cd, ci, cn, cap, tps_a >= 1, false, st);
             sh.nflag.ensure(sizeof(int), sh.device);
             sh.flagged.ensure(sizeof(int) * (size_t)nq, sh.device);
             HIPANN_CHECK(hipMemsetAsync(sh.nflag.p, 0, sizeof(int), st));

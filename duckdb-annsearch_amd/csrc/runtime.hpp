@@ -368,7 +368,9 @@ size_t flat_bf16_k64_cap();
 void launch_flat_bf16_k64(const void *qimg, const float *qn, int64_t nq, const void *ximg, const float *xn, int64_t N,
                           int nk, int metric, int nqt, int nsplit, int64_t tiles_per_split, int64_t tile_begin,
                           int64_t tile_end, const float *bound, float *cand_d, int *cand_i, int *cand_n, int cap,
-                          bool resume, hipStream_t st);
+                          bool resume, bool keys, hipStream_t st);
+int flat_keys_kth_max();
+void launch_flat_keys_kth(const float *keys, int S, int64_t nq, int k, float *bound, hipStream_t st);
 void launch_flat_cand_bound(const float *cand_d, const int *cand_n, int nsplit, int cap, int64_t nq, int k,
                             float *bound, hipStream_t st);
 void launch_flat_cand_select(const float *cand_d, const int *cand_i, const int *cand_n, int nsplit, int cap, int64_t nq,
