@@ -236,10 +236,11 @@ def attach_traffic(roof, key, algorithmic_bytes):
 # ------------------------------------------------------------------------------------------------
 # Flat
 # ------------------------------------------------------------------------------------------------
-FLAT_FORMS = {4: ("flat_bf16_topk", 1, BF16_MFMA_PEAK_TF,
-                  "bf16 MFMA (v_mfma_f32_32x32x16_bf16), one bf16 product per fp32 product over a tiled bf16 image of the "
-                  "rows; the scan keeps 16 (IP: 32) per (split, query) as a filter, merge_ms = exact fp32 direct-form "
-                  "rerank + bound check (E = 2^-7·(|q|²+max|x|²))"),
+FLAT_FORMS = {4: ("flat_bf16_k64", 1, BF16_MFMA_PEAK_TF,
+                  "bf16 MFMA (v_mfma_f32_16x16x32_bf16), one bf16 product per fp32 product over a tiled bf16 image of "
+                  "the rows; kernel_ms = the keys-mode seed pass + two bounded passes (rows with scan key <= a per-query "
+                  "bound to candidate buffers) + the bound / select kernels; merge_ms = exact fp32 direct-form rerank "
+                  "of the 32 best + bound check (Cauchy-Schwarz bound of the bf16 residuals)"),
               0: ("flat_gemm_topk2", 1, FP32_MFMA_PEAK_TF, "fp32 MFMA (v_mfma_f32_32x32x2_f32)"),
               1: ("flat_gemm_topk_bf", 6, BF16_MFMA_PEAK_TF,
                   "bf16 MFMA (v_mfma_f32_32x32x16_bf16) over a 3-term split: 6 bf16 products per fp32 product"),
@@ -298,22 +299,26 @@ def flat_config(args, torch, dist, hipann, rank, world, dev, n, d, nq, k, metric
         roof["frac_vs_fp32_peak"] = round(flops / (kern_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TF, 4)
         roof["fp32_peak"] = FP32_MFMA_PEAK_TF
     if form == 4 and kern_ms > 0:
-        # LDS-DMA fill of the bf16 scan: per 32-dim chunk the 256-row database tile (16 KB) — plus the query tile
-        # when the queries are not loaded straight into registers (RA, 256-query blocks)
+        # operand delivery of the bf16 scan (256 x 256 tiles): per 64-dim K-step the database tile (32 KB, LDS-DMA)
+        # and the 256 queries' fragments (32 KB, straight into registers) through the vector-memory return path —
+        # the unit the PMC pass finds busiest (profiles/r03/pmc_flat_k64.json)
         qm = 256 if nq >= 256 else 128 if nq >= 128 else 64
-        a_rows = 0 if qm == 256 and os.environ.get("HIPANN_B16_RA", "1") != "0" else qm  # RA: queries via VGPRs
-        fill = -(-nq // qm) * -(-n_local // 256) * -(-d // 32) * (a_rows + 256) * 64.0
-        roof["lds_fill"] = {"bytes_per_launch_gb": round(fill / 1e9, 2),
-                            "achieved_tbps": round(fill / (kern_ms * 1e-3) / 1e12, 2),
-                            "ceiling_note": "MI355X_MICROARCH.md: LDS-DMA streams measured at 6.4-6.8 TB/s chip-wide "
-                                            "(ldsdma-fill), an all-LDS-DMA prologue at 12-13 B/cycle/CU",
-                            "flop_per_byte": round(2.0 * nq * n_local * d / fill, 1)}
+        fill = -(-nq // qm) * -(-n_local // 256) * -(-d // 32) * (qm + 256) * 64.0
+        roof["operand_delivery"] = {"bytes_per_launch_gb": round(fill / 1e9, 2),
+                                    "achieved_tbps": round(fill / (kern_ms * 1e-3) / 1e12, 2),
+                                    "flop_per_byte": round(2.0 * nq * n_local * d / fill, 1),
+                                    "note": "L2 -> CU bytes of A + B per launch; TD busy 0.78 at 10M x 768 (PMC)"}
     if world == 1:
         attach_traffic(roof, f"flat_{n}x{d}{'' if metric == 0 else '_ip'}", 4.0 * n_local * d)
     out = {"workload": f"FAISS Flat {'L2' if metric == 0 else 'IP'}, {n}x{d} fp32, batch={nq}, k={k}",
            "value": round(nq * steps / el, 1), "unit": "queries/s", "ms_per_step": round(el * 1e3 / steps, 3),
            "steps": steps, "recall_at_10": None, "roofline": roof, "setup_s": round(setup_s, 1),
            "rerank_fallbacks_total": index.rerank_fallbacks()}
+    if form in (3, 4):
+        out["precision"] = ("returned distances are fp32 " + ("direct-form Σ(q−x)²" if metric == 0 else "dot products")
+                            + ", recomputed exactly for the kept candidates; FAISS CPU's BLAS path (nq >= 20) returns "
+                            "max(0, ‖q‖²+‖x‖²−2q·x) from sgemm: the same ids (parity tests), distances equal up to the "
+                            "fp32 rounding of the two forms. The bf16 scan is a certified filter, not the result.")
     if world > 1:
         return out, index, xb
     if host_rate:
