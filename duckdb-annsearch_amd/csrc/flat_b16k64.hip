@@ -133,7 +133,8 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
     const int64_t G = t1 > t0 ? (t1 - t0) * ns : 0;
 
     const int tid = threadIdx.x;
-    const int wave = tid >> 6, lane = tid & 63;
+    // wave-uniform (readfirstlane): the wave's bases and buffer pointers live in SGPRs, not VGPRs
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int m16 = lane & 15, g4 = lane >> 4;
     const int64_t q0w = q0 + 32 * wave + 4 * g4;  // + 16·mb + i: the lane's accumulator query rows
 

@@ -221,24 +221,31 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     sh.coarse_i.ensure((size_t)nq * np * sizeof(int64_t), sh.device);
     HIPANN_REQUIRE((int64_t)nq * np < (int64_t)0x7fffffff, "nq * nprobe too large");
     sh.slot_off.ensure(sizeof(int) * ((size_t)nq * np + 1), sh.device);
-    if (!sh.ccnt.p) {  // zeroed once; ivf_plan_q leaves it zero after every batch
-        sh.ccnt.ensure(sizeof(int) * (size_t)nlist, sh.device);
-        HIPANN_CHECK(hipMemsetAsync(sh.ccnt.p, 0, sizeof(int) * (size_t)nlist, st));
+    // per-list counts and fill cursors, double-buffered by batch parity (ivf_planfill_q zeroes the other
+    // parity's pair for the next batch; ivf_plan_q zeroes its own after use) — zeroed once per list count
+    if (!sh.ccnt.p || !sh.cursor2.p || sh.plan_nlist != nlist) {
+        sh.ccnt.ensure(sizeof(int) * 2 * (size_t)nlist, sh.device);
+        sh.cursor2.ensure(sizeof(int) * 2 * (size_t)nlist, sh.device);
+        HIPANN_CHECK(hipMemsetAsync(sh.ccnt.p, 0, sizeof(int) * 2 * (size_t)nlist, st));
+        HIPANN_CHECK(hipMemsetAsync(sh.cursor2.p, 0, sizeof(int) * 2 * (size_t)nlist, st));
+        sh.plan_nlist = nlist;
+        sh.plan_batch = 0;
     }
+    const int par = (int)(sh.plan_batch & 1u);
+    int *ccnt_cur = sh.ccnt.get<int>() + (size_t)par * nlist, *ccnt_next = sh.ccnt.get<int>() + (size_t)(1 - par) * nlist;
+    int *cur_cur = sh.cursor2.get<int>() + (size_t)par * nlist, *cur_next = sh.cursor2.get<int>() + (size_t)(1 - par) * nlist;
     sh.qtot.ensure(sizeof(int) * (size_t)nq, sh.device);
-    // ccnt must be zero between batches (ivf_plan_q clears it after use); the coarse select's count step and
-    // the plan add to it, so if anything throws before the plan has consumed this batch's counts, zero it
-    // again on the way out.
+    // this batch's counts must be zero on entry; the coarse select's count step adds to them, so if anything
+    // throws before the plan has consumed them, zero them again on the way out
     struct CcntReset {
-        IvfShard &sh;
+        int *p;
         int nlist;
         hipStream_t st;
         bool armed;
         ~CcntReset() {
-            if (armed && std::uncaught_exceptions() > 0)
-                (void)hipMemsetAsync(sh.ccnt.p, 0, sizeof(int) * (size_t)nlist, st);
+            if (armed && std::uncaught_exceptions() > 0) (void)hipMemsetAsync(p, 0, sizeof(int) * (size_t)nlist, st);
         }
-    } ccnt_reset{sh, nlist, st, true};
+    } ccnt_reset{ccnt_cur, nlist, st, true};
     // the decomposed form needs float4 rows; other shapes take the direct kernel (also on the GPU)
     // the decomposed forms need float4 rows (else the direct kernel, also on the GPU); the MFMA kernel
     // keeps 16-lane lists (k <= 16) and the item's queries in LDS (else the VALU decomposed kernel)
@@ -293,7 +300,7 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
         qsh0.qn_given_nq = nq;
     }
     // the plan's per-query count step rides on the coarse probe select when that path is taken
-    IvfPlanHook hook{sh.list_len.get<int>(), nlist, ivf_chunk_rows(), sh.ccnt.get<int>(), sh.slot_off.get<int>(),
+    IvfPlanHook hook{sh.list_len.get<int>(), nlist, ivf_chunk_rows(), ccnt_cur, sh.slot_off.get<int>(),
                      sh.qtot.get<int>(), false};
     FlatShard &qsh = *sh.quant->shards[0];
     qsh.plan_hook = ivf_plan_query_major() ? &hook : nullptr;
@@ -310,14 +317,14 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     sh.cnt.ensure(sizeof(int) * (nlist + 1), sh.device);
     sh.bucket_off.ensure(sizeof(int) * (nlist + 1), sh.device);
     sh.item_off.ensure(sizeof(int) * (nlist + 1), sh.device);
-    sh.cursor.ensure(sizeof(int) * (nlist + 1), sh.device);
     sh.bucket.ensure(sizeof(int) * (size_t)nq * np, sh.device);
     HIPANN_REQUIRE((int64_t)nq * np < (int64_t)0x7fffffff, "nq * nprobe too large");
     sh.slot_off.ensure(sizeof(int) * ((size_t)nq * np + 1), sh.device);
     launch_ivf_plan(sh.coarse_i.get<int64_t>(), nq, np, sh.list_len.get<int>(), nlist, group, sh.cnt.get<int>(),
-                    sh.bucket_off.get<int>(), sh.item_off.get<int>(), sh.cursor.get<int>(), sh.bucket.get<int>(),
-                    sh.slot_off.get<int>(), st, exact ? sh.nflag.get<int>() : nullptr, qbound, sh.ccnt.get<int>(),
-                    sh.qtot.get<int>(), hook.done);
+                    sh.bucket_off.get<int>(), sh.item_off.get<int>(), cur_cur, sh.bucket.get<int>(),
+                    sh.slot_off.get<int>(), st, exact ? sh.nflag.get<int>() : nullptr, qbound, ccnt_cur,
+                    sh.qtot.get<int>(), hook.done, ccnt_next, cur_next);
+    sh.plan_batch++;
     ccnt_reset.armed = false;
     // 3. scan: one k-list per (query, probe, row chunk) slot — every slot is written by exactly one item
     const size_t parts = (size_t)np * nq * sh.max_nch * k;

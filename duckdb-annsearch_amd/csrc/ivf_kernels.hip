@@ -279,6 +279,108 @@ __global__ void __launch_bounds__(256) ivf_fill_q(const int64_t *__restrict__ pr
     }
 }
 
+// ivf_planfill_q — ivf_plan_q and ivf_fill_q in one launch (nlist ≤ kPlanFillMaxList): every block recomputes
+// the two prefixes it needs from the counts — the lists' bucket offsets (nlist values) and its queries' slot
+// bases (a sum over the preceding queries' totals) — instead of waiting for a one-block scan; block 0
+// publishes the scan's tables (cnt, bucket_off, item_off, the slot total) and the batch's resets.  The
+// per-list counts and fill cursors are double-buffered by batch parity: this batch reads ccnt / cursor (zero
+// on entry) and zeroes the other pair for the next batch (its count step runs after this kernel).
+constexpr int kPlanFillMaxList = 8192;
+__device__ __forceinline__ int block_excl_scan256(int v, int *s_w) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(x, o);
+        if (lane >= o) x += t;
+    }
+    if (lane == 63) s_w[wave] = x;
+    __syncthreads();
+    int base = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) base += w < wave ? s_w[w] : 0;
+    __syncthreads();
+    return base + x - v;
+}
+__global__ void __launch_bounds__(256) ivf_planfill_q(const int64_t *__restrict__ probes, int64_t nq, int nprobe,
+                                                      const int *__restrict__ list_len, int nlist, int group,
+                                                      const int *__restrict__ ccnt, int *__restrict__ ccnt_next,
+                                                      int *__restrict__ cursor, int *__restrict__ cursor_next,
+                                                      const int *__restrict__ qtot, int *__restrict__ slot_off,
+                                                      int64_t npairs, int *__restrict__ cnt, int *__restrict__ bucket_off,
+                                                      int *__restrict__ item_off, int *__restrict__ bucket,
+                                                      int *__restrict__ nflag_reset, unsigned *__restrict__ qbound) {
+    __shared__ int s_boff[kPlanFillMaxList];
+    __shared__ int s_w[4], s_qb[4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t q0 = (int64_t)blockIdx.x * 4;
+    // list bucket offsets: thread t owns lists [t·per, (t+1)·per)
+    const int per = (nlist + 255) / 256;
+    int sum = 0, isum = 0;
+    for (int j = 0; j < per; ++j) {
+        const int l = tid * per + j;
+        if (l < nlist) {
+            const int c = ccnt[l];
+            sum += c;
+            if (blockIdx.x == 0) isum += ((c + group - 1) / group) * ivf_nch(list_len[l]);
+        }
+    }
+    int b = block_excl_scan256(sum, s_w);
+    int ib = blockIdx.x == 0 ? block_excl_scan256(isum, s_w) : 0;
+    for (int j = 0; j < per; ++j) {
+        const int l = tid * per + j;
+        if (l < nlist) {
+            const int c = ccnt[l];
+            s_boff[l] = b;
+            if (blockIdx.x == 0) {
+                cnt[l] = c;
+                bucket_off[l] = b;
+                item_off[l] = ib;
+                ib += ((c + group - 1) / group) * ivf_nch(list_len[l]);
+            }
+            b += c;
+        }
+    }
+    if (blockIdx.x == 0 && tid == 255) {
+        bucket_off[nlist] = b;
+        item_off[nlist] = ib;
+    }
+    // the next batch's counts and cursors start at zero (each block clears a slice)
+    for (int l = (int)blockIdx.x * 256 + tid; l < nlist; l += (int)gridDim.x * 256) {
+        ccnt_next[l] = 0;
+        cursor_next[l] = 0;
+    }
+    // this block's queries' slot bases: Σ qtot over the preceding queries
+    int qs = 0;
+    for (int64_t q = tid; q < q0; q += 256) qs += qtot[q];
+    const int qb0 = block_excl_scan256(qs, s_w) + qs;  // the block-wide total (inclusive of the last thread)
+    if (tid == 255) s_qb[0] = qb0;
+    __syncthreads();
+    if (tid == 0) {
+        int acc = s_qb[0];
+        for (int i = 0; i < 4; ++i) {
+            s_qb[i] = acc;
+            acc += q0 + i < nq ? qtot[q0 + i] : 0;
+        }
+        if (q0 + 4 >= nq) slot_off[npairs] = acc;  // the last block: every query's slots
+        if (blockIdx.x == 0 && nflag_reset) *nflag_reset = 0;
+    }
+    __syncthreads();
+    // fill (one wave per query): slot_off += the query's base, bucket
+    const int64_t q = q0 + wave;
+    if (q >= nq) return;
+    if (qbound && lane == 0) qbound[q] = 0xff800000u;
+    const int base = s_qb[wave];
+    for (int p = lane; p < nprobe; p += 64) {
+        const int64_t i = q * nprobe + p;
+        slot_off[i] += base;
+        const int64_t l = probes[i];
+        if (l < 0 || l >= nlist || list_len[l] <= 0) continue;
+        const int pos = atomicAdd(cursor + l, 1);
+        bucket[s_boff[l] + pos] = (int)i;
+    }
+}
+
 // Row staging: IVF_TR rows × IVF_BK dims = IVF_TR·IVF_BK/4 float4, IVF_SP per thread.
 constexpr int IVF_F4 = IVF_BK / 4;                     // float4 per staged row segment
 constexpr int IVF_SP = IVF_TR * IVF_F4 / IVF_THREADS;  // float4 staged per thread
@@ -1022,18 +1124,31 @@ bool ivf_plan_query_major() {
 
 void launch_ivf_plan(const int64_t *probes, int64_t nq, int nprobe, const int *list_len, int nlist, int group,
                      int *cnt, int *bucket_off, int *item_off, int *cursor, int *bucket, int *slot_off,
-                     hipStream_t st, int *nflag_reset, unsigned *qbound, int *ccnt, int *qtot, bool counted) {
+                     hipStream_t st, int *nflag_reset, unsigned *qbound, int *ccnt, int *qtot, bool counted,
+                     int *ccnt_next, int *cursor_next) {
     const int64_t npairs = nq * nprobe;
     if (ivf_plan_query_major() && ccnt && qtot) {
         const unsigned gq = (unsigned)std::max<int64_t>(1, ceil_div(nq, (int64_t)4));
         if (nq > 0 && !counted)  // counted: the coarse probe select already did this step (IvfPlanHook)
             hipLaunchKernelGGL(ivf_count_q, dim3(gq), dim3(256), 0, st, probes, nq, nprobe, list_len, nlist, ccnt,
                                slot_off, qtot);
+        // one launch (double-buffered counts and cursors) when the lists fit the block's LDS; HIPANN_IVF_PLANFILL=0
+        // keeps the two (A/B)
+        static const bool fused_env = [] { const char *e = std::getenv("HIPANN_IVF_PLANFILL"); return !e || std::atoi(e); }();
+        if (fused_env && ccnt_next && cursor_next && nlist <= kPlanFillMaxList && nq > 0) {
+            hipLaunchKernelGGL(ivf_planfill_q, dim3(gq), dim3(256), 0, st, probes, nq, nprobe, list_len, nlist, group,
+                               ccnt, ccnt_next, cursor, cursor_next, qtot, slot_off, npairs, cnt, bucket_off, item_off,
+                               bucket, nflag_reset, qbound);
+            HIPANN_CHECK(hipGetLastError());
+            return;
+        }
         hipLaunchKernelGGL(ivf_plan_q, dim3(1), dim3(1024), 0, st, ccnt, list_len, nlist, group, cnt, bucket_off,
                            item_off, cursor, qtot, nq, npairs, slot_off, nflag_reset, qbound);
         if (nq > 0)
             hipLaunchKernelGGL(ivf_fill_q, dim3(gq), dim3(256), 0, st, probes, nq, nprobe, list_len, nlist, qtot,
                                bucket_off, cursor, bucket, slot_off);
+        if (cursor_next)  // the fused path expects the other parity's cursors at zero (ivf_plan_q zeroed this one)
+            HIPANN_CHECK(hipMemsetAsync(cursor_next, 0, sizeof(int) * (size_t)nlist, st));
         HIPANN_CHECK(hipGetLastError());
         return;
     }

@@ -253,6 +253,11 @@ struct IvfShard {
     float xmax2 = -1.f;
     DevBuf nflag, flagged, fq, fD, fI, coarse_save, tmpnorm;
     DevBuf ccnt, qtot;             // query-major plan: per-list running counts (kept zero between batches), per-query slot totals
+    // the fused plan + fill (ivf_planfill_q): counts and fill cursors double-buffered by batch parity
+    // ([2][nlist] each in ccnt / cursor2, zeroed at allocation; each batch zeroes the other parity's pair)
+    DevBuf cursor2;
+    uint64_t plan_batch = 0;
+    int plan_nlist = 0;
     DevBuf fpd, fpi;               // device fallback: per (flagged query, probe) partial lists
     DevBuf fb_total;               // u64 running count of flagged queries (device side)
     // MFMA scan copy of the codes, built at the first search that uses it: per list, 32-row passes of
@@ -325,7 +330,7 @@ void launch_flat_scan_topk(const float *Q, int nq, const float *X, int64_t N, in
 void launch_ivf_plan(const int64_t *probes, int64_t nq, int nprobe, const int *list_len, int nlist, int group,
                      int *cnt, int *bucket_off, int *item_off, int *cursor, int *bucket, int *slot_off,
                      hipStream_t st, int *nflag_reset = nullptr, unsigned *qbound = nullptr, int *ccnt = nullptr,
-                     int *qtot = nullptr, bool counted = false);
+                     int *qtot = nullptr, bool counted = false, int *ccnt_next = nullptr, int *cursor_next = nullptr);
 int64_t ivf_max_items(int64_t nq, int nprobe, int nlist, int max_nch, int64_t nrows, int group);
 int ivf_mfma_bf_group(int d, int np);
 bool ivf_mfma_bf_supported(const float *Q, int d, const float *codes, int k, int np);
