@@ -951,8 +951,8 @@ int diskann_hip_search_batch_resident_device(void *h, const uint32_t *eps, int n
                 const double st = (double)std::max<unsigned long long>(hs[2], 1);
                 std::fprintf(stderr,
                              "[bfs-prof] wave-0 cycles per step: select %.0f adjacency %.0f dedupe %.0f visited %.0f "
-                             "dist %.0f insert %.0f\n",
-                             hs[3] / st, hs[4] / st, hs[5] / st, hs[6] / st, hs[7] / st, hs[8] / st);
+                             "dist %.0f insert %.0f; speculated rows used %.3f\n",
+                             hs[3] / st, hs[4] / st, hs[5] / st, hs[6] / st, hs[7] / st, hs[8] / st, hs[9] / st);
             }
             gevals = (int64_t)hs[0];
             gsteps = (int64_t)hs[1];

@@ -42,6 +42,9 @@ namespace {
 #ifndef HIPANN_BFS_PROF
 #define HIPANN_BFS_PROF 0  // tuning builds: per-phase shader-clock totals of wave 0 into stats[3..6]
 #endif
+#ifndef HIPANN_BFS_SPEC
+#define HIPANN_BFS_SPEC 0  // speculative row / visited-word fetch of the next expansion (measured slower, off)
+#endif
 #ifndef HIPANN_BFS_RV
 #define HIPANN_BFS_RV 128  // VGPRs of row data in flight per lane (rows_in_flight)
 #endif
@@ -450,6 +453,33 @@ diskann_bfs(const float *__restrict__ Qs, int nq, int d, const uint8_t *__restri
     int flag = 0;
     unsigned long long evals = 0;
     int steps = 0;
+    // Speculated next expansion (wave 0).  The adjacency row and the visited words of the entry most
+    // likely to be popped next are fetched while the current step's rows are gathered or inserted, so a
+    // correct guess starts the next step's gather without the two dependent round trips (adjacency,
+    // then visited).  A guess never changes what is computed: it is used only when its id equals the
+    // popped one, its visited words were read after every mark of earlier steps (only this workgroup
+    // writes this bitmap), and each mark it implies is confirmed by the returned old word (a
+    // mismatch flags the query for the host path).
+    //   sp_state 0: nothing; 1: sp_nb / sp_md loaded; 2: sp_w (visited word of lane's neighbour) too.
+    unsigned sp_id = kNone;
+    uint32_t sp_nb = kNone, sp_w = 0;
+    bool sp_md = true;
+    int sp_state = 0;
+    unsigned long long sp_hits = 0;
+    uint64_t mark_lanes = 0;    // this step's speculative marks: lanes whose old word must be unmarked
+    uint32_t mark_old = 0, mark_bit = 0;
+    auto adj_row = [&](unsigned id, uint32_t &nb_out, bool &md_out) {
+        nb_out = lane < R ? adj[(size_t)id * R + lane] : kNone;
+        md_out = dupw == nullptr || ((dupw[id >> 5] >> (id & 31)) & 1u);
+    };
+    // visited words of a row's valid neighbours: device-scope loads, which bypass the CU's L1 and read
+    // L2, where the marks (atomics) land
+    auto visited_words = [&](uint32_t nbv) -> uint32_t {
+        const uint64_t s = __ballot(lane < R && nbv == kNone);
+        const int f = s ? __ffsll((unsigned long long)s) - 1 : R;
+        return (lane < f && nbv < N) ? __hip_atomic_load(vis + (nbv >> 5), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                     : 0u;
+    };
 
     const uint64_t lanes_below = (1ull << lane) - 1;  // lane 63: all lower lanes (no overflow)
 #if HIPANN_BFS_PROF
@@ -515,6 +545,10 @@ diskann_bfs(const float *__restrict__ Qs, int nq, int d, const uint8_t *__restri
       if (wave == 0) {
         while (!flag) {
         steps++;
+        if (sp_state == 1) {  // a guessed row arrived during the inserts: its visited words now
+            sp_w = visited_words(sp_nb);
+            sp_state = 2;
+        }
         const float thr = len >= L ? res.get_d(L - 1) : __builtin_inff();
         uint64_t best = ~0ull;
 #pragma unroll
@@ -565,10 +599,16 @@ diskann_bfs(const float *__restrict__ Qs, int nq, int d, const uint8_t *__restri
         }
         BFS_T(0);
         // expand: neighbours up to the first sentinel, ids < N, visited insert in order
-        const uint32_t nb = lane < R ? adj[(size_t)cid * R + lane] : kNone;
+        const bool hit = HIPANN_BFS_SPEC && sp_state != 0 && cid == sp_id;
+        const bool hit_w = hit && sp_state == 2;
+        sp_hits += hit ? 1 : 0;
+        uint32_t nb;
         // rows flagged at registration as holding a repeated id before their first sentinel (none in
         // a Vamana graph) take the dedupe below; every other row skips it
-        const bool maydup = dupw == nullptr || ((dupw[cid >> 5] >> (cid & 31)) & 1u);
+        bool maydup;
+        if (hit) { nb = sp_nb; maydup = sp_md; }
+        else adj_row(cid, nb, maydup);
+        sp_state = 0;
         const uint64_t sent = __ballot(lane < R && nb == kNone);
         BFS_T(1);
         const int first = sent ? __ffsll((unsigned long long)sent) - 1 : R;
@@ -590,8 +630,16 @@ diskann_bfs(const float *__restrict__ Qs, int nq, int d, const uint8_t *__restri
         }
         BFS_T(2);
         bool fresh = false;
-        if (valid && !dup) {
-            const unsigned bit = 1u << (nb & 31);
+        const unsigned bit = 1u << (nb & 31);
+        mark_lanes = 0;
+        if (hit_w) {
+            // visited words read after every earlier mark: fresh is decided now; the marks go out
+            // and their old words are checked after the gather
+            fresh = valid && !dup && !(sp_w & bit);
+            if (fresh) mark_old = atomicOr(vis + (nb >> 5), bit);
+            mark_bit = bit;
+            mark_lanes = __ballot(fresh);
+        } else if (valid && !dup) {
             fresh = !(atomicOr(vis + (nb >> 5), bit) & bit);
         }
         const uint64_t m = __ballot(fresh);
@@ -611,6 +659,9 @@ diskann_bfs(const float *__restrict__ Qs, int nq, int d, const uint8_t *__restri
       __syncthreads();
       if (wave == 0) {
         BFS_T(4);
+        // the speculative marks' old words: each must have been unmarked, as the guess assumed
+        if (__ballot(((mark_lanes >> lane) & 1ull) && (mark_old & mark_bit))) flag = 1;
+        mark_lanes = 0;
         // insert_result in neighbour order
         const float dd = lane < cnt ? s_dist[lane] : 0.f;
         const unsigned nbr = lane < cnt ? s_ids[lane] : kNone;
@@ -619,6 +670,31 @@ diskann_bfs(const float *__restrict__ Qs, int nq, int d, const uint8_t *__restri
         const bool full = len >= L;
         const float thr0 = full ? res.get_d(len - 1) : 0.f;
         uint64_t am = __ballot(lane < cnt && (!full || dd < thr0));
+        if (HIPANN_BFS_SPEC) {
+            // the next pop is almost always the smallest of the unexpanded entries, the spill list and the
+            // admitted candidates (a superset of what the inserts leave poppable): fetch its adjacency row
+            // behind the inserts; its visited words go out at the top of the next step
+            uint64_t b = ~0ull;
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                const int e = s * 64 + lane;
+                if (e < len && !(res.id[s] & kExpanded)) {
+                    const uint64_t c = ((uint64_t)ford(res.d[s]) << 32) | res.id[s];
+                    b = c < b ? c : b;
+                }
+            }
+            if (lane < nspill) b = spill < b ? spill : b;
+            if ((am >> lane) & 1ull) {
+                const uint64_t c = ((uint64_t)ford(dd) << 32) | nbr;
+                b = c < b ? c : b;
+            }
+            b = wmin_u64(b);
+            if (b != ~0ull) {
+                sp_id = (unsigned)b;
+                adj_row(sp_id, sp_nb, sp_md);
+                sp_state = 1;
+            }
+        }
         // Many admitted candidates and no equal / non-finite distance anywhere: the inserts in neighbour
         // order end in exactly the first L of the sorted union (each binary search lands on the unique
         // insertion point; a candidate rejected at its turn already had L smaller entries ahead of it;
@@ -678,6 +754,7 @@ diskann_bfs(const float *__restrict__ Qs, int nq, int d, const uint8_t *__restri
         atomicAdd(stats + 0, evals);
         atomicMax(stats + 1, (unsigned long long)steps);
         atomicAdd(stats + 2, (unsigned long long)steps);
+        atomicAdd(stats + 9, sp_hits);
     }
 }
 

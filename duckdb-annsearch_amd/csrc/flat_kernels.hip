@@ -1481,6 +1481,131 @@ flat_keys_small(const float *__restrict__ Q, const float *__restrict__ qnorm, in
     }
 }
 
+// flat_keys_ksplit — flat_keys_small's 64 × 64 tiles on 8 waves: waves 0-3 run the first half of the k
+// chunks and waves 4-7 the second (each half its own two LDS buffers, the halves in lock step on the block
+// barrier), then half 1 hands its accumulators to half 0 through LDS: key = f(acc₀ + acc₁).  Two waves per
+// SIMD instead of one, so each SIMD's MFMA chain is half as long and the other wave hides its LDS reads and
+// barrier waits.  Needs an even chunk count (d = 768: 12 + 12); the sum differs from the one-pass k order
+// by the split (deterministic; the coarse keys are not bit-pinned to any CPU order).
+template <bool VEC4>
+__device__ __forceinline__ void ks_stage_load(const float *__restrict__ base, int64_t row0, int64_t nrows, int d, int k0,
+                                              int t, float4 (&r)[2]) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const int f = t + 256 * p;
+        const int row = f >> 3, c4 = f & 7;
+        const int64_t grow = row0 + row;
+        const int kk = k0 + 4 * c4;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (grow < nrows) {
+            const float *src = base + grow * (int64_t)d + kk;
+            if (VEC4) {
+                if (kk < d) v = *reinterpret_cast<const float4 *>(src);
+            } else {
+                if (kk + 0 < d) v.x = src[0];
+                if (kk + 1 < d) v.y = src[1];
+                if (kk + 2 < d) v.z = src[2];
+                if (kk + 3 < d) v.w = src[3];
+            }
+        }
+        r[p] = v;
+    }
+}
+__device__ __forceinline__ void ks_stage_store(float *__restrict__ lds, int t, const float4 (&r)[2]) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const int f = t + 256 * p;
+        *reinterpret_cast<float4 *>(lds + (f >> 3) * GLD + 4 * (f & 7)) = r[p];
+    }
+}
+
+template <bool VEC4>
+__global__ void __launch_bounds__(512)
+flat_keys_ksplit(const float *__restrict__ Q, const float *__restrict__ qnorm, int64_t nq, const float *__restrict__ X,
+                 const float *__restrict__ xnorm, int64_t N, int d, int metric, int nqt, float *__restrict__ keys_out,
+                 int64_t ldk) {
+    __shared__ __attribute__((aligned(16))) float As[2][2][SBM * GLD], Bs[2][2][SBM * GLD];
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int qt = lb % nqt;
+    const int64_t q0 = (int64_t)qt * SBM, x0 = (int64_t)(lb / nqt) * SBM;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int half = wave >> 2, t = threadIdx.x & 255;
+    const int wr = (wave >> 1) & 1, wc = wave & 1;
+    const int l31 = lane & 31, h = lane >> 5;
+    const int nkh = ((d + GBK - 1) / GBK) >> 1;  // chunks per half (the launcher checks the count is even)
+    const int kbase = half * nkh * GBK;
+    float4 sa[2][2], sb[2][2];
+    ks_stage_load<VEC4>(Q, q0, nq, d, kbase, t, sa[0]);
+    ks_stage_load<VEC4>(X, x0, N, d, kbase, t, sb[0]);
+    ks_stage_store(As[half][0], t, sa[0]);
+    ks_stage_store(Bs[half][0], t, sb[0]);
+    if (nkh > 1) {
+        ks_stage_load<VEC4>(Q, q0, nq, d, kbase + GBK, t, sa[1]);
+        ks_stage_load<VEC4>(X, x0, N, d, kbase + GBK, t, sb[1]);
+    }
+    if (nkh > 2) {
+        ks_stage_load<VEC4>(Q, q0, nq, d, kbase + 2 * GBK, t, sa[0]);
+        ks_stage_load<VEC4>(X, x0, N, d, kbase + 2 * GBK, t, sb[0]);
+    }
+    __syncthreads();
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    auto step = [&](int kc, auto par_c) {
+        constexpr int P = decltype(par_c)::value;
+        const float *Ab = As[half][P], *Bb = Bs[half][P];
+        f32x4 a4[4], b4[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            a4[u] = *reinterpret_cast<const f32x4 *>(Ab + (32 * wr + l31) * GLD + 16 * h + 4 * u);
+            b4[u] = *reinterpret_cast<const f32x4 *>(Bb + (32 * wc + l31) * GLD + 16 * h + 4 * u);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[u][e], b4[u][e], acc, 0, 0, 0);
+        if (kc + 1 < nkh) {
+            ks_stage_store(As[half][1 - P], t, sa[1 - P]);
+            ks_stage_store(Bs[half][1 - P], t, sb[1 - P]);
+            if (kc + 3 < nkh) {
+                ks_stage_load<VEC4>(Q, q0, nq, d, kbase + (kc + 3) * GBK, t, sa[1 - P]);
+                ks_stage_load<VEC4>(X, x0, N, d, kbase + (kc + 3) * GBK, t, sb[1 - P]);
+            }
+        }
+        __syncthreads();
+    };
+    for (int kc = 0; kc < nkh; kc += 2) {
+        step(kc, std::integral_constant<int, 0>{});
+        if (kc + 1 < nkh) step(kc + 1, std::integral_constant<int, 1>{});
+    }
+    // half 1 → LDS (the tile buffers are free: every read finished before the last barrier) → half 0 adds
+    float *xch = &As[0][0][0];
+    if (half == 1) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) xch[(r * 4 + (wave & 3)) * 64 + lane] = acc[r];
+    }
+    __syncthreads();
+    if (half == 1) return;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] += xch[(r * 4 + wave) * 64 + lane];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int64_t q = q0 + 32 * wr + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int64_t x = x0 + 32 * wc + l31;
+        if (q < nq && x < N) {
+            const float ip = acc[r];
+            float key;
+            if (metric == kL2) {
+                key = fmaf(-2.f, ip, qnorm[q] + xnorm[x]);
+                key = key < 0.f ? 0.f : key;
+            } else {
+                key = -ip;
+            }
+            keys_out[q * ldk + x] = key;
+        }
+    }
+}
+
 // flat_keys_direct — the same 64 × 64 tiles, MFMAs and k order as flat_keys_small (bit-identical keys), but every
 // wave loads its own A / B fragments straight from memory into a 3-chunk register ring: no LDS staging, no
 // per-chunk barrier.  The inputs are small and cache-resident (the coarse quantizer's queries and centroids),
@@ -1600,10 +1725,15 @@ void launch_flat_gemm_keys(const float *Q, const float *qn, int64_t nq, const fl
         const int sq = (int)ceil_div(nq, SBM);
         const int64_t blocks = (int64_t)sq * ceil_div(N, SBM);
         dim3 g((unsigned)blocks), b(256);
-        // HIPANN_KEYS = 0 (default): LDS-staged (flat_keys_small, 29.7 µs for 1024 × 1024 × 768); 3 / 6: the
+        // HIPANN_KEYS = 2 (default; even chunk counts): flat_keys_ksplit; 0 (and odd counts): LDS-staged
+        // (flat_keys_small, 29.7 µs for 1024 × 1024 × 768); 3 / 6: the
         // register-ring flat_keys_direct with that many chunks in flight (A/B: 34.0 / 35.7 µs)
-        static const int mode = [] { const char *e = std::getenv("HIPANN_KEYS"); return e ? std::atoi(e) : 0; }();
-        if (mode == 3) {
+        static const int mode = [] { const char *e = std::getenv("HIPANN_KEYS"); return e ? std::atoi(e) : 2; }();
+        const int nk = (d + GBK - 1) / GBK;
+        if (mode == 2 && nk % 2 == 0) {  // default: the K-split tiles (8 waves, two per SIMD)
+            if (vec4) hipLaunchKernelGGL(flat_keys_ksplit<true>, g, dim3(512), 0, st, Q, qn, nq, X, xn, N, d, metric, sq, keys, ldk);
+            else hipLaunchKernelGGL(flat_keys_ksplit<false>, g, dim3(512), 0, st, Q, qn, nq, X, xn, N, d, metric, sq, keys, ldk);
+        } else if (mode == 3) {
             if (vec4) hipLaunchKernelGGL((flat_keys_direct<true, 3>), g, b, 0, st, Q, qn, nq, X, xn, N, d, metric, sq, keys, ldk);
             else hipLaunchKernelGGL((flat_keys_direct<false, 3>), g, b, 0, st, Q, qn, nq, X, xn, N, d, metric, sq, keys, ldk);
         } else if (mode == 6) {

@@ -1036,27 +1036,59 @@ __global__ void __launch_bounds__(256) ivf_half_residual(const float *__restrict
 __global__ void __launch_bounds__(256) ivf_split_queries_h(const float *__restrict__ Q, int64_t nq, int d, int nsup,
                                                            int es, uint4 *__restrict__ out, float *__restrict__ its,
                                                            float *__restrict__ qres, float *__restrict__ qn, int vec4) {
+    // vec4 rows of ≤ 1024 dims: one load round trip for the row (≤ 4 float4 per lane), staged in LDS for the
+    // split's k-slot order; ‖q‖² and the max come from the same registers (‖q‖² in row_norms_f32's order)
+    __shared__ __attribute__((aligned(16))) float srow[4][1024];
     const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (q >= nq) return;
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const float *src = Q + q * (int64_t)d;
-    if (qn) {
-        float s = 0.f;
-        if (vec4) {
-            const float4 *p4 = reinterpret_cast<const float4 *>(src);
-            for (int j = lane; j < (d >> 2); j += 64) {
-                const float4 v = p4[j];
-                s = fmaf(v.x, v.x, s); s = fmaf(v.y, v.y, s); s = fmaf(v.z, v.z, s); s = fmaf(v.w, v.w, s);
-            }
-        } else {
-            for (int j = lane; j < d; j += 64) s = fmaf(src[j], src[j], s);
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-        if (lane == 0) qn[q] = s;
-    }
     unsigned mb = 0;
-    for (int e = lane; e < d; e += 64) mb = max(mb, __float_as_uint(src[e]) & 0x7fffffffu);
+    if (vec4 && d <= 1024) {
+        const float4 *p4 = reinterpret_cast<const float4 *>(src);
+        const int n4 = d >> 2;
+        float4 r4[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int j = lane + 64 * i;
+            r4[i] = j < n4 ? p4[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float4 v = r4[i];
+            if (lane + 64 * i < n4) {
+                s = fmaf(v.x, v.x, s); s = fmaf(v.y, v.y, s); s = fmaf(v.z, v.z, s); s = fmaf(v.w, v.w, s);
+                reinterpret_cast<float4 *>(srow[wv])[lane + 64 * i] = v;
+            }
+            mb = max(mb, max(max(__float_as_uint(v.x) & 0x7fffffffu, __float_as_uint(v.y) & 0x7fffffffu),
+                             max(__float_as_uint(v.z) & 0x7fffffffu, __float_as_uint(v.w) & 0x7fffffffu)));
+        }
+        if (qn) {
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+            if (lane == 0) qn[q] = s;
+        }
+        __builtin_amdgcn_wave_barrier();
+        src = srow[wv];
+    } else {
+        if (qn) {
+            float s = 0.f;
+            if (vec4) {
+                const float4 *p4 = reinterpret_cast<const float4 *>(src);
+                for (int j = lane; j < (d >> 2); j += 64) {
+                    const float4 v = p4[j];
+                    s = fmaf(v.x, v.x, s); s = fmaf(v.y, v.y, s); s = fmaf(v.z, v.z, s); s = fmaf(v.w, v.w, s);
+                }
+            } else {
+                for (int j = lane; j < d; j += 64) s = fmaf(src[j], src[j], s);
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+            if (lane == 0) qn[q] = s;
+        }
+        for (int e = lane; e < d; e += 64) mb = max(mb, __float_as_uint(src[e]) & 0x7fffffffu);
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) mb = max(mb, (unsigned)__shfl_xor((int)mb, o));
     int eq = 0;
@@ -1388,7 +1420,7 @@ void launch_ivf_scan_mfma_h(const float *Q, int64_t nq, void *qsplit, float *its
     uint4 *qs = static_cast<uint4 *>(qsplit);
     if (!split_done)
         hipLaunchKernelGGL(ivf_split_queries_h, dim3((unsigned)ceil_div(nq, 4)), dim3(256), 0, st, Q, nq, d, nsup, es, qs,
-                           its, qres, nullptr, 0);
+                           its, qres, nullptr, (d % 4 == 0) && ((uintptr_t)Q % 16 == 0));
     const int group = mh_group(d);
     const size_t merge = (size_t)(MF_WAVES / 2) * MF_QTMAX * 4 * 64 * sizeof(float2);
     const size_t smem = std::max((size_t)group * mh_stride(d) * 4, merge);
