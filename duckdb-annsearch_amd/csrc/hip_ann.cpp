@@ -320,6 +320,10 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
     if (exact) k = metric == kIP || form == kFlatBf16Exact ? kFlatRerankKIP : kRerankK;
     int64_t nsplit;
     bool flags_ready = false;  // the bounded passes' select already reset nflag and flagged overflows
+    // the bounded passes' candidate buffers and bound, for the flagged queries' second rerank
+    const float *cr_d = nullptr, *cr_bound = nullptr;
+    const int *cr_i = nullptr, *cr_n = nullptr;
+    int cr_nsplit = 0, cr_cap = 0;
     // the exact forms' max ‖x‖² (cached; its first computation uses sh.nflag as scratch, so before any flags)
     const float xmax2 = exact ? flat_xmax2(sh, d, st) : 0.f;
     if (form == kFlatBf16Exact) {
@@ -435,6 +439,12 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
                              (long long)nsplit, (long long)tps, (long long)tps_a, (double)tot / (double)ncell, mx,
                              (double)hb[0]);
             }
+            cr_d = cd;
+            cr_i = ci;
+            cr_n = cn;
+            cr_nsplit = (int)nsplit;
+            cr_cap = cap;
+            cr_bound = bound;
             nsplit = 1;
             flags_ready = true;
         } else {
@@ -490,17 +500,41 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
     HIPANN_CHECK(hipMemcpyAsync(&nf, sh.nflag.p, sizeof(int), hipMemcpyDeviceToHost, st));
     HIPANN_CHECK(hipStreamSynchronize(st));
     if (nf <= 0) return;
+    int *fl = sh.flagged.get<int>();
+    if (cr_d) {
+        // bounded passes: rerank each flagged query over all its buffered candidates, certified against the pass
+        // bound (launch_flat_cand_rerank); only what that cannot certify re-runs on SPLIT3
+        const int P = flat_cand_rerank_parts(cr_nsplit);
+        sh.crd.ensure(sizeof(float) * (size_t)nf * P * kout, sh.device);
+        sh.cri.ensure(sizeof(long long) * (size_t)nf * P * kout, sh.device);
+        sh.covf.ensure(sizeof(int) * (size_t)nf * P, sh.device);
+        sh.nflag2.ensure(sizeof(int), sh.device);
+        sh.flagged2.ensure(sizeof(int) * (size_t)nf, sh.device);
+        HIPANN_CHECK(hipMemsetAsync(sh.nflag2.p, 0, sizeof(int), st));
+        {
+            ScopedTiming t(ix.timer_merge, st);
+            launch_flat_cand_rerank(fl, nf, cr_d, cr_i, cr_n, cr_nsplit, cr_cap, cr_bound, xq, sh.xb, d, sh.n,
+                                    sh.label_offset, xmax2, sh.bf16_rxmax, metric, kout, sh.crd.get<float>(),
+                                    sh.cri.get<long long>(), sh.covf.get<int>(), D, I, sh.nflag2.get<int>(),
+                                    sh.flagged2.get<int>(), st);
+        }
+        ix.cand_reranked += nf;
+        HIPANN_CHECK(hipMemcpyAsync(&nf, sh.nflag2.p, sizeof(int), hipMemcpyDeviceToHost, st));
+        HIPANN_CHECK(hipStreamSynchronize(st));
+        if (nf <= 0) return;
+        fl = sh.flagged2.get<int>();
+    }
     ix.rerank_fallbacks += nf;
     sh.fq.ensure(sizeof(float) * (size_t)nf * d, sh.device);
     sh.fD.ensure(sizeof(float) * (size_t)nf * kout, sh.device);
     sh.fI.ensure(sizeof(int64_t) * (size_t)nf * kout, sh.device);
-    launch_ivf_gather_queries(xq, sh.flagged.get<int>(), nf, d, sh.fq.get<float>(), st);
+    launch_ivf_gather_queries(xq, fl, nf, d, sh.fq.get<float>(), st);
     {
         TimerPause p0(ix.timer_main), p1(ix.timer_merge);
         flat_shard_search(ix, sh, nf, sh.fq.get<float>(), k_user, kout, sh.fD.get<float>(), sh.fI.get<int64_t>(), st,
                           kFlatSplit3);
     }
-    launch_ivf_scatter_results(sh.fD.get<float>(), sh.fI.get<int64_t>(), sh.flagged.get<int>(), nf, kout, D, I, st);
+    launch_ivf_scatter_results(sh.fD.get<float>(), sh.fI.get<int64_t>(), fl, nf, kout, D, I, st);
 }
 
 }  // namespace hipann

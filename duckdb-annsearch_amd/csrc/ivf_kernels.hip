@@ -1815,6 +1815,151 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Flat form 4, second stage for the flagged queries (flat_cand_rerank_part / _final).  The bounded passes
+// buffered EVERY row whose scan key is ≤ the pass bound T = bound[q] (pass A under T₀ ≥ T, pass B under T),
+// so a row outside the buffers has scan key > T and exact distance > T − E.  Recomputing all of a flagged
+// query's buffered rows in the direct form (≈ 26 per split at 10M rows) and ordering them by (distance,
+// label) gives its exact top-kout whenever the kout-th distance is < T − E: T is the 32nd best key of pass
+// A's ≈ 1/20 of the rows, far looser than the 32nd best key overall that the first rerank had to clear
+// (flat_cand_select).  A query with an overflowed cell, or that fails this check too, goes to flagged2
+// (the SPLIT3 re-run).  part: grid (nf, P) blocks, wave w of block p takes splits p·spb + w, + 4, …; each
+// wave keeps a (distance, label) list of kout, the block merges its 4 lists; final: one wave per query.
+// ---------------------------------------------------------------------------------------------
+constexpr int kCandRerankParts = 16;
+template <bool IP>
+__global__ void __launch_bounds__(256)
+flat_cand_rerank_part(const int *__restrict__ flagged, const float *__restrict__ cand_d, const int *__restrict__ cand_i,
+                      const int *__restrict__ cand_n, int nsplit, int cap, const float *__restrict__ Q,
+                      const float *__restrict__ X, int d, int64_t nrows, int64_t label_offset, int kout,
+                      float *__restrict__ part_d, long long *__restrict__ part_i, int *__restrict__ ovf) {
+    __shared__ float sd[4][64];
+    __shared__ long long si[4][64];
+    const int f = blockIdx.x, p = blockIdx.y, P = gridDim.y;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t q = flagged[f];
+    const float *qp = Q + q * (int64_t)d;
+    const int spb = (nsplit + P - 1) / P;
+    const int s_begin = p * spb, s_end = nsplit < s_begin + spb ? nsplit : s_begin + spb;
+    WaveList<1, long long> L;
+    L.init();
+    bool over = false;
+    for (int s = s_begin + wv; s < s_end; s += 4) {
+        const int64_t cell = q * nsplit + s;
+        const int nr = cand_n[cell];
+        over |= nr > cap;
+        const int n = nr < cap ? nr : cap;
+        for (int r0 = 0; r0 < n; r0 += 4) {
+            const float *xr[4];
+            int row[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int j = r0 + u < n ? r0 + u : n - 1;
+                const int rw = cand_i[cell * cap + j];
+                row[u] = r0 + u < n && rw >= 0 && rw < nrows ? rw : -1;
+                xr[u] = X + (int64_t)(row[u] >= 0 ? row[u] : 0) * d;
+            }
+            float acc[4] = {0.f, 0.f, 0.f, 0.f};
+            rerank_rows4<IP>(qp, xr, d, lane, acc);
+            float mine = __builtin_inff();
+            long long lab = IdTraits<long long>::pad();
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                float a = acc[u];
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+                if (lane == u && row[u] >= 0) { mine = IP ? -a : a; lab = label_offset + row[u]; }
+            }
+            L.offer(mine, lab, kout - 1);
+        }
+    }
+    sd[wv][lane] = L.d[0];
+    si[wv][lane] = L.id[0];
+    const bool bover = __syncthreads_or(over);
+    if (wv != 0) return;
+#pragma unroll
+    for (int w = 1; w < 4; ++w) L.offer(lane < kout ? sd[w][lane] : __builtin_inff(),
+                                        lane < kout ? si[w][lane] : IdTraits<long long>::pad(), kout - 1);
+    if (lane < kout) {
+        part_d[((int64_t)f * P + p) * kout + lane] = L.d[0];
+        part_i[((int64_t)f * P + p) * kout + lane] = L.id[0];
+    }
+    if (lane == 0) ovf[f * P + p] = bover ? 1 : 0;
+}
+
+template <bool IP>
+__global__ void __launch_bounds__(64)
+flat_cand_rerank_final(const int *__restrict__ flagged, int P, const float *__restrict__ bound,
+                       const float *__restrict__ Q, int d, float xmax2, float rxmax, int kout,
+                       const float *__restrict__ part_d, const long long *__restrict__ part_i,
+                       const int *__restrict__ ovf, float *__restrict__ D, int64_t *__restrict__ I,
+                       int *__restrict__ nflag2, int *__restrict__ flagged2) {
+    const int f = blockIdx.x, lane = threadIdx.x;
+    const int64_t q = flagged[f];
+    bool over = false;
+    for (int p = 0; p < P; ++p) over |= ovf[f * P + p] != 0;
+    WaveList<1, long long> L;
+    L.init();
+    for (int p = 0; p < P; ++p)
+        L.offer(lane < kout ? part_d[((int64_t)f * P + p) * kout + lane] : __builtin_inff(),
+                lane < kout ? part_i[((int64_t)f * P + p) * kout + lane] : IdTraits<long long>::pad(), kout - 1);
+    // the bound of the first rerank (ivf_rerank_topk, rxmax >= 0 branch) from this query's own norms
+    const float *qp = Q + q * (int64_t)d;
+    float qq = 0.f, rq2 = 0.f;
+    for (int e = lane; e < d; e += 64) {
+        qq = fmaf(qp[e], qp[e], qq);
+        const float r = qp[e] - (float)(__bf16)qp[e];
+        rq2 = fmaf(r, r, rq2);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        qq += __shfl_xor(qq, o);
+        rq2 += __shfl_xor(rq2, o);
+    }
+    const float qn = sqrtf(qq), rq = sqrtf(rq2), xh = sqrtf(xmax2) + rxmax;
+    const float g = (float)d * 0x1p-24f;
+    const float eip = qn * rxmax + rq * xh + g * (qn + rq) * xh;
+    const float T = bound[q];
+    // + 2^-20 of the key scale: the pass compared s against ‖q‖² − T (IP: −2T) in fp32
+    const float E = 1.01f * ((IP ? 1.f : 2.f) * eip + (float)(d + 8) * 0x1p-24f * 2.f * (qq + xmax2)) +
+                    0x1p-20f * (qq + xmax2 + fabsf(T));
+    const float dk = readlane_f(L.d[0], kout - 1);
+    const bool ok = !over && E <= 3.4e38f && dk < __builtin_inff() && (T == __builtin_inff() || dk < T - E);
+    if (!ok) {
+        if (lane == 0) flagged2[atomicAdd(nflag2, 1)] = (int)q;
+        return;
+    }
+    if (lane < kout) {
+        D[q * kout + lane] = IP ? -L.d[0] : L.d[0];
+        I[q * kout + lane] = (int64_t)L.id[0];
+    }
+}
+
+void launch_flat_cand_rerank(const int *flagged, int nf, const float *cand_d, const int *cand_i, const int *cand_n,
+                             int nsplit, int cap, const float *bound, const float *Q, const float *X, int d,
+                             int64_t nrows, int64_t label_offset, float xmax2, float rxmax, int metric, int kout,
+                             float *part_d, long long *part_i, int *ovf, float *D, int64_t *I, int *nflag2,
+                             int *flagged2, hipStream_t st) {
+    if (nf <= 0) return;
+    HIPANN_REQUIRE(kout >= 1 && kout <= 64 && nsplit >= 1 && cap >= 1, "flat cand rerank: bad arguments");
+    const int P = std::min(kCandRerankParts, nsplit);
+    dim3 g1((unsigned)nf, (unsigned)P);
+    if (metric == kIP) {
+        hipLaunchKernelGGL(flat_cand_rerank_part<true>, g1, dim3(256), 0, st, flagged, cand_d, cand_i, cand_n, nsplit,
+                           cap, Q, X, d, nrows, label_offset, kout, part_d, part_i, ovf);
+        hipLaunchKernelGGL(flat_cand_rerank_final<true>, dim3((unsigned)nf), dim3(64), 0, st, flagged, P, bound, Q, d,
+                           xmax2, rxmax, kout, part_d, part_i, ovf, D, I, nflag2, flagged2);
+    } else {
+        hipLaunchKernelGGL(flat_cand_rerank_part<false>, g1, dim3(256), 0, st, flagged, cand_d, cand_i, cand_n, nsplit,
+                           cap, Q, X, d, nrows, label_offset, kout, part_d, part_i, ovf);
+        hipLaunchKernelGGL(flat_cand_rerank_final<false>, dim3((unsigned)nf), dim3(64), 0, st, flagged, P, bound, Q, d,
+                           xmax2, rxmax, kout, part_d, part_i, ovf, D, I, nflag2, flagged2);
+    }
+    HIPANN_CHECK(hipGetLastError());
+}
+
+int flat_cand_rerank_parts(int nsplit) { return std::min(kCandRerankParts, nsplit); }
+
 // max over rows of ‖x‖² (non-negative floats order as their bit patterns)
 __global__ void __launch_bounds__(256) ivf_max_norm(const float *__restrict__ xn, int64_t n, unsigned *__restrict__ out) {
     float m = 0.f;

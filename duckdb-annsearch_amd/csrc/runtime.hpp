@@ -189,6 +189,7 @@ struct FlatShard {
     // flagged queries of the last batch and the re-run's buffers
     float xmax2 = -1.f;
     DevBuf nflag, flagged, fq, fD, fI, tmpnorm;
+    DevBuf crd, cri, covf, nflag2, flagged2;  // form 4: flagged queries reranked over all their buffered candidates
     // kFlatBf16Exact: tiled bf16 image of the rows (built at the first search after an add) and the
     // batch's query image
     DevBuf xb16, qimg, seed;
@@ -214,6 +215,7 @@ struct FlatIndex : IndexBase {
     std::vector<std::unique_ptr<FlatShard>> shards;
     int form = kFlatBf16Exact;  // BLAS-path q·x form (FlatForm)
     int64_t rerank_fallbacks = 0;  // queries re-run on the 3-term path by the exact form's bound check
+    int64_t cand_reranked = 0;     // form 4: flagged queries sent to the all-candidate rerank first
     HostBuf h_q, h_d, h_i;
     DevBuf gather_d, gather_i, merged_d, merged_i;  // multi-device merge on shards[0]'s device
     FlatIndex() : IndexBase(Kind::Flat) {}
@@ -335,6 +337,15 @@ int64_t ivf_max_items(int64_t nq, int nprobe, int nlist, int max_nch, int64_t nr
 int ivf_mfma_bf_group(int d, int np);
 bool ivf_mfma_bf_supported(const float *Q, int d, const float *codes, int k, int np);
 int64_t ivf_mfma_bf_qsplit_bytes(int64_t nq, int d, int np);
+// Form 4 (bounded passes): the flagged queries' exact top-kout over ALL their buffered candidates, certified
+// against the pass bound (every unbuffered row has scan key > bound[q]); queries it cannot certify (a cell
+// overflowed, or the k-th distance within the error bound of bound[q]) are appended to flagged2.
+void launch_flat_cand_rerank(const int *flagged, int nf, const float *cand_d, const int *cand_i, const int *cand_n,
+                             int nsplit, int cap, const float *bound, const float *Q, const float *X, int d,
+                             int64_t nrows, int64_t label_offset, float xmax2, float rxmax, int metric, int kout,
+                             float *part_d, long long *part_i, int *ovf, float *D, int64_t *I, int *nflag2,
+                             int *flagged2, hipStream_t st);
+int flat_cand_rerank_parts(int nsplit);
 void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int nprobe, int64_t nq, int k, int kout,
                        int metric, const float *Q, const float *codes, int d, const int64_t *ids, int64_t nrows,
                        int64_t label_offset, float xmax2, float *D, int64_t *I, int *nflag, int *flagged,

@@ -101,8 +101,10 @@ int hipann_flat_reconstruct_n(void *index, int64_t i0, int64_t n, float *out, ch
 #define HIPANN_FLAT_FORM_BF16_EXACT 4
 int hipann_flat_set_form(void *index, int form);
 int hipann_flat_get_form(void *index);
-/* Queries the exact forms' bound check flagged since the index was created (each re-run on
- * HIPANN_FLAT_FORM_SPLIT3; the exact results replace the flagged ones). */
+/* Queries re-run on HIPANN_FLAT_FORM_SPLIT3 since the index was created: those the exact forms' bound
+ * check flagged and, for BF16_EXACT's bounded passes, the second rerank (every buffered candidate of
+ * the query, certified against the pass bound) could not certify either; the exact results replace
+ * the flagged ones. */
 int64_t hipann_flat_rerank_fallbacks(void *index);
 
 /* ---------------------------------------------------------------------------------------------

@@ -326,6 +326,29 @@ def test_flat_bf16_two_pass_resume(gpu, oracle, metric):
     check_topk_parity(xb, xq[:48], D1[:48], I1[:48], Do, Io, metric)
 
 
+@pytest.mark.parametrize("metric", [0, 1])
+def test_flat_bf16_flagged_queries_candidate_rerank(gpu, oracle, metric):
+    """Bounded passes with near-duplicate rows (16K base rows x 40 copies + 1e-4 noise, shuffled; 640K x 64,
+    nq 256): every query's 32 best scan keys are copies of one base row, so the first rerank cannot certify
+    it and flags it.  The second rerank recomputes all of a flagged query's buffered candidates and
+    certifies against the pass bound (the 32nd best key of pass A's rows, several base rows away); only
+    what it cannot certify re-runs on SPLIT3.  Ids follow the oracle's parity rule on every query.
+    Reference edge case: duplicate vectors (test/sql/edge_cases.test:75-83)."""
+    rng = np.random.default_rng(23 + metric)
+    base = rng.standard_normal((16_000, 64), dtype=np.float32)
+    xb = np.repeat(base, 40, axis=0)
+    xb += 1e-4 * rng.standard_normal(xb.shape, dtype=np.float32)
+    xb = xb[rng.permutation(len(xb))]
+    xq = rng.standard_normal((256, 64), dtype=np.float32)
+    ix = gpu.HipIndexFlat(64, metric, xb)
+    assert ix.form == ix.FORM_BF16_EXACT
+    D, I = ix.search(xq, 10)
+    Do, Io = oracle.flat_search(xb, xq, 10, metric)
+    check_topk_parity(xb, xq, D, I, Do, Io, metric)
+    # the first rerank flags nearly all of these queries; the candidate rerank certifies most of them
+    assert ix.rerank_fallbacks() < len(xq) // 4, ix.rerank_fallbacks()
+
+
 @pytest.mark.parametrize("n", [200, 1000, 3000])
 @pytest.mark.parametrize("metric", [0, 1])
 @pytest.mark.parametrize("k", [1, 7, 32, 64])

@@ -20,10 +20,11 @@ timeout -k 10 900 python -u bench.py > gpurun_out/bench_default.json 2> gpurun_o
 exit 0
 fi
 bash tools/gpu_profile.sh ivf ivf_scan_mfma_h ivf_10000000x768 --no-alt-forms --no-c5 --steps 10 || exit 1
-PER_STEP=2 bash tools/gpu_profile.sh flat flat_bf16_topk flat_10000000x768 --no-alt-forms --steps 5 || exit 1
-PER_STEP=2 bash tools/gpu_profile.sh flat flat_bf16_topk flat_1000000x768 --no-alt-forms --n 1000000 --steps 10 || exit 1
+# Flat form 4: the seed keys pass + passes A and B of flat_bf16_k64 per step (PER_STEP=3: their sum)
+PER_STEP=3 bash tools/gpu_profile.sh flat flat_bf16_k64 flat_10000000x768 --no-alt-forms --no-c5 --steps 5 || exit 1
+PER_STEP=3 bash tools/gpu_profile.sh flat flat_bf16_k64 flat_1000000x768 --no-alt-forms --no-c5 --n 1000000 --steps 10 || exit 1
 bash tools/gpu_profile.sh diskann diskann_bfs diskann_1000000x1536 --steps 10 || exit 1
-PER_STEP=2 bash tools/gpu_profile.sh flat flat_bf16_topk flat_12500000x768_ip --no-alt-forms --n 12500000 --metric ip --steps 5 || exit 1
+PER_STEP=3 bash tools/gpu_profile.sh flat flat_bf16_k64 flat_12500000x768_ip --no-alt-forms --no-c5 --n 12500000 --metric ip --steps 5 || exit 1
 for key in ivf_10000000x768 flat_10000000x768 flat_1000000x768 diskann_1000000x1536 flat_12500000x768_ip; do
     echo "== $key"; cat gpurun_out/pmc_$key.json
 done
