@@ -511,16 +511,26 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
         sh.nflag2.ensure(sizeof(int), sh.device);
         sh.flagged2.ensure(sizeof(int) * (size_t)nf, sh.device);
         HIPANN_CHECK(hipMemsetAsync(sh.nflag2.p, 0, sizeof(int), st));
+        static const bool dbg = std::getenv("HIPANN_FLAT_CAND_DEBUG") != nullptr;
+        if (dbg) sh.tmpnorm.ensure(sizeof(float) * 4 * (size_t)nf, sh.device);
         {
             ScopedTiming t(ix.timer_merge, st);
             launch_flat_cand_rerank(fl, nf, cr_d, cr_i, cr_n, cr_nsplit, cr_cap, cr_bound, xq, sh.xb, d, sh.n,
                                     sh.label_offset, xmax2, sh.bf16_rxmax, metric, kout, sh.crd.get<float>(),
                                     sh.cri.get<long long>(), sh.covf.get<int>(), D, I, sh.nflag2.get<int>(),
-                                    sh.flagged2.get<int>(), st);
+                                    sh.flagged2.get<int>(), st, dbg ? sh.tmpnorm.get<float>() : nullptr);
         }
         ix.cand_reranked += nf;
+        const int nf1 = nf;
         HIPANN_CHECK(hipMemcpyAsync(&nf, sh.nflag2.p, sizeof(int), hipMemcpyDeviceToHost, st));
         HIPANN_CHECK(hipStreamSynchronize(st));
+        if (dbg) {
+            std::vector<float> h((size_t)nf1 * 4);
+            HIPANN_CHECK(hipMemcpy(h.data(), sh.tmpnorm.p, h.size() * sizeof(float), hipMemcpyDeviceToHost));
+            std::fprintf(stderr, "hipann flat flagged %d -> %d after the candidate rerank\n", nf1, nf);
+            for (int j = 0; j < nf1 && j < 8; ++j)
+                std::fprintf(stderr, "  overflow %g  dk %g  T %g  E %g\n", h[4 * j], h[4 * j + 1], h[4 * j + 2], h[4 * j + 3]);
+        }
         if (nf <= 0) return;
         fl = sh.flagged2.get<int>();
     }

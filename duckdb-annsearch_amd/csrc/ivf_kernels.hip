@@ -1893,7 +1893,7 @@ flat_cand_rerank_final(const int *__restrict__ flagged, int P, const float *__re
                        const float *__restrict__ Q, int d, float xmax2, float rxmax, int kout,
                        const float *__restrict__ part_d, const long long *__restrict__ part_i,
                        const int *__restrict__ ovf, float *__restrict__ D, int64_t *__restrict__ I,
-                       int *__restrict__ nflag2, int *__restrict__ flagged2) {
+                       int *__restrict__ nflag2, int *__restrict__ flagged2, float *__restrict__ dbg) {
     const int f = blockIdx.x, lane = threadIdx.x;
     const int64_t q = flagged[f];
     bool over = false;
@@ -1925,6 +1925,12 @@ flat_cand_rerank_final(const int *__restrict__ flagged, int P, const float *__re
                     0x1p-20f * (qq + xmax2 + fabsf(T));
     const float dk = readlane_f(L.d[0], kout - 1);
     const bool ok = !over && E <= 3.4e38f && dk < __builtin_inff() && (T == __builtin_inff() || dk < T - E);
+    if (dbg && lane == 0) {  // HIPANN_FLAT_CAND_DEBUG: (overflow, k-th distance, pass bound, E) per flagged query
+        dbg[4 * f + 0] = over ? 1.f : 0.f;
+        dbg[4 * f + 1] = dk;
+        dbg[4 * f + 2] = T;
+        dbg[4 * f + 3] = E;
+    }
     if (!ok) {
         if (lane == 0) flagged2[atomicAdd(nflag2, 1)] = (int)q;
         return;
@@ -1939,7 +1945,7 @@ void launch_flat_cand_rerank(const int *flagged, int nf, const float *cand_d, co
                              int nsplit, int cap, const float *bound, const float *Q, const float *X, int d,
                              int64_t nrows, int64_t label_offset, float xmax2, float rxmax, int metric, int kout,
                              float *part_d, long long *part_i, int *ovf, float *D, int64_t *I, int *nflag2,
-                             int *flagged2, hipStream_t st) {
+                             int *flagged2, hipStream_t st, float *dbg) {
     if (nf <= 0) return;
     HIPANN_REQUIRE(kout >= 1 && kout <= 64 && nsplit >= 1 && cap >= 1, "flat cand rerank: bad arguments");
     const int P = std::min(kCandRerankParts, nsplit);
@@ -1948,12 +1954,12 @@ void launch_flat_cand_rerank(const int *flagged, int nf, const float *cand_d, co
         hipLaunchKernelGGL(flat_cand_rerank_part<true>, g1, dim3(256), 0, st, flagged, cand_d, cand_i, cand_n, nsplit,
                            cap, Q, X, d, nrows, label_offset, kout, part_d, part_i, ovf);
         hipLaunchKernelGGL(flat_cand_rerank_final<true>, dim3((unsigned)nf), dim3(64), 0, st, flagged, P, bound, Q, d,
-                           xmax2, rxmax, kout, part_d, part_i, ovf, D, I, nflag2, flagged2);
+                           xmax2, rxmax, kout, part_d, part_i, ovf, D, I, nflag2, flagged2, dbg);
     } else {
         hipLaunchKernelGGL(flat_cand_rerank_part<false>, g1, dim3(256), 0, st, flagged, cand_d, cand_i, cand_n, nsplit,
                            cap, Q, X, d, nrows, label_offset, kout, part_d, part_i, ovf);
         hipLaunchKernelGGL(flat_cand_rerank_final<false>, dim3((unsigned)nf), dim3(64), 0, st, flagged, P, bound, Q, d,
-                           xmax2, rxmax, kout, part_d, part_i, ovf, D, I, nflag2, flagged2);
+                           xmax2, rxmax, kout, part_d, part_i, ovf, D, I, nflag2, flagged2, dbg);
     }
     HIPANN_CHECK(hipGetLastError());
 }

@@ -344,7 +344,7 @@ void launch_flat_cand_rerank(const int *flagged, int nf, const float *cand_d, co
                              int nsplit, int cap, const float *bound, const float *Q, const float *X, int d,
                              int64_t nrows, int64_t label_offset, float xmax2, float rxmax, int metric, int kout,
                              float *part_d, long long *part_i, int *ovf, float *D, int64_t *I, int *nflag2,
-                             int *flagged2, hipStream_t st);
+                             int *flagged2, hipStream_t st, float *dbg = nullptr);
 int flat_cand_rerank_parts(int nsplit);
 void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int nprobe, int64_t nq, int k, int kout,
                        int metric, const float *Q, const float *codes, int d, const int64_t *ids, int64_t nrows,
