@@ -375,7 +375,8 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
             return e ? (int64_t)std::atoll(e) : (int64_t)20;
         }();
         const int64_t tps_a = pass_div > 1 ? tps / pass_div : 0;
-        // per-(query, split) candidate capacity: ≈26 expected at 10M rows with two passes (tail ≈45); one pass
+        // per-(query, split) candidate capacity (128): ≈26 expected at 10M rows with two passes (tail ≈45; 67 seen at
+        // 12.5M IP, which overflowed the former 64 and re-ran two queries per batch on SPLIT3); one pass
         // under the seed alone: 32·N/16K/nsplit (≈300 at 10M) — a larger cap
         const int cap = (int)flat_bf16_k64_cap() * (tps_a >= 1 ? 1 : 8);
         const size_t ncell = (size_t)nq * nsplit;
