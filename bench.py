@@ -116,6 +116,9 @@ def compact_config(name, c):
         out["ids_eq_oracle_bfs"] = c["ids_equal_to_oracle_bfs"]
     if c.get("vs_k10") is not None:
         out["vs_k10"] = c["vs_k10"]
+    if isinstance(c.get("path"), dict):
+        p = c["path"]
+        out["path"] = f"form{p.get('form')} kf{p.get('filter_k')}" + (f" sub{p['sublists']}" if p.get("sublists") else "")
     if isinstance(c.get("latency"), dict):
         out["nq1_ms"] = _rnd((c["latency"].get("nq1") or {}).get("ms_per_call"))
     if "gpu_ids_equal_to_cpu_path" in c:  # C1
@@ -364,6 +367,33 @@ def recall_at(got, gt, k):
     return float(np.mean([len(set(got[i][:k]) & set(gt[i][:k])) / k for i in range(len(gt))]))
 
 
+def request_k_line(torch, index, xq, k_user, n_deleted, base_ms, steps=5):
+    """The extension's request_k = min(k + |tombstones|, ntotal) (src/faiss_index.cpp:713-715) on the same index and
+    batch: k = 10 with 20 deleted rows asks the GPU for 30.  Times `steps` device searches at request_k and reports
+    the step against the k = 10 step (within 1.3x), and the path that ran (hipann_last_search_path)."""
+    rk = k_user + n_deleted
+    nq = xq.shape[0]
+    stream = torch.cuda.current_stream().cuda_stream
+    D = torch.empty((nq, rk), device=xq.device, dtype=torch.float32)
+    I = torch.empty((nq, rk), device=xq.device, dtype=torch.int64)
+    call = lambda: index.search_device(nq, xq.data_ptr(), rk, D.data_ptr(), I.data_ptr(), stream)  # noqa: E731
+    call()
+    torch.cuda.synchronize()
+    index.set_kernel_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        call()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    kms = index.kernel_ms(0)
+    index.set_kernel_timing(False)
+    ms = el * 1e3 / steps
+    return {"workload": f"request_k = {k_user} + {n_deleted} tombstones = {rk} (faiss_index.cpp:713-715)", "k": k_user,
+            "request_k": rk, "value": round(nq / (ms * 1e-3), 1), "ms_per_step": round(ms, 3),
+            "roofline": {"kernel_ms": round(kms, 3)}, "vs_k10": round(ms / base_ms, 3) if base_ms > 0 else None,
+            "path": index.last_search_path()}
+
+
 def pmc_traffic(key: str, kernel: str):
     """HBM bytes per launch of `kernel` for workload `key` (e.g. "ivf_10000000x768") from the newest
     committed FETCH_SIZE pass (profiles/rNN/pmc_<key>.json, written by tools/pmc_traffic.py from a
@@ -408,7 +438,7 @@ FLAT_FORMS = {4: ("flat_bf16_k64", 1, BF16_MFMA_PEAK_TF,
 
 
 def flat_config(args, torch, dist, hipann, rank, world, dev, n, d, nq, k, metric, steps, warmup, alt_forms=True,
-                cpu_seconds=0.0, oracle_queries=0, latency=False, host_rate=True):
+                cpu_seconds=0.0, oracle_queries=0, latency=False, host_rate=True, request_k=False):
     from sharded import ShardedSearch, merge_packed_device_torch, shard_bounds
 
     lo, hi = shard_bounds(n, rank, world)
@@ -476,6 +506,8 @@ def flat_config(args, torch, dist, hipann, rank, world, dev, n, d, nq, k, metric
                             "fp32 rounding of the two forms. The bf16 scan is a certified filter, not the result.")
     if world > 1:
         return out, index, xb
+    if request_k:
+        out["request_k30"] = request_k_line(torch, index, xq, k, 20, el * 1e3 / steps)
     if host_rate:
         out["with_h2d_d2h"] = host_pointer_rate(torch, lambda q: sharded.search(q), xq, nq, k, max(3, steps // 2))
     # exactness: ids against the fp32 form (exact fp32 products, pinned by the C2 parity tests) on the whole
@@ -710,6 +742,8 @@ def ivf_config(args, torch, dist, hipann, rank, world, dev, steps, warmup, suite
     if world > 1:
         return out, index
     out["with_h2d_d2h"] = host_pointer_rate(torch, lambda q: sharded.search(q), xq, nq, k, max(5, steps // 2))
+    if suite_extras:
+        out["request_k30"] = request_k_line(torch, index, xq, k, 20, el * 1e3 / steps)
     if not args.no_alt_forms:
         alt = {}
         for f in (5, 3, 0):
@@ -1148,16 +1182,19 @@ def run_suite(args, torch, dist, hipann, dev):
         cfg[name]["wall_s"] = round(time.perf_counter() - t0, 1)
         torch.cuda.empty_cache()
 
-    def flat(n, metric=0, oracle_queries=0, latency=False, steps=10):
+    def flat(n, metric=0, oracle_queries=0, latency=False, steps=10, request_k=False):
         out, index, xb = flat_config(args, torch, dist, hipann, 0, 1, dev, n, 768, 1024, args.k, metric, steps, 2,
-                                     cpu_seconds=5.0, oracle_queries=oracle_queries, latency=latency)
+                                     cpu_seconds=5.0, oracle_queries=oracle_queries, latency=latency,
+                                     request_k=request_k)
         index.close()
         del index, xb
         return out
 
     guarded("C1_flat_10k_128_cpu_path", lambda: c1_config(torch, hipann, dev))
     guarded("C2_flat_l2_1m_768", lambda: flat(1_000_000, oracle_queries=32))
-    guarded("flat_l2_10m_768", lambda: flat(10_000_000, oracle_queries=20, latency=True, steps=5))
+    guarded("flat_l2_10m_768", lambda: flat(10_000_000, oracle_queries=20, latency=True, steps=5, request_k=True))
+    if "request_k30" in cfg["flat_l2_10m_768"]:
+        cfg["flat_l2_10m_768_request_k30"] = cfg["flat_l2_10m_768"].pop("request_k30")
     guarded("C4_diskann_1m_1536_sq8", lambda: diskann_config(args, torch, dist, hipann, 0, 1, dev, 1_000_000, 1536,
                                                              1024, args.k, 128, 64, 10, 2))
     # C4 through the path hip_ffi.rs's fallback takes when the graph is not registered: DiskProvider::search_batch's
@@ -1336,8 +1373,11 @@ def main():
             index.close()
             del index
             torch.cuda.empty_cache()
+        rk_line = line.pop("request_k30", None)
         if args.suite and world == 1:
             line["configs"] = run_suite(args, torch, dist, hipann, dev)
+        if rk_line is not None:
+            line.setdefault("configs", {})["C3_ivf_request_k30"] = rk_line
         if not args.no_c5 and args.workload == "ivf":
             t0 = time.perf_counter()
             try:

@@ -58,6 +58,9 @@ enum IvfForm : int {
     kFormHalfExact = 6
 };
 constexpr int kRerankK = 16, kRerankMaxK = 12;
+// request_k in (kRerankMaxK, kIvfSubMaxK] on the IVF exact forms: sub-list slots (one 16-list per scan wave) and a
+// rerank filter of min(64, max(kout + 4, 2·kout)) candidates (ivf.cpp); above: the 3-term scan
+constexpr int kIvfSubMaxK = 60;
 // Flat exact form, IP: 32 candidates per (split, query).  At 10M × 768 (U(-1,1) rows) 16 left ≈0.2% of
 // the IP queries failing the bound (each a re-scan of the shard: 61 → 67 ms per batch), 32 none (65 ms);
 // L2 had no failures at 16, and 32 costs it 60 → 66 ms (the fuller epilogue lists), so L2 keeps 16.

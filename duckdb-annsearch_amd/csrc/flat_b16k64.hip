@@ -451,7 +451,6 @@ void launch_flat_keys_kth(const float *keys, int S, int64_t nq, int k, float *bo
 
 bool flat_bf16_k64_supported(int nk, int k) { return nk % 2 == 0 && k <= 64; }
 
-size_t flat_bf16_k64_cap() { return 128; }  // mean ≈ 29 per cell at 12.5M rows (IP), max 67 seen at 64: overflows re-ran on SPLIT3
 
 void launch_flat_bf16_k64(const void *qimg, const float *qn, int64_t nq, const void *ximg, const float *xn, int64_t N,
                           int nk, int metric, int nqt, int nsplit, int64_t tiles_per_split, int64_t tile_begin,

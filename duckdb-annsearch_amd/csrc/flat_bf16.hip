@@ -372,6 +372,13 @@ __global__ void __launch_bounds__(256) flat_bf16_seed(const float *__restrict__ 
 constexpr int kB16StagesDefault = 4;  // 10M x 768: 19.16 (3) / 18.68 (4) / 19.06 (5) ms
 int flat_bf16_waves(int64_t nq) { return nq >= 256 ? 8 : nq >= 128 ? 4 : 2; }
 int flat_bf16_tile_rows() { return B16_TN; }
+// the largest list length k (≤ 64) of flat_bf16_topk's LDS lists at this batch size (its launcher's LDS check)
+int flat_bf16_topk_kmax(int64_t nq) {
+    const int QM = 32 * flat_bf16_waves(nq);
+    int k = 64;
+    while (k > 1 && (size_t)3 * (QM * 4 + B16_TN * 4) * 16 + (size_t)QM * k * 8 > 160 * 1024) --k;
+    return k;
+}
 
 size_t flat_bf16_img_bytes(int64_t n, int d, int R) {
     return (size_t)ceil_div(std::max<int64_t>(n, 1), R) * b16_nk(d) * R * 4 * 16;

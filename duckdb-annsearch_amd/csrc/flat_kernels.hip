@@ -594,6 +594,12 @@ struct FbProducts<2> {
 };
 
 size_t gemm_bf_smem_bytes(int np, int k, int w) { return (size_t)2 * np * FB_STAGE16 * 16 + (size_t)32 * w * k * 8; }
+// the largest list length k (≤ 64) whose LDS lists fit either block shape
+int flat_gemm_topk_bf_kmax(int np) {
+    int k = 64;
+    while (k > 1 && gemm_bf_smem_bytes(np, k, 8) > 160 * 1024) --k;
+    return k;
+}
 
 template <bool VEC4, bool L2M, int NP, int W>
 __global__ void __launch_bounds__(64 * W, 8 / W)

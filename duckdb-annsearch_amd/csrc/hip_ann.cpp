@@ -312,12 +312,35 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
         sh.qn_nq = nq;
     }
     int form = form_override >= 0 ? form_override : ix.form;
-    const bool exact = (form == kFlatSplit2Exact || form == kFlatBf16Exact) && kout <= kRerankMaxK;
-    if ((form == kFlatSplit2Exact || form == kFlatBf16Exact) && !exact) form = kFlatSplit3;
+    static const bool seed_env = [] { const char *e = std::getenv("HIPANN_FLAT_BF16_SEED"); return !e || std::atoi(e); }();
+    // The exact forms keep kf candidates per query (per split and query on the list kernels) as the filter; the
+    // rerank returns kout.  kout ≤ kRerankMaxK: kf = 32 (the bf16 image: at 10M × 768 the 10th and 16th distances
+    // are ≈2 apart, inside its rounding bound ≈1.3, the 10th and 32nd ≈5; the split scan: IP 32, L2 16).  Larger
+    // kout (request_k = k + |tombstones|, faiss_index.cpp:713-715): kf = min(64, max(base, 2·kout)).  The list
+    // kernels hold kf in LDS (capped by their launchers' LDS budget) and need kf ≥ kout + 4 of margin; the bounded
+    // passes take any kout ≤ kf ≤ 64 — a query whose kout-th distance is within the bound of the kf-th key goes to
+    // the all-candidate rerank, certified against the pass bound.  Otherwise: the 3-term split (fp32-level).
+    int kf = 0;
+    bool bounded = false;
+    if (form == kFlatSplit2Exact || form == kFlatBf16Exact) {
+        const int base = metric == kIP || form == kFlatBf16Exact ? kFlatRerankKIP : kRerankK;
+        kf = kout <= kRerankMaxK ? base : std::min(64, std::max(base, 2 * kout));
+        if (form == kFlatBf16Exact) {
+            bounded = flat_bf16_resumable(nq, d, kf) && seed_env && sh.n >= 8 * 65536;
+            if (!bounded) kf = std::min(kf, flat_bf16_topk_kmax(nq));
+        } else {
+            kf = std::min(kf, flat_gemm_topk_bf_kmax(2));
+        }
+    }
+    const bool exact = kf > 0 && (kout <= kRerankMaxK || (bounded ? kout <= kf : kout + 4 <= kf));
+    if (kf > 0 && !exact) form = kFlatSplit3;
     const int k_user = k;
-    // kept per (split, query); the rerank returns kout.  The bf16 filter keeps 32: at 10M × 768 the 10th and
-    // 16th distances are ≈2 apart, inside its rounding bound (≈1.3), the 10th and 32nd ≈5
-    if (exact) k = metric == kIP || form == kFlatBf16Exact ? kFlatRerankKIP : kRerankK;
+    if (exact) k = kf;
+    if (form_override < 0) {
+        ix.last_form = form;
+        ix.last_kfilt = exact ? kf : 0;
+        ix.last_sublists = 0;
+    }
     int64_t nsplit;
     bool flags_ready = false;  // the bounded passes' select already reset nflag and flagged overflows
     // the bounded passes' candidate buffers and bound, for the flagged queries' second rerank
@@ -367,29 +390,41 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
         // tile per block) and their k-th order statistic (flat_keys_kth); otherwise the 32-dim list kernel over
         // 64K rows and flat_bf16_seed (its lists start empty: every row an insert, ≈1 ms at 1024 queries — what
         // the keys mode replaces).  The main passes then admit only keys ≤ that bound.
-        static const bool seed_env = [] { const char *e = std::getenv("HIPANN_FLAT_BF16_SEED"); return !e || std::atoi(e); }();
-        const bool bounded = flat_bf16_resumable(nq, d, k);
         const bool seeded = seed_env && sh.n >= 8 * 65536;
         static const int64_t pass_div = [] {
             const char *e = std::getenv("HIPANN_FLAT_PASS_A");  // A/B: 1/x of each split in pass A; 0 = one pass
             return e ? (int64_t)std::atoll(e) : (int64_t)20;
         }();
         const int64_t tps_a = pass_div > 1 ? tps / pass_div : 0;
-        // per-(query, split) candidate capacity (128): ≈26 expected at 10M rows with two passes (tail ≈45; 67 seen at
-        // 12.5M IP, which overflowed the former 64 and re-ran two queries per batch on SPLIT3); one pass
-        // under the seed alone: 32·N/16K/nsplit (≈300 at 10M) — a larger cap
-        const int cap = (int)flat_bf16_k64_cap() * (tps_a >= 1 ? 1 : 8);
-        const size_t ncell = (size_t)nq * nsplit;
         const int64_t sample = std::min<int64_t>(16384, flat_keys_kth_max());
+        // per-(query, split) candidate capacity from the expected fill: pass A admits ≈ k·rows_A/S per cell (keys ≤
+        // the k-th of S sample rows), pass B ≈ k·rows_B/(nsplit·rows_A) (the k-th over pass A's rows); 3× + 32 of
+        // headroom (clustered 12.5M IP rows peaked at 2.3× the mean), a multiple of 32.  At 10M rows, 1024 queries,
+        // k 32: ≈25 expected → 128; larger batches (fewer, longer splits) and larger k scale it.
+        const double rows_split = (double)tps * flat_bf16_tile_rows();
+        const double rows_a = (double)tps_a * flat_bf16_tile_rows();
+        const double fill = tps_a >= 1 ? k * rows_a / (double)sample + k * (rows_split - rows_a) / (rows_a * (double)nsplit)
+                                       : k * rows_split / (double)sample;
+        const int cap = (int)std::min<double>(1 << 20, (double)ceil_div((int64_t)(3.0 * fill + 32.0), 32) * 32);
+        const size_t ncell = (size_t)nq * nsplit;
+        // the keys-mode seed pass runs per chunk of 1024 queries (4 query tiles) through one 64 MB slab of keys
+        const int64_t seed_qc = 1024;
         ScopedTiming t(ix.timer_main, st);
         if (seeded && bounded) {
             sh.seed.ensure(sizeof(float) * (size_t)nq, sh.device);
-            sh.cand.ensure(std::max(ncell * ((size_t)cap * 8 + 4), (size_t)nq * sample * sizeof(float)), sh.device);
+            sh.cand.ensure(std::max(ncell * ((size_t)cap * 8 + 4), (size_t)std::min(nq, seed_qc) * sample * sizeof(float)),
+                           sh.device);
             launch_b16_tile_rows(xq, nq, d, 32 * W, sh.qimg.p, st);
-            launch_flat_bf16_k64(sh.qimg.p, qn, nq, sh.xb16.p, sh.xn.get<float>(), sample, (int)ceil_div(d, 32), metric,
-                                 (int)nqt, (int)(sample / flat_bf16_tile_rows()), 1, 0, 1, nullptr, sh.cand.get<float>(),
-                                 nullptr, nullptr, 0, false, true, st);
-            launch_flat_keys_kth(sh.cand.get<float>(), (int)sample, nq, k, sh.seed.get<float>(), st);
+            const size_t qtile_bytes = flat_bf16_img_bytes(32 * W, d, 32 * W);
+            for (int64_t c0 = 0; c0 < nq; c0 += seed_qc) {
+                const int64_t cn = std::min(seed_qc, nq - c0);
+                launch_flat_bf16_k64(static_cast<const char *>(sh.qimg.p) + (size_t)(c0 / (32 * W)) * qtile_bytes,
+                                     qn ? qn + c0 : nullptr, cn, sh.xb16.p, sh.xn.get<float>(), sample,
+                                     (int)ceil_div(d, 32), metric, (int)ceil_div(cn, 32 * W),
+                                     (int)(sample / flat_bf16_tile_rows()), 1, 0, 1, nullptr, sh.cand.get<float>(), nullptr,
+                                     nullptr, 0, false, true, st);
+                launch_flat_keys_kth(sh.cand.get<float>(), (int)sample, cn, k, sh.seed.get<float>() + c0, st);
+            }
         } else if (seeded) {
             const int64_t seed_rows = 65536;
             const int64_t stiles = seed_rows / flat_bf16_tile_rows();
@@ -860,6 +895,16 @@ int64_t hipann_flat_rerank_fallbacks(void *h) {
     auto *ix = static_cast<IndexBase *>(h);
     if (ix->kind != Kind::Flat) return -1;
     return static_cast<FlatIndex *>(ix)->rerank_fallbacks;
+}
+
+int hipann_last_search_path(void *h, int *form, int *filter_k, int *sublists) {
+    if (!h) return -1;
+    auto *ix = static_cast<IndexBase *>(h);
+    std::lock_guard<std::mutex> lk(ix->mu);
+    if (form) *form = ix->last_form;
+    if (filter_k) *filter_k = ix->last_kfilt;
+    if (sublists) *sublists = ix->last_sublists;
+    return 0;
 }
 
 int hipann_flat_get_form(void *h) {

@@ -250,16 +250,23 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     // the decomposed forms need float4 rows (else the direct kernel, also on the GPU); the MFMA kernel
     // keeps 16-lane lists (k <= 16) and the item's queries in LDS (else the VALU decomposed kernel)
     int req = form_override >= 0 ? form_override : ix.form;
+    // request_k above kRerankMaxK on the exact forms (k + |tombstones|, faiss_index.cpp:713-715): the scans keep
+    // their 16-lane lists but write every wave's list as a sub-list of the slot (mf_finish_item), and the rerank
+    // takes the kf best candidates, certified against its kf-th merged key AND the smallest full sub-list's
+    // 16th key (every pruned row lies above both).  Beyond kIvfSubMaxK: the 3-term scan.
+    const bool sub_req = (req == kFormHalfExact || req == kFormSplit2Exact) && kout > kRerankMaxK &&
+                         kout <= kIvfSubMaxK && !bigk;
     // kFormHalfExact: the fp16-image scan as the filter of the same rerank (else kFormSplit2Exact)
     bool half = false;
     if (req == kFormHalfExact) {
-        half = kout <= kRerankMaxK && !bigk && ivf_mfma_h_supported(d, kRerankK) && ensure_half_codes(sh, d, nlist, st);
+        half = (kout <= kRerankMaxK || sub_req) && !bigk && ivf_mfma_h_supported(d, kRerankK) &&
+               ensure_half_codes(sh, d, nlist, st);
         req = kFormSplit2Exact;
     }
-    // kFormSplit2Exact: the 2-term scan keeps kRerankK per list, the rerank makes the results exact
-    // (k > kRerankMaxK leaves too little margin: the 3-term scan instead)
+    // kFormSplit2Exact: the 2-term scan keeps kRerankK per list (per wave with sub-lists), the rerank makes the
+    // results exact
     const bool want_exact = req == kFormSplit2Exact;
-    if (want_exact) req = kout <= kRerankMaxK ? kFormSplit2 : kFormSplit3;
+    if (want_exact) req = kout <= kRerankMaxK || sub_req ? kFormSplit2 : kFormSplit3;
     const int k_user = k;
     const int kscan = want_exact && req == kFormSplit2 ? kRerankK : k;
     int form = req != kFormDirect && !bigk && ivf_dot_supported(xq, d, sh.codes) ? req : kFormDirect;
@@ -268,7 +275,16 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
         form = kFormDecomposed;
     if (form == kFormDecomposed && !ivf_mfma_supported(xq, d, sh.codes, kscan)) form = kFormDecomposedValu;
     const bool exact = want_exact && form == kFormSplit2;
+    const bool sub = exact && sub_req;
     k = kscan;  // per-list k of the scan (the output keeps kout)
+    // entries per (query, probe, chunk) slot, and the rerank's filter depth
+    const int kslot = sub ? ivf_scan_sublists() * k : k;
+    const int kfilt = sub ? std::min(64, std::max(kout + 4, 2 * kout)) : k;
+    if (form_override < 0) {
+        ix.last_form = exact ? (half ? kFormHalfExact : kFormSplit2Exact) : form;
+        ix.last_kfilt = exact ? kfilt : 0;
+        ix.last_sublists = sub ? ivf_scan_sublists() : 0;
+    }
     const bool tiled = form == kFormDecomposed || ivf_form_split(form);  // the matrix-core scans
     const int group = half ? ivf_mfma_h_group(d) : ivf_group_size(form, d);
     float xmax2 = 0.f;
@@ -327,7 +343,7 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     sh.plan_batch++;
     ccnt_reset.armed = false;
     // 3. scan: one k-list per (query, probe, row chunk) slot — every slot is written by exactly one item
-    const size_t parts = (size_t)np * nq * sh.max_nch * k;
+    const size_t parts = (size_t)np * nq * sh.max_nch * kslot;
     HIPANN_REQUIRE((int64_t)np * nq * sh.max_nch < (int64_t)0x7fffffff, "too many partial lists");
     sh.part_d.ensure(parts * sizeof(float), sh.device);
     sh.part_i.ensure(parts * sizeof(int), sh.device);
@@ -356,7 +372,8 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
                                    metric, sh.codes_h.p, sh.tpass_off.get<int64_t>(), sh.xnorm.get<float>(),
                                    sh.list_off.get<int64_t>(), sh.cnt.get<int>(), sh.bucket_off.get<int>(),
                                    sh.item_off.get<int>(), sh.bucket.get<int>(), sh.slot_off.get<int>(), nlist, np, k,
-                                   max_items, qbound, sh.part_d.get<float>(), sh.part_i.get<int>(), st, true);
+                                   max_items, qbound, sh.part_d.get<float>(), sh.part_i.get<int>(), st, true,
+                                   sub ? 1 : 0);
         else if (bigk)
             launch_ivf_scan_bigk(xq, d, metric, sh.codes, sh.list_off.get<int64_t>(), sh.coarse_i.get<int64_t>(),
                                  nq * np, np, sh.slot_off.get<int>(), nq * np * std::max(sh.max_nch, 1), k,
@@ -366,7 +383,7 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
                                     sh.tpass_off.get<int64_t>(), sh.xnorm.get<float>(), sh.list_off.get<int64_t>(),
                                     sh.cnt.get<int>(), sh.bucket_off.get<int>(), sh.item_off.get<int>(),
                                     sh.bucket.get<int>(), sh.slot_off.get<int>(), nlist, np, k, max_items, qbound,
-                                    sh.part_d.get<float>(), sh.part_i.get<int>(), st);
+                                    sh.part_d.get<float>(), sh.part_i.get<int>(), st, sub ? 1 : 0);
         else if (form == kFormDecomposed)
             launch_ivf_scan_mfma(xq, qn, d, metric, sh.codes_t.get<float>(), sh.tpass_off.get<int64_t>(),
                                  sh.xnorm.get<float>(), sh.list_off.get<int64_t>(), sh.cnt.get<int>(),
@@ -388,11 +405,12 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     }
     {
         ScopedTiming t(ix.timer_merge, st);
-        launch_ivf_rerank(sh.part_d.get<float>(), sh.part_i.get<int>(), sh.slot_off.get<int>(), np, nq, k, kout, metric,
-                          xq, sh.codes, d, sh.ids, sh.n, 0, xmax2, D, I, sh.nflag.get<int>(), sh.flagged.get<int>(), st,
-                          kSplit2Eps, half ? sh.half_rxmax : -1.f, half ? sh.hres.get<float>() : nullptr,
-                          sh.coarse_i.get<int64_t>(), sh.list_off.get<int64_t>(), nlist, qbound,
-                          half && metric == kL2 ? qn : nullptr);
+        launch_ivf_rerank(sh.part_d.get<float>(), sh.part_i.get<int>(), sh.slot_off.get<int>(), np, nq, kfilt, kout,
+                          metric, xq, sh.codes, d, sh.ids, sh.n, 0, xmax2, D, I, sh.nflag.get<int>(),
+                          sh.flagged.get<int>(), st, kSplit2Eps, half ? sh.half_rxmax : -1.f,
+                          half ? sh.hres.get<float>() : nullptr, sh.coarse_i.get<int64_t>(),
+                          sh.list_off.get<int64_t>(), nlist, qbound, half && metric == kL2 ? qn : nullptr, kslot,
+                          sub ? 1 : 0);
     }
     if (!host_fallback()) {
         // flagged queries re-run on the device in the direct form (ivf_fallback_query, one block per flagged

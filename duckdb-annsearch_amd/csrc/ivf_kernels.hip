@@ -1630,19 +1630,31 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
                 int *__restrict__ nflag, int *__restrict__ flagged, float eps, float rxmax,
                 const float *__restrict__ qres, const int64_t *__restrict__ probes,
                 const int64_t *__restrict__ list_off, int nlist, const unsigned *__restrict__ qbound,
-                const float *__restrict__ qnorm) {
+                const float *__restrict__ qnorm, int kslot, int sub) {
     const int64_t q = WV == 1 ? (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6) : (int64_t)blockIdx.x;
     if (q >= nq) return;
     const int lane = threadIdx.x & 63;
     const int wv = WV == 1 ? 0 : (int)(threadIdx.x >> 6);
-    // 1. the kRerankK best (scan key, row) of the query's partial lists
+    // 1. the k best (scan key, row) of the query's partial lists (kslot entries per slot)
     WaveList<1, int> L;
     L.init();
     // slot_off == nullptr: the query's lists are the nprobe consecutive slots [q·nprobe, (q+1)·nprobe)
     // (the Flat exact form: one list per database split, query-major)
     const int64_t s0 = slot_off ? slot_off[q * nprobe] : q * nprobe;
     const int64_t s1 = slot_off ? slot_off[(q + 1) * nprobe] : (q + 1) * nprobe;
-    const int64_t total = (s1 - s0) * k;
+    const int64_t total = (s1 - s0) * kslot;
+    pd += s0 * kslot;
+    pi += s0 * kslot;
+    // sub-list slots (the IVF scans at request_k > 12, mf_finish_item): T_sub = qbound[q], the smallest k-th key
+    // over the query's full sub-lists — every row a sub-list or the running bound pruned has scan key ≥ T_sub.
+    // Candidates with key ≥ T_sub never matter when the check below passes (their exact distance is ≥ T_sub − E
+    // > the kout-th), so they are not offered.
+    float tsub = __builtin_inff();
+    if (sub && qbound) {
+        const unsigned b = qbound[q];
+        const float t = __uint_as_float((b & 0x80000000u) ? (b & 0x7fffffffu) : ~b);
+        tsub = t == t ? t : __builtin_inff();
+    }
     // WV > 1 and ≤ 64·WV·RS_J candidates (block-uniform): the block's bitwise select (rerank_block_select)
     // instead of per-wave lists and serial inserts
     constexpr int RS_J = 16;
@@ -1654,12 +1666,12 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
 #pragma unroll
         for (int u = 0; u < MU; ++u) {
             const int64_t c = cb + (int64_t)u * 64 * WV + lane;
-            vv[u] = c < total ? pd[s0 * k + c] : __builtin_inff();
-            rr[u] = c < total ? pi[s0 * k + c] : -1;
+            vv[u] = c < total ? pd[c] : __builtin_inff();
+            rr[u] = c < total ? pi[c] : -1;
         }
 #pragma unroll
         for (int u = 0; u < MU; ++u) {
-            const bool ok = rr[u] >= 0 && rr[u] < nrows && !(vv[u] == __builtin_inff());
+            const bool ok = rr[u] >= 0 && rr[u] < nrows && !(vv[u] == __builtin_inff()) && vv[u] < tsub;
             L.offer(ok ? vv[u] : __builtin_inff(), ok ? rr[u] : IdTraits<int>::pad(), k - 1);
         }
     }
@@ -1674,9 +1686,10 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
         if (bsel) {
             // the scan's final bound (order-preserving bits of a full slot list's k-th key, atomicMin'ed): >= the
             // k-th smallest key of the query's candidates
-            const unsigned qb = qbound ? qbound[q] : 0xffffffffu;
-            const float bound = (qb & 0x80000000u) ? __uint_as_float(qb & 0x7fffffffu) : __builtin_inff();
-            rerank_block_select<WV, RS_J>(pd + s0 * k, pi + s0 * k, total, k, nrows, sd, si, scnt, L, bound);
+            // (sub-lists: T_sub — the candidates above it are irrelevant, see above)
+            const unsigned qb = qbound && !sub ? qbound[q] : 0xffffffffu;
+            const float bound = sub ? tsub : (qb & 0x80000000u) ? __uint_as_float(qb & 0x7fffffffu) : __builtin_inff();
+            rerank_block_select<WV, RS_J>(pd, pi, total, k, nrows, sd, si, scnt, L, bound);
             if (wv == 0) srow[lane] = lane < k ? L.id[0] : IdTraits<int>::pad();
         } else {
             sd[wv * 64 + lane] = lane < k ? L.d[0] : __builtin_inff();
@@ -1804,8 +1817,10 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
     } else {
         E = eps * (qq + xmax2);
     }
-    // a non-finite bound (a query outside the fp16 form's safe scale range) is always re-run
-    const bool flag = !(E <= 3.4e38f) || (ncand == k && !(dk < k16 - E));
+    // a non-finite bound (a query outside the fp16 form's safe scale range) is always re-run; sub-lists: the
+    // kout-th distance must also clear the smallest full sub-list's k-th key
+    const bool flag = !(E <= 3.4e38f) || (ncand == k && !(dk < k16 - E)) ||
+                      (sub && tsub < __builtin_inff() && !(dk < tsub - E));
     if (flag && lane == 0) flagged[atomicAdd(nflag, 1)] = (int)q;
     const float pad_d = IP ? -__builtin_inff() : __builtin_inff();
     if (lane < kout) {
@@ -2039,14 +2054,18 @@ void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int 
                        int metric, const float *Q, const float *codes, int d, const int64_t *ids, int64_t nrows,
                        int64_t label_offset, float xmax2, float *D, int64_t *I, int *nflag, int *flagged,
                        hipStream_t st, float eps, float rxmax, const float *qres, const int64_t *probes,
-                       const int64_t *list_off, int nlist, const unsigned *qbound, const float *qnorm) {
+                       const int64_t *list_off, int nlist, const unsigned *qbound, const float *qnorm, int kslot,
+                       int sub) {
     if (nq <= 0) return;
-    HIPANN_REQUIRE(k >= kRerankK && k <= 64 && kout >= 1 && kout <= kRerankMaxK, "ivf rerank: k / kout out of range");
+    if (kslot <= 0) kslot = k;
+    // the filter depth k bounds kout (kout = k leaves no margin: those queries are flagged and re-run exactly)
+    HIPANN_REQUIRE(k >= kRerankK && k <= 64 && kout >= 1 && kout <= k && kslot >= 1 && (!sub || qbound),
+                   "ivf rerank: k / kout out of range");
     // small batches: one 4-wave block per query (fills more of the chip, shorter per-query chain)
     const bool wide = nq < HIPANN_RR_WIDE;
     dim3 grid((unsigned)(wide ? nq : ceil_div(nq, 4))), block(256);
 #define RR_ARGS pd, pi, slot_off, nprobe, nq, k, kout, Q, codes, d, ids, nrows, label_offset, xmax2, D, I, nflag, flagged, \
-                eps, rxmax, qres, probes, list_off, nlist, qbound, qnorm
+                eps, rxmax, qres, probes, list_off, nlist, qbound, qnorm, kslot, sub
     if (metric == kIP) {
         if (wide) hipLaunchKernelGGL((ivf_rerank_topk<true, 4>), grid, block, 0, st, RR_ARGS);
         else hipLaunchKernelGGL((ivf_rerank_topk<true, 1>), grid, block, 0, st, RR_ARGS);

@@ -158,6 +158,67 @@ __device__ __forceinline__ uint64_t row_kth(uint64_t l, int kth, int g) {
     return ((uint64_t)sh << 32) | sl;
 }
 
+// ---- end of an item: the waves' lists → the slot's partial list ------------------------------------
+// sub = 0: the 8 waves' lists are merged pairwise through LDS (3 rounds) and wave 0 writes the slot's k-list.
+// sub = 1 (the exact forms at request_k > 12, ivf.cpp): no merge — every wave writes its own k-list as
+// sub-list `wave` of the slot (MF_WAVES·k entries per slot).  A full sub-list's k-th key still tightens the
+// query's running bound, so at the end qbound[q] is the smallest k-th key over the query's full sub-lists:
+// every row some sub-list (or the bound) pruned has a scan key ≥ it, which is what ivf_rerank_topk certifies
+// against besides its own k-th merged key.
+template <int QT>
+__device__ __forceinline__ void mf_finish_item(uint64_t (&lst)[QT][4], float *smem, int nqi,
+                                               const int *__restrict__ bucket, int boff, int nprobe,
+                                               const int *__restrict__ slot_off, int chunk, int k, int sub,
+                                               unsigned *__restrict__ qbound, float *__restrict__ part_d,
+                                               int *__restrict__ part_i) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int m = lane & 15, g = lane >> 4;
+    if (!sub) {  // block-uniform
+        // the query image is dead once every wave has left its main loop (first barrier)
+        uint64_t *scratch = reinterpret_cast<uint64_t *>(smem);
+#pragma unroll 1
+        for (int half = MF_WAVES / 2; half > 0; half >>= 1) {
+            __syncthreads();
+            if (wave >= half && wave < 2 * half) {
+                uint64_t *dst = scratch + (size_t)(wave - half) * QT * 4 * 64;
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) dst[(qt * 4 + v) * 64 + lane] = lst[qt][v];
+            }
+            __syncthreads();
+            if (wave < half) {
+                const uint64_t *src = scratch + (size_t)wave * QT * 4 * 64;
+#pragma unroll
+                for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) row_merge16(lst[qt][v], src[(qt * 4 + v) * 64 + lane], m);
+            }
+        }
+    }
+    if ((sub || wave == 0) && m < k) {
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const int q = qt * 16 + 4 * g + v;
+                if (q < nqi) {
+                    const int pr = bucket[boff + q];
+                    const int64_t slot = (int64_t)slot_off[pr] + chunk;
+                    const int64_t off = (sub ? slot * MF_WAVES + wave : slot) * k + m;
+                    const uint64_t e = lst[qt][v];
+                    const unsigned id = (unsigned)e;
+                    const bool real = e != MF_EMPTY && id != MF_PAD_ID;
+                    part_d[off] = real ? mf_unsortable((unsigned)(e >> 32)) : __builtin_inff();
+                    part_i[off] = real ? (int)id : (int)MF_PAD_ID;
+                    // a real k-th tightens the query's bound for the items that start later
+                    if (m == k - 1 && real) atomicMin(qbound + pr / nprobe, (unsigned)(e >> 32));
+                }
+            }
+    }
+}
+
 // ---- one wave's share of an item -----------------------------------------------------------------
 template <int QT, bool IP>
 __device__ __forceinline__ void mf_item(int d, const float *__restrict__ codes_t, int64_t tp0,
@@ -165,7 +226,7 @@ __device__ __forceinline__ void mf_item(int d, const float *__restrict__ codes_t
                                         int64_t r0, int64_t r1, int nqi, const float *__restrict__ qs, int stride,
                                         const float (&qn)[QT][4], const unsigned (&qb)[QT][4],
                                         const int *__restrict__ bucket, int boff, int nprobe,
-                                        const int *__restrict__ slot_off, int chunk, int k, float *smem,
+                                        const int *__restrict__ slot_off, int chunk, int k, int sub, float *smem,
                                         unsigned *__restrict__ qbound, float *__restrict__ part_d,
                                         int *__restrict__ part_i) {
     const int lane = threadIdx.x & 63;
@@ -319,48 +380,7 @@ __device__ __forceinline__ void mf_item(int d, const float *__restrict__ codes_t
 
     if (HIPANN_MF_EXPERIMENT == 1 && sink == 1) part_d[0] = 0.f;
 
-    // ---- merge the 8 waves' lists: rounds of (upper half writes → barrier → lower half merges) ----
-    // the query image is dead once every wave has left its main loop (first barrier)
-    uint64_t *scratch = reinterpret_cast<uint64_t *>(smem);
-#pragma unroll 1
-    for (int half = MF_WAVES / 2; half > 0; half >>= 1) {
-        __syncthreads();
-        if (wave >= half && wave < 2 * half) {
-            uint64_t *dst = scratch + (size_t)(wave - half) * QT * 4 * 64;
-#pragma unroll
-            for (int qt = 0; qt < QT; ++qt)
-#pragma unroll
-                for (int v = 0; v < 4; ++v)
-                    dst[(qt * 4 + v) * 64 + lane] = lst[qt][v];
-        }
-        __syncthreads();
-        if (wave < half) {
-            const uint64_t *src = scratch + (size_t)wave * QT * 4 * 64;
-#pragma unroll
-            for (int qt = 0; qt < QT; ++qt)
-#pragma unroll
-                for (int v = 0; v < 4; ++v) row_merge16(lst[qt][v], src[(qt * 4 + v) * 64 + lane], m);
-        }
-    }
-    if (wave == 0 && m < k) {
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt)
-#pragma unroll
-            for (int v = 0; v < 4; ++v) {
-                const int q = qt * 16 + 4 * g + v;
-                if (q < nqi) {
-                    const int pr = bucket[boff + q];
-                    const int64_t off = (int64_t)(slot_off[pr] + chunk) * k + m;
-                    const uint64_t e = lst[qt][v];
-                    const unsigned id = (unsigned)e;
-                    const bool real = e != MF_EMPTY && id != MF_PAD_ID;
-                    part_d[off] = real ? mf_unsortable((unsigned)(e >> 32)) : __builtin_inff();
-                    part_i[off] = real ? (int)id : (int)MF_PAD_ID;
-                    // a real k-th tightens the query's bound for the items that start later
-                    if (m == k - 1 && real) atomicMin(qbound + pr / nprobe, (unsigned)(e >> 32));
-                }
-            }
-    }
+    mf_finish_item<QT>(lst, smem, nqi, bucket, boff, nprobe, slot_off, chunk, k, sub, qbound, part_d, part_i);
 }
 
 template <bool IP>
@@ -369,7 +389,7 @@ ivf_scan_mfma(const float *__restrict__ Q, const float *__restrict__ qnorm, int 
               const int64_t *__restrict__ tpass_off,
               const float *__restrict__ xn, const int64_t *__restrict__ list_off, const int *__restrict__ cnt,
               const int *__restrict__ bucket_off, const int *__restrict__ item_off, const int *__restrict__ bucket,
-              const int *__restrict__ slot_off, int nlist, int nprobe, int group, int k,
+              const int *__restrict__ slot_off, int nlist, int nprobe, int group, int k, int sub,
               unsigned *__restrict__ qbound, float *__restrict__ part_d, int *__restrict__ part_i) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int total = item_off[nlist];
@@ -407,7 +427,7 @@ ivf_scan_mfma(const float *__restrict__ Q, const float *__restrict__ qnorm, int 
 
     const int lane = threadIdx.x & 63, g = lane >> 4;
     const int64_t tp0 = tpass_off[l] + (int64_t)chunk * (MF_CH / MF_PASS);
-#define MF_ARGS d, codes_t, tp0, xn, r0, r1, nqi, smem, stride, qn, qb, bucket, boff, nprobe, slot_off, chunk, k, smem, \
+#define MF_ARGS d, codes_t, tp0, xn, r0, r1, nqi, smem, stride, qn, qb, bucket, boff, nprobe, slot_off, chunk, k, sub, smem, \
                 qbound, part_d, part_i
 #define MF_QN(QTV)                                                                                          \
     float qn[QTV][4];                                                                                       \
@@ -481,7 +501,7 @@ void launch_ivf_scan_mfma(const float *Q, const float *qn, int d, int metric, co
                           const int64_t *tpass_off, const float *xn,
                           const int64_t *list_off, const int *cnt, const int *bucket_off, const int *item_off,
                           const int *bucket, const int *slot_off, int nlist, int nprobe, int k, int64_t max_items,
-                          unsigned *qbound, float *pd, int *pi, hipStream_t st) {
+                          unsigned *qbound, float *pd, int *pi, hipStream_t st, int sub) {
     if (max_items <= 0) return;
     HIPANN_REQUIRE(max_items < (int64_t)0x7fffffff, "too many IVF work items");
     HIPANN_REQUIRE(ivf_mfma_supported(Q, d, codes_t, k), "MFMA IVF scan needs d % 4 == 0, 16-B aligned data, k <= 16");
@@ -491,7 +511,7 @@ void launch_ivf_scan_mfma(const float *Q, const float *qn, int d, int metric, co
     const size_t smem = std::max((size_t)group * mf_stride(d) * 4, merge);
     dim3 grid((unsigned)max_items), block(MF_THREADS);
 #define MF_LAUNCH_ARGS Q, qn, d, codes_t, tpass_off, xn, list_off, cnt, bucket_off, item_off, bucket, slot_off, nlist, nprobe, group, k, \
-                       qbound, pd, pi
+                       sub, qbound, pd, pi
     if (metric == kIP) hipLaunchKernelGGL((ivf_scan_mfma<true>), grid, block, smem, st, MF_LAUNCH_ARGS);
     else hipLaunchKernelGGL((ivf_scan_mfma<false>), grid, block, smem, st, MF_LAUNCH_ARGS);
 #undef MF_LAUNCH_ARGS
@@ -597,7 +617,7 @@ __device__ __forceinline__ void mb_item(int d, const float *__restrict__ codes_t
                                         unsigned *__restrict__ qs, int stride, const uint4 *__restrict__ qsplit,
                                         const float (&qn)[QT][4],
                                         const unsigned (&qb)[QT][4], const int *__restrict__ bucket, int boff,
-                                        int nprobe, const int *__restrict__ slot_off, int chunk, int k, float *smem,
+                                        int nprobe, const int *__restrict__ slot_off, int chunk, int k, int sub, float *smem,
                                         unsigned *__restrict__ qbound, float *__restrict__ part_d,
                                         int *__restrict__ part_i) {
     const int lane = threadIdx.x & 63;
@@ -745,44 +765,7 @@ __device__ __forceinline__ void mb_item(int d, const float *__restrict__ codes_t
         for (int r = 0; r < MF_RT; ++r) xnr[r] = xnr_next[r];
     }
 
-    uint64_t *scratch = reinterpret_cast<uint64_t *>(smem);
-#pragma unroll 1
-    for (int half = MF_WAVES / 2; half > 0; half >>= 1) {
-        __syncthreads();
-        if (wave >= half && wave < 2 * half) {
-            uint64_t *dst = scratch + (size_t)(wave - half) * QT * 4 * 64;
-#pragma unroll
-            for (int qt = 0; qt < QT; ++qt)
-#pragma unroll
-                for (int v = 0; v < 4; ++v) dst[(qt * 4 + v) * 64 + lane] = lst[qt][v];
-        }
-        __syncthreads();
-        if (wave < half) {
-            const uint64_t *src = scratch + (size_t)wave * QT * 4 * 64;
-#pragma unroll
-            for (int qt = 0; qt < QT; ++qt)
-#pragma unroll
-                for (int v = 0; v < 4; ++v) row_merge16(lst[qt][v], src[(qt * 4 + v) * 64 + lane], m);
-        }
-    }
-    if (wave == 0 && m < k) {
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt)
-#pragma unroll
-            for (int v = 0; v < 4; ++v) {
-                const int q = qt * 16 + 4 * g + v;
-                if (q < nqi) {
-                    const int pr = bucket[boff + q];
-                    const int64_t off = (int64_t)(slot_off[pr] + chunk) * k + m;
-                    const uint64_t e = lst[qt][v];
-                    const unsigned id = (unsigned)e;
-                    const bool real = e != MF_EMPTY && id != MF_PAD_ID;
-                    part_d[off] = real ? mf_unsortable((unsigned)(e >> 32)) : __builtin_inff();
-                    part_i[off] = real ? (int)id : (int)MF_PAD_ID;
-                    if (m == k - 1 && real) atomicMin(qbound + pr / nprobe, (unsigned)(e >> 32));
-                }
-            }
-    }
+    mf_finish_item<QT>(lst, smem, nqi, bucket, boff, nprobe, slot_off, chunk, k, sub, qbound, part_d, part_i);
 }
 
 template <bool IP, int NP, int NH>
@@ -791,7 +774,7 @@ ivf_scan_mfma_bf(const uint4 *__restrict__ qsplit, const float *__restrict__ qno
                  const int64_t *__restrict__ tpass_off, const float *__restrict__ xn,
                  const int64_t *__restrict__ list_off, const int *__restrict__ cnt, const int *__restrict__ bucket_off,
                  const int *__restrict__ item_off, const int *__restrict__ bucket, const int *__restrict__ slot_off,
-                 int nlist, int nprobe, int group, int k, unsigned *__restrict__ qbound, float *__restrict__ part_d,
+                 int nlist, int nprobe, int group, int k, int sub, unsigned *__restrict__ qbound, float *__restrict__ part_d,
                  int *__restrict__ part_i) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int total = item_off[nlist];
@@ -823,7 +806,7 @@ ivf_scan_mfma_bf(const uint4 *__restrict__ qsplit, const float *__restrict__ qno
 
     const int lane = threadIdx.x & 63, g = lane >> 4;
     const int64_t tp0 = tpass_off[l] + (int64_t)chunk * (MF_CH / MF_PASS);
-#define MB_ARGS d, codes_t, tp0, xn, r0, r1, nqi, qs, stride, qsplit, qn, qb, bucket, boff, nprobe, slot_off, chunk, k, smem, \
+#define MB_ARGS d, codes_t, tp0, xn, r0, r1, nqi, qs, stride, qsplit, qn, qb, bucket, boff, nprobe, slot_off, chunk, k, sub, smem, \
                 qbound, part_d, part_i
 #define MB_QN(QTV)                                                                                          \
     float qn[QTV][4];                                                                                       \
@@ -880,7 +863,7 @@ void launch_ivf_scan_mfma_bf(int np, const float *Q, int64_t nq, void *qsplit, c
                              const float *codes_t, const int64_t *tpass_off, const float *xn, const int64_t *list_off,
                              const int *cnt, const int *bucket_off, const int *item_off, const int *bucket,
                              const int *slot_off, int nlist, int nprobe, int k, int64_t max_items, unsigned *qbound,
-                             float *pd, int *pi, hipStream_t st) {
+                             float *pd, int *pi, hipStream_t st, int sub) {
     if (max_items <= 0 || nq <= 0) return;
     HIPANN_REQUIRE(np == 2 || np == 3, "split-bf16 scan: 2 or 3 terms");
     HIPANN_REQUIRE(max_items < (int64_t)0x7fffffff, "too many IVF work items");
@@ -898,7 +881,7 @@ void launch_ivf_scan_mfma_bf(int np, const float *Q, int64_t nq, void *qsplit, c
     const size_t smem = std::max((size_t)group * mb_stride(d, np, nh) * 4, merge);
     dim3 grid((unsigned)max_items), block(MF_THREADS);
 #define MB_LAUNCH_ARGS qs, qn, d, codes_t, tpass_off, xn, list_off, cnt, bucket_off, item_off, bucket, slot_off, nlist, nprobe, \
-                       group, k, qbound, pd, pi
+                       group, k, sub, qbound, pd, pi
 #define MB_LAUNCH(NP_, NH_)                                                                                         \
     do {                                                                                                            \
         if (metric == kIP) hipLaunchKernelGGL((ivf_scan_mfma_bf<true, NP_, NH_>), grid, block, smem, st, MB_LAUNCH_ARGS); \
@@ -1136,7 +1119,7 @@ __device__ __forceinline__ void mh_item(int d, const uint4 *__restrict__ codes_h
                                         const unsigned *__restrict__ qs, int stride, const float (&qn)[QT][4],
                                         const float (&qits)[QT][4], const unsigned (&qb)[QT][4],
                                         const int *__restrict__ bucket, int boff, int nprobe,
-                                        const int *__restrict__ slot_off, int chunk, int k, float *smem,
+                                        const int *__restrict__ slot_off, int chunk, int k, int sub, float *smem,
                                         unsigned *__restrict__ qbound, float *__restrict__ part_d,
                                         int *__restrict__ part_i) {
     const int lane = threadIdx.x & 63;
@@ -1263,44 +1246,7 @@ __device__ __forceinline__ void mh_item(int d, const uint4 *__restrict__ codes_h
         for (int r = 0; r < MF_RT; ++r) xnr[r] = xnr_next[r];
     }
 
-    uint64_t *scratch = reinterpret_cast<uint64_t *>(smem);
-#pragma unroll 1
-    for (int half = MF_WAVES / 2; half > 0; half >>= 1) {
-        __syncthreads();
-        if (wave >= half && wave < 2 * half) {
-            uint64_t *dst = scratch + (size_t)(wave - half) * QT * 4 * 64;
-#pragma unroll
-            for (int qt = 0; qt < QT; ++qt)
-#pragma unroll
-                for (int v = 0; v < 4; ++v) dst[(qt * 4 + v) * 64 + lane] = lst[qt][v];
-        }
-        __syncthreads();
-        if (wave < half) {
-            const uint64_t *src = scratch + (size_t)wave * QT * 4 * 64;
-#pragma unroll
-            for (int qt = 0; qt < QT; ++qt)
-#pragma unroll
-                for (int v = 0; v < 4; ++v) row_merge16(lst[qt][v], src[(qt * 4 + v) * 64 + lane], m);
-        }
-    }
-    if (wave == 0 && m < k) {
-#pragma unroll
-        for (int qt = 0; qt < QT; ++qt)
-#pragma unroll
-            for (int v = 0; v < 4; ++v) {
-                const int q = qt * 16 + 4 * g + v;
-                if (q < nqi) {
-                    const int pr = bucket[boff + q];
-                    const int64_t off = (int64_t)(slot_off[pr] + chunk) * k + m;
-                    const uint64_t e = lst[qt][v];
-                    const unsigned id = (unsigned)e;
-                    const bool real = e != MF_EMPTY && id != MF_PAD_ID;
-                    part_d[off] = real ? mf_unsortable((unsigned)(e >> 32)) : __builtin_inff();
-                    part_i[off] = real ? (int)id : (int)MF_PAD_ID;
-                    if (m == k - 1 && real) atomicMin(qbound + pr / nprobe, (unsigned)(e >> 32));
-                }
-            }
-    }
+    mf_finish_item<QT>(lst, smem, nqi, bucket, boff, nprobe, slot_off, chunk, k, sub, qbound, part_d, part_i);
 }
 
 template <bool IP>
@@ -1309,7 +1255,7 @@ ivf_scan_mfma_h(const uint4 *__restrict__ qsplit, const float *__restrict__ qnor
                 const uint4 *__restrict__ codes_h, const int64_t *__restrict__ tpass_off, const float *__restrict__ xn,
                 const int64_t *__restrict__ list_off, const int *__restrict__ cnt, const int *__restrict__ bucket_off,
                 const int *__restrict__ item_off, const int *__restrict__ bucket, const int *__restrict__ slot_off,
-                int nlist, int nprobe, int group, int k, unsigned *__restrict__ qbound, float *__restrict__ part_d,
+                int nlist, int nprobe, int group, int k, int sub, unsigned *__restrict__ qbound, float *__restrict__ part_d,
                 int *__restrict__ part_i) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int total = item_off[nlist];
@@ -1340,7 +1286,7 @@ ivf_scan_mfma_h(const uint4 *__restrict__ qsplit, const float *__restrict__ qnor
 
     const int lane = threadIdx.x & 63, g = lane >> 4;
     const int64_t tp0 = tpass_off[l] + (int64_t)chunk * (MF_CH / MF_PASS);
-#define MH_ARGS d, codes_h, tp0, xn, r0, r1, nqi, qs, stride, qn, qi_s, qb, bucket, boff, nprobe, slot_off, chunk, k, smem, \
+#define MH_ARGS d, codes_h, tp0, xn, r0, r1, nqi, qs, stride, qn, qi_s, qb, bucket, boff, nprobe, slot_off, chunk, k, sub, smem, \
                 qbound, part_d, part_i
 #define MH_QN(QTV)                                                                                          \
     float qn[QTV][4], qi_s[QTV][4];                                                                         \
@@ -1367,6 +1313,7 @@ ivf_scan_mfma_h(const uint4 *__restrict__ qsplit, const float *__restrict__ qnor
 }
 
 int ivf_mfma_h_group(int d) { return mh_group(d); }
+int ivf_scan_sublists() { return MF_WAVES; }
 int64_t ivf_half_pass_bytes(int d) { return (int64_t)mh_nsup(d) * MF_RT * 64 * 16; }
 int64_t ivf_half_qsplit_bytes(int64_t nq, int d) { return nq * 2 * mh_nsup(d) * 64; }
 bool ivf_mfma_h_supported(int d, int k) { return d >= 1 && k >= 1 && k <= MF_KMAX && mh_group(d) >= 16; }
@@ -1410,7 +1357,7 @@ void launch_ivf_scan_mfma_h(const float *Q, int64_t nq, void *qsplit, float *its
                             int d, int metric, const void *codes_h, const int64_t *tpass_off, const float *xn,
                             const int64_t *list_off, const int *cnt, const int *bucket_off, const int *item_off,
                             const int *bucket, const int *slot_off, int nlist, int nprobe, int k, int64_t max_items,
-                            unsigned *qbound, float *pd, int *pi, hipStream_t st, bool split_done) {
+                            unsigned *qbound, float *pd, int *pi, hipStream_t st, bool split_done, int sub) {
     if (max_items <= 0 || nq <= 0) return;
     HIPANN_REQUIRE(max_items < (int64_t)0x7fffffff, "too many IVF work items");
     HIPANN_REQUIRE(qsplit && its && qres && codes_h, "fp16 IVF scan: missing buffers");
@@ -1427,7 +1374,7 @@ void launch_ivf_scan_mfma_h(const float *Q, int64_t nq, void *qsplit, float *its
     dim3 grid((unsigned)max_items), block(MF_THREADS);
     const uint4 *ch = static_cast<const uint4 *>(codes_h);
 #define MH_LAUNCH_ARGS qs, qn, its, d, ch, tpass_off, xn, list_off, cnt, bucket_off, item_off, bucket, slot_off, nlist, nprobe, \
-                       group, k, qbound, pd, pi
+                       group, k, sub, qbound, pd, pi
     if (metric == kIP) hipLaunchKernelGGL((ivf_scan_mfma_h<true>), grid, block, smem, st, MH_LAUNCH_ARGS);
     else hipLaunchKernelGGL((ivf_scan_mfma_h<false>), grid, block, smem, st, MH_LAUNCH_ARGS);
 #undef MH_LAUNCH_ARGS

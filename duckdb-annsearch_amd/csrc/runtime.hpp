@@ -205,6 +205,9 @@ struct IndexBase {
     int metric = kL2;
     std::mutex mu;
     KernelTimer timer_main, timer_merge;
+    // the last search's path (hipann_last_search_path): the scan form that ran (FlatForm / IvfForm; an exact
+    // form's flagged re-runs excluded), its rerank filter depth (0: no rerank) and sub-lists per slot (IVF)
+    int last_form = -1, last_kfilt = 0, last_sublists = 0;
     explicit IndexBase(Kind k) : kind(k) {}
     virtual ~IndexBase() = default;
     virtual int64_t ntotal() const = 0;
@@ -351,9 +354,10 @@ void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int 
                        int64_t label_offset, float xmax2, float *D, int64_t *I, int *nflag, int *flagged,
                        hipStream_t st, float eps = kSplit2Eps, float rxmax = -1.f, const float *qres = nullptr,
                        const int64_t *probes = nullptr, const int64_t *list_off = nullptr, int nlist = 0,
-                       const unsigned *qbound = nullptr, const float *qnorm = nullptr);
+                       const unsigned *qbound = nullptr, const float *qnorm = nullptr, int kslot = 0, int sub = 0);
 // ivf_mfma.hip, fp16-image scan (kFormHalfExact)
 int ivf_mfma_h_group(int d);
+int ivf_scan_sublists();  // sub-lists per slot of the matrix-core scans in sub-list mode (one per wave)
 int64_t ivf_half_pass_bytes(int d);
 int64_t ivf_half_qsplit_bytes(int64_t nq, int d);
 bool ivf_mfma_h_supported(int d, int k);
@@ -365,13 +369,16 @@ void launch_ivf_scan_mfma_h(const float *Q, int64_t nq, void *qsplit, float *its
                             int d, int metric, const void *codes_h, const int64_t *tpass_off, const float *xn,
                             const int64_t *list_off, const int *cnt, const int *bucket_off, const int *item_off,
                             const int *bucket, const int *slot_off, int nlist, int nprobe, int k, int64_t max_items,
-                            unsigned *qbound, float *pd, int *pi, hipStream_t st, bool split_done = false);
+                            unsigned *qbound, float *pd, int *pi, hipStream_t st, bool split_done = false,
+                            int sub = 0);
 // the batch's fp16 query terms (+ 1/(t·s), split residuals) and, when qn != nullptr, ‖q‖² (row_norms_f32's bits)
 void launch_ivf_split_queries_h(const float *Q, int64_t nq, int d, int es, void *qsplit, float *its, float *qres,
                                 float *qn, hipStream_t st);
 // flat_bf16.hip
 int flat_bf16_waves(int64_t nq);
 int flat_bf16_tile_rows();
+int flat_bf16_topk_kmax(int64_t nq);
+int flat_gemm_topk_bf_kmax(int np);
 size_t flat_bf16_img_bytes(int64_t n, int d, int R);
 void launch_b16_tile_rows(const float *X, int64_t n, int d, int R, void *out, hipStream_t st);
 void launch_b16_row_residual2(const float *X, int64_t n, int d, float *out, hipStream_t st);
@@ -380,7 +387,6 @@ void launch_flat_bf16_topk(const float *Q, const float *qn, int64_t nq, void *qi
                            const float *seed, bool image_ready, hipStream_t st);
 // bounded passes of the 64-dim K-step kernel (flat_b16k64.hip): candidate buffers, their bound and select
 bool flat_bf16_resumable(int64_t nq, int d, int k);
-size_t flat_bf16_k64_cap();
 void launch_flat_bf16_k64(const void *qimg, const float *qn, int64_t nq, const void *ximg, const float *xn, int64_t N,
                           int nk, int metric, int nqt, int nsplit, int64_t tiles_per_split, int64_t tile_begin,
                           int64_t tile_end, const float *bound, float *cand_d, int *cand_i, int *cand_n, int cap,
@@ -405,7 +411,7 @@ void launch_ivf_scan_mfma_bf(int np, const float *Q, int64_t nq, void *qsplit, c
                              const float *codes_t, const int64_t *tpass_off, const float *xn, const int64_t *list_off,
                              const int *cnt, const int *bucket_off, const int *item_off, const int *bucket,
                              const int *slot_off, int nlist, int nprobe, int k, int64_t max_items, unsigned *qbound,
-                             float *pd, int *pi, hipStream_t st);
+                             float *pd, int *pi, hipStream_t st, int sub = 0);
 int ivf_group_size(int form, int d);  // queries per work item of the form's scan kernel
 int ivf_chunk_rows();
 bool ivf_plan_query_major();
@@ -427,7 +433,7 @@ void launch_ivf_scan_mfma(const float *Q, const float *qn, int d, int metric, co
                           const int64_t *tpass_off, const float *xn,
                           const int64_t *list_off, const int *cnt, const int *bucket_off, const int *item_off,
                           const int *bucket, const int *slot_off, int nlist, int nprobe, int k, int64_t max_items,
-                          unsigned *qbound, float *pd, int *pi, hipStream_t st);
+                          unsigned *qbound, float *pd, int *pi, hipStream_t st, int sub = 0);
 void launch_ivf_merge(const float *pd, const int *pi, const int64_t *ids, int64_t nrows, const int *slot_off, int nprobe, int64_t nq,
                       int k, int kout, float out_sign, float *D, int64_t *I, hipStream_t st);
 template <typename InId>

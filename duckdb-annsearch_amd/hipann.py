@@ -94,6 +94,7 @@ def lib() -> C.CDLL:
             "hipann_flat_search_device": ([vp, i64, vp, i64, vp, vp, vp, cp, i32], i32),
             "hipann_flat_set_form": ([vp, i32], i32),
             "hipann_flat_get_form": ([vp], i32),
+            "hipann_last_search_path": ([vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)], i32),
             "hipann_flat_rerank_fallbacks": ([vp], i64),
             "hipann_merge_topk_device": ([i32, i32, i64, i64, vp, vp, vp, vp, vp, cp, i32], i32),
             "hipann_merge_topk_packed_device": ([i32, i32, i64, i64, vp, i64, vp, vp, vp, cp, i32], i32),
@@ -222,6 +223,13 @@ class _Handle:
 
     def set_kernel_timing(self, on: bool) -> None:
         lib().hipann_set_kernel_timing(self._h, 1 if on else 0)
+
+    def last_search_path(self) -> dict:
+        """hipann_last_search_path: the form the last search's scan ran, its rerank filter depth (0 = none) and
+        the IVF sub-lists per slot (0 = merged lists)."""
+        f, kf, sl = C.c_int(-1), C.c_int(0), C.c_int(0)
+        lib().hipann_last_search_path(self._h, C.byref(f), C.byref(kf), C.byref(sl))
+        return {"form": f.value, "filter_k": kf.value, "sublists": sl.value}
 
     def kernel_ms(self, which: int = 0) -> float:
         return float(lib().hipann_last_kernel_ms(self._h, which))

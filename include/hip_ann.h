@@ -107,6 +107,14 @@ int hipann_flat_get_form(void *index);
  * the flagged ones. */
 int64_t hipann_flat_rerank_fallbacks(void *index);
 
+/* The path the last search of `index` (Flat or IVF) took: *form = the distance form its scan ran
+ * (HIPANN_FLAT_FORM_* / HIPANN_IVF_FORM_*; the exact forms' re-runs of flagged queries not counted),
+ * *filter_k = the exact forms' rerank depth (candidates per query; 0 = no rerank), *sublists = IVF sub-lists
+ * per (query, list, chunk) slot (0 = one merged list).  Any output may be NULL.  Request_k above 12 — the
+ * extension asks for k + |tombstones| (faiss_index.cpp:713-715) — stays on the exact forms up to 64 (Flat
+ * bounded passes) / 60 (IVF) with a deeper filter; this is how tests and the bench see it.  Returns 0 / -1. */
+int hipann_last_search_path(void *index, int *form, int *filter_k, int *sublists);
+
 /* ---------------------------------------------------------------------------------------------
  * Device-resident variants (inputs and outputs already in HBM).  Used by the multi-GPU sharded
  * search (one process per GPU, partial top-k gathered over RCCL) and by bench.py, whose timed

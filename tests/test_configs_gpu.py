@@ -118,6 +118,22 @@ def test_c2_flat_1m_768_nq1024(gpu, c2_data, c2_oracle, form):
     ix.close()
 
 
+def test_c2_flat_1m_768_request_k30(gpu, c2_data, oracle):
+    """C2 with request_k = 30 (k = 10 plus 20 tombstones, faiss_index.cpp:713-715): the bounded passes with a
+    60-candidate filter, exact; the oracle's parity rule on 128 queries."""
+    import torch
+
+    xb_t, xq_t, xb, xq = c2_data
+    ix = gpu.HipIndexFlatDevice(768, 0, xb_t.data_ptr(), xb_t.shape[0], 0, copy=False)
+    D, I = _dev_search(ix, xq_t, 30, torch)
+    assert ix.last_search_path() == {"form": 4, "filter_k": 60, "sublists": 0}
+    Do, Io = oracle.flat_search(xb, xq[:128], 30, 0)
+    st = check_topk_parity(xb, xq[:128], D[:128], I[:128], Do, Io, 0)
+    assert st["exact_fraction"] >= 0.995, st
+    assert ix.rerank_fallbacks() == 0
+    ix.close()
+
+
 @pytest.fixture(scope="module")
 def c3_index(gpu):
     import torch
@@ -167,6 +183,26 @@ def test_c3_ivf_nlist1024_nprobe32_d768_nq1024(gpu, c3_index, c3_oracle, form):
     if form in (5, 6):  # returned distances are the direct fp32 form, like the oracle's scanner
         v = I[same] >= 0
         assert np.allclose(D[same][v], Do[same][v], rtol=2e-6, atol=1e-6)
+    index.form = 6
+
+
+@pytest.mark.parametrize("form", [6, 5])
+def test_c3_request_k30(gpu, c3_index, oracle, form):
+    """C3 shape with request_k = 30 (k = 10 plus 20 tombstones): sub-list slots and a 60-candidate rerank,
+    exact fp32 direct-form distances; ids follow the oracle's parity rule on every query whose probe list is
+    the oracle's."""
+    import torch
+
+    index, info, xb, xq_t, xq, (cen, off, ids, codes) = c3_index
+    index.form = form
+    D, I = _dev_search(index, xq_t, 30, torch)
+    assert index.last_search_path() == {"form": form, "filter_k": 60, "sublists": 8}
+    Do, Io, Po = oracle.ivf_search(cen, off, ids, codes, xq, 30, 32, 0)
+    same = check_probe_parity(cen, xq, index.last_probes(len(xq)), Po, 0)
+    st = check_topk_parity(xb, xq[same], D[same], I[same], Do[same], Io[same], 0)
+    assert st["exact_fraction"] >= 0.995, st
+    v = I[same] >= 0
+    assert np.allclose(D[same][v], Do[same][v], rtol=2e-6, atol=1e-6)
     index.form = 6
 
 
