@@ -42,19 +42,21 @@ int to_hip_metric(faiss::MetricType m) {
     throw std::runtime_error("HIP GPU backend supports METRIC_L2 and METRIC_INNER_PRODUCT only");
 }
 
-struct Handle {
-    void *h = nullptr;
-    explicit Handle(void *p) : h(p) {}
-    ~Handle() { hipann_free(h); }
-    Handle(const Handle &) = delete;
-    Handle &operator=(const Handle &) = delete;
-};
-
 void check(int rc, const char *err) {
     if (rc != 0) throw std::runtime_error(std::string("HIP search failed: ") + err);
 }
 
 }  // namespace
+
+// Owner of a libhipann handle (hipann_free on destruction).  A named type: the index classes below have external
+// linkage, so their members must not use the anonymous namespace.
+struct HipAnnHandle {
+    void *h = nullptr;
+    explicit HipAnnHandle(void *p) : h(p) {}
+    ~HipAnnHandle() { hipann_free(h); }
+    HipAnnHandle(const HipAnnHandle &) = delete;
+    HipAnnHandle &operator=(const HipAnnHandle &) = delete;
+};
 
 // A faiss::Index whose search runs on the MI355X (the HipIndexFlat of SURVEY §8b B1).
 class HipIndexFlat : public faiss::Index {
@@ -64,7 +66,7 @@ public:
         void *h = hipann_flat_create((int)cpu.d, to_hip_metric(cpu.metric_type), cpu.get_xb(), cpu.ntotal, nullptr,
                                      0, err, sizeof err);
         if (!h) throw std::runtime_error(std::string("hipann_flat_create: ") + err);
-        handle_ = std::make_unique<Handle>(h);
+        handle_ = std::make_unique<HipAnnHandle>(h);
         ntotal = cpu.ntotal;
         is_trained = true;
     }
@@ -88,7 +90,7 @@ public:
     void *handle() const { return handle_->h; }
 
 private:
-    std::unique_ptr<Handle> handle_;
+    std::unique_ptr<HipAnnHandle> handle_;
 };
 
 class HipIndexIVFFlat : public faiss::Index {
@@ -113,7 +115,7 @@ public:
                                     flatq->get_xb(), offsets.data(), ids.data(), codes.data(), nullptr, 0, err,
                                     sizeof err);
         if (!h) throw std::runtime_error(std::string("hipann_ivf_create: ") + err);
-        handle_ = std::make_unique<Handle>(h);
+        handle_ = std::make_unique<HipAnnHandle>(h);
         ntotal = cpu.ntotal;
         is_trained = true;
         nprobe_ = cpu.nprobe;
@@ -147,7 +149,7 @@ public:
     void *handle() const { return handle_->h; }
 
 private:
-    std::unique_ptr<Handle> handle_;
+    std::unique_ptr<HipAnnHandle> handle_;
     size_t nlist_ = 0, nprobe_ = 1;
 };
 
