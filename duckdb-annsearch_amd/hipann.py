@@ -109,6 +109,9 @@ def lib() -> C.CDLL:
             "hipann_ivf_search_np": ([vp, i32, i64, f, i64, f, i64p, cp, i32], i32),
             "hipann_ivf_add": ([vp, i64, f, i64p, cp, i32], i32),
             "hipann_ivf_export": ([vp, f, i64p, i64p, f, cp, i32], i32),
+            "hipann_ivf_train": ([i32, i32, i32, i64, f, i64, i32, C.c_uint64, i32, i32, f, i64p, cp, i32], i32),
+            "hipann_ivf_train_device": ([i32, i32, i32, i64, vp, i64, i32, C.c_uint64, i32, i32, vp, vp, cp, i32],
+                                        i32),
             "hipann_flat_reconstruct_n": ([vp, i64, i64, f, cp, i32], i32),
             "hipann_ivf_set_form": ([vp, i32], i32),
             "hipann_ivf_get_form": ([vp], i32),
@@ -470,6 +473,32 @@ class HipIndexIVFFlat(_Handle):
         eb = _err()
         _check(lib().hipann_ivf_last_probes(self._h, _ptr(P, C.c_int64), P.size, eb, 1024), eb)
         return P
+
+
+KMEANS_INIT_RANDOM, KMEANS_INIT_PLUSPLUS = 0, 1
+
+
+def ivf_train(x, nlist: int, metric: int = METRIC_L2, train_sample: int = 0, niter: int = 25, seed: int = 1234,
+              init: int = KMEANS_INIT_PLUSPLUS, device: int = 0) -> Tuple[np.ndarray, np.ndarray]:
+    """hipann_ivf_train: IndexIVFFlat::train on the GPU (k-means over the stride sample of train_sample rows,
+    faiss_index.cpp:302-319).  Returns (centroids nlist x d, the last iteration's cluster sizes)."""
+    x = _f32_2d(x)
+    n, d = x.shape
+    cen = np.empty((nlist, d), np.float32)
+    sizes = np.empty(nlist, np.int64)
+    eb = _err()
+    _check(lib().hipann_ivf_train(d, metric, nlist, n, _ptr(x, C.c_float), train_sample, niter, seed, init, device,
+                                  _ptr(cen, C.c_float), _ptr(sizes, C.c_int64), eb, 1024), eb)
+    return cen, sizes
+
+
+def ivf_train_device(d: int, nlist: int, n: int, x_ptr: int, centroids_ptr: int, metric: int = METRIC_L2,
+                     train_sample: int = 0, niter: int = 25, seed: int = 1234, init: int = KMEANS_INIT_PLUSPLUS,
+                     device: int = 0, stream: int = 0) -> None:
+    """hipann_ivf_train_device: the same with the rows (n x d fp32) and the centroids (nlist x d) in HBM."""
+    eb = _err()
+    _check(lib().hipann_ivf_train_device(d, metric, nlist, n, C.c_void_p(x_ptr), train_sample, niter, seed, init,
+                                         device, C.c_void_p(centroids_ptr), C.c_void_p(stream or None), eb, 1024), eb)
 
 
 # ------------------------------------------------------------------------------------------------

@@ -4,8 +4,10 @@ The extension builds its IVF index on the CPU with FAISS (faiss_index.cpp:302-33
 stride sample, then add) and copies it to the GPU (index_cpu_to_metal_ivf,
 MetalIndexIVFFlat.mm:283-326).  FAISS is absent here, so this module does the same work on the GPU
 (SURVEY §8f rank 4): k-means over a 256·nlist-point sample (FAISS's default max_points_per_centroid,
-25 iterations, seeded init from the sample), assignment of every row with the Flat kernels (k = 1),
+25 iterations, k-means++ init) through the C ABI (hipann_ivf_train_device: the same entry point the extension's
+CREATE INDEX would call, faiss_index.cpp:302-319), assignment of every row with the Flat kernels (k = 1),
 a stable counting sort into list-contiguous storage, and hipann_ivf_create_device on the result.
+``kmeans_torch`` is the r01-r03 torch implementation, kept as the comparison the C-ABI training is held to.
 
 Training sample: the first 256·nlist rows of the database (identical for every world size, so the
 1/2/4/8-GPU runs search the same lists).
@@ -43,7 +45,20 @@ def kmeans_pp_init(torch, x, nlist: int, g):
 
 
 def kmeans(torch, hipann, x, nlist: int, niter: int = 25, seed: int = 1234, metric: int = 0, init: str = "kmeans++"):
-    """Lloyd k-means on the GPU (assignment through the Flat kernels).  x: (m, d) CUDA fp32."""
+    """IVF training through the C ABI (hipann_ivf_train_device): k-means++ init + Lloyd on the GPU, no torch in the
+    loop.  x: (m, d) CUDA fp32 (m <= 256·nlist: the whole of it is the training set)."""
+    m, d = x.shape
+    cen = torch.empty((nlist, d), device=x.device, dtype=torch.float32)
+    torch.cuda.synchronize()
+    hipann.ivf_train_device(d, nlist, m, x.data_ptr(), cen.data_ptr(), metric=metric, train_sample=0, niter=niter,
+                            seed=seed, init=hipann.KMEANS_INIT_PLUSPLUS if init == "kmeans++" else hipann.KMEANS_INIT_RANDOM,
+                            device=x.device.index, stream=torch.cuda.current_stream().cuda_stream)
+    return cen
+
+
+def kmeans_torch(torch, hipann, x, nlist: int, niter: int = 25, seed: int = 1234, metric: int = 0,
+                 init: str = "kmeans++"):
+    """The r01-r03 Lloyd k-means in torch (assignment through the Flat kernels).  x: (m, d) CUDA fp32."""
     m, d = x.shape
     g = torch.Generator(device="cpu")
     g.manual_seed(seed)
@@ -74,7 +89,7 @@ def kmeans(torch, hipann, x, nlist: int, niter: int = 25, seed: int = 1234, metr
 
 
 def build_ivf_shard(torch, hipann, xb, row0: int, n_total: int, nlist: int, nprobe: int, metric: int, rank: int,
-                    world: int, centres_seed: int = 1234, train_points_per_list: int = 256):
+                    world: int, centres_seed: int = 1234, train_points_per_list: int = 256, train=None):
     """Returns (HipIndexIVFFlat over this rank's rows, info dict)."""
     import torch.distributed as dist
 
@@ -83,7 +98,7 @@ def build_ivf_shard(torch, hipann, xb, row0: int, n_total: int, nlist: int, npro
     # ---- train (rank 0, on the first 256·nlist rows; rank 0 holds them in both layouts) ----
     if rank == 0:
         m = min(n_local, train_points_per_list * nlist)
-        cen = kmeans(torch, hipann, xb[:m].contiguous(), nlist, seed=centres_seed)
+        cen = (train or kmeans)(torch, hipann, xb[:m].contiguous(), nlist, seed=centres_seed)
     else:
         cen = torch.empty((nlist, d), device=dev, dtype=torch.float32)
     if world > 1:

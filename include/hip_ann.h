@@ -191,6 +191,33 @@ int hipann_ivf_nlist(void *index);
  * (NULL: ntotal + i).  Replaces the reference's invalidate-on-append (faiss_index.cpp:469). */
 int hipann_ivf_add(void *index, int64_t n, const float *xb, const int64_t *ids, char *err_buf, int err_len);
 
+/* IVF training on the GPU — the k-means behind IndexIVFFlat::train (FAISS 1.13.2 IndexIVF::train_q1 →
+ * Clustering::train), which the extension runs on the CPU at CREATE INDEX on a stride sample
+ * (src/faiss_index.cpp:302-319).  From the n rows `x` (host, n*d fp32):
+ *   1. training rows: when 0 < train_sample < n, rows floor(i * n / train_sample), i < train_sample — the
+ *      reference's deterministic stride sample; else all n rows (n must be >= nlist);
+ *   2. at most 256 rows per centroid (FAISS's max_points_per_centroid): above that, a uniform subset;
+ *   3. init: HIPANN_KMEANS_INIT_RANDOM (FAISS's: nlist random training rows) or HIPANN_KMEANS_INIT_PLUSPLUS
+ *      (k-means++ D² sampling on the GPU);
+ *   4. niter Lloyd iterations (FAISS's default 25): assignment by the GPU Flat search (k = 1, exact fp32
+ *      products), centroids = fp64 means, FAISS's split of empty clusters, and for IP the spherical
+ *      renormalisation (IndexIVF sets cp.spherical for METRIC_INNER_PRODUCT).
+ * Every random draw comes from splitmix64(seed), so a result is reproducible and equals the oracle's
+ * restatement (oracle/oracle.c oracle_kmeans_train) up to assignment ties; FAISS's own draws are not
+ * reproduced.  centroids: nlist*d fp32 (host); list_sizes (optional, nlist int64): the cluster sizes of the
+ * last iteration's assignment.  The result feeds hipann_ivf_create (or the CPU index's quantizer). */
+#define HIPANN_KMEANS_INIT_RANDOM 0
+#define HIPANN_KMEANS_INIT_PLUSPLUS 1
+int hipann_ivf_train(int d, int metric, int nlist, int64_t n, const float *x, int64_t train_sample, int niter,
+                     uint64_t seed, int init, int device, float *centroids, int64_t *list_sizes, char *err_buf,
+                     int err_len);
+
+/* The same with the rows and the result in HBM on `device` (x_dev: n*d fp32, centroids_dev: nlist*d fp32);
+ * runs on `stream` and returns when the centroids are written. */
+int hipann_ivf_train_device(int d, int metric, int nlist, int64_t n, const float *x_dev, int64_t train_sample,
+                            int niter, uint64_t seed, int init, int device, float *centroids_dev, void *stream,
+                            char *err_buf, int err_len);
+
 /* Copy the index back to host in FAISS's ArrayInvertedLists CSR form — the inverse of hipann_ivf_create
  * (GpuBackend::GpuToCpu, gpu_backend_metal.mm:62-67 → index_metal_to_cpu_ivf, MetalIndexIVFFlat.mm:328-356):
  * centroids (nlist*d), list_offsets (nlist+1), ids (ntotal) and codes (ntotal*d, raw fp32 rows), lists in

@@ -605,3 +605,200 @@ int oracle_num_threads(void) {
     return 1;
 #endif
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* IVF training (k-means): the restatement hipann_ivf_train is checked against                */
+/* ------------------------------------------------------------------------------------------ */
+/*
+ * The extension trains its IndexIVFFlat on the CPU at CREATE INDEX (src/faiss_index.cpp:302-319: a
+ * deterministic stride sample of train_sample rows, then faiss_idx->train → FAISS 1.13.2 IndexIVF::train_q1 →
+ * Clustering::train, external).  hipann_ivf_train runs the same pipeline on the GPU; FAISS's own random draws
+ * (its RandomGenerator over rand_perm / rand_float) are not reproduced, so the GPU is pinned to THIS
+ * restatement, which fixes every draw to splitmix64(seed):
+ *   1. training rows: the reference's stride sample (faiss_index.cpp:307-313) when 0 < train_sample < n;
+ *   2. FAISS's max_points_per_centroid = 256: above 256·nlist rows, a uniform subset (partial Fisher-Yates,
+ *      kept in ascending row order);
+ *   3. init 0: FAISS's random init (the first nlist rows of a partial Fisher-Yates); init 1: k-means++ (D²
+ *      sampling) with fp64 squared distances — each row's 64 lane-strided partial sums then an xor butterfly,
+ *      the GPU kernel's order — and weights w = floor(d² · 2^32 / max d²) as integers, so the draw
+ *      t = r mod Σw picks the same row whatever the summation order of the weights;
+ *   4. niter Lloyd iterations (FAISS Clustering::train): assignment = the Flat search with k = 1 (this
+ *      oracle's FAISS restatement: BLAS form at >= 20 rows), centroids = fp64 means in row order,
+ *      FAISS's split_clusters for empty ones (EPS = 1/1024, split probability (n_j − 1)/(m − nlist)),
+ *      and for IP the spherical renormalisation (IndexIVF sets cp.spherical for METRIC_INNER_PRODUCT).
+ */
+static uint64_t km_next(uint64_t *s) {
+    uint64_t z = (*s += 0x9e3779b97f4a7c15ULL);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+static float km_rand_float(uint64_t *s) { return (float)(km_next(s) >> 40) * 0x1p-24f; }
+
+/* squared L2 in fp64: 64 lane partials (lane l sums dims l, l+64, … in order), then the xor butterfly */
+static double km_dist64(const float *a, const float *b, int d) {
+    double p[64], t[64];
+    for (int l = 0; l < 64; ++l) {
+        double acc = 0.0;
+        for (int e = l; e < d; e += 64) {
+            const double df = (double)a[e] - (double)b[e];
+            acc = acc + df * df;
+        }
+        p[l] = acc;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        for (int l = 0; l < 64; ++l) t[l] = p[l] + p[l ^ o];
+        memcpy(p, t, sizeof p);
+    }
+    return p[0];
+}
+
+int oracle_kmeans_train(const float *x, int64_t n, int d, int metric, int nlist, int64_t train_sample, int niter,
+                        uint64_t seed, int init, float *centroids, int64_t *sizes_out) {
+    if (d <= 0 || nlist <= 0 || n <= 0) return -1;
+    uint64_t rs = seed;
+    /* 1. stride sample */
+    int64_t m = n;
+    int64_t *rows = NULL;
+    if (train_sample > 0 && train_sample < n) {
+        m = train_sample;
+        rows = (int64_t *)malloc(sizeof(int64_t) * (size_t)m);
+        const double stride = (double)n / (double)train_sample;
+        for (int64_t i = 0; i < m; ++i) rows[i] = (int64_t)((double)i * stride);
+    } else {
+        rows = (int64_t *)malloc(sizeof(int64_t) * (size_t)m);
+        for (int64_t i = 0; i < m; ++i) rows[i] = i;
+    }
+    if (m < nlist) { free(rows); return -1; }
+    /* 2. at most 256 per centroid */
+    const int64_t maxp = (int64_t)256 * nlist;
+    if (m > maxp) {
+        int64_t *perm = (int64_t *)malloc(sizeof(int64_t) * (size_t)m);
+        for (int64_t i = 0; i < m; ++i) perm[i] = i;
+        for (int64_t i = 0; i < maxp; ++i) {
+            const int64_t j = i + (int64_t)(km_next(&rs) % (uint64_t)(m - i));
+            const int64_t tmp = perm[i]; perm[i] = perm[j]; perm[j] = tmp;
+        }
+        /* ascending row order: mark the chosen, then collect */
+        char *pick = (char *)calloc((size_t)m, 1);
+        for (int64_t i = 0; i < maxp; ++i) pick[perm[i]] = 1;
+        int64_t w = 0;
+        for (int64_t i = 0; i < m; ++i)
+            if (pick[i]) rows[w++] = rows[i];
+        free(pick);
+        free(perm);
+        m = maxp;
+    }
+    float *T = (float *)malloc(sizeof(float) * (size_t)m * d);
+    for (int64_t i = 0; i < m; ++i) memcpy(T + i * (int64_t)d, x + rows[i] * (int64_t)d, sizeof(float) * (size_t)d);
+    free(rows);
+    /* 3. init */
+    if (init == 0) {
+        int64_t *perm = (int64_t *)malloc(sizeof(int64_t) * (size_t)m);
+        for (int64_t i = 0; i < m; ++i) perm[i] = i;
+        for (int64_t i = 0; i < nlist; ++i) {
+            const int64_t j = i + (int64_t)(km_next(&rs) % (uint64_t)(m - i));
+            const int64_t tmp = perm[i]; perm[i] = perm[j]; perm[j] = tmp;
+            memcpy(centroids + i * (int64_t)d, T + perm[i] * (int64_t)d, sizeof(float) * (size_t)d);
+        }
+        free(perm);
+    } else {
+        double *d2 = (double *)malloc(sizeof(double) * (size_t)m);
+        uint64_t *wt = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)m);
+        for (int64_t i = 0; i < m; ++i) d2[i] = DBL_MAX;
+        int64_t pick = (int64_t)(km_next(&rs) % (uint64_t)m);
+        memcpy(centroids, T + pick * (int64_t)d, sizeof(float) * (size_t)d);
+        for (int j = 1; j < nlist; ++j) {
+            const float *c = centroids + (int64_t)(j - 1) * d;
+            double mx = 0.0;
+#pragma omp parallel for reduction(max : mx)
+            for (int64_t i = 0; i < m; ++i) {
+                const double v = km_dist64(T + i * (int64_t)d, c, d);
+                if (v < d2[i]) d2[i] = v;
+                if (d2[i] > mx) mx = d2[i];
+            }
+            const uint64_t r = km_next(&rs);
+            if (mx > 0.0) {
+                const double scale = 4294967296.0 / mx;
+                uint64_t tot = 0;
+                for (int64_t i = 0; i < m; ++i) { wt[i] = (uint64_t)(d2[i] * scale); tot += wt[i]; }
+                const uint64_t t = r % tot;
+                uint64_t acc = 0;
+                pick = m - 1;
+                for (int64_t i = 0; i < m; ++i) {
+                    acc += wt[i];
+                    if (acc > t) { pick = i; break; }
+                }
+            } else {
+                pick = (int64_t)(r % (uint64_t)m);
+            }
+            memcpy(centroids + (int64_t)j * d, T + pick * (int64_t)d, sizeof(float) * (size_t)d);
+        }
+        free(d2);
+        free(wt);
+    }
+    /* 4. Lloyd */
+    float *D = (float *)malloc(sizeof(float) * (size_t)m);
+    int64_t *I = (int64_t *)malloc(sizeof(int64_t) * (size_t)m);
+    double *S = (double *)malloc(sizeof(double) * (size_t)nlist * d);
+    int64_t *cnt = (int64_t *)malloc(sizeof(int64_t) * (size_t)nlist);
+    float *hs = (float *)malloc(sizeof(float) * (size_t)nlist);
+    const float EPS = 1.f / 1024.f;
+    for (int it = 0; it < niter; ++it) {
+        oracle_flat_search(centroids, nlist, d, T, m, 1, metric, 0, D, I);
+        memset(S, 0, sizeof(double) * (size_t)nlist * d);
+        memset(cnt, 0, sizeof(int64_t) * (size_t)nlist);
+        for (int64_t i = 0; i < m; ++i) {
+            const int64_t a = I[i];
+            if (a < 0 || a >= nlist) continue;
+            cnt[a]++;
+            double *s = S + a * (int64_t)d;
+            const float *xi = T + i * (int64_t)d;
+            for (int e = 0; e < d; ++e) s[e] = s[e] + (double)xi[e];
+        }
+        for (int c = 0; c < nlist; ++c) {
+            if (!cnt[c]) continue;
+            for (int e = 0; e < d; ++e)
+                centroids[(int64_t)c * d + e] = (float)(S[(int64_t)c * d + e] / (double)cnt[c]);
+        }
+        /* FAISS split_clusters (clustering.cpp): its cluster sizes are floats (hassign), halved exactly */
+        for (int c = 0; c < nlist; ++c) hs[c] = (float)cnt[c];
+        for (int ci = 0; ci < nlist; ++ci) {
+            if (hs[ci] != 0.f) continue;
+            int cj = 0;
+            for (;; cj = (cj + 1) % nlist) {
+                const float p = (float)(((double)hs[cj] - 1.0) / (double)(float)(m - nlist));
+                const float r = km_rand_float(&rs);
+                if (r < p) break;
+            }
+            float *a = centroids + (int64_t)ci * d, *b = centroids + (int64_t)cj * d;
+            memcpy(a, b, sizeof(float) * (size_t)d);
+            for (int e = 0; e < d; ++e) {
+                if (e % 2 == 0) { a[e] *= 1 + EPS; b[e] *= 1 - EPS; }
+                else { a[e] *= 1 - EPS; b[e] *= 1 + EPS; }
+            }
+            hs[ci] = hs[cj] / 2;
+            hs[cj] -= hs[ci];
+        }
+        if (metric == ORACLE_IP) { /* spherical: renormalise every centroid */
+            for (int c = 0; c < nlist; ++c) {
+                float *a = centroids + (int64_t)c * d;
+                double s = 0.0;
+                for (int e = 0; e < d; ++e) s = s + (double)a[e] * (double)a[e];
+                if (s > 0.0) {
+                    const float inv = (float)(1.0 / sqrt(s));
+                    for (int e = 0; e < d; ++e) a[e] *= inv;
+                }
+            }
+        }
+    }
+    if (sizes_out)
+        for (int c = 0; c < nlist; ++c) sizes_out[c] = niter > 0 ? cnt[c] : 0;
+    free(D);
+    free(I);
+    free(S);
+    free(cnt);
+    free(hs);
+    free(T);
+    return 0;
+}

@@ -47,6 +47,8 @@ def lib():
         _lib.oracle_diskann_search_batch.argtypes = [f, u8, f, f, C.c_uint32, i32, u32, i32, u32, i32, f, i32, i32,
                                                      i32, i32, i64, f, i64]
         _lib.oracle_num_threads.restype = C.c_int
+        _lib.oracle_kmeans_train.argtypes = [f, C.c_int64, i32, i32, i32, C.c_int64, i32, C.c_uint64, i32, f, i64]
+        _lib.oracle_kmeans_train.restype = C.c_int
     return _lib
 
 
@@ -183,3 +185,17 @@ def diskann_search_batch(adj, entry_points, queries, k, l_search, metric=L2, vec
                                       eps.size, _p(queries, C.c_float), nq, kk, l_search, metric,
                                       _p(out_i, C.c_int64), _p(out_d, C.c_float), _p(stats, C.c_int64))
     return out_i, out_d, {"evals": int(stats[0]), "steps": int(stats[1])}
+
+
+def kmeans_train(x, nlist, metric=L2, train_sample=0, niter=25, seed=1234, init=1):
+    """oracle_kmeans_train: the restatement of hipann_ivf_train (stride sample, subsample, init, Lloyd with
+    FAISS's split_clusters / spherical renorm).  Returns (centroids nlist x d, last iteration's cluster sizes)."""
+    x = _f32(x)
+    n, d = x.shape
+    cen = np.empty((nlist, d), np.float32)
+    sizes = np.empty(nlist, np.int64)
+    rc = lib().oracle_kmeans_train(_p(x, C.c_float), n, d, metric, nlist, train_sample, niter, seed, init,
+                                   _p(cen, C.c_float), _p(sizes, C.c_int64))
+    if rc != 0:
+        raise ValueError("oracle_kmeans_train: bad arguments (n < nlist?)")
+    return cen, sizes

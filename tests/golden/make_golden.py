@@ -93,8 +93,38 @@ def sql_known_answers():
     }
 
 
+# hipann_ivf_train fixtures (oracle_kmeans_train): (name, metric, nlist, train_sample, niter, seed, init, duplicated)
+TRAIN_CASES = [("l2_pp", 0, 24, 0, 25, 1234, 1, False), ("l2_rand_stride", 0, 24, 3000, 20, 99, 0, False),
+               ("ip_pp", 1, 24, 0, 15, 5, 1, False), ("l2_subsample", 0, 8, 0, 10, 3, 1, False),
+               ("l2_rand_split", 0, 40, 0, 12, 17, 0, True)]
+
+
+def train_data(duplicated: bool):
+    """6000 x 48 rows around 24 centres, all from mt19937(11) U(-1,1) (tests/_data.py); duplicated: 750 base rows
+    repeated 8 times (random init then picks equal rows, so clusters empty out and are split)."""
+    from _data import mt19937_uniform
+
+    a = mt19937_uniform(24 * 48 + 6000 * 48 + 6000, seed=11)
+    cen = a[: 24 * 48].reshape(24, 48) * np.float32(3.0)
+    noise = a[24 * 48: 24 * 48 + 6000 * 48].reshape(6000, 48) * np.float32(0.5)
+    pick = (np.abs(a[-6000:]) * 24).astype(np.int64) % 24
+    x = np.ascontiguousarray((cen[pick] + noise).astype(np.float32))
+    if duplicated:
+        x = np.ascontiguousarray(np.repeat(x[:750], 8, axis=0))
+    return x
+
+
+def ivf_train_fixture():
+    out = {}
+    for name, metric, nlist, ts, niter, seed, init, dup in TRAIN_CASES:
+        cen, sizes = O.kmeans_train(train_data(dup), nlist, metric, ts, niter, seed, init)
+        out[name + "_cen"], out[name + "_sizes"] = cen, sizes
+    np.savez_compressed(HERE / "ivf_train.npz", **out)
+
+
 def main():
     (HERE / "sql_known_answers.json").write_text(json.dumps(sql_known_answers(), indent=1) + "\n")
+    ivf_train_fixture()
 
     flat = {}
     for (nv, nq, d, k, m) in FLAT_CASES:
@@ -140,4 +170,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["train"]:  # only the k-means fixture
+        ivf_train_fixture()
+    else:
+        main()

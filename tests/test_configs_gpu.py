@@ -186,6 +186,30 @@ def test_c3_ivf_nlist1024_nprobe32_d768_nq1024(gpu, c3_index, c3_oracle, form):
     index.form = 6
 
 
+def test_c3_ivf_train_c_abi_recall(gpu, c3_index):
+    """SURVEY §8f rank 4 at the C3 shape: the index built on centroids from the C ABI's training
+    (hipann_ivf_train_device, used by ivf_build / the bench) reaches a recall@10 at nprobe 32 no worse than the
+    same build with the r01-r03 torch k-means (ivf_build.kmeans_torch), against exact Flat on the same rows."""
+    import torch
+
+    import bench
+    from ivf_build import build_ivf_shard, flat_ground_truth, kmeans_torch
+
+    index, info, xb, xq_t, xq, _ = c3_index  # built through the C ABI's training
+    gt = flat_ground_truth(torch, gpu, 768, 0, xq_t, 10, len(xb), 0, 1, ivf_info_tensor=index)
+    _, I = _dev_search(index, xq_t, 10, torch)
+    r_hip = bench.recall_at(I, gt, 10)
+    xb_t = torch.from_numpy(xb).cuda()
+    index_t, _ = build_ivf_shard(torch, gpu, xb_t, 0, len(xb), 1024, 32, 0, 0, 1, centres_seed=1234,
+                                 train=kmeans_torch)
+    del xb_t
+    _, It = _dev_search(index_t, xq_t, 10, torch)
+    r_torch = bench.recall_at(It, gt, 10)
+    index_t.close()
+    assert r_hip >= r_torch - 0.005, (r_hip, r_torch)
+    assert r_hip >= 0.9, r_hip
+
+
 @pytest.mark.parametrize("form", [6, 5])
 def test_c3_request_k30(gpu, c3_index, oracle, form):
     """C3 shape with request_k = 30 (k = 10 plus 20 tombstones): sub-list slots and a 60-candidate rerank,

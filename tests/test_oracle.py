@@ -9,6 +9,7 @@ from __future__ import annotations
 import json
 import shutil
 import subprocess
+import sys
 from pathlib import Path
 
 import numpy as np
@@ -267,3 +268,53 @@ def test_sq8_code_div255_fma_step_is_ieee():
         e = rnd32(Fraction(float(code)) - Fraction(float(q0)) * 255)
         a = rnd32(Fraction(float(e)) * Fraction(float(r)) + Fraction(float(q0)))
         assert a == np.float32(code) / np.float32(255.0), code
+
+
+# ---- k-means restatement behind hipann_ivf_train (oracle_kmeans_train) ----
+def _train_cases():
+    sys.path.insert(0, str(Path(__file__).resolve().parent / "golden"))
+    from make_golden import TRAIN_CASES, train_data
+
+    return TRAIN_CASES, train_data
+
+
+def test_kmeans_oracle_matches_committed_fixture():
+    """The committed ivf_train.npz (make_golden.py) is reproduced bit for bit: the restatement is deterministic
+    given the seed (splitmix64 draws, integer D² weights, fp64 sums in row order)."""
+    from oracle import oracle as O
+
+    cases, train_data = _train_cases()
+    z = np.load(Path(__file__).resolve().parent / "golden" / "ivf_train.npz")
+    for name, metric, nlist, ts, niter, seed, init, dup in cases:
+        cen, sizes = O.kmeans_train(train_data(dup), nlist, metric, ts, niter, seed, init)
+        assert np.array_equal(cen, z[name + "_cen"]), name
+        assert np.array_equal(sizes, z[name + "_sizes"]), name
+
+
+def test_kmeans_oracle_semantics():
+    """Stride sample of train_sample rows (faiss_index.cpp:307-313): the cluster sizes sum to train_sample;
+    256 points per centroid at most; IP centroids are unit vectors (spherical); n < nlist is refused;
+    k-means++ on 24 well-separated centres puts one centroid next to each."""
+    from oracle import oracle as O
+
+    cases, train_data = _train_cases()
+    x = train_data(False)
+    _, sizes = O.kmeans_train(x, 24, 0, 3000, 5, 1, 1)
+    assert sizes.sum() == 3000
+    _, sizes = O.kmeans_train(x, 8, 0, 0, 5, 1, 1)
+    assert sizes.sum() == 256 * 8
+    cen, _ = O.kmeans_train(x, 24, 1, 0, 5, 1, 1)
+    assert np.allclose(np.linalg.norm(cen, axis=1), 1.0, atol=1e-6)
+    with pytest.raises(ValueError):
+        O.kmeans_train(x[:10], 24)
+    # Lloyd lowers the k-means objective from the k-means++ start, and most true centres get their own centroid
+    def inertia(c):
+        _, a = O.flat_search(c, x, 1, 0)
+        return float(((x - c[a[:, 0]]).astype(np.float64) ** 2).sum())
+
+    c0, _ = O.kmeans_train(x, 24, 0, 0, 0, 1234, 1)
+    cen, sizes = O.kmeans_train(x, 24, 0, 0, 25, 1234, 1)
+    assert inertia(cen) < inertia(c0) and (sizes > 0).all()
+    true = mt19937_uniform(24 * 48, seed=11).reshape(24, 48) * np.float32(3.0)
+    d = ((cen[:, None, :] - true[None, :, :]) ** 2).sum(-1)
+    assert len(set(d.argmin(1).tolist())) >= 22

@@ -6,7 +6,7 @@ cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
 TAG=${1:-r04}
-timeout -k 10 600 python -u -m pytest tests/test_request_k_gpu.py -x -v --timeout 180 --timeout-method thread > gpurun_out/${TAG}_reqk.log 2>&1 || { echo "request_k tests failed"; tail -80 gpurun_out/${TAG}_reqk.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_request_k_gpu.py tests/test_ivf_train_gpu.py -x -v --timeout 180 --timeout-method thread > gpurun_out/${TAG}_reqk.log 2>&1 || { echo "request_k tests failed"; tail -80 gpurun_out/${TAG}_reqk.log; exit 1; }
 tail -1 gpurun_out/${TAG}_reqk.log
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/${TAG}_gpu_suite.log 2>&1 || { echo "suite failed"; tail -80 gpurun_out/${TAG}_gpu_suite.log; exit 1; }
 tail -1 gpurun_out/${TAG}_gpu_suite.log
