@@ -336,6 +336,10 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
     if (kf > 0 && !exact) form = kFlatSplit3;
     const int k_user = k;
     if (exact) k = kf;
+    // the split scans' LDS lists hold fewer rows at 3 terms (k <= 38 at 8 waves): a longer list takes the fp32
+    // matrix cores (exact fp32 products, lists up to 64)
+    if ((form == kFlatSplit3 || form == kFlatSplit2) && k > flat_gemm_topk_bf_kmax(form == kFlatSplit3 ? 3 : 2))
+        form = kFlatFp32;
     if (form_override < 0) {
         ix.last_form = form;
         ix.last_kfilt = exact ? kf : 0;

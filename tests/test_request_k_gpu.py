@@ -71,8 +71,8 @@ def test_flat_list_kernels_request_k(gpu, oracle, k, nq):
     path = ix.last_search_path()
     if path["filter_k"]:
         assert path["form"] == ix.FORM_BF16_EXACT and path["filter_k"] >= k + 4, path
-    else:
-        assert path["form"] == ix.FORM_SPLIT3, path
+    else:  # the 3-term split, or the fp32 matrix cores where its LDS lists are too short (k > 38)
+        assert path["form"] in (ix.FORM_SPLIT3, ix.FORM_FP32), path
     if k <= 28:  # the list holds >= 32 at every block shape: exact
         assert path["filter_k"] >= k + 4, path
     ix.close()
