@@ -177,7 +177,11 @@ pub fn hip_multi_batch_distances(
 
 /// HBM-resident database for DiskProvider: register once at
 /// DiskProvider::open, then each lock-step BFS step ships only (id, query) pairs.
-pub struct HipDiskDb(*mut core::ffi::c_void);
+pub struct HipDiskDb {
+    h: *mut core::ffi::c_void,
+    n: usize,
+    dim: usize,
+}
 
 unsafe impl Send for HipDiskDb {}
 unsafe impl Sync for HipDiskDb {}
@@ -185,24 +189,38 @@ unsafe impl Sync for HipDiskDb {}
 impl HipDiskDb {
     /// fp32 rows (the .diskann vector segment, e.g. straight from the mmap).
     pub fn from_f32(vectors: &[f32], n: usize, dim: usize) -> Option<Self> {
-        if !is_hip_available() {
+        // the C side copies n × dim values: a shorter slice would be read out of bounds
+        if !is_hip_available() || dim == 0 || dim > i32::MAX as usize || vectors.len() < n.checked_mul(dim)? {
             return None;
         }
         let h = unsafe {
             diskann_hip_register_db(vectors.as_ptr() as *const _, n as i64, dim as i32, 0, std::ptr::null(), std::ptr::null())
         };
-        if h.is_null() { None } else { Some(HipDiskDb(h)) }
+        if h.is_null() { None } else { Some(HipDiskDb { h, n, dim }) }
     }
 
     /// SQ8 codes with the provider's per-dimension min / scale (provider.rs:25-38).
     pub fn from_sq8(codes: &[u8], n: usize, dim: usize, min: &[f32], scale: &[f32]) -> Option<Self> {
-        if !is_hip_available() {
+        if !is_hip_available()
+            || dim == 0
+            || dim > i32::MAX as usize
+            || codes.len() < n.checked_mul(dim)?
+            || min.len() < dim
+            || scale.len() < dim
+        {
             return None;
         }
         let h = unsafe {
             diskann_hip_register_db(codes.as_ptr() as *const _, n as i64, dim as i32, 1, min.as_ptr(), scale.as_ptr())
         };
-        if h.is_null() { None } else { Some(HipDiskDb(h)) }
+        if h.is_null() { None } else { Some(HipDiskDb { h, n, dim }) }
+    }
+
+    /// Slice shapes of a query batch: nq × dim queries, every count within the C ABI's i32.
+    fn batch_ok(&self, queries: &[f32], nq: usize, k: usize) -> bool {
+        nq <= i32::MAX as usize
+            && k <= i32::MAX as usize
+            && nq.checked_mul(self.dim).map_or(false, |m| queries.len() >= m)
     }
 
     /// out[i] = dist(queries[query_map[i]], db[ids[i]]) — replaces the gather + metal_multi_batch_distances
@@ -211,9 +229,19 @@ impl HipDiskDb {
         if ids.is_empty() {
             return true;
         }
+        // every index the kernel follows must be inside the slices it reads (ids < n, query_map < nq)
+        if !self.batch_ok(queries, nq, 0)
+            || ids.len() > i32::MAX as usize
+            || query_map.len() != ids.len()
+            || out.len() < ids.len()
+            || ids.iter().any(|&i| i as usize >= self.n)
+            || query_map.iter().any(|&q| q as usize >= nq)
+        {
+            return false;
+        }
         let ret = unsafe {
             diskann_hip_multi_batch_distances_ids(
-                self.0,
+                self.h,
                 queries.as_ptr(),
                 nq as i32,
                 ids.as_ptr(),
@@ -247,10 +275,11 @@ impl HipDiskDb {
     /// next to the registered vectors, once at DiskProvider::open.  After this, search_batch_resident runs
     /// the whole lock-step BFS of DiskProvider::search_batch (disk_provider.rs:470-652) on the GPU.
     pub fn register_graph(&self, adjacency: &[u32], max_degree: usize) -> bool {
-        if max_degree == 0 || adjacency.len() % max_degree != 0 {
+        // the C side copies n × max_degree ids (diskann.hip diskann_hip_register_graph)
+        if max_degree == 0 || max_degree > i32::MAX as usize || self.n.checked_mul(max_degree) != Some(adjacency.len()) {
             return false;
         }
-        unsafe { diskann_hip_register_graph(self.0, adjacency.as_ptr(), max_degree as i32) == 0 }
+        unsafe { diskann_hip_register_graph(self.h, adjacency.as_ptr(), max_degree as i32) == 0 }
     }
 
     /// DiskProvider::search_batch with the traversal on the GPU (one workgroup per query runs the reference's
@@ -268,13 +297,16 @@ impl HipDiskDb {
         if nq == 0 || k == 0 {
             return Some(vec![Vec::new(); nq]);
         }
+        if !self.batch_ok(queries_flat, nq, k) || l_search > i32::MAX as usize || entry_points.len() > i32::MAX as usize {
+            return None;
+        }
         let mut ids = vec![-1i64; nq * k];
         let mut dists = vec![f32::MAX; nq * k];
         let mut stats = [0i64; 4];
         let mut err = [0 as core::ffi::c_char; 256];
         let ret = unsafe {
             diskann_hip_search_batch_resident(
-                self.0,
+                self.h,
                 entry_points.as_ptr(),
                 entry_points.len() as i32,
                 queries_flat.as_ptr(),
@@ -312,13 +344,22 @@ impl HipDiskDb {
         if nq == 0 || k == 0 {
             return Some(vec![Vec::new(); nq]);
         }
+        if !self.batch_ok(queries_flat, nq, k)
+            || l_search > i32::MAX as usize
+            || entry_points.len() > i32::MAX as usize
+            || max_degree == 0
+            || max_degree > i32::MAX as usize
+            || self.n.checked_mul(max_degree) != Some(adjacency.len())
+        {
+            return None;
+        }
         let mut ids = vec![-1i64; nq * k];
         let mut dists = vec![f32::MAX; nq * k];
         let mut stats = [0i64; 4];
         let mut err = [0 as core::ffi::c_char; 256];
         let ret = unsafe {
             diskann_hip_search_batch(
-                self.0,
+                self.h,
                 adjacency.as_ptr(),
                 max_degree as i32,
                 entry_points.as_ptr(),
@@ -344,6 +385,6 @@ impl HipDiskDb {
 
 impl Drop for HipDiskDb {
     fn drop(&mut self) {
-        unsafe { diskann_hip_release_db(self.0) }
+        unsafe { diskann_hip_release_db(self.h) }
     }
 }

@@ -1817,9 +1817,11 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
     } else {
         E = eps * (qq + xmax2);
     }
-    // a non-finite bound (a query outside the fp16 form's safe scale range) is always re-run; sub-lists: the
+    // a non-finite bound (a query outside the fp16 form's safe scale range) is always re-run — unless the query
+    // has no candidate at all: empty probe lists, or the Flat bounded passes' overflowed query, which
+    // flat_cand_select already flagged (flagged holds nq entries: no query may be appended twice); sub-lists: the
     // kout-th distance must also clear the smallest full sub-list's k-th key
-    const bool flag = !(E <= 3.4e38f) || (ncand == k && !(dk < k16 - E)) ||
+    const bool flag = (ncand > 0 && !(E <= 3.4e38f)) || (ncand == k && !(dk < k16 - E)) ||
                       (sub && tsub < __builtin_inff() && !(dk < tsub - E));
     if (flag && lane == 0) flagged[atomicAdd(nflag, 1)] = (int)q;
     const float pad_d = IP ? -__builtin_inff() : __builtin_inff();

@@ -119,9 +119,12 @@ int hipann_last_search_path(void *index, int *form, int *filter_k, int *sublists
  * Device-resident variants (inputs and outputs already in HBM).  Used by the multi-GPU sharded
  * search (one process per GPU, partial top-k gathered over RCCL) and by bench.py, whose timed
  * region starts with the inputs resident.  `stream` is a hipStream_t (NULL = the default/null
- * stream, HIP's convention and PyTorch's default stream); the call is asynchronous on that stream:
+ * stream, HIP's convention and PyTorch's default stream).  IVF: the call is asynchronous on that stream —
  * it returns with its kernels still queued (no host synchronisation, the exact forms' flagged queries
- * included — they are re-run on the device).  Calls on one handle may use different streams: each call
+ * included: they are re-run on the device).  Flat: the exact forms (HIPANN_FLAT_FORM_SPLIT2_EXACT,
+ * HIPANN_FLAT_FORM_BF16_EXACT) synchronise the stream once per call to read the flagged-query count (twice
+ * when the bounded passes' candidate rerank ran), and a table's first exact-form search also builds its bf16
+ * image and bound; the other forms return with their kernels queued.  Calls on one handle may use different streams: each call
  * makes its stream wait for an event recorded at the end of the handle's previous call (the per-handle
  * scratch is reused), so they execute in the order they were issued.  The caller still orders its own
  * buffers (queries written / results read on other streams) with its own events.
