@@ -367,3 +367,28 @@ def test_flat_small_table_select_exact_ties(gpu, oracle, n, metric, k):
     Do, Io = oracle.flat_search(xb, xq, k, metric)
     assert np.array_equal(I, Io)
     assert np.array_equal(D, Do)
+
+
+def test_flat_ip_four_shards_in_process_c5_path(gpu, oracle):
+    """The extension's in-process multi-device handle (hipann_flat_create with devices [0, 0, 0, 0]): rows
+    sharded contiguously over four shards, each shard searched with its own stream and scratch (the bounded-pass
+    bf16 filter: 1M rows per shard), per-shard top-k gathered by peer copy onto shard 0's device and merged
+    (DESIGN §7).  C5's per-GPU path (Flat IP, d 768, batch 1024) at 1M rows per shard: ids equal a single-shard
+    index's exact fp32 form except in near-tie windows, and follow the oracle's parity rule on 12 queries."""
+    rng = np.random.default_rng(55)
+    n, d, nq = 4_000_000, 768, 1024
+    xb = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    xq = rng.uniform(-1, 1, (nq, d)).astype(np.float32)
+    ix4 = gpu.HipIndexFlat(d, 1, xb, devices=[0, 0, 0, 0])
+    D4, I4 = ix4.search(xq, 10)
+    assert ix4.rerank_fallbacks() == 0
+    ix4.close()
+    ix1 = gpu.HipIndexFlat(d, 1, xb)
+    ix1.form = ix1.FORM_FP32
+    D1, I1 = ix1.search(xq, 10)
+    ix1.close()
+    assert (I4 == I1).mean() >= 0.995
+    scale = np.sqrt(np.sum(xq.astype(np.float64) ** 2, 1))[:, None] * np.sqrt(d)
+    assert (np.abs(D4 - D1) <= 1e-5 * scale).all()
+    Do, Io = oracle.flat_search(xb, xq[:12], 10, 1)
+    check_topk_parity(xb, xq[:12], D4[:12], I4[:12], Do, Io, 1)
