@@ -119,7 +119,8 @@ def test_ivf_exact_forms_request_k(gpu, oracle, form, metric, k):
     if k <= 60:
         assert path == {"form": form, "filter_k": _ivf_kf(k), "sublists": 8}, path
     else:
-        assert path["filter_k"] == 0 and path["form"] == ix.FORM_SPLIT3, path
+        # the 3-term scan keeps 16-lists, so k = 64 takes the VALU decomposed scan (exact fp32 products)
+        assert path["filter_k"] == 0 and path["form"] == ix.FORM_DECOMPOSED_VALU, path
     Do, Io, Po = oracle.ivf_search(cen, off, ids, codes, xq, k, 8, metric)
     assert np.array_equal(ix.last_probes(len(xq)), Po)
     check_topk_parity(xb, xq, D, I, Do, Io, metric)
