@@ -46,6 +46,7 @@ sys.path.insert(0, str(ROOT))
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 FP32_MFMA_PEAK_TF = 157.3  # MI355X_MICROARCH.md: fp32 MFMA = fp32 vector peak
 BF16_MFMA_PEAK_TF = 16 * FP32_MFMA_PEAK_TF  # dense bf16 MFMA = 16x the fp32 matrix rate (~2.5 PF)
+I8_MFMA_PEAK_TOPS = 2 * BF16_MFMA_PEAK_TF  # dense int8 MFMA: the bf16 cycles at twice the K (MI355X_MICROARCH.md)
 METRIC = "queries/sec @ recall@10>=0.95, 10Mx768 fp32, batch=1024"
 
 
@@ -116,6 +117,10 @@ def compact_config(name, c):
         out["ids_eq_oracle_bfs"] = c["ids_equal_to_oracle_bfs"]
     if c.get("vs_k10") is not None:
         out["vs_k10"] = c["vs_k10"]
+    if isinstance(c.get("form_qps"), dict):  # the other forms: [QPS, fraction of ids equal to the reported form's]
+        out["form_qps"] = c["form_qps"]
+    if c.get("form") is not None and isinstance(c.get("roofline"), dict):
+        out["form"] = c["form"]
     if isinstance(c.get("path"), dict):
         p = c["path"]
         out["path"] = f"form{p.get('form')} kf{p.get('filter_k')}" + (f" sub{p['sublists']}" if p.get("sublists") else "")
@@ -421,7 +426,11 @@ def attach_traffic(roof, key, algorithmic_bytes):
 # ------------------------------------------------------------------------------------------------
 # Flat
 # ------------------------------------------------------------------------------------------------
-FLAT_FORMS = {4: ("flat_bf16_k64", 1, BF16_MFMA_PEAK_TF,
+FLAT_FORMS = {5: ("flat_bf16_k64<I8>", 1, I8_MFMA_PEAK_TOPS,
+                  "int8 MFMA (v_mfma_i32_16x16x64_i8, exact int32 sums), one int8 product per fp32 product over a "
+                  "tiled int8 image with per-row scales; the bounded passes and exact fp32 rerank of form 4 with a "
+                  "64-deep filter (the bound from the measured int8 residuals)"),
+              4: ("flat_bf16_k64", 1, BF16_MFMA_PEAK_TF,
                   "bf16 MFMA (v_mfma_f32_16x16x32_bf16), one bf16 product per fp32 product over a tiled bf16 image of "
                   "the rows; kernel_ms = the keys-mode seed pass + two bounded passes (rows with scan key <= a per-query "
                   "bound to candidate buffers) + the bound / select kernels; merge_ms = exact fp32 direct-form rerank "
@@ -483,12 +492,16 @@ def flat_config(args, torch, dist, hipann, rank, world, dev, n, d, nq, k, metric
         # computes each product once in bf16 as a certified filter (exact fp32 rerank), so it can pass that peak
         roof["frac_vs_fp32_peak"] = round(flops / (kern_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TF, 4)
         roof["fp32_peak"] = FP32_MFMA_PEAK_TF
-    if form == 4 and kern_ms > 0:
+    if form == 5 and kern_ms > 0:
+        roof["unit"] = "TOPS"
+        roof["frac_vs_bf16_peak"] = round(flops / (kern_ms * 1e-3) / 1e12 / BF16_MFMA_PEAK_TF, 4)
+    if form in (4, 5) and kern_ms > 0:
         # operand delivery of the bf16 scan (256 x 256 tiles): per 64-dim K-step the database tile (32 KB, LDS-DMA)
         # and the 256 queries' fragments (32 KB, straight into registers) through the vector-memory return path —
         # the unit the PMC pass finds busiest (profiles/r03/pmc_flat_k64.json)
         qm = 256 if nq >= 256 else 128 if nq >= 128 else 64
-        fill = -(-nq // qm) * -(-n_local // 256) * -(-d // 32) * (qm + 256) * 64.0
+        dpc = 64 if form == 5 else 32  # dims per 64-B chunk row of the image
+        fill = -(-nq // qm) * -(-n_local // 256) * -(-d // dpc) * (qm + 256) * 64.0
         roof["operand_delivery"] = {"bytes_per_launch_gb": round(fill / 1e9, 2),
                                     "achieved_tbps": round(fill / (kern_ms * 1e-3) / 1e12, 2),
                                     "flop_per_byte": round(2.0 * nq * n_local * d / fill, 1),
@@ -498,8 +511,8 @@ def flat_config(args, torch, dist, hipann, rank, world, dev, n, d, nq, k, metric
     out = {"workload": f"FAISS Flat {'L2' if metric == 0 else 'IP'}, {n}x{d} fp32, batch={nq}, k={k}",
            "value": round(nq * steps / el, 1), "unit": "queries/s", "ms_per_step": round(el * 1e3 / steps, 3),
            "steps": steps, "recall_at_10": None, "roofline": roof, "setup_s": round(setup_s, 1),
-           "rerank_fallbacks_total": index.rerank_fallbacks()}
-    if form in (3, 4):
+           "rerank_fallbacks_total": index.rerank_fallbacks(), "form": form}
+    if form in (3, 4, 5):
         out["precision"] = ("returned distances are fp32 " + ("direct-form Σ(q−x)²" if metric == 0 else "dot products")
                             + ", recomputed exactly for the kept candidates; FAISS CPU's BLAS path (nq >= 20) returns "
                             "max(0, ‖q‖²+‖x‖²−2q·x) from sgemm: the same ids (parity tests), distances equal up to the "
@@ -514,8 +527,8 @@ def flat_config(args, torch, dist, hipann, rank, world, dev, n, d, nq, k, metric
     # batch, and against the CPU oracle (FAISS BLAS-path restatement) on a query subset
     if alt_forms:
         alt = {}
-        for f in (0, 1, 3):
-            if f == form:
+        for f in (0, 1, 3, 4, 5):
+            if f == form or (f == 3 and n_local > 2_000_000):  # the 2-term split at 10M+: ~60 ms a step, skip
                 continue
             index.form = f
             step()
@@ -533,6 +546,7 @@ def flat_config(args, torch, dist, hipann, rank, world, dev, n, d, nq, k, metric
             Ia = Ia.cpu().numpy()
             alt[FLAT_FORMS[f][3]] = {"queries_per_s": round(nq * 2 / ea, 1), "kernel_ms": round(kms, 3),
                                      "ids_equal_to_reported_form": round(float((Ia == Ir).mean()), 6)}
+            out.setdefault("form_qps", {})[f"form{f}"] = [round(nq * 2 / ea, 1), round(float((Ia == Ir).mean()), 5)]
             if f == 0:  # exact fp32 products: the reference for recall
                 out["recall_at_10"] = round(recall_at(Ir, Ia, k), 6)
                 out["recall_reference"] = "the fp32-MFMA form's top-k on the same batch (exact fp32 products)"

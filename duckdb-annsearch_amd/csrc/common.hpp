@@ -74,7 +74,16 @@ constexpr int kFlatRerankKIP = 32;
 // kFlatBf16Exact (default): the same filter + rerank on ONE plain bf16 product per element (flat_bf16.hip:
 // a tiled bf16 image of the database built once; 32 kept per (split, query); the rerank's bound is the
 // Cauchy-Schwarz bound of the actual bf16 rounding residuals), failures re-run on kFlatSplit3.
-enum FlatForm : int { kFlatFp32 = 0, kFlatSplit3 = 1, kFlatSplit2 = 2, kFlatSplit2Exact = 3, kFlatBf16Exact = 4 };
+// kFlatI8Exact: the same bounded passes over a tiled int8 image (per-row scale max|x|/127) on the int8 matrix
+// cores (int32 sums: exact; twice the bf16 rate and half its bytes); the bound uses the int8 residuals.
+enum FlatForm : int {
+    kFlatFp32 = 0,
+    kFlatSplit3 = 1,
+    kFlatSplit2 = 2,
+    kFlatSplit2Exact = 3,
+    kFlatBf16Exact = 4,
+    kFlatI8Exact = 5
+};
 // rerank bound E = eps·(‖q‖² + max‖x‖²) of the 2-term split scans' filters
 constexpr float kSplit2Eps = 0x1p-12f;
 __host__ __device__ inline bool ivf_form_split(int f) { return f == kFormSplit3 || f == kFormSplit2; }

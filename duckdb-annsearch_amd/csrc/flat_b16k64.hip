@@ -22,6 +22,7 @@
 #include "runtime.hpp"
 #include "wave_topk.hpp"
 
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 #include <utility>
@@ -31,6 +32,7 @@ namespace hipann {
 typedef __bf16 k64_b16x8 __attribute__((ext_vector_type(8)));
 typedef float k64_f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned k64_u32x4 __attribute__((ext_vector_type(4)));
+typedef int k64_i32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void k64_lds_void;
 
 constexpr int K64_TN = 256;               // database rows per tile
@@ -109,13 +111,18 @@ __device__ __forceinline__ void k64_epilogue_row(const k64_f32x4 (&acc)[2][16], 
 // with margin, flat_keys_kth / flat_cand_bound).
 // KEYS (the sample pass that seeds the bound): no filter, every key of the block's tiles goes to
 // cand_d[q·N + row] (a dense nq × N key matrix over the N sample rows; bound, cand_i, cand_n unused).
-template <bool L2M, bool KEYS>
+// I8 (form kFlatI8Exact): the same tiles and schedule over an int8 image (a 16-B unit = 16 dims, so one 64-B
+// chunk row covers 64 dims and a K-step 128) on v_mfma_i32_16x16x64_i8 — twice the dims per instruction and
+// per byte moved.  The int32 sums are exact (|acc| <= d·127² < 2^24 for d <= 1040) and live in the float
+// accumulators' registers bit for bit until the tile's epilogue turns them into q·x = acc·s_q·s_x with the
+// per-query / per-row scales (qscale / xscale); everything after that is the bf16 path's.
+template <bool L2M, bool KEYS, bool I8 = false>
 __global__ void __launch_bounds__(64 * K64_W, 1)
 flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm, int64_t nq,
               const k64_u32x4 *__restrict__ Xt, const float *xnorm, int64_t N, int nk, int nqt, int nsplit,
               int64_t tiles_per_split, int64_t tile_begin, int64_t tile_end, const float *__restrict__ bound,
               float *__restrict__ cand_d, int *__restrict__ cand_i, int *__restrict__ cand_n, int cap,
-              int resume) {
+              int resume, const float *__restrict__ qscale, const float *xscale) {
     constexpr int NB = K64_NB;
     extern __shared__ __attribute__((aligned(16))) k64_u32x4 smem_k64[];
 
@@ -158,6 +165,15 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
                 cth[mb][i] = L2M ? qn - thr : -2.f * thr;
             }
         }
+    // int8: 2·s_q of the lane's accumulator query rows (the 2 of s = 2·q·x − ‖x‖² folded in)
+    float csq[2][4];
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int64_t q = q0w + 16 * mb + i;
+            csq[mb][i] = I8 && q < nq ? 2.f * qscale[q] : 2.f;
+        }
     const int64_t cq = (int64_t)nsplit * cap;  // buffer stride between consecutive queries
     const int64_t cbase = ((q0 + 32 * wave) * nsplit + split) * (int64_t)cap;
 
@@ -197,12 +213,13 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
         for (int jb = 0; jb < 16; ++jb) acc[mb][jb] = (k64_f32x4){0.f, 0.f, 0.f, 0.f};
     // ‖x‖² of tile tt, row 64·j + lane in xr[j] (0 for IP)
     float xr[4] = {0.f, 0.f, 0.f, 0.f};
+    float xsc[4] = {1.f, 1.f, 1.f, 1.f};  // int8: the tile's row scales, row 64·j + lane in xsc[j]
     auto load_xn = [&](int64_t tt) {
-        if constexpr (!L2M) return;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int64_t x = tt * K64_TN + 64 * j + lane;
-            xr[j] = xnorm[x < N ? x : N - 1];  // rows past N: +inf at the use (G > 0: N > 0)
+            if constexpr (L2M) xr[j] = xnorm[x < N ? x : N - 1];  // rows past N: +inf at the use (G > 0: N > 0)
+            if constexpr (I8) xsc[j] = xscale[x < N ? x : N - 1];
         }
     };
     // Per K-step g the vector-memory ops go out as ‖x‖²(g) (L2), A(g+1), B(g+3); at its end A(g+1) and B(g+1)
@@ -250,8 +267,18 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
             for (int jb = 0; jb < 16; ++jb) bf[jb] = __builtin_bit_cast(k64_b16x8, Bc[16 * jb]);
 #pragma unroll
             for (int jb = 0; jb < 16; ++jb) {
-                acc[0][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[jb], acc[0][jb], 0, 0, 0);
-                acc[1][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf[jb], acc[1][jb], 0, 0, 0);
+                if constexpr (I8) {  // int32 sums carried in the accumulators' registers, bit for bit
+                    const k64_i32x4 ai0 = __builtin_bit_cast(k64_i32x4, a0);
+                    const k64_i32x4 ai1 = __builtin_bit_cast(k64_i32x4, a1);
+                    const k64_i32x4 bi = __builtin_bit_cast(k64_i32x4, bf[jb]);
+                    acc[0][jb] = __builtin_bit_cast(k64_f32x4, __builtin_amdgcn_mfma_i32_16x16x64_i8(
+                                                                   ai0, bi, __builtin_bit_cast(k64_i32x4, acc[0][jb]), 0, 0, 0));
+                    acc[1][jb] = __builtin_bit_cast(k64_f32x4, __builtin_amdgcn_mfma_i32_16x16x64_i8(
+                                                                   ai1, bi, __builtin_bit_cast(k64_i32x4, acc[1][jb]), 0, 0, 0));
+                } else {
+                    acc[0][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[jb], acc[0][jb], 0, 0, 0);
+                    acc[1][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf[jb], acc[1][jb], 0, 0, 0);
+                }
             }
             if (h == 1) issue_b(clampg(g + 3), stage < 2 ? stage + 3 : stage - 2);
             // schedule (same region): four LDS reads ahead, then one read per MFMA pair, one vector-memory op per
@@ -279,10 +306,19 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
             for (int jb = 0; jb < 16; ++jb) {
                 const float xs = __shfl(xr[jb >> 2], 16 * (jb & 3) + m16);
                 const float xv = x0 + 16 * jb + m16 < N ? xs : __builtin_inff();
+                if constexpr (I8) {
+                    const float sx = __shfl(xsc[jb >> 2], 16 * (jb & 3) + m16);
 #pragma unroll
-                for (int mb = 0; mb < 2; ++mb)
+                    for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) acc[mb][jb][i] = fmaf(2.f, acc[mb][jb][i], -xv);
+                        for (int i = 0; i < 4; ++i)
+                            acc[mb][jb][i] = fmaf(csq[mb][i] * sx, (float)__builtin_bit_cast(int, acc[mb][jb][i]), -xv);
+                } else {
+#pragma unroll
+                    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) acc[mb][jb][i] = fmaf(2.f, acc[mb][jb][i], -xv);
+                }
             }
             if constexpr (KEYS) {
                 // every key (L2: ‖q‖² − s clamped at 0; IP: −s/2) into the dense key matrix
@@ -451,22 +487,114 @@ void launch_flat_keys_kth(const float *keys, int S, int64_t nq, int k, float *bo
 
 bool flat_bf16_k64_supported(int nk, int k) { return nk % 2 == 0 && k <= 64; }
 
+// ---- int8 image (form kFlatI8Exact) ------------------------------------------------------------------
+// Per row: s = max|x| / 127 and x̂ = clamp(rint(x / s), ±127) (s = 0: a zero row); the tiled image has the bf16
+// image's geometry with 64 dims per 64-B chunk row (16-B unit c of chunk kc = dims 64·kc + 16c .. +15), the chunk
+// count rounded up to even (the K-step is two chunks) and zero-filled.
+constexpr int I8_KC = 64;
+int flat_i8_nk(int d) {
+    const int nk = (d + I8_KC - 1) / I8_KC;
+    return nk + (nk & 1);
+}
+size_t flat_i8_img_bytes(int64_t n, int d, int R) {
+    return (size_t)ceil_div(std::max<int64_t>(n, 1), R) * flat_i8_nk(d) * R * 4 * 16;
+}
+__device__ __forceinline__ int i8_quant(float x, float s) {
+    return s > 0.f ? (int)fminf(fmaxf(rintf(x / s), -127.f), 127.f) : 0;
+}
+
+// one wave per row: scale[row] = max|x| / 127, resid[row] = ‖x − s·x̂‖ (×1.0001: the fp32 sum of d exact-ish squares)
+__global__ void __launch_bounds__(256) i8_row_scale(const float *__restrict__ X, int64_t n, int d,
+                                                    float *__restrict__ scale, float *__restrict__ resid) {
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= n) return;
+    const int lane = threadIdx.x & 63;
+    const float *x = X + row * (int64_t)d;
+    float m = 0.f;
+    for (int e = lane; e < d; e += 64) m = fmaxf(m, fabsf(x[e]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    const float s = m > 0.f && m < 3.0e38f ? m / 127.f : 0.f;
+    float r2 = 0.f;
+    for (int e = lane; e < d; e += 64) {
+        const float r = x[e] - s * (float)i8_quant(x[e], s);
+        r2 = fmaf(r, r, r2);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) r2 += __shfl_xor(r2, o);
+    if (lane == 0) {
+        scale[row] = s;
+        resid[row] = m < 3.0e38f ? sqrtf(r2) * 1.0001f : __builtin_inff();  // non-finite rows: no bound
+    }
+}
+
+// unit u = ((t·nk + kc)·4 + c)·R + (row ^ 2c), one thread per unit (16 int8 values)
+__global__ void __launch_bounds__(256) i8_tile_rows(const float *__restrict__ X, const float *__restrict__ scale,
+                                                    int64_t n, int d, int R, int nk, int64_t total,
+                                                    uint4 *__restrict__ out) {
+    const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (u >= total) return;
+    const int rr = (int)(u % R);
+    int64_t rest = u / R;
+    const int c = (int)(rest & 3);
+    rest >>= 2;
+    const int kc = (int)(rest % nk);
+    const int64_t t = rest / nk;
+    const int row = rr ^ (c << 1);
+    const int64_t grow = t * R + row;
+    const int dim0 = kc * I8_KC + 16 * c;
+    unsigned w[4] = {0u, 0u, 0u, 0u};
+    if (grow < n) {
+        const float s = scale[grow];
+        const float *x = X + grow * (int64_t)d;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int v = dim0 + i < d ? i8_quant(x[dim0 + i], s) : 0;
+            w[i >> 2] |= ((unsigned)v & 0xffu) << (8 * (i & 3));
+        }
+    }
+    out[u] = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+void launch_i8_row_scale(const float *X, int64_t n, int d, float *scale, float *resid, hipStream_t st) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(i8_row_scale, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, st, X, n, d, scale, resid);
+    HIPANN_CHECK(hipGetLastError());
+}
+
+void launch_i8_tile_rows(const float *X, const float *scale, int64_t n, int d, int R, void *out, hipStream_t st) {
+    const int nk = flat_i8_nk(d);
+    const int64_t total = ceil_div(std::max<int64_t>(n, 1), R) * nk * R * 4;
+    hipLaunchKernelGGL(i8_tile_rows, dim3((unsigned)ceil_div(total, 256)), dim3(256), 0, st, X, scale, n, d, R, nk,
+                       total, static_cast<uint4 *>(out));
+    HIPANN_CHECK(hipGetLastError());
+}
+
 
 void launch_flat_bf16_k64(const void *qimg, const float *qn, int64_t nq, const void *ximg, const float *xn, int64_t N,
                           int nk, int metric, int nqt, int nsplit, int64_t tiles_per_split, int64_t tile_begin,
                           int64_t tile_end, const float *bound, float *cand_d, int *cand_i, int *cand_n, int cap,
-                          bool resume, bool keys, hipStream_t st) {
+                          bool resume, bool keys, hipStream_t st, const float *qscale, const float *xscale) {
     HIPANN_REQUIRE(nk % 2 == 0 && cand_d && (keys || (bound && cand_i && cand_n && cap > 0)),
                    "flat_bf16_k64: bad arguments");
+    HIPANN_REQUIRE(!qscale == !xscale, "flat_bf16_k64: int8 needs both scales");
     HIPANN_REQUIRE((int64_t)nqt * nsplit < 0x7fffffff, "grid too large");
     dim3 grid((unsigned)(nqt * nsplit)), block(64 * K64_W);
     const k64_u32x4 *qa = static_cast<const k64_u32x4 *>(qimg);
     const k64_u32x4 *xa = static_cast<const k64_u32x4 *>(ximg);
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, grid, block, K64_LDS, st, qa, qn, nq, xa, xn, N, nk, nqt, nsplit, tiles_per_split,
-                           tile_begin, tile_end, bound, cand_d, cand_i, cand_n, cap, resume ? 1 : 0);
+                           tile_begin, tile_end, bound, cand_d, cand_i, cand_n, cap, resume ? 1 : 0, qscale, xscale);
     };
-    if (keys) {
+    if (qscale) {
+        if (keys) {
+            if (metric == kL2) go(flat_bf16_k64<true, true, true>);
+            else go(flat_bf16_k64<false, true, true>);
+        } else {
+            if (metric == kL2) go(flat_bf16_k64<true, false, true>);
+            else go(flat_bf16_k64<false, false, true>);
+        }
+    } else if (keys) {
         if (metric == kL2) go(flat_bf16_k64<true, true>);
         else go(flat_bf16_k64<false, true>);
     } else {

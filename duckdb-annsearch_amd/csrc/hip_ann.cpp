@@ -123,8 +123,11 @@ void shard_append(FlatShard &sh, int d, int metric, const float *x_host, const f
     HIPANN_CHECK(hipStreamSynchronize(sh.stream));
     sh.n = need;
     sh.xmax2 = -1.f;  // new rows: the exact form's bound is recomputed
-    sh.xb16_ok = false;  // and the bf16 image rebuilt
+    sh.xb16_ok = false;  // and the bf16 / int8 images rebuilt
     sh.xb16.release();
+    sh.xi8_ok = false;
+    sh.xi8.release();
+    sh.xscale.release();
 }
 
 }  // namespace
@@ -322,7 +325,17 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
     // the all-candidate rerank, certified against the pass bound.  Otherwise: the 3-term split (fp32-level).
     int kf = 0;
     bool bounded = false;
-    if (form == kFlatSplit2Exact || form == kFlatBf16Exact) {
+    // kFlatI8Exact runs only as the bounded passes (256-query blocks, >= 512K rows, d <= 1024 so the int32 sums
+    // convert to fp32 exactly); elsewhere the bf16 image's paths
+    if (form == kFlatI8Exact &&
+        !(flat_bf16_resumable(nq, d, 64) && seed_env && sh.n >= 8 * 65536 && d <= 1024))
+        form = kFlatBf16Exact;
+    if (form == kFlatI8Exact) {
+        // the int8 rounding bound is ≈3× the bf16 one (E ≈ 4.4 against 1.3-1.7 at 768 dims on U(-1, 1)): a
+        // 64-deep filter keeps the 10th distance clear of it (the 10th-to-32nd gap is ≈5, the 10th-to-64th ≈8)
+        kf = 64;
+        bounded = true;
+    } else if (form == kFlatSplit2Exact || form == kFlatBf16Exact) {
         const int base = metric == kIP || form == kFlatBf16Exact ? kFlatRerankKIP : kRerankK;
         kf = kout <= kRerankMaxK ? base : std::min(64, std::max(base, 2 * kout));
         if (form == kFlatBf16Exact) {
@@ -353,9 +366,30 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
     int cr_nsplit = 0, cr_cap = 0;
     // the exact forms' max ‖x‖² (cached; its first computation uses sh.nflag as scratch, so before any flags)
     const float xmax2 = exact ? flat_xmax2(sh, d, st) : 0.f;
-    if (form == kFlatBf16Exact) {
+    const bool i8 = form == kFlatI8Exact;
+    float rxmax = sh.bf16_rxmax;  // the rerank bound's row term of the form that filtered
+    if (i8) {
+        // one int8 product per element (int32 sums) over a tiled int8 image with per-row scales, built once
+        if (!sh.xi8_ok) {
+            sh.xi8.ensure(flat_i8_img_bytes(sh.n, d, flat_bf16_tile_rows()), sh.device);
+            sh.xscale.ensure(sizeof(float) * (size_t)sh.n, sh.device);
+            sh.tmpnorm.ensure(sizeof(float) * (size_t)sh.n, sh.device);
+            launch_i8_row_scale(sh.xb, sh.n, d, sh.xscale.get<float>(), sh.tmpnorm.get<float>(), st);
+            launch_i8_tile_rows(sh.xb, sh.xscale.get<float>(), sh.n, d, flat_bf16_tile_rows(), sh.xi8.p, st);
+            sh.nflag.ensure(sizeof(int), sh.device);
+            launch_ivf_max_norm(sh.tmpnorm.get<float>(), sh.n, sh.nflag.get<unsigned>(), st);  // max of non-negative
+            unsigned bits = 0;
+            HIPANN_CHECK(hipMemcpyAsync(&bits, sh.nflag.p, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+            HIPANN_CHECK(hipStreamSynchronize(st));
+            sh.tmpnorm.release();
+            std::memcpy(&sh.i8_rxmax, &bits, sizeof(float));
+            sh.xi8_ok = true;
+        }
+        rxmax = sh.i8_rxmax;
+    }
+    if (form == kFlatBf16Exact || i8) {
         // one plain bf16 product per element over the tiled bf16 image (flat_bf16.hip), built once
-        if (!sh.xb16_ok) {
+        if (!i8 && !sh.xb16_ok) {
             sh.xb16.ensure(flat_bf16_img_bytes(sh.n, d, flat_bf16_tile_rows()), sh.device);
             launch_b16_tile_rows(sh.xb, sh.n, d, flat_bf16_tile_rows(), sh.xb16.p, st);
             // the rows' largest bf16 rounding residual ‖x̂ − x‖ (the rerank's bound)
@@ -374,6 +408,10 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
         }
         const int W = flat_bf16_waves(nq);
         const int64_t nqt = ceil_div(nq, 32 * W);
+        // the scan's operand images, chunk count and (int8) scales
+        const void *ximg = i8 ? sh.xi8.p : sh.xb16.p;
+        const int nk = i8 ? flat_i8_nk(d) : (int)ceil_div(d, 32);
+        const float *qsc = nullptr, *xsc = i8 ? sh.xscale.get<float>() : nullptr;
         const int64_t ntiles = ceil_div(sh.n, flat_bf16_tile_rows());
         static const int64_t blocks_env = [] {
             const char *e = std::getenv("HIPANN_FLAT_BF16_BLOCKS");  // A/B: target grid size
@@ -388,7 +426,7 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
         HIPANN_REQUIRE(nqt * nsplit < (int64_t)0x7fffffff, "grid too large");
         sh.part_d.ensure((size_t)nsplit * nq * k * sizeof(float), sh.device);
         sh.part_i.ensure((size_t)nsplit * nq * k * sizeof(int), sh.device);
-        sh.qimg.ensure(flat_bf16_img_bytes(nq, d, 32 * W), sh.device);
+        sh.qimg.ensure(i8 ? flat_i8_img_bytes(nq, d, 32 * W) : flat_bf16_img_bytes(nq, d, 32 * W), sh.device);
         // seed bound (large tables): the k-th best key of each query over a sample of the first rows.  Bounded
         // passes (below): the sample's keys from the same kernel in its keys mode (a dense nq × S matrix, one
         // tile per block) and their k-th order statistic (flat_keys_kth); otherwise the 32-dim list kernel over
@@ -418,15 +456,23 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
             sh.seed.ensure(sizeof(float) * (size_t)nq, sh.device);
             sh.cand.ensure(std::max(ncell * ((size_t)cap * 8 + 4), (size_t)std::min(nq, seed_qc) * sample * sizeof(float)),
                            sh.device);
-            launch_b16_tile_rows(xq, nq, d, 32 * W, sh.qimg.p, st);
-            const size_t qtile_bytes = flat_bf16_img_bytes(32 * W, d, 32 * W);
+            if (i8) {  // the queries' scales, residuals (the rerank's query term) and int8 image
+                sh.qscale.ensure(sizeof(float) * (size_t)nq, sh.device);
+                sh.qres.ensure(sizeof(float) * (size_t)nq, sh.device);
+                launch_i8_row_scale(xq, nq, d, sh.qscale.get<float>(), sh.qres.get<float>(), st);
+                launch_i8_tile_rows(xq, sh.qscale.get<float>(), nq, d, 32 * W, sh.qimg.p, st);
+                qsc = sh.qscale.get<float>();
+            } else {
+                launch_b16_tile_rows(xq, nq, d, 32 * W, sh.qimg.p, st);
+            }
+            const size_t qtile_bytes = i8 ? flat_i8_img_bytes(32 * W, d, 32 * W) : flat_bf16_img_bytes(32 * W, d, 32 * W);
             for (int64_t c0 = 0; c0 < nq; c0 += seed_qc) {
                 const int64_t cn = std::min(seed_qc, nq - c0);
                 launch_flat_bf16_k64(static_cast<const char *>(sh.qimg.p) + (size_t)(c0 / (32 * W)) * qtile_bytes,
-                                     qn ? qn + c0 : nullptr, cn, sh.xb16.p, sh.xn.get<float>(), sample,
-                                     (int)ceil_div(d, 32), metric, (int)ceil_div(cn, 32 * W),
-                                     (int)(sample / flat_bf16_tile_rows()), 1, 0, 1, nullptr, sh.cand.get<float>(), nullptr,
-                                     nullptr, 0, false, true, st);
+                                     qn ? qn + c0 : nullptr, cn, ximg, sh.xn.get<float>(), sample, nk, metric,
+                                     (int)ceil_div(cn, 32 * W), (int)(sample / flat_bf16_tile_rows()), 1, 0, 1, nullptr,
+                                     sh.cand.get<float>(), nullptr, nullptr, 0, false, true, st, qsc ? qsc + c0 : nullptr,
+                                     xsc);
                 launch_flat_keys_kth(sh.cand.get<float>(), (int)sample, cn, k, sh.seed.get<float>() + c0, st);
             }
         } else if (seeded) {
@@ -451,15 +497,14 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
             float *cd = sh.cand.get<float>();
             int *ci = reinterpret_cast<int *>(cd + ncell * cap);
             int *cn = ci + ncell * cap;
-            const int nk = (int)ceil_div(d, 32);
             float *bound = sh.seed.get<float>();
             if (tps_a >= 1) {
-                launch_flat_bf16_k64(sh.qimg.p, qn, nq, sh.xb16.p, sh.xn.get<float>(), sh.n, nk, metric, (int)nqt,
-                                     (int)nsplit, tps, 0, tps_a, bound, cd, ci, cn, cap, false, false, st);
+                launch_flat_bf16_k64(sh.qimg.p, qn, nq, ximg, sh.xn.get<float>(), sh.n, nk, metric, (int)nqt,
+                                     (int)nsplit, tps, 0, tps_a, bound, cd, ci, cn, cap, false, false, st, qsc, xsc);
                 launch_flat_cand_bound(cd, cn, (int)nsplit, cap, nq, k, bound, st);
             }
-            launch_flat_bf16_k64(sh.qimg.p, qn, nq, sh.xb16.p, sh.xn.get<float>(), sh.n, nk, metric, (int)nqt,
-                                 (int)nsplit, tps, tps_a, tps, bound, cd, ci, cn, cap, tps_a >= 1, false, st);
+            launch_flat_bf16_k64(sh.qimg.p, qn, nq, ximg, sh.xn.get<float>(), sh.n, nk, metric, (int)nqt,
+                                 (int)nsplit, tps, tps_a, tps, bound, cd, ci, cn, cap, tps_a >= 1, false, st, qsc, xsc);
             sh.nflag.ensure(sizeof(int), sh.device);
             sh.flagged.ensure(sizeof(int) * (size_t)nq, sh.device);
             HIPANN_CHECK(hipMemsetAsync(sh.nflag.p, 0, sizeof(int), st));
@@ -532,9 +577,11 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
     }
     {
         ScopedTiming t(ix.timer_merge, st);
+        // (int8: the row term and each query's own residual from the int8 images; qres makes the rerank read them)
         launch_ivf_rerank(sh.part_d.get<float>(), sh.part_i.get<int>(), nullptr, (int)nsplit, nq, k, kout, metric, xq,
                           sh.xb, d, nullptr, sh.n, sh.label_offset, xmax2, D, I, sh.nflag.get<int>(),
-                          sh.flagged.get<int>(), st, kSplit2Eps, form == kFlatBf16Exact ? sh.bf16_rxmax : -1.f);
+                          sh.flagged.get<int>(), st, kSplit2Eps, form == kFlatBf16Exact || i8 ? rxmax : -1.f,
+                          i8 ? sh.qres.get<float>() : nullptr);
     }
     int nf = 0;
     HIPANN_CHECK(hipMemcpyAsync(&nf, sh.nflag.p, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -556,9 +603,10 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
         {
             ScopedTiming t(ix.timer_merge, st);
             launch_flat_cand_rerank(fl, nf, cr_d, cr_i, cr_n, cr_nsplit, cr_cap, cr_bound, xq, sh.xb, d, sh.n,
-                                    sh.label_offset, xmax2, sh.bf16_rxmax, metric, kout, sh.crd.get<float>(),
+                                    sh.label_offset, xmax2, rxmax, metric, kout, sh.crd.get<float>(),
                                     sh.cri.get<long long>(), sh.covf.get<int>(), D, I, sh.nflag2.get<int>(),
-                                    sh.flagged2.get<int>(), st, dbg ? sh.tmpnorm.get<float>() : nullptr);
+                                    sh.flagged2.get<int>(), st, dbg ? sh.tmpnorm.get<float>() : nullptr,
+                                    i8 ? sh.qres.get<float>() : nullptr);
         }
         ix.cand_reranked += nf;
         const int nf1 = nf;
@@ -885,7 +933,7 @@ int hipann_metric(void *h) { return h ? static_cast<IndexBase *>(h)->metric : -1
 int64_t hipann_memory_bytes(void *h) { return h ? static_cast<IndexBase *>(h)->memory_bytes() : -1; }
 
 int hipann_flat_set_form(void *h, int form) {
-    if (!h || form < kFlatFp32 || form > kFlatBf16Exact) return -1;
+    if (!h || form < kFlatFp32 || form > kFlatI8Exact) return -1;
     auto *ix = static_cast<IndexBase *>(h);
     if (ix->kind != Kind::Flat) return -1;
     auto *fx = static_cast<FlatIndex *>(ix);

@@ -1910,7 +1910,8 @@ flat_cand_rerank_final(const int *__restrict__ flagged, int P, const float *__re
                        const float *__restrict__ Q, int d, float xmax2, float rxmax, int kout,
                        const float *__restrict__ part_d, const long long *__restrict__ part_i,
                        const int *__restrict__ ovf, float *__restrict__ D, int64_t *__restrict__ I,
-                       int *__restrict__ nflag2, int *__restrict__ flagged2, float *__restrict__ dbg) {
+                       int *__restrict__ nflag2, int *__restrict__ flagged2, float *__restrict__ dbg,
+                       const float *__restrict__ qres) {
     const int f = blockIdx.x, lane = threadIdx.x;
     const int64_t q = flagged[f];
     bool over = false;
@@ -1933,8 +1934,9 @@ flat_cand_rerank_final(const int *__restrict__ flagged, int P, const float *__re
         qq += __shfl_xor(qq, o);
         rq2 += __shfl_xor(rq2, o);
     }
-    const float qn = sqrtf(qq), rq = sqrtf(rq2), xh = sqrtf(xmax2) + rxmax;
-    const float g = (float)d * 0x1p-24f;
+    // qres (the int8 form): the query's own int8 residual, and 2d terms of accumulation margin as the first rerank
+    const float qn = sqrtf(qq), rq = qres ? qres[q] : sqrtf(rq2), xh = sqrtf(xmax2) + rxmax;
+    const float g = (float)(qres ? 2 * d : d) * 0x1p-24f;
     const float eip = qn * rxmax + rq * xh + g * (qn + rq) * xh;
     const float T = bound[q];
     // + 2^-20 of the key scale: the pass compared s against ‖q‖² − T (IP: −2T) in fp32
@@ -1962,7 +1964,7 @@ void launch_flat_cand_rerank(const int *flagged, int nf, const float *cand_d, co
                              int nsplit, int cap, const float *bound, const float *Q, const float *X, int d,
                              int64_t nrows, int64_t label_offset, float xmax2, float rxmax, int metric, int kout,
                              float *part_d, long long *part_i, int *ovf, float *D, int64_t *I, int *nflag2,
-                             int *flagged2, hipStream_t st, float *dbg) {
+                             int *flagged2, hipStream_t st, float *dbg, const float *qres) {
     if (nf <= 0) return;
     HIPANN_REQUIRE(kout >= 1 && kout <= 64 && nsplit >= 1 && cap >= 1, "flat cand rerank: bad arguments");
     const int P = std::min(kCandRerankParts, nsplit);
@@ -1971,12 +1973,12 @@ void launch_flat_cand_rerank(const int *flagged, int nf, const float *cand_d, co
         hipLaunchKernelGGL(flat_cand_rerank_part<true>, g1, dim3(256), 0, st, flagged, cand_d, cand_i, cand_n, nsplit,
                            cap, Q, X, d, nrows, label_offset, kout, part_d, part_i, ovf);
         hipLaunchKernelGGL(flat_cand_rerank_final<true>, dim3((unsigned)nf), dim3(64), 0, st, flagged, P, bound, Q, d,
-                           xmax2, rxmax, kout, part_d, part_i, ovf, D, I, nflag2, flagged2, dbg);
+                           xmax2, rxmax, kout, part_d, part_i, ovf, D, I, nflag2, flagged2, dbg, qres);
     } else {
         hipLaunchKernelGGL(flat_cand_rerank_part<false>, g1, dim3(256), 0, st, flagged, cand_d, cand_i, cand_n, nsplit,
                            cap, Q, X, d, nrows, label_offset, kout, part_d, part_i, ovf);
         hipLaunchKernelGGL(flat_cand_rerank_final<false>, dim3((unsigned)nf), dim3(64), 0, st, flagged, P, bound, Q, d,
-                           xmax2, rxmax, kout, part_d, part_i, ovf, D, I, nflag2, flagged2, dbg);
+                           xmax2, rxmax, kout, part_d, part_i, ovf, D, I, nflag2, flagged2, dbg, qres);
     }
     HIPANN_CHECK(hipGetLastError());
 }

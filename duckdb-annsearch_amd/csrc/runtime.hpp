@@ -196,6 +196,11 @@ struct FlatShard {
     DevBuf cand;  // bounded passes: per-(query, split) candidate buffers and counts
     bool xb16_ok = false;
     float bf16_rxmax = 0.f;  // max over rows of ‖bf16(x) − x‖ (the rerank's bound)
+    // kFlatI8Exact: tiled int8 image, per-row scales, max row residual ‖x − s·x̂‖; the batch's query scales and
+    // residuals (the rerank's query term)
+    DevBuf xi8, xscale, qscale, qres;
+    bool xi8_ok = false;
+    float i8_rxmax = 0.f;
     StreamFence fence;       // cross-stream ordering of this shard's calls
 };
 
@@ -347,7 +352,7 @@ void launch_flat_cand_rerank(const int *flagged, int nf, const float *cand_d, co
                              int nsplit, int cap, const float *bound, const float *Q, const float *X, int d,
                              int64_t nrows, int64_t label_offset, float xmax2, float rxmax, int metric, int kout,
                              float *part_d, long long *part_i, int *ovf, float *D, int64_t *I, int *nflag2,
-                             int *flagged2, hipStream_t st, float *dbg = nullptr);
+                             int *flagged2, hipStream_t st, float *dbg = nullptr, const float *qres = nullptr);
 int flat_cand_rerank_parts(int nsplit);
 void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int nprobe, int64_t nq, int k, int kout,
                        int metric, const float *Q, const float *codes, int d, const int64_t *ids, int64_t nrows,
@@ -390,7 +395,14 @@ bool flat_bf16_resumable(int64_t nq, int d, int k);
 void launch_flat_bf16_k64(const void *qimg, const float *qn, int64_t nq, const void *ximg, const float *xn, int64_t N,
                           int nk, int metric, int nqt, int nsplit, int64_t tiles_per_split, int64_t tile_begin,
                           int64_t tile_end, const float *bound, float *cand_d, int *cand_i, int *cand_n, int cap,
-                          bool resume, bool keys, hipStream_t st);
+                          bool resume, bool keys, hipStream_t st, const float *qscale = nullptr,
+                          const float *xscale = nullptr);
+// form kFlatI8Exact (flat_b16k64.hip): per-row int8 scale s = max|x|/127 and residual ‖x − s·x̂‖ (×1.0001) per row;
+// the tiled int8 image (64 dims per 64-B chunk row, chunk count rounded up to even, zero-filled); its bytes
+int flat_i8_nk(int d);
+size_t flat_i8_img_bytes(int64_t n, int d, int R);
+void launch_i8_row_scale(const float *X, int64_t n, int d, float *scale, float *resid, hipStream_t st);
+void launch_i8_tile_rows(const float *X, const float *scale, int64_t n, int d, int R, void *out, hipStream_t st);
 int flat_keys_kth_max();
 void launch_flat_keys_kth(const float *keys, int S, int64_t nq, int k, float *bound, hipStream_t st);
 void launch_flat_cand_bound(const float *cand_d, const int *cand_n, int nsplit, int cap, int64_t nq, int k,

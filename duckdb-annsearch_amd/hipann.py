@@ -250,6 +250,7 @@ class _FlatForm:
     FORM_SPLIT2 = 2        # 2-term split (~2^-16 relative per product; measurement only)
     FORM_SPLIT2_EXACT = 3  # the 2-term scan as a filter + exact direct-form rerank with a bound check
     FORM_BF16_EXACT = 4    # default: one bf16 product per element (tiled bf16 image) as the filter, same rerank
+    FORM_I8_EXACT = 5      # one int8 product per element (tiled int8 image, int32 sums) as the filter, same rerank
 
     @property
     def form(self) -> int:
@@ -259,7 +260,7 @@ class _FlatForm:
     def form(self, v: int) -> None:
         if lib().hipann_flat_set_form(self._h, int(v)) != 0:
             raise HipAnnError("form must be 0 (fp32), 1 (split bf16, 3 terms), 2 (split bf16, 2 terms), "
-                              "3 (split bf16 + exact rerank) or 4 (bf16 + exact rerank)")
+                              "3 (split bf16 + exact rerank), 4 (bf16 + exact rerank) or 5 (int8 + exact rerank)")
 
     def rerank_fallbacks(self) -> int:
         """Queries the exact form's bound check re-ran on the 3-term path since creation."""

@@ -99,6 +99,12 @@ int hipann_flat_reconstruct_n(void *index, int64_t i0, int64_t n, float *out, ch
 #define HIPANN_FLAT_FORM_SPLIT2 2
 #define HIPANN_FLAT_FORM_SPLIT2_EXACT 3
 #define HIPANN_FLAT_FORM_BF16_EXACT 4
+/* HIPANN_FLAT_FORM_I8_EXACT: the BF16_EXACT pipeline with the scan over a tiled int8 image (per-row scale
+ * max|x|/127, round to nearest) on the int8 matrix cores (v_mfma_i32_16x16x64_i8: exact int32 sums, twice the
+ * bf16 rate, half its bytes per element) as the filter; a 64-deep filter, the bound from the measured int8
+ * residuals of the rows and of each query.  Runs as the bounded passes only (>= 256 queries, >= 512K rows,
+ * d <= 1024); elsewhere BF16_EXACT. */
+#define HIPANN_FLAT_FORM_I8_EXACT 5
 int hipann_flat_set_form(void *index, int form);
 int hipann_flat_get_form(void *index);
 /* Queries re-run on HIPANN_FLAT_FORM_SPLIT3 since the index was created: those the exact forms' bound

@@ -100,7 +100,7 @@ def c2_oracle(c2_data, oracle):
     return oracle.flat_search(xb, xq[:256], 10, 0)
 
 
-@pytest.mark.parametrize("form", [4, 3, 1, 0])
+@pytest.mark.parametrize("form", [5, 4, 3, 1, 0])
 def test_c2_flat_1m_768_nq1024(gpu, c2_data, c2_oracle, form):
     """C2: 1M × 768, nq = 1024, k = 10 through hipann_flat_search_device (the bench's call), every
     fp32-level form; the oracle's BLAS-path top-k on 256 queries; all 1024 rows sorted and distinct."""

@@ -242,7 +242,7 @@ def test_flat_large_properties(gpu, oracle):
     check_topk_parity(xb, xq[:64], D[:64], I[:64], Do, Io)
 
 
-@pytest.mark.parametrize("form", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("form", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("metric", [0, 1])
 @pytest.mark.parametrize("nq,d", [(20, 64), (129, 33), (300, 768), (64, 5), (257, 100), (600, 96)])
 def test_flat_forms_blas_path(gpu, oracle, form, metric, nq, d):
@@ -262,7 +262,7 @@ def test_flat_forms_blas_path(gpu, oracle, form, metric, nq, d):
         hit = np.mean([len(set(a) & set(b)) / 10 for a, b in zip(I.tolist(), Io.tolist())])
         assert hit >= 0.97, hit
     with pytest.raises(gpu.HipAnnError):
-        ix.form = 5
+        ix.form = 6
 
 
 def test_flat_exact_form_ties_fall_back(gpu, oracle):
@@ -304,8 +304,9 @@ def test_flat_exact_form_matches_fp32_form_at_scale(gpu, form):
     assert (I1 == I0).mean() >= 0.995
 
 
+@pytest.mark.parametrize("form", [4, 5])
 @pytest.mark.parametrize("metric", [0, 1])
-def test_flat_bf16_two_pass_resume(gpu, oracle, metric):
+def test_flat_bf16_two_pass_resume(gpu, oracle, metric, form):
     """The bf16 filter's two-pass schedule (1M rows, 64 splits of 61 tiles, nq = 512: pass A over the first
     6 tiles of every split under the 64K-row seed bound, the bound re-merged, pass B resumed from pass A's
     lists): the fp32 form's lists except inside near-tie windows, and the oracle's parity rule on a
@@ -317,8 +318,9 @@ def test_flat_bf16_two_pass_resume(gpu, oracle, metric):
     ix = gpu.HipIndexFlat(d, metric, xb)
     ix.form = ix.FORM_FP32
     D0, I0 = ix.search(xq, 10)
-    ix.form = ix.FORM_BF16_EXACT
+    ix.form = form
     D1, I1 = ix.search(xq, 10)
+    assert ix.last_search_path()["form"] == form
     scale = np.sum(xq.astype(np.float64) ** 2, 1)[:, None] + np.max(np.sum(xb.astype(np.float64) ** 2, 1))
     assert (np.abs(D1 - D0) <= 1e-5 * scale).all()
     assert (I1 == I0).mean() >= 0.995
@@ -326,8 +328,9 @@ def test_flat_bf16_two_pass_resume(gpu, oracle, metric):
     check_topk_parity(xb, xq[:48], D1[:48], I1[:48], Do, Io, metric)
 
 
+@pytest.mark.parametrize("form", [4, 5])
 @pytest.mark.parametrize("metric", [0, 1])
-def test_flat_bf16_flagged_queries_candidate_rerank(gpu, oracle, metric):
+def test_flat_bf16_flagged_queries_candidate_rerank(gpu, oracle, metric, form):
     """Bounded passes with near-duplicate rows (16K base rows x 40 copies + 1e-4 noise, shuffled; 640K x 64,
     nq 256): every query's 32 best scan keys are copies of one base row, so the first rerank cannot certify
     it and flags it.  The second rerank recomputes all of a flagged query's buffered candidates and
@@ -342,7 +345,9 @@ def test_flat_bf16_flagged_queries_candidate_rerank(gpu, oracle, metric):
     xq = rng.standard_normal((256, 64), dtype=np.float32)
     ix = gpu.HipIndexFlat(64, metric, xb)
     assert ix.form == ix.FORM_BF16_EXACT
+    ix.form = form
     D, I = ix.search(xq, 10)
+    assert ix.last_search_path()["form"] == form
     Do, Io = oracle.flat_search(xb, xq, 10, metric)
     check_topk_parity(xb, xq, D, I, Do, Io, metric)
     # the first rerank flags nearly all of these queries; the candidate rerank certifies most of them
@@ -392,3 +397,30 @@ def test_flat_ip_four_shards_in_process_c5_path(gpu, oracle):
     assert (np.abs(D4 - D1) <= 1e-5 * scale).all()
     Do, Io = oracle.flat_search(xb, xq[:12], 10, 1)
     check_topk_parity(xb, xq[:12], D4[:12], I4[:12], Do, Io, 1)
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+def test_flat_i8_form_row_scales_and_edge_rows(gpu, oracle, metric):
+    """Form 5 (int8 filter): per-row scales over rows whose magnitudes span 2^-20 .. 2^20 (the scale follows each
+    row, the bound follows the measured residuals), all-zero rows and an all-zero query, a query equal to a row;
+    600k x 128, nq 256, the oracle's parity rule on 40 queries and the fp32 form's ids elsewhere."""
+    rng = np.random.default_rng(91 + metric)
+    n, d, nq = 600_000, 128, 256
+    xb = rng.standard_normal((n, d), dtype=np.float32)
+    xb *= np.exp2(rng.integers(-20, 21, size=(n, 1))).astype(np.float32)
+    xb[::1000] = 0.0
+    xq = rng.standard_normal((nq, d), dtype=np.float32)
+    xq[7] = 0.0
+    xq[8] = xb[12345]
+    ix = gpu.HipIndexFlat(d, metric, xb)
+    ix.form = ix.FORM_I8_EXACT
+    D, I = ix.search(xq, 10)
+    assert ix.last_search_path() == {"form": 5, "filter_k": 64, "sublists": 0}
+    ix.form = ix.FORM_FP32
+    D0, I0 = ix.search(xq, 10)
+    assert (I == I0).mean() >= 0.99
+    Do, Io = oracle.flat_search(xb, xq[:40], 10, metric)
+    check_topk_parity(xb, xq[:40], D[:40], I[:40], Do, Io, metric)
+    if metric == 0:
+        assert I[8, 0] == 12345 and D[8, 0] == 0.0
+    ix.close()

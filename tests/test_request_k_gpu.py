@@ -33,9 +33,10 @@ def _ivf_kf(k):
     return 16 if k <= 12 else min(64, max(k + 4, 2 * k))
 
 
+@pytest.mark.parametrize("form", [4, 5])
 @pytest.mark.parametrize("metric", [0, 1])
 @pytest.mark.parametrize("k", [13, 20, 30, 32, 64])
-def test_flat_bounded_passes_request_k(gpu, oracle, metric, k):
+def test_flat_bounded_passes_request_k(gpu, oracle, metric, k, form):
     """Flat form 4 through the bounded passes (600k x 64 rows >= the 512K-row seed threshold, nq 256): exact at
     request_k 13-64, ids as the fp32 form's except in near-tie windows, the oracle's parity rule on 48 queries."""
     rng = np.random.default_rng(100 + k + metric)
@@ -43,10 +44,10 @@ def test_flat_bounded_passes_request_k(gpu, oracle, metric, k):
     xb = rng.standard_normal((n, d), dtype=np.float32)
     xq = rng.standard_normal((nq, d), dtype=np.float32)
     ix = gpu.HipIndexFlat(d, metric, xb)
-    assert ix.form == ix.FORM_BF16_EXACT
+    ix.form = form
     D, I = ix.search(xq, k)
     path = ix.last_search_path()
-    assert path["form"] == ix.FORM_BF16_EXACT and path["filter_k"] == _flat_kf(k), path
+    assert path["form"] == form and path["filter_k"] == (_flat_kf(k) if form == 4 else 64), path
     assert ix.rerank_fallbacks() <= nq // 16, ix.rerank_fallbacks()
     Do, Io = oracle.flat_search(xb, xq[:48], k, metric)
     check_topk_parity(xb, xq[:48], D[:48], I[:48], Do, Io, metric)
