@@ -403,6 +403,18 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
                          kout, out_sign, D, I, st);
         return;
     }
+    // flagged queries re-run on the device in the direct form, each by the rerank wave that flagged it
+    // (ivf_block_fallback inline: no host readback and no launch of its own); HIPANN_IVF_HOST_FALLBACK=1: from the
+    // host on the 3-term path (A/B)
+    const bool inline_fb = !host_fallback();
+    if (inline_fb) {
+        if (!sh.fb_total.p) {
+            sh.fb_total.ensure(sizeof(unsigned long long), sh.device);
+            HIPANN_CHECK(hipMemsetAsync(sh.fb_total.p, 0, sizeof(unsigned long long), st));
+        }
+        sh.fpd.ensure(sizeof(float) * (size_t)nq * np * kout, sh.device);
+        sh.fpi.ensure(sizeof(long long) * (size_t)nq * np * kout, sh.device);
+    }
     {
         ScopedTiming t(ix.timer_merge, st);
         launch_ivf_rerank(sh.part_d.get<float>(), sh.part_i.get<int>(), sh.slot_off.get<int>(), np, nq, kfilt, kout,
@@ -410,23 +422,11 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
                           sh.flagged.get<int>(), st, kSplit2Eps, half ? sh.half_rxmax : -1.f,
                           half ? sh.hres.get<float>() : nullptr, sh.coarse_i.get<int64_t>(),
                           sh.list_off.get<int64_t>(), nlist, qbound, half && metric == kL2 ? qn : nullptr, kslot,
-                          sub ? 1 : 0);
+                          sub ? 1 : 0, inline_fb ? sh.list_len.get<int>() : nullptr,
+                          inline_fb ? sh.fpd.get<float>() : nullptr, inline_fb ? sh.fpi.get<long long>() : nullptr,
+                          inline_fb ? sh.fb_total.get<unsigned long long>() : nullptr);
     }
-    if (!host_fallback()) {
-        // flagged queries re-run on the device in the direct form (ivf_fallback_query, one block per flagged
-        // query, bounded by the device flag count): no host readback, the next batch queues behind this one
-        if (!sh.fb_total.p) {
-            sh.fb_total.ensure(sizeof(unsigned long long), sh.device);
-            HIPANN_CHECK(hipMemsetAsync(sh.fb_total.p, 0, sizeof(unsigned long long), st));
-        }
-        sh.fpd.ensure(sizeof(float) * (size_t)nq * np * kout, sh.device);
-        sh.fpi.ensure(sizeof(long long) * (size_t)nq * np * kout, sh.device);
-        launch_ivf_fallback(sh.nflag.get<int>(), sh.flagged.get<int>(), nq, sh.coarse_i.get<int64_t>(), np, metric, xq,
-                            sh.codes, d, sh.list_off.get<int64_t>(), sh.list_len.get<int>(), nlist, sh.ids, 0, kout,
-                            sh.fpd.get<float>(), sh.fpi.get<long long>(), D, I, sh.fb_total.get<unsigned long long>(),
-                            st);
-        return;
-    }
+    if (inline_fb) return;
     int nf = 0;
     HIPANN_CHECK(hipMemcpyAsync(&nf, sh.nflag.p, sizeof(int), hipMemcpyDeviceToHost, st));
     HIPANN_CHECK(hipStreamSynchronize(st));

@@ -1508,8 +1508,7 @@ __device__ __forceinline__ int ivf_probe_rank_of_row(int64_t row, const int64_t 
 // every row's distance in the direct form (the same lane-strided fmaf chain and xor butterfly as
 // rerank_rows4: the rerank's values bit for bit), a (distance, CSR row) list of kout per
 // list into fpd/fpi[q][p][kout], then wave 0 applies FAISS's scan-order rule (ivf_scan_order_topk) and
-// writes D/I.  ivf_fallback_query runs it for every flagged query (persistent grid bounded by the device flag
-// count): one launch per batch instead of the scan + merge pair.
+// writes D/I.  The IVF rerank runs it with WV = 1 in the wave that flagged the query (no launch of its own).
 template <bool IP, int WV>
 __device__ __forceinline__ void ivf_block_fallback(int64_t q, int nprobe, int kout, const float *__restrict__ Q,
                                                 const float *__restrict__ codes, int d, const int64_t *__restrict__ ids,
@@ -1518,7 +1517,8 @@ __device__ __forceinline__ void ivf_block_fallback(int64_t q, int nprobe, int ko
                                                 int nlist, float *__restrict__ fpd, long long *__restrict__ fpi,
                                                 float *__restrict__ D, int64_t *__restrict__ I,
                                                 unsigned long long *__restrict__ total, float *sd2, long long *si2) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // WV = 1: one wave on its own (the rerank's inline re-run): sd2 / si2 are that wave's 64 entries
+    const int lane = threadIdx.x & 63, wv = WV == 1 ? 0 : threadIdx.x >> 6;
     const float *qp = Q + q * (int64_t)d;
     for (int p = 0; p < nprobe; ++p) {
         const int64_t l = probes[q * nprobe + p];
@@ -1559,19 +1559,22 @@ __device__ __forceinline__ void ivf_block_fallback(int64_t q, int nprobe, int ko
                         kout - 1);
             }
         }
-        sd2[wv * 64 + lane] = L.d[0];
-        si2[wv * 64 + lane] = L.id[0];
-        __syncthreads();
-        if (wv == 0) {
-            L.init();
+        if constexpr (WV > 1) {
+            sd2[wv * 64 + lane] = L.d[0];
+            si2[wv * 64 + lane] = L.id[0];
+            __syncthreads();
+            if (wv == 0) {
+                L.init();
 #pragma unroll
-            for (int w = 0; w < WV; ++w) L.offer(sd2[w * 64 + lane], si2[w * 64 + lane], kout - 1);
-            if (lane < kout) {
-                fpd[(q * nprobe + p) * kout + lane] = L.d[0];
-                fpi[(q * nprobe + p) * kout + lane] = L.id[0];
+                for (int w = 0; w < WV; ++w) L.offer(sd2[w * 64 + lane], si2[w * 64 + lane], kout - 1);
             }
         }
-        __syncthreads();
+        if (wv == 0 && lane < kout) {
+            fpd[(q * nprobe + p) * kout + lane] = L.d[0];
+            fpi[(q * nprobe + p) * kout + lane] = L.id[0];
+        }
+        if constexpr (WV > 1) __syncthreads();
+        else __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // this wave's fpd stores land before its reads below
     }
     if (wv != 0) return;
     WaveList<1, long long> R;
@@ -1608,9 +1611,9 @@ __device__ __forceinline__ void ivf_block_fallback(int64_t q, int nprobe, int ko
 // the running per-query bound and the merge all keep the 16 best), and |scan key − exact distance| ≤
 // E = 2⁻¹²·(‖q‖² + max‖x‖²) (the dropped split terms, ≤ 3·2⁻¹⁶·‖q‖‖x‖ per q·x, doubled, plus fp32
 // rounding of the norms and of both sums, with margin).  A query whose kout-th exact distance is not
-// < K16 − E (or < −K16... for IP the same bound on −q·x) is flagged; the host re-runs the flagged
-// queries on the device in the direct form (ivf_fallback_query; the Flat form: on the host, 3-term
-// path).  With fewer than 16 merged candidates nothing was pruned.
+// < K16 − E (or < −K16... for IP the same bound on −q·x) is flagged; IVF: the flagging wave re-runs the query at
+// once in the direct form (ivf_block_fallback, fpd != nullptr); the Flat forms: the host's candidate rerank /
+// 3-term path.  With fewer than 16 merged candidates nothing was pruned.
 // The list length k (16; 32 for Flat IP, common.hpp) is the number of candidates reranked.
 // rxmax >= 0 (Flat form kFlatBf16Exact: one plain bf16 product per element): the bound is the
 // Cauchy-Schwarz bound of the bf16 rounding instead, from this query's own rounding residual and the
@@ -1630,7 +1633,8 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
                 int *__restrict__ nflag, int *__restrict__ flagged, float eps, float rxmax,
                 const float *__restrict__ qres, const int64_t *__restrict__ probes,
                 const int64_t *__restrict__ list_off, int nlist, const unsigned *__restrict__ qbound,
-                const float *__restrict__ qnorm, int kslot, int sub) {
+                const float *__restrict__ qnorm, int kslot, int sub, const int *__restrict__ list_len,
+                float *__restrict__ fpd, long long *__restrict__ fpi, unsigned long long *__restrict__ fb_total) {
     const int64_t q = WV == 1 ? (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6) : (int64_t)blockIdx.x;
     if (q >= nq) return;
     const int lane = threadIdx.x & 63;
@@ -1825,6 +1829,16 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
                       (sub && tsub < __builtin_inff() && !(dk < tsub - E));
     if (flag && lane == 0) flagged[atomicAdd(nflag, 1)] = (int)q;
     const float pad_d = IP ? -__builtin_inff() : __builtin_inff();
+    if (flag && fpd) {
+        // IVF: this wave re-runs the query at once over its probe lists in the direct form with FAISS's scan-order
+        // tie rule (the device fallback, ivf_block_fallback) — no separate launch per batch
+        __shared__ float fsd[4 * 64];
+        __shared__ long long fsi[4 * 64];
+        const int pw = (int)(threadIdx.x >> 6);
+        ivf_block_fallback<IP, 1>(q, nprobe, kout, Q, codes, d, ids, label_offset, probes, list_off, list_len, nlist,
+                                  fpd, fpi, D, I, fb_total, fsd + pw * 64, fsi + pw * 64);
+        return;
+    }
     if (lane < kout) {
         const bool pad = R.id[0] == IdTraits<long long>::pad();
         D[q * kout + lane] = pad ? pad_d : (IP ? -R.d[0] : R.d[0]);
@@ -2012,44 +2026,6 @@ __global__ void __launch_bounds__(256) ivf_scatter_results(const float *__restri
     I[(int64_t)idx[j] * kout + e] = If[t];
 }
 
-// ---------------------------------------------------------------------------------------------
-// Device-side re-run of the queries ivf_rerank_topk flagged (no host round trip per batch): one block per
-// flagged query (ivf_block_fallback), a persistent grid bounded by the device flag count, so a batch with
-// nothing flagged costs one near-empty launch.
-// ---------------------------------------------------------------------------------------------
-template <bool IP>
-__global__ void __launch_bounds__(256)
-ivf_fallback_query(const int *__restrict__ nflag, const int *__restrict__ flagged, const int64_t *__restrict__ probes,
-                   int nprobe, const float *__restrict__ Q, const float *__restrict__ codes, int d,
-                   const int64_t *__restrict__ list_off, const int *__restrict__ list_len, int nlist,
-                   const int64_t *__restrict__ ids, int64_t label_offset, int kout, float *__restrict__ fpd,
-                   long long *__restrict__ fpi, float *__restrict__ D, int64_t *__restrict__ I,
-                   unsigned long long *__restrict__ total) {
-    __shared__ float sd2[4 * 64];
-    __shared__ long long si2[4 * 64];
-    const int nf = *nflag;
-    for (int f = blockIdx.x; f < nf; f += gridDim.x)
-        ivf_block_fallback<IP, 4>(flagged[f], nprobe, kout, Q, codes, d, ids, label_offset, probes, list_off, list_len,
-                                  nlist, fpd, fpi, D, I, total, sd2, si2);
-}
-
-void launch_ivf_fallback(const int *nflag, const int *flagged, int64_t nq, const int64_t *probes, int nprobe, int metric,
-                         const float *Q, const float *codes, int d, const int64_t *list_off, const int *list_len,
-                         int nlist, const int64_t *ids, int64_t label_offset, int kout, float *fpd, long long *fpi,
-                         float *D, int64_t *I, unsigned long long *total, hipStream_t st) {
-    if (nq <= 0) return;
-    HIPANN_REQUIRE(kout >= 1 && kout <= 64, "ivf fallback: kout out of range");
-    // one block per flagged query (persistent grid bounded by the device flag count); fpd/fpi: [q][p][kout]
-    const unsigned g = (unsigned)std::min<int64_t>(512, nq);
-    if (metric == kIP)
-        hipLaunchKernelGGL(ivf_fallback_query<true>, dim3(g), dim3(256), 0, st, nflag, flagged, probes, nprobe, Q, codes,
-                           d, list_off, list_len, nlist, ids, label_offset, kout, fpd, fpi, D, I, total);
-    else
-        hipLaunchKernelGGL(ivf_fallback_query<false>, dim3(g), dim3(256), 0, st, nflag, flagged, probes, nprobe, Q, codes,
-                           d, list_off, list_len, nlist, ids, label_offset, kout, fpd, fpi, D, I, total);
-    HIPANN_CHECK(hipGetLastError());
-}
-
 #ifndef HIPANN_RR_WIDE
 #define HIPANN_RR_WIDE (1 << 30)  // below this many queries: one 4-wave block per query (nq 1024: 80 -> 65 us)
 #endif
@@ -2059,17 +2035,18 @@ void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int 
                        int64_t label_offset, float xmax2, float *D, int64_t *I, int *nflag, int *flagged,
                        hipStream_t st, float eps, float rxmax, const float *qres, const int64_t *probes,
                        const int64_t *list_off, int nlist, const unsigned *qbound, const float *qnorm, int kslot,
-                       int sub) {
+                       int sub, const int *list_len, float *fpd, long long *fpi, unsigned long long *fb_total) {
     if (nq <= 0) return;
     if (kslot <= 0) kslot = k;
     // the filter depth k bounds kout (kout = k leaves no margin: those queries are flagged and re-run exactly)
     HIPANN_REQUIRE(k >= kRerankK && k <= 64 && kout >= 1 && kout <= k && kslot >= 1 && (!sub || qbound),
                    "ivf rerank: k / kout out of range");
+    HIPANN_REQUIRE(!fpd || (fpi && list_len && probes && list_off && fb_total), "ivf rerank: inline re-run buffers");
     // small batches: one 4-wave block per query (fills more of the chip, shorter per-query chain)
     const bool wide = nq < HIPANN_RR_WIDE;
     dim3 grid((unsigned)(wide ? nq : ceil_div(nq, 4))), block(256);
 #define RR_ARGS pd, pi, slot_off, nprobe, nq, k, kout, Q, codes, d, ids, nrows, label_offset, xmax2, D, I, nflag, flagged, \
-                eps, rxmax, qres, probes, list_off, nlist, qbound, qnorm, kslot, sub
+                eps, rxmax, qres, probes, list_off, nlist, qbound, qnorm, kslot, sub, list_len, fpd, fpi, fb_total
     if (metric == kIP) {
         if (wide) hipLaunchKernelGGL((ivf_rerank_topk<true, 4>), grid, block, 0, st, RR_ARGS);
         else hipLaunchKernelGGL((ivf_rerank_topk<true, 1>), grid, block, 0, st, RR_ARGS);

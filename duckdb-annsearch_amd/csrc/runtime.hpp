@@ -359,7 +359,9 @@ void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int 
                        int64_t label_offset, float xmax2, float *D, int64_t *I, int *nflag, int *flagged,
                        hipStream_t st, float eps = kSplit2Eps, float rxmax = -1.f, const float *qres = nullptr,
                        const int64_t *probes = nullptr, const int64_t *list_off = nullptr, int nlist = 0,
-                       const unsigned *qbound = nullptr, const float *qnorm = nullptr, int kslot = 0, int sub = 0);
+                       const unsigned *qbound = nullptr, const float *qnorm = nullptr, int kslot = 0, int sub = 0,
+                       const int *list_len = nullptr, float *fpd = nullptr, long long *fpi = nullptr,
+                       unsigned long long *fb_total = nullptr);  // fpd != nullptr: flagged IVF queries re-run inline
 // ivf_mfma.hip, fp16-image scan (kFormHalfExact)
 int ivf_mfma_h_group(int d);
 int ivf_scan_sublists();  // sub-lists per slot of the matrix-core scans in sub-list mode (one per wave)
@@ -412,10 +414,6 @@ void launch_flat_cand_select(const float *cand_d, const int *cand_i, const int *
 void launch_flat_bf16_seed(const float *pd, int nsplit, int64_t nq, int k, float *seed, hipStream_t st);
 bool flat_bf16_k64_supported(int nk, int k);
 void launch_ivf_max_norm(const float *xn, int64_t n, unsigned *out, hipStream_t st);
-void launch_ivf_fallback(const int *nflag, const int *flagged, int64_t nq, const int64_t *probes, int nprobe, int metric,
-                         const float *Q, const float *codes, int d, const int64_t *list_off, const int *list_len,
-                         int nlist, const int64_t *ids, int64_t label_offset, int kout, float *fpd, long long *fpi,
-                         float *D, int64_t *I, unsigned long long *total, hipStream_t st);
 void launch_ivf_gather_queries(const float *Q, const int *idx, int nf, int d, float *out, hipStream_t st);
 void launch_ivf_scatter_results(const float *Df, const int64_t *If, const int *idx, int nf, int kout, float *D,
                                 int64_t *I, hipStream_t st);
