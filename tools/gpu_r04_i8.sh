@@ -9,6 +9,10 @@ timeout -k 10 600 python -u -m pytest tests/test_flat_gpu.py tests/test_request_
     --timeout 300 --timeout-method thread -k "i8 or two_pass or candidate_rerank or forms_blas or bounded_passes or c2_flat" \
     > gpurun_out/r04_i8_tests.log 2>&1 || { echo "i8 tests failed"; tail -60 gpurun_out/r04_i8_tests.log; exit 1; }
 tail -1 gpurun_out/r04_i8_tests.log
+timeout -k 10 600 python -u -m pytest tests/test_ivf_gpu.py tests/test_request_k_gpu.py tests/test_configs_gpu.py -x -q \
+    --timeout 300 --timeout-method thread -k "fallback or ties or half_form or exact_form or ivf_exact_forms_request_k or c3" \
+    > gpurun_out/r04_ivf_fb_tests.log 2>&1 || { echo "ivf fallback tests failed"; tail -60 gpurun_out/r04_ivf_fb_tests.log; exit 1; }
+tail -1 gpurun_out/r04_ivf_fb_tests.log
 for f in 5 4; do
   HIPANN_FLAT_FORM=$f timeout -k 10 300 python -u bench.py --workload flat --no-cpu-baseline --steps 10 --warmup 2 \
       > gpurun_out/r04_flat10m_f$f.json 2> gpurun_out/r04_flat10m_f$f.err || { echo "flat form $f failed"; tail -20 gpurun_out/r04_flat10m_f$f.err; exit 1; }
