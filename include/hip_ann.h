@@ -203,8 +203,8 @@ int hipann_ivf_add(void *index, int64_t n, const float *xb, const int64_t *ids, 
 /* IVF training on the GPU — the k-means behind IndexIVFFlat::train (FAISS 1.13.2 IndexIVF::train_q1 →
  * Clustering::train), which the extension runs on the CPU at CREATE INDEX on a stride sample
  * (src/faiss_index.cpp:302-319).  From the n rows `x` (host, n*d fp32):
- *   1. training rows: when 0 < train_sample < n, rows floor(i * n / train_sample), i < train_sample — the
- *      reference's deterministic stride sample; else all n rows (n must be >= nlist);
+ *   1. training rows: when 0 < train_sample < n, rows (int64)(i * ((double)n / train_sample)), i < train_sample
+ *      — the reference's deterministic stride sample (faiss_index.cpp:308-311); else all n rows (n must be >= nlist);
  *   2. at most 256 rows per centroid (FAISS's max_points_per_centroid): above that, a uniform subset;
  *   3. init: HIPANN_KMEANS_INIT_RANDOM (FAISS's: nlist random training rows) or HIPANN_KMEANS_INIT_PLUSPLUS
  *      (k-means++ D² sampling on the GPU);

@@ -14,6 +14,9 @@
 //   FaissIndex::Search              :708-762 (request_k = min(k + |deleted|, ntotal), nprobe, search(1, …),
 //                                   −1 / tombstone skip, label → rowid)
 //   FaissIndex::SearchBatch         rank 1: the same rules, ONE search(nq, …) call
+//   PhysicalCreateFaissIndex::Finalize training (:302-319) and the Vacuum retrain (:876-878) — INTEGRATION.md
+//                                   §1.4: IVF k-means on the GPU (hipann_ivf_train) when the mode is not CPU;
+//                                   the CPU twin trains with the oracle's restatement (same draws)
 // The "CPU FAISS index" is the oracle's restatement of IndexFlat / IndexIVFFlat (oracle/oracle.c, test
 // infrastructure); the "GPU index" is libhipann.so.  Every scenario compares the GPU-backed FaissIndex with a
 // CPU-mode twin fed the same operations.  Output: one "CHECK <name> ok|FAIL <detail>" line per check, exit
@@ -42,6 +45,8 @@ void oracle_flat_search(const float *xb, int64_t n, int d, const float *xq, int6
 void oracle_ivf_search(const float *centroids, int nlist, const int64_t *list_off, const int64_t *ids,
                        const float *codes, int d, const float *xq, int64_t nq, int k, int nprobe, int metric, float *D,
                        int64_t *I, int64_t *probes_out);
+int oracle_kmeans_train(const float *x, int64_t n, int d, int metric, int nlist, int64_t train_sample, int niter,
+                        uint64_t seed, int init, float *centroids, int64_t *sizes_out);
 }
 
 namespace {
@@ -169,8 +174,33 @@ struct FaissIndexModel {
         }
     }
 
-    // Finalize (:287-414, the parts after training): add, label↔rowid maps, EnsureGpuIndex (:364)
-    void Finalize(const std::vector<float> &x, const std::vector<row_t> &rowids) {
+    // IVF training: GPU k-means when a GPU may serve, the CPU train otherwise.  Both take
+    // the reference's stride sample of train_sample rows (:304-315) and the same seed.
+    static constexpr int kTrainIters = 25;
+    static constexpr uint64_t kTrainSeed = 1234;
+    int gpu_trains = 0;
+    void Train(const float *x, int64_t n, int64_t train_sample) {
+        CpuIndex &c = *faiss_index_;
+        if (!c.ivf || n <= 0) return;
+        c.centroids.assign((size_t)c.nlist * c.d, 0.f);
+        if (mode_ != Mode::CPU && hipann_available()) {
+            char err[512] = {0};
+            const int rc = hipann_ivf_train(c.d, c.metric, c.nlist, n, x, train_sample, kTrainIters, kTrainSeed,
+                                            HIPANN_KMEANS_INIT_RANDOM, 0, c.centroids.data(), nullptr, err, sizeof err);
+            if (rc == 0) {
+                ++gpu_trains;
+                return;
+            }
+            if (mode_ == Mode::GPU) throw std::runtime_error(err);
+        }
+        if (oracle_kmeans_train(x, n, c.d, c.metric, c.nlist, train_sample, kTrainIters, kTrainSeed,
+                                HIPANN_KMEANS_INIT_RANDOM, c.centroids.data(), nullptr) != 0)
+            throw std::runtime_error("CPU training failed");
+    }
+
+    // Finalize (:287-414): train (IVF), add, label↔rowid maps, EnsureGpuIndex (:364)
+    void Finalize(const std::vector<float> &x, const std::vector<row_t> &rowids, int64_t train_sample = -1) {
+        if (train_sample >= 0) Train(x.data(), (int64_t)rowids.size(), train_sample);
         faiss_index_->add((int64_t)rowids.size(), x.data());
         for (size_t i = 0; i < rowids.size(); ++i) {
             label_to_rowid_.push_back(rowids[i]);
@@ -212,7 +242,7 @@ struct FaissIndexModel {
         }
     }
 
-    void Vacuum() {  // :840-899 (the IVF retrain keeps the trained centroids here: training is out of scope)
+    void Vacuum(bool retrain = false) {  // :840-899; retrain: the fresh IVF index is trained on every kept row (:876-878)
         if (deleted_labels_.empty() || !faiss_index_) return;
         const int64_t old_ntotal = faiss_index_->ntotal;
         std::vector<float> kept;
@@ -231,6 +261,9 @@ struct FaissIndexModel {
         fresh->centroids = faiss_index_->centroids;
         fresh->list_ids.assign(fresh->nlist, {});
         fresh->list_codes.assign(fresh->nlist, {});
+        std::swap(faiss_index_, fresh);
+        if (retrain && !kept_rowids.empty()) Train(kept.data(), (int64_t)kept_rowids.size(), 0);
+        std::swap(faiss_index_, fresh);
         if (!kept_rowids.empty()) fresh->add((int64_t)kept_rowids.size(), kept.data());
         label_to_rowid_.assign(kept_rowids.begin(), kept_rowids.end());
         rowid_to_label_.clear();
@@ -363,20 +396,26 @@ std::vector<float> uniform(std::mt19937 &rng, int64_t n) {  // faiss-metal's tes
 // One scenario: a GPU-mode (or AUTO) FaissIndex and its CPU-mode twin through build → search → delete →
 // append → search → vacuum → lazy re-upload → search.
 void scenario(const std::string &type, int d, int metric, int64_t n, int nq, int k, int nlist, int nprobe,
-              Mode mode) {
-    const std::string tag = type + (metric ? "_ip" : "_l2") + "_d" + std::to_string(d);
+              Mode mode, int64_t train_sample = -1) {
+    // train_sample >= 0: the IVF quantizer is trained at Finalize (and again at Vacuum) — §1.4
+    const bool train = type == "IVFFlat" && train_sample >= 0;
+    const std::string tag = type + (metric ? "_ip" : "_l2") + "_d" + std::to_string(d) + (train ? "_trained" : "");
     std::mt19937 rng(42);
     std::vector<float> xb = uniform(rng, n * d), xq = uniform(rng, (int64_t)nq * d);
     std::vector<float> cen;
-    if (type == "IVFFlat")  // a trained quantizer: every (n / nlist)-th row (k-means is out of scope)
+    if (type == "IVFFlat" && !train)  // a given quantizer: every (n / nlist)-th row
         for (int l = 0; l < nlist; ++l) cen.insert(cen.end(), xb.begin() + (int64_t)l * (n / nlist) * d,
                                                   xb.begin() + ((int64_t)l * (n / nlist) + 1) * d);
     std::vector<row_t> rowids(n);
     for (int64_t i = 0; i < n; ++i) rowids[i] = 1000000 + 7 * i;  // DuckDB row ids, not labels
     auto gpu = make_model(type, d, metric, mode, nlist, cen, nprobe);
     auto cpu = make_model(type, d, metric, Mode::CPU, nlist, cen, nprobe);
-    gpu->Finalize(xb, rowids);
-    cpu->Finalize(xb, rowids);
+    gpu->Finalize(xb, rowids, train ? train_sample : -1);
+    cpu->Finalize(xb, rowids, train ? train_sample : -1);
+    if (train) {
+        check(gpu->gpu_trains == 1 && cpu->gpu_trains == 0, tag + "/finalize/trained_on_gpu");
+        check(gpu->faiss_index_->centroids == cpu->faiss_index_->centroids, tag + "/finalize/centroids_equal_cpu_train");
+    }
     check(gpu->gpu_index_ != nullptr && gpu->uploads == 1, tag + "/finalize_uploads");
     check(cpu->gpu_index_ == nullptr && cpu->uploads == 0, tag + "/cpu_mode_never_uploads");
 
@@ -436,8 +475,12 @@ void scenario(const std::string &type, int d, int metric, int64_t n, int nq, int
     }
 
     // vacuum: relabels → the copy is dropped; the next search re-uploads it once (rank 2's lazy re-upload)
-    gpu->Vacuum();
-    cpu->Vacuum();
+    gpu->Vacuum(train);
+    cpu->Vacuum(train);
+    if (train) {
+        check(gpu->gpu_trains == 2, tag + "/vacuum/retrained_on_gpu");
+        check(gpu->faiss_index_->centroids == cpu->faiss_index_->centroids, tag + "/vacuum/centroids_equal_cpu_train");
+    }
     check(gpu->gpu_index_ == nullptr, tag + "/vacuum/invalidated");
     run("vacuumed");
     check(gpu->gpu_index_ != nullptr && gpu->uploads == 2, tag + "/vacuum/lazy_reupload_once",
@@ -463,6 +506,9 @@ int main() {
     scenario("Flat", 96, 1, 12000, 40, 10, 0, 1, Mode::GPU);
     scenario("IVFFlat", 64, 0, 30000, 48, 10, 32, 8, Mode::GPU);
     scenario("IVFFlat", 64, 1, 30000, 48, 10, 32, 8, Mode::GPU);
+    // CREATE INDEX training on the GPU (§1.4): stride sample of 6000 rows; the VACUUM retrain uses every kept row
+    scenario("IVFFlat", 64, 0, 30000, 48, 10, 32, 8, Mode::GPU, 6000);
+    scenario("IVFFlat", 48, 1, 24000, 40, 10, 24, 6, Mode::AUTO, 0);
     // AUTO below the gate stays on the CPU (ntotal·d < HIPANN_AUTO_MIN_WORK)
     {
         std::mt19937 rng(7);

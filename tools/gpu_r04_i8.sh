@@ -13,6 +13,10 @@ timeout -k 10 600 python -u -m pytest tests/test_ivf_gpu.py tests/test_request_k
     --timeout 300 --timeout-method thread -k "fallback or ties or half_form or exact_form or ivf_exact_forms_request_k or c3" \
     > gpurun_out/r04_ivf_fb_tests.log 2>&1 || { echo "ivf fallback tests failed"; tail -60 gpurun_out/r04_ivf_fb_tests.log; exit 1; }
 tail -1 gpurun_out/r04_ivf_fb_tests.log
+timeout -k 10 300 python -u -m pytest tests/test_harness_gpu.py tests/test_ivf_train_gpu.py -x -q --timeout 240 \
+    --timeout-method thread > gpurun_out/r04_harness.log 2>&1 || { echo "harness failed"; tail -40 gpurun_out/r04_harness.log; \
+    grep FAIL gpurun_out/faiss_index_harness.log | head; exit 1; }
+tail -1 gpurun_out/r04_harness.log
 for f in 5 4; do
   HIPANN_FLAT_FORM=$f timeout -k 10 300 python -u bench.py --workload flat --no-cpu-baseline --steps 10 --warmup 2 \
       > gpurun_out/r04_flat10m_f$f.json 2> gpurun_out/r04_flat10m_f$f.err || { echo "flat form $f failed"; tail -20 gpurun_out/r04_flat10m_f$f.err; exit 1; }
