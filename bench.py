@@ -1402,6 +1402,11 @@ def main():
             line.setdefault("configs", {})["C5_flat_ip_100m_768_sharded"] = c5
     line["world_check"] = wcheck
     line["build"] = build_provenance()
+    if os.environ.get("HIPANN_RR_PROF_DUMP"):  # tuning builds only (HIPANN_RR_PROF): the rerank's phase clocks
+        import ctypes
+        buf = (ctypes.c_ulonglong * 8)()
+        if hipann.lib().hipann_debug_rr_prof(buf) == 0 and buf[7]:
+            log("rerank phase clocks per query (wave 0):", [round(buf[i] / buf[7]) for i in range(5)], "queries", buf[7])
     emit(line, rank)
     if world > 1:
         dist.destroy_process_group()

@@ -307,12 +307,18 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
                 const float xs = __shfl(xr[jb >> 2], 16 * (jb & 3) + m16);
                 const float xv = x0 + 16 * jb + m16 < N ? xs : __builtin_inff();
                 if constexpr (I8) {
+                    // whole-vector reinterpret + convert: per-element extracts of the bit-cast i32 MFMA result were
+                    // miscompiled (only element 0 of each accumulator was read; the others came from stale
+                    // registers — found by the form's parity tests, every query with index % 4 != 0 wrong)
                     const float sx = __shfl(xsc[jb >> 2], 16 * (jb & 3) + m16);
 #pragma unroll
-                    for (int mb = 0; mb < 2; ++mb)
+                    for (int mb = 0; mb < 2; ++mb) {
+                        const k64_f32x4 v = __builtin_convertvector(__builtin_bit_cast(k64_i32x4, acc[mb][jb]), k64_f32x4);
+                        k64_f32x4 r;
 #pragma unroll
-                        for (int i = 0; i < 4; ++i)
-                            acc[mb][jb][i] = fmaf(csq[mb][i] * sx, (float)__builtin_bit_cast(int, acc[mb][jb][i]), -xv);
+                        for (int i = 0; i < 4; ++i) r[i] = fmaf(csq[mb][i] * sx, v[i], -xv);
+                        acc[mb][jb] = r;
+                    }
                 } else {
 #pragma unroll
                     for (int mb = 0; mb < 2; ++mb)

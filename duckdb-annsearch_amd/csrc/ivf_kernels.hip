@@ -1621,6 +1621,15 @@ __device__ __forceinline__ void ivf_block_fallback(int64_t q, int nprobe, int ko
 // plus the fp32 accumulation of d exact products (≤ d·2⁻²⁴·‖q̂‖‖x̂‖), doubled for L2, plus the fp32
 // rounding of the key and of the reranked direct distance (≤ (d + 8)·2⁻²⁴·2(‖q‖² + max‖x‖²)), all ×1.01.
 // ---------------------------------------------------------------------------------------------
+#ifndef HIPANN_RR_PROF
+#define HIPANN_RR_PROF 0  // tuning builds: wave 0's per-phase shader clocks of the wide rerank, summed in rr_prof
+#endif
+#if HIPANN_RR_PROF
+__device__ unsigned long long rr_prof[8];
+#define RR_MARK(i) do { if (wv == 0) { const long long t_ = clock64(); if (lane == 0) atomicAdd(&rr_prof[i], (unsigned long long)(t_ - rr_t)); rr_t = t_; } } while (0)
+#else
+#define RR_MARK(i) do { } while (0)
+#endif
 // WV = 1: one wave per query, four queries per block (large batches).  WV > 1 (small batches, the
 // extension's nq = 1 call): one block of WV waves per query — the waves merge disjoint parts of the
 // partial lists and compute a share of the candidates' distances, wave 0 finishes.
@@ -1639,6 +1648,9 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
     if (q >= nq) return;
     const int lane = threadIdx.x & 63;
     const int wv = WV == 1 ? 0 : (int)(threadIdx.x >> 6);
+#if HIPANN_RR_PROF
+    long long rr_t = clock64();
+#endif
     // 1. the k best (scan key, row) of the query's partial lists (kslot entries per slot)
     WaveList<1, int> L;
     L.init();
@@ -1693,7 +1705,9 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
             // (sub-lists: T_sub — the candidates above it are irrelevant, see above)
             const unsigned qb = qbound && !sub ? qbound[q] : 0xffffffffu;
             const float bound = sub ? tsub : (qb & 0x80000000u) ? __uint_as_float(qb & 0x7fffffffu) : __builtin_inff();
+            RR_MARK(0);
             rerank_block_select<WV, RS_J>(pd, pi, total, k, nrows, sd, si, scnt, L, bound);
+            RR_MARK(1);
             if (wv == 0) srow[lane] = lane < k ? L.id[0] : IdTraits<int>::pad();
         } else {
             sd[wv * 64 + lane] = lane < k ? L.d[0] : __builtin_inff();
@@ -1729,6 +1743,7 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
             }
         }
         __syncthreads();
+        RR_MARK(2);
         if (wv != 0) return;
         myrow = L.id[0];
         ncand = __popcll(__ballot(lane < k && myrow != IdTraits<int>::pad()));
@@ -1809,6 +1824,7 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
             ivf_scan_order_topk(64, kout, [&](int64_t) { return ScanCand{mk, pos, lab}; }, R);
         }
     }
+    if constexpr (WV > 1) RR_MARK(3);
     // 4. exactness check
     const float dk = readlane_f(R.d[0], kout - 1);
     float E;
@@ -1843,6 +1859,12 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
         const bool pad = R.id[0] == IdTraits<long long>::pad();
         D[q * kout + lane] = pad ? pad_d : (IP ? -R.d[0] : R.d[0]);
         I[q * kout + lane] = pad ? -1 : (int64_t)R.id[0];
+    }
+    if constexpr (WV > 1) {
+        RR_MARK(4);
+#if HIPANN_RR_PROF
+        if (lane == 0) atomicAdd(&rr_prof[7], 1ull);
+#endif
     }
 }
 
@@ -2056,6 +2078,20 @@ void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int 
     }
 #undef RR_ARGS
     HIPANN_CHECK(hipGetLastError());
+}
+
+// tuning builds (HIPANN_RR_PROF): the wide rerank's per-phase clock sums [0..4] and query count [7]; reset after reading
+extern "C" int hipann_debug_rr_prof(unsigned long long *out8) {
+#if HIPANN_RR_PROF
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(rr_prof), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+    unsigned long long z[8] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(rr_prof), z, sizeof z) != hipSuccess) return -1;
+    return 0;
+#else
+    (void)out8;
+    return -1;
+#endif
 }
 
 void launch_ivf_max_norm(const float *xn, int64_t n, unsigned *out, hipStream_t st) {

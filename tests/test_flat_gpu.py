@@ -424,3 +424,27 @@ def test_flat_i8_form_row_scales_and_edge_rows(gpu, oracle, metric):
     if metric == 0:
         assert I[8, 0] == 12345 and D[8, 0] == 0.0
     ix.close()
+
+
+@pytest.mark.parametrize("nq", [4096, 8192])
+def test_flat_bf16_large_batch_buffers_do_not_overflow(gpu, oracle, nq):
+    """Large batches on the bounded passes: the per-(query, split) candidate buffer is sized from
+    the expected fill (k · rows / sample over the splits), so at nq 4096 and 8192 (few splits per query block,
+    many rows per split) no query overflows into the SPLIT3 re-run.  2M x 128 uniform rows: ids equal the fp32
+    form's except in near-tie windows, re-runs stay under 1% of the batch, and the oracle's parity rule holds on
+    16 queries."""
+    rng = np.random.default_rng(nq)
+    n, d = 2_000_000, 128
+    xb = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    xq = rng.uniform(-1, 1, (nq, d)).astype(np.float32)
+    ix = gpu.HipIndexFlat(d, 0, xb)
+    D, I = ix.search(xq, 10)
+    assert ix.last_search_path()["form"] == ix.FORM_BF16_EXACT
+    assert ix.rerank_fallbacks() <= nq // 100, ix.rerank_fallbacks()
+    ix.form = ix.FORM_FP32
+    D0, I0 = ix.search(xq, 10)
+    assert (I == I0).mean() >= 0.995
+    scale = np.sum(xq.astype(np.float64) ** 2, 1)[:, None] + np.max(np.sum(xb.astype(np.float64) ** 2, 1))
+    assert (np.abs(D - D0) <= 1e-5 * scale).all()
+    Do, Io = oracle.flat_search(xb, xq[:16], 10, 0)
+    check_topk_parity(xb, xq[:16], D[:16], I[:16], Do, Io, 0)

@@ -6,7 +6,7 @@ cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
 timeout -k 10 600 python -u -m pytest tests/test_flat_gpu.py tests/test_request_k_gpu.py tests/test_configs_gpu.py -x -q \
-    --timeout 300 --timeout-method thread -k "i8 or two_pass or candidate_rerank or forms_blas or bounded_passes or c2_flat" \
+    --timeout 300 --timeout-method thread -k "i8 or two_pass or candidate_rerank or forms_blas or bounded_passes or c2_flat or large_batch" \
     > gpurun_out/r04_i8_tests.log 2>&1 || { echo "i8 tests failed"; tail -60 gpurun_out/r04_i8_tests.log; exit 1; }
 tail -1 gpurun_out/r04_i8_tests.log
 timeout -k 10 600 python -u -m pytest tests/test_ivf_gpu.py tests/test_request_k_gpu.py tests/test_configs_gpu.py -x -q \
