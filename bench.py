@@ -426,6 +426,7 @@ def attach_traffic(roof, key, algorithmic_bytes):
 # ------------------------------------------------------------------------------------------------
 # Flat
 # ------------------------------------------------------------------------------------------------
+FLAT_DEFAULT_FORM = 5
 FLAT_FORMS = {5: ("flat_bf16_k64<I8>", 1, I8_MFMA_PEAK_TOPS,
                   "int8 MFMA (v_mfma_i32_16x16x64_i8, exact int32 sums), one int8 product per fp32 product over a "
                   "tiled int8 image with per-row scales; the bounded passes and exact fp32 rerank of form 4 with a "
@@ -458,7 +459,7 @@ def flat_config(args, torch, dist, hipann, rank, world, dev, n, d, nq, k, metric
     gen_uniform_rows(torch, xb, lo, 42)
     xq = uniform_queries(torch, nq, d, dev)
     index = hipann.HipIndexFlatDevice(d, metric, xb.data_ptr(), n_local, dev.index, copy=False, label_offset=lo)
-    if os.environ.get("HIPANN_FLAT_FORM"):  # A/B; the library default is form 4 (bf16 filter + exact rerank)
+    if os.environ.get("HIPANN_FLAT_FORM"):  # A/B; the library default is form 5 (int8 filter + exact rerank)
         index.form = int(os.environ["HIPANN_FLAT_FORM"])
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t_setup
@@ -478,7 +479,7 @@ def flat_config(args, torch, dist, hipann, rank, world, dev, n, d, nq, k, metric
     Dr, Ir = step()
     torch.cuda.synchronize()
     Ir = Ir.cpu().numpy().copy()
-    form = index.form
+    form = index.last_search_path()["form"]  # the form the scan ran (the default falls back to 4 on small shapes)
     kname, terms, peak, fdesc = FLAT_FORMS[form]
     flops = 2.0 * nq * n_local * d
     achieved = terms * flops / (kern_ms * 1e-3) / 1e12 if kern_ms > 0 else 0.0
@@ -516,7 +517,7 @@ def flat_config(args, torch, dist, hipann, rank, world, dev, n, d, nq, k, metric
         out["precision"] = ("returned distances are fp32 " + ("direct-form Σ(q−x)²" if metric == 0 else "dot products")
                             + ", recomputed exactly for the kept candidates; FAISS CPU's BLAS path (nq >= 20) returns "
                             "max(0, ‖q‖²+‖x‖²−2q·x) from sgemm: the same ids (parity tests), distances equal up to the "
-                            "fp32 rounding of the two forms. The bf16 scan is a certified filter, not the result.")
+                            "fp32 rounding of the two forms. The bf16 / int8 scan is a certified filter, not the result.")
     if world > 1:
         return out, index, xb
     if request_k:
@@ -533,6 +534,8 @@ def flat_config(args, torch, dist, hipann, rank, world, dev, n, d, nq, k, metric
             index.form = f
             step()
             torch.cuda.synchronize()
+            if index.last_search_path()["form"] != f:  # this shape runs another form under that setting
+                continue
             index.set_kernel_timing(True)
             ta = time.perf_counter()
             for _ in range(2):
@@ -550,7 +553,7 @@ def flat_config(args, torch, dist, hipann, rank, world, dev, n, d, nq, k, metric
             if f == 0:  # exact fp32 products: the reference for recall
                 out["recall_at_10"] = round(recall_at(Ir, Ia, k), 6)
                 out["recall_reference"] = "the fp32-MFMA form's top-k on the same batch (exact fp32 products)"
-        index.form = form
+        index.form = FLAT_DEFAULT_FORM if not os.environ.get("HIPANN_FLAT_FORM") else int(os.environ["HIPANN_FLAT_FORM"])
         out["other_forms"] = alt
     if oracle_queries:
         try:
@@ -1352,7 +1355,9 @@ def main():
             sub, index, xb_keep = flat_config(args, torch, dist, hipann, rank, world, dev, args.n, args.d, args.nq, args.k,
                                         metric, args.steps, args.warmup, alt_forms=not args.no_alt_forms,
                                         cpu_seconds=0.0 if args.no_cpu_baseline else args.cpu_seconds)
-            dtype, data = "f32 results (bf16-image certified filter + exact fp32 rerank)", "U(-1,1) rows"
+            dtype = ("f32 results (int8-image certified filter, int32 sums + exact fp32 rerank)" if sub.get("form") == 5
+                     else "f32 results (bf16-image certified filter + exact fp32 rerank)" if sub.get("form") == 4 else "f32")
+            data = "U(-1,1) rows"
         else:
             sub, index = ivf_config(args, torch, dist, hipann, rank, world, dev, args.steps, args.warmup,
                                     suite_extras=args.suite and world == 1)
@@ -1404,9 +1409,11 @@ def main():
     line["build"] = build_provenance()
     if os.environ.get("HIPANN_RR_PROF_DUMP"):  # tuning builds only (HIPANN_RR_PROF): the rerank's phase clocks
         import ctypes
-        buf = (ctypes.c_ulonglong * 8)()
+        buf = (ctypes.c_ulonglong * 16)()
         if hipann.lib().hipann_debug_rr_prof(buf) == 0 and buf[7]:
-            log("rerank phase clocks per query (wave 0):", [round(buf[i] / buf[7]) for i in range(5)], "queries", buf[7])
+            names = {0: "setup", 1: "loads", 5: "bound_count", 2: "select_sort", 3: "distances", 4: "order_ties", 8: "write"}
+            log("rerank phase clocks per query (wave 0):", {v: round(buf[i] / buf[7]) for i, v in names.items()},
+                "compaction-path", buf[6], "list-path", buf[9], "queries", buf[7])
     emit(line, rank)
     if world > 1:
         dist.destroy_process_group()

@@ -71,10 +71,11 @@ constexpr int kFlatRerankKIP = 32;
 // (default): the 2-term scan keeps kRerankK rows per database split and query as a filter, every
 // returned distance is recomputed exactly in the direct form with the IVF exact form's bound check
 // (ivf_rerank_topk), failures re-run on kFlatSplit3; kout <= kRerankMaxK (else kFlatSplit3).
-// kFlatBf16Exact (default): the same filter + rerank on ONE plain bf16 product per element (flat_bf16.hip:
+// kFlatBf16Exact: the same filter + rerank on ONE plain bf16 product per element (flat_bf16.hip:
 // a tiled bf16 image of the database built once; 32 kept per (split, query); the rerank's bound is the
 // Cauchy-Schwarz bound of the actual bf16 rounding residuals), failures re-run on kFlatSplit3.
-// kFlatI8Exact: the same bounded passes over a tiled int8 image (per-row scale max|x|/127) on the int8 matrix
+// kFlatI8Exact (default; shapes the bounded passes do not take fall back to kFlatBf16Exact): the same bounded
+// passes over a tiled int8 image (per-row scale max|x|/127) on the int8 matrix
 // cores (int32 sums: exact; twice the bf16 rate and half its bytes); the bound uses the int8 residuals.
 enum FlatForm : int {
     kFlatFp32 = 0,

@@ -319,7 +319,9 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     IvfPlanHook hook{sh.list_len.get<int>(), nlist, ivf_chunk_rows(), ccnt_cur, sh.slot_off.get<int>(),
                      sh.qtot.get<int>(), false};
     FlatShard &qsh = *sh.quant->shards[0];
-    qsh.plan_hook = ivf_plan_query_major() ? &hook : nullptr;
+    // HIPANN_IVF_SELECT_HOOK=0 (A/B): the count step in its own launch (ivf_count_q) instead of the select's tail
+    static const bool hook_env = [] { const char *e = std::getenv("HIPANN_IVF_SELECT_HOOK"); return !e || std::atoi(e); }();
+    qsh.plan_hook = ivf_plan_query_major() && hook_env ? &hook : nullptr;
     try {
         flat_shard_search(*sh.quant, qsh, nq, xq, np, np, sh.coarse_d.get<float>(), sh.coarse_i.get<int64_t>(), st);
     } catch (...) {

@@ -1286,6 +1286,20 @@ __device__ __forceinline__ void rerank_rows4(const float *__restrict__ qp, const
     }
 }
 
+#ifndef HIPANN_RR_PROF
+#define HIPANN_RR_PROF 0  // tuning builds: wave 0's per-phase shader clocks of the wide rerank, summed in rr_prof
+#endif
+#if HIPANN_RR_PROF
+__device__ unsigned long long rr_prof[16];
+#define RR_MARK(i) do { if (wv == 0) { const long long t_ = clock64(); if (lane == 0) atomicAdd(&rr_prof[i], (unsigned long long)(t_ - rr_t)); rr_t = t_; } } while (0)
+#else
+#define RR_MARK(i) do { } while (0)
+#endif
+#if HIPANN_RR_PROF
+#define RR_COUNT(i) do { if (wv == 0 && lane == 0) atomicAdd(&rr_prof[i], 1ull); } while (0)
+#else
+#define RR_COUNT(i) do { } while (0)
+#endif
 // HIPANN_RERANK_LISTS=1: the rerank merges with per-wave lists only (A/B of rerank_block_select).
 __device__ __forceinline__ bool rerank_lists() {
 #ifdef HIPANN_RERANK_LISTS
@@ -1311,8 +1325,9 @@ template <int WV, int J>
 __device__ __forceinline__ void rerank_block_select(const float *__restrict__ pd, const int *__restrict__ pi,
                                                     int64_t total, int k, int64_t nrows, float *sd, int *si,
                                                     int (*scnt)[WV], WaveList<1, int> &L,
-                                                    float bound = __builtin_inff()) {
+                                                    float bound, long long &rr_t) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    (void)rr_t;
     float v[J];
     int r[J];
     unsigned u[J];
@@ -1329,6 +1344,7 @@ __device__ __forceinline__ void rerank_block_select(const float *__restrict__ pd
         const unsigned b = __float_as_uint(f);
         u[j] = ok ? ((b >> 31) ? ~b : (b | 0x80000000u)) : 0xffffffffu;
     }
+    RR_MARK(1);  // candidate loads
     if (bound < __builtin_inff()) {
         const unsigned long long lt = (1ull << lane) - 1ull;
         int nb = 0;
@@ -1342,7 +1358,9 @@ __device__ __forceinline__ void rerank_block_select(const float *__restrict__ pd
             tot += scnt[0][w];
             off += w < wv ? scnt[0][w] : 0;
         }
+        RR_MARK(5);  // bound count + barrier
         if (tot <= 64) {  // block-uniform
+            RR_COUNT(6);
 #pragma unroll
             for (int j = 0; j < J; ++j) {
                 const bool a = u[j] != 0xffffffffu && v[j] <= bound;
@@ -1358,6 +1376,7 @@ __device__ __forceinline__ void rerank_block_select(const float *__restrict__ pd
                 L.d[0] = lane < k ? kk : __builtin_inff();
                 L.id[0] = lane < k ? cc : IdTraits<int>::pad();
             }
+            RR_MARK(2);  // compaction + sort
             return;
         }
         __syncthreads();  // every wave has read scnt before the search reuses it
@@ -1416,6 +1435,7 @@ __device__ __forceinline__ void rerank_block_select(const float *__restrict__ pd
         L.d[0] = kk;
         L.id[0] = cc;
     }
+    RR_MARK(2);  // 32-step search + compaction + sort
 }
 
 
@@ -1621,15 +1641,6 @@ __device__ __forceinline__ void ivf_block_fallback(int64_t q, int nprobe, int ko
 // plus the fp32 accumulation of d exact products (≤ d·2⁻²⁴·‖q̂‖‖x̂‖), doubled for L2, plus the fp32
 // rounding of the key and of the reranked direct distance (≤ (d + 8)·2⁻²⁴·2(‖q‖² + max‖x‖²)), all ×1.01.
 // ---------------------------------------------------------------------------------------------
-#ifndef HIPANN_RR_PROF
-#define HIPANN_RR_PROF 0  // tuning builds: wave 0's per-phase shader clocks of the wide rerank, summed in rr_prof
-#endif
-#if HIPANN_RR_PROF
-__device__ unsigned long long rr_prof[8];
-#define RR_MARK(i) do { if (wv == 0) { const long long t_ = clock64(); if (lane == 0) atomicAdd(&rr_prof[i], (unsigned long long)(t_ - rr_t)); rr_t = t_; } } while (0)
-#else
-#define RR_MARK(i) do { } while (0)
-#endif
 // WV = 1: one wave per query, four queries per block (large batches).  WV > 1 (small batches, the
 // extension's nq = 1 call): one block of WV waves per query — the waves merge disjoint parts of the
 // partial lists and compute a share of the candidates' distances, wave 0 finishes.
@@ -1648,9 +1659,7 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
     if (q >= nq) return;
     const int lane = threadIdx.x & 63;
     const int wv = WV == 1 ? 0 : (int)(threadIdx.x >> 6);
-#if HIPANN_RR_PROF
-    long long rr_t = clock64();
-#endif
+    long long rr_t = HIPANN_RR_PROF ? clock64() : 0;
     // 1. the k best (scan key, row) of the query's partial lists (kslot entries per slot)
     WaveList<1, int> L;
     L.init();
@@ -1675,6 +1684,7 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
     // instead of per-wave lists and serial inserts
     constexpr int RS_J = 16;
     const bool bsel = WV > 1 && total <= (int64_t)64 * WV * RS_J && !rerank_lists();
+    if (WV > 1 && !bsel) RR_COUNT(9);
     constexpr int MU = 4;  // candidate chunks loaded ahead of their offers
     for (int64_t cb = (int64_t)wv * 64; !bsel && cb < total; cb += 64 * WV * MU) {
         float vv[MU];
@@ -1706,8 +1716,7 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
             const unsigned qb = qbound && !sub ? qbound[q] : 0xffffffffu;
             const float bound = sub ? tsub : (qb & 0x80000000u) ? __uint_as_float(qb & 0x7fffffffu) : __builtin_inff();
             RR_MARK(0);
-            rerank_block_select<WV, RS_J>(pd, pi, total, k, nrows, sd, si, scnt, L, bound);
-            RR_MARK(1);
+            rerank_block_select<WV, RS_J>(pd, pi, total, k, nrows, sd, si, scnt, L, bound, rr_t);
             if (wv == 0) srow[lane] = lane < k ? L.id[0] : IdTraits<int>::pad();
         } else {
             sd[wv * 64 + lane] = lane < k ? L.d[0] : __builtin_inff();
@@ -1743,7 +1752,7 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
             }
         }
         __syncthreads();
-        RR_MARK(2);
+        RR_MARK(3);  // distances
         if (wv != 0) return;
         myrow = L.id[0];
         ncand = __popcll(__ballot(lane < k && myrow != IdTraits<int>::pad()));
@@ -1824,7 +1833,7 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
             ivf_scan_order_topk(64, kout, [&](int64_t) { return ScanCand{mk, pos, lab}; }, R);
         }
     }
-    if constexpr (WV > 1) RR_MARK(3);
+    if constexpr (WV > 1) RR_MARK(4);  // (distance, label) order + tie rule
     // 4. exactness check
     const float dk = readlane_f(R.d[0], kout - 1);
     float E;
@@ -1861,7 +1870,7 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
         I[q * kout + lane] = pad ? -1 : (int64_t)R.id[0];
     }
     if constexpr (WV > 1) {
-        RR_MARK(4);
+        RR_MARK(8);  // bound check + write
 #if HIPANN_RR_PROF
         if (lane == 0) atomicAdd(&rr_prof[7], 1ull);
 #endif
@@ -2080,16 +2089,18 @@ void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int 
     HIPANN_CHECK(hipGetLastError());
 }
 
-// tuning builds (HIPANN_RR_PROF): the wide rerank's per-phase clock sums [0..4] and query count [7]; reset after reading
-extern "C" int hipann_debug_rr_prof(unsigned long long *out8) {
+// tuning builds (HIPANN_RR_PROF): the wide rerank's wave-0 clock sums per phase — [0] setup, [1] candidate loads,
+// [5] bound count, [2] compaction / search + sort, [3] distances, [4] order + ties, [8] bound check + write — and the
+// counts [6] compaction path, [9] list path, [7] queries (16 entries); reset after reading
+extern "C" int hipann_debug_rr_prof(unsigned long long *out16) {
 #if HIPANN_RR_PROF
     if (hipDeviceSynchronize() != hipSuccess) return -1;
-    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(rr_prof), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
-    unsigned long long z[8] = {0};
+    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(rr_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+    unsigned long long z[16] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(rr_prof), z, sizeof z) != hipSuccess) return -1;
     return 0;
 #else
-    (void)out8;
+    (void)out16;
     return -1;
 #endif
 }

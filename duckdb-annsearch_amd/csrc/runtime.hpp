@@ -221,7 +221,7 @@ struct IndexBase {
 
 struct FlatIndex : IndexBase {
     std::vector<std::unique_ptr<FlatShard>> shards;
-    int form = kFlatBf16Exact;  // BLAS-path q·x form (FlatForm)
+    int form = kFlatI8Exact;  // BLAS-path q·x form (FlatForm); shapes the int8 passes do not take run kFlatBf16Exact
     int64_t rerank_fallbacks = 0;  // queries re-run on the 3-term path by the exact form's bound check
     int64_t cand_reranked = 0;     // form 4: flagged queries sent to the all-candidate rerank first
     HostBuf h_q, h_d, h_i;

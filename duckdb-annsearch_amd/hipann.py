@@ -249,8 +249,8 @@ class _FlatForm:
     FORM_SPLIT3 = 1        # 3-term split-bf16 products (fp32-level) on the bf16 matrix cores
     FORM_SPLIT2 = 2        # 2-term split (~2^-16 relative per product; measurement only)
     FORM_SPLIT2_EXACT = 3  # the 2-term scan as a filter + exact direct-form rerank with a bound check
-    FORM_BF16_EXACT = 4    # default: one bf16 product per element (tiled bf16 image) as the filter, same rerank
-    FORM_I8_EXACT = 5      # one int8 product per element (tiled int8 image, int32 sums) as the filter, same rerank
+    FORM_BF16_EXACT = 4    # one bf16 product per element (tiled bf16 image) as the filter, same rerank
+    FORM_I8_EXACT = 5      # default (bounded passes: nq >= 256, >= 512K rows, d <= 1024; else form 4): one int8 product per element (tiled int8 image, int32 sums) as the filter, same rerank
 
     @property
     def form(self) -> int:

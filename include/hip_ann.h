@@ -90,7 +90,7 @@ int hipann_flat_reconstruct_n(void *index, int64_t i0, int64_t n, float *out, ch
  * 16 best rows (32 for IP) per database split and query only as a filter; every returned distance is
  * recomputed in FAISS's direct fp32 form (Σ(q−x)² / q·x) and a per-query bound (|scan key − exact| ≤
  * 2^-12·(‖q‖² + max‖x‖²)) proves no pruned row reaches the top-k — queries that fail it re-run on
- * SPLIT3 (k ≤ 12; larger k use SPLIT3).  HIPANN_FLAT_FORM_BF16_EXACT (default): the same filter +
+ * SPLIT3 (k ≤ 12; larger k use SPLIT3).  HIPANN_FLAT_FORM_BF16_EXACT: the same filter +
  * rerank, the scan computing ONE bf16 product per element over a tiled bf16 image of the rows (built
  * once); the bound is the Cauchy-Schwarz bound of the measured bf16 residuals.  Returns 0, or -1 for a
  * bad handle / form. */
@@ -99,11 +99,12 @@ int hipann_flat_reconstruct_n(void *index, int64_t i0, int64_t n, float *out, ch
 #define HIPANN_FLAT_FORM_SPLIT2 2
 #define HIPANN_FLAT_FORM_SPLIT2_EXACT 3
 #define HIPANN_FLAT_FORM_BF16_EXACT 4
-/* HIPANN_FLAT_FORM_I8_EXACT: the BF16_EXACT pipeline with the scan over a tiled int8 image (per-row scale
+/* HIPANN_FLAT_FORM_I8_EXACT (default): the BF16_EXACT pipeline with the scan over a tiled int8 image (per-row scale
  * max|x|/127, round to nearest) on the int8 matrix cores (v_mfma_i32_16x16x64_i8: exact int32 sums, twice the
  * bf16 rate, half its bytes per element) as the filter; a 64-deep filter, the bound from the measured int8
  * residuals of the rows and of each query.  Runs as the bounded passes only (>= 256 queries, >= 512K rows,
- * d <= 1024); elsewhere BF16_EXACT. */
+ * d <= 1024); elsewhere BF16_EXACT.  At 10M x 768, 1024 queries: 9.6 ms per batch against BF16_EXACT's 14.3,
+ * identical ids. */
 #define HIPANN_FLAT_FORM_I8_EXACT 5
 int hipann_flat_set_form(void *index, int form);
 int hipann_flat_get_form(void *index);
@@ -128,9 +129,9 @@ int hipann_last_search_path(void *index, int *form, int *filter_k, int *sublists
  * stream, HIP's convention and PyTorch's default stream).  IVF: the call is asynchronous on that stream —
  * it returns with its kernels still queued (no host synchronisation, the exact forms' flagged queries
  * included: they are re-run on the device).  Flat: the exact forms (HIPANN_FLAT_FORM_SPLIT2_EXACT,
- * HIPANN_FLAT_FORM_BF16_EXACT) synchronise the stream once per call to read the flagged-query count (twice
- * when the bounded passes' candidate rerank ran), and a table's first exact-form search also builds its bf16
- * image and bound; the other forms return with their kernels queued.  Calls on one handle may use different streams: each call
+ * HIPANN_FLAT_FORM_BF16_EXACT, HIPANN_FLAT_FORM_I8_EXACT) synchronise the stream once per call to read the flagged-query count (twice
+ * when the bounded passes' candidate rerank ran), and a table's first exact-form search also builds its bf16 /
+ * int8 image and bound; the other forms return with their kernels queued.  Calls on one handle may use different streams: each call
  * makes its stream wait for an event recorded at the end of the handle's previous call (the per-handle
  * scratch is reused), so they execute in the order they were issued.  The caller still orders its own
  * buffers (queries written / results read on other streams) with its own events.

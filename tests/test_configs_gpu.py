@@ -120,13 +120,13 @@ def test_c2_flat_1m_768_nq1024(gpu, c2_data, c2_oracle, form):
 
 def test_c2_flat_1m_768_request_k30(gpu, c2_data, oracle):
     """C2 with request_k = 30 (k = 10 plus 20 tombstones, faiss_index.cpp:713-715): the bounded passes with a
-    60-candidate filter, exact; the oracle's parity rule on 128 queries."""
+    64-candidate int8 filter (the default form), exact; the oracle's parity rule on 128 queries."""
     import torch
 
     xb_t, xq_t, xb, xq = c2_data
     ix = gpu.HipIndexFlatDevice(768, 0, xb_t.data_ptr(), xb_t.shape[0], 0, copy=False)
     D, I = _dev_search(ix, xq_t, 30, torch)
-    assert ix.last_search_path() == {"form": 4, "filter_k": 60, "sublists": 0}
+    assert ix.last_search_path() == {"form": 5, "filter_k": 64, "sublists": 0}
     Do, Io = oracle.flat_search(xb, xq[:128], 30, 0)
     st = check_topk_parity(xb, xq[:128], D[:128], I[:128], Do, Io, 0)
     assert st["exact_fraction"] >= 0.995, st

@@ -251,7 +251,7 @@ def test_flat_forms_blas_path(gpu, oracle, form, metric, nq, d):
     measurement only) keeps ≈2^-16 relative products, so only its recall is checked."""
     xb, xq = faiss_metal_case(20000, nq, d)  # > 16384 rows: the fused path (smaller tables select from keys)
     ix = gpu.HipIndexFlat(d, metric, xb)
-    assert ix.form == ix.FORM_BF16_EXACT
+    assert ix.form == ix.FORM_I8_EXACT
     ix.form = form
     assert ix.form == form
     D, I = ix.search(xq, 10)
@@ -344,7 +344,7 @@ def test_flat_bf16_flagged_queries_candidate_rerank(gpu, oracle, metric, form):
     xb = xb[rng.permutation(len(xb))]
     xq = rng.standard_normal((256, 64), dtype=np.float32)
     ix = gpu.HipIndexFlat(64, metric, xb)
-    assert ix.form == ix.FORM_BF16_EXACT
+    assert ix.form == ix.FORM_I8_EXACT
     ix.form = form
     D, I = ix.search(xq, 10)
     assert ix.last_search_path()["form"] == form
@@ -439,7 +439,7 @@ def test_flat_bf16_large_batch_buffers_do_not_overflow(gpu, oracle, nq):
     xq = rng.uniform(-1, 1, (nq, d)).astype(np.float32)
     ix = gpu.HipIndexFlat(d, 0, xb)
     D, I = ix.search(xq, 10)
-    assert ix.last_search_path()["form"] == ix.FORM_BF16_EXACT
+    assert ix.last_search_path()["form"] == ix.FORM_I8_EXACT
     assert ix.rerank_fallbacks() <= nq // 100, ix.rerank_fallbacks()
     ix.form = ix.FORM_FP32
     D0, I0 = ix.search(xq, 10)
