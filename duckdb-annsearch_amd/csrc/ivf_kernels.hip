@@ -1286,6 +1286,9 @@ __device__ __forceinline__ void rerank_rows4(const float *__restrict__ qp, const
     }
 }
 
+#ifndef HIPANN_RR_OLDSEL
+#define HIPANN_RR_OLDSEL 0  // A/B builds: the 32-barrier block select instead of rerank_wave_select
+#endif
 #ifndef HIPANN_RR_PROF
 #define HIPANN_RR_PROF 0  // tuning builds: wave 0's per-phase shader clocks of the wide rerank, summed in rr_prof
 #endif
@@ -1438,6 +1441,177 @@ __device__ __forceinline__ void rerank_block_select(const float *__restrict__ pd
     RR_MARK(2);  // 32-step search + compaction + sort
 }
 
+
+// The k best scan keys of a query's ≤ 64·WV·J candidates with ONE block barrier (rerank_block_select needs 32):
+//   1. each wave loads its candidates (key, row) (c = (j·WV + wave)·64 + lane) in one round trip;
+//   2. compacts the keys ≤ bound (finite, row in range) into its own LDS run in (j, lane) order, then finds its
+//      run's k best by
+//      a wave-local bitwise search (32 steps of ⌈m/64⌉ ballots, no barrier) — the bound (the scan's final
+//      per-query bound) usually leaves a few dozen per wave;
+//   3. after the barrier wave 0 takes the ≤ WV·k survivors, selects the k best the same way and sorts them by
+//      (key, row) (wave_rank_sort).
+// Ties at the k-th key keep the first in (wave, position) order — any choice is harmless: every row left out
+// still has scan key ≥ K_k, all the bound check assumes.
+// Ascending (key, id) order of the first n lanes' pairs (n ≤ 64, wave-uniform; lanes ≥ n end as (+inf, pad)):
+// each lane counts the pairs below its own (n broadcasts, no shuffle chain), then one ds_permute per word moves
+// every pair to its rank.  Keys compare as order-preserving bits (−0 = +0, NaN last), equal pairs by lane, so the
+// ranks are a permutation whatever the input.
+template <typename IdT>
+__device__ __forceinline__ void wave_rank_sort(float &k, IdT &id, int n) {
+    const int lane = threadIdx.x & 63;
+    const float kz = k == 0.f ? 0.f : k;
+    const unsigned kb = k == k ? ((__float_as_uint(kz) >> 31) ? ~__float_as_uint(kz) : (__float_as_uint(kz) | 0x80000000u))
+                               : 0xffffffffu;
+    int rank = 0;
+    for (int j = 0; j < n; ++j) {
+        const unsigned bj = (unsigned)__builtin_amdgcn_readlane((int)kb, j);
+        const IdT ij = readlane_i(id, j);
+        rank += (bj < kb || (bj == kb && (ij < id || (ij == id && j < lane)))) ? 1 : 0;
+    }
+    const bool live = lane < n;
+    const int dst = (live ? rank : lane) << 2;  // lanes >= n keep their place (their pads stay pads)
+    const float kr = __int_as_float(__builtin_amdgcn_ds_permute(dst, __float_as_int(live ? k : __builtin_inff())));
+    IdT ir;
+    if constexpr (sizeof(IdT) == 8) {
+        const unsigned long long u = (unsigned long long)(live ? id : IdTraits<IdT>::pad());
+        const unsigned lo = (unsigned)__builtin_amdgcn_ds_permute(dst, (int)(unsigned)(u & 0xffffffffull));
+        const unsigned hi = (unsigned)__builtin_amdgcn_ds_permute(dst, (int)(unsigned)(u >> 32));
+        ir = (IdT)(((unsigned long long)hi << 32) | lo);
+    } else {
+        ir = (IdT)__builtin_amdgcn_ds_permute(dst, (int)(live ? id : IdTraits<IdT>::pad()));
+    }
+    k = lane < n ? kr : __builtin_inff();
+    id = lane < n ? ir : IdTraits<IdT>::pad();
+}
+
+template <int J>
+__device__ __forceinline__ unsigned rws_kth_bits(const float *__restrict__ mk, int m, int k, unsigned &n_lt_out) {
+    const int lane = threadIdx.x & 63;
+    const int nj = (m + 63) >> 6;
+    unsigned u[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int e = j * 64 + lane;
+        float f = j < nj && e < m ? mk[e] : __builtin_inff();
+        f = f == 0.f ? 0.f : f;
+        const unsigned b = __float_as_uint(f);
+        u[j] = j < nj && e < m ? ((b >> 31) ? ~b : (b | 0x80000000u)) : 0xffffffffu;
+    }
+    unsigned T = 0;
+    for (int bit = 31; bit >= 0; --bit) {
+        const unsigned cand = T | (1u << bit);
+        int cnt = 0;
+#pragma unroll
+        for (int j = 0; j < J; ++j)
+            if (j < nj) cnt += __popcll(__ballot(u[j] < cand));
+        if (cnt < k) T = cand;
+    }
+    (void)n_lt_out;
+    return T;
+}
+__device__ __forceinline__ unsigned rws_bits(float f) {
+    f = f == 0.f ? 0.f : f;
+    const unsigned b = __float_as_uint(f);
+    return (b >> 31) ? ~b : (b | 0x80000000u);
+}
+// Copy the ≤ k best of run (mk, mp)[0, m) — keys < T, then the first keys == T — to (ok, op); returns the count.
+template <int J>
+__device__ __forceinline__ int rws_take(const float *__restrict__ mk, const int *__restrict__ mp, int m, int k, unsigned T,
+                                        float *__restrict__ ok, int *__restrict__ op) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    const int nj = (m + 63) >> 6;
+    int base = 0;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int e = j * 64 + lane;
+        const bool a = j < nj && e < m && rws_bits(mk[e]) < T;
+        const unsigned long long ma = __ballot(a);
+        if (a) { const int p = base + __popcll(ma & lt); ok[p] = mk[e]; op[p] = mp[e]; }
+        base += __popcll(ma);
+    }
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int e = j * 64 + lane;
+        const bool b = j < nj && e < m && rws_bits(mk[e]) == T;
+        const unsigned long long mb = __ballot(b);
+        if (b) { const int p = base + __popcll(mb & lt); if (p < k) { ok[p] = mk[e]; op[p] = mp[e]; } }
+        base += __popcll(mb);
+    }
+    return base < k ? base : k;
+}
+template <int WV, int J>
+__device__ __forceinline__ void rerank_wave_select(const float *__restrict__ pd, const int *__restrict__ pi,
+                                                   int64_t total, int k, int64_t nrows, float bound,
+                                                   float *wk, int *wp, float *sk, int *sp, int *scnt,
+                                                   WaveList<1, int> &L, bool &bad, long long &rr_t) {
+    (void)rr_t;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    float v[J];
+    int r[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int64_t c = ((int64_t)j * WV + wv) * 64 + lane;
+        v[j] = c < total ? pd[c] : __builtin_inff();
+        r[j] = c < total ? pi[c] : -1;
+    }
+    RR_MARK(1);  // candidate loads issued
+    float *mk = wk + wv * 64 * J;
+    int *mp = wp + wv * 64 * J;
+    int m = 0;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        // NaN and +inf never; rows out of range never (pads)
+        const bool a = v[j] <= bound && !(v[j] == __builtin_inff()) && r[j] >= 0 && r[j] < nrows;
+        const unsigned long long ma = __ballot(a);
+        if (a) { const int p = m + __popcll(ma & lt); mk[p] = v[j]; mp[p] = r[j]; }
+        m += __popcll(ma);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the run's LDS writes before this wave reads it
+    int kw;
+    if (m <= k) {
+        kw = m;
+        for (int e = lane; e < m; e += 64) { sk[wv * 64 + e] = mk[e]; sp[wv * 64 + e] = mp[e]; }
+    } else {
+        unsigned dummy = 0;
+        const unsigned T = rws_kth_bits<J>(mk, m, k, dummy);
+        kw = rws_take<J>(mk, mp, m, k, T, sk + wv * 64, sp + wv * 64);
+    }
+    if (lane == 0) scnt[wv] = kw;
+    RR_MARK(5);  // wave-local select
+    __syncthreads();
+    if (wv != 0) return;
+    // wave 0: the ≤ WV·k survivors, in wave order, compacted into its own run, then the k best
+    int m0 = 0;
+#pragma unroll
+    for (int w = 0; w < WV; ++w) {
+        const int n = scnt[w];
+        const bool a = lane < n;
+        float kk = a ? sk[w * 64 + lane] : 0.f;
+        int pp = a ? sp[w * 64 + lane] : 0;
+        if (a) { mk[m0 + lane] = kk; mp[m0 + lane] = pp; }
+        m0 += n;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    int nsel = m0;
+    if (m0 > k) {
+        unsigned dummy = 0;
+        const unsigned T = rws_kth_bits<WV>(mk, m0, k, dummy);
+        nsel = rws_take<WV>(mk, mp, m0, k, T, sk, sp);  // wave 0's survivor slots are free again
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    } else {
+        for (int e = lane; e < m0; e += 64) { sk[e] = mk[e]; sp[e] = mp[e]; }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+    float kk = lane < nsel ? sk[lane] : __builtin_inff();
+    int row = lane < nsel ? sp[lane] : IdTraits<int>::pad();
+    wave_rank_sort(kk, row, nsel);
+    bad = false;
+    L.d[0] = lane < k ? kk : __builtin_inff();
+    L.id[0] = lane < k ? row : IdTraits<int>::pad();
+    RR_MARK(2);  // merge + sort
+}
 
 // ---------------------------------------------------------------------------------------------
 // FAISS IndexIVFFlat's exact-tie membership.  Its scanner admits a candidate only when it is strictly
@@ -1705,6 +1879,10 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
     float mine = __builtin_inff();
     int myrow, ncand;
     float k16;
+    bool sel_bad = false;  // a selected candidate with an out-of-range row id (rerank_wave_select): flag the query
+    // the per-query scalars of the bound check, loaded now (their latency hides under the candidate loads)
+    const float qn_pre = qres && qnorm ? qnorm[q] : 0.f;
+    const float qres_pre = qres ? qres[q] : 0.f;
     if constexpr (WV > 1) {
         __shared__ float sd[WV * 64], sdist[64];
         __shared__ int si[WV * 64], srow[64];
@@ -1713,10 +1891,22 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
             // the scan's final bound (order-preserving bits of a full slot list's k-th key, atomicMin'ed): >= the
             // k-th smallest key of the query's candidates
             // (sub-lists: T_sub — the candidates above it are irrelevant, see above)
-            const unsigned qb = qbound && !sub ? qbound[q] : 0xffffffffu;
-            const float bound = sub ? tsub : (qb & 0x80000000u) ? __uint_as_float(qb & 0x7fffffffu) : __builtin_inff();
+            float bound = __builtin_inff();
+            if (sub) {
+                bound = tsub;
+            } else if (qbound) {
+                const unsigned qb = qbound[q];
+                const float t = __uint_as_float((qb & 0x80000000u) ? (qb & 0x7fffffffu) : ~qb);
+                bound = t == t ? t : __builtin_inff();
+            }
             RR_MARK(0);
+#if HIPANN_RR_OLDSEL
             rerank_block_select<WV, RS_J>(pd, pi, total, k, nrows, sd, si, scnt, L, bound, rr_t);
+#else
+            __shared__ float wk[WV * 64 * RS_J];
+            __shared__ int wp[WV * 64 * RS_J];
+            rerank_wave_select<WV, RS_J>(pd, pi, total, k, nrows, bound, wk, wp, sd, si, scnt[0], L, sel_bad, rr_t);
+#endif
             if (wv == 0) srow[lane] = lane < k ? L.id[0] : IdTraits<int>::pad();
         } else {
             sd[wv * 64 + lane] = lane < k ? L.d[0] : __builtin_inff();
@@ -1767,7 +1957,7 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
     // 2. exact direct-form distances of the candidates (4 rows in flight, wave reduction per row)
     float qq = 0.f, rq2 = 0.f;
     if (qres && qnorm) {
-        qq = qnorm[q];  // the IVF fp16 form: ‖q‖² prepared with the query terms, its own split residual in qres
+        qq = qn_pre;  // the IVF fp16 form: ‖q‖² prepared with the query terms, its own split residual in qres
     } else {
         int e = lane;
         for (; e + 192 < d; e += 256) {  // 4 strides of loads in flight, sums in e order
@@ -1815,9 +2005,15 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
     }
     // 3. (distance, label) order, first kout
     WaveList<1, long long> R;
-    R.init();
     const long long lab = real ? (long long)(ids ? ids[myrow] : label_offset + myrow) : IdTraits<long long>::pad();
-    R.offer(real ? mine : __builtin_inff(), lab, kout - 1);
+    {
+        // the ncand reranked candidates sit in lanes < ncand: their (distance, label) order by rank (no insert chain)
+        float rk = real ? mine : __builtin_inff();
+        long long rl = lab;
+        wave_rank_sort(rk, rl, ncand);
+        R.d[0] = rk;
+        R.id[0] = rl;
+    }
     // 3b. exact ties at the kout-th distance with more tied rows than slots left: FAISS's scan-order
     // admission decides which tied labels stay (ivf_scan_order_topk).  Every row with distance <= the
     // kout-th is among the candidates whenever the bound check below passes (they all have scan key
@@ -1839,7 +2035,7 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
     float E;
     if (rxmax >= 0.f) {
         // qres (IVF fp16 form): the query's own split residual, and 2d products per accumulator chain
-        const float qn = sqrtf(qq), rq = qres ? qres[q] : sqrtf(rq2), xh = sqrtf(xmax2) + rxmax;
+        const float qn = sqrtf(qq), rq = qres ? qres_pre : sqrtf(rq2), xh = sqrtf(xmax2) + rxmax;
         const float g = (float)(qres ? 2 * d : d) * 0x1p-24f;
         const float eip = qn * rxmax + rq * xh + g * (qn + rq) * xh;
         E = 1.01f * ((IP ? 1.f : 2.f) * eip + (float)(d + 8) * 0x1p-24f * 2.f * (qq + xmax2));
@@ -1850,7 +2046,7 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
     // has no candidate at all: empty probe lists, or the Flat bounded passes' overflowed query, which
     // flat_cand_select already flagged (flagged holds nq entries: no query may be appended twice); sub-lists: the
     // kout-th distance must also clear the smallest full sub-list's k-th key
-    const bool flag = (ncand > 0 && !(E <= 3.4e38f)) || (ncand == k && !(dk < k16 - E)) ||
+    const bool flag = sel_bad || (ncand > 0 && !(E <= 3.4e38f)) || (ncand == k && !(dk < k16 - E)) ||
                       (sub && tsub < __builtin_inff() && !(dk < tsub - E));
     if (flag && lane == 0) flagged[atomicAdd(nflag, 1)] = (int)q;
     const float pad_d = IP ? -__builtin_inff() : __builtin_inff();
