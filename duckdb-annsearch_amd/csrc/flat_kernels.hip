@@ -1150,7 +1150,7 @@ rows_select_small(const float *__restrict__ keys, int64_t ldk, int ncols, int64_
     if (ccnt && live) {  // the IVF plan's per-query step (ivf_count_q) on the probes just selected (kout ≤ 64)
         const int64_t l = lane < kout && !pad ? (int64_t)cc + label_offset : -1;
         const int len = l >= 0 && l < nlist ? list_len[l] : 0;
-        if (len > 0) atomicAdd(ccnt + l, 1);
+        if (len > 0) atomicAdd(ccnt + (int64_t)(q % kPlanCopies) * nlist + l, 1);
         const int v = len > 0 ? (len + chunk_rows - 1) / chunk_rows : 0;
         int x = v;
 #pragma unroll
@@ -1248,7 +1248,7 @@ rows_select_block(const float *__restrict__ keys, int64_t ldk, int ncols, int64_
     if (ccnt) {  // the IVF plan's per-query step (ivf_count_q) on the probes just selected (kout ≤ 64)
         const int64_t l = lane < kout && !pad ? (int64_t)cc + label_offset : -1;
         const int len = l >= 0 && l < nlist ? list_len[l] : 0;
-        if (len > 0) atomicAdd(ccnt + l, 1);
+        if (len > 0) atomicAdd(ccnt + (int64_t)(q % kPlanCopies) * nlist + l, 1);
         const int vv = len > 0 ? (len + chunk_rows - 1) / chunk_rows : 0;
         int x = vv;
 #pragma unroll

@@ -224,16 +224,17 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     // per-list counts and fill cursors, double-buffered by batch parity (ivf_planfill_q zeroes the other
     // parity's pair for the next batch; ivf_plan_q zeroes its own after use) — zeroed once per list count
     if (!sh.ccnt.p || !sh.cursor2.p || sh.plan_nlist != nlist) {
-        sh.ccnt.ensure(sizeof(int) * 2 * (size_t)nlist, sh.device);
-        sh.cursor2.ensure(sizeof(int) * 2 * (size_t)nlist, sh.device);
-        HIPANN_CHECK(hipMemsetAsync(sh.ccnt.p, 0, sizeof(int) * 2 * (size_t)nlist, st));
-        HIPANN_CHECK(hipMemsetAsync(sh.cursor2.p, 0, sizeof(int) * 2 * (size_t)nlist, st));
+        sh.ccnt.ensure(sizeof(int) * 2 * kPlanCopies * (size_t)nlist, sh.device);
+        sh.cursor2.ensure(sizeof(int) * 2 * kPlanCopies * (size_t)nlist, sh.device);
+        HIPANN_CHECK(hipMemsetAsync(sh.ccnt.p, 0, sizeof(int) * 2 * kPlanCopies * (size_t)nlist, st));
+        HIPANN_CHECK(hipMemsetAsync(sh.cursor2.p, 0, sizeof(int) * 2 * kPlanCopies * (size_t)nlist, st));
         sh.plan_nlist = nlist;
         sh.plan_batch = 0;
     }
     const int par = (int)(sh.plan_batch & 1u);
-    int *ccnt_cur = sh.ccnt.get<int>() + (size_t)par * nlist, *ccnt_next = sh.ccnt.get<int>() + (size_t)(1 - par) * nlist;
-    int *cur_cur = sh.cursor2.get<int>() + (size_t)par * nlist, *cur_next = sh.cursor2.get<int>() + (size_t)(1 - par) * nlist;
+    const size_t pstride = (size_t)kPlanCopies * nlist;  // one parity's [copy][list] counts / cursors
+    int *ccnt_cur = sh.ccnt.get<int>() + par * pstride, *ccnt_next = sh.ccnt.get<int>() + (1 - par) * pstride;
+    int *cur_cur = sh.cursor2.get<int>() + par * pstride, *cur_next = sh.cursor2.get<int>() + (1 - par) * pstride;
     sh.qtot.ensure(sizeof(int) * (size_t)nq, sh.device);
     // this batch's counts must be zero on entry; the coarse select's count step adds to them, so if anything
     // throws before the plan has consumed them, zero them again on the way out
@@ -243,7 +244,8 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
         hipStream_t st;
         bool armed;
         ~CcntReset() {
-            if (armed && std::uncaught_exceptions() > 0) (void)hipMemsetAsync(p, 0, sizeof(int) * (size_t)nlist, st);
+            if (armed && std::uncaught_exceptions() > 0)
+                (void)hipMemsetAsync(p, 0, sizeof(int) * kPlanCopies * (size_t)nlist, st);
         }
     } ccnt_reset{ccnt_cur, nlist, st, true};
     // the decomposed form needs float4 rows; other shapes take the direct kernel (also on the GPU)

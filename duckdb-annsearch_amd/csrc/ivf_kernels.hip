@@ -32,7 +32,10 @@ constexpr int IVF_QW = IVF_G / IVF_WAVES;  // queries per wave
 constexpr int IVF_TR = 256;             // list rows per tile (4 per lane)
 constexpr int IVF_BK = 24;              // dims per LDS chunk
 constexpr int IVF_LD = IVF_BK + 4;      // padded row stride: 28 dwords → 16 rows hit 16 distinct b128 slots
-constexpr int IVF_CH = 2048;            // list rows per work item (big lists split into chunks)
+#ifndef HIPANN_IVF_CH
+#define HIPANN_IVF_CH 2048  // tuning builds: list rows per work item
+#endif
+constexpr int IVF_CH = HIPANN_IVF_CH;   // list rows per work item (big lists split into chunks)
 
 __device__ __forceinline__ int ivf_nch(int len) { return (len + IVF_CH - 1) / IVF_CH; }
 
@@ -181,7 +184,7 @@ __global__ void __launch_bounds__(256) ivf_count_q(const int64_t *__restrict__ p
         const int64_t l = p < nprobe ? probes[i] : -1;
         const bool ok = l >= 0 && l < nlist;
         const int len = ok ? list_len[l] : 0;
-        if (len > 0) atomicAdd(ccnt + l, 1);
+        if (len > 0) atomicAdd(ccnt + (int64_t)(q % kPlanCopies) * nlist + l, 1);
         const int v = len > 0 ? ivf_nch(len) : 0;
         int x = v;
 #pragma unroll
@@ -211,7 +214,9 @@ __global__ void __launch_bounds__(1024) ivf_plan_q(int *__restrict__ ccnt, const
     __syncthreads();
     for (int base = 0; base < nlist; base += 1024) {
         const int l = base + tid;
-        const int c = l < nlist ? ccnt[l] : 0;
+        int c = 0;
+        if (l < nlist)
+            for (int cp = 0; cp < kPlanCopies; ++cp) c += ccnt[(int64_t)cp * nlist + l];
         const int items = l < nlist ? ((c + group - 1) / group) * ivf_nch(list_len[l]) : 0;
         sb[tid] = c;
         si[tid] = items;
@@ -226,10 +231,16 @@ __global__ void __launch_bounds__(1024) ivf_plan_q(int *__restrict__ ccnt, const
         }
         if (l < nlist) {
             cnt[l] = c;
-            ccnt[l] = 0;
             bucket_off[l] = carry_b + sb[tid] - c;
             item_off[l] = carry_i + si[tid] - items;
-            cursor[l] = 0;
+            int pre = 0;  // copy cp's fills start after copies 0..cp-1 (ivf_fill_q adds to its copy's cursor)
+            for (int cp = 0; cp < kPlanCopies; ++cp) {
+                const int64_t e = (int64_t)cp * nlist + l;
+                const int n = ccnt[e];
+                cursor[e] = pre;
+                ccnt[e] = 0;
+                pre += n;
+            }
         }
         __syncthreads();
         if (tid == 1023) { carry_b += sb[1023]; carry_i += si[1023]; }
@@ -274,7 +285,7 @@ __global__ void __launch_bounds__(256) ivf_fill_q(const int64_t *__restrict__ pr
         slot_off[i] += b;
         const int64_t l = probes[i];
         if (l < 0 || l >= nlist || list_len[l] <= 0) continue;
-        const int pos = atomicAdd(cursor + l, 1);
+        const int pos = atomicAdd(cursor + (int64_t)(q % kPlanCopies) * nlist + l, 1);
         bucket[bucket_off[l] + pos] = (int)i;
     }
 }
@@ -320,7 +331,8 @@ __global__ void __launch_bounds__(256) ivf_planfill_q(const int64_t *__restrict_
     for (int j = 0; j < per; ++j) {
         const int l = tid * per + j;
         if (l < nlist) {
-            const int c = ccnt[l];
+            int c = 0;
+            for (int cp = 0; cp < kPlanCopies; ++cp) c += ccnt[(int64_t)cp * nlist + l];
             sum += c;
             if (blockIdx.x == 0) isum += ((c + group - 1) / group) * ivf_nch(list_len[l]);
         }
@@ -330,7 +342,8 @@ __global__ void __launch_bounds__(256) ivf_planfill_q(const int64_t *__restrict_
     for (int j = 0; j < per; ++j) {
         const int l = tid * per + j;
         if (l < nlist) {
-            const int c = ccnt[l];
+            int c = 0;
+            for (int cp = 0; cp < kPlanCopies; ++cp) c += ccnt[(int64_t)cp * nlist + l];
             s_boff[l] = b;
             if (blockIdx.x == 0) {
                 cnt[l] = c;
@@ -346,7 +359,7 @@ __global__ void __launch_bounds__(256) ivf_planfill_q(const int64_t *__restrict_
         item_off[nlist] = ib;
     }
     // the next batch's counts and cursors start at zero (each block clears a slice)
-    for (int l = (int)blockIdx.x * 256 + tid; l < nlist; l += (int)gridDim.x * 256) {
+    for (int64_t l = (int64_t)blockIdx.x * 256 + tid; l < (int64_t)kPlanCopies * nlist; l += (int64_t)gridDim.x * 256) {
         ccnt_next[l] = 0;
         cursor_next[l] = 0;
     }
@@ -376,8 +389,12 @@ __global__ void __launch_bounds__(256) ivf_planfill_q(const int64_t *__restrict_
         slot_off[i] += base;
         const int64_t l = probes[i];
         if (l < 0 || l >= nlist || list_len[l] <= 0) continue;
-        const int pos = atomicAdd(cursor + l, 1);
-        bucket[s_boff[l] + pos] = (int)i;
+        // this query's copy of the list's cursor; its rows follow copies 0..cp-1 in the list's bucket
+        const int cp = (int)(q % kPlanCopies);
+        int pre = 0;
+        for (int c2 = 0; c2 < cp; ++c2) pre += ccnt[(int64_t)c2 * nlist + l];
+        const int pos = atomicAdd(cursor + (int64_t)cp * nlist + l, 1);
+        bucket[s_boff[l] + pre + pos] = (int)i;
     }
 }
 
@@ -1147,8 +1164,8 @@ void launch_ivf_plan(const int64_t *probes, int64_t nq, int nprobe, const int *l
         if (nq > 0)
             hipLaunchKernelGGL(ivf_fill_q, dim3(gq), dim3(256), 0, st, probes, nq, nprobe, list_len, nlist, qtot,
                                bucket_off, cursor, bucket, slot_off);
-        if (cursor_next)  // the fused path expects the other parity's cursors at zero (ivf_plan_q zeroed this one)
-            HIPANN_CHECK(hipMemsetAsync(cursor_next, 0, sizeof(int) * (size_t)nlist, st));
+        if (cursor_next)  // the fused path expects the other parity's cursors at zero
+            HIPANN_CHECK(hipMemsetAsync(cursor_next, 0, sizeof(int) * kPlanCopies * (size_t)nlist, st));
         HIPANN_CHECK(hipGetLastError());
         return;
     }

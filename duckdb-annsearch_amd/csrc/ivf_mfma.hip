@@ -55,7 +55,10 @@ typedef float mf_f32x4 __attribute__((ext_vector_type(4)));
 #endif
 constexpr int MF_WAVES = HIPANN_MF_WAVES;
 constexpr int MF_THREADS = 64 * MF_WAVES;
-constexpr int MF_CH = 2048;   // rows per item (= IVF_CH of ivf_kernels.hip)
+#ifndef HIPANN_IVF_CH
+#define HIPANN_IVF_CH 2048
+#endif
+constexpr int MF_CH = HIPANN_IVF_CH;   // rows per item (= IVF_CH of ivf_kernels.hip)
 constexpr int MF_PASS = 32;   // rows per wave pass (2 MFMA row tiles)
 constexpr int MF_RT = 2;      // row tiles per pass
 constexpr int MF_P = HIPANN_MF_P;  // sixteen-dim steps in flight per wave (register ring depth)
