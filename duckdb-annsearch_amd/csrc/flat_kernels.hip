@@ -1167,7 +1167,9 @@ rows_select_small(const float *__restrict__ keys, int64_t ldk, int ncols, int64_
 // block of 4 waves (column c = 256·wave + 64·j + lane, J = 4 registers per lane); each search step sums
 // the waves' ballot counts through LDS (one barrier), the compaction runs in (wave, j, lane) = column
 // order, and wave 0 sorts and writes the output (and the IVF plan's count step).  A quarter of the
-// per-wave ballot chain of the one-wave version (16 µs for 1024 × 1024 keys).
+// per-wave ballot chain of the one-wave version (16 µs for 1024 × 1024 keys).  Measured and rejected (r04): a
+// one-barrier variant (each wave selects its 256 columns' k best, wave 0 merges): 13.5 µs, the same — the
+// barriers are not the critical path.
 __global__ void __launch_bounds__(256)
 rows_select_block(const float *__restrict__ keys, int64_t ldk, int ncols, int64_t nq, int k, int kout,
                   int64_t label_offset, float out_sign, float *__restrict__ D, int64_t *__restrict__ I,
@@ -1260,6 +1262,7 @@ rows_select_block(const float *__restrict__ keys, int64_t ldk, int ncols, int64_
         if (lane == 63) qtot[q] = x;
     }
 }
+
 
 // Raw merge: nparts partial [part][nq][k] (keys, int ids) → one [nq][k] partial (keys, int ids).
 template <int S>

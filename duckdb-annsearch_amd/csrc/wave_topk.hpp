@@ -83,6 +83,38 @@ __device__ __forceinline__ void wave_sort(float &k, IdT &id) {
         }
 }
 
+// Ascending (key, id) order of the first n lanes' pairs (n ≤ 64, wave-uniform; lanes ≥ n end as (+inf, pad)):
+// each lane counts the pairs below its own (n broadcasts, no shuffle chain), then one ds_permute per word moves
+// every pair to its rank.  Keys compare as order-preserving bits (−0 = +0, NaN last), equal pairs by lane, so the
+// ranks are a permutation whatever the input.
+template <typename IdT>
+__device__ __forceinline__ void wave_rank_sort(float &k, IdT &id, int n) {
+    const int lane = threadIdx.x & 63;
+    const float kz = k == 0.f ? 0.f : k;
+    const unsigned kb = k == k ? ((__float_as_uint(kz) >> 31) ? ~__float_as_uint(kz) : (__float_as_uint(kz) | 0x80000000u))
+                               : 0xffffffffu;
+    int rank = 0;
+    for (int j = 0; j < n; ++j) {
+        const unsigned bj = (unsigned)__builtin_amdgcn_readlane((int)kb, j);
+        const IdT ij = readlane_i(id, j);
+        rank += (bj < kb || (bj == kb && (ij < id || (ij == id && j < lane)))) ? 1 : 0;
+    }
+    const bool live = lane < n;
+    const int dst = (live ? rank : lane) << 2;  // lanes >= n keep their place (their pads stay pads)
+    const float kr = __int_as_float(__builtin_amdgcn_ds_permute(dst, __float_as_int(live ? k : __builtin_inff())));
+    IdT ir;
+    if constexpr (sizeof(IdT) == 8) {
+        const unsigned long long u = (unsigned long long)(live ? id : IdTraits<IdT>::pad());
+        const unsigned lo = (unsigned)__builtin_amdgcn_ds_permute(dst, (int)(unsigned)(u & 0xffffffffull));
+        const unsigned hi = (unsigned)__builtin_amdgcn_ds_permute(dst, (int)(unsigned)(u >> 32));
+        ir = (IdT)(((unsigned long long)hi << 32) | lo);
+    } else {
+        ir = (IdT)__builtin_amdgcn_ds_permute(dst, (int)(live ? id : IdTraits<IdT>::pad()));
+    }
+    k = lane < n ? kr : __builtin_inff();
+    id = lane < n ? ir : IdTraits<IdT>::pad();
+}
+
 // One wave-distributed list of 64*S elements.
 template <int S, typename IdT = int>
 struct WaveList {
