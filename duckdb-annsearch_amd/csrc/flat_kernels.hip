@@ -1141,7 +1141,7 @@ rows_select_small(const float *__restrict__ keys, int64_t ldk, int ncols, int64_
     __syncthreads();
     float kk = lane < nsel ? sk[wv][lane] : __builtin_inff();
     int cc = lane < nsel ? sc[wv][lane] : 0x7fffffff;
-    wave_sort(kk, cc);
+    wave_rank_sort(kk, cc, nsel);
     const bool pad = lane >= nsel || kk == __builtin_inff();
     if (live && lane < kout) {
         D[q * kout + lane] = pad ? (out_sign > 0.f ? __builtin_inff() : -__builtin_inff()) : kk * out_sign;
@@ -1241,7 +1241,7 @@ rows_select_block(const float *__restrict__ keys, int64_t ldk, int ncols, int64_
     if (wv != 0) return;
     float kk = lane < nsel ? sk[lane] : __builtin_inff();
     int cc = lane < nsel ? sc[lane] : 0x7fffffff;
-    wave_sort(kk, cc);
+    wave_rank_sort(kk, cc, nsel);
     const bool pad = lane >= nsel || kk == __builtin_inff();
     if (lane < kout) {
         D[q * kout + lane] = pad ? (out_sign > 0.f ? __builtin_inff() : -__builtin_inff()) : kk * out_sign;
