@@ -1615,106 +1615,6 @@ flat_keys_ksplit(const float *__restrict__ Q, const float *__restrict__ qnorm, i
     }
 }
 
-// flat_keys_kparts — flat_keys_ksplit with the k chunks over KP groups of 4 waves (KP = 4: 16 waves, four per SIMD,
-// each group a quarter of the chunks in its own two LDS buffers, dynamic LDS 4 × 36 KB): each group's chunk chain is
-// 1/KP of the tile's, so the load latency of a chunk (the queries and centroids come from L2 / the Infinity Cache)
-// is hidden by the other groups' MFMAs.  Groups 1..KP−1 hand their accumulators to group 0 through LDS, which
-// adds them in group order (deterministic; the coarse keys are not bit-pinned to a CPU order).  HIPANN_KEYS = 4.
-template <bool VEC4, int KP>
-__global__ void __launch_bounds__(256 * KP)
-flat_keys_kparts(const float *__restrict__ Q, const float *__restrict__ qnorm, int64_t nq, const float *__restrict__ X,
-                 const float *__restrict__ xnorm, int64_t N, int d, int metric, int nqt, float *__restrict__ keys_out,
-                 int64_t ldk) {
-    extern __shared__ __attribute__((aligned(16))) float kp_smem[];
-    constexpr int BUF = SBM * GLD;  // one 64-row × 32-dim staging buffer (padded rows)
-    const int lb = xcd_remap(blockIdx.x, gridDim.x);
-    const int qt = lb % nqt;
-    const int64_t q0 = (int64_t)qt * SBM, x0 = (int64_t)(lb / nqt) * SBM;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int part = wave >> 2, t = threadIdx.x & 255;
-    const int wr = (wave >> 1) & 1, wc = wave & 1;
-    const int l31 = lane & 31, h = lane >> 5;
-    float *As0 = kp_smem + (size_t)part * 4 * BUF, *As1 = As0 + BUF, *Bs0 = As0 + 2 * BUF, *Bs1 = As0 + 3 * BUF;
-    const int nkp = ((d + GBK - 1) / GBK) / KP;  // chunks per group (the launcher checks divisibility)
-    const int kbase = part * nkp * GBK;
-    float4 sa[2][2], sb[2][2];
-    ks_stage_load<VEC4>(Q, q0, nq, d, kbase, t, sa[0]);
-    ks_stage_load<VEC4>(X, x0, N, d, kbase, t, sb[0]);
-    ks_stage_store(As0, t, sa[0]);
-    ks_stage_store(Bs0, t, sb[0]);
-    if (nkp > 1) {
-        ks_stage_load<VEC4>(Q, q0, nq, d, kbase + GBK, t, sa[1]);
-        ks_stage_load<VEC4>(X, x0, N, d, kbase + GBK, t, sb[1]);
-    }
-    if (nkp > 2) {
-        ks_stage_load<VEC4>(Q, q0, nq, d, kbase + 2 * GBK, t, sa[0]);
-        ks_stage_load<VEC4>(X, x0, N, d, kbase + 2 * GBK, t, sb[0]);
-    }
-    __syncthreads();
-    f32x16 acc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    auto step = [&](int kc, auto par_c) {
-        constexpr int P = decltype(par_c)::value;
-        const float *Ab = P ? As1 : As0, *Bb = P ? Bs1 : Bs0;
-        f32x4 a4[4], b4[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            a4[u] = *reinterpret_cast<const f32x4 *>(Ab + (32 * wr + l31) * GLD + 16 * h + 4 * u);
-            b4[u] = *reinterpret_cast<const f32x4 *>(Bb + (32 * wc + l31) * GLD + 16 * h + 4 * u);
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[u][e], b4[u][e], acc, 0, 0, 0);
-        if (kc + 1 < nkp) {
-            ks_stage_store(P ? As0 : As1, t, sa[1 - P]);
-            ks_stage_store(P ? Bs0 : Bs1, t, sb[1 - P]);
-            if (kc + 3 < nkp) {
-                ks_stage_load<VEC4>(Q, q0, nq, d, kbase + (kc + 3) * GBK, t, sa[1 - P]);
-                ks_stage_load<VEC4>(X, x0, N, d, kbase + (kc + 3) * GBK, t, sb[1 - P]);
-            }
-        }
-        __syncthreads();
-    };
-    for (int kc = 0; kc < nkp; kc += 2) {
-        step(kc, std::integral_constant<int, 0>{});
-        if (kc + 1 < nkp) step(kc + 1, std::integral_constant<int, 1>{});
-    }
-    // groups 1..KP−1 → LDS (every staging read finished before the last barrier) → group 0 adds them in order
-    if (part > 0) {
-        float *xch = kp_smem + (size_t)(part - 1) * 16 * 4 * 64;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) xch[(r * 4 + (wave & 3)) * 64 + lane] = acc[r];
-    }
-    __syncthreads();
-    if (part > 0) return;
-#pragma unroll
-    for (int p = 0; p < KP - 1; ++p) {
-        const float *xch = kp_smem + (size_t)p * 16 * 4 * 64;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] += xch[(r * 4 + wave) * 64 + lane];
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int64_t q = q0 + 32 * wr + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int64_t x = x0 + 32 * wc + l31;
-        if (q < nq && x < N) {
-            const float ip = acc[r];
-            float key;
-            if (metric == kL2) {
-                key = fmaf(-2.f, ip, qnorm[q] + xnorm[x]);
-                key = key < 0.f ? 0.f : key;
-            } else {
-                key = -ip;
-            }
-            keys_out[q * ldk + x] = key;
-        }
-    }
-}
-constexpr size_t kKpartsLds4 = (size_t)4 * 4 * SBM * GLD * sizeof(float);
-static_assert(kKpartsLds4 <= 160 * 1024, "flat_keys_kparts<4> LDS");
-
 // flat_keys_direct — the same 64 × 64 tiles, MFMAs and k order as flat_keys_small (bit-identical keys), but every
 // wave loads its own A / B fragments straight from memory into a 3-chunk register ring: no LDS staging, no
 // per-chunk barrier.  The inputs are small and cache-resident (the coarse quantizer's queries and centroids),
@@ -1836,13 +1736,11 @@ void launch_flat_gemm_keys(const float *Q, const float *qn, int64_t nq, const fl
         dim3 g((unsigned)blocks), b(256);
         // HIPANN_KEYS = 2 (default; even chunk counts): flat_keys_ksplit; 0 (and odd counts): LDS-staged
         // (flat_keys_small, 29.7 µs for 1024 × 1024 × 768); 3 / 6: the
-        // register-ring flat_keys_direct with that many chunks in flight (A/B: 34.0 / 35.7 µs)
+        // register-ring flat_keys_direct with that many chunks in flight (A/B: 34.0 / 35.7 µs).  Measured and
+        // dropped at r04: four K-groups of 4 waves (24.0 µs) and 64-dim stages (25.0 µs) against 23.9 µs.
         static const int mode = [] { const char *e = std::getenv("HIPANN_KEYS"); return e ? std::atoi(e) : 2; }();
         const int nk = (d + GBK - 1) / GBK;
-        if (mode == 4 && nk % 4 == 0) {  // the K-parts tiles (16 waves, four per SIMD)
-            if (vec4) hipLaunchKernelGGL((flat_keys_kparts<true, 4>), g, dim3(1024), kKpartsLds4, st, Q, qn, nq, X, xn, N, d, metric, sq, keys, ldk);
-            else hipLaunchKernelGGL((flat_keys_kparts<false, 4>), g, dim3(1024), kKpartsLds4, st, Q, qn, nq, X, xn, N, d, metric, sq, keys, ldk);
-        } else if ((mode == 2 || mode == 4) && nk % 2 == 0) {  // default: the K-split tiles (8 waves, two per SIMD)
+        if (mode == 2 && nk % 2 == 0) {  // default: the K-split tiles (8 waves, two per SIMD)
             if (vec4) hipLaunchKernelGGL(flat_keys_ksplit<true>, g, dim3(512), 0, st, Q, qn, nq, X, xn, N, d, metric, sq, keys, ldk);
             else hipLaunchKernelGGL(flat_keys_ksplit<false>, g, dim3(512), 0, st, Q, qn, nq, X, xn, N, d, metric, sq, keys, ldk);
         } else if (mode == 3) {
