@@ -448,3 +448,22 @@ def test_flat_bf16_large_batch_buffers_do_not_overflow(gpu, oracle, nq):
     assert (np.abs(D - D0) <= 1e-5 * scale).all()
     Do, Io = oracle.flat_search(xb, xq[:16], 10, 0)
     check_topk_parity(xb, xq[:16], D[:16], I[:16], Do, Io, 0)
+
+
+@pytest.mark.parametrize("n,d,nq,expect", [(600_000, 1280, 256, 4), (600_000, 128, 200, 4), (300_000, 128, 256, 4),
+                                           (600_000, 1024, 256, 5)])
+def test_flat_default_form_falls_back_where_int8_does_not_run(gpu, oracle, n, d, nq, expect):
+    """The default form 5 runs only as the bounded passes with d <= 1024 (exact int32 sums), nq >= 256 and
+    >= 512K rows; other shapes run form 4 (the bf16 image), and the path reports the form that ran.  Ids follow
+    the oracle's parity rule on 16 queries either way."""
+    rng = np.random.default_rng(n + d + nq)
+    xb = rng.standard_normal((n, d), dtype=np.float32)
+    xq = rng.standard_normal((nq, d), dtype=np.float32)
+    ix = gpu.HipIndexFlat(d, 0, xb)
+    assert ix.form == ix.FORM_I8_EXACT
+    D, I = ix.search(xq, 10)
+    assert ix.last_search_path()["form"] == expect, ix.last_search_path()
+    Do, Io = oracle.flat_search(xb, xq[:16], 10, 0)
+    check_topk_parity(xb, xq[:16], D[:16], I[:16], Do, Io, 0)
+    assert ix.rerank_fallbacks() == 0
+    ix.close()
