@@ -577,6 +577,182 @@ void launch_i8_tile_rows(const float *X, const float *scale, int64_t n, int d, i
 }
 
 
+// ---- small batches (nq < 20, FAISS's direct-form path) over the int8 image ---------------------------------
+// flat_i8_scan: the extension's per-query call (faiss_index.cpp:737, search(1, …)) streams the int8 image instead
+// of the fp32 rows — a quarter of the bytes.  Lane = database row: a wave takes 64-row groups (a quarter of a
+// 256-row tile: each 16-B unit of the group is one coalesced 1-KiB read, the rows' XOR swizzle permutes lanes
+// within it), accumulates the exact int32 dot products with the queries' int8 images (v_dot4, 4 per unit; the
+// query units in LDS, read as broadcasts), and offers key = ‖q‖² + ‖x‖² − 2·s_q·s_x·dot (IP: −s_q·s_x·dot) to one
+// 64-deep wave list per query.  The lists are a filter: flat_i8_group_merge + ivf_rerank_topk recompute the
+// survivors in the direct fp32 form and certify them with the int8 residual bound of the batched form 5.
+constexpr int I8S_K = 64;  // filter depth (the batched form 5's)
+__device__ __forceinline__ int i8s_dot16(uint4 x, uint4 q, int acc) {
+    acc = __builtin_amdgcn_sdot4((int)x.x, (int)q.x, acc, false);
+    acc = __builtin_amdgcn_sdot4((int)x.y, (int)q.y, acc, false);
+    acc = __builtin_amdgcn_sdot4((int)x.z, (int)q.z, acc, false);
+    return __builtin_amdgcn_sdot4((int)x.w, (int)q.w, acc, false);
+}
+template <int NQ, bool IP>
+__global__ void __launch_bounds__(256)
+flat_i8_scan(const uint4 *__restrict__ qimg, const float *__restrict__ qscale, const float *__restrict__ qnorm,
+             const uint4 *__restrict__ ximg, const float *__restrict__ xscale, const float *xnorm, int64_t N, int nk,
+             int64_t groups_per_wave, float *__restrict__ part_d, int *__restrict__ part_i) {
+    extern __shared__ uint4 i8s_q[];  // [NQ][nk][4] query units
+    for (int i = threadIdx.x; i < NQ * nk * 4; i += 256) i8s_q[i] = qimg[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t ngroups = (N + 63) / 64;
+    const int64_t g0 = gw * groups_per_wave;
+    const int64_t g1 = g0 + groups_per_wave < ngroups ? g0 + groups_per_wave : ngroups;
+    float qsc[NQ], qn[NQ];
+#pragma unroll
+    for (int qi = 0; qi < NQ; ++qi) {
+        qsc[qi] = qscale[qi];
+        qn[qi] = IP ? 0.f : qnorm[qi];
+    }
+    WaveList<1, int> L[NQ];
+#pragma unroll
+    for (int qi = 0; qi < NQ; ++qi) L[qi].init();
+    for (int64_t g = g0; g < g1; ++g) {
+        const int64_t t = g >> 2;
+        const int rin = 64 * (int)(g & 3) + lane;  // row within the tile
+        const int64_t row = t * 256 + rin;
+        const bool valid = row < N;
+        const uint4 *tb = ximg + t * (int64_t)nk * 4 * 256;
+        int acc[NQ];
+#pragma unroll
+        for (int qi = 0; qi < NQ; ++qi) acc[qi] = 0;
+        for (int kc = 0; kc < nk; kc += 2) {  // nk is even (flat_i8_nk)
+            uint4 xv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int c = u & 3;
+                xv[u] = tb[((int64_t)(kc + (u >> 2)) * 4 + c) * 256 + (rin ^ (c << 1))];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+#pragma unroll
+                for (int qi = 0; qi < NQ; ++qi) acc[qi] = i8s_dot16(xv[u], i8s_q[(qi * nk + kc) * 4 + u], acc[qi]);
+        }
+        const int64_t rr = valid ? row : N - 1;
+        const float sx = xscale[rr], xv2 = IP ? 0.f : xnorm[rr];
+#pragma unroll
+        for (int qi = 0; qi < NQ; ++qi) {
+            const float s = qsc[qi] * sx * (float)acc[qi];
+            float key;
+            if (IP) {
+                key = -s;
+            } else {
+                key = fmaf(-2.f, s, qn[qi] + xv2);
+                key = key < 0.f ? 0.f : key;
+            }
+            L[qi].offer(valid ? key : __builtin_inff(), valid ? (int)row : IdTraits<int>::pad(), I8S_K - 1);
+        }
+    }
+#pragma unroll
+    for (int qi = 0; qi < NQ; ++qi) {
+        part_d[(gw * NQ + qi) * I8S_K + lane] = L[qi].d[0];
+        part_i[(gw * NQ + qi) * I8S_K + lane] = L[qi].id[0];
+    }
+}
+
+// The scan's per-wave lists [wave][q][64] merged in groups of `per` waves into [q][group][64] (the rerank's
+// query-major slot lists).  One wave per (group, query); four lists' loads issued ahead of their offers.
+__global__ void __launch_bounds__(256)
+flat_i8_group_merge(const float *__restrict__ pd, const int *__restrict__ pi, int nw, int nq, int per, int ngroup,
+                    float *__restrict__ od, int *__restrict__ oi) {
+    const int64_t item = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (item >= (int64_t)ngroup * nq) return;
+    const int q = (int)(item / ngroup), grp = (int)(item - (int64_t)q * ngroup);
+    const int lane = threadIdx.x & 63;
+    WaveList<1, int> L;
+    L.init();
+    const int w0 = grp * per, w1 = w0 + per < nw ? w0 + per : nw;
+    for (int w = w0; w < w1; w += 4) {
+        float v[4];
+        int id[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const bool ok = w + u < w1;
+            const int64_t off = ((int64_t)(ok ? w + u : w0) * nq + q) * I8S_K + lane;
+            v[u] = ok ? pd[off] : __builtin_inff();
+            id[u] = ok ? pi[off] : IdTraits<int>::pad();
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) L.offer(v[u], id[u], I8S_K - 1);
+    }
+    od[((int64_t)q * ngroup + grp) * I8S_K + lane] = L.d[0];
+    oi[((int64_t)q * ngroup + grp) * I8S_K + lane] = L.id[0];
+}
+
+// The queries' int8 units, [q][kc][c] (16 dims each, zero past d), quantized with their scales (i8_row_scale).
+__global__ void __launch_bounds__(256) i8_query_units(const float *__restrict__ Q, const float *__restrict__ scale,
+                                                      int64_t nq, int d, int nk, uint4 *__restrict__ out) {
+    const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (u >= nq * nk * 4) return;
+    const int64_t q = u / (nk * 4);
+    const int rem = (int)(u - q * nk * 4), kc = rem >> 2, c = rem & 3;
+    const float s = scale[q];
+    const float *x = Q + q * (int64_t)d;
+    const int dim0 = kc * I8_KC + 16 * c;
+    unsigned w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int v = dim0 + i < d ? i8_quant(x[dim0 + i], s) : 0;
+        w[i >> 2] |= ((unsigned)v & 0xffu) << (8 * (i & 3));
+    }
+    out[u] = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+int flat_i8_scan_k() { return I8S_K; }
+// up to 16 queries the per-query lists stay in registers (17-19 spill to scratch: those batches take the fp32 scan)
+int flat_i8_scan_max_nq() { return 16; }
+int64_t flat_i8_scan_waves(int64_t n) {
+    // ≈ 2048 waves (8 per CU), ≥ 16 groups of 64 rows each
+    const int64_t ngroups = (n + 63) / 64;
+    return std::max<int64_t>(1, std::min<int64_t>(2048, ngroups / 16));
+}
+void launch_flat_i8_scan(const float *Q, int64_t nq, int d, int metric, const void *ximg, const float *xscale,
+                         const float *xnorm, int64_t n, float *qscale, float *qres, const float *qnorm, void *qimg,
+                         float *part_d, int *part_i, int64_t nw, hipStream_t st) {
+    HIPANN_REQUIRE(nq >= 1 && nq <= flat_i8_scan_max_nq() && n >= 1 && nw >= 1, "flat_i8_scan: shape");
+    const int nk = flat_i8_nk(d);
+    launch_i8_row_scale(Q, nq, d, qscale, qres, st);
+    const int64_t units = nq * nk * 4;
+    hipLaunchKernelGGL(i8_query_units, dim3((unsigned)ceil_div(units, 256)), dim3(256), 0, st, Q, qscale, nq, d, nk,
+                       static_cast<uint4 *>(qimg));
+    const int64_t ngroups = (n + 63) / 64;
+    const int64_t gpw = ceil_div(ngroups, nw);
+    const size_t smem = (size_t)nq * nk * 4 * sizeof(uint4);
+    HIPANN_REQUIRE(smem <= 64 * 1024, "flat_i8_scan: query units exceed LDS");
+    dim3 grid((unsigned)ceil_div(nw, 4)), block(256);
+    const uint4 *qa = static_cast<const uint4 *>(qimg), *xa = static_cast<const uint4 *>(ximg);
+#define I8S_CASE(NQV)                                                                                                  \
+    case NQV:                                                                                                          \
+        if (metric == kIP) hipLaunchKernelGGL((flat_i8_scan<NQV, true>), grid, block, smem, st, qa, qscale, qnorm, xa, \
+                                              xscale, xnorm, n, nk, gpw, part_d, part_i);                              \
+        else hipLaunchKernelGGL((flat_i8_scan<NQV, false>), grid, block, smem, st, qa, qscale, qnorm, xa, xscale,      \
+                                xnorm, n, nk, gpw, part_d, part_i);                                                    \
+        break;
+    switch ((int)nq) {
+        I8S_CASE(1) I8S_CASE(2) I8S_CASE(3) I8S_CASE(4) I8S_CASE(5) I8S_CASE(6) I8S_CASE(7) I8S_CASE(8) I8S_CASE(9)
+        I8S_CASE(10) I8S_CASE(11) I8S_CASE(12) I8S_CASE(13) I8S_CASE(14) I8S_CASE(15) I8S_CASE(16)
+        default: throw HipError("flat_i8_scan: nq");
+    }
+#undef I8S_CASE
+    HIPANN_CHECK(hipGetLastError());
+}
+void launch_flat_i8_group_merge(const float *pd, const int *pi, int nw, int nq, int ngroup, float *od, int *oi,
+                                hipStream_t st) {
+    const int per = (int)ceil_div(nw, ngroup);
+    const int64_t items = (int64_t)ngroup * nq;
+    hipLaunchKernelGGL(flat_i8_group_merge, dim3((unsigned)ceil_div(items, 4)), dim3(256), 0, st, pd, pi, nw, nq, per,
+                       ngroup, od, oi);
+    HIPANN_CHECK(hipGetLastError());
+}
+
+
 void launch_flat_bf16_k64(const void *qimg, const float *qn, int64_t nq, const void *ximg, const float *xn, int64_t N,
                           int nk, int metric, int nqt, int nsplit, int64_t tiles_per_split, int64_t tile_begin,
                           int64_t tile_end, const float *bound, float *cand_d, int *cand_i, int *cand_n, int cap,

@@ -211,6 +211,25 @@ static void flat_shard_search_bigk(FlatIndex &ix, FlatShard &sh, int64_t nq, con
                             D, I, st);
 }
 
+// The shard's tiled int8 image (form kFlatI8Exact): per-row scales max|x|/127, the rows' int8 units in the bf16
+// image's tile geometry, and the largest row residual ‖x − s·x̂‖ (the rerank bound's row term).  Built once.
+static void ensure_i8_image(FlatShard &sh, int d, hipStream_t st) {
+    if (sh.xi8_ok) return;
+    sh.xi8.ensure(flat_i8_img_bytes(sh.n, d, flat_bf16_tile_rows()), sh.device);
+    sh.xscale.ensure(sizeof(float) * (size_t)sh.n, sh.device);
+    sh.tmpnorm.ensure(sizeof(float) * (size_t)sh.n, sh.device);
+    launch_i8_row_scale(sh.xb, sh.n, d, sh.xscale.get<float>(), sh.tmpnorm.get<float>(), st);
+    launch_i8_tile_rows(sh.xb, sh.xscale.get<float>(), sh.n, d, flat_bf16_tile_rows(), sh.xi8.p, st);
+    sh.nflag.ensure(sizeof(int), sh.device);
+    launch_ivf_max_norm(sh.tmpnorm.get<float>(), sh.n, sh.nflag.get<unsigned>(), st);  // max of non-negative
+    unsigned bits = 0;
+    HIPANN_CHECK(hipMemcpyAsync(&bits, sh.nflag.p, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    HIPANN_CHECK(hipStreamSynchronize(st));
+    sh.tmpnorm.release();
+    std::memcpy(&sh.i8_rxmax, &bits, sizeof(float));
+    sh.xi8_ok = true;
+}
+
 // Search one shard: queries already on the shard's device.  Writes D (nq×kout fp32: raw distances,
 // ±inf pads) and I (nq×kout int64 labels, −1 pads) on the same device, asynchronously on `st`.
 // max‖x‖² of the shard (once per row set): the exact form's error bound
@@ -270,7 +289,78 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
         flat_shard_search_bigk(ix, sh, nq, xq, qn, k, kout, D, I, st);
         return;
     }
+    // nq < 20 on a large table (the extension's per-query calls, faiss_index.cpp:737): form 5's int8 image as the
+    // filter — flat_i8_scan (a quarter of the fp32 rows' bytes), 64 candidates per query, the exact direct-form
+    // rerank with the int8 residual bound; queries it cannot certify re-run on the fp32 direct scan below.
+    // HIPANN_FLAT_I8_SMALL=0 keeps every nq < 20 call on the fp32 scan (A/B).
+    static const bool i8_small_env = [] { const char *e = std::getenv("HIPANN_FLAT_I8_SMALL"); return !e || std::atoi(e); }();
+    const int req_form = form_override >= 0 ? form_override : ix.form;
+    if (nq <= flat_i8_scan_max_nq() && req_form == kFlatI8Exact && i8_small_env && sh.n >= 65536 && d <= 1024 &&
+        kout <= flat_i8_scan_k() && k <= flat_i8_scan_k()) {
+        const int kf = flat_i8_scan_k();
+        ensure_i8_image(sh, d, st);
+        const float xmax2 = flat_xmax2(sh, d, st);
+        const int64_t nw = flat_i8_scan_waves(sh.n);
+        const int G = (int)std::min<int64_t>(64, nw);
+        const float *qn = nullptr;
+        if (metric == kL2) {
+            sh.qn.ensure((size_t)nq * sizeof(float), sh.device);
+            launch_row_norms(xq, nq, d, sh.qn.get<float>(), st);
+            qn = sh.qn.get<float>();
+        }
+        sh.qscale.ensure(sizeof(float) * (size_t)nq, sh.device);
+        sh.qres.ensure(sizeof(float) * (size_t)nq, sh.device);
+        sh.qimg.ensure((size_t)nq * flat_i8_nk(d) * 4 * 16, sh.device);
+        sh.part_d.ensure((size_t)nw * nq * kf * sizeof(float), sh.device);
+        sh.part_i.ensure((size_t)nw * nq * kf * sizeof(int), sh.device);
+        sh.mid_d.ensure((size_t)G * nq * kf * sizeof(float), sh.device);
+        sh.mid_i.ensure((size_t)G * nq * kf * sizeof(long long), sh.device);
+        {
+            ScopedTiming t(ix.timer_main, st);
+            launch_flat_i8_scan(xq, nq, d, metric, sh.xi8.p, sh.xscale.get<float>(), sh.xn.get<float>(), sh.n,
+                                sh.qscale.get<float>(), sh.qres.get<float>(), qn, sh.qimg.p, sh.part_d.get<float>(),
+                                sh.part_i.get<int>(), nw, st);
+        }
+        sh.nflag.ensure(sizeof(int), sh.device);
+        sh.flagged.ensure(sizeof(int) * (size_t)nq, sh.device);
+        HIPANN_CHECK(hipMemsetAsync(sh.nflag.p, 0, sizeof(int), st));
+        {
+            ScopedTiming t(ix.timer_merge, st);
+            float *md = sh.mid_d.get<float>();
+            int *mi = reinterpret_cast<int *>(sh.mid_i.p);
+            launch_flat_i8_group_merge(sh.part_d.get<float>(), sh.part_i.get<int>(), (int)nw, (int)nq, G, md, mi, st);
+            launch_ivf_rerank(md, mi, nullptr, G, nq, kf, kout, metric, xq, sh.xb, d, nullptr, sh.n, sh.label_offset,
+                              xmax2, D, I, sh.nflag.get<int>(), sh.flagged.get<int>(), st, kSplit2Eps, sh.i8_rxmax,
+                              sh.qres.get<float>());
+        }
+        if (form_override < 0) {
+            ix.last_form = kFlatI8Exact;
+            ix.last_kfilt = kf;
+            ix.last_sublists = 0;
+        }
+        int nf = 0;
+        HIPANN_CHECK(hipMemcpyAsync(&nf, sh.nflag.p, sizeof(int), hipMemcpyDeviceToHost, st));
+        HIPANN_CHECK(hipStreamSynchronize(st));
+        if (nf <= 0) return;
+        ix.rerank_fallbacks += nf;
+        sh.fq.ensure(sizeof(float) * (size_t)nf * d, sh.device);
+        sh.fD.ensure(sizeof(float) * (size_t)nf * kout, sh.device);
+        sh.fI.ensure(sizeof(int64_t) * (size_t)nf * kout, sh.device);
+        launch_ivf_gather_queries(xq, sh.flagged.get<int>(), nf, d, sh.fq.get<float>(), st);
+        {
+            TimerPause p0(ix.timer_main), p1(ix.timer_merge);
+            flat_shard_search(ix, sh, nf, sh.fq.get<float>(), k, kout, sh.fD.get<float>(), sh.fI.get<int64_t>(), st,
+                              kFlatFp32);
+        }
+        launch_ivf_scatter_results(sh.fD.get<float>(), sh.fI.get<int64_t>(), sh.flagged.get<int>(), nf, kout, D, I, st);
+        return;
+    }
     if (nq < kBlasThreshold) {
+        if (form_override < 0) {
+            ix.last_form = kFlatFp32;  // the direct form
+            ix.last_kfilt = 0;
+            ix.last_sublists = 0;
+        }
         // direct form (fvec_L2sqr / fvec_inner_product)
         // ≥ 512 rows per wave on large tables; small ones (the IVF coarse quantizer's 1024 centroids at
         // nq = 1) are spread over waves of ≥ 16 rows (2 waves of 512 rows took 234 us for 1024 × 768)
@@ -370,21 +460,7 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
     float rxmax = sh.bf16_rxmax;  // the rerank bound's row term of the form that filtered
     if (i8) {
         // one int8 product per element (int32 sums) over a tiled int8 image with per-row scales, built once
-        if (!sh.xi8_ok) {
-            sh.xi8.ensure(flat_i8_img_bytes(sh.n, d, flat_bf16_tile_rows()), sh.device);
-            sh.xscale.ensure(sizeof(float) * (size_t)sh.n, sh.device);
-            sh.tmpnorm.ensure(sizeof(float) * (size_t)sh.n, sh.device);
-            launch_i8_row_scale(sh.xb, sh.n, d, sh.xscale.get<float>(), sh.tmpnorm.get<float>(), st);
-            launch_i8_tile_rows(sh.xb, sh.xscale.get<float>(), sh.n, d, flat_bf16_tile_rows(), sh.xi8.p, st);
-            sh.nflag.ensure(sizeof(int), sh.device);
-            launch_ivf_max_norm(sh.tmpnorm.get<float>(), sh.n, sh.nflag.get<unsigned>(), st);  // max of non-negative
-            unsigned bits = 0;
-            HIPANN_CHECK(hipMemcpyAsync(&bits, sh.nflag.p, sizeof(unsigned), hipMemcpyDeviceToHost, st));
-            HIPANN_CHECK(hipStreamSynchronize(st));
-            sh.tmpnorm.release();
-            std::memcpy(&sh.i8_rxmax, &bits, sizeof(float));
-            sh.xi8_ok = true;
-        }
+        ensure_i8_image(sh, d, st);
         rxmax = sh.i8_rxmax;
     }
     if (form == kFlatBf16Exact || i8) {

@@ -405,6 +405,14 @@ int flat_i8_nk(int d);
 size_t flat_i8_img_bytes(int64_t n, int d, int R);
 void launch_i8_row_scale(const float *X, int64_t n, int d, float *scale, float *resid, hipStream_t st);
 void launch_i8_tile_rows(const float *X, const float *scale, int64_t n, int d, int R, void *out, hipStream_t st);
+int flat_i8_scan_k();
+int flat_i8_scan_max_nq();
+int64_t flat_i8_scan_waves(int64_t n);
+void launch_flat_i8_scan(const float *Q, int64_t nq, int d, int metric, const void *ximg, const float *xscale,
+                         const float *xnorm, int64_t n, float *qscale, float *qres, const float *qnorm, void *qimg,
+                         float *part_d, int *part_i, int64_t nw, hipStream_t st);
+void launch_flat_i8_group_merge(const float *pd, const int *pi, int nw, int nq, int ngroup, float *od, int *oi,
+                                hipStream_t st);
 int flat_keys_kth_max();
 void launch_flat_keys_kth(const float *keys, int S, int64_t nq, int k, float *bound, hipStream_t st);
 void launch_flat_cand_bound(const float *cand_d, const int *cand_n, int nsplit, int cap, int64_t nq, int k,

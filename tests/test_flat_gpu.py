@@ -467,3 +467,32 @@ def test_flat_default_form_falls_back_where_int8_does_not_run(gpu, oracle, n, d,
     check_topk_parity(xb, xq[:16], D[:16], I[:16], Do, Io, 0)
     assert ix.rerank_fallbacks() == 0
     ix.close()
+
+
+@pytest.mark.parametrize("scaled", [False, True])
+@pytest.mark.parametrize("nq", [1, 3, 16, 17])
+@pytest.mark.parametrize("metric", [0, 1])
+def test_flat_small_batch_int8_filter(gpu, oracle, nq, metric, scaled):
+    """nq < 20 (FAISS's direct-form path, the extension's per-query call) on a large table: the int8 image as the
+    filter (flat_i8_scan, 64 candidates per query) and the exact direct-form rerank — ids and distances follow the
+    oracle's direct-form parity rule, no query re-runs; 17+ queries and HIPANN_FLAT_I8_SMALL=0 take the fp32 scan.
+    Includes a query equal to a row (distance 0); `scaled`: rows with magnitudes over 2^-10 .. 2^10, whose largest
+    int8 residual makes the bound too loose to certify — every query re-runs on the fp32 scan, same results."""
+    rng = np.random.default_rng(7 * nq + metric)
+    n, d = 300_000, 192
+    xb = rng.standard_normal((n, d), dtype=np.float32)
+    if scaled:
+        xb *= np.exp2(rng.integers(-10, 11, size=(n, 1))).astype(np.float32)
+    xq = rng.standard_normal((nq, d), dtype=np.float32)
+    xq[0] = xb[4321]
+    ix = gpu.HipIndexFlat(d, metric, xb)
+    D, I = ix.search(xq, 10)
+    path = ix.last_search_path()
+    assert path["form"] == (ix.FORM_I8_EXACT if nq <= 16 else ix.FORM_FP32), path
+    Do, Io = oracle.flat_search(xb, xq, 10, metric)
+    check_topk_parity(xb, xq, D, I, Do, Io, metric)
+    if metric == 0:
+        assert I[0, 0] == 4321 and D[0, 0] == 0.0
+    if not scaled:
+        assert ix.rerank_fallbacks() == 0
+    ix.close()

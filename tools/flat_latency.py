@@ -18,7 +18,7 @@ bench.gen_uniform_rows(torch, xb, 0, 42)
 xq = bench.uniform_queries(torch, 1024, 768, dev)
 ix = hipann.HipIndexFlatDevice(768, 0, xb.data_ptr(), n, 0)
 print(json.dumps(bench.flat_latency(torch, hipann, ix, xb, xq, n, 768, 10, 0)))
-for nq in (1, 4):
+for nq in (1, 4, 16):
     ix.set_kernel_timing(True)
     D = torch.empty((nq, 10), device=dev)
     I = torch.empty((nq, 10), device=dev, dtype=torch.int64)
