@@ -596,13 +596,20 @@ def flat_latency(torch, hipann, index, xb, xq, n, d, k, metric):
         el = time.perf_counter() - t0
         kms = index.kernel_ms(0)
         index.set_kernel_timing(False)
-        bytes_ = 4.0 * n * d
+        path = index.last_search_path()
+        if path["form"] == 5:  # flat_i8_scan: the int8 image (64 dims per 64-B unit row, even chunk count) + scale, ‖x‖²
+            nk = -(-d // 64)
+            nk += nk & 1
+            bytes_ = float(n) * (nk * 64 + 8)
+            kname, alg = "flat_i8_scan", f"N*(int8 row + scale + norm) = {bytes_ / 1e9:.3f} GB per call (int8 filter)"
+        else:
+            bytes_ = 4.0 * n * d
+            kname, alg = "flat_scan_topk", f"N*d*4 = {bytes_ / 1e9:.3f} GB per call"
         gbs = bytes_ / (kms * 1e-3) / 1e9 if kms > 0 else 0.0
-        res[f"nq{nq}"] = {"ms_per_call": round(el * 1e3 / it, 4), "kernel": "flat_scan_topk",
-                          "kernel_ms": round(kms, 4),
+        res[f"nq{nq}"] = {"ms_per_call": round(el * 1e3 / it, 4), "kernel": kname,
+                          "kernel_ms": round(kms, 4), "path": path,
                           "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                       "frac": round(gbs / HBM_PEAK_GBS, 4),
-                                       "algorithmic": f"N*d*4 = {bytes_ / 1e9:.3f} GB per call"}}
+                                       "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic": alg}}
     return res
 
 
