@@ -444,42 +444,301 @@ __global__ void __launch_bounds__(256) flat_cand_select(const float *__restrict_
     if (over && lane == 0) flagged[atomicAdd(nflag, 1)] = (int)q;
 }
 
-// The k-th smallest of each query's S sample keys (keys[q·S + j]), with the margin of flat_bf16_seed: the seed
-// bound of the bounded passes.  One 256-thread block per query, the keys in registers (S ≤ 256·KPT), the k-th
-// order statistic by bisection on order-preserving bits (32 rounds of count-and-reduce).
-constexpr int KTH_KPT = 64;
-__global__ void __launch_bounds__(256) flat_keys_kth(const float *__restrict__ keys, int S, int64_t nq, int k,
-                                                     float *__restrict__ bound) {
-    const int64_t q = blockIdx.x;
-    if (q >= nq) return;
-    __shared__ int part[4];
-    unsigned u[KTH_KPT];
-#pragma unroll
-    for (int j = 0; j < KTH_KPT; ++j) {
-        const int c = j * 256 + (int)threadIdx.x;
-        const unsigned b = c < S ? __float_as_uint(keys[q * S + c]) : 0x7f800000u;  // +inf past S
-        u[j] = (b & 0x80000000u) ? ~b : (b | 0x80000000u);                        // order-preserving
+// ---- the candidate kernels narrowed (one 256-thread block per query) ---------------------------------------
+// flat_cand_bound / flat_cand_select offer every buffered candidate to a wave list (≈ 26 per (query, split)
+// cell at 10M rows, 64 splits: 26 dependent insert rounds of one wave per query — 26 + 72 µs per 1024-query
+// C2 batch).  Here the block's 4 waves each take every 4th entry of the query's cells (lane = split), and the
+// order statistic is narrowed as in flat_keys_kth: T_hi = the k-th smallest per-thread minimum, the entries
+// ≤ T_hi (key bits + cell slot) go to an LDS list, and wave 0 finishes on ≤ KTH_CAP entries.  A longer list (or
+// k > 64) falls back to the wave list in wave 0.  Same bound bit for bit; the same k (key, row) pairs in the same
+// order (ties by row, as the wave list).
+constexpr int CN_CAP = 256;
+struct CandNarrow {
+    unsigned key[CN_CAP];
+    int slot[CN_CAP];
+    int n;
+    int part[4];
+    int over;
+};
+__device__ __forceinline__ unsigned cn_bits(float v) {
+    const float f = v == 0.f ? 0.f : v;
+    const unsigned b = __float_as_uint(f);
+    return v == v ? ((b >> 31) ? ~b : (b | 0x80000000u)) : 0xffffffffu;
+}
+__device__ __forceinline__ float cn_unbits(unsigned b) {
+    return __uint_as_float((b & 0x80000000u) ? (b & 0x7fffffffu) : ~b);
+}
+// block-wide: smallest t with #{m_thread ≤ t} ≥ k over the block's 256 values (32 rounds, one ballot per wave)
+__device__ __forceinline__ unsigned cn_block_kth(unsigned m, int k, int *part) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    unsigned lo = 0u, hi = 0xffffffffu;
+    while (lo < hi) {
+        const unsigned mid = lo + (hi - lo) / 2u;
+        const int c = (int)__popcll(__ballot(m <= mid));
+        __syncthreads();
+        if (lane == 0) part[wv] = c;
+        __syncthreads();
+        if (part[0] + part[1] + part[2] + part[3] >= k) hi = mid;
+        else lo = mid + 1u;
     }
-    unsigned lo = 0u, hi = 0xffffffffu;  // smallest t with #{u ≤ t} ≥ k
+    return lo;
+}
+// the query's entries ≤ T_hi into S (S.n may exceed CN_CAP: then only the count is exact); S.over = some cell
+// overflowed its capacity
+__device__ __forceinline__ void cand_narrow(const float *__restrict__ cand_d, const int *__restrict__ cand_n,
+                                            int nsplit, int cap, int64_t q, int k, CandNarrow &S) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (threadIdx.x == 0) { S.n = 0; S.over = 0; }
+    unsigned m = 0xffffffffu;
+    bool over = false;
+    for (int s0 = 0; s0 < nsplit; s0 += 64) {
+        const int s = s0 + lane;
+        const int nr = s < nsplit ? cand_n[q * nsplit + s] : 0;
+        over |= nr > cap;
+        const int n = nr < cap ? nr : cap;
+        const int64_t base = (q * nsplit + s) * (int64_t)cap;
+#pragma unroll 4
+        for (int j = wv; j < n; j += 4) m = min(m, cn_bits(cand_d[base + j]));
+    }
+    const unsigned th = cn_block_kth(m, k, S.part);  // its barriers order the S.n / S.over reset
+    if (__ballot(over) != 0ull && lane == 0) S.over = 1;
+    for (int s0 = 0; s0 < nsplit; s0 += 64) {
+        const int s = s0 + lane;
+        const int nr = s < nsplit ? cand_n[q * nsplit + s] : 0;
+        const int n = nr < cap ? nr : cap;
+        const int64_t base = (q * nsplit + s) * (int64_t)cap;
+        for (int j = wv; j < n; j += 4) {
+            const unsigned b = cn_bits(cand_d[base + j]);
+            if (b <= th) {
+                const int p = atomicAdd(&S.n, 1);
+                if (p < CN_CAP) { S.key[p] = b; S.slot[p] = s * cap + j; }
+            }
+        }
+    }
+    __syncthreads();
+}
+// wave 0: the k-th smallest key bits of the S list (n ≤ CN_CAP entries); ~0u when n < k
+__device__ __forceinline__ unsigned cn_wave_kth(const CandNarrow &S, int n, int k, unsigned (&v)[CN_CAP / 64]) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int i = 0; i < CN_CAP / 64; ++i) v[i] = lane + 64 * i < n ? S.key[lane + 64 * i] : 0xffffffffu;
+    if (n < k) return 0xffffffffu;
+    unsigned lo = 0u, hi = 0xffffffffu;
     while (lo < hi) {
         const unsigned mid = lo + (hi - lo) / 2u;
         int c = 0;
 #pragma unroll
-        for (int j = 0; j < KTH_KPT; ++j) c += u[j] <= mid ? 1 : 0;
+        for (int i = 0; i < CN_CAP / 64; ++i) c += (int)__popcll(__ballot(v[i] <= mid));
+        if (c >= k) hi = mid;
+        else lo = mid + 1u;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(256) flat_cand_bound_nw(const float *__restrict__ cand_d, const int *__restrict__ cand_n,
+                                                          int nsplit, int cap, int64_t nq, int k,
+                                                          float *__restrict__ bound) {
+    const int64_t q = blockIdx.x;
+    if (q >= nq) return;
+    __shared__ CandNarrow S;
+    cand_narrow(cand_d, cand_n, nsplit, cap, q, k, S);
+    if (threadIdx.x >= 64) return;
+    const int lane = threadIdx.x;
+    const int n = S.n;
+    float t;
+    if (n <= CN_CAP) {
+        unsigned v[CN_CAP / 64];
+        const unsigned b = cn_wave_kth(S, n, k, v);
+        t = b == 0xffffffffu ? __builtin_inff() : cn_unbits(b);
+    } else {  // a long tie run at T_hi: the wave list over every entry
+        WaveList<1, int> L;
+        L.init();
+        cand_offer_all<false>(cand_d, nullptr, cand_n, nsplit, cap, q, lane,
+                              [&](float v, int id) { L.offer(v, id, k - 1); });
+        t = readlane_f(L.d[0], k - 1);
+    }
+    if (lane == 0) {
+        const float tm = t == __builtin_inff() ? t : fmaxf(t * (1.f + 0x1p-20f), t + 0x1p-100f);
+        bound[q] = fminf(bound[q], tm);
+    }
+}
+
+__global__ void __launch_bounds__(256) flat_cand_select_nw(const float *__restrict__ cand_d, const int *__restrict__ cand_i,
+                                                           const int *__restrict__ cand_n, int nsplit, int cap,
+                                                           int64_t nq, int k, float *__restrict__ out_d,
+                                                           int *__restrict__ out_i, int *__restrict__ nflag,
+                                                           int *__restrict__ flagged) {
+    const int64_t q = blockIdx.x;
+    if (q >= nq) return;
+    __shared__ CandNarrow S;
+    __shared__ unsigned sel_k[64];
+    __shared__ int sel_r[64];
+    cand_narrow(cand_d, cand_n, nsplit, cap, q, k, S);
+    if (threadIdx.x >= 64) return;
+    const int lane = threadIdx.x;
+    const int n = S.n;
+    const int64_t cbase = q * nsplit * (int64_t)cap;
+    float kk = __builtin_inff();
+    int row = 0x7fffffff;
+    int nsel = 0;
+    if (S.over) {  // as flat_cand_select: an all-pad list, the query flagged for the exact fallback
+        if (lane == 0) flagged[atomicAdd(nflag, 1)] = (int)q;
+    } else if (n <= 64) {
+        if (lane < n) {
+            kk = cn_unbits(S.key[lane]);
+            row = cand_i[cbase + S.slot[lane]];
+        }
+        wave_rank_sort(kk, row, n);
+        nsel = n < k ? n : k;
+    } else if (n <= CN_CAP && k <= 64) {
+        // T = the k-th key; all keys < T, then the keys == T with the smallest rows up to k (ties by row)
+        unsigned v[CN_CAP / 64];
+        const unsigned T = cn_wave_kth(S, n, k, v);
+        int r[CN_CAP / 64];
+        int clt = 0;
+#pragma unroll
+        for (int i = 0; i < CN_CAP / 64; ++i) {
+            r[i] = v[i] == T && lane + 64 * i < n ? cand_i[cbase + S.slot[lane + 64 * i]] : 0x7fffffff;
+            clt += (int)__popcll(__ballot(v[i] < T));
+        }
+        const int need = k - clt;  // ≥ 1 tied entries to take
+        unsigned lo = 0u, hi = 0x7fffffffu;  // the need-th smallest row among the ties (rows are distinct)
+        while (lo < hi) {
+            const unsigned mid = lo + (hi - lo) / 2u;
+            int c = 0;
+#pragma unroll
+            for (int i = 0; i < CN_CAP / 64; ++i) c += (int)__popcll(__ballot((unsigned)r[i] <= mid));
+            if (c >= need) hi = mid;
+            else lo = mid + 1u;
+        }
+        const unsigned long long lt = (1ull << lane) - 1ull;
+        int base = 0;
+#pragma unroll
+        for (int i = 0; i < CN_CAP / 64; ++i) {
+            const bool take = lane + 64 * i < n && (v[i] < T || (v[i] == T && (unsigned)r[i] <= lo));
+            const unsigned long long mk = __ballot(take);
+            if (take) {
+                const int p = base + (int)__popcll(mk & lt);
+                sel_k[p] = v[i];
+                sel_r[p] = lane + 64 * i;
+            }
+            base += (int)__popcll(mk);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (lane < k) {
+            kk = cn_unbits(sel_k[lane]);
+            row = cand_i[cbase + S.slot[sel_r[lane]]];
+        }
+        wave_rank_sort(kk, row, k);
+        nsel = k;
+    } else {  // a long tie run at T_hi: the wave list over every entry
+        WaveList<1, int> L;
+        L.init();
+        cand_offer_all<true>(cand_d, cand_i, cand_n, nsplit, cap, q, lane,
+                             [&](float v, int id) { L.offer(v, id, k - 1); });
+        kk = L.d[0];
+        row = L.id[0];
+        nsel = k;
+    }
+    if (lane < k) {
+        out_d[q * k + lane] = lane < nsel ? kk : __builtin_inff();
+        out_i[q * k + lane] = lane < nsel ? row : 0x7fffffff;
+    }
+}
+
+// The k-th smallest of each query's S sample keys (keys[q·S + j]), with the margin of flat_bf16_seed: the seed
+// bound of the bounded passes.  One 256-thread block per query, the keys in registers (S ≤ 256·KPT).  A bisection
+// on order-preserving bits over all 256·KPT registers costs 32 × KPT compares per thread (50 µs per 1024-query
+// batch at 16K keys: VALU-bound), so the order statistic is narrowed first: T_hi = the k-th smallest of the 256
+// per-thread minima (k of the keys lie at or below it, so the answer is ≤ T_hi; for i.i.d. keys ≈ 34 keys of 16K
+// lie below it at k = 32, ≈ 74 at k = 64), the keys ≤ T_hi go to an LDS list, and one wave bisects that list.  A list longer than
+// KTH_CAP falls back to the full bisection on [0, T_hi].  Same result as the full bisection, bit for bit.
+constexpr int KTH_KPT = 64;
+constexpr int KTH_CAP = 256;  // the one-wave finish: 4 list entries per lane
+template <int KPT>
+__global__ void __launch_bounds__(256) flat_keys_kth(const float *__restrict__ keys, int S, int64_t nq, int k,
+                                                     float *__restrict__ bound, int narrow) {
+    const int64_t q = blockIdx.x;
+    if (q >= nq) return;
+    __shared__ int part[4];
+    __shared__ unsigned cand[KTH_CAP];
+    __shared__ int ncand;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    unsigned u[KPT];
+    unsigned m = 0xffffffffu;
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+        const int c = j * 256 + (int)threadIdx.x;
+        const unsigned b = c < S ? __float_as_uint(keys[q * S + c]) : 0x7f800000u;  // +inf past S
+        u[j] = (b & 0x80000000u) ? ~b : (b | 0x80000000u);                        // order-preserving
+        m = min(m, u[j]);
+    }
+    if (threadIdx.x == 0) ncand = 0;
+    unsigned lo = 0u, hi = 0xffffffffu;  // smallest t with #{u ≤ t} ≥ k
+    auto finish = [&]() {
+        if (threadIdx.x == 0) {
+            const unsigned b = (lo & 0x80000000u) ? (lo & 0x7fffffffu) : ~lo;
+            const float t = __uint_as_float(b);
+            bound[q] = t == __builtin_inff() ? t : fmaxf(t * (1.f + 0x1p-20f), t + 0x1p-100f);
+        }
+    };
+    if (narrow && k <= 256) {
+        // T_hi: the k-th smallest thread minimum (one ballot per wave per round)
+        while (lo < hi) {
+            const unsigned mid = lo + (hi - lo) / 2u;
+            const int c = (int)__popcll(__ballot(m <= mid));
+            __syncthreads();
+            if (lane == 0) part[wv] = c;
+            __syncthreads();
+            const int tot = part[0] + part[1] + part[2] + part[3];
+            if (tot >= k) hi = mid;
+            else lo = mid + 1u;
+        }
+        const unsigned th = lo;
+#pragma unroll
+        for (int j = 0; j < KPT; ++j)
+            if (u[j] <= th) {
+                const int p = atomicAdd(&ncand, 1);
+                if (p < KTH_CAP) cand[p] = u[j];
+            }
+        __syncthreads();
+        const int nc = ncand;
+        if (nc <= KTH_CAP) {
+            if (wv != 0) return;
+            unsigned v[KTH_CAP / 64];
+#pragma unroll
+            for (int i = 0; i < KTH_CAP / 64; ++i) v[i] = lane + 64 * i < nc ? cand[lane + 64 * i] : 0xffffffffu;
+            lo = 0u;
+            hi = th;  // mid < hi ≤ th never counts the ~0 pads
+            while (lo < hi) {
+                const unsigned mid = lo + (hi - lo) / 2u;
+                int c = 0;
+#pragma unroll
+                for (int i = 0; i < KTH_CAP / 64; ++i) c += (int)__popcll(__ballot(v[i] <= mid));
+                if (c >= k) hi = mid;
+                else lo = mid + 1u;
+            }
+            finish();
+            return;
+        }
+        lo = 0u;
+        hi = th;
+    }
+    while (lo < hi) {
+        const unsigned mid = lo + (hi - lo) / 2u;
+        int c = 0;
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) c += u[j] <= mid ? 1 : 0;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
         __syncthreads();
-        if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+        if (lane == 0) part[wv] = c;
         __syncthreads();
         const int tot = part[0] + part[1] + part[2] + part[3];
         if (tot >= k) hi = mid;
         else lo = mid + 1u;
     }
-    if (threadIdx.x == 0) {
-        const unsigned b = (lo & 0x80000000u) ? (lo & 0x7fffffffu) : ~lo;
-        const float t = __uint_as_float(b);
-        bound[q] = t == __builtin_inff() ? t : fmaxf(t * (1.f + 0x1p-20f), t + 0x1p-100f);
-    }
+    finish();
 }
 
 int flat_keys_kth_max() { return 256 * KTH_KPT; }
@@ -487,8 +746,26 @@ int flat_keys_kth_max() { return 256 * KTH_KPT; }
 void launch_flat_keys_kth(const float *keys, int S, int64_t nq, int k, float *bound, hipStream_t st) {
     if (nq <= 0) return;
     HIPANN_REQUIRE(S >= k && S <= 256 * KTH_KPT, "flat_keys_kth: sample size");
-    hipLaunchKernelGGL(flat_keys_kth, dim3((unsigned)nq), dim3(256), 0, st, keys, S, nq, k, bound);
+    // HIPANN_FLAT_KTH_NARROW=0 (A/B): the full 32-round bisection over every register
+    static const int narrow = [] { const char *e = std::getenv("HIPANN_FLAT_KTH_NARROW"); return e ? std::atoi(e) : 1; }();
+    // keys per thread sized to the sample
+    if (S <= 256 * 16)
+        hipLaunchKernelGGL(flat_keys_kth<16>, dim3((unsigned)nq), dim3(256), 0, st, keys, S, nq, k, bound, narrow);
+    else
+        hipLaunchKernelGGL(flat_keys_kth<KTH_KPT>, dim3((unsigned)nq), dim3(256), 0, st, keys, S, nq, k, bound, narrow);
     HIPANN_CHECK(hipGetLastError());
+}
+
+// test hook (tests/test_flat_kth_gpu.py): the seed k-th pass on device keys, narrowed (narrow = 1) or the full
+// bisection (0); synchronous; 0 on success, -1 on a bad shape or a HIP error
+extern "C" int hipann_debug_flat_keys_kth(const float *keys, int S, int64_t nq, int k, float *bound, int narrow) {
+    if (nq <= 0 || k <= 0 || S < k || S > 256 * KTH_KPT || !keys || !bound) return -1;
+    if (S <= 256 * 16)
+        hipLaunchKernelGGL(flat_keys_kth<16>, dim3((unsigned)nq), dim3(256), 0, 0, keys, S, nq, k, bound, narrow);
+    else
+        hipLaunchKernelGGL(flat_keys_kth<KTH_KPT>, dim3((unsigned)nq), dim3(256), 0, 0, keys, S, nq, k, bound, narrow);
+    if (hipGetLastError() != hipSuccess) return -1;
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
 }
 
 bool flat_bf16_k64_supported(int nk, int k) { return nk % 2 == 0 && k <= 64; }
@@ -786,19 +1063,33 @@ void launch_flat_bf16_k64(const void *qimg, const float *qn, int64_t nq, const v
     HIPANN_CHECK(hipGetLastError());
 }
 
+// HIPANN_FLAT_CAND_NARROW=0 (A/B): the one-wave-per-query wave-list kernels
+static bool cand_narrow_on(int k) {
+    static const bool env = [] { const char *e = std::getenv("HIPANN_FLAT_CAND_NARROW"); return !e || std::atoi(e); }();
+    return env && k <= 64;
+}
+
 void launch_flat_cand_bound(const float *cand_d, const int *cand_n, int nsplit, int cap, int64_t nq, int k,
                             float *bound, hipStream_t st) {
     if (nq <= 0) return;
-    hipLaunchKernelGGL(flat_cand_bound, dim3((unsigned)ceil_div(nq, 4)), dim3(256), 0, st, cand_d, cand_n, nsplit, cap,
-                       nq, k, bound);
+    if (cand_narrow_on(k))
+        hipLaunchKernelGGL(flat_cand_bound_nw, dim3((unsigned)nq), dim3(256), 0, st, cand_d, cand_n, nsplit, cap, nq, k,
+                           bound);
+    else
+        hipLaunchKernelGGL(flat_cand_bound, dim3((unsigned)ceil_div(nq, 4)), dim3(256), 0, st, cand_d, cand_n, nsplit,
+                           cap, nq, k, bound);
     HIPANN_CHECK(hipGetLastError());
 }
 
 void launch_flat_cand_select(const float *cand_d, const int *cand_i, const int *cand_n, int nsplit, int cap, int64_t nq,
                              int k, float *out_d, int *out_i, int *nflag, int *flagged, hipStream_t st) {
     if (nq <= 0) return;
-    hipLaunchKernelGGL(flat_cand_select, dim3((unsigned)ceil_div(nq, 4)), dim3(256), 0, st, cand_d, cand_i, cand_n,
-                       nsplit, cap, nq, k, out_d, out_i, nflag, flagged);
+    if (cand_narrow_on(k))
+        hipLaunchKernelGGL(flat_cand_select_nw, dim3((unsigned)nq), dim3(256), 0, st, cand_d, cand_i, cand_n, nsplit, cap,
+                           nq, k, out_d, out_i, nflag, flagged);
+    else
+        hipLaunchKernelGGL(flat_cand_select, dim3((unsigned)ceil_div(nq, 4)), dim3(256), 0, st, cand_d, cand_i, cand_n,
+                           nsplit, cap, nq, k, out_d, out_i, nflag, flagged);
     HIPANN_CHECK(hipGetLastError());
 }
 

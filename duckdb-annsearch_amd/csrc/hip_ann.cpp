@@ -514,7 +514,11 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
             return e ? (int64_t)std::atoll(e) : (int64_t)20;
         }();
         const int64_t tps_a = pass_div > 1 ? tps / pass_div : 0;
-        const int64_t sample = std::min<int64_t>(16384, flat_keys_kth_max());
+        static const int64_t sample_env = [] {
+            const char *e = std::getenv("HIPANN_FLAT_SAMPLE");  // A/B: rows of the seed sample (multiple of 256)
+            return e ? (int64_t)std::atoll(e) : (int64_t)16384;
+        }();
+        const int64_t sample = std::max<int64_t>(256, std::min<int64_t>(sample_env / 256 * 256, flat_keys_kth_max()));
         // per-(query, split) candidate capacity from the expected fill: pass A admits ≈ k·rows_A/S per cell (keys ≤
         // the k-th of S sample rows), pass B ≈ k·rows_B/(nsplit·rows_A) (the k-th over pass A's rows); 3× + 32 of
         // headroom (clustered 12.5M IP rows peaked at 2.3× the mean), a multiple of 32.  At 10M rows, 1024 queries,

@@ -79,8 +79,10 @@ struct KernelTimer {
         if (!on) return {nullptr, nullptr};
         if (used == ev.size()) {
             hipEvent_t a, b;
-            HIPANN_CHECK(hipEventCreate(&a));
-            HIPANN_CHECK(hipEventCreate(&b));
+            // timing-only events: no system-scope fence (an L2 writeback + invalidate per record, ≈5 µs of
+            // idle GPU between the timed kernel and the next launch); average_ms reads them after a sync
+            HIPANN_CHECK(hipEventCreateWithFlags(&a, hipEventDisableSystemFence));
+            HIPANN_CHECK(hipEventCreateWithFlags(&b, hipEventDisableSystemFence));
             ev.push_back({a, b});
         }
         return ev[used++];
