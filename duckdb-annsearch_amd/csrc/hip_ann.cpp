@@ -253,6 +253,37 @@ static float flat_xmax2(FlatShard &sh, int d, hipStream_t st) {
     return v;
 }
 
+// The bounded passes' plan: tile boundaries 0 = b₀ < b₁ < … < b_P = tps within every split.  Pass 0 admits the
+// rows under the seed (the k-th of S sample keys): ≈ k·(b₁·nsplit·rows)/S candidates per query; pass p ≥ 1 runs
+// under the k-th over every earlier row: ≈ k·(b_{p+1} − b_p)/b_p.  Every candidate costs a scattered store and
+// the epilogue's slow path (measured ≈ 0.54 µs per candidate per query per 1024-query batch: C2 and 10M pass-A
+// sweeps, profiles/r04/passa_sweep_r04.txt), every pass ≈ 55 µs (its pipeline fill + the bound kernel), so P and
+// geometric boundaries b_p ≈ (S/(nsplit·rows))·g^p, g = (N/S)^{1/P}, minimise candidates·nq·0.54 ns + P·55 µs.
+// HIPANN_FLAT_PASSES pins P (A/B).
+static std::vector<int64_t> flat_pass_plan(int64_t tps, int64_t nsplit, int64_t tile_rows, int64_t sample, int k,
+                                           int64_t nq) {
+    static const int forced = [] { const char *e = std::getenv("HIPANN_FLAT_PASSES"); return e ? std::atoi(e) : 0; }();
+    const double unit = (double)sample / ((double)nsplit * (double)tile_rows);  // the sample in tiles per split
+    std::vector<int64_t> best{0, tps};
+    double best_cost = 1e300;
+    for (int P = 1; P <= 6; ++P) {
+        if (forced > 0 && P != forced) continue;
+        std::vector<int64_t> b{0};
+        const double g = std::pow((double)tps / unit, 1.0 / P);
+        for (int p = 1; p < P; ++p) {
+            const int64_t t = std::llround(unit * std::pow(g, p));
+            if (t > b.back() && t < tps) b.push_back(t);
+        }
+        b.push_back(tps);
+        if ((int)b.size() != P + 1) continue;  // too few tiles for P passes
+        double cand = k * (double)b[1] / unit;
+        for (size_t p = 1; p + 1 < b.size(); ++p) cand += k * (double)(b[p + 1] - b[p]) / (double)b[p];
+        const double cost = cand * (double)nq * 0.54e-9 + P * 55e-6;
+        if (cost < best_cost) { best_cost = cost; best = b; }
+    }
+    return best;
+}
+
 void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq, int k, int kout, float *D,
                        int64_t *I, hipStream_t st, int form_override) {
     DeviceGuard g(sh.device);
@@ -510,23 +541,26 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
         // the keys mode replaces).  The main passes then admit only keys ≤ that bound.
         const bool seeded = seed_env && sh.n >= 8 * 65536;
         static const int64_t pass_div = [] {
-            const char *e = std::getenv("HIPANN_FLAT_PASS_A");  // A/B: 1/x of each split in pass A; 0 = one pass
-            return e ? (int64_t)std::atoll(e) : (int64_t)20;
+            const char *e = std::getenv("HIPANN_FLAT_PASS_A");  // A/B: two passes, 1/x of each split in pass A
+            return e ? (int64_t)std::atoll(e) : (int64_t)-1;
         }();
-        const int64_t tps_a = pass_div > 1 ? tps / pass_div : 0;
         static const int64_t sample_env = [] {
             const char *e = std::getenv("HIPANN_FLAT_SAMPLE");  // A/B: rows of the seed sample (multiple of 256)
             return e ? (int64_t)std::atoll(e) : (int64_t)16384;
         }();
         const int64_t sample = std::max<int64_t>(256, std::min<int64_t>(sample_env / 256 * 256, flat_keys_kth_max()));
-        // per-(query, split) candidate capacity from the expected fill: pass A admits ≈ k·rows_A/S per cell (keys ≤
-        // the k-th of S sample rows), pass B ≈ k·rows_B/(nsplit·rows_A) (the k-th over pass A's rows); 3× + 32 of
-        // headroom (clustered 12.5M IP rows peaked at 2.3× the mean), a multiple of 32.  At 10M rows, 1024 queries,
-        // k 32: ≈25 expected → 128; larger batches (fewer, longer splits) and larger k scale it.
-        const double rows_split = (double)tps * flat_bf16_tile_rows();
-        const double rows_a = (double)tps_a * flat_bf16_tile_rows();
-        const double fill = tps_a >= 1 ? k * rows_a / (double)sample + k * (rows_split - rows_a) / (rows_a * (double)nsplit)
-                                       : k * rows_split / (double)sample;
+        // the passes' tile boundaries within every split: pass p scans tiles [pb[p], pb[p+1]) under the bound
+        // from everything before it (the seed for pass 0)
+        const std::vector<int64_t> pb = pass_div >= 0
+            ? std::vector<int64_t>(pass_div > 1 && tps / pass_div >= 1 ? std::vector<int64_t>{0, tps / pass_div, tps}
+                                                                     : std::vector<int64_t>{0, tps})
+            : flat_pass_plan(tps, nsplit, flat_bf16_tile_rows(), sample, k, nq);
+        // per-(query, split) candidate capacity from the expected fill: pass 0 admits ≈ k·rows₀/S per cell (keys ≤
+        // the k-th of S sample rows), pass p ≈ k·rows_p/(nsplit·rows_<p) (the k-th over all earlier rows); 3× + 32
+        // of headroom (clustered 12.5M IP rows peaked at 2.3× the mean), a multiple of 32.
+        double fill = k * (double)(pb[1] * flat_bf16_tile_rows()) / (double)sample;
+        for (size_t p = 1; p + 1 < pb.size(); ++p)
+            fill += k * (double)(pb[p + 1] - pb[p]) / ((double)pb[p] * (double)nsplit);
         const int cap = (int)std::min<double>(1 << 20, (double)ceil_div((int64_t)(3.0 * fill + 32.0), 32) * 32);
         const size_t ncell = (size_t)nq * nsplit;
         // the keys-mode seed pass runs per chunk of 1024 queries (4 query tiles) through one 64 MB slab of keys
@@ -568,23 +602,23 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
             launch_flat_bf16_seed(spd, (int)ceil_div(stiles, stps), nq, k, sh.seed.get<float>(), st);
         }
         // bounded passes (64-dim K-step kernel, flat_b16k64.hip): every row with key ≤ the bound goes to a
-        // per-(query, split) candidate buffer.  Pass A covers the first ≈1/20 of every split under the 16K-row
-        // seed bound; the bound is then re-merged from its candidates (the k-th best key over ≈N/20 rows) and
-        // pass B covers the rest — ≈16 + 10 candidates per query and split at 10M rows (expected 32·rows/sample
-        // per query), no row scanned twice.  flat_cand_select keeps each query's k best for the rerank.
+        // per-(query, split) candidate buffer.  Pass 0 covers the first tiles of every split under the 16K-row
+        // seed bound; after each pass the bound is re-merged from all candidates so far (the k-th best key over
+        // every row scanned) and the next pass continues (flat_pass_plan: at 10M rows 4 passes over 5 / 20 / 98 /
+        // 488 tiles per split, ≈ 8.5 candidates per query and split), no row scanned twice.  flat_cand_select keeps
+        // each query's k best for the rerank.
         if (seeded && bounded) {
             static const bool dbg = std::getenv("HIPANN_FLAT_CAND_DEBUG") != nullptr;
             float *cd = sh.cand.get<float>();
             int *ci = reinterpret_cast<int *>(cd + ncell * cap);
             int *cn = ci + ncell * cap;
             float *bound = sh.seed.get<float>();
-            if (tps_a >= 1) {
+            for (size_t p = 0; p + 1 < pb.size(); ++p) {
                 launch_flat_bf16_k64(sh.qimg.p, qn, nq, ximg, sh.xn.get<float>(), sh.n, nk, metric, (int)nqt,
-                                     (int)nsplit, tps, 0, tps_a, bound, cd, ci, cn, cap, false, false, st, qsc, xsc);
-                launch_flat_cand_bound(cd, cn, (int)nsplit, cap, nq, k, bound, st);
+                                     (int)nsplit, tps, pb[p], pb[p + 1], bound, cd, ci, cn, cap, p > 0, false, st, qsc,
+                                     xsc);
+                if (p + 2 < pb.size()) launch_flat_cand_bound(cd, cn, (int)nsplit, cap, nq, k, bound, st);
             }
-            launch_flat_bf16_k64(sh.qimg.p, qn, nq, ximg, sh.xn.get<float>(), sh.n, nk, metric, (int)nqt,
-                                 (int)nsplit, tps, tps_a, tps, bound, cd, ci, cn, cap, tps_a >= 1, false, st, qsc, xsc);
             sh.nflag.ensure(sizeof(int), sh.device);
             sh.flagged.ensure(sizeof(int) * (size_t)nq, sh.device);
             HIPANN_CHECK(hipMemsetAsync(sh.nflag.p, 0, sizeof(int), st));
@@ -600,8 +634,8 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
                 long long tot = 0;
                 int mx = 0;
                 for (int v : hn) { tot += v; mx = std::max(mx, v); }
-                std::fprintf(stderr, "hipann flat cand: nsplit %lld tps %lld tps_a %lld mean %.2f max %d bound[0] %g\n",
-                             (long long)nsplit, (long long)tps, (long long)tps_a, (double)tot / (double)ncell, mx,
+                std::fprintf(stderr, "hipann flat cand: nsplit %lld tps %lld passes %zu pass0 %lld cap %d mean %.2f max %d bound[0] %g\n",
+                             (long long)nsplit, (long long)tps, pb.size() - 1, (long long)pb[1], cap, (double)tot / (double)ncell, mx,
                              (double)hb[0]);
             }
             cr_d = cd;
