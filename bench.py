@@ -433,7 +433,7 @@ FLAT_FORMS = {5: ("flat_bf16_k64<I8>", 1, I8_MFMA_PEAK_TOPS,
                   "64-deep filter (the bound from the measured int8 residuals)"),
               4: ("flat_bf16_k64", 1, BF16_MFMA_PEAK_TF,
                   "bf16 MFMA (v_mfma_f32_16x16x32_bf16), one bf16 product per fp32 product over a tiled bf16 image of "
-                  "the rows; kernel_ms = the keys-mode seed pass + two bounded passes (rows with scan key <= a per-query "
+                  "the rows; kernel_ms = the keys-mode seed pass + the planned bounded passes (rows with scan key <= a per-query "
                   "bound to candidate buffers) + the bound / select kernels; merge_ms = exact fp32 direct-form rerank "
                   "of the 32 best + bound check (Cauchy-Schwarz bound of the bf16 residuals)"),
               0: ("flat_gemm_topk2", 1, FP32_MFMA_PEAK_TF, "fp32 MFMA (v_mfma_f32_32x32x2_f32)"),

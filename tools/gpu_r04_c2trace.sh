@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp
 for spec in ${C2_VARIANTS:-default=}; do
 v=${spec%%=*}; envset=${spec#*=}
-unset HIPANN_FLAT_SAMPLE HIPANN_FLAT_CAND_REGS HIPANN_FLAT_KTH_NARROW HIPANN_FLAT_CAND_NARROW
+unset HIPANN_FLAT_SAMPLE HIPANN_FLAT_CAND_REGS HIPANN_FLAT_KTH_NARROW HIPANN_FLAT_CAND_NARROW HIPANN_FLAT_PASS_A
 if [ -n "$envset" ]; then export "$envset"; fi
 echo "## $v"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$root/gpurun_out/trace_c2_r04_$v" -o run -- \
