@@ -113,6 +113,11 @@ def compact_config(name, c):
         out["rerank_fallbacks"] = c["rerank_fallbacks_total"]
     if isinstance(c.get("ids_equal_to_oracle"), dict) and "fraction" in c["ids_equal_to_oracle"]:
         out["ids_eq_oracle"] = c["ids_equal_to_oracle"]["fraction"]
+    par = c.get("parity_vs_cpu_path")
+    if isinstance(par, dict):
+        out["ids_eq_cpu_path"] = par.get("ids_eq_cpu_path")
+        out["parity_ok"] = par.get("parity_ok")
+        out["parity_queries"] = par.get("queries")
     if c.get("ids_equal_to_oracle_bfs") is not None:
         out["ids_eq_oracle_bfs"] = c["ids_equal_to_oracle_bfs"]
     if c.get("vs_k10") is not None:
@@ -156,6 +161,11 @@ def compact_line(full):
         line["roofline"] = compact_roofline(full["roofline"])
     if "cpu_baseline" in full:
         line["cpu_baseline"] = compact_cpu(full["cpu_baseline"])
+    par = full.get("parity_vs_cpu_path")
+    if isinstance(par, dict):
+        line["ids_eq_cpu_path"] = par.get("ids_eq_cpu_path")
+        line["parity_ok"] = par.get("parity_ok")
+        line["parity_queries"] = par.get("queries")
     if isinstance(full.get("with_h2d_d2h"), dict):
         line["with_h2d_d2h_qps"] = full["with_h2d_d2h"].get("queries_per_s")
     if isinstance(full.get("latency"), dict):
@@ -173,7 +183,7 @@ def compact_line(full):
     if len(s) > LINE_BUDGET:  # never lose the headline: drop the per-config extras first
         for name, c in line.get("configs", {}).items():
             line["configs"][name] = {k: c[k] for k in ("value", "ms_per_step", "recall_at_10", "frac", "kernel_ms",
-                                                       "cpu_qps", "error") if k in c}
+                                                       "cpu_qps", "ids_eq_cpu_path", "parity_ok", "error") if k in c}
         line.get("cpu_baseline", {}).pop("sample", None)
     return line
 
@@ -368,6 +378,20 @@ def host_pointer_rate(torch, search_dev, xq, nq, k, steps):
             "includes": "pinned H2D of the queries + search + D2H of D/I per step"}
 
 
+PARITY_RULE = ("tests/_data.check_topk_parity (oracle/parity.py): ids and order identical except at fp64 near-ties "
+               "within tau*scale (tau 1e-6), label sets equal below the CPU k-th key - window, distances within 1e-5 "
+               "(relative) + 8e-6*scale of fp64")
+
+
+def max_sqnorm_dev(x, chunk=1 << 20):
+    """max_i ‖x_i‖² of a device tensor, in row chunks (no full-size temporary)."""
+    m = 0.0
+    for r0 in range(0, x.shape[0], chunk):
+        c = x[r0:r0 + chunk]
+        m = max(m, float((c * c).sum(1).max().item()))
+    return m
+
+
 def recall_at(got, gt, k):
     return float(np.mean([len(set(got[i][:k]) & set(gt[i][:k])) / k for i in range(len(gt))]))
 
@@ -479,6 +503,7 @@ def flat_config(args, torch, dist, hipann, rank, world, dev, n, d, nq, k, metric
     Dr, Ir = step()
     torch.cuda.synchronize()
     Ir = Ir.cpu().numpy().copy()
+    Dr = Dr.cpu().numpy().copy()  # (the alternative forms below reuse the output buffers)
     form = index.last_search_path()["form"]  # the form the scan ran (the default falls back to 4 on small shapes)
     kname, terms, peak, fdesc = FLAT_FORMS[form]
     flops = 2.0 * nq * n_local * d
@@ -556,14 +581,25 @@ def flat_config(args, torch, dist, hipann, rank, world, dev, n, d, nq, k, metric
         index.form = FLAT_DEFAULT_FORM if not os.environ.get("HIPANN_FLAT_FORM") else int(os.environ["HIPANN_FLAT_FORM"])
         out["other_forms"] = alt
     if oracle_queries:
+        # the extension's CPU path (FAISS IndexFlat::search, BLAS form at nq >= 20: oracle.c) on the first
+        # oracle_queries of the batch, against the GPU's answers under the parity rule (oracle/parity.py)
         try:
             from oracle import oracle as O
+            from oracle.parity import topk_parity
             xb_h = xb.cpu().numpy()
             xq_h = xq[:oracle_queries].cpu().numpy()
-            _, Io = O.flat_search(xb_h, xq_h, k, metric)
+            t_o = time.perf_counter()
+            Do, Io = O.flat_search(xb_h, xq_h, k, metric, label_offset=0)
+            dt_o = time.perf_counter() - t_o
+            Dg = Dr[:oracle_queries]
+            par = topk_parity(lambda labs: xb_h[labs], xq_h, Dg, Ir[:oracle_queries], Do, Io, metric,
+                              max_sqnorm_dev(xb))
+            par["rule"] = PARITY_RULE
+            par["cpu_path_s"] = round(dt_o, 1)
             out["ids_equal_to_oracle"] = {"fraction": float((Io == Ir[:oracle_queries]).mean()),
                                           "queries": oracle_queries,
                                           "oracle": "FAISS IndexFlat BLAS-path restatement (oracle.c)"}
+            out["parity_vs_cpu_path"] = par
             del xb_h
         except Exception as e:  # report, never fail the line
             out["ids_equal_to_oracle"] = {"error": repr(e)}
@@ -728,6 +764,7 @@ def ivf_config(args, torch, dist, hipann, rank, world, dev, steps, warmup, suite
     Dr, Ir = step()
     torch.cuda.synchronize()
     Ir = Ir.cpu().numpy().copy()
+    Dr = Dr.cpu().numpy().copy()
     gt = flat_ground_truth(torch, hipann, d, metric, xq, k, n, rank, world, ivf_info_tensor=index)
     recall = recall_at(Ir, gt, k) if rank == 0 and gt is not None else None
     b_alg = info["scan_bytes_per_batch_local"]
@@ -804,7 +841,10 @@ def ivf_config(args, torch, dist, hipann, rank, world, dev, steps, warmup, suite
     if suite_extras:
         out["latency"] = ivf_latency(torch, index, xq, k, d, metric)
     if not args.no_cpu_baseline:
-        out["cpu_baseline"] = ivf_cpu_baseline(index, xq, k, nprobe, metric, args.cpu_seconds)
+        out["cpu_baseline"] = ivf_cpu_baseline(index, xq, k, nprobe, metric, args.cpu_seconds, gpu_DI=(Dr, Ir))
+        par = out["cpu_baseline"].pop("parity", None)
+        if par is not None:
+            out["parity_vs_cpu_path"] = par
     return out, index
 
 
@@ -840,7 +880,11 @@ def ivf_latency(torch, index, xq, k, d, metric=0):
     return res
 
 
-def ivf_cpu_baseline(index, xq, k, nprobe, metric, cpu_seconds):
+def ivf_cpu_baseline(index, xq, k, nprobe, metric, cpu_seconds, gpu_DI=None):
+    """The CPU path timed on the host cores, and (gpu_DI = the GPU's (D, I) for the same batch) its answers
+    compared with the GPU's under the parity rule (oracle/parity.py): north_star's "returned ids match the
+    extension's CPU FAISS path on identical inputs" at the headline size (faiss_index.cpp:729-737).  Every
+    query of the batch runs whenever the oracle does it in ≤ 60 s (≈ 3.4 s for 1024 at 10M x 768)."""
     from oracle import cpu_baseline as CB
 
     try:
@@ -848,14 +892,26 @@ def ivf_cpu_baseline(index, xq, k, nprobe, metric, cpu_seconds):
         cen_h, codes_h, ids_h = cen.cpu().numpy(), codes.cpu().numpy(), ids.cpu().numpy()
         off = index._offsets
         xq_h = xq.cpu().numpy()
-        s0 = min(16, xq_h.shape[0])
+        nq = xq_h.shape[0]
+        s0 = min(16, nq)
         _, dt0, _ = CB.ivf_qps(cen_h, off, ids_h, codes_h, xq_h[:s0], k, nprobe, metric)
-        s = int(min(xq_h.shape[0], max(s0, s0 * cpu_seconds / max(dt0, 1e-3))))
-        qps, dt, nth = CB.ivf_qps(cen_h, off, ids_h, codes_h, xq_h[:s], k, nprobe, metric)
-        return {"value": round(qps, 2), "unit": "queries/s", "cores": nth, "kind": "port",
-                "sample": f"first {s} of {xq_h.shape[0]} queries ({dt:.1f} s) through the C oracle's FAISS "
-                          f"IndexIVFFlat::search restatement (coarse quantizer + direct SIMD distances + heaps, "
-                          f"OpenMP over queries) on the same centroids and lists"}
+        per_q = max(dt0, 1e-3) / s0
+        s = nq if per_q * nq <= 60.0 else int(min(nq, max(s0, cpu_seconds / per_q)))
+        qps, dt, nth, Do, Io = CB.ivf_search_timed(cen_h, off, ids_h, codes_h, xq_h[:s], k, nprobe, metric)
+        res = {"value": round(qps, 2), "unit": "queries/s", "cores": nth, "kind": "port",
+               "sample": f"first {s} of {nq} queries ({dt:.1f} s) through the C oracle's FAISS "
+                         f"IndexIVFFlat::search restatement (coarse quantizer + direct SIMD distances + heaps, "
+                         f"OpenMP over queries) on the same centroids and lists"}
+        if gpu_DI is not None:
+            from oracle.parity import topk_parity
+
+            pos = np.empty(ids_h.shape[0], np.int64)
+            pos[ids_h] = np.arange(ids_h.shape[0], dtype=np.int64)
+            Dg, Ig = gpu_DI
+            res["parity"] = topk_parity(lambda labs: codes_h[pos[labs]], xq_h[:s], Dg[:s], Ig[:s], Do, Io, metric,
+                                        max_sqnorm_dev(codes), same_rtol=2e-6)
+            res["parity"]["rule"] = PARITY_RULE + "; at equal ids, within 2e-6 of the CPU path's fp32 direct-form distance"
+        return res
     except Exception as e:
         return {"value": None, "error": repr(e)}
 
@@ -1215,8 +1271,8 @@ def run_suite(args, torch, dist, hipann, dev):
         return out
 
     guarded("C1_flat_10k_128_cpu_path", lambda: c1_config(torch, hipann, dev))
-    guarded("C2_flat_l2_1m_768", lambda: flat(1_000_000, oracle_queries=32))
-    guarded("flat_l2_10m_768", lambda: flat(10_000_000, oracle_queries=20, latency=True, steps=5, request_k=True))
+    guarded("C2_flat_l2_1m_768", lambda: flat(1_000_000, oracle_queries=1024))
+    guarded("flat_l2_10m_768", lambda: flat(10_000_000, oracle_queries=256, latency=True, steps=5, request_k=True))
     if "request_k30" in cfg["flat_l2_10m_768"]:
         cfg["flat_l2_10m_768_request_k30"] = cfg["flat_l2_10m_768"].pop("request_k30")
     guarded("C4_diskann_1m_1536_sq8", lambda: diskann_config(args, torch, dist, hipann, 0, 1, dev, 1_000_000, 1536,
@@ -1244,7 +1300,8 @@ def c5_config(args, torch, dist, hipann, rank, world, dev):
     n = C5_ROWS_PER_GPU * world
     steps = max(3, min(args.steps, 10))
     out, index, xb = flat_config(args, torch, dist, hipann, rank, world, dev, n, 768, 1024, args.k, 1, steps, 2,
-                                 alt_forms=world == 1 and not args.no_alt_forms, host_rate=False)
+                                 alt_forms=world == 1 and not args.no_alt_forms, host_rate=False,
+                                 oracle_queries=64 if world == 1 and not args.no_cpu_baseline else 0)
     index.close()
     del index, xb
     torch.cuda.empty_cache()

@@ -986,14 +986,16 @@ int flat_i8_scan_k() { return I8S_K; }
 // up to 16 queries the per-query lists stay in registers (17-19 spill to scratch: those batches take the fp32 scan)
 int flat_i8_scan_max_nq() { return 16; }
 int64_t flat_i8_scan_waves(int64_t n) {
-    // ≈ 2048 waves (8 per CU), ≥ 16 groups of 64 rows each
+    // ≈ 2048 waves (8 per CU), ≥ 16 groups of 64 rows each; a multiple of 4 — the grid is whole 4-wave blocks and
+    // every wave writes its lists, so the caller's part buffers (nw·nq·64) must cover every launched wave (waves
+    // past the last group write all-pad lists)
     const int64_t ngroups = (n + 63) / 64;
-    return std::max<int64_t>(1, std::min<int64_t>(2048, ngroups / 16));
+    return (std::max<int64_t>(1, std::min<int64_t>(2048, ngroups / 16)) + 3) / 4 * 4;
 }
 void launch_flat_i8_scan(const float *Q, int64_t nq, int d, int metric, const void *ximg, const float *xscale,
                          const float *xnorm, int64_t n, float *qscale, float *qres, const float *qnorm, void *qimg,
                          float *part_d, int *part_i, int64_t nw, hipStream_t st) {
-    HIPANN_REQUIRE(nq >= 1 && nq <= flat_i8_scan_max_nq() && n >= 1 && nw >= 1, "flat_i8_scan: shape");
+    HIPANN_REQUIRE(nq >= 1 && nq <= flat_i8_scan_max_nq() && n >= 1 && nw >= 4 && nw % 4 == 0, "flat_i8_scan: shape");
     const int nk = flat_i8_nk(d);
     launch_i8_row_scale(Q, nq, d, qscale, qres, st);
     const int64_t units = nq * nk * 4;
@@ -1094,3 +1096,7 @@ void launch_flat_cand_select(const float *cand_d, const int *cand_i, const int *
 }
 
 }  // namespace hipann
+
+// test hook (tests/test_abi.py): the small-batch int8 scan's wave count for an n-row table — a whole number of
+// 4-wave blocks, so the launched grid never writes past the nw·nq·64 part buffers (no device needed)
+extern "C" int64_t hipann_debug_flat_i8_scan_waves(int64_t n) { return hipann::flat_i8_scan_waves(n); }

@@ -196,6 +196,20 @@ std::vector<int64_t> training_rows(int64_t n, int64_t train_sample, int nlist, u
 
 // The k-means core over the m training rows T (HBM, m × d).  Centroids → cen_dev (nlist × d, HBM) and the
 // final host copy cen_host; the last iteration's cluster sizes → sizes (optional).
+// spherical k-means: every centroid renormalised to unit L2 norm (FAISS Clustering::post_process_centroids; fp64
+// sum of squares, as oracle_kmeans_train's km_renorm)
+static void km_renorm(std::vector<float> &cen, int nlist, int d) {
+    for (int c = 0; c < nlist; ++c) {
+        float *a = cen.data() + (size_t)c * d;
+        double s = 0.0;
+        for (int e = 0; e < d; ++e) s = s + (double)a[e] * (double)a[e];
+        if (s > 0.0) {
+            const float inv = (float)(1.0 / std::sqrt(s));
+            for (int e = 0; e < d; ++e) a[e] *= inv;
+        }
+    }
+}
+
 void kmeans_core(int d, int metric, int nlist, const float *T, int64_t m, int niter, uint64_t rs, int init,
                  float *cen_dev, std::vector<float> &cen_host, int64_t *sizes, int device, hipStream_t st) {
     DevBuf sc;
@@ -243,6 +257,11 @@ void kmeans_core(int d, int metric, int nlist, const float *T, int64_t m, int ni
     cen_host.resize((size_t)nlist * d);
     HIPANN_CHECK(hipMemcpyAsync(cen_host.data(), cen_dev, sizeof(float) * cen_host.size(), hipMemcpyDeviceToHost, st));
     HIPANN_CHECK(hipStreamSynchronize(st));
+    if (metric == kIP) {  // FAISS post_process_centroids after the init: unit-norm centroids before the first assignment
+        km_renorm(cen_host, nlist, d);
+        HIPANN_CHECK(hipMemcpyAsync(cen_dev, cen_host.data(), sizeof(float) * cen_host.size(), hipMemcpyHostToDevice, st));
+        HIPANN_CHECK(hipStreamSynchronize(st));
+    }
     if (niter <= 0) {
         if (sizes) std::fill(sizes, sizes + nlist, (int64_t)0);
         return;
@@ -334,17 +353,7 @@ void kmeans_core(int d, int metric, int nlist, const float *T, int64_t m, int ni
             hs[(size_t)ci] = hs[(size_t)cj] / 2;
             hs[(size_t)cj] -= hs[(size_t)ci];
         }
-        if (metric == kIP) {
-            for (int c = 0; c < nlist; ++c) {
-                float *a = cen_host.data() + (size_t)c * d;
-                double s = 0.0;
-                for (int e = 0; e < d; ++e) s = s + (double)a[e] * (double)a[e];
-                if (s > 0.0) {
-                    const float inv = (float)(1.0 / std::sqrt(s));
-                    for (int e = 0; e < d; ++e) a[e] *= inv;
-                }
-            }
-        }
+        if (metric == kIP) km_renorm(cen_host, nlist, d);  // spherical
         HIPANN_CHECK(hipMemcpyAsync(cen_dev, cen_host.data(), sizeof(float) * cen_host.size(), hipMemcpyHostToDevice, st));
         HIPANN_CHECK(hipStreamSynchronize(st));
     }

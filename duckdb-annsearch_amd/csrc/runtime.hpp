@@ -237,7 +237,9 @@ struct FlatIndex : IndexBase {
     }
     int64_t memory_bytes() const override {
         int64_t b = 0;
-        for (auto &s : shards) b += s->n * (int64_t)d * 4 + (metric == kL2 ? s->n * 4 : 0) + (int64_t)s->xb16.bytes;
+        for (auto &s : shards)
+            b += s->n * (int64_t)d * 4 + (metric == kL2 ? s->n * 4 : 0) + (int64_t)s->xb16.bytes +
+                 (int64_t)s->xi8.bytes + (int64_t)s->xscale.bytes;
         return b;
     }
 };

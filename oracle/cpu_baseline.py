@@ -56,9 +56,16 @@ def flat_blas_qps(xb_slice: np.ndarray, xq: np.ndarray, k: int, n_full: int, met
 
 def ivf_qps(centroids, list_off, ids, codes, xq, k: int, nprobe: int, metric: int = 0):
     """Time the C oracle's IndexIVFFlat::search on ``xq``; return (queries/s, seconds, threads)."""
+    qps, dt, nth, _, _ = ivf_search_timed(centroids, list_off, ids, codes, xq, k, nprobe, metric)
+    return qps, dt, nth
+
+
+def ivf_search_timed(centroids, list_off, ids, codes, xq, k: int, nprobe: int, metric: int = 0):
+    """ivf_qps plus the CPU path's answers (D, I) for those queries — bench.py compares them with the GPU ids
+    (oracle/parity.py).  Returns (queries/s, seconds, threads, D, I)."""
     from . import oracle as O
 
     t0 = time.perf_counter()
-    O.ivf_search(centroids, list_off, ids, codes, xq, k, nprobe, metric)
+    D, I, _ = O.ivf_search(centroids, list_off, ids, codes, xq, k, nprobe, metric)
     dt = time.perf_counter() - t0
-    return xq.shape[0] / dt, dt, O.num_threads()
+    return xq.shape[0] / dt, dt, O.num_threads(), D, I

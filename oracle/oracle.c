@@ -625,7 +625,8 @@ int oracle_num_threads(void) {
  *   4. niter Lloyd iterations (FAISS Clustering::train): assignment = the Flat search with k = 1 (this
  *      oracle's FAISS restatement: BLAS form at >= 20 rows), centroids = fp64 means in row order,
  *      FAISS's split_clusters for empty ones (EPS = 1/1024, split probability (n_j − 1)/(m − nlist)),
- *      and for IP the spherical renormalisation (IndexIVF sets cp.spherical for METRIC_INNER_PRODUCT).
+ *      and for IP the spherical renormalisation (IndexIVF sets cp.spherical for METRIC_INNER_PRODUCT) — after
+ *      the init too (post_process_centroids runs before the first assignment).
  */
 static uint64_t km_next(uint64_t *s) {
     uint64_t z = (*s += 0x9e3779b97f4a7c15ULL);
@@ -651,6 +652,19 @@ static double km_dist64(const float *a, const float *b, int d) {
         memcpy(p, t, sizeof p);
     }
     return p[0];
+}
+
+/* spherical k-means: every centroid renormalised to unit L2 norm (FAISS Clustering::post_process_centroids) */
+static void km_renorm(float *centroids, int nlist, int d) {
+    for (int c = 0; c < nlist; ++c) {
+        float *a = centroids + (int64_t)c * d;
+        double s = 0.0;
+        for (int e = 0; e < d; ++e) s = s + (double)a[e] * (double)a[e];
+        if (s > 0.0) {
+            const float inv = (float)(1.0 / sqrt(s));
+            for (int e = 0; e < d; ++e) a[e] *= inv;
+        }
+    }
 }
 
 int oracle_kmeans_train(const float *x, int64_t n, int d, int metric, int nlist, int64_t train_sample, int niter,
@@ -737,6 +751,9 @@ int oracle_kmeans_train(const float *x, int64_t n, int d, int metric, int nlist,
         free(d2);
         free(wt);
     }
+    /* FAISS Clustering::train_encoded calls post_process_centroids() right after the init as well as after every
+     * iteration: with spherical (IP) the initial centroids are unit vectors before the first assignment */
+    if (metric == ORACLE_IP) km_renorm(centroids, nlist, d);
     /* 4. Lloyd */
     float *D = (float *)malloc(sizeof(float) * (size_t)m);
     int64_t *I = (int64_t *)malloc(sizeof(int64_t) * (size_t)m);
@@ -780,17 +797,7 @@ int oracle_kmeans_train(const float *x, int64_t n, int d, int metric, int nlist,
             hs[ci] = hs[cj] / 2;
             hs[cj] -= hs[ci];
         }
-        if (metric == ORACLE_IP) { /* spherical: renormalise every centroid */
-            for (int c = 0; c < nlist; ++c) {
-                float *a = centroids + (int64_t)c * d;
-                double s = 0.0;
-                for (int e = 0; e < d; ++e) s = s + (double)a[e] * (double)a[e];
-                if (s > 0.0) {
-                    const float inv = (float)(1.0 / sqrt(s));
-                    for (int e = 0; e < d; ++e) a[e] *= inv;
-                }
-            }
-        }
+        if (metric == ORACLE_IP) km_renorm(centroids, nlist, d); /* spherical */
     }
     if (sizes_out)
         for (int c = 0; c < nlist; ++c) sizes_out[c] = niter > 0 ? cnt[c] : 0;

@@ -117,3 +117,18 @@ def test_auto_gate_mirror(hipann_mod):
     assert not b.auto_upload(10 ** 7, 768, "HNSW")
     if not hipann_mod.is_available():
         assert not hipann_mod.GpuBackend().auto_upload(10 ** 7, 768)
+
+
+def test_flat_i8_scan_grid_is_whole_blocks(hipann_mod):
+    """flat_i8_scan launches ceil(nw/4) 4-wave blocks and every wave writes its lists, so the wave
+    count that sizes the part buffers (nw·nq·64) must be a multiple of 4 — n = 300000 gave 293 waves before."""
+    L = hipann_mod.lib()
+    f = L.hipann_debug_flat_i8_scan_waves
+    f.restype = C.c_int64
+    f.argtypes = [C.c_int64]
+    for n in (1, 63, 65536, 100_000, 300_000, 1_000_003, 10_000_000, 12_500_000):
+        nw = f(n)
+        ngroups = -(-n // 64)
+        assert nw % 4 == 0 and nw >= 4, (n, nw)
+        assert nw <= 2048 and nw >= min(2048, max(1, ngroups // 16)), (n, nw)
+    assert f(300_000) == 296

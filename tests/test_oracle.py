@@ -318,3 +318,40 @@ def test_kmeans_oracle_semantics():
     true = mt19937_uniform(24 * 48, seed=11).reshape(24, 48) * np.float32(3.0)
     d = ((cen[:, None, :] - true[None, :, :]) ** 2).sum(-1)
     assert len(set(d.argmin(1).tolist())) >= 22
+
+
+def test_bench_parity_report_agrees_with_the_test_rule():
+    """oracle/parity.py (the bench line's ids_eq_cpu_path / parity_ok) restates tests/_data.check_topk_parity without
+    asserts: on the oracle's own answers, and on answers with an exact-tie swap, it reports parity_ok like the test
+    rule passes; a swap beyond the tie window and a wrong distance are counted as violations."""
+    from oracle import oracle as O
+    from oracle.parity import topk_parity
+    from _data import check_topk_parity, max_sqnorm
+
+    xb, xq = faiss_metal_case(4000, 24, 32)
+    xb = xb.copy()
+    xb[7] = xb[3]  # an exact duplicate: its rank order is a tie
+    D, I = O.flat_search(xb, xq, 10)
+    xm = max_sqnorm(xb)
+    rows = lambda labs: xb[labs]  # noqa: E731
+    r = topk_parity(rows, xq, D, I, D, I, 0, xm)
+    assert r["parity_ok"] and r["ids_eq_cpu_path"] == 1.0 and r["queries_identical"] == 24
+    check_topk_parity(xb, xq, D, I, D, I)
+    # a query whose answer contains the duplicate pair: swap them (inside the window)
+    Dq, Iq = O.flat_search(xb, xb[3:4] + np.float32(1e-3), 10)
+    I2 = Iq.copy()
+    a, b = list(I2[0]).index(3), list(I2[0]).index(7)
+    I2[0, a], I2[0, b] = I2[0, b], I2[0, a]
+    r = topk_parity(rows, xb[3:4] + np.float32(1e-3), Dq, I2, Dq, Iq, 0, xm)
+    assert r["parity_ok"] and r["differing_slots"] == 2
+    # beyond the window: swap ranks 0 and 9 of query 0
+    I3 = I.copy()
+    I3[0, 0], I3[0, 9] = I3[0, 9], I3[0, 0]
+    r = topk_parity(rows, xq, D, I3, D, I, 0, xm)
+    assert not r["parity_ok"] and r["violations"].get("outside_window", 0) >= 1
+    with pytest.raises(AssertionError):
+        check_topk_parity(xb, xq, D, I3, D, I)
+    D4 = D.copy()
+    D4[1, 2] *= 1.01
+    r = topk_parity(rows, xq, D4, I, D, I, 0, xm, same_rtol=2e-6)
+    assert not r["parity_ok"] and r["violations"]["distance"] == 1 and r["violations"]["same_id_distance"] == 1
