@@ -136,7 +136,9 @@ namespace hipann {
 
 FlatIndex::~FlatIndex() {
     for (auto &s : shards) {
-        if (s->stream) { DeviceGuard g(s->device); (void)hipStreamDestroy(s->stream); }
+        DeviceGuard g(s->device);
+        if (s->done) (void)hipEventDestroy(s->done);
+        if (s->stream) (void)hipStreamDestroy(s->stream);
     }
 }
 
@@ -213,7 +215,7 @@ static void flat_shard_search_bigk(FlatIndex &ix, FlatShard &sh, int64_t nq, con
 
 // The shard's tiled int8 image (form kFlatI8Exact): per-row scales max|x|/127, the rows' int8 units in the bf16
 // image's tile geometry, and the largest row residual ‖x − s·x̂‖ (the rerank bound's row term).  Built once.
-static void ensure_i8_image(FlatShard &sh, int d, hipStream_t st) {
+static void ensure_i8_image(FlatIndex &ix, FlatShard &sh, int d, hipStream_t st) {
     if (sh.xi8_ok) return;
     sh.xi8.ensure(flat_i8_img_bytes(sh.n, d, flat_bf16_tile_rows()), sh.device);
     sh.xscale.ensure(sizeof(float) * (size_t)sh.n, sh.device);
@@ -225,6 +227,7 @@ static void ensure_i8_image(FlatShard &sh, int d, hipStream_t st) {
     unsigned bits = 0;
     HIPANN_CHECK(hipMemcpyAsync(&bits, sh.nflag.p, sizeof(unsigned), hipMemcpyDeviceToHost, st));
     HIPANN_CHECK(hipStreamSynchronize(st));
+    ++ix.host_syncs;
     sh.tmpnorm.release();
     std::memcpy(&sh.i8_rxmax, &bits, sizeof(float));
     sh.xi8_ok = true;
@@ -233,7 +236,7 @@ static void ensure_i8_image(FlatShard &sh, int d, hipStream_t st) {
 // Search one shard: queries already on the shard's device.  Writes D (nq×kout fp32: raw distances,
 // ±inf pads) and I (nq×kout int64 labels, −1 pads) on the same device, asynchronously on `st`.
 // max‖x‖² of the shard (once per row set): the exact form's error bound
-static float flat_xmax2(FlatShard &sh, int d, hipStream_t st) {
+static float flat_xmax2(FlatIndex &ix, FlatShard &sh, int d, hipStream_t st) {
     if (sh.xmax2 >= 0.f) return sh.xmax2;
     const float *xn = sh.xn.get<float>();
     if (!xn) {
@@ -246,6 +249,7 @@ static float flat_xmax2(FlatShard &sh, int d, hipStream_t st) {
     unsigned bits = 0;
     HIPANN_CHECK(hipMemcpyAsync(&bits, sh.nflag.p, sizeof(unsigned), hipMemcpyDeviceToHost, st));
     HIPANN_CHECK(hipStreamSynchronize(st));
+    ++ix.host_syncs;
     sh.tmpnorm.release();
     float v;
     std::memcpy(&v, &bits, sizeof(v));
@@ -284,8 +288,19 @@ static std::vector<int64_t> flat_pass_plan(int64_t tps, int64_t nsplit, int64_t 
     return best;
 }
 
-void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq, int k, int kout, float *D,
-                       int64_t *I, hipStream_t st, int form_override) {
+// The flag count of the launch phase's bound check into the shard's pinned host word (a copy kernel through its
+// device mapping, no DMA round trip); the host reads it after its next synchronisation with `st`.
+static void flag_readback(FlatShard &sh, hipStream_t st) {
+    sh.h_nflag.ensure(sizeof(int));
+    launch_copy_words(sh.nflag.p, host_device_ptr(sh.h_nflag.p), sizeof(int), st);
+}
+
+// Launch phase of a shard search: every kernel of the search up to the exact forms' flag count, enqueued on `st`
+// without a host synchronisation.  pend says what flat_shard_finish has left to do (kNone: the output is complete
+// once `st` drains).
+static void flat_shard_launch(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq, int k, int kout, float *D,
+                              int64_t *I, hipStream_t st, int form_override, FlatPending &pend) {
+    pend = FlatPending{};
     DeviceGuard g(sh.device);
     const int d = ix.d, metric = ix.metric;
     const float out_sign = metric == kIP ? -1.f : 1.f;
@@ -329,8 +344,8 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
     if (nq <= flat_i8_scan_max_nq() && req_form == kFlatI8Exact && i8_small_env && sh.n >= 65536 && d <= 1024 &&
         kout <= flat_i8_scan_k() && k <= flat_i8_scan_k()) {
         const int kf = flat_i8_scan_k();
-        ensure_i8_image(sh, d, st);
-        const float xmax2 = flat_xmax2(sh, d, st);
+        ensure_i8_image(ix, sh, d, st);
+        const float xmax2 = flat_xmax2(ix, sh, d, st);
         const int64_t nw = flat_i8_scan_waves(sh.n);
         const int G = (int)std::min<int64_t>(64, nw);
         const float *qn = nullptr;
@@ -369,21 +384,17 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
             ix.last_kfilt = kf;
             ix.last_sublists = 0;
         }
-        int nf = 0;
-        HIPANN_CHECK(hipMemcpyAsync(&nf, sh.nflag.p, sizeof(int), hipMemcpyDeviceToHost, st));
-        HIPANN_CHECK(hipStreamSynchronize(st));
-        if (nf <= 0) return;
-        ix.rerank_fallbacks += nf;
-        sh.fq.ensure(sizeof(float) * (size_t)nf * d, sh.device);
-        sh.fD.ensure(sizeof(float) * (size_t)nf * kout, sh.device);
-        sh.fI.ensure(sizeof(int64_t) * (size_t)nf * kout, sh.device);
-        launch_ivf_gather_queries(xq, sh.flagged.get<int>(), nf, d, sh.fq.get<float>(), st);
-        {
-            TimerPause p0(ix.timer_main), p1(ix.timer_merge);
-            flat_shard_search(ix, sh, nf, sh.fq.get<float>(), k, kout, sh.fD.get<float>(), sh.fI.get<int64_t>(), st,
-                              kFlatFp32);
-        }
-        launch_ivf_scatter_results(sh.fD.get<float>(), sh.fI.get<int64_t>(), sh.flagged.get<int>(), nf, kout, D, I, st);
+        // the flagged count goes to the host with the results; the uncertified queries re-run on the fp32 direct
+        // scan in flat_shard_finish
+        pend = FlatPending{};
+        pend.kind = FlatPending::kSmallI8;
+        pend.nq = nq;
+        pend.xq = xq;
+        pend.k = k;
+        pend.kout = kout;
+        pend.D = D;
+        pend.I = I;
+        flag_readback(sh, st);
         return;
     }
     if (nq < kBlasThreshold) {
@@ -486,12 +497,12 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
     const int *cr_i = nullptr, *cr_n = nullptr;
     int cr_nsplit = 0, cr_cap = 0;
     // the exact forms' max ‖x‖² (cached; its first computation uses sh.nflag as scratch, so before any flags)
-    const float xmax2 = exact ? flat_xmax2(sh, d, st) : 0.f;
+    const float xmax2 = exact ? flat_xmax2(ix, sh, d, st) : 0.f;
     const bool i8 = form == kFlatI8Exact;
     float rxmax = sh.bf16_rxmax;  // the rerank bound's row term of the form that filtered
     if (i8) {
         // one int8 product per element (int32 sums) over a tiled int8 image with per-row scales, built once
-        ensure_i8_image(sh, d, st);
+        ensure_i8_image(ix, sh, d, st);
         rxmax = sh.i8_rxmax;
     }
     if (form == kFlatBf16Exact || i8) {
@@ -507,6 +518,7 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
             unsigned bits = 0;
             HIPANN_CHECK(hipMemcpyAsync(&bits, sh.nflag.p, sizeof(unsigned), hipMemcpyDeviceToHost, st));
             HIPANN_CHECK(hipStreamSynchronize(st));  // later searches may run on other streams
+            ++ix.host_syncs;
             sh.tmpnorm.release();
             float r2;
             std::memcpy(&r2, &bits, sizeof(r2));
@@ -697,12 +709,49 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
                           sh.flagged.get<int>(), st, kSplit2Eps, form == kFlatBf16Exact || i8 ? rxmax : -1.f,
                           i8 ? sh.qres.get<float>() : nullptr);
     }
-    int nf = 0;
-    HIPANN_CHECK(hipMemcpyAsync(&nf, sh.nflag.p, sizeof(int), hipMemcpyDeviceToHost, st));
-    HIPANN_CHECK(hipStreamSynchronize(st));
+    pend = FlatPending{};
+    pend.kind = FlatPending::kExact;
+    pend.nq = nq;
+    pend.xq = xq;
+    pend.k = k_user;
+    pend.kout = kout;
+    pend.D = D;
+    pend.I = I;
+    pend.cr_d = cr_d;
+    pend.cr_bound = cr_bound;
+    pend.cr_i = cr_i;
+    pend.cr_n = cr_n;
+    pend.cr_nsplit = cr_nsplit;
+    pend.cr_cap = cr_cap;
+    pend.xmax2 = xmax2;
+    pend.rxmax = rxmax;
+    pend.i8 = i8;
+    flag_readback(sh, st);
+}
+
+// The second half of a shard search, once the host has synchronised with the launch phase's stream (its flag
+// count read back into sh.h_nflag): nothing to do unless the exact form's bound check flagged queries.  Flagged
+// queries are rare (0 on every benchmark batch); their re-runs are synchronous.
+void flat_shard_finish(FlatIndex &ix, FlatShard &sh, const FlatPending &pend, hipStream_t st) {
+    if (pend.kind == FlatPending::kNone) return;
+    int nf = *sh.h_nflag.get<int>();
     if (nf <= 0) return;
+    DeviceGuard g(sh.device);
+    const int d = ix.d, metric = ix.metric;
+    const int kout = pend.kout;
+    const float *xq = pend.xq;
+    float *D = pend.D;
+    int64_t *I = pend.I;
     int *fl = sh.flagged.get<int>();
-    if (cr_d) {
+    int rerun_form = kFlatSplit3;
+    if (pend.kind == FlatPending::kSmallI8) {
+        rerun_form = kFlatFp32;
+    } else if (pend.cr_d) {
+        const float *cr_d = pend.cr_d, *cr_bound = pend.cr_bound;
+        const int *cr_i = pend.cr_i, *cr_n = pend.cr_n;
+        const int cr_nsplit = pend.cr_nsplit, cr_cap = pend.cr_cap;
+        const float xmax2 = pend.xmax2, rxmax = pend.rxmax;
+        const bool i8 = pend.i8;
         // bounded passes: rerank each flagged query over all its buffered candidates, certified against the pass
         // bound (launch_flat_cand_rerank); only what that cannot certify re-runs on SPLIT3
         const int P = flat_cand_rerank_parts(cr_nsplit);
@@ -726,6 +775,7 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
         const int nf1 = nf;
         HIPANN_CHECK(hipMemcpyAsync(&nf, sh.nflag2.p, sizeof(int), hipMemcpyDeviceToHost, st));
         HIPANN_CHECK(hipStreamSynchronize(st));
+        ++ix.host_syncs;
         if (dbg) {
             std::vector<float> h((size_t)nf1 * 4);
             HIPANN_CHECK(hipMemcpy(h.data(), sh.tmpnorm.p, h.size() * sizeof(float), hipMemcpyDeviceToHost));
@@ -743,10 +793,20 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
     launch_ivf_gather_queries(xq, fl, nf, d, sh.fq.get<float>(), st);
     {
         TimerPause p0(ix.timer_main), p1(ix.timer_merge);
-        flat_shard_search(ix, sh, nf, sh.fq.get<float>(), k_user, kout, sh.fD.get<float>(), sh.fI.get<int64_t>(), st,
-                          kFlatSplit3);
+        flat_shard_search(ix, sh, nf, sh.fq.get<float>(), pend.k, kout, sh.fD.get<float>(), sh.fI.get<int64_t>(), st,
+                          rerun_form);
     }
     launch_ivf_scatter_results(sh.fD.get<float>(), sh.fI.get<int64_t>(), fl, nf, kout, D, I, st);
+}
+
+void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq, int k, int kout, float *D,
+                       int64_t *I, hipStream_t st, int form_override, FlatPending *pend) {
+    FlatPending local;
+    flat_shard_launch(ix, sh, nq, xq, k, kout, D, I, st, form_override, pend ? *pend : local);
+    if (pend || local.kind == FlatPending::kNone) return;
+    HIPANN_CHECK(hipStreamSynchronize(st));
+    ++ix.host_syncs;
+    flat_shard_finish(ix, sh, local, st);
 }
 
 }  // namespace hipann
@@ -846,8 +906,12 @@ static int flat_search_host(FlatIndex &ix, int64_t nq, const float *xq, int64_t 
     ix.h_q.ensure(qbytes);
     std::memcpy(ix.h_q.p, xq, qbytes);
     const size_t ob = (size_t)nq * kout;
-    for (auto &shp : ix.shards) {
-        FlatShard &sh = *shp;
+    const int np = (int)ix.shards.size();
+    // Launch phase: every shard's search on its own stream (devices run concurrently), no host wait.  The exact
+    // forms' flag counts travel to pinned host words with the results (flat_shard_finish reads them).
+    std::vector<FlatPending> pend((size_t)np);
+    for (int p = 0; p < np; ++p) {
+        FlatShard &sh = *ix.shards[p];
         DeviceGuard g(sh.device);
         sh.q.ensure(qbytes, sh.device);
         sh.out_d.ensure(ob * sizeof(float), sh.device);
@@ -856,45 +920,67 @@ static int flat_search_host(FlatIndex &ix, int64_t nq, const float *xq, int64_t 
         if (qbytes <= kKernelCopyMax) launch_copy_words(host_device_ptr(ix.h_q.p), sh.q.p, qbytes, sh.stream);
         else HIPANN_CHECK(hipMemcpyAsync(sh.q.p, ix.h_q.p, qbytes, hipMemcpyHostToDevice, sh.stream));
         flat_shard_search(ix, sh, nq, sh.q.get<float>(), keff, kout, sh.out_d.get<float>(), sh.out_i.get<int64_t>(),
-                          sh.stream);
+                          sh.stream, -1, &pend[(size_t)p]);
+        if (np > 1) {
+            if (!sh.done) HIPANN_CHECK(hipEventCreateWithFlags(&sh.done, hipEventDisableTiming));
+            HIPANN_CHECK(hipEventRecord(sh.done, sh.stream));
+        }
     }
     ix.h_d.ensure(ob * sizeof(float));
     ix.h_i.ensure(ob * sizeof(int64_t));
     FlatShard &s0 = *ix.shards[0];
-    if (ix.shards.size() == 1) {
-        DeviceGuard g(s0.device);
-        if (ob * sizeof(int64_t) <= kKernelCopyMax) {
-            launch_copy_words(s0.out_d.p, host_device_ptr(ix.h_d.p), ob * sizeof(float), s0.stream);
-            launch_copy_words(s0.out_i.p, host_device_ptr(ix.h_i.p), ob * sizeof(int64_t), s0.stream);
+    // Completion: results (merged on shard 0's device when sharded) to the host, ONE host synchronisation — which
+    // also covers every shard's flag count.  Only if a shard flagged queries: its re-runs, then the results again.
+    auto deliver = [&]() {
+        if (np == 1) {
+            DeviceGuard g(s0.device);
+            if (ob * sizeof(int64_t) <= kKernelCopyMax) {
+                launch_copy_words(s0.out_d.p, host_device_ptr(ix.h_d.p), ob * sizeof(float), s0.stream);
+                launch_copy_words(s0.out_i.p, host_device_ptr(ix.h_i.p), ob * sizeof(int64_t), s0.stream);
+            } else {
+                HIPANN_CHECK(hipMemcpyAsync(ix.h_d.p, s0.out_d.p, ob * sizeof(float), hipMemcpyDeviceToHost, s0.stream));
+                HIPANN_CHECK(hipMemcpyAsync(ix.h_i.p, s0.out_i.p, ob * sizeof(int64_t), hipMemcpyDeviceToHost, s0.stream));
+            }
         } else {
-            HIPANN_CHECK(hipMemcpyAsync(ix.h_d.p, s0.out_d.p, ob * sizeof(float), hipMemcpyDeviceToHost, s0.stream));
-            HIPANN_CHECK(hipMemcpyAsync(ix.h_i.p, s0.out_i.p, ob * sizeof(int64_t), hipMemcpyDeviceToHost, s0.stream));
-        }
-        HIPANN_CHECK(hipStreamSynchronize(s0.stream));
-    } else {
-        // gather per-device partial top-k onto shard 0's device, then one device merge
-        const int np = (int)ix.shards.size();
-        ix.gather_d.ensure(ob * np * sizeof(float), s0.device);
-        ix.gather_i.ensure(ob * np * sizeof(int64_t), s0.device);
-        ix.merged_d.ensure(ob * sizeof(float), s0.device);
-        ix.merged_i.ensure(ob * sizeof(int64_t), s0.device);
-        for (int p = 0; p < np; ++p) {
-            FlatShard &sh = *ix.shards[p];
-            DeviceGuard g(sh.device);
-            HIPANN_CHECK(hipStreamSynchronize(sh.stream));
-            HIPANN_CHECK(hipMemcpyPeerAsync(ix.gather_d.get<float>() + p * ob, s0.device, sh.out_d.p, sh.device,
-                                            ob * sizeof(float), s0.stream));
-            HIPANN_CHECK(hipMemcpyPeerAsync(ix.gather_i.get<int64_t>() + p * ob, s0.device, sh.out_i.p, sh.device,
-                                            ob * sizeof(int64_t), s0.stream));
+            // gather the per-device partial top-k onto shard 0's device (shard 0's stream waits for each shard's
+            // launch phase on the device, not the host), then one device merge
+            DeviceGuard g(s0.device);
+            ix.gather_d.ensure(ob * np * sizeof(float), s0.device);
+            ix.gather_i.ensure(ob * np * sizeof(int64_t), s0.device);
+            ix.merged_d.ensure(ob * sizeof(float), s0.device);
+            ix.merged_i.ensure(ob * sizeof(int64_t), s0.device);
+            for (int p = 0; p < np; ++p) {
+                FlatShard &sh = *ix.shards[p];
+                if (p > 0) HIPANN_CHECK(hipStreamWaitEvent(s0.stream, sh.done, 0));
+                HIPANN_CHECK(hipMemcpyPeerAsync(ix.gather_d.get<float>() + p * ob, s0.device, sh.out_d.p, sh.device,
+                                                ob * sizeof(float), s0.stream));
+                HIPANN_CHECK(hipMemcpyPeerAsync(ix.gather_i.get<int64_t>() + p * ob, s0.device, sh.out_i.p, sh.device,
+                                                ob * sizeof(int64_t), s0.stream));
+            }
+            const float sign = ix.metric == kIP ? -1.f : 1.f;
+            launch_merge_parts<long long>(ix.gather_d.get<float>(), ix.gather_i.get<long long>(), np, nq, kout, kout, 0,
+                                          sign, sign, ix.merged_d.get<float>(), ix.merged_i.get<int64_t>(), s0.stream);
+            HIPANN_CHECK(hipMemcpyAsync(ix.h_d.p, ix.merged_d.p, ob * sizeof(float), hipMemcpyDeviceToHost, s0.stream));
+            HIPANN_CHECK(hipMemcpyAsync(ix.h_i.p, ix.merged_i.p, ob * sizeof(int64_t), hipMemcpyDeviceToHost, s0.stream));
         }
         DeviceGuard g(s0.device);
-        const float sign = ix.metric == kIP ? -1.f : 1.f;
-        launch_merge_parts<long long>(ix.gather_d.get<float>(), ix.gather_i.get<long long>(), np, nq, kout, kout, 0,
-                                      sign, sign, ix.merged_d.get<float>(), ix.merged_i.get<int64_t>(), s0.stream);
-        HIPANN_CHECK(hipMemcpyAsync(ix.h_d.p, ix.merged_d.p, ob * sizeof(float), hipMemcpyDeviceToHost, s0.stream));
-        HIPANN_CHECK(hipMemcpyAsync(ix.h_i.p, ix.merged_i.p, ob * sizeof(int64_t), hipMemcpyDeviceToHost, s0.stream));
         HIPANN_CHECK(hipStreamSynchronize(s0.stream));
+        ++ix.host_syncs;
+    };
+    deliver();
+    bool rerun = false;
+    for (int p = 0; p < np; ++p) {
+        FlatShard &sh = *ix.shards[p];
+        if (pend[(size_t)p].kind == FlatPending::kNone || *sh.h_nflag.get<int>() <= 0) continue;
+        FenceScope fs(sh.fence, sh.stream, sh.device);
+        flat_shard_finish(ix, sh, pend[(size_t)p], sh.stream);
+        if (np > 1) {
+            DeviceGuard g(sh.device);
+            HIPANN_CHECK(hipEventRecord(sh.done, sh.stream));
+        }
+        rerun = true;
     }
+    if (rerun) deliver();
     std::memcpy(D, ix.h_d.p, ob * sizeof(float));
     std::memcpy(I, ix.h_i.p, ob * sizeof(int64_t));
     return 0;
@@ -1061,6 +1147,14 @@ int64_t hipann_flat_rerank_fallbacks(void *h) {
     auto *ix = static_cast<IndexBase *>(h);
     if (ix->kind != Kind::Flat) return -1;
     return static_cast<FlatIndex *>(ix)->rerank_fallbacks;
+}
+
+int64_t hipann_flat_host_syncs(void *h) {
+    if (!h) return -1;
+    auto *ix = static_cast<IndexBase *>(h);
+    if (ix->kind != Kind::Flat) return -1;
+    std::lock_guard<std::mutex> lk(ix->mu);
+    return static_cast<FlatIndex *>(ix)->host_syncs;
 }
 
 int hipann_last_search_path(void *h, int *form, int *filter_k, int *sublists) {

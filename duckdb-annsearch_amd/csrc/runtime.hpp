@@ -204,6 +204,26 @@ struct FlatShard {
     bool xi8_ok = false;
     float i8_rxmax = 0.f;
     StreamFence fence;       // cross-stream ordering of this shard's calls
+    HostBuf h_nflag;         // the launch phase's flag count, read back with the results (flat_shard_finish)
+    hipEvent_t done = nullptr;  // multi-device search: the shard's launch phase has drained (shard 0's stream waits)
+};
+
+// What a deferred Flat shard search (flat_shard_search with a FlatPending) leaves to flat_shard_finish: the exact
+// forms' flagged queries, whose count is read back into the shard's h_nflag by the launch phase.
+struct FlatPending {
+    enum Kind { kNone = 0, kSmallI8 = 1, kExact = 2 };
+    int kind = kNone;
+    int64_t nq = 0;
+    const float *xq = nullptr;
+    int k = 0, kout = 0;  // k of the re-run (k_user on the batched exact forms), output width
+    float *D = nullptr;
+    int64_t *I = nullptr;
+    // kExact over the bounded passes: the candidate buffers and pass bound for the all-candidate rerank
+    const float *cr_d = nullptr, *cr_bound = nullptr;
+    const int *cr_i = nullptr, *cr_n = nullptr;
+    int cr_nsplit = 0, cr_cap = 0;
+    float xmax2 = 0.f, rxmax = 0.f;
+    bool i8 = false;
 };
 
 struct IndexBase {
@@ -226,6 +246,7 @@ struct FlatIndex : IndexBase {
     int form = kFlatI8Exact;  // BLAS-path q·x form (FlatForm); shapes the int8 passes do not take run kFlatBf16Exact
     int64_t rerank_fallbacks = 0;  // queries re-run on the 3-term path by the exact form's bound check
     int64_t cand_reranked = 0;     // form 4: flagged queries sent to the all-candidate rerank first
+    int64_t host_syncs = 0;        // host synchronisations in search calls (hipann_flat_host_syncs)
     HostBuf h_q, h_d, h_i;
     DevBuf gather_d, gather_i, merged_d, merged_i;  // multi-device merge on shards[0]'s device
     FlatIndex() : IndexBase(Kind::Flat) {}

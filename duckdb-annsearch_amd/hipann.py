@@ -96,6 +96,7 @@ def lib() -> C.CDLL:
             "hipann_flat_get_form": ([vp], i32),
             "hipann_last_search_path": ([vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)], i32),
             "hipann_flat_rerank_fallbacks": ([vp], i64),
+            "hipann_flat_host_syncs": ([vp], i64),
             "hipann_merge_topk_device": ([i32, i32, i64, i64, vp, vp, vp, vp, vp, cp, i32], i32),
             "hipann_merge_topk_packed_device": ([i32, i32, i64, i64, vp, i64, vp, vp, vp, cp, i32], i32),
             "hipann_ivf_create": ([i32, i32, i32, i32, f, i64p, i64p, f, C.POINTER(C.c_int), i32, cp, i32], vp),
@@ -265,6 +266,10 @@ class _FlatForm:
     def rerank_fallbacks(self) -> int:
         """Queries the exact form's bound check re-ran on the 3-term path since creation."""
         return int(lib().hipann_flat_rerank_fallbacks(self._h))
+
+    def host_syncs(self) -> int:
+        """Host synchronisations made by this index's searches since creation (hipann_flat_host_syncs)."""
+        return int(lib().hipann_flat_host_syncs(self._h))
 
 
 class HipIndexFlat(_FlatForm, _Handle):

@@ -113,6 +113,12 @@ int hipann_flat_get_form(void *index);
  * the query, certified against the pass bound) could not certify either; the exact results replace
  * the flagged ones. */
 int64_t hipann_flat_rerank_fallbacks(void *index);
+/* Host synchronisations made by the search calls of a Flat index since it was created.  hipann_flat_search
+ * launches every shard (one per device of `devices[]`, each on its own stream) before it waits on any, gathers
+ * and merges on the first device behind device-side event waits, and synchronises ONCE, which also reads every
+ * shard's exact-form flag count; only a batch with flagged queries adds the syncs of their re-runs.  Building an
+ * image after an add (first search) adds one.  -1 for a NULL / non-Flat handle. */
+int64_t hipann_flat_host_syncs(void *index);
 
 /* The path the last search of `index` (Flat or IVF) took: *form = the distance form its scan ran
  * (HIPANN_FLAT_FORM_* / HIPANN_IVF_FORM_*; the exact forms' re-runs of flagged queries not counted),

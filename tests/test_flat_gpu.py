@@ -496,3 +496,46 @@ def test_flat_small_batch_int8_filter(gpu, oracle, nq, metric, scaled):
     if not scaled:  # the bound is conservative: a query whose 10th distance sits near its 64th key re-runs
         assert ix.rerank_fallbacks() <= max(1, nq // 4), ix.rerank_fallbacks()
     ix.close()
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+def test_flat_multi_shard_concurrent_one_host_sync(gpu, oracle, metric):
+    """the in-process multi-device handle (devices [0, 0, 0, 0]) launches every shard before it waits
+    on any — one host synchronisation per hipann_flat_search once the images exist, which also reads every shard's
+    exact-form flag count — on the batched int8 bounded passes (nq 256, 600K rows per shard) and the small-batch
+    int8 scan (nq 4); ids follow the oracle's parity rule."""
+    rng = np.random.default_rng(77 + metric)
+    n, d = 2_400_000, 128
+    xb = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    xq = rng.uniform(-1, 1, (256, d)).astype(np.float32)
+    ix = gpu.HipIndexFlat(d, metric, xb, devices=[0, 0, 0, 0])
+    for nq in (256, 4):
+        ix.search(xq[:nq], 10)  # builds the images (their own syncs)
+        s0 = ix.host_syncs()
+        for _ in range(3):
+            D, I = ix.search(xq[:nq], 10)
+        assert ix.host_syncs() - s0 == 3, (nq, ix.host_syncs() - s0)
+        assert ix.last_search_path()["form"] == ix.FORM_I8_EXACT
+        Do, Io = oracle.flat_search(xb, xq[:nq][:32], 10, metric)
+        check_topk_parity(xb, xq[:nq][:32], D[:32], I[:32], Do, Io, metric)
+    assert ix.rerank_fallbacks() == 0
+    ix.close()
+
+
+@pytest.mark.parametrize("nq", [256, 8])
+def test_flat_multi_shard_flagged_queries_finish(gpu, oracle, nq):
+    """Deferred completion with flagged queries: near-duplicate rows (the candidate-rerank case) over 4 shards on
+    one device; the flagged shards re-run after the single synchronisation and the results are delivered again.
+    Ids follow the oracle's parity rule on every query."""
+    rng = np.random.default_rng(31 + nq)
+    base = rng.standard_normal((4_000, 64), dtype=np.float32)
+    xb = np.repeat(base, 80, axis=0)  # 80 copies: deeper than any filter (64), so the bound check flags
+    xb += 1e-4 * rng.standard_normal(xb.shape, dtype=np.float32)
+    xb = xb[rng.permutation(len(xb))]
+    xq = rng.standard_normal((nq, 64), dtype=np.float32)
+    ix = gpu.HipIndexFlat(64, 0, xb, devices=[0, 0, 0, 0])
+    D, I = ix.search(xq, 10)
+    assert ix.rerank_fallbacks() > 0  # the deferred re-runs ran
+    Do, Io = oracle.flat_search(xb, xq, 10)
+    check_topk_parity(xb, xq, D, I, Do, Io)
+    ix.close()
