@@ -82,52 +82,103 @@ constexpr int kFusedMaxK = 64;   // fused GEMM / scan lists: one element per lan
 constexpr int kBlasThreshold = 20;  // FAISS distance_compute_blas_threshold
 constexpr int64_t kSmallTable = 16384;  // rows: below this, GEMM keys + per-query selection
 
-// Append rows to a shard's owned storage (capacity doubling, as MetalIndexFlat::add does).
+// Grow `b` to at least `need` bytes keeping its first `keep` bytes (device-to-device on `st`).
+void grow_keep(DevBuf &b, size_t need, size_t keep, int dev, hipStream_t st) {
+    if (b.p && need <= b.bytes) return;
+    DevBuf nb;
+    nb.ensure(need, dev);
+    if (b.p && keep) HIPANN_CHECK(hipMemcpyAsync(nb.p, b.p, std::min(keep, b.bytes), hipMemcpyDeviceToDevice, st));
+    HIPANN_CHECK(hipStreamSynchronize(st));  // the old buffer is freed on return
+    std::swap(b.p, nb.p);
+    std::swap(b.bytes, nb.bytes);
+    std::swap(b.device, nb.device);
+}
+
+float bits_to_float(unsigned u) {
+    float v;
+    std::memcpy(&v, &u, sizeof(v));
+    return v;
+}
+
+// Append rows to a shard's owned storage (capacity doubling, as MetalIndexFlat::add does, MetalIndexFlat.mm:255-269).
+// The search images built from the rows (int8 / bf16 tiles, per-row int8 scales) grow with the same capacity and
+// only the tiles holding new rows are re-tiled; the exact forms' bound terms (max ‖x‖², the largest int8 / bf16 row
+// residual) become running maxima over the new rows — an append costs the appended rows, not the table.
 void shard_append(FlatShard &sh, int d, int metric, const float *x_host, const float *x_dev, int64_t n) {
     if (n <= 0) return;
     DeviceGuard g(sh.device);
     FenceScope fs(sh.fence, sh.stream, sh.device);  // searches still running on other streams read sh.xb
-    const int64_t need = sh.n + n;
+    hipStream_t st = sh.stream;
+    const int64_t n0 = sh.n, need = sh.n + n;
     if (need > sh.cap || !sh.owns) {
-        int64_t cap = std::max<int64_t>(need, std::max<int64_t>(1024, sh.cap * 2));
+        const int64_t cap = std::max<int64_t>(need, std::max<int64_t>(1024, sh.cap * 2));
         DevBuf nb;
         nb.ensure((size_t)cap * d * sizeof(float), sh.device);
         if (sh.n > 0)
-            HIPANN_CHECK(hipMemcpyAsync(nb.get<float>(), sh.xb, (size_t)sh.n * d * sizeof(float),
-                                        hipMemcpyDeviceToDevice, sh.stream));
-        HIPANN_CHECK(hipStreamSynchronize(sh.stream));
+            HIPANN_CHECK(hipMemcpyAsync(nb.get<float>(), sh.xb, (size_t)sh.n * d * sizeof(float), hipMemcpyDeviceToDevice,
+                                        st));
+        HIPANN_CHECK(hipStreamSynchronize(st));
         std::swap(sh.xb_buf.p, nb.p);
         std::swap(sh.xb_buf.bytes, nb.bytes);
         sh.xb_buf.device = sh.device;
         sh.xb = sh.xb_buf.get<float>();
         sh.cap = cap;
         sh.owns = true;
-        if (metric == kL2) {
-            DevBuf nn;
-            nn.ensure((size_t)cap * sizeof(float), sh.device);
-            if (sh.n > 0)
-                HIPANN_CHECK(hipMemcpyAsync(nn.get<float>(), sh.xn.get<float>(), (size_t)sh.n * sizeof(float),
-                                            hipMemcpyDeviceToDevice, sh.stream));
-            HIPANN_CHECK(hipStreamSynchronize(sh.stream));
-            std::swap(sh.xn.p, nn.p);
-            std::swap(sh.xn.bytes, nn.bytes);
-            sh.xn.device = sh.device;
-        }
+        if (metric == kL2) grow_keep(sh.xn, (size_t)cap * sizeof(float), (size_t)sh.n * sizeof(float), sh.device, st);
     }
-    float *dst = sh.xb + sh.n * (int64_t)d;
+    float *dst = sh.xb + n0 * (int64_t)d;
     if (x_host)
-        HIPANN_CHECK(hipMemcpyAsync(dst, x_host, (size_t)n * d * sizeof(float), hipMemcpyHostToDevice, sh.stream));
+        HIPANN_CHECK(hipMemcpyAsync(dst, x_host, (size_t)n * d * sizeof(float), hipMemcpyHostToDevice, st));
     else
-        HIPANN_CHECK(hipMemcpyAsync(dst, x_dev, (size_t)n * d * sizeof(float), hipMemcpyDeviceToDevice, sh.stream));
-    if (metric == kL2) launch_row_norms(dst, n, d, sh.xn.get<float>() + sh.n, sh.stream);
-    HIPANN_CHECK(hipStreamSynchronize(sh.stream));
+        HIPANN_CHECK(hipMemcpyAsync(dst, x_dev, (size_t)n * d * sizeof(float), hipMemcpyDeviceToDevice, st));
+    if (metric == kL2) launch_row_norms(dst, n, d, sh.xn.get<float>() + n0, st);
     sh.n = need;
-    sh.xmax2 = -1.f;  // new rows: the exact form's bound is recomputed
-    sh.xb16_ok = false;  // and the bf16 / int8 images rebuilt
-    sh.xb16.release();
-    sh.xi8_ok = false;
-    sh.xi8.release();
-    sh.xscale.release();
+    // the images and bound terms, when built: tiles from the first one holding a new row to the end
+    const bool upd = sh.xmax2 >= 0.f || sh.xi8_ok || sh.xb16_ok;
+    if (upd) {
+        const int R = flat_bf16_tile_rows();
+        const int64_t t0 = n0 / R;                  // first tile with a new row (tiles before it are unchanged)
+        const int64_t capr = ceil_div(sh.cap, (int64_t)R) * R;
+        sh.app_stat.ensure(sizeof(unsigned) * 4, sh.device);
+        unsigned *stat = sh.app_stat.get<unsigned>();
+        HIPANN_CHECK(hipMemsetAsync(stat, 0, sizeof(unsigned) * 4, st));
+        sh.tmpnorm.ensure(sizeof(float) * (size_t)n, sh.device);
+        if (sh.xmax2 >= 0.f) {
+            const float *xn_new = sh.xn.get<float>() + n0;
+            if (metric != kL2) {
+                launch_row_norms(dst, n, d, sh.tmpnorm.get<float>(), st);
+                xn_new = sh.tmpnorm.get<float>();
+            }
+            launch_ivf_max_norm(xn_new, n, stat + 0, st);
+        }
+        if (sh.xi8_ok) {
+            const size_t tb = flat_i8_img_bytes(R, d, R);  // one tile
+            grow_keep(sh.xi8, flat_i8_img_bytes(capr, d, R), (size_t)t0 * tb, sh.device, st);
+            grow_keep(sh.xscale, sizeof(float) * (size_t)capr, sizeof(float) * (size_t)n0, sh.device, st);
+            float *rs = sh.tmpnorm.get<float>();
+            launch_i8_row_scale(dst, n, d, sh.xscale.get<float>() + n0, rs, st);
+            launch_ivf_max_norm(rs, n, stat + 1, st);
+            launch_i8_tile_rows(sh.xb + t0 * R * (int64_t)d, sh.xscale.get<float>() + t0 * R, sh.n - t0 * R, d, R,
+                                static_cast<char *>(sh.xi8.p) + (size_t)t0 * tb, st);
+        }
+        if (sh.xb16_ok) {
+            const size_t tb = flat_bf16_img_bytes(R, d, R);
+            grow_keep(sh.xb16, flat_bf16_img_bytes(capr, d, R), (size_t)t0 * tb, sh.device, st);
+            float *rs = sh.tmpnorm.get<float>();
+            launch_b16_row_residual2(dst, n, d, rs, st);
+            launch_ivf_max_norm(rs, n, stat + 2, st);
+            launch_b16_tile_rows(sh.xb + t0 * R * (int64_t)d, sh.n - t0 * R, d, R,
+                                 static_cast<char *>(sh.xb16.p) + (size_t)t0 * tb, st);
+        }
+        unsigned hs[4] = {0u, 0u, 0u, 0u};
+        HIPANN_CHECK(hipMemcpyAsync(hs, stat, sizeof(hs), hipMemcpyDeviceToHost, st));
+        HIPANN_CHECK(hipStreamSynchronize(st));
+        if (sh.xmax2 >= 0.f) sh.xmax2 = std::max(sh.xmax2, bits_to_float(hs[0]));
+        if (sh.xi8_ok) sh.i8_rxmax = std::max(sh.i8_rxmax, bits_to_float(hs[1]));
+        if (sh.xb16_ok) sh.bf16_rxmax = std::max(sh.bf16_rxmax, std::sqrt(bits_to_float(hs[2])) * 1.0001f);
+    } else {
+        HIPANN_CHECK(hipStreamSynchronize(st));
+    }
 }
 
 }  // namespace

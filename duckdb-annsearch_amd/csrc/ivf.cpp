@@ -79,23 +79,35 @@ std::unique_ptr<FlatIndex> make_quantizer(int d, int metric, const float *cen, i
     return q;
 }
 
-void upload_list_meta(IvfShard &sh, const std::vector<int64_t> &off, int nlist) {
+// off: physical list starts (nlist + 1; list l owns rows [off[l], off[l+1])), len: live rows per list (≤ capacity).
+void upload_list_meta(IvfShard &sh, const std::vector<int64_t> &off, const std::vector<int64_t> &len, int nlist) {
     DeviceGuard g(sh.device);
-    std::vector<int> len(nlist);
-    int64_t maxlen = 0;
+    std::vector<int> hl(nlist);
+    int64_t maxlen = 0, live = 0;
     for (int l = 0; l < nlist; ++l) {
-        HIPANN_REQUIRE(off[l + 1] - off[l] < (int64_t)0x7fffffff, "inverted list longer than 2^31-1 rows");
-        len[l] = (int)(off[l + 1] - off[l]);
+        HIPANN_REQUIRE(len[l] >= 0 && len[l] <= off[l + 1] - off[l], "list length exceeds its capacity");
+        HIPANN_REQUIRE(len[l] < (int64_t)0x7fffffff, "inverted list longer than 2^31-1 rows");
+        hl[l] = (int)len[l];
         maxlen = std::max<int64_t>(maxlen, len[l]);
+        live += len[l];
     }
     sh.max_nch = (int)std::max<int64_t>(1, ceil_div(maxlen, ivf_chunk_rows()));
     sh.h_off = off;
+    sh.h_len = len;
+    sh.n = off[nlist];
+    sh.live = live;
     sh.list_off.ensure(sizeof(int64_t) * (nlist + 1), sh.device);
     sh.list_len.ensure(sizeof(int) * nlist, sh.device);
     HIPANN_CHECK(hipMemcpyAsync(sh.list_off.p, off.data(), sizeof(int64_t) * (nlist + 1), hipMemcpyHostToDevice,
                                 sh.stream));
-    HIPANN_CHECK(hipMemcpyAsync(sh.list_len.p, len.data(), sizeof(int) * nlist, hipMemcpyHostToDevice, sh.stream));
+    HIPANN_CHECK(hipMemcpyAsync(sh.list_len.p, hl.data(), sizeof(int) * nlist, hipMemcpyHostToDevice, sh.stream));
     HIPANN_CHECK(hipStreamSynchronize(sh.stream));
+}
+
+std::vector<int64_t> dense_lengths(const std::vector<int64_t> &off, int nlist) {
+    std::vector<int64_t> len(nlist);
+    for (int l = 0; l < nlist; ++l) len[l] = off[l + 1] - off[l];
+    return len;
 }
 
 // 32-row pass offsets of every list (the tiled copies' layout); returns the total pass count.
@@ -116,8 +128,8 @@ void ensure_tiled_codes(IvfShard &sh, int d, int nlist, hipStream_t st) {
     const int64_t np = ensure_tpass(sh, nlist, st);
     const int64_t pf = ivf_mfma_pass_floats(d);
     sh.codes_t.ensure(sizeof(float) * (size_t)std::max<int64_t>(np, 1) * pf, sh.device);
-    launch_ivf_tile_codes(sh.codes, sh.list_off.get<int64_t>(), sh.tpass_off.get<int64_t>(), nlist, np, d,
-                          sh.codes_t.get<float>(), st);
+    launch_ivf_tile_codes(sh.codes, sh.list_off.get<int64_t>(), sh.list_len.get<int>(), sh.tpass_off.get<int64_t>(), nlist,
+                          np, d, sh.codes_t.get<float>(), st);
     HIPANN_CHECK(hipStreamSynchronize(st));
 }
 
@@ -145,8 +157,8 @@ bool ensure_half_codes(IvfShard &sh, int d, int nlist, hipStream_t st) {
     const float scale = std::ldexp(1.f, sh.half_es);
     const int64_t np = ensure_tpass(sh, nlist, st);
     sh.codes_h.ensure((size_t)std::max<int64_t>(np, 1) * (size_t)ivf_half_pass_bytes(d), sh.device);
-    launch_ivf_tile_half(sh.codes, sh.list_off.get<int64_t>(), sh.tpass_off.get<int64_t>(), nlist, np, d, scale,
-                         sh.codes_h.p, st);
+    launch_ivf_tile_half(sh.codes, sh.list_off.get<int64_t>(), sh.list_len.get<int>(), sh.tpass_off.get<int64_t>(), nlist,
+                         np, d, scale, sh.codes_h.p, st);
     launch_ivf_half_residual(sh.codes, sh.n, d, scale, sh.nflag.get<unsigned>(), st);
     HIPANN_CHECK(hipMemcpyAsync(&bits, sh.nflag.p, sizeof(unsigned), hipMemcpyDeviceToHost, st));
     HIPANN_CHECK(hipStreamSynchronize(st));
@@ -374,29 +386,31 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
         if (half)
             launch_ivf_scan_mfma_h(xq, nq, sh.hsplit.p, sh.hits.get<float>(), sh.hres.get<float>(), sh.half_es, qn, d,
                                    metric, sh.codes_h.p, sh.tpass_off.get<int64_t>(), sh.xnorm.get<float>(),
-                                   sh.list_off.get<int64_t>(), sh.cnt.get<int>(), sh.bucket_off.get<int>(),
+                                   sh.list_off.get<int64_t>(), sh.list_len.get<int>(), sh.cnt.get<int>(), sh.bucket_off.get<int>(),
                                    sh.item_off.get<int>(), sh.bucket.get<int>(), sh.slot_off.get<int>(), nlist, np, k,
                                    max_items, qbound, sh.part_d.get<float>(), sh.part_i.get<int>(), st, true,
                                    sub ? 1 : 0);
         else if (bigk)
-            launch_ivf_scan_bigk(xq, d, metric, sh.codes, sh.list_off.get<int64_t>(), sh.coarse_i.get<int64_t>(),
+            launch_ivf_scan_bigk(xq, d, metric, sh.codes, sh.list_off.get<int64_t>(), sh.list_len.get<int>(),
+                                 sh.coarse_i.get<int64_t>(),
                                  nq * np, np, sh.slot_off.get<int>(), nq * np * std::max(sh.max_nch, 1), k,
                                  sh.part_d.get<float>(), sh.part_i.get<int>(), st);
         else if (ivf_form_split(form))
             launch_ivf_scan_mfma_bf(ivf_form_terms(form), xq, nq, sh.qsplit.p, qn, d, metric, sh.codes_t.get<float>(),
                                     sh.tpass_off.get<int64_t>(), sh.xnorm.get<float>(), sh.list_off.get<int64_t>(),
-                                    sh.cnt.get<int>(), sh.bucket_off.get<int>(), sh.item_off.get<int>(),
+                                    sh.list_len.get<int>(), sh.cnt.get<int>(), sh.bucket_off.get<int>(), sh.item_off.get<int>(),
                                     sh.bucket.get<int>(), sh.slot_off.get<int>(), nlist, np, k, max_items, qbound,
                                     sh.part_d.get<float>(), sh.part_i.get<int>(), st, sub ? 1 : 0);
         else if (form == kFormDecomposed)
             launch_ivf_scan_mfma(xq, qn, d, metric, sh.codes_t.get<float>(), sh.tpass_off.get<int64_t>(),
-                                 sh.xnorm.get<float>(), sh.list_off.get<int64_t>(), sh.cnt.get<int>(),
+                                 sh.xnorm.get<float>(), sh.list_off.get<int64_t>(), sh.list_len.get<int>(),
+                                 sh.cnt.get<int>(),
                                  sh.bucket_off.get<int>(), sh.item_off.get<int>(), sh.bucket.get<int>(),
                                  sh.slot_off.get<int>(), nlist, np, k, max_items, qbound, sh.part_d.get<float>(),
                                  sh.part_i.get<int>(), st);
         else
             launch_ivf_scan(xq, qn, d, metric, form, sh.codes, sh.xnorm.get<float>(), sh.list_off.get<int64_t>(),
-                            sh.cnt.get<int>(), sh.bucket_off.get<int>(), sh.item_off.get<int>(), sh.bucket.get<int>(),
+                            sh.list_len.get<int>(), sh.cnt.get<int>(), sh.bucket_off.get<int>(), sh.item_off.get<int>(), sh.bucket.get<int>(),
                             sh.slot_off.get<int>(), nlist, np, nq, k, max_items, qbound, sh.part_d.get<float>(),
                             sh.part_i.get<int>(), st);
     }
@@ -454,11 +468,94 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
 }
 
 
+// Grow a shard's CSR so that list l can take add[l] more rows.  A list that overflows gets capacity
+// max(need, cap + max(cap / 4, 64)) rows — geometric growth (O(1) amortised copies per appended row, the doubling
+// of MetalIndexFlat::add, MetalIndexFlat.mm:255-269, at ×1.25: a 10M × 768 table at ×2 would hold 61 GB of codes);
+// borrowed storage is copied into owned buffers.  Live rows, labels, norms and the tiled images' passes move list by
+// list (device-to-device, in order); the slack rows are zero (whole-table maxima read them).
+static void ivf_relayout(IvfIndex &ix, IvfShard &sh, const std::vector<int64_t> &add) {
+    const int nlist = ix.nlist, d = ix.d;
+    hipStream_t st = sh.stream;
+    std::vector<int64_t> off(nlist + 1, 0);
+    for (int l = 0; l < nlist; ++l) {
+        const int64_t cap = sh.h_off[l + 1] - sh.h_off[l], need = sh.h_len[l] + add[l];
+        const int64_t ncap = need > cap ? std::max(need, cap + std::max<int64_t>(cap / 4, 64)) : cap;
+        off[l + 1] = off[l] + ncap;
+    }
+    const int64_t N = off[nlist];
+    DevBuf codes_nb, ids_nb, xn_nb, h_nb, t_nb, tp_nb;
+    codes_nb.ensure(sizeof(float) * (size_t)std::max<int64_t>(N, 1) * d, sh.device);
+    ids_nb.ensure(sizeof(int64_t) * (size_t)std::max<int64_t>(N, 1), sh.device);
+    HIPANN_CHECK(hipMemsetAsync(codes_nb.p, 0, codes_nb.bytes, st));
+    const bool xn = ix.metric == kL2 && sh.xnorm.p;
+    if (xn) {
+        xn_nb.ensure(sizeof(float) * (size_t)std::max<int64_t>(N, 1), sh.device);
+        HIPANN_CHECK(hipMemsetAsync(xn_nb.p, 0, xn_nb.bytes, st));
+    }
+    std::vector<int64_t> tp_old(nlist + 1, 0), tp(nlist + 1, 0);
+    for (int l = 0; l < nlist; ++l) {
+        tp_old[l + 1] = tp_old[l] + ceil_div(sh.h_off[l + 1] - sh.h_off[l], 32);
+        tp[l + 1] = tp[l] + ceil_div(off[l + 1] - off[l], 32);
+    }
+    const bool img_h = sh.half_state > 0 && sh.codes_h.p, img_t = sh.codes_t.p != nullptr;
+    const size_t hpb = (size_t)ivf_half_pass_bytes(d), tpb = sizeof(float) * (size_t)ivf_mfma_pass_floats(d);
+    if (img_h) {
+        h_nb.ensure(hpb * (size_t)std::max<int64_t>(tp[nlist], 1), sh.device);
+        HIPANN_CHECK(hipMemsetAsync(h_nb.p, 0, h_nb.bytes, st));
+    }
+    if (img_t) {
+        t_nb.ensure(tpb * (size_t)std::max<int64_t>(tp[nlist], 1), sh.device);
+        HIPANN_CHECK(hipMemsetAsync(t_nb.p, 0, t_nb.bytes, st));
+    }
+    for (int l = 0; l < nlist; ++l) {
+        const int64_t len = sh.h_len[l];
+        if (!len) continue;
+        const int64_t o0 = sh.h_off[l], o1 = off[l];
+        HIPANN_CHECK(hipMemcpyAsync(codes_nb.get<float>() + o1 * d, sh.codes + o0 * d, sizeof(float) * (size_t)len * d,
+                                    hipMemcpyDeviceToDevice, st));
+        HIPANN_CHECK(hipMemcpyAsync(ids_nb.get<int64_t>() + o1, sh.ids + o0, sizeof(int64_t) * (size_t)len,
+                                    hipMemcpyDeviceToDevice, st));
+        if (xn)
+            HIPANN_CHECK(hipMemcpyAsync(xn_nb.get<float>() + o1, sh.xnorm.get<float>() + o0, sizeof(float) * (size_t)len,
+                                        hipMemcpyDeviceToDevice, st));
+        const int64_t np = ceil_div(len, 32);  // the passes holding live rows (a pass's rows past len are zero)
+        if (img_h)
+            HIPANN_CHECK(hipMemcpyAsync(static_cast<char *>(h_nb.p) + hpb * (size_t)tp[l],
+                                        static_cast<const char *>(sh.codes_h.p) + hpb * (size_t)tp_old[l],
+                                        hpb * (size_t)np, hipMemcpyDeviceToDevice, st));
+        if (img_t)
+            HIPANN_CHECK(hipMemcpyAsync(static_cast<char *>(t_nb.p) + tpb * (size_t)tp[l],
+                                        static_cast<const char *>(sh.codes_t.p) + tpb * (size_t)tp_old[l],
+                                        tpb * (size_t)np, hipMemcpyDeviceToDevice, st));
+    }
+    tp_nb.ensure(sizeof(int64_t) * (nlist + 1), sh.device);
+    HIPANN_CHECK(hipMemcpyAsync(tp_nb.p, tp.data(), sizeof(int64_t) * (nlist + 1), hipMemcpyHostToDevice, st));
+    HIPANN_CHECK(hipStreamSynchronize(st));
+    auto take = [](DevBuf &dst, DevBuf &src) {
+        std::swap(dst.p, src.p);
+        std::swap(dst.bytes, src.bytes);
+        std::swap(dst.device, src.device);
+    };
+    take(sh.codes_buf, codes_nb);
+    take(sh.ids_buf, ids_nb);
+    sh.codes = sh.codes_buf.get<float>();  // borrowed storage becomes owned here
+    sh.ids = sh.ids_buf.get<int64_t>();
+    sh.owns_codes = true;
+    if (xn) take(sh.xnorm, xn_nb);
+    if (img_h) take(sh.codes_h, h_nb);
+    if (img_t) take(sh.codes_t, t_nb);
+    if (img_h || img_t) take(sh.tpass_off, tp_nb);
+    else sh.tpass_off.release();  // recomputed from the new capacities when an image is built
+    upload_list_meta(sh, off, sh.h_len, nlist);
+}
+
 // IndexIVF::add_with_ids (FAISS 1.13.2, external): rows are assigned to their nearest centroid by the
 // coarse quantizer (quantizer->assign, k = 1, in blocks of 65536 rows — so the Flat nq < 20 direct-form
 // rule applies per block) and appended to their lists in insertion order; labels are `ids` or
-// ntotal + i.  On the GPU copy this replaces the reference's invalidate-on-append
-// (faiss_index.cpp:469): the HBM lists are rebuilt per shard with the new rows in place.
+// ntotal + i.  On the GPU copy this replaces the reference's invalidate-on-append (faiss_index.cpp:469): the new
+// rows go into their lists' slack in HBM (ivf_relayout grows the lists that overflow, amortised), with their norms,
+// the touched passes of the tiled images and running maxima — the cost of an append is the appended rows, not the
+// table.
 static void ivf_add_rows(IvfIndex &ix, int64_t n, const float *xb, const int64_t *ids) {
     const int d = ix.d, nlist = ix.nlist;
     IvfShard &s0 = *ix.shards[0];
@@ -501,59 +598,99 @@ static void ivf_add_rows(IvfIndex &ix, int64_t n, const float *xb, const int64_t
         std::memcpy(hc.get<float>() + j * d, xb + perm[j] * d, sizeof(float) * d);
         hi.get<int64_t>()[j] = ids ? ids[perm[j]] : base + perm[j];
     }
-    // 3. rebuild each shard that owns a list with new rows
+    // 3. every shard that owns a list with new rows: grow the lists that overflow (ivf_relayout, amortised), then
+    //    the new rows straight into their lists' slack (one scatter kernel), their norms and the tiled images' touched
+    //    passes; the bounds' maxima follow the new rows (running maxima, no rescan of the table)
+    const int metric = ix.metric;
     for (size_t s = 0; s < ix.shards.size(); ++s) {
         IvfShard &sh = *ix.shards[s];
+        std::vector<int64_t> add(nlist, 0);
         int64_t add_s = 0;
-        for (int l = 0; l < nlist; ++l)
-            if (ix.owner[l] == (int)s) add_s += cnt[l + 1];
+        bool grow = !sh.owns_codes;
+        for (int l = 0; l < nlist; ++l) {
+            if (ix.owner[l] != (int)s) continue;
+            add[l] = cnt[l + 1];
+            add_s += add[l];
+            if (sh.h_len[l] + add[l] > sh.h_off[l + 1] - sh.h_off[l]) grow = true;
+        }
         if (!add_s) continue;
         DeviceGuard g(sh.device);
-        std::vector<int64_t> off(nlist + 1, 0);
-        for (int l = 0; l < nlist; ++l)
-            off[l + 1] = off[l] + (sh.h_off[l + 1] - sh.h_off[l]) + (ix.owner[l] == (int)s ? cnt[l + 1] : 0);
-        const int64_t n_new = off[nlist];
-        DevBuf stage_c, stage_i, codes_nb, ids_nb;
-        stage_c.ensure(sizeof(float) * (size_t)n * d, sh.device);
-        stage_i.ensure(sizeof(int64_t) * (size_t)n, sh.device);
-        HIPANN_CHECK(hipMemcpyAsync(stage_c.p, hc.p, sizeof(float) * (size_t)n * d, hipMemcpyHostToDevice, sh.stream));
-        HIPANN_CHECK(hipMemcpyAsync(stage_i.p, hi.p, sizeof(int64_t) * (size_t)n, hipMemcpyHostToDevice, sh.stream));
-        codes_nb.ensure(sizeof(float) * (size_t)n_new * d, sh.device);
-        ids_nb.ensure(sizeof(int64_t) * (size_t)n_new, sh.device);
+        hipStream_t ss = sh.stream;
+        if (grow) ivf_relayout(ix, sh, add);
+        // physical destination of every staged row (−1: a list of another shard), and the tiled passes it touches
+        HostBuf hd, hp;
+        hd.ensure(sizeof(int64_t) * (size_t)n);
+        int64_t *dst = hd.get<int64_t>();
+        std::fill(dst, dst + n, (int64_t)-1);
+        std::vector<int64_t> tp(nlist + 1, 0);
+        for (int l = 0; l < nlist; ++l) tp[l + 1] = tp[l] + ceil_div(sh.h_off[l + 1] - sh.h_off[l], 32);
+        std::vector<int64_t> passes;
+        std::vector<int64_t> len = sh.h_len;
         for (int l = 0; l < nlist; ++l) {
-            const int64_t old_len = sh.h_off[l + 1] - sh.h_off[l];
-            if (old_len) {
-                HIPANN_CHECK(hipMemcpyAsync(codes_nb.get<float>() + off[l] * d, sh.codes + sh.h_off[l] * d,
-                                            sizeof(float) * (size_t)old_len * d, hipMemcpyDeviceToDevice, sh.stream));
-                HIPANN_CHECK(hipMemcpyAsync(ids_nb.get<int64_t>() + off[l], sh.ids + sh.h_off[l],
-                                            sizeof(int64_t) * (size_t)old_len, hipMemcpyDeviceToDevice, sh.stream));
-            }
-            const int64_t add_l = ix.owner[l] == (int)s ? cnt[l + 1] : 0;
-            if (add_l) {
-                HIPANN_CHECK(hipMemcpyAsync(codes_nb.get<float>() + (off[l] + old_len) * d,
-                                            stage_c.get<float>() + noff[l] * d, sizeof(float) * (size_t)add_l * d,
-                                            hipMemcpyDeviceToDevice, sh.stream));
-                HIPANN_CHECK(hipMemcpyAsync(ids_nb.get<int64_t>() + off[l] + old_len, stage_i.get<int64_t>() + noff[l],
-                                            sizeof(int64_t) * (size_t)add_l, hipMemcpyDeviceToDevice, sh.stream));
+            if (!add[l]) continue;
+            for (int64_t j = noff[l]; j < noff[l + 1]; ++j) dst[j] = sh.h_off[l] + len[l] + (j - noff[l]);
+            for (int64_t p = len[l] / 32; p < ceil_div(len[l] + add[l], 32); ++p) passes.push_back(tp[l] + p);
+            len[l] += add[l];
+        }
+        const bool img_h = sh.half_state > 0 && sh.codes_h.p, img_t = sh.codes_t.p != nullptr;
+        sh.app_rows.ensure(sizeof(float) * (size_t)n * d, sh.device);
+        sh.app_ids.ensure(sizeof(int64_t) * (size_t)n, sh.device);
+        sh.app_dst.ensure(sizeof(int64_t) * (size_t)n, sh.device);
+        sh.app_norm.ensure(sizeof(float) * (size_t)n, sh.device);
+        sh.app_stat.ensure(sizeof(unsigned) * 4, sh.device);
+        HIPANN_CHECK(hipMemcpyAsync(sh.app_rows.p, hc.p, sizeof(float) * (size_t)n * d, hipMemcpyHostToDevice, ss));
+        HIPANN_CHECK(hipMemcpyAsync(sh.app_ids.p, hi.p, sizeof(int64_t) * (size_t)n, hipMemcpyHostToDevice, ss));
+        HIPANN_CHECK(hipMemcpyAsync(sh.app_dst.p, dst, sizeof(int64_t) * (size_t)n, hipMemcpyHostToDevice, ss));
+        // norms over the staged block with the table's own kernel (the bits a rebuild computes), then the scatter
+        launch_row_norms(sh.app_rows.get<float>(), n, d, sh.app_norm.get<float>(), ss);
+        launch_ivf_append_scatter(sh.app_rows.get<float>(), sh.app_norm.get<float>(), sh.app_ids.get<int64_t>(),
+                                  sh.app_dst.get<int64_t>(), n, d, sh.codes_buf.get<float>(), sh.ids_buf.get<int64_t>(),
+                                  metric == kL2 ? sh.xnorm.get<float>() : nullptr, ss);
+        // the new rows' maxima (over the whole staged block: a superset of this shard's rows, so only conservative)
+        unsigned *stat = sh.app_stat.get<unsigned>();
+        launch_ivf_max_norm(sh.app_norm.get<float>(), n, stat, ss);
+        const float hscale = std::ldexp(1.f, sh.half_es);
+        if (img_h) {
+            launch_ivf_max_abs(sh.app_rows.get<float>(), n * (int64_t)d, stat + 1, ss);
+            launch_ivf_half_residual(sh.app_rows.get<float>(), n, d, hscale, stat + 2, ss);
+        }
+        // live lengths, then the touched passes of the tiled images re-tiled from the (grown) lists
+        upload_list_meta(sh, sh.h_off, len, nlist);
+        if ((img_h || img_t) && !passes.empty()) {
+            hp.ensure(sizeof(int64_t) * passes.size());
+            std::memcpy(hp.p, passes.data(), sizeof(int64_t) * passes.size());
+            sh.app_pass.ensure(sizeof(int64_t) * passes.size(), sh.device);
+            HIPANN_CHECK(hipMemcpyAsync(sh.app_pass.p, hp.p, sizeof(int64_t) * passes.size(), hipMemcpyHostToDevice, ss));
+            const int64_t npass = (int64_t)passes.size();
+            if (img_h)
+                launch_ivf_tile_half(sh.codes, sh.list_off.get<int64_t>(), sh.list_len.get<int>(),
+                                     sh.tpass_off.get<int64_t>(), nlist, npass, d, hscale, sh.codes_h.p, ss,
+                                     sh.app_pass.get<int64_t>());
+            if (img_t)
+                launch_ivf_tile_codes(sh.codes, sh.list_off.get<int64_t>(), sh.list_len.get<int>(),
+                                      sh.tpass_off.get<int64_t>(), nlist, npass, d, sh.codes_t.get<float>(), ss,
+                                      sh.app_pass.get<int64_t>());
+        }
+        unsigned hs[4] = {0u, 0u, 0u, 0u};
+        HIPANN_CHECK(hipMemcpyAsync(hs, stat, sizeof(hs), hipMemcpyDeviceToHost, ss));
+        HIPANN_CHECK(hipStreamSynchronize(ss));
+        float v;
+        std::memcpy(&v, &hs[0], sizeof(v));
+        if (sh.xmax2 >= 0.f) sh.xmax2 = std::max(sh.xmax2, v);  // max ‖x‖² (the rerank bound's row term)
+        if (img_h) {
+            float mx, r2;
+            std::memcpy(&mx, &hs[1], sizeof(mx));
+            std::memcpy(&r2, &hs[2], sizeof(r2));
+            if (hs[1] >= 0x7f800000u) {  // a non-finite new entry: the fp16 form no longer applies (form 5 runs)
+                sh.half_state = -1;
+                sh.codes_h.release();
+            } else if (mx >= std::ldexp(1.f, 14 - sh.half_es)) {  // outside the image's scale: rebuilt at the next search
+                sh.half_state = 0;
+                sh.codes_h.release();
+            } else {
+                sh.half_rxmax = std::max(sh.half_rxmax, std::sqrt(r2) * 1.0001f);
             }
         }
-        HIPANN_CHECK(hipStreamSynchronize(sh.stream));
-        std::swap(sh.codes_buf.p, codes_nb.p);
-        std::swap(sh.codes_buf.bytes, codes_nb.bytes);
-        std::swap(sh.codes_buf.device, codes_nb.device);
-        std::swap(sh.ids_buf.p, ids_nb.p);
-        std::swap(sh.ids_buf.bytes, ids_nb.bytes);
-        std::swap(sh.ids_buf.device, ids_nb.device);
-        sh.codes = sh.codes_buf.get<float>();  // borrowed storage becomes owned here
-        sh.ids = sh.ids_buf.get<int64_t>();
-        sh.n = n_new;
-        upload_list_meta(sh, off, nlist);
-        compute_row_norms(sh, d, ix.metric);
-        sh.codes_t.release();  // the MFMA scans' tiled copies are rebuilt at the next search
-        sh.tpass_off.release();
-        sh.codes_h.release();
-        sh.half_state = 0;
-        sh.xmax2 = -1.f;
     }
 }
 
@@ -627,8 +764,9 @@ void *hipann_ivf_create(int d, int metric, int nlist, int nprobe, const float *c
             }
             sh->codes = sh->codes_buf.get<float>();
             sh->ids = sh->ids_buf.get<int64_t>();
+            sh->owns_codes = true;
             HIPANN_CHECK(hipStreamSynchronize(sh->stream));
-            upload_list_meta(*sh, off, nlist);
+            upload_list_meta(*sh, off, dense_lengths(off, nlist), nlist);
             compute_row_norms(*sh, d, metric);
             sh->quant = make_quantizer(d, metric, sh->centroids, nlist, sh->device, sh->stream);
             ix->shards.push_back(std::move(sh));
@@ -677,13 +815,14 @@ void *hipann_ivf_create_device(int d, int metric, int nlist, int nprobe, const f
             sh->centroids = sh->centroids_buf.get<float>();
             sh->codes = sh->codes_buf.get<float>();
             sh->ids = sh->ids_buf.get<int64_t>();
+            sh->owns_codes = true;
         } else {
             sh->centroids = centroids_dev;
             sh->codes = codes_dev;
             sh->ids = ids_dev;
         }
         std::vector<int64_t> off(list_offsets, list_offsets + nlist + 1);
-        upload_list_meta(*sh, off, nlist);
+        upload_list_meta(*sh, off, dense_lengths(off, nlist), nlist);
         compute_row_norms(*sh, d, metric);
         sh->quant = make_quantizer(d, metric, sh->centroids, nlist, device, sh->stream);
         ix->shards.push_back(std::move(sh));
@@ -812,7 +951,7 @@ int hipann_ivf_search_device(void *h, int64_t nq, const float *xq_dev, int64_t k
         hipStream_t st = static_cast<hipStream_t>(stream);  // NULL = the default (null) stream
         vx->last_nq = nq;
         vx->last_np = std::min(vx->nprobe, vx->nlist);
-        const int keff = (int)std::min<int64_t>(k, std::max<int64_t>(sh.n, 1));
+        const int keff = (int)std::min<int64_t>(k, std::max<int64_t>(sh.live, 1));
         FenceScope fs(sh.fence, st, sh.device);  // the previous call's kernels may still use this shard's scratch
         ivf_shard_search(*vx, sh, nq, xq_dev, keff, (int)k, D_dev, I_dev, st);
         return 0;
@@ -855,7 +994,7 @@ int hipann_ivf_export(void *h, float *centroids, int64_t *list_offsets, int64_t 
         std::vector<int64_t> off(nlist + 1, 0);
         for (int l = 0; l < nlist; ++l) {
             const IvfShard &sh = *vx->shards[vx->owner[l]];
-            off[l + 1] = off[l] + (sh.h_off[l + 1] - sh.h_off[l]);
+            off[l + 1] = off[l] + sh.h_len[l];  // live rows (the shard's physical list may hold append slack)
         }
         if (list_offsets) std::memcpy(list_offsets, off.data(), sizeof(int64_t) * (nlist + 1));
         IvfShard &s0 = *vx->shards[0];

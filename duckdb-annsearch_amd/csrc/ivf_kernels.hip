@@ -563,7 +563,7 @@ __device__ __forceinline__ void ivf_scan_item(const float *__restrict__ Q, int d
 // LDS/VMEM waits need other waves on the SIMD to cover them.
 template <bool VEC4, bool IP>
 __global__ void __launch_bounds__(IVF_THREADS, 2 * IVF_THREADS / 256)
-ivf_scan_topk(const float *__restrict__ Q, int d, const float *__restrict__ codes, const int64_t *__restrict__ list_off,
+ivf_scan_topk(const float *__restrict__ Q, int d, const float *__restrict__ codes, const int64_t *__restrict__ list_off, const int *__restrict__ list_len,
               const int *__restrict__ cnt, const int *__restrict__ bucket_off, const int *__restrict__ item_off,
               const int *__restrict__ bucket, const int *__restrict__ slot_off, int nlist, int nprobe, int64_t nq,
               int k, float *__restrict__ part_d, int *__restrict__ part_i) {
@@ -581,7 +581,7 @@ ivf_scan_topk(const float *__restrict__ Q, int d, const float *__restrict__ code
         if (item_off[mid] <= item) lo = mid; else hi = mid - 1;
     }
     const int l = lo;
-    const int64_t lr0 = list_off[l], lr1 = list_off[l + 1];
+    const int64_t lr0 = list_off[l], lr1 = lr0 + list_len[l];
     const int nch = ivf_nch((int)(lr1 - lr0));
     const int rem = item - item_off[l];
     const int g = rem / nch, chunk = rem - g * nch;  // (query group, row chunk)
@@ -964,7 +964,7 @@ __device__ __forceinline__ void ivf_dot_dispatch(int nwq, int d, const float *co
 template <bool IP>
 __global__ void __launch_bounds__(DT_THREADS, DT_BLOCKS * DT_THREADS / 256)
 ivf_scan_dot(const float *__restrict__ Q, const float *__restrict__ qn, int d, const float *__restrict__ codes,
-             const float *__restrict__ xn, const int64_t *__restrict__ list_off, const int *__restrict__ cnt,
+             const float *__restrict__ xn, const int64_t *__restrict__ list_off, const int *__restrict__ list_len, const int *__restrict__ cnt,
              const int *__restrict__ bucket_off, const int *__restrict__ item_off, const int *__restrict__ bucket,
              const int *__restrict__ slot_off, int nlist, int nprobe, int k, float *__restrict__ part_d,
              int *__restrict__ part_i) {
@@ -978,7 +978,7 @@ ivf_scan_dot(const float *__restrict__ Q, const float *__restrict__ qn, int d, c
         if (item_off[mid] <= item) lo = mid; else hi = mid - 1;
     }
     const int l = lo;
-    const int64_t lr0 = list_off[l], lr1 = list_off[l + 1];
+    const int64_t lr0 = list_off[l], lr1 = lr0 + list_len[l];
     const int c = cnt[l];
     const int ng = (c + DT_G - 1) / DT_G;
     const int rem = item - item_off[l];
@@ -1052,7 +1052,7 @@ ivf_merge_topk(const float *__restrict__ pd, const int *__restrict__ pi, const i
 template <bool IP>
 __global__ void __launch_bounds__(256)
 ivf_scan_slot_bigk(const float *__restrict__ Q, int d, const float *__restrict__ codes,
-                   const int64_t *__restrict__ list_off, const int64_t *__restrict__ probes, int64_t npairs,
+                   const int64_t *__restrict__ list_off, const int *__restrict__ list_len, const int64_t *__restrict__ probes, int64_t npairs,
                    int nprobe, const int *__restrict__ slot_off, int k, float *__restrict__ part_d,
                    int *__restrict__ part_i) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -1070,8 +1070,9 @@ ivf_scan_slot_bigk(const float *__restrict__ Q, int d, const float *__restrict__
     const int64_t pair = lo;
     const int chunk = slot - slot_off[pair];
     const int64_t l = probes[pair];
+    const int64_t lend = list_off[l] + list_len[l];
     const int64_t r0 = list_off[l] + (int64_t)chunk * IVF_CH;
-    const int64_t r1 = r0 + IVF_CH < list_off[l + 1] ? r0 + IVF_CH : list_off[l + 1];
+    const int64_t r1 = r0 + IVF_CH < lend ? r0 + IVF_CH : lend;
     const int len = (int)(r1 - r0);
     const float *q = Q + (pair / nprobe) * (int64_t)d;
     for (int j = threadIdx.x; j < d; j += 256) qv[j] = q[j];
@@ -1116,7 +1117,7 @@ ivf_scan_slot_bigk(const float *__restrict__ Q, int d, const float *__restrict__
 }
 
 void launch_ivf_scan_bigk(const float *Q, int d, int metric, const float *codes, const int64_t *list_off,
-                          const int64_t *probes, int64_t npairs, int nprobe, const int *slot_off, int64_t nslots,
+                          const int *list_len, const int64_t *probes, int64_t npairs, int nprobe, const int *slot_off, int64_t nslots,
                           int k, float *pd, int *pi, hipStream_t st) {
     if (nslots <= 0) return;
     HIPANN_REQUIRE(nslots < (int64_t)0x7fffffff, "too many slots");
@@ -1124,10 +1125,10 @@ void launch_ivf_scan_bigk(const float *Q, int d, int metric, const float *codes,
     HIPANN_REQUIRE(smem <= 64 * 1024, "dimension too large for the k > 64 IVF path");
     dim3 grid((unsigned)nslots), block(256);
     if (metric == kIP)
-        hipLaunchKernelGGL(ivf_scan_slot_bigk<true>, grid, block, smem, st, Q, d, codes, list_off, probes, npairs,
+        hipLaunchKernelGGL(ivf_scan_slot_bigk<true>, grid, block, smem, st, Q, d, codes, list_off, list_len, probes, npairs,
                            nprobe, slot_off, k, pd, pi);
     else
-        hipLaunchKernelGGL(ivf_scan_slot_bigk<false>, grid, block, smem, st, Q, d, codes, list_off, probes, npairs,
+        hipLaunchKernelGGL(ivf_scan_slot_bigk<false>, grid, block, smem, st, Q, d, codes, list_off, list_len, probes, npairs,
                            nprobe, slot_off, k, pd, pi);
     HIPANN_CHECK(hipGetLastError());
 }
@@ -1209,8 +1210,9 @@ bool ivf_dot_supported(const float *Q, int d, const float *codes) {
 }
 
 void launch_ivf_scan(const float *Q, const float *qn, int d, int metric, int form, const float *codes,
-                     const float *xn, const int64_t *list_off, const int *cnt, const int *bucket_off,
-                     const int *item_off, const int *bucket, const int *slot_off, int nlist, int nprobe, int64_t nq,
+                     const float *xn, const int64_t *list_off, const int *list_len, const int *cnt,
+                     const int *bucket_off, const int *item_off, const int *bucket, const int *slot_off, int nlist,
+                     int nprobe, int64_t nq,
                      int k, int64_t max_items, unsigned *qbound, float *pd, int *pi, hipStream_t st) {
     if (max_items <= 0) return;
     HIPANN_REQUIRE(max_items < (int64_t)0x7fffffff, "too many IVF work items");
@@ -1220,7 +1222,7 @@ void launch_ivf_scan(const float *Q, const float *qn, int d, int metric, int for
         HIPANN_REQUIRE(metric == kIP || (qn && xn), "decomposed L2 scan needs query and row norms");
         dim3 grid((unsigned)max_items), block(DT_THREADS);
         const size_t smem = ivf_scan_dot_smem_bytes();
-#define HIPANN_DOT_ARGS Q, qn, d, codes, xn, list_off, cnt, bucket_off, item_off, bucket, slot_off, nlist, nprobe, k, pd, pi
+#define HIPANN_DOT_ARGS Q, qn, d, codes, xn, list_off, list_len, cnt, bucket_off, item_off, bucket, slot_off, nlist, nprobe, k, pd, pi
         if (metric == kIP) hipLaunchKernelGGL((ivf_scan_dot<true>), grid, block, smem, st, HIPANN_DOT_ARGS);
         else hipLaunchKernelGGL((ivf_scan_dot<false>), grid, block, smem, st, HIPANN_DOT_ARGS);
 #undef HIPANN_DOT_ARGS
@@ -1228,7 +1230,7 @@ void launch_ivf_scan(const float *Q, const float *qn, int d, int metric, int for
         const bool vec4 = ivf_dot_supported(Q, d, codes);
         dim3 grid((unsigned)max_items), block(IVF_THREADS);
         const size_t smem = ivf_scan_smem_bytes();
-#define HIPANN_IVF_ARGS Q, d, codes, list_off, cnt, bucket_off, item_off, bucket, slot_off, nlist, nprobe, nq, k, pd, pi
+#define HIPANN_IVF_ARGS Q, d, codes, list_off, list_len, cnt, bucket_off, item_off, bucket, slot_off, nlist, nprobe, nq, k, pd, pi
         if (vec4) {
             if (metric == kIP) hipLaunchKernelGGL((ivf_scan_topk<true, true>), grid, block, smem, st, HIPANN_IVF_ARGS);
             else hipLaunchKernelGGL((ivf_scan_topk<true, false>), grid, block, smem, st, HIPANN_IVF_ARGS);
@@ -2228,6 +2230,27 @@ __global__ void __launch_bounds__(256) ivf_gather_queries(const float *__restric
     out[t] = Q[(int64_t)idx[j] * d + e];
 }
 
+// An append's staged rows (grouped by list, contiguous) into their physical CSR rows: codes, labels and (L2) the row
+// norms computed over the staged block by launch_row_norms — the same bits a rebuild would compute.  dst < 0: a row
+// of a list this shard does not own.
+__global__ void __launch_bounds__(256) ivf_append_scatter(const float *__restrict__ rows, const float *__restrict__ norms,
+                                                         const int64_t *__restrict__ ids_in,
+                                                         const int64_t *__restrict__ dst, int64_t n, int d,
+                                                         float *__restrict__ codes, int64_t *__restrict__ ids,
+                                                         float *__restrict__ xnorm) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= n * d) return;
+    const int64_t j = t / d;
+    const int e = (int)(t - j * d);
+    const int64_t r = dst[j];
+    if (r < 0) return;
+    codes[r * d + e] = rows[t];
+    if (e == 0) {
+        ids[r] = ids_in[j];
+        if (xnorm) xnorm[r] = norms[j];
+    }
+}
+
 __global__ void __launch_bounds__(256) ivf_scatter_results(const float *__restrict__ Df, const int64_t *__restrict__ If,
                                                            const int *__restrict__ idx, int nf, int kout,
                                                            float *__restrict__ D, int64_t *__restrict__ I) {
@@ -2291,6 +2314,15 @@ void launch_ivf_max_norm(const float *xn, int64_t n, unsigned *out, hipStream_t 
     if (n <= 0) return;
     const unsigned blocks = (unsigned)std::min<int64_t>(1024, ceil_div(n, 256));
     hipLaunchKernelGGL(ivf_max_norm, dim3(blocks), dim3(256), 0, st, xn, n, out);
+    HIPANN_CHECK(hipGetLastError());
+}
+
+void launch_ivf_append_scatter(const float *rows, const float *norms, const int64_t *ids_in, const int64_t *dst,
+                               int64_t n, int d, float *codes, int64_t *ids, float *xnorm, hipStream_t st) {
+    if (n <= 0) return;
+    HIPANN_REQUIRE(ceil_div(n * d, 256) < (int64_t)0x7fffffff, "append block too large");
+    hipLaunchKernelGGL(ivf_append_scatter, dim3((unsigned)ceil_div(n * d, 256)), dim3(256), 0, st, rows, norms, ids_in,
+                       dst, n, d, codes, ids, xnorm);
     HIPANN_CHECK(hipGetLastError());
 }
 

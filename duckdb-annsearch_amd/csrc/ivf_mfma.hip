@@ -390,7 +390,7 @@ template <bool IP>
 __global__ void __launch_bounds__(MF_THREADS, MF_WAVES / 4)
 ivf_scan_mfma(const float *__restrict__ Q, const float *__restrict__ qnorm, int d, const float *__restrict__ codes_t,
               const int64_t *__restrict__ tpass_off,
-              const float *__restrict__ xn, const int64_t *__restrict__ list_off, const int *__restrict__ cnt,
+              const float *__restrict__ xn, const int64_t *__restrict__ list_off, const int *__restrict__ list_len, const int *__restrict__ cnt,
               const int *__restrict__ bucket_off, const int *__restrict__ item_off, const int *__restrict__ bucket,
               const int *__restrict__ slot_off, int nlist, int nprobe, int group, int k, int sub,
               unsigned *__restrict__ qbound, float *__restrict__ part_d, int *__restrict__ part_i) {
@@ -404,7 +404,7 @@ ivf_scan_mfma(const float *__restrict__ Q, const float *__restrict__ qnorm, int 
         if (item_off[mid] <= item) lo = mid; else hi = mid - 1;
     }
     const int l = lo;
-    const int64_t lr0 = list_off[l], lr1 = list_off[l + 1];
+    const int64_t lr0 = list_off[l], lr1 = lr0 + list_len[l];
     const int c = cnt[l];
     const int ng = (c + group - 1) / group;
     const int rem = item - item_off[l];
@@ -459,15 +459,16 @@ ivf_scan_mfma(const float *__restrict__ Q, const float *__restrict__ qnorm, int 
 // search over the pass offsets); element (pass, step s, tile r, lane (g, m), e) = row 32·p + 16r + m
 // of the list, dim 16s + 4g + e, zero past the list's end and past d.
 __global__ void __launch_bounds__(256)
-ivf_tile_codes(const float *__restrict__ codes, const int64_t *__restrict__ list_off,
-               const int64_t *__restrict__ tpass_off, int nlist, int d, int nsub, float *__restrict__ dst) {
-    const int64_t pass = blockIdx.x;
+ivf_tile_codes(const float *__restrict__ codes, const int64_t *__restrict__ list_off, const int *__restrict__ list_len,
+               const int64_t *__restrict__ tpass_off, int nlist, int d, int nsub, float *__restrict__ dst,
+               const int64_t *__restrict__ pass_ids) {
+    const int64_t pass = pass_ids ? pass_ids[blockIdx.x] : (int64_t)blockIdx.x;
     int lo = 0, hi = nlist - 1;
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
         if (tpass_off[mid] <= pass) lo = mid; else hi = mid - 1;
     }
-    const int64_t len = list_off[lo + 1] - list_off[lo];
+    const int64_t len = list_len[lo];
     const int64_t prow = (pass - tpass_off[lo]) * MF_PASS;
     const int nf4 = nsub * MF_RT * 64;
     for (int t = threadIdx.x; t < nf4; t += 256) {
@@ -483,13 +484,13 @@ ivf_tile_codes(const float *__restrict__ codes, const int64_t *__restrict__ list
 
 int64_t ivf_mfma_pass_floats(int d) { return (int64_t)mf_nsub(d) * MF_RT * 256; }
 
-void launch_ivf_tile_codes(const float *codes, const int64_t *list_off, const int64_t *tpass_off, int nlist,
-                           int64_t total_pass, int d, float *dst, hipStream_t st) {
+void launch_ivf_tile_codes(const float *codes, const int64_t *list_off, const int *list_len, const int64_t *tpass_off,
+                           int nlist, int64_t total_pass, int d, float *dst, hipStream_t st, const int64_t *pass_ids) {
     if (total_pass <= 0) return;
     HIPANN_REQUIRE(d % 4 == 0 && (uintptr_t)codes % 16 == 0, "tiled codes need d % 4 == 0 and 16-B aligned rows");
     HIPANN_REQUIRE(total_pass < (int64_t)0x7fffffff, "too many passes");
-    hipLaunchKernelGGL(ivf_tile_codes, dim3((unsigned)total_pass), dim3(256), 0, st, codes, list_off, tpass_off, nlist,
-                       d, mf_nsub(d), dst);
+    hipLaunchKernelGGL(ivf_tile_codes, dim3((unsigned)total_pass), dim3(256), 0, st, codes, list_off, list_len,
+                       tpass_off, nlist, d, mf_nsub(d), dst, pass_ids);
     HIPANN_CHECK(hipGetLastError());
 }
 
@@ -502,9 +503,9 @@ int ivf_mfma_group(int d) { return mf_group(d); }
 
 void launch_ivf_scan_mfma(const float *Q, const float *qn, int d, int metric, const float *codes_t,
                           const int64_t *tpass_off, const float *xn,
-                          const int64_t *list_off, const int *cnt, const int *bucket_off, const int *item_off,
-                          const int *bucket, const int *slot_off, int nlist, int nprobe, int k, int64_t max_items,
-                          unsigned *qbound, float *pd, int *pi, hipStream_t st, int sub) {
+                          const int64_t *list_off, const int *list_len, const int *cnt, const int *bucket_off,
+                          const int *item_off, const int *bucket, const int *slot_off, int nlist, int nprobe, int k,
+                          int64_t max_items, unsigned *qbound, float *pd, int *pi, hipStream_t st, int sub) {
     if (max_items <= 0) return;
     HIPANN_REQUIRE(max_items < (int64_t)0x7fffffff, "too many IVF work items");
     HIPANN_REQUIRE(ivf_mfma_supported(Q, d, codes_t, k), "MFMA IVF scan needs d % 4 == 0, 16-B aligned data, k <= 16");
@@ -513,7 +514,7 @@ void launch_ivf_scan_mfma(const float *Q, const float *qn, int d, int metric, co
     const size_t merge = (size_t)(MF_WAVES / 2) * MF_QTMAX * 4 * 64 * sizeof(float2);  // end-of-item scratch
     const size_t smem = std::max((size_t)group * mf_stride(d) * 4, merge);
     dim3 grid((unsigned)max_items), block(MF_THREADS);
-#define MF_LAUNCH_ARGS Q, qn, d, codes_t, tpass_off, xn, list_off, cnt, bucket_off, item_off, bucket, slot_off, nlist, nprobe, group, k, \
+#define MF_LAUNCH_ARGS Q, qn, d, codes_t, tpass_off, xn, list_off, list_len, cnt, bucket_off, item_off, bucket, slot_off, nlist, nprobe, group, k, \
                        sub, qbound, pd, pi
     if (metric == kIP) hipLaunchKernelGGL((ivf_scan_mfma<true>), grid, block, smem, st, MF_LAUNCH_ARGS);
     else hipLaunchKernelGGL((ivf_scan_mfma<false>), grid, block, smem, st, MF_LAUNCH_ARGS);
@@ -775,7 +776,7 @@ template <bool IP, int NP, int NH>
 __global__ void __launch_bounds__(MF_THREADS, MF_WAVES / 4)
 ivf_scan_mfma_bf(const uint4 *__restrict__ qsplit, const float *__restrict__ qnorm, int d, const float *__restrict__ codes_t,
                  const int64_t *__restrict__ tpass_off, const float *__restrict__ xn,
-                 const int64_t *__restrict__ list_off, const int *__restrict__ cnt, const int *__restrict__ bucket_off,
+                 const int64_t *__restrict__ list_off, const int *__restrict__ list_len, const int *__restrict__ cnt, const int *__restrict__ bucket_off,
                  const int *__restrict__ item_off, const int *__restrict__ bucket, const int *__restrict__ slot_off,
                  int nlist, int nprobe, int group, int k, int sub, unsigned *__restrict__ qbound, float *__restrict__ part_d,
                  int *__restrict__ part_i) {
@@ -789,7 +790,7 @@ ivf_scan_mfma_bf(const uint4 *__restrict__ qsplit, const float *__restrict__ qno
         if (item_off[mid] <= item) lo = mid; else hi = mid - 1;
     }
     const int l = lo;
-    const int64_t lr0 = list_off[l], lr1 = list_off[l + 1];
+    const int64_t lr0 = list_off[l], lr1 = lr0 + list_len[l];
     const int c = cnt[l];
     const int ng = (c + group - 1) / group;
     const int rem = item - item_off[l];
@@ -864,7 +865,7 @@ bool ivf_mfma_bf_supported(const float *Q, int d, const float *codes, int k, int
 
 void launch_ivf_scan_mfma_bf(int np, const float *Q, int64_t nq, void *qsplit, const float *qn, int d, int metric,
                              const float *codes_t, const int64_t *tpass_off, const float *xn, const int64_t *list_off,
-                             const int *cnt, const int *bucket_off, const int *item_off, const int *bucket,
+                             const int *list_len, const int *cnt, const int *bucket_off, const int *item_off, const int *bucket,
                              const int *slot_off, int nlist, int nprobe, int k, int64_t max_items, unsigned *qbound,
                              float *pd, int *pi, hipStream_t st, int sub) {
     if (max_items <= 0 || nq <= 0) return;
@@ -883,7 +884,7 @@ void launch_ivf_scan_mfma_bf(int np, const float *Q, int64_t nq, void *qsplit, c
     const size_t merge = (size_t)(MF_WAVES / 2) * MF_QTMAX * 4 * 64 * sizeof(float2);
     const size_t smem = std::max((size_t)group * mb_stride(d, np, nh) * 4, merge);
     dim3 grid((unsigned)max_items), block(MF_THREADS);
-#define MB_LAUNCH_ARGS qs, qn, d, codes_t, tpass_off, xn, list_off, cnt, bucket_off, item_off, bucket, slot_off, nlist, nprobe, \
+#define MB_LAUNCH_ARGS qs, qn, d, codes_t, tpass_off, xn, list_off, list_len, cnt, bucket_off, item_off, bucket, slot_off, nlist, nprobe, \
                        group, k, sub, qbound, pd, pi
 #define MB_LAUNCH(NP_, NH_)                                                                                         \
     do {                                                                                                            \
@@ -961,15 +962,16 @@ __global__ void __launch_bounds__(256) ivf_max_abs(const float *__restrict__ x, 
 // one block per 32-row pass (list found by binary search over the pass offsets); zero past the
 // list's end and past d
 __global__ void __launch_bounds__(256)
-ivf_tile_half(const float *__restrict__ codes, const int64_t *__restrict__ list_off, const int64_t *__restrict__ tpass_off,
-              int nlist, int d, int nsup, float scale, uint4 *__restrict__ dst) {
-    const int64_t pass = blockIdx.x;
+ivf_tile_half(const float *__restrict__ codes, const int64_t *__restrict__ list_off, const int *__restrict__ list_len,
+              const int64_t *__restrict__ tpass_off, int nlist, int d, int nsup, float scale, uint4 *__restrict__ dst,
+              const int64_t *__restrict__ pass_ids) {
+    const int64_t pass = pass_ids ? pass_ids[blockIdx.x] : (int64_t)blockIdx.x;
     int lo = 0, hi = nlist - 1;
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
         if (tpass_off[mid] <= pass) lo = mid; else hi = mid - 1;
     }
-    const int64_t len = list_off[lo + 1] - list_off[lo];
+    const int64_t len = list_len[lo];
     const int64_t prow = (pass - tpass_off[lo]) * MF_PASS;
     const int nt = nsup * MF_RT * 64;
     for (int t = threadIdx.x; t < nt; t += 256) {
@@ -1256,7 +1258,7 @@ template <bool IP>
 __global__ void __launch_bounds__(MF_THREADS, MF_WAVES / 4)
 ivf_scan_mfma_h(const uint4 *__restrict__ qsplit, const float *__restrict__ qnorm, const float *__restrict__ its, int d,
                 const uint4 *__restrict__ codes_h, const int64_t *__restrict__ tpass_off, const float *__restrict__ xn,
-                const int64_t *__restrict__ list_off, const int *__restrict__ cnt, const int *__restrict__ bucket_off,
+                const int64_t *__restrict__ list_off, const int *__restrict__ list_len, const int *__restrict__ cnt, const int *__restrict__ bucket_off,
                 const int *__restrict__ item_off, const int *__restrict__ bucket, const int *__restrict__ slot_off,
                 int nlist, int nprobe, int group, int k, int sub, unsigned *__restrict__ qbound, float *__restrict__ part_d,
                 int *__restrict__ part_i) {
@@ -1270,7 +1272,7 @@ ivf_scan_mfma_h(const uint4 *__restrict__ qsplit, const float *__restrict__ qnor
         if (item_off[mid] <= item) lo = mid; else hi = mid - 1;
     }
     const int l = lo;
-    const int64_t lr0 = list_off[l], lr1 = list_off[l + 1];
+    const int64_t lr0 = list_off[l], lr1 = lr0 + list_len[l];
     const int c = cnt[l];
     const int ng = (c + group - 1) / group;
     const int rem = item - item_off[l];
@@ -1329,12 +1331,13 @@ void launch_ivf_max_abs(const float *x, int64_t cnt, unsigned *out, hipStream_t 
     HIPANN_CHECK(hipGetLastError());
 }
 
-void launch_ivf_tile_half(const float *codes, const int64_t *list_off, const int64_t *tpass_off, int nlist,
-                          int64_t total_pass, int d, float scale, void *dst, hipStream_t st) {
+void launch_ivf_tile_half(const float *codes, const int64_t *list_off, const int *list_len, const int64_t *tpass_off,
+                          int nlist, int64_t total_pass, int d, float scale, void *dst, hipStream_t st,
+                          const int64_t *pass_ids) {
     if (total_pass <= 0) return;
     HIPANN_REQUIRE(total_pass < (int64_t)0x7fffffff, "too many passes");
-    hipLaunchKernelGGL(ivf_tile_half, dim3((unsigned)total_pass), dim3(256), 0, st, codes, list_off, tpass_off, nlist, d,
-                       mh_nsup(d), scale, static_cast<uint4 *>(dst));
+    hipLaunchKernelGGL(ivf_tile_half, dim3((unsigned)total_pass), dim3(256), 0, st, codes, list_off, list_len, tpass_off,
+                       nlist, d, mh_nsup(d), scale, static_cast<uint4 *>(dst), pass_ids);
     HIPANN_CHECK(hipGetLastError());
 }
 
@@ -1358,9 +1361,10 @@ void launch_ivf_split_queries_h(const float *Q, int64_t nq, int d, int es, void 
 
 void launch_ivf_scan_mfma_h(const float *Q, int64_t nq, void *qsplit, float *its, float *qres, int es, const float *qn,
                             int d, int metric, const void *codes_h, const int64_t *tpass_off, const float *xn,
-                            const int64_t *list_off, const int *cnt, const int *bucket_off, const int *item_off,
-                            const int *bucket, const int *slot_off, int nlist, int nprobe, int k, int64_t max_items,
-                            unsigned *qbound, float *pd, int *pi, hipStream_t st, bool split_done, int sub) {
+                            const int64_t *list_off, const int *list_len, const int *cnt, const int *bucket_off,
+                            const int *item_off, const int *bucket, const int *slot_off, int nlist, int nprobe, int k,
+                            int64_t max_items, unsigned *qbound, float *pd, int *pi, hipStream_t st, bool split_done,
+                            int sub) {
     if (max_items <= 0 || nq <= 0) return;
     HIPANN_REQUIRE(max_items < (int64_t)0x7fffffff, "too many IVF work items");
     HIPANN_REQUIRE(qsplit && its && qres && codes_h, "fp16 IVF scan: missing buffers");
@@ -1376,7 +1380,7 @@ void launch_ivf_scan_mfma_h(const float *Q, int64_t nq, void *qsplit, float *its
     const size_t smem = std::max((size_t)group * mh_stride(d) * 4, merge);
     dim3 grid((unsigned)max_items), block(MF_THREADS);
     const uint4 *ch = static_cast<const uint4 *>(codes_h);
-#define MH_LAUNCH_ARGS qs, qn, its, d, ch, tpass_off, xn, list_off, cnt, bucket_off, item_off, bucket, slot_off, nlist, nprobe, \
+#define MH_LAUNCH_ARGS qs, qn, its, d, ch, tpass_off, xn, list_off, list_len, cnt, bucket_off, item_off, bucket, slot_off, nlist, nprobe, \
                        group, k, sub, qbound, pd, pi
     if (metric == kIP) hipLaunchKernelGGL((ivf_scan_mfma_h<true>), grid, block, smem, st, MH_LAUNCH_ARGS);
     else hipLaunchKernelGGL((ivf_scan_mfma_h<false>), grid, block, smem, st, MH_LAUNCH_ARGS);

@@ -205,6 +205,7 @@ struct FlatShard {
     float i8_rxmax = 0.f;
     StreamFence fence;       // cross-stream ordering of this shard's calls
     HostBuf h_nflag;         // the launch phase's flag count, read back with the results (flat_shard_finish)
+    DevBuf app_stat;         // an append's new-row maxima (‖x‖², int8 residual, bf16 residual²)
     hipEvent_t done = nullptr;  // multi-device search: the shard's launch phase has drained (shard 0's stream waits)
 };
 
@@ -269,12 +270,16 @@ struct FlatIndex : IndexBase {
 // (size-balanced); every shard keeps all centroids and an empty range for lists it does not own.
 struct IvfShard {
     int device = 0;
-    int64_t n = 0;                 // rows held by this shard
+    // Physical CSR rows: list l occupies rows [h_off[l], h_off[l+1]) of codes / ids / xnorm, its first h_len[l] live
+    // (the rest is append slack, zero-filled; the kernels read list_len, never the gap).  n = h_off[nlist] (the
+    // physical row count every whole-table kernel walks), live = Σ h_len (ntotal).
+    int64_t n = 0;
+    int64_t live = 0;
     const float *centroids = nullptr;
     const float *codes = nullptr;  // n × d fp32, list-contiguous
     const int64_t *ids = nullptr;  // n labels
     DevBuf centroids_buf, codes_buf, ids_buf;  // owned storage (empty when borrowed)
-    DevBuf list_off;               // int64 nlist+1 (shard-local row offsets)
+    DevBuf list_off;               // int64 nlist+1 (shard-local physical row offsets: list starts)
     DevBuf list_len;               // int nlist (0 = empty or not owned)
     DevBuf xnorm;                  // ‖x‖² per row (L2; the decomposed scan form)
     std::unique_ptr<FlatIndex> quant;  // coarse quantizer over `centroids` (borrowed)
@@ -298,6 +303,8 @@ struct IvfShard {
     // MFMA scan copy of the codes, built at the first search that uses it: per list, 32-row passes of
     // [16-dim step][2 row tiles][64 lanes][float4] (ivf_mfma.hip), zero-padded rows / dims
     std::vector<int64_t> h_off;    // host copy of list_off
+    std::vector<int64_t> h_len;    // host copy of list_len (live rows per list)
+    bool owns_codes = false;       // codes / ids / xnorm in codes_buf / ids_buf (else borrowed: the first add copies)
     DevBuf codes_t, tpass_off;     // tiled codes; int64 nlist+1 pass offsets
     // kFormHalfExact: tiled fp16 image of x·2^half_es (same passes as codes_t), its largest row
     // residual ‖x − x̂·2^−half_es‖ and the batch's query terms / 1/(t·s) / split residuals.
@@ -305,6 +312,9 @@ struct IvfShard {
     int half_state = 0, half_es = 0;
     float half_rxmax = 0.f;
     DevBuf codes_h, hsplit, hits, hres;
+    // an append's staging (hipann_ivf_add): the new rows grouped by list, labels, physical destinations, norms,
+    // the tiled passes they touch, and the new rows' maxima (‖x‖², |x|, fp16 residual²)
+    DevBuf app_rows, app_ids, app_dst, app_norm, app_pass, app_stat;
     int max_nch = 1;  // largest list's row-chunk count
     StreamFence fence;  // cross-stream ordering of this shard's calls (its coarse quantizer's scratch included)
 };
@@ -323,12 +333,14 @@ struct IvfIndex : IndexBase {
     ~IvfIndex() override;
     int64_t ntotal() const override {
         int64_t t = 0;
-        for (auto &s : shards) t += s->n;
+        for (auto &s : shards) t += s->live;
         return t;
     }
     int64_t memory_bytes() const override {
         int64_t b = 0;
-        for (auto &s : shards) b += s->n * ((int64_t)d * 4 + 8 + (metric == kL2 ? 4 : 0)) + (int64_t)nlist * d * 4;
+        for (auto &s : shards)
+            b += s->n * ((int64_t)d * 4 + 8 + (metric == kL2 ? 4 : 0)) + (int64_t)nlist * d * 4 +
+                 (int64_t)s->codes_h.bytes + (int64_t)s->codes_t.bytes;
         return b;
     }
 };
@@ -394,12 +406,14 @@ int64_t ivf_half_pass_bytes(int d);
 int64_t ivf_half_qsplit_bytes(int64_t nq, int d);
 bool ivf_mfma_h_supported(int d, int k);
 void launch_ivf_max_abs(const float *x, int64_t cnt, unsigned *out, hipStream_t st);
-void launch_ivf_tile_half(const float *codes, const int64_t *list_off, const int64_t *tpass_off, int nlist,
-                          int64_t total_pass, int d, float scale, void *dst, hipStream_t st);
+// (pass_ids != nullptr: only the listed global passes, one block each — the passes an append touched)
+void launch_ivf_tile_half(const float *codes, const int64_t *list_off, const int *list_len, const int64_t *tpass_off,
+                          int nlist, int64_t total_pass, int d, float scale, void *dst, hipStream_t st,
+                          const int64_t *pass_ids = nullptr);
 void launch_ivf_half_residual(const float *codes, int64_t n, int d, float scale, unsigned *out, hipStream_t st);
 void launch_ivf_scan_mfma_h(const float *Q, int64_t nq, void *qsplit, float *its, float *qres, int es, const float *qn,
                             int d, int metric, const void *codes_h, const int64_t *tpass_off, const float *xn,
-                            const int64_t *list_off, const int *cnt, const int *bucket_off, const int *item_off,
+                            const int64_t *list_off, const int *list_len, const int *cnt, const int *bucket_off, const int *item_off,
                             const int *bucket, const int *slot_off, int nlist, int nprobe, int k, int64_t max_items,
                             unsigned *qbound, float *pd, int *pi, hipStream_t st, bool split_done = false,
                             int sub = 0);
@@ -448,33 +462,37 @@ void launch_flat_bf16_seed(const float *pd, int nsplit, int64_t nq, int k, float
 bool flat_bf16_k64_supported(int nk, int k);
 void launch_ivf_max_norm(const float *xn, int64_t n, unsigned *out, hipStream_t st);
 void launch_ivf_gather_queries(const float *Q, const int *idx, int nf, int d, float *out, hipStream_t st);
+void launch_ivf_append_scatter(const float *rows, const float *norms, const int64_t *ids_in, const int64_t *dst,
+                               int64_t n, int d, float *codes, int64_t *ids, float *xnorm, hipStream_t st);
 void launch_ivf_scatter_results(const float *Df, const int64_t *If, const int *idx, int nf, int kout, float *D,
                                 int64_t *I, hipStream_t st);
 void launch_ivf_scan_mfma_bf(int np, const float *Q, int64_t nq, void *qsplit, const float *qn, int d, int metric,
                              const float *codes_t, const int64_t *tpass_off, const float *xn, const int64_t *list_off,
-                             const int *cnt, const int *bucket_off, const int *item_off, const int *bucket,
+                             const int *list_len, const int *cnt, const int *bucket_off, const int *item_off, const int *bucket,
                              const int *slot_off, int nlist, int nprobe, int k, int64_t max_items, unsigned *qbound,
                              float *pd, int *pi, hipStream_t st, int sub = 0);
 int ivf_group_size(int form, int d);  // queries per work item of the form's scan kernel
 int ivf_chunk_rows();
 bool ivf_plan_query_major();
 void launch_ivf_scan_bigk(const float *Q, int d, int metric, const float *codes, const int64_t *list_off,
-                          const int64_t *probes, int64_t npairs, int nprobe, const int *slot_off, int64_t nslots,
+                          const int *list_len, const int64_t *probes, int64_t npairs, int nprobe, const int *slot_off, int64_t nslots,
                           int k, float *pd, int *pi, hipStream_t st);
 size_t ivf_scan_smem_bytes();
 bool ivf_dot_supported(const float *Q, int d, const float *codes);
 void launch_ivf_scan(const float *Q, const float *qn, int d, int metric, int form, const float *codes,
-                     const float *xn, const int64_t *list_off, const int *cnt, const int *bucket_off,
-                     const int *item_off, const int *bucket, const int *slot_off, int nlist, int nprobe, int64_t nq,
+                     const float *xn, const int64_t *list_off, const int *list_len, const int *cnt,
+                     const int *bucket_off, const int *item_off, const int *bucket, const int *slot_off, int nlist,
+                     int nprobe, int64_t nq,
                      int k, int64_t max_items, unsigned *qbound, float *pd, int *pi, hipStream_t st);
 bool ivf_mfma_supported(const float *Q, int d, const float *codes, int k);
 int ivf_mfma_group(int d);
 int64_t ivf_mfma_pass_floats(int d);  // floats per 32-row pass of the tiled codes
-void launch_ivf_tile_codes(const float *codes, const int64_t *list_off, const int64_t *tpass_off, int nlist,
-                           int64_t total_pass, int d, float *dst, hipStream_t st);
+void launch_ivf_tile_codes(const float *codes, const int64_t *list_off, const int *list_len, const int64_t *tpass_off,
+                           int nlist, int64_t total_pass, int d, float *dst, hipStream_t st,
+                           const int64_t *pass_ids = nullptr);
 void launch_ivf_scan_mfma(const float *Q, const float *qn, int d, int metric, const float *codes_t,
                           const int64_t *tpass_off, const float *xn,
-                          const int64_t *list_off, const int *cnt, const int *bucket_off, const int *item_off,
+                          const int64_t *list_off, const int *list_len, const int *cnt, const int *bucket_off, const int *item_off,
                           const int *bucket, const int *slot_off, int nlist, int nprobe, int k, int64_t max_items,
                           unsigned *qbound, float *pd, int *pi, hipStream_t st, int sub = 0);
 void launch_ivf_merge(const float *pd, const int *pi, const int64_t *ids, int64_t nrows, const int *slot_off, int nprobe, int64_t nq,

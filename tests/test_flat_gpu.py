@@ -539,3 +539,44 @@ def test_flat_multi_shard_flagged_queries_finish(gpu, oracle, nq):
     Do, Io = oracle.flat_search(xb, xq, 10)
     check_topk_parity(xb, xq, D, I, Do, Io)
     ix.close()
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+def test_flat_successive_appends_incremental(gpu, oracle, metric):
+    """20 successive 2048-row appends after the int8 and bf16 images exist.  Each append tiles
+    only the tiles holding new rows and updates max ‖x‖² and the residual maxima as running maxima; the batched int8
+    passes (nq 256), the bf16 passes (form 4) and the small-batch int8 scan (nq 4) on the grown table follow the
+    oracle's parity rule, and the last chunk (rows ×3) is found by the queries placed next to it."""
+    rng = np.random.default_rng(61 + metric)
+    d, n0, step, steps = 64, 600_000, 2048, 20
+    xb = rng.uniform(-1, 1, (n0 + step * steps, d)).astype(np.float32)
+    xb[-step:] *= np.float32(3.0)
+    xq = rng.uniform(-1, 1, (256, d)).astype(np.float32)
+    xq[:16] = xb[-16:] + np.float32(1e-3)
+    ix = gpu.HipIndexFlat(d, metric, xb[:n0])
+    ix.search(xq, 10)          # int8 image (bounded passes)
+    ix.form = ix.FORM_BF16_EXACT
+    ix.search(xq, 10)          # bf16 image
+    ix.form = ix.FORM_I8_EXACT
+    ix.search(xq[:4], 10)      # small-batch int8 scan
+    for a in range(steps):
+        lo = n0 + a * step
+        ix.add(xb[lo:lo + step])
+    assert ix.ntotal == len(xb)
+    Do, Io = oracle.flat_search(xb, xq[:64], 10, metric)
+    for form, nq in ((ix.FORM_I8_EXACT, 256), (ix.FORM_BF16_EXACT, 256), (ix.FORM_I8_EXACT, 4)):
+        ix.form = form
+        D, I = ix.search(xq[:nq], 10)
+        assert ix.last_search_path()["form"] == form, (form, nq)
+        m = min(nq, 64)
+        check_topk_parity(xb, xq[:m], D[:m], I[:m], Do[:m], Io[:m], metric)
+        # a table built from scratch over the same rows: same answers, and the same bound terms (the running maxima
+        # equal the rebuild's), so the same number of flagged re-runs
+        fresh = gpu.HipIndexFlat(d, metric, xb)
+        fresh.form = form
+        before = ix.rerank_fallbacks()
+        D2, I2 = fresh.search(xq[:nq], 10)
+        D, I = ix.search(xq[:nq], 10)
+        assert np.array_equal(I, I2) and np.array_equal(D, D2), (form, nq)
+        assert ix.rerank_fallbacks() - before == fresh.rerank_fallbacks(), (form, nq)
+        fresh.close()

@@ -458,3 +458,63 @@ def test_ivf_exact_ties_scan_order_unflagged(gpu, oracle, form, metric):
     assert np.allclose(D[v], Do[v], rtol=2e-6, atol=1e-6)
     # most queries were resolved by the rerank itself (the fallback covers the rest)
     assert ix.rerank_fallbacks() - before < len(xq) // 2
+
+
+@pytest.mark.parametrize("form", [6, 5, 0])
+def test_ivf_successive_appends_incremental(gpu, oracle, form):
+    """20 successive 2048-row appends (DuckDB's Append chunks, faiss_index.cpp:469) after the
+    scan's tiled image exists.  Each append writes its rows into their lists' slack (ivf_relayout grows only the
+    lists that overflow), re-tiles the touched passes and updates the bound maxima; the grown index exports the
+    oracle's CSR lists and its ids equal the oracle's IndexIVFFlat::search on every query (exact forms: exactly)."""
+    rng = np.random.default_rng(5 + form)
+    d, nlist, n0, step, steps = 64, 64, 40_000, 2048, 20
+    xb = rng.standard_normal((n0 + step * steps, d), dtype=np.float32)
+    xb[-step:] *= np.float32(3.0)  # the last chunk raises max|x|, max‖x‖² and the residual maxima
+    xq = rng.standard_normal((256, d), dtype=np.float32)
+    xq[:16] = xb[-16:] + np.float32(1e-3)  # queries whose answers are the grown rows
+    cen = np.ascontiguousarray(xb[:nlist * 50:50])
+    off0, ids0, codes0 = build_ivf_lists(xb[:n0], cen)
+    ix = gpu.HipIndexIVFFlat(cen, off0, ids0, codes0, 8)
+    ix.form = form
+    ix.search(xq, 10)  # builds the tiled image the appends must maintain
+    for a in range(steps):
+        lo = n0 + a * step
+        ix.add(xb[lo:lo + step])
+    assert ix.ntotal == len(xb)
+    off, ids, codes = build_ivf_lists(xb, cen)
+    ex = ix.export()
+    assert np.array_equal(ex["list_offsets"], off) and np.array_equal(ex["ids"], ids)
+    assert np.array_equal(ex["codes"], codes)
+    D, I = ix.search(xq, 10)
+    assert ix.last_search_path()["form"] == form
+    Do, Io, Po = oracle.ivf_search(cen, off, ids, codes, xq, 10, 8)
+    assert np.array_equal(ix.last_probes(256), Po)
+    st = check_topk_parity(xb, xq, D, I, Do, Io)
+    if form in (5, 6):
+        assert st["exact_fraction"] == 1.0, st
+    # a fresh index over the exported lists answers identically (the slack layout is invisible)
+    fresh = gpu.HipIndexIVFFlat(cen, off, ids, codes, 8)
+    fresh.form = form
+    D2, I2 = fresh.search(xq, 10)
+    assert np.array_equal(I, I2) and np.array_equal(D, D2)
+
+
+def test_ivf_append_rescales_fp16_image(gpu, oracle):
+    """An append whose rows leave the fp16 image's scale (max|x| past 2^e of the build) drops the image; the next
+    search rebuilds it at the new scale and stays exact against the oracle."""
+    rng = np.random.default_rng(12)
+    d, nlist = 32, 16
+    xb = rng.uniform(-1, 1, (6000, d)).astype(np.float32)
+    xb[5000:] *= np.float32(40.0)
+    xq = np.concatenate([xb[5000:5020] + np.float32(1e-2), rng.uniform(-1, 1, (20, d)).astype(np.float32)])
+    cen = np.ascontiguousarray(xb[:nlist * 100:100])
+    off0, ids0, codes0 = build_ivf_lists(xb[:5000], cen)
+    ix = gpu.HipIndexIVFFlat(cen, off0, ids0, codes0, 4)
+    ix.search(xq, 10)
+    ix.add(xb[5000:])
+    D, I = ix.search(xq, 10)
+    assert ix.last_search_path()["form"] == ix.FORM_HALF_EXACT
+    off, ids, codes = build_ivf_lists(xb, cen)
+    Do, Io, _ = oracle.ivf_search(cen, off, ids, codes, xq, 10, 4)
+    st = check_topk_parity(xb, xq, D, I, Do, Io)
+    assert st["exact_fraction"] == 1.0, st
