@@ -170,6 +170,9 @@ def compact_line(full):
         line["with_h2d_d2h_qps"] = full["with_h2d_d2h"].get("queries_per_s")
     if isinstance(full.get("latency"), dict):
         line["nq1_ms"] = (full["latency"].get("nq1") or {}).get("ms_per_call")
+    if isinstance(full.get("append"), dict):
+        a = full["append"]
+        line["append2048"] = {k: a.get(k) for k in ("append_ms", "append_plus_search_ms", "vs_search_step")}
     fb = (full.get("ivf") or {}).get("rerank_fallbacks_total", full.get("rerank_fallbacks_total"))
     if fb is not None:
         line["rerank_fallbacks"] = fb
@@ -845,7 +848,53 @@ def ivf_config(args, torch, dist, hipann, rank, world, dev, steps, warmup, suite
         par = out["cpu_baseline"].pop("parity", None)
         if par is not None:
             out["parity_vs_cpu_path"] = par
+    if suite_extras:  # last: it grows the index
+        out["append"] = ivf_append_line(torch, index, xq, k, d, r_dim, eta, el * 1e3 / steps)
     return out, index
+
+
+def ivf_append_line(torch, index, xq, k, d, r_dim, eta, base_ms, rows=2048, reps=10):
+    """The extension's INSERT path on the GPU copy (faiss_index.cpp:469: Append per data chunk of <= 2048 rows):
+    hipann_ivf_add of a 2048-row chunk (host rows: coarse assignment on the GPU, rows into their lists' slack, touched
+    fp16-image passes re-tiled) followed by the next 1024-query search, timed together, against the plain search step
+    (within 1.3x).  The first append moves the borrowed lists into owned storage with slack (timed apart)."""
+    dev = xq.device
+    gc = torch.Generator(device=dev)
+    gc.manual_seed(7)
+    basis = lowrank_basis(torch, r_dim, d, gc)
+    new = torch.empty(((reps + 1) * rows, d), device=dev, dtype=torch.float32)
+    gen_lowrank_rows(torch, new, 0, basis, eta, 777)
+    new_h = new.cpu().numpy()
+    del new
+    nq = xq.shape[0]
+    stream = torch.cuda.current_stream().cuda_stream
+    D = torch.empty((nq, k), device=dev, dtype=torch.float32)
+    I = torch.empty((nq, k), device=dev, dtype=torch.int64)
+    search = lambda: index.search_device(nq, xq.data_ptr(), k, D.data_ptr(), I.data_ptr(), stream)  # noqa: E731
+    n_before = index.ntotal
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    index.add(new_h[:rows])
+    first_ms = (time.perf_counter() - t0) * 1e3
+    search()
+    torch.cuda.synchronize()
+    t_add = t_pair = 0.0
+    for r in range(1, reps + 1):
+        t0 = time.perf_counter()
+        index.add(new_h[r * rows:(r + 1) * rows])
+        t1 = time.perf_counter()
+        search()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        t_add += t1 - t0
+        t_pair += t2 - t0
+    pair_ms = t_pair * 1e3 / reps
+    return {"workload": f"hipann_ivf_add of {rows} host rows + the next {nq}-query search, {reps} times",
+            "append_ms": round(t_add * 1e3 / reps, 3), "append_plus_search_ms": round(pair_ms, 3),
+            "search_step_ms": round(base_ms, 3), "vs_search_step": round(pair_ms / base_ms, 3) if base_ms > 0 else None,
+            "first_append_ms": round(first_ms, 1),
+            "first_append_note": "moves the borrowed CSR into owned lists with slack (once)",
+            "ntotal": [n_before, index.ntotal], "rows_per_s": round(rows * reps / t_add, 1) if t_add > 0 else None}
 
 
 def ivf_latency(torch, index, xq, k, d, metric=0):

@@ -9,6 +9,8 @@
 #include "ivf.hpp"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <exception>
@@ -468,18 +470,20 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
 }
 
 
-// Grow a shard's CSR so that list l can take add[l] more rows.  A list that overflows gets capacity
-// max(need, cap + max(cap / 4, 64)) rows — geometric growth (O(1) amortised copies per appended row, the doubling
-// of MetalIndexFlat::add, MetalIndexFlat.mm:255-269, at ×1.25: a 10M × 768 table at ×2 would hold 61 GB of codes);
+// Grow a shard's CSR so that list l can take add[l] more rows: every list gets capacity max(cap, need + max(need / 4,
+// 64)) rows — geometric growth (O(1) amortised copies per appended row, the doubling of MetalIndexFlat::add,
+// MetalIndexFlat.mm:255-269, at ×1.25: a 10M × 768 table at ×2 would hold 61 GB of codes);
 // borrowed storage is copied into owned buffers.  Live rows, labels, norms and the tiled images' passes move list by
 // list (device-to-device, in order); the slack rows are zero (whole-table maxima read them).
 static void ivf_relayout(IvfIndex &ix, IvfShard &sh, const std::vector<int64_t> &add) {
     const int nlist = ix.nlist, d = ix.d;
     hipStream_t st = sh.stream;
+    // every list leaves with room for a quarter more than it will hold (≥ 64 rows): DuckDB's 2048-row chunks touch
+    // most lists of a 1024-list index, so growing only the overflowing ones would relayout on nearly every append
     std::vector<int64_t> off(nlist + 1, 0);
     for (int l = 0; l < nlist; ++l) {
         const int64_t cap = sh.h_off[l + 1] - sh.h_off[l], need = sh.h_len[l] + add[l];
-        const int64_t ncap = need > cap ? std::max(need, cap + std::max<int64_t>(cap / 4, 64)) : cap;
+        const int64_t ncap = std::max(cap, need + std::max<int64_t>(need / 4, 64));
         off[l + 1] = off[l] + ncap;
     }
     const int64_t N = off[nlist];
@@ -550,58 +554,63 @@ static void ivf_relayout(IvfIndex &ix, IvfShard &sh, const std::vector<int64_t> 
 }
 
 // IndexIVF::add_with_ids (FAISS 1.13.2, external): rows are assigned to their nearest centroid by the
-// coarse quantizer (quantizer->assign, k = 1, in blocks of 65536 rows — so the Flat nq < 20 direct-form
-// rule applies per block) and appended to their lists in insertion order; labels are `ids` or
-// ntotal + i.  On the GPU copy this replaces the reference's invalidate-on-append (faiss_index.cpp:469): the new
+// coarse quantizer (quantizer->assign, k = 1) and appended to their lists in insertion order; labels are `ids`
+// or ntotal + i.  On the GPU copy this replaces the reference's invalidate-on-append (faiss_index.cpp:469): the new
 // rows go into their lists' slack in HBM (ivf_relayout grows the lists that overflow, amortised), with their norms,
 // the touched passes of the tiled images and running maxima — the cost of an append is the appended rows, not the
 // table.
+static void ivf_add_block(IvfIndex &ix, int64_t n, const float *xb, const int64_t *ids, int64_t base);
+
 static void ivf_add_rows(IvfIndex &ix, int64_t n, const float *xb, const int64_t *ids) {
-    const int d = ix.d, nlist = ix.nlist;
+    // every shard's pending searches (possibly on other streams) finish before its buffers change
+    std::vector<std::unique_ptr<FenceScope>> fences;
+    for (auto &shp : ix.shards) fences.push_back(std::make_unique<FenceScope>(shp->fence, shp->stream, shp->device));
+    // FAISS assigns in blocks of 65536 rows (so the Flat nq < 20 direct-form rule applies per block); each block's
+    // rows follow the previous block's in their lists (insertion order)
+    const int64_t bs = 65536;
+    for (int64_t r0 = 0; r0 < n; r0 += bs) {
+        const int64_t m = std::min(bs, n - r0);
+        ivf_add_block(ix, m, xb + r0 * (int64_t)ix.d, ids ? ids + r0 : nullptr, ix.ntotal());
+    }
+}
+
+// One block of an add: rows to the device once, coarse assignment on the GPU (shard 0's quantizer; every shard holds
+// all centroids), one readback of the assignment; then per shard owning a list with new rows: grow the lists that
+// overflow (ivf_relayout, amortised), scatter each row straight into its list's slack (one kernel: codes, label,
+// norm), update the live lengths, re-tile the tiled images' touched passes, and fold the new rows into the bounds'
+// running maxima (no rescan of the table).  Two host synchronisations per block.
+static void ivf_add_block(IvfIndex &ix, int64_t n, const float *xb, const int64_t *ids, int64_t base) {
+    const int d = ix.d, nlist = ix.nlist, metric = ix.metric;
     IvfShard &s0 = *ix.shards[0];
     DeviceGuard g0(s0.device);
     hipStream_t st = s0.stream;
-    // every shard's pending searches (possibly on other streams) finish before its buffers are rebuilt
-    std::vector<std::unique_ptr<FenceScope>> fences;
-    for (auto &shp : ix.shards) fences.push_back(std::make_unique<FenceScope>(shp->fence, shp->stream, shp->device));
-    const int64_t base = ix.ntotal();
-    // 1. assignment on the GPU (shard 0's quantizer; every shard holds all centroids)
-    std::vector<int64_t> assign((size_t)n);
-    const int64_t bs = 65536;
-    DevBuf rows, dd, ii;
-    rows.ensure(sizeof(float) * (size_t)std::min(n, bs) * d, s0.device);
-    dd.ensure(sizeof(float) * (size_t)std::min(n, bs), s0.device);
-    ii.ensure(sizeof(int64_t) * (size_t)std::min(n, bs), s0.device);
-    for (int64_t r0 = 0; r0 < n; r0 += bs) {
-        const int64_t m = std::min(bs, n - r0);
-        HIPANN_CHECK(hipMemcpyAsync(rows.p, xb + r0 * d, sizeof(float) * (size_t)m * d, hipMemcpyHostToDevice, st));
-        flat_shard_search(*s0.quant, *s0.quant->shards[0], m, rows.get<float>(), 1, 1, dd.get<float>(),
-                          ii.get<int64_t>(), st);
-        HIPANN_CHECK(hipMemcpyAsync(assign.data() + r0, ii.p, sizeof(int64_t) * (size_t)m, hipMemcpyDeviceToHost, st));
+    // HIPANN_APPEND_PROF=1 (tuning): host-side phase times of each block on stderr
+    static const bool prof = std::getenv("HIPANN_APPEND_PROF") != nullptr;
+    using clk = std::chrono::steady_clock;
+    const auto t_0 = clk::now();
+    auto us = [&](clk::time_point a) { return std::chrono::duration<double, std::micro>(clk::now() - a).count(); };
+    s0.app_rows.ensure(sizeof(float) * (size_t)n * d, s0.device);
+    s0.app_norm.ensure(sizeof(float) * (size_t)n, s0.device);
+    s0.app_assign.ensure(sizeof(int64_t) * (size_t)n, s0.device);
+    HIPANN_CHECK(hipMemcpyAsync(s0.app_rows.p, xb, sizeof(float) * (size_t)n * d, hipMemcpyHostToDevice, st));
+    double t_h2d = 0.0;
+    if (prof) {
+        HIPANN_CHECK(hipStreamSynchronize(st));
+        t_h2d = us(t_0);
     }
+    flat_shard_search(*s0.quant, *s0.quant->shards[0], n, s0.app_rows.get<float>(), 1, 1, s0.app_norm.get<float>(),
+                      s0.app_assign.get<int64_t>(), st);
+    s0.app_hassign.ensure(sizeof(int64_t) * (size_t)n);
+    const int64_t *assign = s0.app_hassign.get<int64_t>();
+    HIPANN_CHECK(hipMemcpyAsync(s0.app_hassign.p, s0.app_assign.p, sizeof(int64_t) * (size_t)n, hipMemcpyDeviceToHost,
+                                st));
     HIPANN_CHECK(hipStreamSynchronize(st));
-    rows.release();
-    // 2. per list, the new rows in insertion order (stable counting sort)
-    std::vector<int64_t> cnt(nlist + 1, 0);
+    const double t_assign = prof ? us(t_0) : 0.0;
+    std::vector<int64_t> cnt(nlist, 0);
     for (int64_t i = 0; i < n; ++i) {
         HIPANN_REQUIRE(assign[i] >= 0 && assign[i] < nlist, "coarse assignment out of range");
-        ++cnt[assign[i] + 1];
+        ++cnt[assign[i]];
     }
-    std::vector<int64_t> noff(nlist + 1, 0);  // offsets of the new rows, grouped by list
-    for (int l = 0; l < nlist; ++l) noff[l + 1] = noff[l] + cnt[l + 1];
-    std::vector<int64_t> perm((size_t)n), cur(noff.begin(), noff.end() - 1);
-    for (int64_t i = 0; i < n; ++i) perm[cur[assign[i]]++] = i;
-    HostBuf hc, hi;
-    hc.ensure(sizeof(float) * (size_t)n * d);
-    hi.ensure(sizeof(int64_t) * (size_t)n);
-    for (int64_t j = 0; j < n; ++j) {
-        std::memcpy(hc.get<float>() + j * d, xb + perm[j] * d, sizeof(float) * d);
-        hi.get<int64_t>()[j] = ids ? ids[perm[j]] : base + perm[j];
-    }
-    // 3. every shard that owns a list with new rows: grow the lists that overflow (ivf_relayout, amortised), then
-    //    the new rows straight into their lists' slack (one scatter kernel), their norms and the tiled images' touched
-    //    passes; the bounds' maxima follow the new rows (running maxima, no rescan of the table)
-    const int metric = ix.metric;
     for (size_t s = 0; s < ix.shards.size(); ++s) {
         IvfShard &sh = *ix.shards[s];
         std::vector<int64_t> add(nlist, 0);
@@ -609,71 +618,78 @@ static void ivf_add_rows(IvfIndex &ix, int64_t n, const float *xb, const int64_t
         bool grow = !sh.owns_codes;
         for (int l = 0; l < nlist; ++l) {
             if (ix.owner[l] != (int)s) continue;
-            add[l] = cnt[l + 1];
+            add[l] = cnt[l];
             add_s += add[l];
             if (sh.h_len[l] + add[l] > sh.h_off[l + 1] - sh.h_off[l]) grow = true;
         }
         if (!add_s) continue;
         DeviceGuard g(sh.device);
         hipStream_t ss = sh.stream;
+        if (&sh != &s0) {  // the block's rows on this shard's device too
+            sh.app_rows.ensure(sizeof(float) * (size_t)n * d, sh.device);
+            sh.app_norm.ensure(sizeof(float) * (size_t)n, sh.device);
+            HIPANN_CHECK(hipMemcpyAsync(sh.app_rows.p, xb, sizeof(float) * (size_t)n * d, hipMemcpyHostToDevice, ss));
+        }
         if (grow) ivf_relayout(ix, sh, add);
-        // physical destination of every staged row (−1: a list of another shard), and the tiled passes it touches
-        HostBuf hd, hp;
-        hd.ensure(sizeof(int64_t) * (size_t)n);
-        int64_t *dst = hd.get<int64_t>();
-        std::fill(dst, dst + n, (int64_t)-1);
-        std::vector<int64_t> tp(nlist + 1, 0);
-        for (int l = 0; l < nlist; ++l) tp[l + 1] = tp[l] + ceil_div(sh.h_off[l + 1] - sh.h_off[l], 32);
-        std::vector<int64_t> passes;
+        // one pinned upload: [physical destination per row (−1: another shard's list) | label per row | the tiled
+        // passes the rows touch | the new live length per list (int)]
         std::vector<int64_t> len = sh.h_len;
+        std::vector<int64_t> tp0(nlist);
+        int64_t np = 0, tp = 0;
         for (int l = 0; l < nlist; ++l) {
-            if (!add[l]) continue;
-            for (int64_t j = noff[l]; j < noff[l + 1]; ++j) dst[j] = sh.h_off[l] + len[l] + (j - noff[l]);
-            for (int64_t p = len[l] / 32; p < ceil_div(len[l] + add[l], 32); ++p) passes.push_back(tp[l] + p);
-            len[l] += add[l];
+            tp0[l] = tp;
+            tp += ceil_div(sh.h_off[l + 1] - sh.h_off[l], 32);
+            if (add[l]) np += ceil_div(len[l] + add[l], 32) - len[l] / 32;
         }
+        const size_t up_bytes = sizeof(int64_t) * (size_t)(2 * n + np) + sizeof(int) * (size_t)nlist;
+        sh.app_hup.ensure(up_bytes);
+        int64_t *dst = sh.app_hup.get<int64_t>(), *lab = dst + n, *passes = lab + n;
+        int *newlen = reinterpret_cast<int *>(passes + np);
+        for (int64_t i = 0; i < n; ++i) {
+            const int64_t l = assign[i];
+            dst[i] = ix.owner[l] == (int)s ? sh.h_off[l] + len[l]++ : -1;
+            lab[i] = ids ? ids[i] : base + i;
+        }
+        int64_t pi = 0, maxlen = 0, live = 0;
+        for (int l = 0; l < nlist; ++l) {
+            for (int64_t p = sh.h_len[l] / 32; add[l] && p < ceil_div(len[l], 32); ++p) passes[pi++] = tp0[l] + p;
+            HIPANN_REQUIRE(len[l] < (int64_t)0x7fffffff, "inverted list longer than 2^31-1 rows");
+            newlen[l] = (int)len[l];
+            maxlen = std::max(maxlen, len[l]);
+            live += len[l];
+        }
+        sh.app_up.ensure(up_bytes, sh.device);
+        HIPANN_CHECK(hipMemcpyAsync(sh.app_up.p, sh.app_hup.p, up_bytes, hipMemcpyHostToDevice, ss));
+        const int64_t *ddst = sh.app_up.get<int64_t>(), *dlab = ddst + n, *dpass = dlab + n;
+        const int *dlen = reinterpret_cast<const int *>(dpass + np);
         const bool img_h = sh.half_state > 0 && sh.codes_h.p, img_t = sh.codes_t.p != nullptr;
-        sh.app_rows.ensure(sizeof(float) * (size_t)n * d, sh.device);
-        sh.app_ids.ensure(sizeof(int64_t) * (size_t)n, sh.device);
-        sh.app_dst.ensure(sizeof(int64_t) * (size_t)n, sh.device);
-        sh.app_norm.ensure(sizeof(float) * (size_t)n, sh.device);
-        sh.app_stat.ensure(sizeof(unsigned) * 4, sh.device);
-        HIPANN_CHECK(hipMemcpyAsync(sh.app_rows.p, hc.p, sizeof(float) * (size_t)n * d, hipMemcpyHostToDevice, ss));
-        HIPANN_CHECK(hipMemcpyAsync(sh.app_ids.p, hi.p, sizeof(int64_t) * (size_t)n, hipMemcpyHostToDevice, ss));
-        HIPANN_CHECK(hipMemcpyAsync(sh.app_dst.p, dst, sizeof(int64_t) * (size_t)n, hipMemcpyHostToDevice, ss));
-        // norms over the staged block with the table's own kernel (the bits a rebuild computes), then the scatter
-        launch_row_norms(sh.app_rows.get<float>(), n, d, sh.app_norm.get<float>(), ss);
-        launch_ivf_append_scatter(sh.app_rows.get<float>(), sh.app_norm.get<float>(), sh.app_ids.get<int64_t>(),
-                                  sh.app_dst.get<int64_t>(), n, d, sh.codes_buf.get<float>(), sh.ids_buf.get<int64_t>(),
-                                  metric == kL2 ? sh.xnorm.get<float>() : nullptr, ss);
-        // the new rows' maxima (over the whole staged block: a superset of this shard's rows, so only conservative)
-        unsigned *stat = sh.app_stat.get<unsigned>();
-        launch_ivf_max_norm(sh.app_norm.get<float>(), n, stat, ss);
         const float hscale = std::ldexp(1.f, sh.half_es);
-        if (img_h) {
-            launch_ivf_max_abs(sh.app_rows.get<float>(), n * (int64_t)d, stat + 1, ss);
-            launch_ivf_half_residual(sh.app_rows.get<float>(), n, d, hscale, stat + 2, ss);
-        }
-        // live lengths, then the touched passes of the tiled images re-tiled from the (grown) lists
-        upload_list_meta(sh, sh.h_off, len, nlist);
-        if ((img_h || img_t) && !passes.empty()) {
-            hp.ensure(sizeof(int64_t) * passes.size());
-            std::memcpy(hp.p, passes.data(), sizeof(int64_t) * passes.size());
-            sh.app_pass.ensure(sizeof(int64_t) * passes.size(), sh.device);
-            HIPANN_CHECK(hipMemcpyAsync(sh.app_pass.p, hp.p, sizeof(int64_t) * passes.size(), hipMemcpyHostToDevice, ss));
-            const int64_t npass = (int64_t)passes.size();
-            if (img_h)
-                launch_ivf_tile_half(sh.codes, sh.list_off.get<int64_t>(), sh.list_len.get<int>(),
-                                     sh.tpass_off.get<int64_t>(), nlist, npass, d, hscale, sh.codes_h.p, ss,
-                                     sh.app_pass.get<int64_t>());
-            if (img_t)
-                launch_ivf_tile_codes(sh.codes, sh.list_off.get<int64_t>(), sh.list_len.get<int>(),
-                                      sh.tpass_off.get<int64_t>(), nlist, npass, d, sh.codes_t.get<float>(), ss,
-                                      sh.app_pass.get<int64_t>());
-        }
-        unsigned hs[4] = {0u, 0u, 0u, 0u};
-        HIPANN_CHECK(hipMemcpyAsync(hs, stat, sizeof(hs), hipMemcpyDeviceToHost, ss));
-        HIPANN_CHECK(hipStreamSynchronize(ss));
+        // norms over the block with the table's own kernel (the bits a rebuild computes), then one kernel: rows,
+        // labels and norms into their CSR rows, the new lengths, this shard's new-row maxima
+        sh.app_stat.ensure(sizeof(unsigned) * 4, sh.device);
+        unsigned *stat = sh.app_stat.get<unsigned>();
+        launch_row_norms(sh.app_rows.get<float>(), n, d, sh.app_norm.get<float>(), ss);
+        launch_ivf_append_rows(sh.app_rows.get<float>(), sh.app_norm.get<float>(), ddst, dlab, n, d,
+                               sh.codes_buf.get<float>(), sh.ids_buf.get<int64_t>(),
+                               metric == kL2 ? sh.xnorm.get<float>() : nullptr, dlen, sh.list_len.get<int>(), nlist,
+                               img_h ? hscale : 0.f, stat, ss);
+        sh.h_len = len;
+        sh.live = live;
+        sh.max_nch = (int)std::max<int64_t>(1, ceil_div(maxlen, ivf_chunk_rows()));
+        // the touched passes of the tiled images, re-tiled from the grown lists
+        if (np > 0 && img_h)
+            launch_ivf_tile_half(sh.codes, sh.list_off.get<int64_t>(), sh.list_len.get<int>(), sh.tpass_off.get<int64_t>(),
+                                 nlist, np, d, hscale, sh.codes_h.p, ss, dpass);
+        if (np > 0 && img_t)
+            launch_ivf_tile_codes(sh.codes, sh.list_off.get<int64_t>(), sh.list_len.get<int>(),
+                                  sh.tpass_off.get<int64_t>(), nlist, np, d, sh.codes_t.get<float>(), ss, dpass);
+        sh.app_hstat.ensure(sizeof(unsigned) * 4);
+        unsigned *hs = sh.app_hstat.get<unsigned>();
+        HIPANN_CHECK(hipMemcpyAsync(hs, stat, sizeof(unsigned) * 4, hipMemcpyDeviceToHost, ss));
+        HIPANN_CHECK(hipStreamSynchronize(ss));  // (the pinned staging above is reused by the next block)
+        if (prof)
+            std::fprintf(stderr, "hipann append: n %lld h2d %.0f us, assign %.0f us, shard %zu done %.0f us (grow %d, %lld passes)\n",
+                         (long long)n, t_h2d, t_assign, s, us(t_0), (int)grow, (long long)np);
         float v;
         std::memcpy(&v, &hs[0], sizeof(v));
         if (sh.xmax2 >= 0.f) sh.xmax2 = std::max(sh.xmax2, v);  // max ‖x‖² (the rerank bound's row term)

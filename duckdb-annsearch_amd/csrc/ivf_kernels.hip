@@ -2230,27 +2230,6 @@ __global__ void __launch_bounds__(256) ivf_gather_queries(const float *__restric
     out[t] = Q[(int64_t)idx[j] * d + e];
 }
 
-// An append's staged rows (grouped by list, contiguous) into their physical CSR rows: codes, labels and (L2) the row
-// norms computed over the staged block by launch_row_norms — the same bits a rebuild would compute.  dst < 0: a row
-// of a list this shard does not own.
-__global__ void __launch_bounds__(256) ivf_append_scatter(const float *__restrict__ rows, const float *__restrict__ norms,
-                                                         const int64_t *__restrict__ ids_in,
-                                                         const int64_t *__restrict__ dst, int64_t n, int d,
-                                                         float *__restrict__ codes, int64_t *__restrict__ ids,
-                                                         float *__restrict__ xnorm) {
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (t >= n * d) return;
-    const int64_t j = t / d;
-    const int e = (int)(t - j * d);
-    const int64_t r = dst[j];
-    if (r < 0) return;
-    codes[r * d + e] = rows[t];
-    if (e == 0) {
-        ids[r] = ids_in[j];
-        if (xnorm) xnorm[r] = norms[j];
-    }
-}
-
 __global__ void __launch_bounds__(256) ivf_scatter_results(const float *__restrict__ Df, const int64_t *__restrict__ If,
                                                            const int *__restrict__ idx, int nf, int kout,
                                                            float *__restrict__ D, int64_t *__restrict__ I) {
@@ -2314,15 +2293,6 @@ void launch_ivf_max_norm(const float *xn, int64_t n, unsigned *out, hipStream_t 
     if (n <= 0) return;
     const unsigned blocks = (unsigned)std::min<int64_t>(1024, ceil_div(n, 256));
     hipLaunchKernelGGL(ivf_max_norm, dim3(blocks), dim3(256), 0, st, xn, n, out);
-    HIPANN_CHECK(hipGetLastError());
-}
-
-void launch_ivf_append_scatter(const float *rows, const float *norms, const int64_t *ids_in, const int64_t *dst,
-                               int64_t n, int d, float *codes, int64_t *ids, float *xnorm, hipStream_t st) {
-    if (n <= 0) return;
-    HIPANN_REQUIRE(ceil_div(n * d, 256) < (int64_t)0x7fffffff, "append block too large");
-    hipLaunchKernelGGL(ivf_append_scatter, dim3((unsigned)ceil_div(n * d, 256)), dim3(256), 0, st, rows, norms, ids_in,
-                       dst, n, d, codes, ids, xnorm);
     HIPANN_CHECK(hipGetLastError());
 }
 

@@ -1013,6 +1013,52 @@ __global__ void __launch_bounds__(256) ivf_half_residual(const float *__restrict
     if (lane == 0 && row < n) atomicMax(out, __float_as_uint(s));
 }
 
+// An append block (hipann_ivf_add), one wave per row j of the block: the row into its physical CSR row dst[j] (codes,
+// label, and the L2 norm launch_row_norms computed over the block — the bits a rebuild computes); rows of another
+// shard's lists (dst < 0) are skipped.  The same pass folds this shard's new rows into the running maxima: stat[0] =
+// max ‖x‖² (float bits), stat[1] = max |x| (magnitude bits: NaN above +inf, as ivf_max_abs), stat[2] = max fp16
+// residual² ‖x − x̂/s‖² at the image's scale s (hscale > 0; ivf_half_residual's summation order).  Threads below
+// nlist also publish the new live lengths (read by the re-tile that follows and by the next search).
+__global__ void __launch_bounds__(256)
+ivf_append_rows(const float *__restrict__ rows, const float *__restrict__ norms, const int64_t *__restrict__ dst,
+                const int64_t *__restrict__ ids_in, int64_t n, int d, float *__restrict__ codes,
+                int64_t *__restrict__ ids, float *__restrict__ xnorm, const int *__restrict__ newlen,
+                int *__restrict__ list_len, int nlist, float hscale, unsigned *__restrict__ stat) {
+    const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (gid < nlist) list_len[gid] = newlen[gid];
+    const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (j >= n) return;
+    const int64_t r = dst[j];
+    if (r < 0) return;
+    const float *src = rows + j * (int64_t)d;
+    float *out = codes + r * (int64_t)d;
+    const float inv = hscale > 0.f ? 1.f / hscale : 0.f;
+    unsigned mabs = 0;
+    float res = 0.f;
+    for (int e = lane; e < d; e += 64) {
+        const float x = src[e];
+        out[e] = x;
+        mabs = max(mabs, __float_as_uint(x) & 0x7fffffffu);
+        if (hscale > 0.f) {
+            const float q = x - mh_val(mh_half_bits(x * hscale)) * inv;
+            res = fmaf(q, q, res);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mabs = max(mabs, (unsigned)__shfl_xor((int)mabs, o));
+        res += __shfl_xor(res, o);
+    }
+    if (lane == 0) {
+        ids[r] = ids_in[j];
+        if (xnorm) xnorm[r] = norms[j];
+        atomicMax(stat + 0, __float_as_uint(norms[j]));
+        atomicMax(stat + 1, mabs);
+        if (hscale > 0.f) atomicMax(stat + 2, __float_as_uint(res));
+    }
+}
+
 // The batch's queries, one wave per query: t = 2^(14 − e_q), q·t split into two fp16 terms in the
 // image's k-slot order, qsplit [query][term][super-step][g][8 halves]; its[q] = 1/(t·s) (a power of
 // two) and qres[q] = ‖q − (h + l)/t‖ (×1.0001 for the fp32 sum).  A query whose scale leaves the safe
@@ -1347,6 +1393,17 @@ void launch_ivf_half_residual(const float *codes, int64_t n, int d, float scale,
     HIPANN_REQUIRE(ceil_div(n, 4) < (int64_t)0x7fffffff, "too many rows");
     hipLaunchKernelGGL(ivf_half_residual, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, st, codes, n, d, scale,
                        1.f / scale, out);
+    HIPANN_CHECK(hipGetLastError());
+}
+
+void launch_ivf_append_rows(const float *rows, const float *norms, const int64_t *dst, const int64_t *ids_in, int64_t n,
+                            int d, float *codes, int64_t *ids, float *xnorm, const int *newlen, int *list_len, int nlist,
+                            float hscale, unsigned *stat, hipStream_t st) {
+    const int64_t blocks = std::max(ceil_div(n, (int64_t)4), ceil_div((int64_t)nlist, (int64_t)256));
+    HIPANN_REQUIRE(blocks < (int64_t)0x7fffffff, "append block too large");
+    HIPANN_CHECK(hipMemsetAsync(stat, 0, sizeof(unsigned) * 4, st));
+    hipLaunchKernelGGL(ivf_append_rows, dim3((unsigned)blocks), dim3(256), 0, st, rows, norms, dst, ids_in, n, d, codes,
+                       ids, xnorm, newlen, list_len, nlist, hscale, stat);
     HIPANN_CHECK(hipGetLastError());
 }
 

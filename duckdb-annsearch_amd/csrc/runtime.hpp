@@ -314,7 +314,10 @@ struct IvfShard {
     DevBuf codes_h, hsplit, hits, hres;
     // an append's staging (hipann_ivf_add): the new rows grouped by list, labels, physical destinations, norms,
     // the tiled passes they touch, and the new rows' maxima (‖x‖², |x|, fp16 residual²)
-    DevBuf app_rows, app_ids, app_dst, app_norm, app_pass, app_stat;
+    DevBuf app_rows, app_norm, app_assign, app_up, app_stat;
+    // pinned: the assignment on its way down, [destinations | labels | touched passes | live lengths] on their way
+    // up (one copy), the maxima on their way down
+    HostBuf app_hassign, app_hup, app_hstat;
     int max_nch = 1;  // largest list's row-chunk count
     StreamFence fence;  // cross-stream ordering of this shard's calls (its coarse quantizer's scratch included)
 };
@@ -462,8 +465,11 @@ void launch_flat_bf16_seed(const float *pd, int nsplit, int64_t nq, int k, float
 bool flat_bf16_k64_supported(int nk, int k);
 void launch_ivf_max_norm(const float *xn, int64_t n, unsigned *out, hipStream_t st);
 void launch_ivf_gather_queries(const float *Q, const int *idx, int nf, int d, float *out, hipStream_t st);
-void launch_ivf_append_scatter(const float *rows, const float *norms, const int64_t *ids_in, const int64_t *dst,
-                               int64_t n, int d, float *codes, int64_t *ids, float *xnorm, hipStream_t st);
+// hipann_ivf_add: an append block's rows into their CSR rows + the new live lengths + the new rows' maxima
+// (stat[0] max ‖x‖², stat[1] max |x| bits, stat[2] max fp16 residual² at hscale; hscale 0: no residual)
+void launch_ivf_append_rows(const float *rows, const float *norms, const int64_t *dst, const int64_t *ids_in, int64_t n,
+                            int d, float *codes, int64_t *ids, float *xnorm, const int *newlen, int *list_len, int nlist,
+                            float hscale, unsigned *stat, hipStream_t st);
 void launch_ivf_scatter_results(const float *Df, const int64_t *If, const int *idx, int nf, int kout, float *D,
                                 int64_t *I, hipStream_t st);
 void launch_ivf_scan_mfma_bf(int np, const float *Q, int64_t nq, void *qsplit, const float *qn, int d, int metric,

@@ -580,3 +580,29 @@ def test_flat_successive_appends_incremental(gpu, oracle, metric):
         assert np.array_equal(I, I2) and np.array_equal(D, D2), (form, nq)
         assert ix.rerank_fallbacks() - before == fresh.rerank_fallbacks(), (form, nq)
         fresh.close()
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+@pytest.mark.parametrize("nq", [4, 256])
+def test_flat_nan_and_overflow_queries_pad_like_faiss(gpu, oracle, metric, nq):
+    """a NaN query (and, for L2, a query whose distances overflow to +inf) is never admitted by FAISS's
+    heap (strict C::cmp(top, dis) with NaN / inf against ±FLT_MAX), so the CPU path returns all −1 labels for it.
+    The small-batch int8 scan (nq 4) and the int8 bounded passes (nq 256) return the same −1 labels, and the other
+    queries of the batch keep the oracle's parity."""
+    rng = np.random.default_rng(3 + metric)
+    n, d = 600_000, 64
+    xb = rng.uniform(-1, 1, (n, d)).astype(np.float32)
+    xq = rng.uniform(-1, 1, (nq, d)).astype(np.float32)
+    xq[1, 5] = np.nan
+    bad = [1]
+    if metric == 0:
+        xq[2] = np.float32(3e38)  # ‖q − x‖² overflows to +inf for every row
+        bad.append(2)
+    ix = gpu.HipIndexFlat(d, metric, xb)
+    D, I = ix.search(xq, 10)
+    Do, Io = oracle.flat_search(xb, xq, 10, metric)
+    for b in bad:
+        assert (Io[b] == -1).all()
+        assert (I[b] == -1).all(), (b, I[b])
+    good = np.array([i for i in range(nq) if i not in bad])
+    check_topk_parity(xb, xq[good], D[good], I[good], Do[good], Io[good], metric)

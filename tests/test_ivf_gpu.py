@@ -518,3 +518,28 @@ def test_ivf_append_rescales_fp16_image(gpu, oracle):
     Do, Io, _ = oracle.ivf_search(cen, off, ids, codes, xq, 10, 4)
     st = check_topk_parity(xb, xq, D, I, Do, Io)
     assert st["exact_fraction"] == 1.0, st
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+def test_ivf_nan_and_overflow_queries_pad_like_faiss(gpu, oracle, metric):
+    """on the IVF exact form a NaN query (and, for L2, an overflowing one) returns FAISS's all −1 labels
+    (its heap admits neither NaN nor +inf); the batch's other queries keep exact parity."""
+    rng = np.random.default_rng(8 + metric)
+    xb = rng.standard_normal((20_000, 48), dtype=np.float32)
+    xq = rng.standard_normal((40, 48), dtype=np.float32)
+    xq[3, 0] = np.nan
+    bad = [3]
+    if metric == 0:
+        xq[4] = np.float32(3e38)
+        bad.append(4)
+    cen = np.ascontiguousarray(xb[::500][:40])
+    off, ids, codes = build_ivf_lists(xb, cen, metric)
+    ix = gpu.HipIndexIVFFlat(cen, off, ids, codes, 6, metric=metric)
+    D, I = ix.search(xq, 10)
+    Do, Io, _ = oracle.ivf_search(cen, off, ids, codes, xq, 10, 6, metric)
+    for b in bad:
+        assert (Io[b] == -1).all()
+        assert (I[b] == -1).all(), (b, I[b])
+    good = np.array([i for i in range(len(xq)) if i not in bad])
+    st = check_topk_parity(xb, xq[good], D[good], I[good], Do[good], Io[good], metric)
+    assert st["exact_fraction"] == 1.0, st
