@@ -750,14 +750,29 @@ def ivf_config(args, torch, dist, hipann, rank, world, dev, steps, warmup, suite
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t_setup
 
+    # list sharding at N > 1: the coarse step partitioned over the ranks (each computes its slice's probe lists, one
+    # all-gather of the lists) instead of N identical coarse passes; HIPANN_IVF_COARSE=replicated for A/B
+    from sharded import PartitionedProbes, coarse_partition_ok
+    pp = None
+    if world > 1 and os.environ.get("HIPANN_IVF_SHARD", "lists") == "lists" and \
+            os.environ.get("HIPANN_IVF_COARSE", "partitioned") == "partitioned" and coarse_partition_ok(nq, world):
+        pp = PartitionedProbes(lambda qs, out: index.coarse_device(qs.shape[0], qs.data_ptr(), out.data_ptr(), stream),
+                               nq, min(nprobe, nlist), dev)
+
     def local(q, D, I):
-        index.search_device(q.shape[0], q.data_ptr(), k, D.data_ptr(), I.data_ptr(), stream)
+        if pp is not None:
+            P = pp.probes(q)
+            index.search_probes_device(q.shape[0], q.data_ptr(), P.data_ptr(), k, D.data_ptr(), I.data_ptr(), stream)
+        else:
+            index.search_device(q.shape[0], q.data_ptr(), k, D.data_ptr(), I.data_ptr(), stream)
 
     sharded = ShardedSearch(local, merge_packed_device_torch(hipann, metric), nq, k, dev)
     step = lambda: sharded.search(xq)  # noqa: E731
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
+    info["coarse_step"] = "partitioned over ranks + one all-gather of the probe lists" if pp is not None else \
+        "replicated on every rank" if world > 1 else "single GPU"
     probes = index.last_probes(nq)
     info.update(ivf_scan_stats(index, probes, d, nlist, ivf_row_bytes(index.form, d, metric)))
     index.set_kernel_timing(True)

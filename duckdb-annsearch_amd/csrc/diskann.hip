@@ -462,8 +462,20 @@ int bfs_threads(int nq) {
     return std::max(1, t);
 }
 
+int bfs_groups(int nq) {
+    int g = 2;  // HIPANN_BFS_GROUPS=1: the unpipelined loop (A/B)
+    if (const char *e = std::getenv("HIPANN_BFS_GROUPS")) g = std::atoi(e);
+    g = std::min(g, std::max(1, nq / 64));  // ≥ 64 queries per group
+    return std::max(1, std::min(g, 8));
+}
+
 // Host-driven lock-step BFS (the reference's structure: host state, one id-gather launch per step).
 // Caller holds db.mu and the device.  Also the fallback of the resident path for flagged queries.
+//
+// The queries run in G groups (2 by default), each its own lock-step loop, pipelined: while the GPU gathers group
+// g's distances, the host threads insert and expand group g+1's.  A query's trajectory depends only on its own
+// state, so grouping changes no result; the batch's step count (the reference's loop iterations) is the largest
+// group's.
 void host_bfs(DiskDB *db, const uint32_t *adj, int R, const uint32_t *eps, int n_ep, const float *queries, int nq,
               int k, int l_search, int metric, int64_t *out_ids, float *out_d, int64_t *stats) {
     const uint32_t N = (uint32_t)db->n;
@@ -495,37 +507,49 @@ void host_bfs(DiskDB *db, const uint32_t *adj, int R, const uint32_t *eps, int n
     float *hout = db->hout.get<float>();
     for (size_t i = 0; i < cap; ++i) hm[i] = (uint32_t)(i / S);
     HIPANN_CHECK(hipMemcpyAsync(db->m.p, hm, cap * 4, hipMemcpyHostToDevice, st));
-    // Only the slot prefix up to the last query with work is shipped each step.
-    auto gpu_dists = [&](size_t span) {
-        HIPANN_CHECK(hipMemcpyAsync(db->ids.p, hid, span * 4, hipMemcpyHostToDevice, st));
-        {
-            ScopedTiming tm(db->timer, st);
-            launch_ids(*db, db->q.get<float>(), db->ids.get<unsigned>(), db->m.get<unsigned>(), (int)span, metric,
-                       db->out.get<float>(), st);
-        }
-        HIPANN_CHECK(hipMemcpyAsync(hout, db->out.p, span * 4, hipMemcpyDeviceToHost, st));
-        HIPANN_CHECK(hipStreamSynchronize(st));
-        ncalls++;
-    };
     std::vector<QState> Sq((size_t)nq);
     SpinPool pool(bfs_threads(nq));
     const int T = pool.size();
-    auto chunk = [&](int t, int &q0, int &q1) {
-        q0 = (int)((int64_t)nq * t / T);
-        q1 = (int)((int64_t)nq * (t + 1) / T);
+    struct Group {
+        int q0 = 0, q1 = 0;
+        bool seed = true, done = false, launched = false;
+        int64_t steps = 0;
+        hipEvent_t ev = nullptr;
     };
-    // per-thread reductions: [0] active queries, [1] distances, [2] last query with work + 1
-    std::vector<int64_t> red((size_t)T * 3 * 8, 0);  // padded against false sharing
-    auto reduce = [&](int j) {
-        int64_t v = 0;
-        for (int t = 0; t < T; ++t) v = (j == 2) ? std::max(v, red[(size_t)t * 24 + j]) : v + red[(size_t)t * 24 + j];
-        return v;
+    const int G = bfs_groups(nq);
+    std::vector<Group> grp((size_t)G);
+    for (int g = 0; g < G; ++g) {
+        grp[g].q0 = (int)((int64_t)nq * g / G);
+        grp[g].q1 = (int)((int64_t)nq * (g + 1) / G);
+        HIPANN_CHECK(hipEventCreateWithFlags(&grp[g].ev, hipEventDisableTiming));
+    }
+    struct EvFree {
+        std::vector<Group> &g;
+        ~EvFree() { for (auto &x : g) if (x.ev) (void)hipEventDestroy(x.ev); }
+    } ev_free{grp};
+    // the group's slots with work (up to its last query with new candidates) through the id-gather kernel
+    auto launch = [&](Group &g) {
+        int last = g.q0;
+        int64_t tot = 0;
+        for (int qi = g.q0; qi < g.q1; ++qi)
+            if (Sq[qi].nnew) { last = qi + 1; tot += Sq[qi].nnew; }
+        g.launched = tot > 0;
+        if (!tot) return;
+        const size_t o = (size_t)g.q0 * S, span = (size_t)(last - g.q0) * S;
+        HIPANN_CHECK(hipMemcpyAsync(db->ids.get<unsigned>() + o, hid + o, span * 4, hipMemcpyHostToDevice, st));
+        {
+            ScopedTiming tm(db->timer, st);
+            launch_ids(*db, db->q.get<float>(), db->ids.get<unsigned>() + o, db->m.get<unsigned>() + o, (int)span,
+                       metric, db->out.get<float>() + o, st);
+        }
+        HIPANN_CHECK(hipMemcpyAsync(hout + o, db->out.get<float>() + o, span * 4, hipMemcpyDeviceToHost, st));
+        HIPANN_CHECK(hipEventRecord(g.ev, st));
+        ncalls++;
+        nevals += tot;
     };
     // seed entry points (disk_provider.rs:524-538)
     pool.run([&](int t) {
-        int q0, q1;
-        chunk(t, q0, q1);
-        int64_t tot = 0, last = 0;
+        const int q0 = (int)((int64_t)nq * t / T), q1 = (int)((int64_t)nq * (t + 1) / T);
         for (int qi = q0; qi < q1; ++qi) {
             QState &s = Sq[qi];
             s.visited.init(std::max<size_t>(l * 2, 1024));
@@ -539,44 +563,32 @@ void host_bfs(DiskDB *db, const uint32_t *adj, int R, const uint32_t *eps, int n
             }
             for (size_t j = (size_t)cnt; j < S; ++j) slot[j] = 0xffffffffu;
             s.nnew = cnt;
-            tot += cnt;
-            if (cnt) last = qi + 1;
-        }
-        red[(size_t)t * 24 + 1] = tot;
-        red[(size_t)t * 24 + 2] = last;
-    });
-    if (reduce(1)) {
-        gpu_dists((size_t)reduce(2) * S);
-        nevals += reduce(1);
-    }
-    pool.run([&](int t) {
-        int q0, q1;
-        chunk(t, q0, q1);
-        for (int qi = q0; qi < q1; ++qi) {
-            QState &s = Sq[qi];
-            const uint32_t *slot = hid + (size_t)qi * S;
-            const float *dd = hout + (size_t)qi * S;
-            for (int j = 0; j < s.nnew; ++j) {
-                s.cands.push_back(Cand{dd[j], slot[j]});
-                std::push_heap(s.cands.begin(), s.cands.end(), CandGreater());
-                s.result.push_back(Cand{dd[j], slot[j]});
-            }
-            std::stable_sort(s.result.begin(), s.result.end(), [](const Cand &x, const Cand &y) { return x.d < y.d; });
         }
     });
-    // Lock-step iterations (disk_provider.rs:545-652).  One fork-join per step: the insert phase of
-    // step s (results of its GPU call) and the pop/expand phase of step s+1 run back to back per query.
-    bool first = true;
-    for (;;) {
+    for (auto &g : grp) launch(g);
+    // One host phase of a group: the results of its last GPU call (the seeds' into cands + result; later steps'
+    // through insert_result), then the loop head (disk_provider.rs:545-652): pop, stop rule, expansion.
+    // Returns the loop-head active count.
+    std::vector<int64_t> red((size_t)T * 8, 0);  // per-thread head counts, padded against false sharing
+    auto phase = [&](Group &g) {
+        const int n = g.q1 - g.q0;
+        const bool seed = g.seed;
         pool.run([&](int t) {
-            int q0, q1;
-            chunk(t, q0, q1);
-            int64_t head = 0, tot = 0, last = 0;
+            const int q0 = g.q0 + (int)((int64_t)n * t / T), q1 = g.q0 + (int)((int64_t)n * (t + 1) / T);
+            int64_t head = 0;
             for (int qi = q0; qi < q1; ++qi) {
                 QState &s = Sq[qi];
                 uint32_t *slot = hid + (size_t)qi * S;
-                if (!first) {
-                    const float *dd = hout + (size_t)qi * S;
+                const float *dd = hout + (size_t)qi * S;
+                if (seed) {
+                    for (int j = 0; j < s.nnew; ++j) {
+                        s.cands.push_back(Cand{dd[j], slot[j]});
+                        std::push_heap(s.cands.begin(), s.cands.end(), CandGreater());
+                        s.result.push_back(Cand{dd[j], slot[j]});
+                    }
+                    std::stable_sort(s.result.begin(), s.result.end(),
+                                     [](const Cand &x, const Cand &y) { return x.d < y.d; });
+                } else {
                     for (int j = 0; j < s.nnew; ++j) insert_result(s, l, dd[j], slot[j]);
                 }
                 const int prev = s.nnew;  // slots >= prev are already empty
@@ -606,21 +618,28 @@ void host_bfs(DiskDB *db, const uint32_t *adj, int R, const uint32_t *eps, int n
                     }
                 }
                 for (int j = s.nnew; j < prev; ++j) slot[j] = 0xffffffffu;
-                tot += s.nnew;
-                if (s.nnew) last = qi + 1;
             }
-            red[(size_t)t * 24 + 0] = head;
-            red[(size_t)t * 24 + 1] = tot;
-            red[(size_t)t * 24 + 2] = last;
+            red[(size_t)t * 8] = head;
         });
-        first = false;
-        const int64_t head = reduce(0), tot = reduce(1);
-        if (!head) break;  // no active query at the loop head
-        nsteps++;
-        if (!tot) continue;
-        gpu_dists((size_t)reduce(2) * S);
-        nevals += tot;
+        g.seed = false;
+        int64_t head = 0;
+        for (int t = 0; t < T; ++t) head += red[(size_t)t * 8];
+        return head;
+    };
+    for (int live = G; live > 0;) {
+        for (auto &g : grp) {
+            if (g.done) continue;
+            if (g.launched) HIPANN_CHECK(hipEventSynchronize(g.ev));
+            if (!phase(g)) {
+                g.done = true;
+                --live;
+                continue;
+            }
+            g.steps++;
+            launch(g);  // (nothing when no query of the group expanded new neighbours)
+        }
     }
+    for (auto &g : grp) nsteps = std::max(nsteps, g.steps);
     for (int qi = 0; qi < nq; ++qi) {
         const auto &r = Sq[qi].result;
         for (int j = 0; j < k; ++j) {

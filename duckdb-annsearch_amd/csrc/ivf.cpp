@@ -222,7 +222,7 @@ float shard_xmax2(IvfShard &sh, int d, hipStream_t st) {
 }
 
 void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, int k, int kout, float *D, int64_t *I,
-                      hipStream_t st, int form_override) {
+                      hipStream_t st, int form_override, const int64_t *probes_in) {
     DeviceGuard g(sh.device);
     const int nlist = ix.nlist, d = ix.d, metric = ix.metric;
     const int np = std::min(ix.nprobe, nlist);
@@ -337,13 +337,20 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     FlatShard &qsh = *sh.quant->shards[0];
     // HIPANN_IVF_SELECT_HOOK=0 (A/B): the count step in its own launch (ivf_count_q) instead of the select's tail
     static const bool hook_env = [] { const char *e = std::getenv("HIPANN_IVF_SELECT_HOOK"); return !e || std::atoi(e); }();
-    qsh.plan_hook = ivf_plan_query_major() && hook_env ? &hook : nullptr;
-    try {
-        flat_shard_search(*sh.quant, qsh, nq, xq, np, np, sh.coarse_d.get<float>(), sh.coarse_i.get<int64_t>(), st);
-    } catch (...) {
-        qsh.plan_hook = nullptr;
-        qsh.qn_given = nullptr;
-        throw;
+    if (probes_in) {
+        // the probe lists come from the caller (the coarse step partitioned over ranks, hipann_ivf_coarse_device +
+        // one all-gather): no quantizer launch; the plan counts the probes itself
+        HIPANN_CHECK(hipMemcpyAsync(sh.coarse_i.p, probes_in, sizeof(int64_t) * (size_t)nq * np, hipMemcpyDeviceToDevice,
+                                    st));
+    } else {
+        qsh.plan_hook = ivf_plan_query_major() && hook_env ? &hook : nullptr;
+        try {
+            flat_shard_search(*sh.quant, qsh, nq, xq, np, np, sh.coarse_d.get<float>(), sh.coarse_i.get<int64_t>(), st);
+        } catch (...) {
+            qsh.plan_hook = nullptr;
+            qsh.qn_given = nullptr;
+            throw;
+        }
     }
     qsh.plan_hook = nullptr;
     qsh.qn_given = nullptr;
@@ -369,7 +376,9 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     const float *qn = nullptr;
     if (form != kFormDirect && metric == kL2) {
         const FlatShard &qs = *sh.quant->shards[0];
-        if (qs.qn_of == xq && qs.qn_nq == nq) {
+        if (probes_in && half) {
+            qn = qsh0.qn.get<float>();  // the query preparation wrote ‖q‖² there (row_norms_f32's bits)
+        } else if (qs.qn_of == xq && qs.qn_nq == nq) {
             qn = qs.qn.get<float>();  // the coarse quantizer's ‖q‖² of the same queries
         } else {
             sh.qn.ensure(sizeof(float) * (size_t)nq, sh.device);
@@ -970,6 +979,51 @@ int hipann_ivf_search_device(void *h, int64_t nq, const float *xq_dev, int64_t k
         const int keff = (int)std::min<int64_t>(k, std::max<int64_t>(sh.live, 1));
         FenceScope fs(sh.fence, st, sh.device);  // the previous call's kernels may still use this shard's scratch
         ivf_shard_search(*vx, sh, nq, xq_dev, keff, (int)k, D_dev, I_dev, st);
+        return 0;
+    });
+}
+
+int hipann_ivf_coarse_device(void *h, int64_t nq, const float *xq_dev, int64_t *probes_dev, void *stream, char *eb,
+                             int el) {
+    return guard_int(eb, el, [&]() -> int {
+        HIPANN_REQUIRE(h, "null index");
+        auto *ix = static_cast<IndexBase *>(h);
+        HIPANN_REQUIRE(ix->kind == Kind::IVF, "not an IVFFlat index");
+        auto *vx = static_cast<IvfIndex *>(ix);
+        std::lock_guard<std::mutex> lk(vx->mu);
+        HIPANN_REQUIRE(vx->shards.size() == 1, "device coarse step needs a single-device index");
+        HIPANN_REQUIRE(nq >= 0 && (nq == 0 || (xq_dev && probes_dev)), "invalid arguments");
+        if (nq == 0) return 0;
+        IvfShard &sh = *vx->shards[0];
+        DeviceGuard g(sh.device);
+        hipStream_t st = static_cast<hipStream_t>(stream);
+        const int np = std::min(vx->nprobe, vx->nlist);
+        FenceScope fs(sh.fence, st, sh.device);
+        sh.app_cd.ensure(sizeof(float) * (size_t)nq * np, sh.device);
+        // FAISS quantizer->search(nq, x, nprobe): the Flat rules of the coarse quantizer (exact fp32 products)
+        flat_shard_search(*sh.quant, *sh.quant->shards[0], nq, xq_dev, np, np, sh.app_cd.get<float>(), probes_dev, st);
+        return 0;
+    });
+}
+
+int hipann_ivf_search_probes_device(void *h, int64_t nq, const float *xq_dev, const int64_t *probes_dev, int64_t k,
+                                    float *D_dev, int64_t *I_dev, void *stream, char *eb, int el) {
+    return guard_int(eb, el, [&]() -> int {
+        HIPANN_REQUIRE(h, "null index");
+        auto *ix = static_cast<IndexBase *>(h);
+        HIPANN_REQUIRE(ix->kind == Kind::IVF, "not an IVFFlat index");
+        auto *vx = static_cast<IvfIndex *>(ix);
+        std::lock_guard<std::mutex> lk(vx->mu);
+        HIPANN_REQUIRE(vx->shards.size() == 1, "device search needs a single-device index");
+        HIPANN_REQUIRE(k > 0 && k <= HIPANN_MAX_K, "k out of range");
+        HIPANN_REQUIRE(nq >= 0 && (nq == 0 || (xq_dev && probes_dev && D_dev && I_dev)), "invalid arguments");
+        IvfShard &sh = *vx->shards[0];
+        hipStream_t st = static_cast<hipStream_t>(stream);
+        vx->last_nq = nq;
+        vx->last_np = std::min(vx->nprobe, vx->nlist);
+        const int keff = (int)std::min<int64_t>(k, std::max<int64_t>(sh.live, 1));
+        FenceScope fs(sh.fence, st, sh.device);
+        ivf_shard_search(*vx, sh, nq, xq_dev, keff, (int)k, D_dev, I_dev, st, -1, probes_dev);
         return 0;
     });
 }

@@ -11,6 +11,7 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
                        int64_t *I, hipStream_t st, int form_override = -1, FlatPending *pend = nullptr);
 void flat_shard_finish(FlatIndex &ix, FlatShard &sh, const FlatPending &pend, hipStream_t st);
 // form_override >= 0 replaces ix.form for this call (the exact form's re-run of flagged queries)
+// probes_in (device, nq × min(nprobe, nlist) int64): the caller's probe lists replace the coarse quantizer's
 void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, int k, int kout, float *D, int64_t *I,
-                      hipStream_t st, int form_override = -1);
+                      hipStream_t st, int form_override = -1, const int64_t *probes_in = nullptr);
 }  // namespace hipann

@@ -315,6 +315,7 @@ struct IvfShard {
     // an append's staging (hipann_ivf_add): the new rows grouped by list, labels, physical destinations, norms,
     // the tiled passes they touch, and the new rows' maxima (‖x‖², |x|, fp16 residual²)
     DevBuf app_rows, app_norm, app_assign, app_up, app_stat;
+    DevBuf app_cd;  // hipann_ivf_coarse_device: the coarse distances (discarded)
     // pinned: the assignment on its way down, [destinations | labels | touched passes | live lengths] on their way
     // up (one copy), the maxima on their way down
     HostBuf app_hassign, app_hup, app_hstat;

@@ -103,6 +103,8 @@ def lib() -> C.CDLL:
             "hipann_ivf_create_device": ([i32, i32, i32, i32, vp, i64p, vp, vp, i32, i32, cp, i32], vp),
             "hipann_ivf_search": ([vp, i64, f, i64, f, i64p, cp, i32], i32),
             "hipann_ivf_search_device": ([vp, i64, vp, i64, vp, vp, vp, cp, i32], i32),
+            "hipann_ivf_coarse_device": ([vp, i64, vp, vp, vp, cp, i32], i32),
+            "hipann_ivf_search_probes_device": ([vp, i64, vp, vp, i64, vp, vp, vp, cp, i32], i32),
             "hipann_ivf_last_probes": ([vp, i64p, i64, cp, i32], i32),
             "hipann_ivf_set_nprobe": ([vp, i32], i32),
             "hipann_ivf_get_nprobe": ([vp], i32),
@@ -469,6 +471,20 @@ class HipIndexIVFFlat(_Handle):
         eb = _err()
         _check(lib().hipann_ivf_search_device(self._h, nq, C.c_void_p(xq_ptr), k, C.c_void_p(d_ptr),
                                               C.c_void_p(i_ptr), C.c_void_p(stream or None), eb, 1024), eb)
+
+    def coarse_device(self, nq: int, xq_ptr: int, probes_ptr: int, stream: int = 0) -> None:
+        """The coarse step alone (hipann_ivf_coarse_device): nq x min(nprobe, nlist) int64 probe lists."""
+        eb = _err()
+        _check(lib().hipann_ivf_coarse_device(self._h, nq, C.c_void_p(xq_ptr), C.c_void_p(probes_ptr),
+                                              C.c_void_p(stream or None), eb, 1024), eb)
+
+    def search_probes_device(self, nq: int, xq_ptr: int, probes_ptr: int, k: int, d_ptr: int, i_ptr: int,
+                             stream: int = 0) -> None:
+        """search_device with the caller's probe lists (hipann_ivf_search_probes_device): no coarse step."""
+        eb = _err()
+        _check(lib().hipann_ivf_search_probes_device(self._h, nq, C.c_void_p(xq_ptr), C.c_void_p(probes_ptr), k,
+                                                     C.c_void_p(d_ptr), C.c_void_p(i_ptr), C.c_void_p(stream or None),
+                                                     eb, 1024), eb)
 
     def rerank_fallbacks(self) -> int:
         """Queries the exact form's bound check flagged since creation (re-run on the device in the direct form)."""

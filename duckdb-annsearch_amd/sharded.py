@@ -5,8 +5,9 @@ MI355X-native addition of SURVEY §8e:
 
 * Flat: database rows split into contiguous ranges, one per rank (``shard_bounds``);
 * IVFFlat: whole inverted lists dealt to ranks by size-balanced greedy assignment, largest first onto
-  the least-loaded rank (``assign_lists``) — every rank replicates the 3 MB coarse quantizer and scans
-  only the probed lists it owns.
+  the least-loaded rank (``assign_lists``) — every rank holds the 3 MB coarse quantizer, computes the probe lists
+  of its slice of the batch, one all-gather of the probe lists (``PartitionedProbes``) gives every rank the whole
+  batch's, and each rank scans only the probed lists it owns.
 
 Every rank searches only its shard on its own GPU, with labels already global.  Its top-k is packed
 into one buffer per rank — ``[labels int64 nq·k][distances fp32 nq·k]``, 12·nq·k bytes (123 KB at
@@ -112,6 +113,62 @@ class ShardedSearch:
             for r, p in enumerate(parts):
                 self.gathered[r].copy_(p)
         return self.merge(self.gathered, self.nq, self.k)
+
+
+def query_bounds(nq: int, rank: int, world: int) -> Tuple[int, int]:
+    """The slice of the batch whose coarse step `rank` computes (contiguous, as shard_bounds)."""
+    return shard_bounds(nq, rank, world)
+
+
+def coarse_partition_ok(nq: int, world: int) -> bool:
+    """Partition the coarse step only when every rank's slice keeps FAISS's BLAS form (>= 20 queries,
+    distance_compute_blas_threshold): a query's probe list then does not depend on the slice it was computed in."""
+    return world > 1 and nq // world >= 20
+
+
+class PartitionedProbes:
+    """The IVF coarse step partitioned over ranks: rank r computes the probe lists of its slice of the
+    batch (``coarse(q_slice, probes_out)``, e.g. hipann_ivf_coarse_device), and ONE all-gather of the padded
+    [world][ceil(nq/world)][nprobe] int64 lists (256 KB at nq 1024, nprobe 32) gives every rank the whole batch's —
+    instead of every rank running the same coarse quantizer over all nq queries.  The lists are bit-identical to the
+    replicated step's while ``coarse_partition_ok``."""
+
+    def __init__(self, coarse: Callable, nq: int, nprobe: int, device, group=None):
+        import torch
+        import torch.distributed as dist
+
+        self.coarse = coarse
+        self.group = group
+        self.nq, self.nprobe = nq, nprobe
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.rows = -(-nq // self.world)
+        self.lo, self.hi = query_bounds(nq, self.rank, self.world)
+        self.local = torch.full((self.rows, nprobe), -1, dtype=torch.int64, device=device)
+        self.gathered = torch.empty((self.world, self.rows, nprobe), dtype=torch.int64, device=device)
+        self.bounds = [query_bounds(nq, r, self.world) for r in range(self.world)]
+        self.out = torch.empty((nq, nprobe), dtype=torch.int64, device=device)
+
+    def probes(self, xq):
+        """(nq, nprobe) int64 probe lists of the whole batch xq on every rank."""
+        import torch.distributed as dist
+
+        m = self.hi - self.lo
+        if m:
+            self.coarse(xq[self.lo:self.hi], self.local[:m])
+        if self.world == 1:
+            return self.local[: self.nq]
+        if self.local.is_cuda and dist.get_backend(self.group) == "nccl":
+            dist.all_gather_into_tensor(self.gathered.view(-1), self.local.view(-1), group=self.group)
+        else:  # gloo: through host memory
+            host = self.local.cpu()
+            parts = [torch_empty_like_cpu(host) for _ in range(self.world)]
+            dist.all_gather(parts, host, group=self.group)
+            for r, p in enumerate(parts):
+                self.gathered[r].copy_(p)
+        for r, (lo, hi) in enumerate(self.bounds):
+            self.out[lo:hi].copy_(self.gathered[r, : hi - lo])
+        return self.out
 
 
 def torch_empty_like_cpu(t):

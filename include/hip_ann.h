@@ -196,6 +196,17 @@ int hipann_ivf_search_device(void *index, int64_t nq, const float *xq_dev, int64
 
 /* Probe lists chosen by the last search (nq*nprobe int64, host) — for parity tests. */
 int hipann_ivf_last_probes(void *index, int64_t *probes, int64_t cap, char *err_buf, int err_len);
+/* The coarse step partitioned over ranks (list-sharded multi-GPU IVF): each rank computes the probe
+ * lists of ITS slice of the batch (hipann_ivf_coarse_device: FAISS quantizer->search(nq, x, nprobe) on the
+ * coarse quantizer, probes_dev = nq × min(nprobe, nlist) int64 list ids in probe order), one all-gather makes the
+ * whole batch's lists, and hipann_ivf_search_probes_device searches every query with those probe lists instead of
+ * running the coarse step again — bit-identical to the replicated scheme (a query's probe list does not depend on
+ * the other queries of the batch while every slice has >= 20 queries, FAISS's BLAS-form threshold).  Both are
+ * asynchronous on `stream`, like hipann_ivf_search_device; single-device handles only.  0 / -1. */
+int hipann_ivf_coarse_device(void *index, int64_t nq, const float *xq_dev, int64_t *probes_dev, void *stream,
+                             char *err_buf, int err_len);
+int hipann_ivf_search_probes_device(void *index, int64_t nq, const float *xq_dev, const int64_t *probes_dev,
+                                    int64_t k, float *D_dev, int64_t *I_dev, void *stream, char *err_buf, int err_len);
 
 int hipann_ivf_set_nprobe(void *index, int nprobe);
 int hipann_ivf_get_nprobe(void *index);

@@ -377,3 +377,110 @@ def test_bench_selftest_world1():
     assert r.returncode == 0, r.stderr[-3000:]
     js = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
     assert js["n_gpus"] == 1 and js["world_check"]["ranks_seen"] == [0]
+
+
+# ------------------------------------------------------------------------------------------------
+# the IVF coarse step partitioned over ranks: PartitionedProbes
+# ------------------------------------------------------------------------------------------------
+def _worker_partitioned_probes(rank, world, port, result_path):
+    dist = _setup(rank, world, port)
+    import torch
+    from oracle import oracle as O
+    from sharded import PartitionedProbes
+    from _data import faiss_metal_case
+
+    xb, xq = faiss_metal_case(3000, 50, 40)
+    cen = np.ascontiguousarray(xb[::100][:30])
+
+    def coarse(q, out):  # FAISS quantizer->search(nq, x, nprobe) on this rank's slice
+        _, P = O.flat_search(cen, q.numpy(), 7)
+        out.copy_(torch.from_numpy(P))
+
+    pp = PartitionedProbes(coarse, 50, 7, "cpu")
+    P = pp.probes(torch.from_numpy(xq)).numpy().copy()
+    if rank == 0:
+        np.savez(result_path, P=P, rows=pp.rows)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_partitioned_probes_gloo_world2(tmp_path):
+    """Each of two ranks computes the probe lists of its 25-query slice (>= 20: FAISS's BLAS form, as for the whole
+    batch); one all-gather gives every rank the lists of all 50 queries, identical to the replicated coarse step."""
+    import torch.multiprocessing as mp
+    from oracle import oracle as O
+    from _data import build_ivf_lists, faiss_metal_case
+
+    out = tmp_path / "res.npz"
+    mp.spawn(_worker_partitioned_probes, args=(2, _free_port(), str(out)), nprocs=2, join=True)
+    r = np.load(out)
+    xb, xq = faiss_metal_case(3000, 50, 40)
+    cen = np.ascontiguousarray(xb[::100][:30])
+    off, ids, codes = build_ivf_lists(xb, cen)
+    _, _, Po = O.ivf_search(cen, off, ids, codes, xq, 10, 7)
+    assert np.array_equal(r["P"], Po) and int(r["rows"]) == 25
+
+
+def test_coarse_partition_rule():
+    sys.path.insert(0, str(ROOT / "duckdb-annsearch_amd"))
+    from sharded import coarse_partition_ok, query_bounds
+    assert coarse_partition_ok(1024, 8) and coarse_partition_ok(40, 2)
+    assert not coarse_partition_ok(1024, 1) and not coarse_partition_ok(39, 2) and not coarse_partition_ok(100, 8)
+    b = [query_bounds(1024, r, 8) for r in range(8)]
+    assert b[0] == (0, 128) and b[-1] == (896, 1024)
+
+
+def _worker_gpu_partitioned(rank, world, port, result_path):
+    dist = _setup(rank, world, port)
+    import torch
+    import hipann
+    import bench
+    from ivf_build import build_ivf_list_shard
+    from sharded import PartitionedProbes, ShardedSearch, merge_packed_device_torch
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    n, d, nq, k = 60_000, 96, 200, 10
+    stream = torch.cuda.current_stream().cuda_stream
+    xq = bench.uniform_queries(torch, nq, d, dev)
+    gen = lambda out, row0: bench.gen_uniform_rows(torch, out, row0, 42)  # noqa: E731
+    index, info = build_ivf_list_shard(torch, hipann, gen, n, d, 64, 8, 0, rank, world, dev)
+    # the replicated scheme: every rank's own coarse step over the whole batch
+    rep = ShardedSearch(lambda q, D, I: index.search_device(nq, q.data_ptr(), k, D.data_ptr(), I.data_ptr(), stream),
+                        merge_packed_device_torch(hipann, 0), nq, k, dev)
+    D0, I0 = rep.search(xq)
+    D0, I0 = D0.clone(), I0.clone()
+    torch.cuda.synchronize()
+    P0 = index.last_probes(nq)
+    pp = PartitionedProbes(lambda qs, out: index.coarse_device(qs.shape[0], qs.data_ptr(), out.data_ptr(), stream),
+                           nq, 8, dev)
+
+    def local(q, D, I):
+        P = pp.probes(q)
+        index.search_probes_device(nq, q.data_ptr(), P.data_ptr(), k, D.data_ptr(), I.data_ptr(), stream)
+
+    part = ShardedSearch(local, merge_packed_device_torch(hipann, 0), nq, k, dev)
+    D1, I1 = part.search(xq)
+    torch.cuda.synchronize()
+    P1 = pp.probes(xq).cpu().numpy().copy()
+    np.savez(f"{result_path}.{rank}.npz", P0=P0, P1=P1, D0=D0.cpu().numpy(), I0=I0.cpu().numpy(), D1=D1.cpu().numpy(),
+             I1=I1.cpu().numpy(), last=index.last_probes(nq))
+    dist.barrier()
+    index.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_sharded_ivf_partitioned_coarse_world2_on_one_device(gpu, tmp_path):
+    """list-sharded IVF with the coarse step partitioned over two ranks (hipann_ivf_coarse_device
+    on each rank's 100-query slice, one all-gather, hipann_ivf_search_probes_device): the probe lists are bit-identical
+    to the replicated coarse step's, and the merged top-k (ids and distances) is identical to the replicated scheme's."""
+    import torch.multiprocessing as mp
+
+    res = str(tmp_path / "res")
+    mp.spawn(_worker_gpu_partitioned, args=(2, _free_port(), res), nprocs=2, join=True)
+    for r in range(2):
+        z = np.load(f"{res}.{r}.npz")
+        assert np.array_equal(z["P1"], z["P0"])
+        assert np.array_equal(z["last"], z["P0"])  # the search ran with those lists
+        assert np.array_equal(z["I1"], z["I0"]) and np.array_equal(z["D1"], z["D0"])
