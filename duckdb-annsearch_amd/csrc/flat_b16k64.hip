@@ -36,36 +36,42 @@ typedef int k64_i32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void k64_lds_void;
 
 constexpr int K64_TN = 256;               // database rows per tile
-constexpr int K64_QM = 256;               // queries per block (8 waves × 32)
-constexpr int K64_W = 8;
+constexpr int K64_QM = 256;               // queries per block (8 waves × 32, or 4 waves × 64)
+constexpr int K64_W = 8;                  // waves per block of the 2-row-block (MBW = 2) variant
 constexpr int K64_NB = 5;                 // LDS stages: g read, g+1 .. g+3 landing / in flight
 constexpr int K64_BU = K64_TN * 4;        // 16-B units of one 32-dim chunk of a database tile
 constexpr int K64_SU = 2 * K64_BU;        // units per stage (one 64-dim K-step): 32 KB
-constexpr int K64_PIECES = K64_SU / 64 / K64_W;  // 1-KiB LDS-DMA pieces per wave per K-step
 constexpr size_t K64_LDS = (size_t)K64_NB * K64_SU * 16;
-static_assert(K64_PIECES * 64 * K64_W == K64_SU, "pieces split evenly");
 static_assert(K64_LDS <= 160 * 1024, "LDS");
+// MBW = 16-query accumulator row blocks per wave: 2 → 8 waves of 32 queries (two waves per SIMD, 256 registers);
+// 4 → 4 waves of 64 queries (one wave per SIMD, 512 registers: the accumulators in AGPRs), each B fragment read
+// from LDS feeding four MFMAs instead of two — half the LDS reads and barrier arrivals per MFMA
+template <int MBW> struct K64Geom {
+    static constexpr int W = 16 / MBW;                 // waves per block
+    static constexpr int PIECES = K64_SU / 64 / W;     // 1-KiB LDS-DMA pieces per wave per K-step
+    static_assert(PIECES * 64 * W == K64_SU, "pieces split evenly");
+};
 
-// Epilogue of one tile for accumulator row (MB, I).  On entry acc[mb][jb][i] = s = 2·q·x − ‖x‖² (L2; 2·q·x
-// for IP; −inf past N) of query 32·wave + 16·mb + 4·(lane >> 4) + i and database row x0 + 16·jb + (lane & 15);
-// a row passes its query's bound when s ≥ cth = ‖q‖² − T (L2) or −2·T (IP) — cth[mb][i] is the lane's own
-// query's (its 16-lane group).  Passing rows (rare) are appended to the query's buffer with key = ‖q‖² − s
+// Epilogue of one tile for accumulator row (MB, I).  On entry sm[jb][i] = s = 2·q·x − ‖x‖² (L2; 2·q·x for IP;
+// −inf past N) of the wave's query 16·MB + 4·(lane >> 4) + i and database row x0 + 16·jb + (lane & 15); a row
+// passes its query's bound when s ≥ cth = ‖q‖² − T (L2) or −2·T (IP) — cthm[i] is the lane's own query's (its
+// 16-lane group).  Passing rows (rare) are appended to the query's buffer with key = ‖q‖² − s
 // (L2, clamped at 0) or −s/2 = −q·x (IP); cntv lane j holds the count of the wave's query j (it keeps
 // counting past cap: flat_cand_select flags an overflowed query for the exact fallback).
 template <bool L2M, int MB, int I>
-__device__ __forceinline__ void k64_epilogue_row(const k64_f32x4 (&acc)[2][16], const float (&cth)[2][4], float qnl,
+__device__ __forceinline__ void k64_epilogue_row(const k64_f32x4 (&sm)[16], const float (&cthm)[4], float qnl,
                                                  int &cntv, int64_t x0, float *__restrict__ cand_d,
                                                  int *__restrict__ cand_i, int64_t cbase, int64_t cq, int cap,
                                                  int lane) {
     bool any = false;
 #pragma unroll
-    for (int jb = 0; jb < 16; ++jb) any |= acc[MB][jb][I] >= cth[MB][I];
+    for (int jb = 0; jb < 16; ++jb) any |= sm[jb][I] >= cthm[I];
     const unsigned long long m = __ballot(any);
     if (m == 0ull) return;
     // the lane's passing columns (bit jb)
     unsigned pm = 0;
 #pragma unroll
-    for (int jb = 0; jb < 16; ++jb) pm |= acc[MB][jb][I] >= cth[MB][I] ? 1u << jb : 0u;
+    for (int jb = 0; jb < 16; ++jb) pm |= sm[jb][I] >= cthm[I] ? 1u << jb : 0u;
 #pragma unroll 1
     for (int fq = 0; fq < 4; ++fq) {
         unsigned grp = (unsigned)(m >> (16 * fq)) & 0xffffu;  // lanes of query fq holding a passing row
@@ -83,9 +89,9 @@ __device__ __forceinline__ void k64_epilogue_row(const k64_f32x4 (&acc)[2][16], 
             while (pml) {
                 const int jb = __ffs(pml) - 1;
                 pml &= pml - 1;
-                float sv = acc[MB][0][I];
+                float sv = sm[0][I];
 #pragma unroll
-                for (int j = 1; j < 16; ++j) sv = jb == j ? acc[MB][j][I] : sv;
+                for (int j = 1; j < 16; ++j) sv = jb == j ? sm[j][I] : sv;
                 sv = readlane_f(sv, src);
                 float key;
                 if (L2M) {
@@ -116,14 +122,16 @@ __device__ __forceinline__ void k64_epilogue_row(const k64_f32x4 (&acc)[2][16], 
 // per byte moved.  The int32 sums are exact (|acc| <= d·127² < 2^24 for d <= 1040) and live in the float
 // accumulators' registers bit for bit until the tile's epilogue turns them into q·x = acc·s_q·s_x with the
 // per-query / per-row scales (qscale / xscale); everything after that is the bf16 path's.
-template <bool L2M, bool KEYS, bool I8 = false>
-__global__ void __launch_bounds__(64 * K64_W, 1)
+template <bool L2M, bool KEYS, bool I8 = false, int MBW = 2>
+__global__ void __launch_bounds__(64 * K64Geom<MBW>::W, 1) __attribute__((amdgpu_waves_per_eu(1, MBW == 4 ? 1 : 2)))
 flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm, int64_t nq,
               const k64_u32x4 *__restrict__ Xt, const float *xnorm, int64_t N, int nk, int nqt, int nsplit,
               int64_t tiles_per_split, int64_t tile_begin, int64_t tile_end, const float *__restrict__ bound,
               float *__restrict__ cand_d, int *__restrict__ cand_i, int *__restrict__ cand_n, int cap,
               int resume, const float *__restrict__ qscale, const float *xscale) {
     constexpr int NB = K64_NB;
+    constexpr int QW = 16 * MBW;  // queries per wave
+    constexpr int PIECES = K64Geom<MBW>::PIECES;
     extern __shared__ __attribute__((aligned(16))) k64_u32x4 smem_k64[];
 
     const int nblocks = nqt * nsplit;
@@ -143,17 +151,17 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
     // wave-uniform (readfirstlane): the wave's bases and buffer pointers live in SGPRs, not VGPRs
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int m16 = lane & 15, g4 = lane >> 4;
-    const int64_t q0w = q0 + 32 * wave + 4 * g4;  // + 16·mb + i: the lane's accumulator query rows
+    const int64_t q0w = q0 + QW * wave + 4 * g4;  // + 16·mb + i: the lane's accumulator query rows
 
-    // per-lane state of the wave's 32 queries (lane j: query 32·wave + j): ‖q‖², candidate count
-    const int64_t qlane = q0 + 32 * wave + (lane & 31);
+    // per-lane state of the wave's QW queries (lane j: query QW·wave + j): ‖q‖², candidate count
+    const int64_t qlane = q0 + QW * wave + (lane & (QW - 1));
     float qnl = 0.f;
     if (L2M) qnl = qlane < nq ? qnorm[qlane] : 0.f;
     int cntv = 0;
-    if (!KEYS && resume && lane < 32 && qlane < nq) cntv = cand_n[qlane * nsplit + split];
-    float cth[2][4];
+    if (!KEYS && resume && lane < QW && qlane < nq) cntv = cand_n[qlane * nsplit + split];
+    float cth[MBW][4];
 #pragma unroll
-    for (int mb = 0; mb < 2; ++mb)
+    for (int mb = 0; mb < MBW; ++mb)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int64_t q = q0w + 16 * mb + i;
@@ -166,51 +174,55 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
             }
         }
     // int8: 2·s_q of the lane's accumulator query rows (the 2 of s = 2·q·x − ‖x‖² folded in)
-    float csq[2][4];
+    float csq[MBW][4];
 #pragma unroll
-    for (int mb = 0; mb < 2; ++mb)
+    for (int mb = 0; mb < MBW; ++mb)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int64_t q = q0w + 16 * mb + i;
             csq[mb][i] = I8 && q < nq ? 2.f * qscale[q] : 2.f;
         }
     const int64_t cq = (int64_t)nsplit * cap;  // buffer stride between consecutive queries
-    const int64_t cbase = ((q0 + 32 * wave) * nsplit + split) * (int64_t)cap;
+    const int64_t cbase = ((q0 + QW * wave) * nsplit + split) * (int64_t)cap;
 
     // K-step g = (t − t0)·ns + s covers image chunks 2s, 2s + 1 of tile t: 2·K64_BU consecutive units
     const k64_u32x4 *Xb = Xt + t0 * nk * K64_BU + lane;
-    // the lane's query fragments: rows 32·wave + 16·mb + m16, unit c = g4 of each 32-dim chunk
+    // the lane's query fragments: rows QW·wave + 16·mb + m16, unit c = g4 of each 32-dim chunk
     const k64_u32x4 *Qw = Qt + (int64_t)qt * nk * (K64_QM * 4) + g4 * K64_QM;
-    const int qrow0 = (32 * wave + m16) ^ (g4 << 1), qrow1 = (32 * wave + 16 + m16) ^ (g4 << 1);
+    int qrow[MBW];
+#pragma unroll
+    for (int mb = 0; mb < MBW; ++mb) qrow[mb] = (QW * wave + 16 * mb + m16) ^ (g4 << 1);
     // query fragments: a 2-slot register ring (K-step g+1's loaded while g is computed); the loop is unrolled by
     // two so the slot is a compile-time index
     int ks_a = 0;
-    k64_u32x4 ar[2][2][2];  // [ring slot][chunk of the K-step][mb]
+    k64_u32x4 ar[2][2][MBW];  // [ring slot][chunk of the K-step][mb]
     auto issue_a = [&](auto slot_c) {
         constexpr int SL = decltype(slot_c)::value;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int64_t kc = 2 * ks_a + h;
-            ar[SL][h][0] = Qw[kc * (K64_QM * 4) + qrow0];
-            ar[SL][h][1] = Qw[kc * (K64_QM * 4) + qrow1];
+#pragma unroll
+            for (int mb = 0; mb < MBW; ++mb) ar[SL][h][mb] = Qw[kc * (K64_QM * 4) + qrow[mb]];
         }
         ks_a = ks_a + 1 < ns ? ks_a + 1 : 0;
     };
     auto issue_b = [&](int64_t g, int stage) {
         k64_u32x4 *dst = smem_k64 + stage * K64_SU;
 #pragma unroll
-        for (int i = 0; i < K64_PIECES; ++i) {
-            const int inst = wave * K64_PIECES + i;
+        for (int i = 0; i < PIECES; ++i) {
+            const int inst = wave * PIECES + i;
             __builtin_amdgcn_global_load_lds((const void *)(Xb + g * K64_SU + inst * 64),
                                              (k64_lds_void *)(dst + inst * 64), 16, 0, 0);
         }
     };
 
-    k64_f32x4 acc[2][16];
+    // the accumulators: int32 sums (I8) or fp32 (bf16), in their MFMA's own type
+    using AccT = std::conditional_t<I8, k64_i32x4, k64_f32x4>;
+    AccT acc[MBW][16];
 #pragma unroll
-    for (int mb = 0; mb < 2; ++mb)
+    for (int mb = 0; mb < MBW; ++mb)
 #pragma unroll
-        for (int jb = 0; jb < 16; ++jb) acc[mb][jb] = (k64_f32x4){0.f, 0.f, 0.f, 0.f};
+        for (int jb = 0; jb < 16; ++jb) acc[mb][jb] = (AccT){0, 0, 0, 0};
     // ‖x‖² of tile tt, row 64·j + lane in xr[j] (0 for IP)
     float xr[4] = {0.f, 0.f, 0.f, 0.f};
     float xsc[4] = {1.f, 1.f, 1.f, 1.f};  // int8: the tile's row scales, row 64·j + lane in xsc[j]
@@ -227,7 +239,8 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
     // in issue order, so the tile pieces lead by three K-steps (HBM misses) and the query fragments by one (L2
     // hits) without either wait covering the other.  The waits are the builtin (s_waitcnt vmcnt(4) expcnt(7)
     // lgkmcnt(15)), not inline asm: the compiler's wait pass must see them.
-    constexpr unsigned kWaitStep = 0xF70u | K64_PIECES;
+    constexpr unsigned kWaitStep = 0xF70u | PIECES;
+    static_assert(PIECES < 16, "vmcnt low field");
     auto clampg = [&](int64_t g) { return g < G ? g : G - 1; };  // past the end: the last K-step again, never read
     if (G > 0) {
         // the steady state's order: B(0), B(1), A(0), B(2)
@@ -240,8 +253,11 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
 
     int ks = 0, stage = 0;
     int64_t t = t0;
-    auto body = [&](int64_t g, auto slot_c) {
+    // FIRST (the 4-wave variant's first K-step of a tile): the chunk-0 MFMAs start from a zero C operand instead of
+    // the accumulators, so the accumulator chains never pass through an explicit reset
+    auto body = [&](int64_t g, auto slot_c, auto first_c) {
         constexpr int SL = decltype(slot_c)::value;
+        constexpr bool FIRST = decltype(first_c)::value;
         // K-step g landed (the wait at the end of the previous K-step), every wave done reading the stage about to
         // be refilled (g−2's): one barrier
         __builtin_amdgcn_s_barrier();
@@ -260,35 +276,40 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
             if (h == 0) issue_a(std::integral_constant<int, 1 - SL>{});
             // B fragment of rows 16·jb + m16, unit c = g4: slot c·256 + 16·jb + (m16 ^ 2c)
             const k64_u32x4 *Bc = Bb + h * K64_BU + g4 * K64_TN + (m16 ^ (g4 << 1));
-            const k64_b16x8 a0 = __builtin_bit_cast(k64_b16x8, ar[SL][h][0]);
-            const k64_b16x8 a1 = __builtin_bit_cast(k64_b16x8, ar[SL][h][1]);
             k64_b16x8 bf[16];
 #pragma unroll
             for (int jb = 0; jb < 16; ++jb) bf[jb] = __builtin_bit_cast(k64_b16x8, Bc[16 * jb]);
 #pragma unroll
             for (int jb = 0; jb < 16; ++jb) {
-                if constexpr (I8) {  // int32 sums carried in the accumulators' registers, bit for bit
-                    const k64_i32x4 ai0 = __builtin_bit_cast(k64_i32x4, a0);
-                    const k64_i32x4 ai1 = __builtin_bit_cast(k64_i32x4, a1);
-                    const k64_i32x4 bi = __builtin_bit_cast(k64_i32x4, bf[jb]);
-                    acc[0][jb] = __builtin_bit_cast(k64_f32x4, __builtin_amdgcn_mfma_i32_16x16x64_i8(
-                                                                   ai0, bi, __builtin_bit_cast(k64_i32x4, acc[0][jb]), 0, 0, 0));
-                    acc[1][jb] = __builtin_bit_cast(k64_f32x4, __builtin_amdgcn_mfma_i32_16x16x64_i8(
-                                                                   ai1, bi, __builtin_bit_cast(k64_i32x4, acc[1][jb]), 0, 0, 0));
-                } else {
-                    acc[0][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bf[jb], acc[0][jb], 0, 0, 0);
-                    acc[1][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bf[jb], acc[1][jb], 0, 0, 0);
+#pragma unroll
+                for (int mb = 0; mb < MBW; ++mb) {
+                    const bool zc = FIRST && h == 0;  // (constant once unrolled)
+                    if constexpr (I8) {  // int32 sums carried in the accumulators' registers, bit for bit
+                        const k64_i32x4 ai = __builtin_bit_cast(k64_i32x4, ar[SL][h][mb]);
+                        const k64_i32x4 bi = __builtin_bit_cast(k64_i32x4, bf[jb]);
+                        acc[mb][jb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ai, bi, zc ? (AccT){0, 0, 0, 0} : acc[mb][jb], 0,
+                                                                             0, 0);
+                    } else {
+                        acc[mb][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(k64_b16x8, ar[SL][h][mb]),
+                                                                              bf[jb], zc ? (AccT){0, 0, 0, 0} : acc[mb][jb],
+                                                                              0, 0, 0);
+                    }
                 }
             }
             if (h == 1) issue_b(clampg(g + 3), stage < 2 ? stage + 3 : stage - 2);
-            // schedule (same region): four LDS reads ahead, then one read per MFMA pair, one vector-memory op per
-            // eight MFMAs
+            // schedule (same region): four LDS reads ahead, then one read per MBW MFMAs; the vector-memory ops (A
+            // in chunk 0, B at the end of chunk 1) spread over the MFMAs
+            const int NV = h == 0 ? 2 * MBW : PIECES;  // vector-memory ops of this chunk (constant once unrolled)
             __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
 #pragma unroll
             for (int p = 0; p < 16; ++p) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, MBW, 0);
                 if (p < 12) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                if (h == 0 ? p % 4 == 1 : p >= 12) __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+                if (h == 0) {
+                    if (p % (16 / NV) == 1 % (16 / NV)) __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+                } else if (p >= 16 - NV) {
+                    __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+                }
             }
             // chunk fence: A(g+1) stays in chunk 0, B(g+3) at the end of chunk 1 (their order is what the counted
             // wait assumes)
@@ -297,75 +318,101 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
         // A(g+1), B(g+1) landed; B(g+2), B(g+3) stay in flight
         __builtin_amdgcn_s_waitcnt(kWaitStep);
         stage = stage + 1 < NB ? stage + 1 : 0;
-        if (++ks == ns) {
-            ks = 0;
-            const int64_t x0 = t * K64_TN;
-            // s = 2·q·x − ‖x‖² in place (the filter's left side; the key follows from it with one more rounding,
-            // inside the rerank bound's (d + 8)·2⁻²⁴ term); xr: row 64·j + l in lane l's xr[j]
+    };
+    // the tile's epilogue (after its last K-step)
+    auto epilogue = [&]() {
+        const int64_t x0 = t * K64_TN;
+        // s = 2·q·x − ‖x‖² (the filter's left side; the key follows from it with one more rounding, inside the
+        // rerank bound's (d + 8)·2⁻²⁴ term); xr: row 64·j + l in lane l's xr[j].  One 16-query row block at a
+        // time: its accumulators move to VGPRs (s), are filtered and reset before the next block's — with MBW = 4
+        // the 256 accumulators stay in AGPRs and only 64 values are live in VGPRs.
+        float xvj[16], sxj[16];
+#pragma unroll
+        for (int jb = 0; jb < 16; ++jb) {
+            const float xs = __shfl(xr[jb >> 2], 16 * (jb & 3) + m16);
+            xvj[jb] = x0 + 16 * jb + m16 < N ? xs : __builtin_inff();
+            sxj[jb] = I8 ? __shfl(xsc[jb >> 2], 16 * (jb & 3) + m16) : 1.f;
+        }
+        auto tile_mb = [&](auto mb_c) {
+            constexpr int MB = decltype(mb_c)::value;
+            k64_f32x4 sm[16];
 #pragma unroll
             for (int jb = 0; jb < 16; ++jb) {
-                const float xs = __shfl(xr[jb >> 2], 16 * (jb & 3) + m16);
-                const float xv = x0 + 16 * jb + m16 < N ? xs : __builtin_inff();
                 if constexpr (I8) {
                     // whole-vector reinterpret + convert: per-element extracts of the bit-cast i32 MFMA result were
                     // miscompiled (only element 0 of each accumulator was read; the others came from stale
                     // registers — found by the form's parity tests, every query with index % 4 != 0 wrong)
-                    const float sx = __shfl(xsc[jb >> 2], 16 * (jb & 3) + m16);
+                    const k64_f32x4 v = __builtin_convertvector(acc[MB][jb], k64_f32x4);
 #pragma unroll
-                    for (int mb = 0; mb < 2; ++mb) {
-                        const k64_f32x4 v = __builtin_convertvector(__builtin_bit_cast(k64_i32x4, acc[mb][jb]), k64_f32x4);
-                        k64_f32x4 r;
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) r[i] = fmaf(csq[mb][i] * sx, v[i], -xv);
-                        acc[mb][jb] = r;
-                    }
+                    for (int i = 0; i < 4; ++i) sm[jb][i] = fmaf(csq[MB][i] * sxj[jb], v[i], -xvj[jb]);
                 } else {
 #pragma unroll
-                    for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) acc[mb][jb][i] = fmaf(2.f, acc[mb][jb][i], -xv);
+                    for (int i = 0; i < 4; ++i) sm[jb][i] = fmaf(2.f, acc[MB][jb][i], -xvj[jb]);
                 }
+                if constexpr (MBW != 4) acc[MB][jb] = (AccT){0, 0, 0, 0};  // (4: the FIRST K-steps start from 0)
             }
             if constexpr (KEYS) {
                 // every key (L2: ‖q‖² − s clamped at 0; IP: −s/2) into the dense key matrix
 #pragma unroll
-                for (int mb = 0; mb < 2; ++mb)
+                for (int i = 0; i < 4; ++i) {
+                    const int64_t q = q0w + 16 * MB + i;
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int64_t q = q0w + 16 * mb + i;
-#pragma unroll
-                        for (int jb = 0; jb < 16; ++jb) {
-                            const int64_t x = x0 + 16 * jb + m16;
-                            float key;
-                            if (L2M) {
-                                key = cth[mb][i] - acc[mb][jb][i];
-                                key = key < 0.f ? 0.f : key;
-                            } else {
-                                key = -0.5f * acc[mb][jb][i];
-                            }
-                            if (q < nq && x < N) cand_d[q * N + x] = key;
+                    for (int jb = 0; jb < 16; ++jb) {
+                        const int64_t x = x0 + 16 * jb + m16;
+                        float key;
+                        if (L2M) {
+                            key = cth[MB][i] - sm[jb][i];
+                            key = key < 0.f ? 0.f : key;
+                        } else {
+                            key = -0.5f * sm[jb][i];
                         }
+                        if (q < nq && x < N) cand_d[q * N + x] = key;
                     }
+                }
             } else {
-                [&]<int... P>(std::integer_sequence<int, P...>) {
-                    (k64_epilogue_row<L2M, P / 4, P % 4>(acc, cth, qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane),
-                     ...);
-                }(std::make_integer_sequence<int, 8>{});
+                k64_epilogue_row<L2M, MB, 0>(sm, cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
+                k64_epilogue_row<L2M, MB, 1>(sm, cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
+                k64_epilogue_row<L2M, MB, 2>(sm, cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
+                k64_epilogue_row<L2M, MB, 3>(sm, cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
             }
-#pragma unroll
-            for (int mb = 0; mb < 2; ++mb)
-#pragma unroll
-                for (int jb = 0; jb < 16; ++jb) acc[mb][jb] = (k64_f32x4){0.f, 0.f, 0.f, 0.f};
-            ++t;
-        }
+        };
+        [&]<int... M>(std::integer_sequence<int, M...>) {
+            (tile_mb(std::integral_constant<int, M>{}), ...);
+        }(std::make_integer_sequence<int, MBW>{});
+        ++t;
     };
-    for (int64_t g = 0; g < G; g += 2) {
-        body(g, std::integral_constant<int, 0>{});
-        if (g + 1 < G) body(g + 1, std::integral_constant<int, 1>{});
+    if constexpr (MBW == 4) {
+        // tile loop around an even K-step loop (the host takes this variant only when ns is even): the epilogue is
+        // outside the K-steps, so the 256 accumulators stay in place in AGPRs across the MFMA chains
+        for (int64_t g = 0; g < G;) {
+            body(g, std::integral_constant<int, 0>{}, std::true_type{});
+            body(g + 1, std::integral_constant<int, 1>{}, std::false_type{});
+            g += 2;
+            for (int s2 = 2; s2 < ns; s2 += 2, g += 2) {
+                body(g, std::integral_constant<int, 0>{}, std::false_type{});
+                body(g + 1, std::integral_constant<int, 1>{}, std::false_type{});
+            }
+            epilogue();
+        }
+    } else {
+        for (int64_t g = 0; g < G; g += 2) {
+            body(g, std::integral_constant<int, 0>{}, std::false_type{});
+            if (++ks == ns) {
+                ks = 0;
+                epilogue();
+            }
+            if (g + 1 < G) {
+                body(g + 1, std::integral_constant<int, 1>{}, std::false_type{});
+                if (++ks == ns) {
+                    ks = 0;
+                    epilogue();
+                }
+            }
+        }
     }
     // no LDS-DMA copy may land after the block's LDS is handed to the next block
     __builtin_amdgcn_s_waitcnt(0xF70u);
-    if (!KEYS && lane < 32 && qlane < nq) cand_n[qlane * nsplit + split] = cntv;
+    if (!KEYS && lane < QW && qlane < nq) cand_n[qlane * nsplit + split] = cntv;
 }
 
 // Candidates of query q, one split per lane: round j offers entry j of splits s0 + lane (64 splits at a time),
@@ -1040,14 +1087,25 @@ void launch_flat_bf16_k64(const void *qimg, const float *qn, int64_t nq, const v
                    "flat_bf16_k64: bad arguments");
     HIPANN_REQUIRE(!qscale == !xscale, "flat_bf16_k64: int8 needs both scales");
     HIPANN_REQUIRE((int64_t)nqt * nsplit < 0x7fffffff, "grid too large");
-    dim3 grid((unsigned)(nqt * nsplit)), block(64 * K64_W);
+    // HIPANN_FLAT_W4=1 (A/B): the int8 passes on the 4-wave, 512-register variant (MBW = 4)
+    static const bool w4 = [] { const char *e = std::getenv("HIPANN_FLAT_W4"); return e && std::atoi(e) != 0; }();
+    const bool use_w4 = w4 && qscale && (nk / 2) % 2 == 0;  // (its tile loop runs K-steps in pairs)
+    dim3 grid((unsigned)(nqt * nsplit)), block(64 * (use_w4 ? K64Geom<4>::W : K64Geom<2>::W));
     const k64_u32x4 *qa = static_cast<const k64_u32x4 *>(qimg);
     const k64_u32x4 *xa = static_cast<const k64_u32x4 *>(ximg);
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, grid, block, K64_LDS, st, qa, qn, nq, xa, xn, N, nk, nqt, nsplit, tiles_per_split,
                            tile_begin, tile_end, bound, cand_d, cand_i, cand_n, cap, resume ? 1 : 0, qscale, xscale);
     };
-    if (qscale) {
+    if (qscale && use_w4) {
+        if (keys) {
+            if (metric == kL2) go(flat_bf16_k64<true, true, true, 4>);
+            else go(flat_bf16_k64<false, true, true, 4>);
+        } else {
+            if (metric == kL2) go(flat_bf16_k64<true, false, true, 4>);
+            else go(flat_bf16_k64<false, false, true, 4>);
+        }
+    } else if (qscale) {
         if (keys) {
             if (metric == kL2) go(flat_bf16_k64<true, true, true>);
             else go(flat_bf16_k64<false, true, true>);
