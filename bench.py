@@ -224,7 +224,10 @@ def build_provenance():
             out["make"] = bi.get("make")
             out["built_at"] = bi.get("built_at")
             out["recorded_sha16"] = bi.get("so_sha16")
-        except ValueError:
+            out["so_is_recorded_build"] = out.get("so_sha16") == bi.get("so_sha16")
+            import __graft_entry__ as ge
+            out["built_from_these_sources"] = bi.get("src_sha16") == ge.sources_sha16()
+        except (ValueError, OSError):
             pass
     return out
 

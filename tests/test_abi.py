@@ -132,3 +132,20 @@ def test_flat_i8_scan_grid_is_whole_blocks(hipann_mod):
         assert nw % 4 == 0 and nw >= 4, (n, nw)
         assert nw <= 2048 and nw >= min(2048, max(1, ngroups // 16)), (n, nw)
     assert f(300_000) == 296
+
+
+def test_shipped_library_is_built_from_these_sources(hipann_mod):
+    """Provenance: libhipann.so is up to date with its sources (`make -q`), and build_info.json, written
+    by __graft_entry__.build(), records this library's hash and the hash of the sources it was built from — bench.py
+    reports both checks in its `build` record."""
+    import hashlib
+    import json
+    import subprocess
+
+    import __graft_entry__ as ge
+    csrc = ROOT / "duckdb-annsearch_amd" / "csrc"
+    assert subprocess.run(["make", "-q", "-C", str(csrc)], stdout=subprocess.DEVNULL,
+                          stderr=subprocess.DEVNULL).returncode == 0, "libhipann.so is older than its sources"
+    bi = json.loads((ROOT / "duckdb-annsearch_amd" / "build_info.json").read_text())
+    assert bi["so_sha16"] == hashlib.sha256(hipann_mod.LIB_PATH.read_bytes()).hexdigest()[:16]
+    assert bi["src_sha16"] == ge.sources_sha16()
