@@ -24,6 +24,7 @@
 #include "runtime.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <cfloat>
 #include <cstring>
 #include <atomic>
@@ -132,9 +133,11 @@ __device__ __forceinline__ float sq8_value(float code, float scale, float mn) {
     return b + mn;
 }
 
-// SQ8: half-wave (32 lanes) per candidate, 16 codes (one uint4) per lane per step.  `ab` holds
-// per-dimension (scale, min) pairs in LDS.  Requires d % 16 == 0 (host checks; otherwise the
-// scalar path below).
+// SQ8: a quarter wave (16 lanes) per candidate, 16 codes (one uint4) per lane per unit, every unit of the lane's
+// share of the row (d <= 2048: up to 8) issued before any is consumed — 96 code loads of 16 B in flight per wave at
+// d 1536, the gather's latency hidden by loads rather than waves.  `ab` holds per-dimension (scale, min) pairs in
+// LDS, loaded once per block; blocks loop over groups of 16 candidates.  Requires d % 16 == 0 and d <= 2048 (host
+// checks; otherwise the scalar path below).
 template <bool IP>
 __global__ void __launch_bounds__(256) dist_ids_sq8(const float *__restrict__ queries, const uint8_t *__restrict__ codes,
                                                     const float2 *__restrict__ ab_g, const unsigned *__restrict__ ids,
@@ -143,35 +146,46 @@ __global__ void __launch_bounds__(256) dist_ids_sq8(const float *__restrict__ qu
     extern __shared__ __attribute__((aligned(16))) float2 ab[];
     for (int j = threadIdx.x; j < d; j += 256) ab[j] = ab_g[j];
     __syncthreads();
-    const int hl = threadIdx.x & 31;
-    const int64_t c = (int64_t)blockIdx.x * 8 + (threadIdx.x >> 5);
-    const unsigned id = c < total_n ? ids[c] : 0xffffffffu;
-    const bool valid = id < n;  // also skips empty slots of the BFS's fixed per-query layout
-    float s = 0.f;
-    if (valid) {
-        const float *q = queries + (int64_t)qmap[c] * d;
-        const uint8_t *row = codes + (int64_t)id * d;
-        for (int j0 = hl * 16; j0 < d; j0 += 32 * 16) {
-            const uint4 raw = *reinterpret_cast<const uint4 *>(row + j0);
-            const unsigned wv[4] = {raw.x, raw.y, raw.z, raw.w};
+    const int ql = threadIdx.x & 15;
+    for (int64_t c0 = (int64_t)blockIdx.x * 16; c0 < total_n; c0 += (int64_t)gridDim.x * 16) {
+        const int64_t c = c0 + (threadIdx.x >> 4);
+        const unsigned id = c < total_n ? ids[c] : 0xffffffffu;
+        const bool valid = id < n;  // also skips empty slots of the BFS's fixed per-query layout
+        float s = 0.f;
+        if (valid) {
+            const float *q = queries + (int64_t)qmap[c] * d;
+            const uint8_t *row = codes + (int64_t)id * d;
+            uint4 raws[8];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float4 qv = *reinterpret_cast<const float4 *>(q + j0 + 4 * e);
-                const float qa[4] = {qv.x, qv.y, qv.z, qv.w};
+            for (int u = 0; u < 8; ++u) {
+                const int j0 = ql * 16 + u * 256;
+                if (j0 < d) raws[u] = *reinterpret_cast<const uint4 *>(row + j0);
+            }
 #pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    const float code = (float)((wv[e] >> (8 * b)) & 0xffu);
-                    const float2 p = ab[j0 + 4 * e + b];
-                    const float v = sq8_value(code, p.x, p.y);
-                    if (IP) s = fmaf(qa[b], v, s);
-                    else { const float t = qa[b] - v; s = fmaf(t, t, s); }
+            for (int u = 0; u < 8; ++u) {
+                const int j0 = ql * 16 + u * 256;
+                if (j0 >= d) break;
+                const uint4 raw = raws[u];
+                const unsigned wv[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float4 qv = *reinterpret_cast<const float4 *>(q + j0 + 4 * e);
+                    const float qa[4] = {qv.x, qv.y, qv.z, qv.w};
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        const float code = (float)((wv[e] >> (8 * b)) & 0xffu);
+                        const float2 p = ab[j0 + 4 * e + b];
+                        const float v = sq8_value(code, p.x, p.y);
+                        if (IP) s = fmaf(qa[b], v, s);
+                        else { const float t = qa[b] - v; s = fmaf(t, t, s); }
+                    }
                 }
             }
         }
-    }
 #pragma unroll
-    for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o);
-    if (valid && hl == 0) out[c] = IP ? -s : s;
+        for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o);
+        if (valid && ql == 0) out[c] = IP ? -s : s;
+    }
 }
 
 template <bool IP>
@@ -290,8 +304,9 @@ void launch_ids(DiskDB &db, const float *q, const unsigned *ids, const unsigned 
     } else {
         const uint8_t *x = db.data.get<uint8_t>();
         const float2 *ab = db.ab_raw.get<float2>();
-        if (d % 16 == 0 && (uintptr_t)q % 16 == 0 && d * sizeof(float2) <= 64 * 1024) {
-            dim3 grid((unsigned)ceil_div(total_n, 8)), block(256);
+        if (d % 16 == 0 && d <= 2048 && (uintptr_t)q % 16 == 0) {
+            // ≤ 8 blocks per CU, each looping over groups of 16 candidates (dist_ids_sq8)
+            dim3 grid((unsigned)std::min<int64_t>(ceil_div(total_n, 16), 2048)), block(256);
             const size_t smem = (size_t)d * sizeof(float2);
             if (metric == kIP) hipLaunchKernelGGL(dist_ids_sq8<true>, grid, block, smem, st, q, x, ab, ids, m, total_n, d, db.n, out);
             else hipLaunchKernelGGL(dist_ids_sq8<false>, grid, block, smem, st, q, x, ab, ids, m, total_n, d, db.n, out);
@@ -349,6 +364,7 @@ struct VisitedSet {
         count = 0;
     }
     static uint32_t hash(uint32_t v) { return (v * 0x9E3779B1u) ^ (v >> 15); }
+    void prefetch(uint32_t v) const { __builtin_prefetch(slot.data() + (hash(v) & mask), 1); }
     // Returns true if v was newly inserted (HashSet::insert).  v == kEmpty is stored out of band.
     bool insert(uint32_t v) {
         if (v == kEmpty) {
@@ -463,7 +479,10 @@ int bfs_threads(int nq) {
 }
 
 int bfs_groups(int nq) {
-    int g = 2;  // HIPANN_BFS_GROUPS=1: the unpipelined loop (A/B)
+    // two pipelined groups: the GPU gathers one group's distances while the host threads run the other's inserts and
+    // expansions (C4 host path, 16 threads: 1 group 34.8K QPS with 9.6 ms of GPU waits per batch, 2 groups 39.9K with
+    // 0.5 ms, profiles/r05/diskann_host_bfs_r05.txt); HIPANN_BFS_GROUPS=1..8 for A/B
+    int g = 2;
     if (const char *e = std::getenv("HIPANN_BFS_GROUPS")) g = std::atoi(e);
     g = std::min(g, std::max(1, nq / 64));  // ≥ 64 queries per group
     return std::max(1, std::min(g, 8));
@@ -505,6 +524,7 @@ void host_bfs(DiskDB *db, const uint32_t *adj, int R, const uint32_t *eps, int n
     uint32_t *hid = db->hids.get<uint32_t>();
     uint32_t *hm = db->hm.get<uint32_t>();
     float *hout = db->hout.get<float>();
+    float *hout_dev = static_cast<float *>(host_device_ptr(hout));
     for (size_t i = 0; i < cap; ++i) hm[i] = (uint32_t)(i / S);
     HIPANN_CHECK(hipMemcpyAsync(db->m.p, hm, cap * 4, hipMemcpyHostToDevice, st));
     std::vector<QState> Sq((size_t)nq);
@@ -538,11 +558,12 @@ void host_bfs(DiskDB *db, const uint32_t *adj, int R, const uint32_t *eps, int n
         const size_t o = (size_t)g.q0 * S, span = (size_t)(last - g.q0) * S;
         HIPANN_CHECK(hipMemcpyAsync(db->ids.get<unsigned>() + o, hid + o, span * 4, hipMemcpyHostToDevice, st));
         {
+            // the distances go straight into the pinned host buffer through its device mapping (posted writes: no
+            // device-to-host copy and its round trip per step)
             ScopedTiming tm(db->timer, st);
             launch_ids(*db, db->q.get<float>(), db->ids.get<unsigned>() + o, db->m.get<unsigned>() + o, (int)span,
-                       metric, db->out.get<float>() + o, st);
+                       metric, hout_dev + o, st);
         }
-        HIPANN_CHECK(hipMemcpyAsync(hout + o, db->out.get<float>() + o, span * 4, hipMemcpyDeviceToHost, st));
         HIPANN_CHECK(hipEventRecord(g.ev, st));
         ncalls++;
         nevals += tot;
@@ -605,19 +626,35 @@ void host_bfs(DiskDB *db, const uint32_t *adj, int R, const uint32_t *eps, int n
                             s.active = false;
                         } else {
                             const uint32_t *nbr = adj + (size_t)c.id * R;
+                            // the row's valid neighbours first, with their visited-set slots prefetched: the set
+                            // (≈ 6K ids, 32-64 KB per query) misses cache on nearly every probe, and 64 overlapped
+                            // misses cost about one
+                            uint32_t nv[256];
                             int cnt = 0;
-                            for (int r = 0; r < R; ++r) {
-                                const uint32_t nb = nbr[r];
-                                if (nb == 0xffffffffu) break;  // get_neighbors trims at the first sentinel
-                                if (nb >= N) continue;
-                                if (!s.visited.insert(nb)) continue;
-                                slot[cnt++] = nb;
+                            bool end = false;
+                            for (int r0 = 0; r0 < R && !end; r0 += 256) {  // (rows wider than 256 in pieces)
+                                int m = 0;
+                                for (int r = r0; r < R && r < r0 + 256; ++r) {
+                                    const uint32_t nb = nbr[r];
+                                    if (nb == 0xffffffffu) {  // get_neighbors trims at the first sentinel
+                                        end = true;
+                                        break;
+                                    }
+                                    if (nb >= N) continue;
+                                    nv[m++] = nb;
+                                    s.visited.prefetch(nb);
+                                }
+                                for (int j = 0; j < m; ++j)
+                                    if (s.visited.insert(nv[j])) slot[cnt++] = nv[j];
                             }
                             s.nnew = cnt;
                         }
                     }
                 }
                 for (int j = s.nnew; j < prev; ++j) slot[j] = 0xffffffffu;
+                // the adjacency row the next pop most likely takes (the heap's top now; the next step's inserts rarely
+                // change it), into cache while the GPU computes this step's distances
+                if (s.active && !s.cands.empty()) __builtin_prefetch(adj + (size_t)s.cands.front().id * R);
             }
             red[(size_t)t * 8] = head;
         });
@@ -626,19 +663,37 @@ void host_bfs(DiskDB *db, const uint32_t *adj, int R, const uint32_t *eps, int n
         for (int t = 0; t < T; ++t) head += red[(size_t)t * 8];
         return head;
     };
+    // HIPANN_BFS_PROF=1 (tuning): host time in the GPU waits, the host phases and the launches, on stderr
+    static const bool prof = std::getenv("HIPANN_BFS_PROF") != nullptr;
+    using clk = std::chrono::steady_clock;
+    double t_wait = 0, t_phase = 0, t_launch = 0;
+    auto since = [](clk::time_point a) { return std::chrono::duration<double, std::micro>(clk::now() - a).count(); };
+    const auto t_all = clk::now();
     for (int live = G; live > 0;) {
         for (auto &g : grp) {
             if (g.done) continue;
+            auto t0 = clk::now();
             if (g.launched) HIPANN_CHECK(hipEventSynchronize(g.ev));
-            if (!phase(g)) {
+            auto t1 = clk::now();
+            const int64_t head = phase(g);
+            auto t2 = clk::now();
+            if (prof) {
+                t_wait += std::chrono::duration<double, std::micro>(t1 - t0).count();
+                t_phase += std::chrono::duration<double, std::micro>(t2 - t1).count();
+            }
+            if (!head) {
                 g.done = true;
                 --live;
                 continue;
             }
             g.steps++;
             launch(g);  // (nothing when no query of the group expanded new neighbours)
+            if (prof) t_launch += since(t2);
         }
     }
+    if (prof)
+        std::fprintf(stderr, "hipann bfs: nq %d groups %d threads %d calls %lld: total %.0f us, waits %.0f, phases %.0f, "
+                             "launches %.0f\n", nq, G, T, (long long)ncalls, since(t_all), t_wait, t_phase, t_launch);
     for (auto &g : grp) nsteps = std::max(nsteps, g.steps);
     for (int qi = 0; qi < nq; ++qi) {
         const auto &r = Sq[qi].result;
