@@ -172,7 +172,8 @@ def compact_line(full):
         line["nq1_ms"] = (full["latency"].get("nq1") or {}).get("ms_per_call")
     if isinstance(full.get("append"), dict):
         a = full["append"]
-        line["append2048"] = {k: a.get(k) for k in ("append_ms", "append_plus_search_ms", "vs_search_step")}
+        line["append2048"] = {k: a.get(k) for k in ("append_ms", "append_plus_search_ms", "vs_search_step",
+                                                     "vs_search_from_idle")}
     fb = (full.get("ivf") or {}).get("rerank_fallbacks_total", full.get("rerank_fallbacks_total"))
     if fb is not None:
         line["rerank_fallbacks"] = fb
@@ -891,6 +892,13 @@ def ivf_append_line(torch, index, xq, k, d, r_dim, eta, base_ms, rows=2048, reps
     search = lambda: index.search_device(nq, xq.data_ptr(), k, D.data_ptr(), I.data_ptr(), stream)  # noqa: E731
     n_before = index.ntotal
     torch.cuda.synchronize()
+    t_idle = 0.0  # the same search from an idle GPU (its launch latency exposed, as after an append)
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        search()
+        torch.cuda.synchronize()
+        t_idle += time.perf_counter() - t0
+    idle_ms = t_idle * 1e3 / reps
     t0 = time.perf_counter()
     index.add(new_h[:rows])
     first_ms = (time.perf_counter() - t0) * 1e3
@@ -910,6 +918,7 @@ def ivf_append_line(torch, index, xq, k, d, r_dim, eta, base_ms, rows=2048, reps
     return {"workload": f"hipann_ivf_add of {rows} host rows + the next {nq}-query search, {reps} times",
             "append_ms": round(t_add * 1e3 / reps, 3), "append_plus_search_ms": round(pair_ms, 3),
             "search_step_ms": round(base_ms, 3), "vs_search_step": round(pair_ms / base_ms, 3) if base_ms > 0 else None,
+            "search_from_idle_ms": round(idle_ms, 3), "vs_search_from_idle": round(pair_ms / idle_ms, 3) if idle_ms > 0 else None,
             "first_append_ms": round(first_ms, 1),
             "first_append_note": "moves the borrowed CSR into owned lists with slack (once)",
             "ntotal": [n_before, index.ntotal], "rows_per_s": round(rows * reps / t_add, 1) if t_add > 0 else None}
