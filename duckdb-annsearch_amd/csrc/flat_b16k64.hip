@@ -35,6 +35,11 @@ typedef unsigned k64_u32x4 __attribute__((ext_vector_type(4)));
 typedef int k64_i32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void k64_lds_void;
 
+// Tuning builds only (timing ablations, wrong results): bit 0 drops the database-tile DMA, bit 1 the query-fragment
+// loads, bit 2 the epilogue's candidate filter, bit 3 the per-K-step barrier.  Product builds: 0.
+#ifndef HIPANN_K64_ABLATE
+#define HIPANN_K64_ABLATE 0
+#endif
 constexpr int K64_TN = 256;               // database rows per tile
 constexpr int K64_QM = 256;               // queries per block (8 waves × 32, or 4 waves × 64)
 constexpr int K64_W = 8;                  // waves per block of the 2-row-block (MBW = 2) variant
@@ -198,6 +203,7 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
     k64_u32x4 ar[2][2][MBW];  // [ring slot][chunk of the K-step][mb]
     auto issue_a = [&](auto slot_c) {
         constexpr int SL = decltype(slot_c)::value;
+        if constexpr ((HIPANN_K64_ABLATE & 2) != 0) return;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int64_t kc = 2 * ks_a + h;
@@ -207,6 +213,7 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
         ks_a = ks_a + 1 < ns ? ks_a + 1 : 0;
     };
     auto issue_b = [&](int64_t g, int stage) {
+        if constexpr ((HIPANN_K64_ABLATE & 1) != 0) return;
         k64_u32x4 *dst = smem_k64 + stage * K64_SU;
 #pragma unroll
         for (int i = 0; i < PIECES; ++i) {
@@ -260,7 +267,7 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
         constexpr bool FIRST = decltype(first_c)::value;
         // K-step g landed (the wait at the end of the previous K-step), every wave done reading the stage about to
         // be refilled (g−2's): one barrier
-        __builtin_amdgcn_s_barrier();
+        if constexpr ((HIPANN_K64_ABLATE & 8) == 0) __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         // the tile's ‖x‖² for the epilogue (xnorm is deliberately not __restrict__: a read-only noalias argument's
         // loads get sunk into the epilogue's block, where the wait for them is a vmcnt(0))
@@ -369,6 +376,8 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
                         if (q < nq && x < N) cand_d[q * N + x] = key;
                     }
                 }
+            } else if constexpr ((HIPANN_K64_ABLATE & 4) != 0) {
+                cntv += sm[0][0] > 1e30f ? 1 : 0;  // (keeps the conversion live)
             } else {
                 k64_epilogue_row<L2M, MB, 0>(sm, cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
                 k64_epilogue_row<L2M, MB, 1>(sm, cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
