@@ -33,10 +33,12 @@ typedef __bf16 k64_b16x8 __attribute__((ext_vector_type(8)));
 typedef float k64_f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned k64_u32x4 __attribute__((ext_vector_type(4)));
 typedef int k64_i32x4 __attribute__((ext_vector_type(4)));
+typedef float k64_f32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) void k64_lds_void;
 
 // Tuning builds only (timing ablations, wrong results): bit 0 drops the database-tile DMA, bit 1 the query-fragment
-// loads, bit 2 the epilogue's candidate filter, bit 3 the per-K-step barrier.  Product builds: 0.
+// loads, bit 2 the epilogue's candidate filter, bit 3 the per-K-step barrier, bit 4 the filter's append path (the
+// compare and ballot kept).  Product builds: 0.
 #ifndef HIPANN_K64_ABLATE
 #define HIPANN_K64_ABLATE 0
 #endif
@@ -64,15 +66,18 @@ template <int MBW> struct K64Geom {
 // (L2, clamped at 0) or −s/2 = −q·x (IP); cntv lane j holds the count of the wave's query j (it keeps
 // counting past cap: flat_cand_select flags an overflowed query for the exact fallback).
 template <bool L2M, int MB, int I>
-__device__ __forceinline__ void k64_epilogue_row(const k64_f32x4 (&sm)[16], const float (&cthm)[4], float qnl,
+__device__ __forceinline__ void k64_epilogue_row(const k64_f32x4 (&sm)[16], float mxi, const float (&cthm)[4], float qnl,
                                                  int &cntv, int64_t x0, float *__restrict__ cand_d,
                                                  int *__restrict__ cand_i, int64_t cbase, int64_t cq, int cap,
                                                  int lane) {
-    bool any = false;
-#pragma unroll
-    for (int jb = 0; jb < 16; ++jb) any |= sm[jb][I] >= cthm[I];
-    const unsigned long long m = __ballot(any);
+    // mxi = max over the lane's 16 rows of sm[·][I] (the caller's reduction): one compare for the 16 (NaN never
+    // passes: fmaxf drops NaN operands, an all-NaN max compares false)
+    const unsigned long long m = __ballot(mxi >= cthm[I]);
     if (m == 0ull) return;
+    if constexpr ((HIPANN_K64_ABLATE & 16) != 0) {  // (tuning: the slow path's cost, not its work)
+        cntv += __popcll(m);
+        return;
+    }
     // the lane's passing columns (bit jb)
     unsigned pm = 0;
 #pragma unroll
@@ -269,9 +274,12 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
         // be refilled (g−2's): one barrier
         if constexpr ((HIPANN_K64_ABLATE & 8) == 0) __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        // the tile's ‖x‖² for the epilogue (xnorm is deliberately not __restrict__: a read-only noalias argument's
-        // loads get sunk into the epilogue's block, where the wait for them is a vmcnt(0))
-        load_xn(t);
+        // the tile's ‖x‖² (and int8 row scales) for the epilogue, in its last K-step only — one K-step ahead of the
+        // use, 8 vector-memory ops per tile instead of per K-step (xnorm is deliberately not __restrict__: a
+        // read-only noalias argument's loads get sunk into the epilogue's block, where the wait for them is a
+        // vmcnt(0)).  Issued first in the K-step, they are older than B(g+3), which the end-of-K-step wait's count
+        // assumes.
+        if (g % ns == ns - 1) load_xn(t);
         __builtin_amdgcn_sched_barrier(0);
         const k64_u32x4 *Bb = smem_k64 + stage * K64_SU;
 #pragma unroll
@@ -348,10 +356,17 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
                 if constexpr (I8) {
                     // whole-vector reinterpret + convert: per-element extracts of the bit-cast i32 MFMA result were
                     // miscompiled (only element 0 of each accumulator was read; the others came from stale
-                    // registers — found by the form's parity tests, every query with index % 4 != 0 wrong)
+                    // registers — found by the form's parity tests, every query with index % 4 != 0 wrong).
+                    // s = (s_q·s_x)·acc − ‖x‖² on packed fp32 pairs (v_pk_mul_f32 / v_pk_fma_f32: the same two
+                    // roundings as the scalar form, half the VALU issue; every wave runs this epilogue at the same
+                    // barrier-aligned moment, so its VALU time adds to the tile's)
                     const k64_f32x4 v = __builtin_convertvector(acc[MB][jb], k64_f32x4);
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) sm[jb][i] = fmaf(csq[MB][i] * sxj[jb], v[i], -xvj[jb]);
+                    const k64_f32x2 sxx = {sxj[jb], sxj[jb]}, nxv = {-xvj[jb], -xvj[jb]};
+                    const k64_f32x2 a01 = (k64_f32x2){csq[MB][0], csq[MB][1]} * sxx;
+                    const k64_f32x2 a23 = (k64_f32x2){csq[MB][2], csq[MB][3]} * sxx;
+                    const k64_f32x2 s01 = __builtin_elementwise_fma(a01, (k64_f32x2){v[0], v[1]}, nxv);
+                    const k64_f32x2 s23 = __builtin_elementwise_fma(a23, (k64_f32x2){v[2], v[3]}, nxv);
+                    sm[jb] = (k64_f32x4){s01[0], s01[1], s23[0], s23[1]};
                 } else {
 #pragma unroll
                     for (int i = 0; i < 4; ++i) sm[jb][i] = fmaf(2.f, acc[MB][jb][i], -xvj[jb]);
@@ -379,10 +394,14 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
             } else if constexpr ((HIPANN_K64_ABLATE & 4) != 0) {
                 cntv += sm[0][0] > 1e30f ? 1 : 0;  // (keeps the conversion live)
             } else {
-                k64_epilogue_row<L2M, MB, 0>(sm, cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
-                k64_epilogue_row<L2M, MB, 1>(sm, cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
-                k64_epilogue_row<L2M, MB, 2>(sm, cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
-                k64_epilogue_row<L2M, MB, 3>(sm, cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
+                // the lane's largest s per accumulator row (the filter's one compare per row); NaN-dropping max
+                k64_f32x4 mx = sm[0];
+#pragma unroll
+                for (int jb = 1; jb < 16; ++jb) mx = __builtin_elementwise_max(mx, sm[jb]);
+                k64_epilogue_row<L2M, MB, 0>(sm, mx[0], cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
+                k64_epilogue_row<L2M, MB, 1>(sm, mx[1], cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
+                k64_epilogue_row<L2M, MB, 2>(sm, mx[2], cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
+                k64_epilogue_row<L2M, MB, 3>(sm, mx[3], cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
             }
         };
         [&]<int... M>(std::integer_sequence<int, M...>) {
