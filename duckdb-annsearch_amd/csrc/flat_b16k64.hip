@@ -38,13 +38,12 @@ typedef __attribute__((address_space(3))) void k64_lds_void;
 
 // Tuning builds only (timing ablations, wrong results): bit 0 drops the database-tile DMA, bit 1 the query-fragment
 // loads, bit 2 the epilogue's candidate filter, bit 3 the per-K-step barrier, bit 4 the filter's append path (the
-// compare and ballot kept).  Product builds: 0.
+// compare and ballot kept), bit 5 the per-query scales (one per tile), bit 6 the accumulator reset.  Product builds: 0.
 #ifndef HIPANN_K64_ABLATE
 #define HIPANN_K64_ABLATE 0
 #endif
 constexpr int K64_TN = 256;               // database rows per tile
 constexpr int K64_QM = 256;               // queries per block (8 waves × 32, or 4 waves × 64)
-constexpr int K64_W = 8;                  // waves per block of the 2-row-block (MBW = 2) variant
 constexpr int K64_NB = 5;                 // LDS stages: g read, g+1 .. g+3 landing / in flight
 constexpr int K64_BU = K64_TN * 4;        // 16-B units of one 32-dim chunk of a database tile
 constexpr int K64_SU = 2 * K64_BU;        // units per stage (one 64-dim K-step): 32 KB
@@ -65,23 +64,24 @@ template <int MBW> struct K64Geom {
 // 16-lane group).  Passing rows (rare) are appended to the query's buffer with key = ‖q‖² − s
 // (L2, clamped at 0) or −s/2 = −q·x (IP); cntv lane j holds the count of the wave's query j (it keeps
 // counting past cap: flat_cand_select flags an overflowed query for the exact fallback).
-template <bool L2M, int MB, int I>
-__device__ __forceinline__ void k64_epilogue_row(const k64_f32x4 (&sm)[16], float mxi, const float (&cthm)[4], float qnl,
+template <bool L2M, int MB, int I, int JB0>
+__device__ __forceinline__ void k64_epilogue_row(const k64_f32x4 (&sm)[8], float mxi, const float (&cthm)[4], float qnl,
                                                  int &cntv, int64_t x0, float *__restrict__ cand_d,
                                                  int *__restrict__ cand_i, int64_t cbase, int64_t cq, int cap,
                                                  int lane) {
-    // mxi = max over the lane's 16 rows of sm[·][I] (the caller's reduction): one compare for the 16 (NaN never
-    // passes: fmaxf drops NaN operands, an all-NaN max compares false)
+    // sm[j] = s of row block JB0 + j (one half of the tile's 16; the halves keep the epilogue's live registers to 32
+    // values).  mxi = max over the lane's 8 rows of sm[·][I] (the caller's reduction): one compare for the 8 (NaN
+    // never passes: fmaxf drops NaN operands, an all-NaN max compares false)
     const unsigned long long m = __ballot(mxi >= cthm[I]);
     if (m == 0ull) return;
     if constexpr ((HIPANN_K64_ABLATE & 16) != 0) {  // (tuning: the slow path's cost, not its work)
         cntv += __popcll(m);
         return;
     }
-    // the lane's passing columns (bit jb)
+    // the lane's passing columns (bit j: row block JB0 + j)
     unsigned pm = 0;
 #pragma unroll
-    for (int jb = 0; jb < 16; ++jb) pm |= sm[jb][I] >= cthm[I] ? 1u << jb : 0u;
+    for (int j = 0; j < 8; ++j) pm |= sm[j][I] >= cthm[I] ? 1u << j : 0u;
 #pragma unroll 1
     for (int fq = 0; fq < 4; ++fq) {
         unsigned grp = (unsigned)(m >> (16 * fq)) & 0xffffu;  // lanes of query fq holding a passing row
@@ -97,11 +97,12 @@ __device__ __forceinline__ void k64_epilogue_row(const k64_f32x4 (&sm)[16], floa
             const int src = 16 * fq + l;
             unsigned pml = (unsigned)__builtin_amdgcn_readlane((int)pm, src);
             while (pml) {
-                const int jb = __ffs(pml) - 1;
+                const int jl = __ffs(pml) - 1;
                 pml &= pml - 1;
+                const int jb = JB0 + jl;
                 float sv = sm[0][I];
 #pragma unroll
-                for (int j = 1; j < 16; ++j) sv = jb == j ? sm[j][I] : sv;
+                for (int j = 1; j < 8; ++j) sv = jl == j ? sm[j][I] : sv;
                 sv = readlane_f(sv, src);
                 float key;
                 if (L2M) {
@@ -133,7 +134,7 @@ __device__ __forceinline__ void k64_epilogue_row(const k64_f32x4 (&sm)[16], floa
 // accumulators' registers bit for bit until the tile's epilogue turns them into q·x = acc·s_q·s_x with the
 // per-query / per-row scales (qscale / xscale); everything after that is the bf16 path's.
 template <bool L2M, bool KEYS, bool I8 = false, int MBW = 2>
-__global__ void __launch_bounds__(64 * K64Geom<MBW>::W, 1) __attribute__((amdgpu_waves_per_eu(1, MBW == 4 ? 1 : 2)))
+__global__ void __launch_bounds__(64 * K64Geom<MBW>::W, 1) __attribute__((amdgpu_waves_per_eu(1, 2)))
 flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm, int64_t nq,
               const k64_u32x4 *__restrict__ Xt, const float *xnorm, int64_t N, int nk, int nqt, int nsplit,
               int64_t tiles_per_split, int64_t tile_begin, int64_t tile_end, const float *__restrict__ bound,
@@ -202,10 +203,10 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
     int qrow[MBW];
 #pragma unroll
     for (int mb = 0; mb < MBW; ++mb) qrow[mb] = (QW * wave + 16 * mb + m16) ^ (g4 << 1);
-    // query fragments: a 2-slot register ring (K-step g+1's loaded while g is computed); the loop is unrolled by
-    // two so the slot is a compile-time index
-    int ks_a = 0;
-    k64_u32x4 ar[2][2][MBW];  // [ring slot][chunk of the K-step][mb]
+    // query fragments: a 3-slot register ring (K-step g+2's loaded while g is computed); the loop is unrolled by
+    // three so the slot is a compile-time index
+    int ks_a = 0;             // K-step (within the tile) of the next fragments issued
+    k64_u32x4 ar[3][2][MBW];  // [ring slot][chunk of the K-step][mb]
     auto issue_a = [&](auto slot_c) {
         constexpr int SL = decltype(slot_c)::value;
         if constexpr ((HIPANN_K64_ABLATE & 2) != 0) return;
@@ -246,49 +247,55 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
             if constexpr (I8) xsc[j] = xscale[x < N ? x : N - 1];
         }
     };
-    // Per K-step g the vector-memory ops go out as ‖x‖²(g) (L2), A(g+1), B(g+3); at its end A(g+1) and B(g+1)
-    // must have landed and only B(g+3) is younger than A(g+1): vmcnt(4).  Loads retire
-    // in issue order, so the tile pieces lead by three K-steps (HBM misses) and the query fragments by one (L2
-    // hits) without either wait covering the other.  The waits are the builtin (s_waitcnt vmcnt(4) expcnt(7)
-    // lgkmcnt(15)), not inline asm: the compiler's wait pass must see them.
-    constexpr unsigned kWaitStep = 0xF70u | PIECES;
-    static_assert(PIECES < 16, "vmcnt low field");
+    constexpr int NXN = (L2M ? 4 : 0) + (I8 ? 4 : 0);  // load_xn's vector-memory ops
+    // Per K-step g the vector-memory ops go out as A(g+2) (chunk 0) and B(g+3) (end of chunk 1); at its end A(g+1)
+    // and B(g+1) must have landed, and B(g+2), A(g+2), B(g+3) — the three youngest groups — may stay in flight:
+    // vmcnt(2·PIECES + 2·MBW).  Loads retire in issue order, so the query fragments must be issued before B(g+2)
+    // for the wait not to cover it: with a one-K-step fragment lead (A(g+1) issued in K-step g, after B(g+2)) the
+    // wait for A(g+1) also waited for B(g+2), and the tile pieces led by one K-step, not two.  The tile's ‖x‖² and
+    // scales (NXN loads) go out at the start of K-step ns − 2 (its wait allows them in flight too; the epilogue's own
+    // wait for them, two K-steps later, covers nothing younger than they are that is still needed).  The waits are the
+    // builtin (s_waitcnt vmcnt(n) expcnt(7) lgkmcnt(15)), not inline asm: the compiler's wait pass must see them.
+    constexpr int NA = (HIPANN_K64_ABLATE & 2) != 0 ? 0 : 2 * MBW;
+    constexpr int NB_OPS = (HIPANN_K64_ABLATE & 1) != 0 ? 0 : PIECES;
+    constexpr int kVm = 2 * NB_OPS + NA, kVmXn = kVm + NXN;
+    static_assert(kVmXn < 64, "vmcnt field");
+    constexpr unsigned kWaitStep = 0xF70u | (kVm & 15) | ((kVm >> 4) << 14);
+    constexpr unsigned kWaitStepXn = 0xF70u | (kVmXn & 15) | ((kVmXn >> 4) << 14);
     auto clampg = [&](int64_t g) { return g < G ? g : G - 1; };  // past the end: the last K-step again, never read
     if (G > 0) {
-        // the steady state's order: B(0), B(1), A(0), B(2)
+        // the steady state's order: B(0), A(0), B(1), A(1), B(2)
         issue_b(0, 0);
-        issue_b(clampg(1), 1);
         issue_a(std::integral_constant<int, 0>{});
+        issue_b(clampg(1), 1);
+        issue_a(std::integral_constant<int, 1>{});
         issue_b(clampg(2), 2);
     }
-    __builtin_amdgcn_s_waitcnt(kWaitStep);  // B(0), B(1), A(0) landed (B(2) in flight)
+    __builtin_amdgcn_s_waitcnt(kWaitStep);  // B(0), A(0) landed (B(1), A(1), B(2) in flight)
 
     int ks = 0, stage = 0;
     int64_t t = t0;
-    // FIRST (the 4-wave variant's first K-step of a tile): the chunk-0 MFMAs start from a zero C operand instead of
-    // the accumulators, so the accumulator chains never pass through an explicit reset
-    auto body = [&](int64_t g, auto slot_c, auto first_c) {
+    const int ks_xn = ns >= 2 ? ns - 2 : 0;  // the K-step (within a tile) that issues the tile's ‖x‖² / scales
+    auto body = [&](int64_t g, auto slot_c) __attribute__((always_inline)) {
         constexpr int SL = decltype(slot_c)::value;
-        constexpr bool FIRST = decltype(first_c)::value;
+        const bool xn = ks == ks_xn;  // wave-uniform
         // K-step g landed (the wait at the end of the previous K-step), every wave done reading the stage about to
         // be refilled (g−2's): one barrier
         if constexpr ((HIPANN_K64_ABLATE & 8) == 0) __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        // the tile's ‖x‖² (and int8 row scales) for the epilogue, in its last K-step only — one K-step ahead of the
-        // use, 8 vector-memory ops per tile instead of per K-step (xnorm is deliberately not __restrict__: a
-        // read-only noalias argument's loads get sunk into the epilogue's block, where the wait for them is a
-        // vmcnt(0)).  Issued first in the K-step, they are older than B(g+3), which the end-of-K-step wait's count
-        // assumes.
-        if (g % ns == ns - 1) load_xn(t);
+        // the tile's ‖x‖² (and int8 row scales) for the epilogue, once per tile (xnorm is deliberately not
+        // __restrict__: a read-only noalias argument's loads get sunk into the epilogue's block, where the wait for
+        // them is a vmcnt(0))
+        if (xn) load_xn(t);
         __builtin_amdgcn_sched_barrier(0);
         const k64_u32x4 *Bb = smem_k64 + stage * K64_SU;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            // A(g+1) spread over chunk 0's MFMAs, B(g+3) over chunk 1's last eight, after the K-step's last LDS
+            // A(g+2) spread over chunk 0's MFMAs, B(g+3) over chunk 1's last eight, after the K-step's last LDS
             // read (the compiler keeps LDS reads behind an LDS-DMA in program order).  Issued together after the
             // barrier instead, the eight vector-memory ops of all eight waves queue at once and hold back the
             // MFMAs (17.4 vs 16.6 ms with one K-step in flight).
-            if (h == 0) issue_a(std::integral_constant<int, 1 - SL>{});
+            if (h == 0) issue_a(std::integral_constant<int, (SL + 2) % 3>{});
             // B fragment of rows 16·jb + m16, unit c = g4: slot c·256 + 16·jb + (m16 ^ 2c)
             const k64_u32x4 *Bc = Bb + h * K64_BU + g4 * K64_TN + (m16 ^ (g4 << 1));
             k64_b16x8 bf[16];
@@ -298,16 +305,13 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
             for (int jb = 0; jb < 16; ++jb) {
 #pragma unroll
                 for (int mb = 0; mb < MBW; ++mb) {
-                    const bool zc = FIRST && h == 0;  // (constant once unrolled)
                     if constexpr (I8) {  // int32 sums carried in the accumulators' registers, bit for bit
                         const k64_i32x4 ai = __builtin_bit_cast(k64_i32x4, ar[SL][h][mb]);
                         const k64_i32x4 bi = __builtin_bit_cast(k64_i32x4, bf[jb]);
-                        acc[mb][jb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ai, bi, zc ? (AccT){0, 0, 0, 0} : acc[mb][jb], 0,
-                                                                             0, 0);
+                        acc[mb][jb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ai, bi, acc[mb][jb], 0, 0, 0);
                     } else {
                         acc[mb][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(k64_b16x8, ar[SL][h][mb]),
-                                                                              bf[jb], zc ? (AccT){0, 0, 0, 0} : acc[mb][jb],
-                                                                              0, 0, 0);
+                                                                              bf[jb], acc[mb][jb], 0, 0, 0);
                     }
                 }
             }
@@ -326,117 +330,114 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
                     __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
                 }
             }
-            // chunk fence: A(g+1) stays in chunk 0, B(g+3) at the end of chunk 1 (their order is what the counted
+            // chunk fence: A(g+2) stays in chunk 0, B(g+3) at the end of chunk 1 (their order is what the counted
             // wait assumes)
             __builtin_amdgcn_sched_barrier(0);
         }
-        // A(g+1), B(g+1) landed; B(g+2), B(g+3) stay in flight
-        __builtin_amdgcn_s_waitcnt(kWaitStep);
+        // A(g+1), B(g+1) landed; B(g+2), A(g+2), B(g+3) (and this K-step's ‖x‖² / scales) stay in flight
+        if (xn) __builtin_amdgcn_s_waitcnt(kWaitStepXn);
+        else __builtin_amdgcn_s_waitcnt(kWaitStep);
         stage = stage + 1 < NB ? stage + 1 : 0;
     };
     // the tile's epilogue (after its last K-step)
-    auto epilogue = [&]() {
+    auto epilogue = [&]() __attribute__((always_inline)) {
         const int64_t x0 = t * K64_TN;
         // s = 2·q·x − ‖x‖² (the filter's left side; the key follows from it with one more rounding, inside the
-        // rerank bound's (d + 8)·2⁻²⁴ term); xr: row 64·j + l in lane l's xr[j].  One 16-query row block at a
-        // time: its accumulators move to VGPRs (s), are filtered and reset before the next block's — with MBW = 4
-        // the 256 accumulators stay in AGPRs and only 64 values are live in VGPRs.
-        float xvj[16], sxj[16];
+        // rerank bound's (d + 8)·2⁻²⁴ term); xr: row 64·j + l in lane l's xr[j].  Eight row blocks at a time (two
+        // halves), each 16-query row block's accumulators converted, filtered and reset before the next: 32 values
+        // and 16 row terms live besides the accumulators.
 #pragma unroll
-        for (int jb = 0; jb < 16; ++jb) {
-            const float xs = __shfl(xr[jb >> 2], 16 * (jb & 3) + m16);
-            xvj[jb] = x0 + 16 * jb + m16 < N ? xs : __builtin_inff();
-            sxj[jb] = I8 ? __shfl(xsc[jb >> 2], 16 * (jb & 3) + m16) : 1.f;
-        }
-        auto tile_mb = [&](auto mb_c) {
-            constexpr int MB = decltype(mb_c)::value;
-            k64_f32x4 sm[16];
+        for (int hf = 0; hf < 2; ++hf) {
+            float xvj[8], sxj[8];
 #pragma unroll
-            for (int jb = 0; jb < 16; ++jb) {
-                if constexpr (I8) {
-                    // whole-vector reinterpret + convert: per-element extracts of the bit-cast i32 MFMA result were
-                    // miscompiled (only element 0 of each accumulator was read; the others came from stale
-                    // registers — found by the form's parity tests, every query with index % 4 != 0 wrong).
-                    // s = (s_q·s_x)·acc − ‖x‖² on packed fp32 pairs (v_pk_mul_f32 / v_pk_fma_f32: the same two
-                    // roundings as the scalar form, half the VALU issue; every wave runs this epilogue at the same
-                    // barrier-aligned moment, so its VALU time adds to the tile's)
-                    const k64_f32x4 v = __builtin_convertvector(acc[MB][jb], k64_f32x4);
-                    const k64_f32x2 sxx = {sxj[jb], sxj[jb]}, nxv = {-xvj[jb], -xvj[jb]};
-                    const k64_f32x2 a01 = (k64_f32x2){csq[MB][0], csq[MB][1]} * sxx;
-                    const k64_f32x2 a23 = (k64_f32x2){csq[MB][2], csq[MB][3]} * sxx;
-                    const k64_f32x2 s01 = __builtin_elementwise_fma(a01, (k64_f32x2){v[0], v[1]}, nxv);
-                    const k64_f32x2 s23 = __builtin_elementwise_fma(a23, (k64_f32x2){v[2], v[3]}, nxv);
-                    sm[jb] = (k64_f32x4){s01[0], s01[1], s23[0], s23[1]};
-                } else {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) sm[jb][i] = fmaf(2.f, acc[MB][jb][i], -xvj[jb]);
-                }
-                if constexpr (MBW != 4) acc[MB][jb] = (AccT){0, 0, 0, 0};  // (4: the FIRST K-steps start from 0)
+            for (int j = 0; j < 8; ++j) {
+                const int jb = 8 * hf + j;
+                const float xs = __shfl(xr[jb >> 2], 16 * (jb & 3) + m16);
+                xvj[j] = x0 + 16 * jb + m16 < N ? xs : __builtin_inff();
+                sxj[j] = I8 ? __shfl(xsc[jb >> 2], 16 * (jb & 3) + m16) : 1.f;
             }
-            if constexpr (KEYS) {
-                // every key (L2: ‖q‖² − s clamped at 0; IP: −s/2) into the dense key matrix
+            auto tile_mb = [&](auto mb_c) __attribute__((always_inline)) {
+                constexpr int MB = decltype(mb_c)::value;
+                k64_f32x4 sm[8];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int64_t q = q0w + 16 * MB + i;
+                for (int j = 0; j < 8; ++j) {
+                    const int jb = 8 * hf + j;
+                    if constexpr (I8) {
+                        // whole-vector reinterpret + convert: per-element extracts of the bit-cast i32 MFMA result
+                        // were miscompiled (only element 0 of each accumulator was read; the others came from stale
+                        // registers — found by the form's parity tests, every query with index % 4 != 0 wrong).
+                        // Scalar fp32 (packed v_pk_mul/fma pairs pushed the kernel past 256 registers: spills,
+                        // 8.26 vs 7.71 ms at 10M)
+                        const k64_f32x4 v = __builtin_convertvector(acc[MB][jb], k64_f32x4);
+                        if constexpr ((HIPANN_K64_ABLATE & 32) != 0) {  // (tuning: one query scale per tile)
+                            const float cj = csq[0][0] * sxj[j];
 #pragma unroll
-                    for (int jb = 0; jb < 16; ++jb) {
-                        const int64_t x = x0 + 16 * jb + m16;
-                        float key;
-                        if (L2M) {
-                            key = cth[MB][i] - sm[jb][i];
-                            key = key < 0.f ? 0.f : key;
+                            for (int i = 0; i < 4; ++i) sm[j][i] = fmaf(cj, v[i], -xvj[j]);
                         } else {
-                            key = -0.5f * sm[jb][i];
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) sm[j][i] = fmaf(csq[MB][i] * sxj[j], v[i], -xvj[j]);
                         }
-                        if (q < nq && x < N) cand_d[q * N + x] = key;
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) sm[j][i] = fmaf(2.f, acc[MB][jb][i], -xvj[j]);
+                    }
+                    if constexpr ((HIPANN_K64_ABLATE & 64) == 0) acc[MB][jb] = (AccT){0, 0, 0, 0};  // (64: tuning)
+                }
+                if constexpr (KEYS) {
+                    // every key (L2: ‖q‖² − s clamped at 0; IP: −s/2) into the dense key matrix
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int64_t q = q0w + 16 * MB + i;
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) {
+                            const int64_t x = x0 + 16 * (8 * hf + j) + m16;
+                            float key;
+                            if (L2M) {
+                                key = cth[MB][i] - sm[j][i];
+                                key = key < 0.f ? 0.f : key;
+                            } else {
+                                key = -0.5f * sm[j][i];
+                            }
+                            if (q < nq && x < N) cand_d[q * N + x] = key;
+                        }
+                    }
+                } else if constexpr ((HIPANN_K64_ABLATE & 4) != 0) {
+                    cntv += sm[0][0] > 1e30f ? 1 : 0;  // (keeps the conversion live)
+                } else {
+                    // the lane's largest s per accumulator row (the filter's one compare per row); NaN-dropping max
+                    k64_f32x4 mx = sm[0];
+#pragma unroll
+                    for (int j = 1; j < 8; ++j) mx = __builtin_elementwise_max(mx, sm[j]);
+                    if (hf == 0) {
+                        k64_epilogue_row<L2M, MB, 0, 0>(sm, mx[0], cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
+                        k64_epilogue_row<L2M, MB, 1, 0>(sm, mx[1], cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
+                        k64_epilogue_row<L2M, MB, 2, 0>(sm, mx[2], cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
+                        k64_epilogue_row<L2M, MB, 3, 0>(sm, mx[3], cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
+                    } else {
+                        k64_epilogue_row<L2M, MB, 0, 8>(sm, mx[0], cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
+                        k64_epilogue_row<L2M, MB, 1, 8>(sm, mx[1], cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
+                        k64_epilogue_row<L2M, MB, 2, 8>(sm, mx[2], cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
+                        k64_epilogue_row<L2M, MB, 3, 8>(sm, mx[3], cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
                     }
                 }
-            } else if constexpr ((HIPANN_K64_ABLATE & 4) != 0) {
-                cntv += sm[0][0] > 1e30f ? 1 : 0;  // (keeps the conversion live)
-            } else {
-                // the lane's largest s per accumulator row (the filter's one compare per row); NaN-dropping max
-                k64_f32x4 mx = sm[0];
-#pragma unroll
-                for (int jb = 1; jb < 16; ++jb) mx = __builtin_elementwise_max(mx, sm[jb]);
-                k64_epilogue_row<L2M, MB, 0>(sm, mx[0], cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
-                k64_epilogue_row<L2M, MB, 1>(sm, mx[1], cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
-                k64_epilogue_row<L2M, MB, 2>(sm, mx[2], cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
-                k64_epilogue_row<L2M, MB, 3>(sm, mx[3], cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
-            }
-        };
-        [&]<int... M>(std::integer_sequence<int, M...>) {
-            (tile_mb(std::integral_constant<int, M>{}), ...);
-        }(std::make_integer_sequence<int, MBW>{});
+            };
+            [&]<int... M>(std::integer_sequence<int, M...>) {
+                (tile_mb(std::integral_constant<int, M>{}), ...);
+            }(std::make_integer_sequence<int, MBW>{});
+        }
         ++t;
     };
-    if constexpr (MBW == 4) {
-        // tile loop around an even K-step loop (the host takes this variant only when ns is even): the epilogue is
-        // outside the K-steps, so the 256 accumulators stay in place in AGPRs across the MFMA chains
-        for (int64_t g = 0; g < G;) {
-            body(g, std::integral_constant<int, 0>{}, std::true_type{});
-            body(g + 1, std::integral_constant<int, 1>{}, std::false_type{});
-            g += 2;
-            for (int s2 = 2; s2 < ns; s2 += 2, g += 2) {
-                body(g, std::integral_constant<int, 0>{}, std::false_type{});
-                body(g + 1, std::integral_constant<int, 1>{}, std::false_type{});
-            }
+    auto step = [&](int64_t g, auto slot_c) __attribute__((always_inline)) {
+        body(g, slot_c);
+        if (++ks == ns) {
+            ks = 0;
             epilogue();
         }
-    } else {
-        for (int64_t g = 0; g < G; g += 2) {
-            body(g, std::integral_constant<int, 0>{}, std::false_type{});
-            if (++ks == ns) {
-                ks = 0;
-                epilogue();
-            }
-            if (g + 1 < G) {
-                body(g + 1, std::integral_constant<int, 1>{}, std::false_type{});
-                if (++ks == ns) {
-                    ks = 0;
-                    epilogue();
-                }
-            }
-        }
+    };
+    for (int64_t g = 0; g < G; g += 3) {
+        step(g, std::integral_constant<int, 0>{});
+        if (g + 1 < G) step(g + 1, std::integral_constant<int, 1>{});
+        if (g + 2 < G) step(g + 2, std::integral_constant<int, 2>{});
     }
     // no LDS-DMA copy may land after the block's LDS is handed to the next block
     __builtin_amdgcn_s_waitcnt(0xF70u);
@@ -1115,25 +1116,17 @@ void launch_flat_bf16_k64(const void *qimg, const float *qn, int64_t nq, const v
                    "flat_bf16_k64: bad arguments");
     HIPANN_REQUIRE(!qscale == !xscale, "flat_bf16_k64: int8 needs both scales");
     HIPANN_REQUIRE((int64_t)nqt * nsplit < 0x7fffffff, "grid too large");
-    // HIPANN_FLAT_W4=1 (A/B): the int8 passes on the 4-wave, 512-register variant (MBW = 4)
-    static const bool w4 = [] { const char *e = std::getenv("HIPANN_FLAT_W4"); return e && std::atoi(e) != 0; }();
-    const bool use_w4 = w4 && qscale && (nk / 2) % 2 == 0;  // (its tile loop runs K-steps in pairs)
-    dim3 grid((unsigned)(nqt * nsplit)), block(64 * (use_w4 ? K64Geom<4>::W : K64Geom<2>::W));
+    // (r05, measured and dropped: a 4-wave 512-register variant — 64 queries per wave, half the LDS reads per MFMA —
+    // 9.93 vs 8.22 ms at 10M, its accumulators shuffled between AGPRs and VGPRs; a tile loop whose first K-step starts
+    // from a zero C operand instead of resetting the accumulators — 43 spills, 10.75 vs 7.71 ms)
+    dim3 grid((unsigned)(nqt * nsplit)), block(64 * K64Geom<2>::W);
     const k64_u32x4 *qa = static_cast<const k64_u32x4 *>(qimg);
     const k64_u32x4 *xa = static_cast<const k64_u32x4 *>(ximg);
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, grid, block, K64_LDS, st, qa, qn, nq, xa, xn, N, nk, nqt, nsplit, tiles_per_split,
                            tile_begin, tile_end, bound, cand_d, cand_i, cand_n, cap, resume ? 1 : 0, qscale, xscale);
     };
-    if (qscale && use_w4) {
-        if (keys) {
-            if (metric == kL2) go(flat_bf16_k64<true, true, true, 4>);
-            else go(flat_bf16_k64<false, true, true, 4>);
-        } else {
-            if (metric == kL2) go(flat_bf16_k64<true, false, true, 4>);
-            else go(flat_bf16_k64<false, false, true, 4>);
-        }
-    } else if (qscale) {
+    if (qscale) {
         if (keys) {
             if (metric == kL2) go(flat_bf16_k64<true, true, true>);
             else go(flat_bf16_k64<false, true, true>);
