@@ -503,10 +503,8 @@ def flat_config(args, torch, dist, hipann, rank, world, dev, n, d, nq, k, metric
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
-    index.set_kernel_timing(True)
     el = timed_steps(torch, dist, world, step, steps)
-    kern_ms, merge_ms = index.kernel_ms(0), index.kernel_ms(1)
-    index.set_kernel_timing(False)
+    kern_ms, merge_ms = kernel_timing_steps(torch, index, step, steps)
     Dr, Ir = step()
     torch.cuda.synchronize()
     Ir = Ir.cpu().numpy().copy()
@@ -738,6 +736,18 @@ def ivf_scan_stats(index, probes, d, nlist, row_bytes=None):
             "probes_per_list_p50_p90_max": [int(np.percentile(cnt, 50)), int(np.percentile(cnt, 90)), int(cnt.max())]}
 
 
+def kernel_timing_steps(torch, index, step, steps):
+    """(main kernel ms, merge ms) of the last of a few extra steps run with the library's event timers on.  The
+    timed steps run with the timers off: the event records around the kernels are not part of the measured step."""
+    index.set_kernel_timing(True)
+    for _ in range(max(2, min(steps, 5))):
+        step()
+    torch.cuda.synchronize()
+    out = index.kernel_ms(0), index.kernel_ms(1)
+    index.set_kernel_timing(False)
+    return out
+
+
 def ivf_config(args, torch, dist, hipann, rank, world, dev, steps, warmup, suite_extras=False):
     from ivf_build import flat_ground_truth
     from sharded import ShardedSearch, merge_packed_device_torch
@@ -779,10 +789,8 @@ def ivf_config(args, torch, dist, hipann, rank, world, dev, steps, warmup, suite
         "replicated on every rank" if world > 1 else "single GPU"
     probes = index.last_probes(nq)
     info.update(ivf_scan_stats(index, probes, d, nlist, ivf_row_bytes(index.form, d, metric)))
-    index.set_kernel_timing(True)
     el = timed_steps(torch, dist, world, step, steps)
-    kern_ms, merge_ms = index.kernel_ms(0), index.kernel_ms(1)
-    index.set_kernel_timing(False)
+    kern_ms, merge_ms = kernel_timing_steps(torch, index, step, steps)
     Dr, Ir = step()
     torch.cuda.synchronize()
     Ir = Ir.cpu().numpy().copy()

@@ -1,6 +1,7 @@
 // runtime.hpp — device buffers, per-handle streams/scratch and the index objects behind hip_ann.h.
 #pragma once
 #include "common.hpp"
+#include <cstdlib>
 #include <memory>
 #include <mutex>
 #include <vector>
@@ -134,23 +135,37 @@ struct StreamFence {
     StreamFence(const StreamFence &) = delete;
     StreamFence &operator=(const StreamFence &) = delete;
     ~StreamFence() { if (ev) { DeviceGuard g(device); (void)hipEventDestroy(ev); } }
+    // Default (lazy): nothing is recorded per call — an event record is a marker packet the next kernel waits
+    // behind (≈6 µs of idle GPU between consecutive searches on one stream, r05 kernel traces) — and a call on a
+    // different stream than the previous call first synchronises the device (the previous stream may have been
+    // destroyed since, so no event is recorded on it then).  HIPANN_FENCE_EAGER=1: the event recorded at the end of
+    // every call, waited for by a call on another stream.
+    static bool eager() {
+        static const bool v = [] { const char *e = std::getenv("HIPANN_FENCE_EAGER"); return e && std::atoi(e) != 0; }();
+        return v;
+    }
     void enter(hipStream_t st) {
-        if (armed && st != last) HIPANN_CHECK(hipStreamWaitEvent(st, ev, 0));
+        if (!armed || st == last) return;
+        if (eager()) {
+            HIPANN_CHECK(hipStreamWaitEvent(st, ev, 0));
+        } else {
+            DeviceGuard g(device);
+            HIPANN_CHECK(hipDeviceSynchronize());
+        }
     }
     void leave(hipStream_t st, int dev) {
-        if (!ev) {
-            DeviceGuard g(dev);
-            HIPANN_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-            device = dev;
+        if (eager()) {
+            if (!ev) {
+                DeviceGuard g(dev);
+                HIPANN_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            }
+            HIPANN_CHECK(hipEventRecord(ev, st));
         }
-        HIPANN_CHECK(hipEventRecord(ev, st));
+        device = dev;
         last = st;
         armed = true;
     }
 };
-
-// enter() at construction, leave() when the scope ends (normally or by an exception: whatever was
-// enqueued before the throw is fenced too).
 struct FenceScope {
     StreamFence &f;
     hipStream_t st;

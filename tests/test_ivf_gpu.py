@@ -7,6 +7,7 @@ faiss-metal/tests/test_metal_ivfflat.mm:28-166 (nv=2000, d=64, nlist=16, nprobe=
 from __future__ import annotations
 
 import json
+import os
 import sys
 from pathlib import Path
 
@@ -198,6 +199,59 @@ def test_ivf_backend_and_device_api(gpu, oracle):
     ix.search_device(100, q_t.data_ptr(), 10, Dt.data_ptr(), It.data_ptr(), torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     assert np.array_equal(It.cpu().numpy(), I) and np.array_equal(Dt.cpu().numpy(), D)
+
+
+@pytest.mark.parametrize("eager", [False, True])
+def test_ivf_device_api_alternating_streams(gpu, eager):
+    """Consecutive calls on one handle from different streams (StreamFence): a call on a new stream may not start
+    before the previous call's kernels are done with the shard's scratch (lazy default: a device synchronisation on
+    a stream switch; HIPANN_FENCE_EAGER=1: per-call events, run in a child process).  Each batch's answers equal the
+    same batch searched alone."""
+    import subprocess
+    import torch
+    if eager:
+        code = ("import sys; sys.path.insert(0, %r); import test_ivf_gpu as t; t._alternating_streams_body()"
+                % str(Path(__file__).resolve().parent))
+        env = dict(os.environ, HIPANN_FENCE_EAGER="1")
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        return
+    _alternating_streams_body()
+
+
+def _alternating_streams_body():
+    import torch
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "duckdb-annsearch_amd"))
+    import hipann as gpu
+    rng = np.random.default_rng(11)
+    d, n, nlist = 64, 40000, 64
+    xb = rng.standard_normal((n, d)).astype(np.float32)
+    cen = np.ascontiguousarray(xb[:: n // nlist][:nlist])
+    off, ids, codes = build_ivf_lists(xb, cen)
+    dev = torch.device("cuda", 0)
+    c_t, i_t, x_t = (torch.from_numpy(a).to(dev) for a in (cen, ids, codes))
+    ix = gpu.HipIndexIVFFlat.from_device(d, 0, nlist, 8, c_t.data_ptr(), off, i_t.data_ptr(), x_t.data_ptr(), 0)
+    batches = [torch.from_numpy(rng.standard_normal((512, d)).astype(np.float32)).to(dev) for _ in range(6)]
+    ref = []
+    for q in batches:  # each batch alone, synchronised
+        D = torch.empty((512, 10), device=dev)
+        I = torch.empty((512, 10), device=dev, dtype=torch.int64)
+        ix.search_device(512, q.data_ptr(), 10, D.data_ptr(), I.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        ref.append((D.cpu().numpy(), I.cpu().numpy()))
+    streams = [torch.cuda.Stream(device=dev) for _ in range(2)]
+    outs = []
+    for j, q in enumerate(batches):  # back to back, alternating streams, no host synchronisation in between
+        s = streams[j % 2]
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            D = torch.empty((512, 10), device=dev)
+            I = torch.empty((512, 10), device=dev, dtype=torch.int64)
+            ix.search_device(512, q.data_ptr(), 10, D.data_ptr(), I.data_ptr(), s.cuda_stream)
+        outs.append((D, I))
+    torch.cuda.synchronize()
+    for (D, I), (Dr, Ir) in zip(outs, ref):
+        assert np.array_equal(I.cpu().numpy(), Ir) and np.array_equal(D.cpu().numpy(), Dr)
 
 
 def test_ivf_gpu_build_recall(gpu):
