@@ -85,15 +85,32 @@ __global__ void __launch_bounds__(256) dist_rows(const float *__restrict__ queri
     if (lane == 0) out[w] = IP ? -s : s;
 }
 
+// The host BFS's visited sets on the device (vbits != nullptr): one bit per (query, row), vwords words per query.
+// A candidate whose bit was already set (an earlier step of its query, or an earlier slot of the same step) is not
+// evaluated: its output is kVisitedBits, a NaN payload no distance arithmetic produces.
+constexpr unsigned kVisitedBits = 0x7fc0deadu;
+__device__ __forceinline__ bool visit_first(unsigned *vbits, int64_t vwords, unsigned qi, unsigned id) {
+    const unsigned bit = 1u << (id & 31u);
+    return (atomicOr(vbits + (int64_t)qi * vwords + (id >> 5), bit) & bit) == 0u;
+}
+
 template <bool IP, bool VEC4>
 __global__ void __launch_bounds__(256) dist_ids_f32(const float *__restrict__ queries, const float *__restrict__ db,
                                                     const unsigned *__restrict__ ids, const unsigned *__restrict__ qmap,
-                                                    int total_n, int d, int64_t n, float *__restrict__ out) {
+                                                    int total_n, int d, int64_t n, float *__restrict__ out,
+                                                    unsigned *__restrict__ vbits, int64_t vwords) {
     const int lane = threadIdx.x & 63;
     const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (w >= total_n) return;
     const unsigned id = ids[w];
     if (id >= n) return;  // empty slot of the BFS's fixed per-query layout
+    if (vbits) {
+        const int first = lane == 0 ? (int)visit_first(vbits, vwords, qmap[w], id) : 0;
+        if (!__shfl(first, 0)) {
+            if (lane == 0) out[w] = __uint_as_float(kVisitedBits);
+            return;
+        }
+    }
     const float *q = queries + (int64_t)qmap[w] * d;
     const float *c = db + (int64_t)id * d;
     float s = 0.f;
@@ -142,7 +159,8 @@ template <bool IP>
 __global__ void __launch_bounds__(256) dist_ids_sq8(const float *__restrict__ queries, const uint8_t *__restrict__ codes,
                                                     const float2 *__restrict__ ab_g, const unsigned *__restrict__ ids,
                                                     const unsigned *__restrict__ qmap, int total_n, int d,
-                                                    int64_t n, float *__restrict__ out) {
+                                                    int64_t n, float *__restrict__ out, unsigned *__restrict__ vbits,
+                                                    int64_t vwords) {
     extern __shared__ __attribute__((aligned(16))) float2 ab[];
     for (int j = threadIdx.x; j < d; j += 256) ab[j] = ab_g[j];
     __syncthreads();
@@ -150,7 +168,13 @@ __global__ void __launch_bounds__(256) dist_ids_sq8(const float *__restrict__ qu
     for (int64_t c0 = (int64_t)blockIdx.x * 16; c0 < total_n; c0 += (int64_t)gridDim.x * 16) {
         const int64_t c = c0 + (threadIdx.x >> 4);
         const unsigned id = c < total_n ? ids[c] : 0xffffffffu;
-        const bool valid = id < n;  // also skips empty slots of the BFS's fixed per-query layout
+        bool valid = id < n;  // also skips empty slots of the BFS's fixed per-query layout
+        if (vbits) {  // the candidate's visited bit, by the first lane of its quarter wave
+            const int first = valid && ql == 0 ? (int)visit_first(vbits, vwords, qmap[c], id) : 0;
+            const bool fresh = __shfl(first, (int)(threadIdx.x & 63) & ~15) != 0;
+            if (valid && !fresh && ql == 0) out[c] = __uint_as_float(kVisitedBits);
+            valid = valid && fresh;
+        }
         float s = 0.f;
         if (valid) {
             const float *q = queries + (int64_t)qmap[c] * d;
@@ -193,12 +217,20 @@ __global__ void __launch_bounds__(256) dist_ids_sq8_scalar(const float *__restri
                                                            const uint8_t *__restrict__ codes,
                                                            const float2 *__restrict__ ab, const unsigned *__restrict__ ids,
                                                            const unsigned *__restrict__ qmap, int total_n, int d,
-                                                           int64_t n, float *__restrict__ out) {
+                                                           int64_t n, float *__restrict__ out, unsigned *__restrict__ vbits,
+                                                           int64_t vwords) {
     const int lane = threadIdx.x & 63;
     const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (w >= total_n) return;
     const unsigned id = ids[w];
     if (id >= n) return;
+    if (vbits) {
+        const int first = lane == 0 ? (int)visit_first(vbits, vwords, qmap[w], id) : 0;
+        if (!__shfl(first, 0)) {
+            if (lane == 0) out[w] = __uint_as_float(kVisitedBits);
+            return;
+        }
+    }
     const float *q = queries + (int64_t)qmap[w] * d;
     const uint8_t *row = codes + (int64_t)id * d;
     float s = 0.f;
@@ -280,6 +312,7 @@ struct DiskDB {
     // resident graph + BFS scratch (diskann_hip_register_graph / _search_batch_resident)
     int R = 0;
     DevBuf adj_dev, dupw, visited, flags, bstats, eps_dev;
+    DevBuf vbits;  // host BFS: the queries' visited bits on the device (one bit per row and query)
     std::vector<uint32_t> adj_host;
     ~DiskDB() {
         if (stream) { DeviceGuard g(device); (void)hipStreamDestroy(stream); }
@@ -287,7 +320,7 @@ struct DiskDB {
 };
 
 void launch_ids(DiskDB &db, const float *q, const unsigned *ids, const unsigned *m, int total_n, int metric,
-                float *out, hipStream_t st) {
+                float *out, hipStream_t st, unsigned *vbits = nullptr, int64_t vwords = 0) {
     if (total_n <= 0) return;
     const int d = db.dim;
     if (db.fmt == DISKANN_HIP_FMT_F32) {
@@ -295,11 +328,11 @@ void launch_ids(DiskDB &db, const float *q, const unsigned *ids, const unsigned 
         const bool v4 = (d % 4 == 0) && ((uintptr_t)q % 16 == 0);
         dim3 grid((unsigned)ceil_div(total_n, 4)), block(256);
         if (metric == kIP) {
-            if (v4) hipLaunchKernelGGL((dist_ids_f32<true, true>), grid, block, 0, st, q, x, ids, m, total_n, d, db.n, out);
-            else hipLaunchKernelGGL((dist_ids_f32<true, false>), grid, block, 0, st, q, x, ids, m, total_n, d, db.n, out);
+            if (v4) hipLaunchKernelGGL((dist_ids_f32<true, true>), grid, block, 0, st, q, x, ids, m, total_n, d, db.n, out, vbits, vwords);
+            else hipLaunchKernelGGL((dist_ids_f32<true, false>), grid, block, 0, st, q, x, ids, m, total_n, d, db.n, out, vbits, vwords);
         } else {
-            if (v4) hipLaunchKernelGGL((dist_ids_f32<false, true>), grid, block, 0, st, q, x, ids, m, total_n, d, db.n, out);
-            else hipLaunchKernelGGL((dist_ids_f32<false, false>), grid, block, 0, st, q, x, ids, m, total_n, d, db.n, out);
+            if (v4) hipLaunchKernelGGL((dist_ids_f32<false, true>), grid, block, 0, st, q, x, ids, m, total_n, d, db.n, out, vbits, vwords);
+            else hipLaunchKernelGGL((dist_ids_f32<false, false>), grid, block, 0, st, q, x, ids, m, total_n, d, db.n, out, vbits, vwords);
         }
     } else {
         const uint8_t *x = db.data.get<uint8_t>();
@@ -308,12 +341,12 @@ void launch_ids(DiskDB &db, const float *q, const unsigned *ids, const unsigned 
             // ≤ 8 blocks per CU, each looping over groups of 16 candidates (dist_ids_sq8)
             dim3 grid((unsigned)std::min<int64_t>(ceil_div(total_n, 16), 2048)), block(256);
             const size_t smem = (size_t)d * sizeof(float2);
-            if (metric == kIP) hipLaunchKernelGGL(dist_ids_sq8<true>, grid, block, smem, st, q, x, ab, ids, m, total_n, d, db.n, out);
-            else hipLaunchKernelGGL(dist_ids_sq8<false>, grid, block, smem, st, q, x, ab, ids, m, total_n, d, db.n, out);
+            if (metric == kIP) hipLaunchKernelGGL(dist_ids_sq8<true>, grid, block, smem, st, q, x, ab, ids, m, total_n, d, db.n, out, vbits, vwords);
+            else hipLaunchKernelGGL(dist_ids_sq8<false>, grid, block, smem, st, q, x, ab, ids, m, total_n, d, db.n, out, vbits, vwords);
         } else {
             dim3 grid((unsigned)ceil_div(total_n, 4)), block(256);
-            if (metric == kIP) hipLaunchKernelGGL(dist_ids_sq8_scalar<true>, grid, block, 0, st, q, x, ab, ids, m, total_n, d, db.n, out);
-            else hipLaunchKernelGGL(dist_ids_sq8_scalar<false>, grid, block, 0, st, q, x, ab, ids, m, total_n, d, db.n, out);
+            if (metric == kIP) hipLaunchKernelGGL(dist_ids_sq8_scalar<true>, grid, block, 0, st, q, x, ab, ids, m, total_n, d, db.n, out, vbits, vwords);
+            else hipLaunchKernelGGL(dist_ids_sq8_scalar<false>, grid, block, 0, st, q, x, ab, ids, m, total_n, d, db.n, out, vbits, vwords);
         }
     }
     HIPANN_CHECK(hipGetLastError());
@@ -525,9 +558,25 @@ void host_bfs(DiskDB *db, const uint32_t *adj, int R, const uint32_t *eps, int n
     uint32_t *hm = db->hm.get<uint32_t>();
     float *hout = db->hout.get<float>();
     float *hout_dev = static_cast<float *>(host_device_ptr(hout));
+    // HIPANN_BFS_ZC_IDS=0 (A/B): the step's ids copied to the device before each gather instead of read in place
+    static const bool zc_ids = [] { const char *e = std::getenv("HIPANN_BFS_ZC_IDS"); return !e || std::atoi(e); }();
+    const unsigned *hid_dev = static_cast<const unsigned *>(host_device_ptr(hid));
     for (size_t i = 0; i < cap; ++i) hm[i] = (uint32_t)(i / S);
     HIPANN_CHECK(hipMemcpyAsync(db->m.p, hm, cap * 4, hipMemcpyHostToDevice, st));
     std::vector<QState> Sq((size_t)nq);
+    // The visited sets live on the device (default): the id-gather kernel sets each candidate's bit and skips the ones
+    // already set, so the host phases never probe a per-query hash set (≈ 6K ids, 32-64 KB per query: a cache miss
+    // per neighbour).  The host hands over every valid neighbour of the expanded row; an already-visited one comes
+    // back as kVisitedBits and is dropped.  HIPANN_BFS_GPU_VISITED=0 (A/B), or more than 1 GiB of bits: the host sets.
+    static const bool gv_env = [] { const char *e = std::getenv("HIPANN_BFS_GPU_VISITED"); return !e || std::atoi(e); }();
+    const int64_t vwords = ((int64_t)N + 31) / 32;
+    const bool gv = gv_env && (int64_t)nq * vwords * 4 <= ((int64_t)1 << 30);
+    if (gv) {
+        db->vbits.ensure((size_t)nq * vwords * 4, db->device);
+        HIPANN_CHECK(hipMemsetAsync(db->vbits.p, 0, (size_t)nq * vwords * 4, st));
+    }
+    unsigned *vbits = gv ? db->vbits.get<unsigned>() : nullptr;
+    auto visited_mark = [](float v) { return __builtin_bit_cast(uint32_t, v) == kVisitedBits; };
     SpinPool pool(bfs_threads(nq));
     const int T = pool.size();
     struct Group {
@@ -556,31 +605,34 @@ void host_bfs(DiskDB *db, const uint32_t *adj, int R, const uint32_t *eps, int n
         g.launched = tot > 0;
         if (!tot) return;
         const size_t o = (size_t)g.q0 * S, span = (size_t)(last - g.q0) * S;
-        HIPANN_CHECK(hipMemcpyAsync(db->ids.get<unsigned>() + o, hid + o, span * 4, hipMemcpyHostToDevice, st));
+        // zc_ids: the kernel reads the step's ids straight from the pinned host buffer (its device mapping) instead of
+        // a host-to-device copy ahead of it (a DMA operation the kernel waits behind, per step)
+        if (!zc_ids)
+            HIPANN_CHECK(hipMemcpyAsync(db->ids.get<unsigned>() + o, hid + o, span * 4, hipMemcpyHostToDevice, st));
         {
             // the distances go straight into the pinned host buffer through its device mapping (posted writes: no
             // device-to-host copy and its round trip per step)
             ScopedTiming tm(db->timer, st);
-            launch_ids(*db, db->q.get<float>(), db->ids.get<unsigned>() + o, db->m.get<unsigned>() + o, (int)span,
-                       metric, hout_dev + o, st);
+            launch_ids(*db, db->q.get<float>(), (zc_ids ? hid_dev : db->ids.get<unsigned>()) + o,
+                       db->m.get<unsigned>() + o, (int)span, metric, hout_dev + o, st, vbits, vwords);
         }
         HIPANN_CHECK(hipEventRecord(g.ev, st));
         ncalls++;
-        nevals += tot;
+        if (!gv) nevals += tot;  // (gv: the first visits, counted as the phases read them)
     };
     // seed entry points (disk_provider.rs:524-538)
     pool.run([&](int t) {
         const int q0 = (int)((int64_t)nq * t / T), q1 = (int)((int64_t)nq * (t + 1) / T);
         for (int qi = q0; qi < q1; ++qi) {
             QState &s = Sq[qi];
-            s.visited.init(std::max<size_t>(l * 2, 1024));
+            if (!gv) s.visited.init(std::max<size_t>(l * 2, 1024));
             s.cands.reserve(l * 2);
             s.result.reserve(l + 1);
             uint32_t *slot = hid + (size_t)qi * S;
             int cnt = 0;
             for (int e = 0; e < n_ep; ++e) {
                 const uint32_t ep = eps[e];
-                if (s.visited.insert(ep) && ep < N) slot[cnt++] = ep;
+                if (gv ? ep < N : (s.visited.insert(ep) && ep < N)) slot[cnt++] = ep;
             }
             for (size_t j = (size_t)cnt; j < S; ++j) slot[j] = 0xffffffffu;
             s.nnew = cnt;
@@ -591,18 +643,34 @@ void host_bfs(DiskDB *db, const uint32_t *adj, int R, const uint32_t *eps, int n
     // through insert_result), then the loop head (disk_provider.rs:545-652): pop, stop rule, expansion.
     // Returns the loop-head active count.
     std::vector<int64_t> red((size_t)T * 8, 0);  // per-thread head counts, padded against false sharing
+    // HIPANN_BFS_CHUNK (A/B): queries per work item taken from a shared counter (default 0: a static 1/T range per
+    // thread — measured r05: 8-query chunks 27.6 ms of phases per batch against 19.7 static, 2-query chunks 38 ms: a
+    // query's state stays in one core's caches only when the same thread keeps it)
+    static const int chunk = [] { const char *e = std::getenv("HIPANN_BFS_CHUNK"); return e ? std::atoi(e) : 0; }();
+    std::atomic<int> next_q{0};
     auto phase = [&](Group &g) {
         const int n = g.q1 - g.q0;
         const bool seed = g.seed;
+        next_q.store(g.q0, std::memory_order_relaxed);
         pool.run([&](int t) {
-            const int q0 = g.q0 + (int)((int64_t)n * t / T), q1 = g.q0 + (int)((int64_t)n * (t + 1) / T);
-            int64_t head = 0;
+            int64_t head = 0, evals = 0;
+            int q0, q1;
+            if (chunk > 0) {
+                q0 = next_q.fetch_add(chunk, std::memory_order_relaxed);
+                q1 = std::min(q0 + chunk, g.q1);
+            } else {
+                q0 = g.q0 + (int)((int64_t)n * t / T);
+                q1 = g.q0 + (int)((int64_t)n * (t + 1) / T);
+            }
+            for (; q0 < g.q1; ) {
             for (int qi = q0; qi < q1; ++qi) {
                 QState &s = Sq[qi];
                 uint32_t *slot = hid + (size_t)qi * S;
                 const float *dd = hout + (size_t)qi * S;
                 if (seed) {
                     for (int j = 0; j < s.nnew; ++j) {
+                        if (gv && visited_mark(dd[j])) continue;  // a repeated entry point
+                        ++evals;
                         s.cands.push_back(Cand{dd[j], slot[j]});
                         std::push_heap(s.cands.begin(), s.cands.end(), CandGreater());
                         s.result.push_back(Cand{dd[j], slot[j]});
@@ -610,7 +678,11 @@ void host_bfs(DiskDB *db, const uint32_t *adj, int R, const uint32_t *eps, int n
                     std::stable_sort(s.result.begin(), s.result.end(),
                                      [](const Cand &x, const Cand &y) { return x.d < y.d; });
                 } else {
-                    for (int j = 0; j < s.nnew; ++j) insert_result(s, l, dd[j], slot[j]);
+                    for (int j = 0; j < s.nnew; ++j) {
+                        if (gv && visited_mark(dd[j])) continue;
+                        ++evals;
+                        insert_result(s, l, dd[j], slot[j]);
+                    }
                 }
                 const int prev = s.nnew;  // slots >= prev are already empty
                 s.nnew = 0;
@@ -626,6 +698,15 @@ void host_bfs(DiskDB *db, const uint32_t *adj, int R, const uint32_t *eps, int n
                             s.active = false;
                         } else {
                             const uint32_t *nbr = adj + (size_t)c.id * R;
+                            if (gv) {  // every valid neighbour: the device keeps the visited sets
+                                int cnt = 0;
+                                for (int r = 0; r < R; ++r) {
+                                    const uint32_t nb = nbr[r];
+                                    if (nb == 0xffffffffu) break;  // get_neighbors trims at the first sentinel
+                                    if (nb < N) slot[cnt++] = nb;
+                                }
+                                s.nnew = cnt;
+                            } else {
                             // the row's valid neighbours first, with their visited-set slots prefetched: the set
                             // (≈ 6K ids, 32-64 KB per query) misses cache on nearly every probe, and 64 overlapped
                             // misses cost about one
@@ -648,6 +729,7 @@ void host_bfs(DiskDB *db, const uint32_t *adj, int R, const uint32_t *eps, int n
                                     if (s.visited.insert(nv[j])) slot[cnt++] = nv[j];
                             }
                             s.nnew = cnt;
+                            }
                         }
                     }
                 }
@@ -656,11 +738,19 @@ void host_bfs(DiskDB *db, const uint32_t *adj, int R, const uint32_t *eps, int n
                 // change it), into cache while the GPU computes this step's distances
                 if (s.active && !s.cands.empty()) __builtin_prefetch(adj + (size_t)s.cands.front().id * R);
             }
+            if (chunk <= 0) break;
+            q0 = next_q.fetch_add(chunk, std::memory_order_relaxed);
+            q1 = std::min(q0 + chunk, g.q1);
+            }
             red[(size_t)t * 8] = head;
+            red[(size_t)t * 8 + 1] = evals;
         });
         g.seed = false;
         int64_t head = 0;
-        for (int t = 0; t < T; ++t) head += red[(size_t)t * 8];
+        for (int t = 0; t < T; ++t) {
+            head += red[(size_t)t * 8];
+            if (gv) nevals += red[(size_t)t * 8 + 1];
+        }
         return head;
     };
     // HIPANN_BFS_PROF=1 (tuning): host time in the GPU waits, the host phases and the launches, on stderr
