@@ -137,9 +137,12 @@ int hipann_last_search_path(void *index, int *form, int *filter_k, int *sublists
  * included: they are re-run on the device).  Flat: the exact forms (HIPANN_FLAT_FORM_SPLIT2_EXACT,
  * HIPANN_FLAT_FORM_BF16_EXACT, HIPANN_FLAT_FORM_I8_EXACT) synchronise the stream once per call to read the flagged-query count (twice
  * when the bounded passes' candidate rerank ran), and a table's first exact-form search also builds its bf16 /
- * int8 image and bound; the other forms return with their kernels queued.  Calls on one handle may use different streams: each call
- * makes its stream wait for an event recorded at the end of the handle's previous call (the per-handle
- * scratch is reused), so they execute in the order they were issued.  The caller still orders its own
+ * int8 image and bound; the other forms return with their kernels queued.  Calls on one handle may use different streams:
+ * a call whose stream differs from the handle's previous call's first synchronises the device (the per-handle scratch is
+ * reused, and the previous stream may have been destroyed since), so they execute in the order they were issued; calls
+ * on one stream add nothing between them (no event per call — an event marker costs ≈6 µs of idle GPU between
+ * back-to-back searches).  HIPANN_FENCE_EAGER=1 instead records an event at the end of every call and makes a call on
+ * another stream wait for it (the previous stream must then outlive the next call).  The caller still orders its own
  * buffers (queries written / results read on other streams) with its own events.
  * ------------------------------------------------------------------------------------------- */
 
