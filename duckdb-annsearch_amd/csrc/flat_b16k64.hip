@@ -38,7 +38,8 @@ typedef __attribute__((address_space(3))) void k64_lds_void;
 
 // Tuning builds only (timing ablations, wrong results): bit 0 drops the database-tile DMA, bit 1 the query-fragment
 // loads, bit 2 the epilogue's candidate filter, bit 3 the per-K-step barrier, bit 4 the filter's append path (the
-// compare and ballot kept), bit 5 the per-query scales (one per tile), bit 6 the accumulator reset.  Product builds: 0.
+// compare and ballot kept), bit 5 the per-query scales (one per tile), bit 6 the accumulator reset, bit 7 the whole
+// epilogue (the accumulators xor-reduced and reset).  Product builds: 0.
 #ifndef HIPANN_K64_ABLATE
 #define HIPANN_K64_ABLATE 0
 #endif
@@ -358,6 +359,17 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
             }
             auto tile_mb = [&](auto mb_c) __attribute__((always_inline)) {
                 constexpr int MB = decltype(mb_c)::value;
+                if constexpr ((HIPANN_K64_ABLATE & 128) != 0 && !KEYS) {  // (tuning: the epilogue's cost — the
+                    // accumulators consumed by one xor each and reset, no conversion or filter)
+                    k64_f32x4 x = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        x = __builtin_elementwise_max(x, __builtin_convertvector(acc[MB][8 * hf + j], k64_f32x4));
+                        acc[MB][8 * hf + j] = (AccT){0, 0, 0, 0};
+                    }
+                    cntv += x[0] + x[1] + x[2] + x[3] == 1234.5f ? 1 : 0;
+                    return;
+                }
                 k64_f32x4 sm[8];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
