@@ -1311,6 +1311,17 @@ __device__ __forceinline__ void rerank_rows4(const float *__restrict__ qp, const
 #ifndef HIPANN_RR_PROF
 #define HIPANN_RR_PROF 0  // tuning builds: wave 0's per-phase shader clocks of the wide rerank, summed in rr_prof
 #endif
+#ifndef HIPANN_RR_STAMP
+#define HIPANN_RR_STAMP 0  // tuning builds: per-query wall-clock stamps (100 MHz) of the wide rerank's phases
+#endif
+#if HIPANN_RR_STAMP
+__device__ long long rr_stamp[4096 * 8];
+#define RR_STAMP_Q(qq, i) do { if (threadIdx.x == 0 && (qq) < 4096) rr_stamp[(qq) * 8 + (i)] = (long long)__builtin_amdgcn_s_memrealtime(); } while (0)
+#define RR_STAMP(i) RR_STAMP_Q(q, i)
+#else
+#define RR_STAMP(i) do { } while (0)
+#define RR_STAMP_Q(qq, i) do { } while (0)
+#endif
 #if HIPANN_RR_PROF
 __device__ unsigned long long rr_prof[16];
 #define RR_MARK(i) do { if (wv == 0) { const long long t_ = clock64(); if (lane == 0) atomicAdd(&rr_prof[i], (unsigned long long)(t_ - rr_t)); rr_t = t_; } } while (0)
@@ -1527,12 +1538,55 @@ __device__ __forceinline__ int rws_take(const float *__restrict__ mk, const int 
     }
     return base < k ? base : k;
 }
+// The k best of a wave's run (mk, mp)[0, m) for m > 64 by narrowing (as flat_keys_kth): T_hi = the k-th smallest of
+// the 64 lanes' minima (at least k entries lie at or below it), the entries ≤ T_hi compacted in (register, lane) order
+// into (tk, tp), then the exact k-th and the take over that list of ≤ 64 — the same k entries as the bisection over
+// the whole run (ties at the k-th keep the first in run order either way).  −1 when more than 64 entries are ≤ T_hi
+// (the caller bisects the whole run).  r05: the whole-run bisection (32 steps × up to 16 ballots per wave, four
+// resident blocks per CU sharing each SIMD's issue) was 13.4 of the kernel's ≈ 34 µs (tools/rr_stamps.py).
+template <int J>
+__device__ __forceinline__ int rws_select_narrow(const float *mk, const int *mp, int m, int k, float *tk, int *tp,
+                                                 float *ok, int *op) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    const int nj = (m + 63) >> 6;
+    unsigned u[J];
+    unsigned mn = 0xffffffffu;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int e = j * 64 + lane;
+        u[j] = j < nj && e < m ? rws_bits(mk[e]) : 0xffffffffu;
+        mn = min(mn, u[j]);
+    }
+    unsigned th = 0;
+    for (int bit = 31; bit >= 0; --bit) {
+        const unsigned cand = th | (1u << bit);
+        if ((int)__popcll(__ballot(mn < cand)) < k) th = cand;
+    }
+    int c = 0;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const bool a = u[j] <= th && u[j] != 0xffffffffu;
+        const unsigned long long ma = __ballot(a);
+        const int p = c + (int)__popcll(ma & lt);
+        if (a && p < 64) { tk[p] = mk[j * 64 + lane]; tp[p] = mp[j * 64 + lane]; }
+        c += (int)__popcll(ma);
+    }
+    if (c > 64) return -1;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    unsigned dummy = 0;
+    const unsigned T = rws_kth_bits<1>(tk, c, k, dummy);
+    return rws_take<1>(tk, tp, c, k, T, ok, op);
+}
+
 template <int WV, int J>
 __device__ __forceinline__ void rerank_wave_select(const float *__restrict__ pd, const int *__restrict__ pi,
                                                    int64_t total, int k, int64_t nrows, float bound,
                                                    float *wk, int *wp, float *sk, int *sp, int *scnt,
-                                                   WaveList<1, int> &L, bool &bad, long long &rr_t) {
+                                                   WaveList<1, int> &L, bool &bad, long long &rr_t, int64_t rr_q,
+                                                   float *ntk, int *ntp) {
     (void)rr_t;
+    (void)rr_q;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const unsigned long long lt = (1ull << lane) - 1ull;
     float v[J];
@@ -1556,17 +1610,26 @@ __device__ __forceinline__ void rerank_wave_select(const float *__restrict__ pd,
         m += __popcll(ma);
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the run's LDS writes before this wave reads it
+    if constexpr (HIPANN_RR_STAMP != 0) { if (m >= 0) RR_STAMP_Q(rr_q, 6); }
     int kw;
     if (m <= k) {
         kw = m;
         for (int e = lane; e < m; e += 64) { sk[wv * 64 + e] = mk[e]; sp[wv * 64 + e] = mp[e]; }
-    } else {
+    } else if (m <= 64) {  // one register of the run
         unsigned dummy = 0;
-        const unsigned T = rws_kth_bits<J>(mk, m, k, dummy);
-        kw = rws_take<J>(mk, mp, m, k, T, sk + wv * 64, sp + wv * 64);
+        const unsigned T = rws_kth_bits<1>(mk, m, k, dummy);
+        kw = rws_take<1>(mk, mp, m, k, T, sk + wv * 64, sp + wv * 64);
+    } else {
+        kw = ntk ? rws_select_narrow<J>(mk, mp, m, k, ntk + wv * 64, ntp + wv * 64, sk + wv * 64, sp + wv * 64) : -1;
+        if (kw < 0) {
+            unsigned dummy = 0;
+            const unsigned T = rws_kth_bits<J>(mk, m, k, dummy);
+            kw = rws_take<J>(mk, mp, m, k, T, sk + wv * 64, sp + wv * 64);
+        }
     }
     if (lane == 0) scnt[wv] = kw;
     RR_MARK(5);  // wave-local select
+    RR_STAMP_Q(rr_q, 7);
     __syncthreads();
     if (wv != 0) return;
     // wave 0: the ≤ WV·k survivors, in wave order, compacted into its own run, then the k best
@@ -1582,10 +1645,15 @@ __device__ __forceinline__ void rerank_wave_select(const float *__restrict__ pd,
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     int nsel = m0;
-    if (m0 > k) {
+    if (m0 > k && m0 <= 64) {  // (k <= 16: always) one register
+        unsigned dummy = 0;
+        const unsigned T = rws_kth_bits<1>(mk, m0, k, dummy);
+        nsel = rws_take<1>(mk, mp, m0, k, T, sk, sp);  // wave 0's survivor slots are free again
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    } else if (m0 > k) {
         unsigned dummy = 0;
         const unsigned T = rws_kth_bits<WV>(mk, m0, k, dummy);
-        nsel = rws_take<WV>(mk, mp, m0, k, T, sk, sp);  // wave 0's survivor slots are free again
+        nsel = rws_take<WV>(mk, mp, m0, k, T, sk, sp);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     } else {
         for (int e = lane; e < m0; e += 64) { sk[e] = mk[e]; sp[e] = mp[e]; }
@@ -1820,6 +1888,7 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
     if (q >= nq) return;
     const int lane = threadIdx.x & 63;
     const int wv = WV == 1 ? 0 : (int)(threadIdx.x >> 6);
+    RR_STAMP(0);
     long long rr_t = HIPANN_RR_PROF ? clock64() : 0;
     // 1. the k best (scan key, row) of the query's partial lists (kslot entries per slot)
     WaveList<1, int> L;
@@ -1829,6 +1898,7 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
     const int64_t s0 = slot_off ? slot_off[q * nprobe] : q * nprobe;
     const int64_t s1 = slot_off ? slot_off[(q + 1) * nprobe] : (q + 1) * nprobe;
     const int64_t total = (s1 - s0) * kslot;
+    if constexpr (HIPANN_RR_STAMP != 0) { if (total >= 0) RR_STAMP(1); }
     pd += s0 * kslot;
     pi += s0 * kslot;
     // sub-list slots (the IVF scans at request_k > 12, mf_finish_item): T_sub = qbound[q], the smallest k-th key
@@ -1892,9 +1962,13 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
 #else
             __shared__ float wk[WV * 64 * RS_J];
             __shared__ int wp[WV * 64 * RS_J];
-            rerank_wave_select<WV, RS_J>(pd, pi, total, k, nrows, bound, wk, wp, sd, si, scnt[0], L, sel_bad, rr_t);
+            __shared__ float ntk[WV * 64];
+            __shared__ int ntp[WV * 64];
+            rerank_wave_select<WV, RS_J>(pd, pi, total, k, nrows, bound, wk, wp, sd, si, scnt[0], L, sel_bad, rr_t, q,
+                                         ntk, ntp);
 #endif
             if (wv == 0) srow[lane] = lane < k ? L.id[0] : IdTraits<int>::pad();
+            RR_STAMP(2);
         } else {
             sd[wv * 64 + lane] = lane < k ? L.d[0] : __builtin_inff();
             si[wv * 64 + lane] = lane < k ? L.id[0] : IdTraits<int>::pad();
@@ -1929,6 +2003,7 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
             }
         }
         __syncthreads();
+        RR_STAMP(3);
         RR_MARK(3);  // distances
         if (wv != 0) return;
         myrow = L.id[0];
@@ -2017,6 +2092,7 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
         }
     }
     if constexpr (WV > 1) RR_MARK(4);  // (distance, label) order + tie rule
+    RR_STAMP(4);
     // 4. exactness check
     const float dk = readlane_f(R.d[0], kout - 1);
     float E;
@@ -2052,6 +2128,7 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
         D[q * kout + lane] = pad ? pad_d : (IP ? -R.d[0] : R.d[0]);
         I[q * kout + lane] = pad ? -1 : (int64_t)R.id[0];
     }
+    RR_STAMP(5);
     if constexpr (WV > 1) {
         RR_MARK(8);  // bound check + write
 #if HIPANN_RR_PROF
@@ -2275,6 +2352,20 @@ void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int 
 // tuning builds (HIPANN_RR_PROF): the wide rerank's wave-0 clock sums per phase — [0] setup, [1] candidate loads,
 // [5] bound count, [2] compaction / search + sort, [3] distances, [4] order + ties, [8] bound check + write — and the
 // counts [6] compaction path, [9] list path, [7] queries (16 entries); reset after reading
+// tuning builds (HIPANN_RR_STAMP): per query q < 4096 eight s_memrealtime stamps (100 MHz) — [0] entry, [1] slot range
+// known, [6] candidates loaded and compacted, [7] wave 0's wave-local select done, [2] candidates selected,
+// [3] distances done, [4] order done, [5] written (tools/rr_stamps.py)
+extern "C" int hipann_debug_rr_stamps(long long *out, int n) {
+#if HIPANN_RR_STAMP
+    if (n > 4096 * 8 || hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(rr_stamp), sizeof(long long) * (size_t)n) == hipSuccess ? 0 : -1;
+#else
+    (void)out;
+    (void)n;
+    return -1;
+#endif
+}
+
 extern "C" int hipann_debug_rr_prof(unsigned long long *out16) {
 #if HIPANN_RR_PROF
     if (hipDeviceSynchronize() != hipSuccess) return -1;
