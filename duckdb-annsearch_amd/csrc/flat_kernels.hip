@@ -1163,6 +1163,132 @@ rows_select_small(const float *__restrict__ keys, int64_t ldk, int ncols, int64_
     }
 }
 
+// rows_select_narrow — rows_select_small's output (and the IVF plan's count step) for rows of 257..64·J keys, one wave
+// per row, narrowed as flat_keys_kth: T_hi = the k-th smallest of the 64 lanes' minima (k keys lie at or below it, so
+// the k-th smallest key does too), the keys ≤ T_hi compacted into LDS in column order (≈ k + a few for i.i.d. rows),
+// then the exact k-th T over that list by the one-register bitwise search and the take (keys < T, then the first keys
+// == T by column) — the same k (key, column) pairs as the search over the whole row, in 2 × 32 one-ballot steps
+// instead of 32 × J.  A list longer than 64 (a row with more than 64 keys at or below T_hi) takes the whole-row search.
+// r05: the coarse select of the IVF headline 12.9 → see DESIGN §5; the extension's nq = 1 call 9.7 µs (one
+// block's 32 barrier-separated steps) → one wave.
+template <int J>
+__global__ void __launch_bounds__(256)
+rows_select_narrow(const float *__restrict__ keys, int64_t ldk, int ncols, int64_t nq, int k, int kout,
+                   int64_t label_offset, float out_sign, float *__restrict__ D, int64_t *__restrict__ I,
+                   const int *__restrict__ list_len, int nlist, int chunk_rows, int *__restrict__ ccnt,
+                   int *__restrict__ slot_off, int *__restrict__ qtot) {
+    __shared__ float sk[4][64];
+    __shared__ int sc[4][64];
+    __shared__ float tk[4][64];
+    __shared__ int tc[4][64];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t q = (int64_t)blockIdx.x * 4 + wv;
+    if (q >= nq) return;  // (no block barrier below: each wave's LDS rows are its own)
+    const float *row = keys + q * ldk;
+    float v[J];
+    unsigned u[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const int c = 64 * j + lane;
+        v[j] = c < ncols ? row[c] : __builtin_nanf("");
+    }
+    unsigned mn = 0xffffffffu;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const float f = v[j] == 0.f ? 0.f : v[j];
+        const unsigned b = __float_as_uint(f);
+        u[j] = v[j] == v[j] ? ((b >> 31) ? ~b : (b | 0x80000000u)) : 0xffffffffu;
+        mn = min(mn, u[j]);
+    }
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    // T_hi: the k-th smallest lane minimum (as rows_select_small's search: the largest T with #{< T} < k)
+    unsigned th = 0;
+    for (int bit = 31; bit >= 0; --bit) {
+        const unsigned cand = th | (1u << bit);
+        if ((int)__popcll(__ballot(mn < cand)) < k) th = cand;
+    }
+    // the keys ≤ T_hi in column order
+    int c = 0;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const bool a = u[j] <= th && u[j] != 0xffffffffu;
+        const unsigned long long ma = __ballot(a);
+        const int p = c + (int)__popcll(ma & lt);
+        if (a && p < 64) { tk[wv][p] = v[j]; tc[wv][p] = 64 * j + lane; }
+        c += (int)__popcll(ma);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    unsigned T = 0;
+    if (c <= 64) {
+        const float f0 = lane < c ? tk[wv][lane] : 0.f;
+        const float f = f0 == 0.f ? 0.f : f0;
+        const unsigned b = __float_as_uint(f);
+        const unsigned ul = lane < c ? ((b >> 31) ? ~b : (b | 0x80000000u)) : 0xffffffffu;
+        for (int bit = 31; bit >= 0; --bit) {
+            const unsigned cand = T | (1u << bit);
+            if ((int)__popcll(__ballot(ul < cand)) < k) T = cand;
+        }
+    } else {  // the whole row
+        for (int bit = 31; bit >= 0; --bit) {
+            const unsigned cand = T | (1u << bit);
+            int cnt = 0;
+#pragma unroll
+            for (int j = 0; j < J; ++j) cnt += __popcll(__ballot(u[j] < cand));
+            if (cnt < k) T = cand;
+        }
+    }
+    // the take, from the row's registers (column order): keys < T, then the first keys == T
+    int base = 0;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const bool s = u[j] < T;
+        const unsigned long long m = __ballot(s);
+        if (s) {
+            const int pos = base + __popcll(m & lt);
+            sk[wv][pos] = v[j];
+            sc[wv][pos] = 64 * j + lane;
+        }
+        base += __popcll(m);
+    }
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+        const bool s = u[j] == T && u[j] != 0xffffffffu;
+        const unsigned long long m = __ballot(s);
+        if (s) {
+            const int pos = base + __popcll(m & lt);
+            if (pos < k) {
+                sk[wv][pos] = v[j];
+                sc[wv][pos] = 64 * j + lane;
+            }
+        }
+        base += __popcll(m);
+    }
+    const int nsel = base < k ? base : k;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    float kk = lane < nsel ? sk[wv][lane] : __builtin_inff();
+    int cc = lane < nsel ? sc[wv][lane] : 0x7fffffff;
+    wave_rank_sort(kk, cc, nsel);
+    const bool pad = lane >= nsel || kk == __builtin_inff();
+    if (lane < kout) {
+        D[q * kout + lane] = pad ? (out_sign > 0.f ? __builtin_inff() : -__builtin_inff()) : kk * out_sign;
+        I[q * kout + lane] = pad ? -1 : (int64_t)cc + label_offset;
+    }
+    if (ccnt) {  // the IVF plan's per-query step (ivf_count_q) on the probes just selected (kout ≤ 64)
+        const int64_t l = lane < kout && !pad ? (int64_t)cc + label_offset : -1;
+        const int len = l >= 0 && l < nlist ? list_len[l] : 0;
+        if (len > 0) atomicAdd(ccnt + (int64_t)(q % kPlanCopies) * nlist + l, 1);
+        const int vv = len > 0 ? (len + chunk_rows - 1) / chunk_rows : 0;
+        int x = vv;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int t = __shfl_up(x, o);
+            if (lane >= o) x += t;
+        }
+        if (lane < kout) slot_off[q * kout + lane] = x - vv;
+        if (lane == 63) qtot[q] = x;
+    }
+}
+
 // rows_select_block — rows of 257..1024 keys: rows_select_small's select with the row spread over a
 // block of 4 waves (column c = 256·wave + 64·j + lane, J = 4 registers per lane); each search step sums
 // the waves' ballot counts through LDS (one barrier), the compaction runs in (wave, j, lane) = column
@@ -1835,8 +1961,13 @@ bool launch_rows_select_out(const float *keys, int64_t ldk, int64_t ncols, int64
         const int *ll = h ? hook->list_len : nullptr;
         const int nl = h ? hook->nlist : 0, cr = h ? hook->chunk_rows : 1;
         int *cc = h ? hook->ccnt : nullptr, *so = h ? hook->slot_off : nullptr, *qt = h ? hook->qtot : nullptr;
+        // HIPANN_ROWSEL_NARROW=0 (A/B): rows of 257..1024 keys on the block select instead of the narrowed wave
+        static const bool narrow = [] { const char *e = std::getenv("HIPANN_ROWSEL_NARROW"); return !e || std::atoi(e); }();
         if (ncols <= 256)
             hipLaunchKernelGGL(rows_select_small<4>, grid, block, 0, st, keys, ldk, (int)ncols, nq, k, kout,
+                               label_offset, out_sign, D, I, ll, nl, cr, cc, so, qt);
+        else if (narrow)
+            hipLaunchKernelGGL(rows_select_narrow<16>, grid, block, 0, st, keys, ldk, (int)ncols, nq, k, kout,
                                label_offset, out_sign, D, I, ll, nl, cr, cc, so, qt);
         else if (!one_wave_rows())
             hipLaunchKernelGGL(rows_select_block, dim3((unsigned)nq), block, 0, st, keys, ldk, (int)ncols, nq, k, kout,
