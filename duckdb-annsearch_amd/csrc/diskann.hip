@@ -763,7 +763,7 @@ void host_bfs(DiskDB *db, const uint32_t *adj, int R, const uint32_t *eps, int n
         for (auto &g : grp) {
             if (g.done) continue;
             auto t0 = clk::now();
-            if (g.launched) HIPANN_CHECK(hipEventSynchronize(g.ev));
+            if (g.launched) wait_event(g.ev);
             auto t1 = clk::now();
             const int64_t head = phase(g);
             auto t2 = clk::now();

@@ -1843,10 +1843,23 @@ void launch_copy_words(const void *src, void *dst, size_t bytes, hipStream_t st)
     HIPANN_CHECK(hipGetLastError());
 }
 
+__global__ void __launch_bounds__(64) post_words(const unsigned *__restrict__ src, unsigned *__restrict__ dst,
+                                                 int words, unsigned token) {
+    for (int i = threadIdx.x; i < words; i += 64) dst[i] = src[i];
+    __threadfence_system();  // the words reach the host before the token does
+    if (threadIdx.x == 0) __hip_atomic_store(dst + words, token, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 void *host_device_ptr(void *pinned) {
     void *p = nullptr;
     HIPANN_CHECK(hipHostGetDevicePointer(&p, pinned, 0));
     return p;
+}
+
+void launch_post_words(const void *src, void *host_dst, int words, unsigned token, hipStream_t st) {
+    hipLaunchKernelGGL(post_words, dim3(1), dim3(64), 0, st, static_cast<const unsigned *>(src),
+                       static_cast<unsigned *>(host_device_ptr(host_dst)), words, token);
+    HIPANN_CHECK(hipGetLastError());
 }
 
 size_t scan_smem_bytes(int nq, int d);

@@ -340,10 +340,11 @@ static std::vector<int64_t> flat_pass_plan(int64_t tps, int64_t nsplit, int64_t 
 }
 
 // The flag count of the launch phase's bound check into the shard's pinned host word (a copy kernel through its
-// device mapping, no DMA round trip); the host reads it after its next synchronisation with `st`.
+// device mapping, no DMA round trip), then a fresh token into the word after it; the host reads the count after
+// its next synchronisation with `st` (or once the token arrives, wait_posted).
 static void flag_readback(FlatShard &sh, hipStream_t st) {
-    sh.h_nflag.ensure(sizeof(int));
-    launch_copy_words(sh.nflag.p, host_device_ptr(sh.h_nflag.p), sizeof(int), st);
+    if (sh.h_nflag.ensure(2 * sizeof(unsigned), hipHostMallocCoherent)) sh.h_nflag.get<unsigned>()[1] = sh.flag_seq;
+    launch_post_words(sh.nflag.p, sh.h_nflag.p, 1, ++sh.flag_seq, st);
 }
 
 // Launch phase of a shard search: every kernel of the search up to the exact forms' flag count, enqueued on `st`
@@ -855,7 +856,7 @@ void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq
     FlatPending local;
     flat_shard_launch(ix, sh, nq, xq, k, kout, D, I, st, form_override, pend ? *pend : local);
     if (pend || local.kind == FlatPending::kNone) return;
-    HIPANN_CHECK(hipStreamSynchronize(st));
+    wait_posted(sh.h_nflag.get<unsigned>() + 1, sh.flag_seq, st);  // the flag count's token: the launch phase is done
     ++ix.host_syncs;
     flat_shard_finish(ix, sh, local, st);
 }

@@ -52,12 +52,14 @@ struct HostBuf {
     HostBuf(const HostBuf &) = delete;
     HostBuf &operator=(const HostBuf &) = delete;
     ~HostBuf() { if (p) (void)hipHostFree(p); }
-    void ensure(size_t need) {
-        if (need <= bytes && p) return;
+    // (returns true when it allocated: the contents are undefined then)
+    bool ensure(size_t need, unsigned flags = hipHostMallocDefault) {
+        if (need <= bytes && p) return false;
         if (p) (void)hipHostFree(p);
         p = nullptr;
-        HIPANN_CHECK(hipHostMalloc(&p, need < 256 ? 256 : need, hipHostMallocDefault));
+        HIPANN_CHECK(hipHostMalloc(&p, need < 256 ? 256 : need, flags));
         bytes = need < 256 ? 256 : need;
+        return true;
     }
     template <typename T> T *get() const { return static_cast<T *>(p); }
 };
@@ -126,6 +128,46 @@ struct TimerPause {
 // lists, flags).  The handle mutex only covers enqueueing, so a call on another stream must not start
 // before the previous call's kernels are done with that scratch: each call waits for the event the
 // previous call recorded (when the streams differ) and records its own at the end.
+// Host waits by polling instead of blocking.  hipStreamSynchronize / hipEventSynchronize may put the thread to
+// sleep until the completion interrupt, whose wake-up adds tens of µs to every short call (r05 C2 traces: a 44 µs
+// idle gap before each search after the previous one's synchronisation).  HIPANN_SPIN_WAIT=0 (A/B): the blocking
+// calls.
+inline bool spin_wait() {
+    static const bool v = [] { const char *e = std::getenv("HIPANN_SPIN_WAIT"); return !e || std::atoi(e) != 0; }();
+    return v;
+}
+// until `ev` has completed (hipEventQuery in a pause loop; errors surface as from the blocking call)
+inline void wait_event(hipEvent_t ev) {
+    if (!spin_wait()) {
+        HIPANN_CHECK(hipEventSynchronize(ev));
+        return;
+    }
+    for (;;) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e == hipSuccess) return;
+        if (e != hipErrorNotReady) HIPANN_CHECK(e);
+        for (int i = 0; i < 16; ++i) __builtin_ia32_pause();
+    }
+}
+// until the token word `tok` (written by launch_post_words, the last work on `st`) reads `token`: every earlier
+// kernel on the stream has completed then.  The stream is queried now and then, so a failed or finished stream
+// ends the wait too (its error raised as hipStreamSynchronize would).
+inline void wait_posted(const volatile unsigned *tok, unsigned token, hipStream_t st) {
+    if (!spin_wait()) {
+        HIPANN_CHECK(hipStreamSynchronize(st));
+        return;
+    }
+    for (unsigned it = 1;; ++it) {
+        if (__atomic_load_n(tok, __ATOMIC_ACQUIRE) == token) return;
+        if ((it & 1023) == 0) {
+            const hipError_t e = hipStreamQuery(st);
+            if (e == hipSuccess) return;
+            if (e != hipErrorNotReady) HIPANN_CHECK(hipStreamSynchronize(st));
+        }
+        __builtin_ia32_pause();
+    }
+}
+
 struct StreamFence {
     hipEvent_t ev = nullptr;
     hipStream_t last = nullptr;
@@ -219,7 +261,9 @@ struct FlatShard {
     bool xi8_ok = false;
     float i8_rxmax = 0.f;
     StreamFence fence;       // cross-stream ordering of this shard's calls
-    HostBuf h_nflag;         // the launch phase's flag count, read back with the results (flat_shard_finish)
+    HostBuf h_nflag;         // the launch phase's flag count, read back with the results (flat_shard_finish),
+                             // and the token word after it (wait_posted)
+    unsigned flag_seq = 0;   // the last token posted
     DevBuf app_stat;         // an append's new-row maxima (‖x‖², int8 residual, bf16 residual²)
     hipEvent_t done = nullptr;  // multi-device search: the shard's launch phase has drained (shard 0's stream waits)
 };
@@ -369,6 +413,10 @@ struct IvfIndex : IndexBase {
 // the pinned buffers' device mapping instead of DMA round trips
 constexpr size_t kKernelCopyMax = (size_t)64 << 10;
 void launch_copy_words(const void *src, void *dst, size_t bytes, hipStream_t st);
+// `words` words from device memory to a pinned host buffer (through its device mapping), then `token` into the
+// word after them once the copy is visible to the host: the host spins on the token (wait_posted) instead of a
+// stream synchronisation.
+void launch_post_words(const void *src, void *host_dst, int words, unsigned token, hipStream_t st);
 void *host_device_ptr(void *pinned);
 void launch_row_norms(const float *x, int64_t n, int d, float *out, hipStream_t st);
 size_t gemm_smem_bytes();
