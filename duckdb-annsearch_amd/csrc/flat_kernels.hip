@@ -1741,6 +1741,130 @@ flat_keys_ksplit(const float *__restrict__ Q, const float *__restrict__ qnorm, i
     }
 }
 
+// flat_keys_bf3 — flat_keys_ksplit's tiles and K split (64 × 64 keys per block, waves 0-3 the first half of the
+// 32-dim chunks, waves 4-7 the second, half 1's accumulators added by half 0 through LDS) with q·x on the bf16
+// matrix cores: both operands are split while they are staged into LDS into three round-to-nearest bf16 terms
+// (fb_split4: x = x₁ + x₂ + x₃ exactly for normal floats), and each 16-dim step runs flat_gemm_topk_bf's six term
+// products (FbProducts<3>, smallest first; the dropped ones are ≤ 2⁻²⁶ relative) on v_mfma_f32_32x32x16_bf16
+// with fp32 accumulation: fp32-level keys at 0.375 of the fp32 matrix-core time (the IVF coarse quantizer,
+// HIPANN_COARSE_BF3).  LDS rows of 32 dims are 80 B (64 + 16 pad): a b128 fragment read by 16 lanes of 16
+// consecutive rows touches 16 distinct 4-bank groups.  LDS: [half][buffer][term][64 query rows + 64 table rows]
+// × 80 B = 120 KiB (one block per CU, as flat_keys_ksplit).
+constexpr int KB3_ROW = 80;                 // bytes per staged row (32 bf16 + pad)
+constexpr int KB3_TERM = 128 * KB3_ROW;     // one term of one buffer: 64 query rows then 64 table rows
+constexpr int KB3_BUF = 3 * KB3_TERM;
+__device__ __forceinline__ void kb3_stage_store(char *__restrict__ buf, int rowbase, int t, const float4 (&r)[2]) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        const int f = t + 256 * p;
+        const int row = rowbase + (f >> 3), c4 = f & 7;
+        uint2 o[3];
+        fb_split4<3>(r[p], o);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) *reinterpret_cast<uint2 *>(buf + j * KB3_TERM + row * KB3_ROW + 8 * c4) = o[j];
+    }
+}
+
+template <bool VEC4, int NS>
+__global__ void __launch_bounds__(512)
+flat_keys_bf3(const float *__restrict__ Q, const float *__restrict__ qnorm, int64_t nq, const float *__restrict__ X,
+              const float *__restrict__ xnorm, int64_t N, int d, int metric, int nqt, float *__restrict__ keys_out,
+              int64_t ldk) {
+    __shared__ __attribute__((aligned(16))) char lds[2 * 2 * KB3_BUF];
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int qt = lb % nqt;
+    const int64_t q0 = (int64_t)qt * SBM, x0 = (int64_t)(lb / nqt) * SBM;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int half = wave >> 2, t = threadIdx.x & 255;
+    const int wr = (wave >> 1) & 1, wc = wave & 1;
+    const int l31 = lane & 31, h = lane >> 5;
+    const int nkh = ((d + GBK - 1) / GBK) >> 1;  // chunks per half (the launcher checks the count is even)
+    const int kbase = half * nkh * GBK;
+    char *hb = lds + half * 2 * KB3_BUF;  // this half's two buffers
+    // NS chunks in flight in registers (set = chunk mod NS) ahead of the LDS buffer being multiplied (2: as
+    // flat_keys_ksplit; deeper rings measured no faster, see the launcher)
+    float4 sa[NS][2], sb[NS][2];
+    ks_stage_load<VEC4>(Q, q0, nq, d, kbase, t, sa[0]);
+    ks_stage_load<VEC4>(X, x0, N, d, kbase, t, sb[0]);
+    kb3_stage_store(hb, 0, t, sa[0]);
+    kb3_stage_store(hb, 64, t, sb[0]);
+#pragma unroll
+    for (int c = 1; c <= NS; ++c)
+        if (c < nkh) {
+            ks_stage_load<VEC4>(Q, q0, nq, d, kbase + c * GBK, t, sa[c % NS]);
+            ks_stage_load<VEC4>(X, x0, N, d, kbase + c * GBK, t, sb[c % NS]);
+        }
+    __syncthreads();
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    // this lane's fragment offsets: query row 32·wr + l31 (A), table row 64 + 32·wc + l31 (B), dims 8h.. of each
+    // 16-dim step s
+    const int aoff = (32 * wr + l31) * KB3_ROW + 16 * h, boff = (64 + 32 * wc + l31) * KB3_ROW + 16 * h;
+    // step kc (U = lcm(2, NS) consecutive steps unrolled: LDS buffer kc & 1, register set (kc + 1) mod NS)
+    auto step = [&](int kc, auto u_c) __attribute__((always_inline)) {
+        constexpr int U = decltype(u_c)::value;
+        constexpr int P = U & 1, S1 = (U + 1) % NS;
+        const char *b = hb + P * KB3_BUF;
+        uint4 af[3][2], bf[3][2];
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                af[j][s] = *reinterpret_cast<const uint4 *>(b + j * KB3_TERM + aoff + 32 * s);
+                bf[j][s] = *reinterpret_cast<const uint4 *>(b + j * KB3_TERM + boff + 32 * s);
+            }
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int pr = 0; pr < FbProducts<3>::n; ++pr)
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(fb_bf16x8, af[FbProducts<3>::a(pr)][s]),
+                                                              __builtin_bit_cast(fb_bf16x8, bf[FbProducts<3>::b(pr)][s]),
+                                                              acc, 0, 0, 0);
+        if (kc + 1 < nkh) {
+            char *nb = hb + (1 - P) * KB3_BUF;
+            kb3_stage_store(nb, 0, t, sa[S1]);
+            kb3_stage_store(nb, 64, t, sb[S1]);
+            if (kc + 1 + NS < nkh) {
+                ks_stage_load<VEC4>(Q, q0, nq, d, kbase + (kc + 1 + NS) * GBK, t, sa[S1]);
+                ks_stage_load<VEC4>(X, x0, N, d, kbase + (kc + 1 + NS) * GBK, t, sb[S1]);
+            }
+        }
+        __syncthreads();
+    };
+    constexpr int UN = NS % 2 == 0 ? NS : 2 * NS;
+    for (int kc = 0; kc < nkh; kc += UN) {
+        [&]<int... U>(std::integer_sequence<int, U...>) __attribute__((always_inline)) {
+            ((kc + U < nkh ? step(kc + U, std::integral_constant<int, U>{}) : void()), ...);
+        }(std::make_integer_sequence<int, UN>{});
+    }
+    float *xch = reinterpret_cast<float *>(lds);
+    if (half == 1) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) xch[(r * 4 + (wave & 3)) * 64 + lane] = acc[r];
+    }
+    __syncthreads();
+    if (half == 1) return;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] += xch[(r * 4 + wave) * 64 + lane];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int64_t q = q0 + 32 * wr + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int64_t x = x0 + 32 * wc + l31;
+        if (q < nq && x < N) {
+            const float ip = acc[r];
+            float key;
+            if (metric == kL2) {
+                key = fmaf(-2.f, ip, qnorm[q] + xnorm[x]);
+                key = key < 0.f ? 0.f : key;
+            } else {
+                key = -ip;
+            }
+            keys_out[q * ldk + x] = key;
+        }
+    }
+}
+
 // flat_keys_direct — the same 64 × 64 tiles, MFMAs and k order as flat_keys_small (bit-identical keys), but every
 // wave loads its own A / B fragments straight from memory into a 3-chunk register ring: no LDS staging, no
 // per-chunk barrier.  The inputs are small and cache-resident (the coarse quantizer's queries and centroids),
@@ -1865,7 +1989,7 @@ void launch_post_words(const void *src, void *host_dst, int words, unsigned toke
 size_t scan_smem_bytes(int nq, int d);
 
 void launch_flat_gemm_keys(const float *Q, const float *qn, int64_t nq, const float *X, const float *xn, int64_t N,
-                           int d, int metric, float *keys, int64_t ldk, hipStream_t st) {
+                           int d, int metric, float *keys, int64_t ldk, hipStream_t st, bool bf3) {
     const int nqt = (int)ceil_div(nq, GBM);
     const int64_t ntiles = ceil_div(N, GBN);
     const bool vec4 = (d % 4 == 0) && ((uintptr_t)Q % 16 == 0) && ((uintptr_t)X % 16 == 0);
@@ -1879,7 +2003,21 @@ void launch_flat_gemm_keys(const float *Q, const float *qn, int64_t nq, const fl
         // dropped at r04: four K-groups of 4 waves (24.0 µs) and 64-dim stages (25.0 µs) against 23.9 µs.
         static const int mode = [] { const char *e = std::getenv("HIPANN_KEYS"); return e ? std::atoi(e) : 2; }();
         const int nk = (d + GBK - 1) / GBK;
-        if (mode == 2 && nk % 2 == 0) {  // default: the K-split tiles (8 waves, two per SIMD)
+        // the IVF coarse quantizer: the same tiles on the bf16 matrix cores (3 terms): 25.4 → 22.6-23.0 µs at 1024 ×
+        // 1024 × 768.  Not the matrix cores' time (3.8 µs) and not the loads' depth: HIPANN_KEYS_DEPTH = 4 / 6 chunks
+        // in flight (22.6 / 23.4 / 23.3 µs for 2 / 4 / 6) and two or four independent accumulator chains (22.8 / 22.6
+        // vs 23.7 µs) were measured and left out; PMC: matrix cores busy ≈ 15 %, TD ≈ 33 %, TA ≈ 20 % of the kernel
+        static const int depth = [] { const char *e = std::getenv("HIPANN_KEYS_DEPTH"); return e ? std::atoi(e) : 2; }();
+        if (bf3 && nk % 2 == 0) {
+#define HIPANN_KB3(NS)                                                                                                    \
+    do {                                                                                                                \
+        if (vec4) hipLaunchKernelGGL((flat_keys_bf3<true, NS>), g, dim3(512), 0, st, Q, qn, nq, X, xn, N, d, metric, sq, keys, ldk); \
+        else hipLaunchKernelGGL((flat_keys_bf3<false, NS>), g, dim3(512), 0, st, Q, qn, nq, X, xn, N, d, metric, sq, keys, ldk); \
+    } while (0)
+            if (depth >= 4) HIPANN_KB3(4);
+            else HIPANN_KB3(2);
+#undef HIPANN_KB3
+        } else if (mode == 2 && nk % 2 == 0) {  // default: the K-split tiles (8 waves, two per SIMD)
             if (vec4) hipLaunchKernelGGL(flat_keys_ksplit<true>, g, dim3(512), 0, st, Q, qn, nq, X, xn, N, d, metric, sq, keys, ldk);
             else hipLaunchKernelGGL(flat_keys_ksplit<false>, g, dim3(512), 0, st, Q, qn, nq, X, xn, N, d, metric, sq, keys, ldk);
         } else if (mode == 3) {

@@ -215,7 +215,7 @@ static void flat_shard_search_bigk(FlatIndex &ix, FlatShard &sh, int64_t nq, con
                 launch_flat_scan_keys(xq, (int)nq, sh.xb, sh.n, d, metric, sh.keys.get<float>(), C, st);
             else
                 launch_flat_gemm_keys(xq, qn, nq, sh.xb, sh.xn.get<float>(), sh.n, d, metric, sh.keys.get<float>(), C,
-                                      st);
+                                      st, sh.keys_bf3);
         }
         {  // kout ≤ 256: one wave selects the whole row and writes the output (no segment lists, no merge)
             ScopedTiming t(ix.timer_merge, st);

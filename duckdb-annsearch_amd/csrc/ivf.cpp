@@ -57,6 +57,18 @@ hipStream_t make_stream(int dev) {
     return s;
 }
 
+// The search-time coarse step's key GEMM on the bf16 matrix cores (flat_keys_bf3: three-term split, fp32-level
+// keys; HIPANN_COARSE_BF3=0 keeps the fp32 matrix cores, A/B).  List assignment (add / append) keeps fp32.
+static bool coarse_bf3() {
+    static const bool v = [] { const char *e = std::getenv("HIPANN_COARSE_BF3"); return !e || std::atoi(e) != 0; }();
+    return v;
+}
+struct CoarseKeysScope {
+    FlatShard &s;
+    explicit CoarseKeysScope(FlatShard &x) : s(x) { s.keys_bf3 = coarse_bf3(); }
+    ~CoarseKeysScope() { s.keys_bf3 = false; }
+};
+
 // Borrowed-centroid coarse quantizer on the shard's device.
 std::unique_ptr<FlatIndex> make_quantizer(int d, int metric, const float *cen, int nlist, int device,
                                           hipStream_t stream) {
@@ -344,6 +356,7 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
                                     st));
     } else {
         qsh.plan_hook = ivf_plan_query_major() && hook_env ? &hook : nullptr;
+        CoarseKeysScope ck(qsh);
         try {
             flat_shard_search(*sh.quant, qsh, nq, xq, np, np, sh.coarse_d.get<float>(), sh.coarse_i.get<int64_t>(), st);
         } catch (...) {
@@ -1001,6 +1014,7 @@ int hipann_ivf_coarse_device(void *h, int64_t nq, const float *xq_dev, int64_t *
         FenceScope fs(sh.fence, st, sh.device);
         sh.app_cd.ensure(sizeof(float) * (size_t)nq * np, sh.device);
         // FAISS quantizer->search(nq, x, nprobe): the Flat rules of the coarse quantizer (exact fp32 products)
+        CoarseKeysScope ck(*sh.quant->shards[0]);
         flat_shard_search(*sh.quant, *sh.quant->shards[0], nq, xq_dev, np, np, sh.app_cd.get<float>(), probes_dev, st);
         return 0;
     });

@@ -254,6 +254,7 @@ struct FlatShard {
     DevBuf xb16, qimg, seed;
     DevBuf cand;  // bounded passes: per-(query, split) candidate buffers and counts
     bool xb16_ok = false;
+    bool keys_bf3 = false;    // the small-table key GEMM on the bf16 matrix cores (3 terms): the IVF coarse step
     float bf16_rxmax = 0.f;  // max over rows of ‖bf16(x) − x‖ (the rerank's bound)
     // kFlatI8Exact: tiled int8 image, per-row scales, max row residual ‖x − s·x̂‖; the batch's query scales and
     // residuals (the rerank's query term)
@@ -429,7 +430,7 @@ void launch_flat_gemm_topk_bf(int np, const float *Q, const float *qn, int64_t n
                               float *pd, int *pi, int qmajor, hipStream_t st);
 size_t scan_smem_bytes(int nq, int d);
 void launch_flat_gemm_keys(const float *Q, const float *qn, int64_t nq, const float *X, const float *xn, int64_t N,
-                           int d, int metric, float *keys, int64_t ldk, hipStream_t st);
+                           int d, int metric, float *keys, int64_t ldk, hipStream_t st, bool bf3 = false);
 void launch_flat_scan_keys(const float *Q, int nq, const float *X, int64_t N, int d, int metric, float *keys,
                            int64_t ldk, hipStream_t st);
 void launch_rows_topk(const float *keys, int64_t ldk, int64_t ncols, int64_t nq, int64_t seg_len, int nseg, int k,
