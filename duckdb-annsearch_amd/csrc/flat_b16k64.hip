@@ -927,6 +927,82 @@ __global__ void __launch_bounds__(256) i8_tile_rows(const float *__restrict__ X,
     out[u] = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// The batch's int8 query preparation in one launch (the bounded passes' queries): one wave per row of the padded
+// tiles — ‖q‖² (optional, row_norms_f32's order and bits), i8_row_scale's scale and residual (same order), and the
+// row's units of i8_tile_rows' image (padding rows: zero units).  Three dependent launches were ≈ 16 µs of kernels
+// plus their host launch time at the start of every C2 search (r05 runtime trace).
+__global__ void __launch_bounds__(256) i8_query_prep(const float *__restrict__ X, int64_t n, int d, int vec4,
+                                                     float *__restrict__ qn, float *__restrict__ scale,
+                                                     float *__restrict__ resid, int R, int nk, int64_t npad,
+                                                     uint4 *__restrict__ out) {
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= npad) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t t = row / R;
+    const int rin = (int)(row - t * R);
+    if (row >= n) {  // a padding row of the last tile
+        for (int uc = lane; uc < nk * 4; uc += 64) {
+            const int kc = uc >> 2, c = uc & 3;
+            out[((t * nk + kc) * 4 + c) * R + (rin ^ (c << 1))] = make_uint4(0u, 0u, 0u, 0u);
+        }
+        return;
+    }
+    const float *x = X + row * (int64_t)d;
+    if (qn) {
+        float s2 = 0.f;
+        if (vec4) {
+            const float4 *p4 = reinterpret_cast<const float4 *>(x);
+            for (int j = lane; j < (d >> 2); j += 64) {
+                const float4 v = p4[j];
+                s2 = fmaf(v.x, v.x, s2); s2 = fmaf(v.y, v.y, s2); s2 = fmaf(v.z, v.z, s2); s2 = fmaf(v.w, v.w, s2);
+            }
+        } else {
+            for (int j = lane; j < d; j += 64) s2 = fmaf(x[j], x[j], s2);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o);
+        if (lane == 0) qn[row] = s2;
+    }
+    float m = 0.f;
+    for (int e = lane; e < d; e += 64) m = fmaxf(m, fabsf(x[e]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    const float s = m > 0.f && m < 3.0e38f ? m / 127.f : 0.f;
+    float r2 = 0.f;
+    for (int e = lane; e < d; e += 64) {
+        const float r = x[e] - s * (float)i8_quant(x[e], s);
+        r2 = fmaf(r, r, r2);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) r2 += __shfl_xor(r2, o);
+    if (lane == 0) {
+        scale[row] = s;
+        resid[row] = m < 3.0e38f ? sqrtf(r2) * 1.0001f : __builtin_inff();
+    }
+    for (int uc = lane; uc < nk * 4; uc += 64) {
+        const int kc = uc >> 2, c = uc & 3;
+        const int dim0 = kc * I8_KC + 16 * c;
+        unsigned w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int v = dim0 + i < d ? i8_quant(x[dim0 + i], s) : 0;
+            w[i >> 2] |= ((unsigned)v & 0xffu) << (8 * (i & 3));
+        }
+        out[((t * nk + kc) * 4 + c) * R + (rin ^ (c << 1))] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+
+void launch_i8_query_prep(const float *X, int64_t n, int d, float *qn, float *scale, float *resid, int R, void *out,
+                          hipStream_t st) {
+    if (n <= 0) return;
+    const int nk = flat_i8_nk(d);
+    const int64_t npad = ceil_div(n, R) * R;
+    const int vec4 = (d % 4 == 0) && ((uintptr_t)X % 16 == 0);
+    hipLaunchKernelGGL(i8_query_prep, dim3((unsigned)ceil_div(npad, 4)), dim3(256), 0, st, X, n, d, vec4, qn, scale,
+                       resid, R, nk, npad, static_cast<uint4 *>(out));
+    HIPANN_CHECK(hipGetLastError());
+}
+
 void launch_i8_row_scale(const float *X, int64_t n, int d, float *scale, float *resid, hipStream_t st) {
     if (n <= 0) return;
     hipLaunchKernelGGL(i8_row_scale, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, st, X, n, d, scale, resid);

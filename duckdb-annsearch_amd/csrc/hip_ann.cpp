@@ -487,17 +487,23 @@ static void flat_shard_launch(FlatIndex &ix, FlatShard &sh, int64_t nq, const fl
                                 sh.label_offset, 1.f, out_sign, D, I, st);
         return;
     }
-    // BLAS form: ‖q‖² + ‖x‖² − 2 q·x on fp32 MFMA
+    // BLAS form: ‖q‖² + ‖x‖² − 2 q·x on fp32 MFMA.  ‖q‖² is launched by qn_now() ahead of its first reader (the int8
+    // bounded passes compute it inside their query preparation instead, the same bits)
     const float *qn = nullptr;
+    bool qn_launch = false;
     if (metric == kL2) {
         if (!(sh.qn_given == xq && sh.qn_given_nq == nq)) {
             sh.qn.ensure((size_t)nq * sizeof(float), sh.device);
-            launch_row_norms(xq, nq, d, sh.qn.get<float>(), st);
+            qn_launch = true;
         }
         qn = sh.qn.get<float>();
         sh.qn_of = xq;
         sh.qn_nq = nq;
     }
+    auto qn_now = [&]() {
+        if (qn_launch) launch_row_norms(xq, nq, d, sh.qn.get<float>(), st);
+        qn_launch = false;
+    };
     int form = form_override >= 0 ? form_override : ix.form;
     static const bool seed_env = [] { const char *e = std::getenv("HIPANN_FLAT_BF16_SEED"); return !e || std::atoi(e); }();
     // The exact forms keep kf candidates per query (per split and query on the list kernels) as the filter; the
@@ -557,6 +563,10 @@ static void flat_shard_launch(FlatIndex &ix, FlatShard &sh, int64_t nq, const fl
         ensure_i8_image(ix, sh, d, st);
         rxmax = sh.i8_rxmax;
     }
+    // HIPANN_I8_PREP_FUSED=0 (A/B): the int8 query preparation as row_norms + i8_row_scale + i8_tile_rows
+    static const bool prep_fused = [] { const char *e = std::getenv("HIPANN_I8_PREP_FUSED"); return !e || std::atoi(e); }();
+    const bool i8_prep = i8 && bounded && seed_env && sh.n >= 8 * 65536 && prep_fused;
+    if (!i8_prep) qn_now();
     if (form == kFlatBf16Exact || i8) {
         // one plain bf16 product per element over the tiled bf16 image (flat_bf16.hip), built once
         if (!i8 && !sh.xb16_ok) {
@@ -637,8 +647,14 @@ static void flat_shard_launch(FlatIndex &ix, FlatShard &sh, int64_t nq, const fl
             if (i8) {  // the queries' scales, residuals (the rerank's query term) and int8 image
                 sh.qscale.ensure(sizeof(float) * (size_t)nq, sh.device);
                 sh.qres.ensure(sizeof(float) * (size_t)nq, sh.device);
-                launch_i8_row_scale(xq, nq, d, sh.qscale.get<float>(), sh.qres.get<float>(), st);
-                launch_i8_tile_rows(xq, sh.qscale.get<float>(), nq, d, 32 * W, sh.qimg.p, st);
+                if (i8_prep) {
+                    launch_i8_query_prep(xq, nq, d, qn_launch ? sh.qn.get<float>() : nullptr, sh.qscale.get<float>(),
+                                         sh.qres.get<float>(), 32 * W, sh.qimg.p, st);
+                    qn_launch = false;
+                } else {
+                    launch_i8_row_scale(xq, nq, d, sh.qscale.get<float>(), sh.qres.get<float>(), st);
+                    launch_i8_tile_rows(xq, sh.qscale.get<float>(), nq, d, 32 * W, sh.qimg.p, st);
+                }
                 qsc = sh.qscale.get<float>();
             } else {
                 launch_b16_tile_rows(xq, nq, d, 32 * W, sh.qimg.p, st);

@@ -512,6 +512,9 @@ int flat_i8_nk(int d);
 size_t flat_i8_img_bytes(int64_t n, int d, int R);
 void launch_i8_row_scale(const float *X, int64_t n, int d, float *scale, float *resid, hipStream_t st);
 void launch_i8_tile_rows(const float *X, const float *scale, int64_t n, int d, int R, void *out, hipStream_t st);
+// ‖q‖² (qn optional), the int8 scales / residuals and the tiled int8 image of a query batch in one launch
+void launch_i8_query_prep(const float *X, int64_t n, int d, float *qn, float *scale, float *resid, int R, void *out,
+                          hipStream_t st);
 int flat_i8_scan_k();
 int flat_i8_scan_max_nq();
 int64_t flat_i8_scan_waves(int64_t n);
