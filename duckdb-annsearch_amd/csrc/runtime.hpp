@@ -32,13 +32,19 @@ struct DevBuf {
         bytes = 0;
     }
     template <typename T> T *get() const { return static_cast<T *>(p); }
-    // Grow to at least `need` bytes on `dev`.  Contents are NOT preserved.
+    // Grow to at least `need` bytes on `dev`.  Contents are NOT preserved.  A buffer that grows again (per-batch
+    // scratch whose size follows the longest list as appends lengthen it) takes a quarter of headroom below 1 GiB, so
+    // a run of appends does not free and re-allocate it — each hipFree synchronises the device — on every search
+    // (HIPANN_BUF_HEADROOM=0: exact sizes, A/B).
     void ensure(size_t need, int dev) {
         if (need <= bytes && dev == device && p) return;
+        static const bool headroom = [] { const char *e = std::getenv("HIPANN_BUF_HEADROOM"); return !e || std::atoi(e); }();
+        const bool regrow = p && dev == device && headroom && need < ((size_t)1 << 30);
         release();
         device = dev;
         DeviceGuard g(dev);
         size_t alloc = need < 256 ? 256 : need;
+        if (regrow) alloc += alloc / 4;
         HIPANN_CHECK(hipMalloc(&p, alloc));
         bytes = alloc;
     }
