@@ -789,6 +789,13 @@ def ivf_config(args, torch, dist, hipann, rank, world, dev, steps, warmup, suite
         "replicated on every rank" if world > 1 else "single GPU"
     probes = index.last_probes(nq)
     info.update(ivf_scan_stats(index, probes, d, nlist, ivf_row_bytes(index.form, d, metric)))
+    if world == 1:  # the list sizes and this batch's probe lists (tests/golden/c3_lists_*.npz: sharding balance tests)
+        try:
+            DETAIL_PATH.parent.mkdir(parents=True, exist_ok=True)
+            np.savez_compressed(DETAIL_PATH.parent / f"ivf_lists_{n}x{d}.npz", sizes=np.diff(index._offsets),
+                                probes=probes.astype(np.int16 if nlist < 32768 else np.int32))
+        except OSError:
+            pass
     el = timed_steps(torch, dist, world, step, steps)
     kern_ms, merge_ms = kernel_timing_steps(torch, index, step, steps)
     Dr, Ir = step()

@@ -1971,6 +1971,7 @@ __global__ void __launch_bounds__(64) post_words(const unsigned *__restrict__ sr
                                                  int words, unsigned token) {
     for (int i = threadIdx.x; i < words; i += 64) dst[i] = src[i];
     __threadfence_system();  // the words reach the host before the token does
+    __syncthreads();         // every lane's words (one wave today; any block size stays ordered)
     if (threadIdx.x == 0) __hip_atomic_store(dst + words, token, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 

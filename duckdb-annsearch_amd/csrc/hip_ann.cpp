@@ -71,6 +71,34 @@ std::vector<int> device_list(const int *devices, int ndev) {
     return v;
 }
 
+}  // namespace
+
+namespace hipann {
+std::vector<int> enable_peer_access(const std::vector<int> &devs) {
+    std::vector<int> st(devs.size(), 2);
+    if (devs.empty()) return st;
+    const int d0 = devs[0];
+    auto enable = [](int from, int to) -> bool {  // `from` may access `to`'s memory
+        int can = 0;
+        if (hipDeviceCanAccessPeer(&can, from, to) != hipSuccess || !can) return false;
+        DeviceGuard g(from);
+        const hipError_t e = hipDeviceEnablePeerAccess(to, 0);
+        if (e == hipErrorPeerAccessAlreadyEnabled) {
+            (void)hipGetLastError();  // clear the sticky-free "already enabled" status
+            return true;
+        }
+        return e == hipSuccess;
+    };
+    for (size_t p = 1; p < devs.size(); ++p) {
+        if (devs[p] == d0) continue;
+        st[p] = enable(d0, devs[p]) && enable(devs[p], d0) ? 1 : 0;
+    }
+    return st;
+}
+}  // namespace hipann
+
+namespace {
+
 hipStream_t make_stream(int dev) {
     DeviceGuard g(dev);
     hipStream_t s;
@@ -895,6 +923,21 @@ int hipann_available(void) {
 
 int hipann_device_count(void) { return device_count(); }
 
+int hipann_peer_access(void *h, int *state, int cap, char *eb, int el) {
+    return guard_int(eb, el, [&]() -> int {
+        HIPANN_REQUIRE(h, "null index");
+        auto *ix = static_cast<IndexBase *>(h);
+        std::lock_guard<std::mutex> lk(ix->mu);
+        // single-device handles (the _device creates) carry no list: one shard, on its own device
+        const std::vector<int> one{2};
+        const std::vector<int> &pv = ix->peer.empty() ? one : ix->peer;
+        const int n = (int)pv.size();
+        HIPANN_REQUIRE(!state || cap >= n, "state buffer too small");
+        if (state) for (int i = 0; i < n; ++i) state[i] = pv[(size_t)i];
+        return n;
+    });
+}
+
 int hipann_device_info(char *buf, int buf_len) {
     try {
         std::string s;
@@ -938,6 +981,7 @@ void *hipann_flat_create(int d, int metric, const float *xb, int64_t n, const in
             off += std::max<int64_t>(cnt, 0);
             ix->shards.push_back(std::move(sh));
         }
+        ix->peer = enable_peer_access(devs);
         return ix.release();
     });
 }

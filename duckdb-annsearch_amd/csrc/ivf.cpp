@@ -200,7 +200,9 @@ namespace hipann {
 IvfIndex::~IvfIndex() {
     for (auto &s : shards) {
         s->quant.reset();
-        if (s->stream) { DeviceGuard g(s->device); (void)hipStreamDestroy(s->stream); }
+        DeviceGuard g(s->device);
+        if (s->done) (void)hipEventDestroy(s->done);
+        if (s->stream) (void)hipStreamDestroy(s->stream);
     }
 }
 
@@ -391,8 +393,10 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
         const FlatShard &qs = *sh.quant->shards[0];
         if (probes_in && half) {
             qn = qsh0.qn.get<float>();  // the query preparation wrote ‖q‖² there (row_norms_f32's bits)
-        } else if (qs.qn_of == xq && qs.qn_nq == nq) {
-            qn = qs.qn.get<float>();  // the coarse quantizer's ‖q‖² of the same queries
+        } else if (!probes_in && qs.qn_of == xq && qs.qn_nq == nq) {
+            // the coarse quantizer's ‖q‖² of the same queries, written by THIS call's coarse step (with probes_in
+            // the quantizer did not run, and a cached pointer match may name a buffer whose contents changed)
+            qn = qs.qn.get<float>();
         } else {
             sh.qn.ensure(sizeof(float) * (size_t)nq, sh.device);
             launch_row_norms(xq, nq, d, sh.qn.get<float>(), st);
@@ -513,7 +517,9 @@ static void ivf_relayout(IvfIndex &ix, IvfShard &sh, const std::vector<int64_t> 
     codes_nb.ensure(sizeof(float) * (size_t)std::max<int64_t>(N, 1) * d, sh.device);
     ids_nb.ensure(sizeof(int64_t) * (size_t)std::max<int64_t>(N, 1), sh.device);
     HIPANN_CHECK(hipMemsetAsync(codes_nb.p, 0, codes_nb.bytes, st));
-    const bool xn = ix.metric == kL2 && sh.xnorm.p;
+    // L2 shards always leave with a norm array: a shard created empty (compute_row_norms skips n = 0) has none yet,
+    // and ivf_append_rows writes the new rows' norms into it (the decomposed / fp16 scans read it)
+    const bool xn = ix.metric == kL2, xn_old = xn && sh.xnorm.p;
     if (xn) {
         xn_nb.ensure(sizeof(float) * (size_t)std::max<int64_t>(N, 1), sh.device);
         HIPANN_CHECK(hipMemsetAsync(xn_nb.p, 0, xn_nb.bytes, st));
@@ -541,7 +547,7 @@ static void ivf_relayout(IvfIndex &ix, IvfShard &sh, const std::vector<int64_t> 
                                     hipMemcpyDeviceToDevice, st));
         HIPANN_CHECK(hipMemcpyAsync(ids_nb.get<int64_t>() + o1, sh.ids + o0, sizeof(int64_t) * (size_t)len,
                                     hipMemcpyDeviceToDevice, st));
-        if (xn)
+        if (xn_old)
             HIPANN_CHECK(hipMemcpyAsync(xn_nb.get<float>() + o1, sh.xnorm.get<float>() + o0, sizeof(float) * (size_t)len,
                                         hipMemcpyDeviceToDevice, st));
         const int64_t np = ceil_div(len, 32);  // the passes holding live rows (a pass's rows past len are zero)
@@ -809,6 +815,7 @@ void *hipann_ivf_create(int d, int metric, int nlist, int nprobe, const float *c
             sh->quant = make_quantizer(d, metric, sh->centroids, nlist, sh->device, sh->stream);
             ix->shards.push_back(std::move(sh));
         }
+        ix->peer = enable_peer_access(devs);
         return ix.release();
     });
 }
@@ -898,6 +905,10 @@ static int ivf_search_host(IvfIndex &ix, int64_t nq, const float *xq, int64_t k,
         else HIPANN_CHECK(hipMemcpyAsync(sh.q.p, ix.h_q.p, qbytes, hipMemcpyHostToDevice, sh.stream));
         ivf_shard_search(ix, sh, nq, sh.q.get<float>(), keff, kout, sh.out_d.get<float>(), sh.out_i.get<int64_t>(),
                          sh.stream);
+        if (ix.shards.size() > 1) {  // shard 0's stream waits for it on the device (no host wait per shard)
+            if (!sh.done) HIPANN_CHECK(hipEventCreateWithFlags(&sh.done, hipEventDisableTiming));
+            HIPANN_CHECK(hipEventRecord(sh.done, sh.stream));
+        }
     }
     ix.h_d.ensure(ob * sizeof(float));
     ix.h_i.ensure(ob * sizeof(int64_t));
@@ -918,16 +929,15 @@ static int ivf_search_host(IvfIndex &ix, int64_t nq, const float *xq, int64_t k,
         ix.gather_i.ensure(ob * np * sizeof(int64_t), s0.device);
         ix.merged_d.ensure(ob * sizeof(float), s0.device);
         ix.merged_i.ensure(ob * sizeof(int64_t), s0.device);
+        DeviceGuard g0(s0.device);
         for (int p = 0; p < np; ++p) {
             IvfShard &sh = *ix.shards[p];
-            DeviceGuard g(sh.device);
-            HIPANN_CHECK(hipStreamSynchronize(sh.stream));
+            if (p > 0) HIPANN_CHECK(hipStreamWaitEvent(s0.stream, sh.done, 0));
             HIPANN_CHECK(hipMemcpyPeerAsync(ix.gather_d.get<float>() + p * ob, s0.device, sh.out_d.p, sh.device,
                                             ob * sizeof(float), s0.stream));
             HIPANN_CHECK(hipMemcpyPeerAsync(ix.gather_i.get<int64_t>() + p * ob, s0.device, sh.out_i.p, sh.device,
                                             ob * sizeof(int64_t), s0.stream));
         }
-        DeviceGuard g(s0.device);
         const float sign = ix.metric == kIP ? -1.f : 1.f;
         launch_merge_parts<long long>(ix.gather_d.get<float>(), ix.gather_i.get<long long>(), np, nq, kout, kout, 0,
                                       sign, sign, ix.merged_d.get<float>(), ix.merged_i.get<int64_t>(), s0.stream);

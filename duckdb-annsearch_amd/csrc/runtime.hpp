@@ -2,6 +2,7 @@
 #pragma once
 #include "common.hpp"
 #include <cstdlib>
+#include <ctime>
 #include <memory>
 #include <mutex>
 #include <vector>
@@ -142,72 +143,95 @@ inline bool spin_wait() {
     static const bool v = [] { const char *e = std::getenv("HIPANN_SPIN_WAIT"); return !e || std::atoi(e) != 0; }();
     return v;
 }
+// The spin is bounded: after HIPANN_SPIN_US microseconds (default 2000 — the C2 batch and every IVF batch finish
+// inside it; a 10M-row Flat batch of ≈8 ms pays one wake-up, < 1 %) the wait blocks, so a long search does not hold a
+// host core (DuckDB's worker pool runs concurrent searches).
+inline int64_t spin_budget_ns() {
+    static const int64_t v = [] {
+        const char *e = std::getenv("HIPANN_SPIN_US");
+        return (int64_t)(e ? std::atoll(e) : 2000) * 1000;
+    }();
+    return v;
+}
+inline int64_t mono_ns() {
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (int64_t)ts.tv_sec * 1000000000 + ts.tv_nsec;
+}
 // until `ev` has completed (hipEventQuery in a pause loop; errors surface as from the blocking call)
 inline void wait_event(hipEvent_t ev) {
-    if (!spin_wait()) {
-        HIPANN_CHECK(hipEventSynchronize(ev));
-        return;
+    if (spin_wait()) {
+        const int64_t t_end = mono_ns() + spin_budget_ns();
+        for (unsigned it = 1;; ++it) {
+            const hipError_t e = hipEventQuery(ev);
+            if (e == hipSuccess) return;
+            if (e != hipErrorNotReady) HIPANN_CHECK(e);
+            for (int i = 0; i < 16; ++i) __builtin_ia32_pause();
+            if ((it & 63) == 0 && mono_ns() > t_end) break;
+        }
     }
-    for (;;) {
-        const hipError_t e = hipEventQuery(ev);
-        if (e == hipSuccess) return;
-        if (e != hipErrorNotReady) HIPANN_CHECK(e);
-        for (int i = 0; i < 16; ++i) __builtin_ia32_pause();
-    }
+    HIPANN_CHECK(hipEventSynchronize(ev));
 }
 // until the token word `tok` (written by launch_post_words, the last work on `st`) reads `token`: every earlier
 // kernel on the stream has completed then.  The stream is queried now and then, so a failed or finished stream
 // ends the wait too (its error raised as hipStreamSynchronize would).
 inline void wait_posted(const volatile unsigned *tok, unsigned token, hipStream_t st) {
-    if (!spin_wait()) {
-        HIPANN_CHECK(hipStreamSynchronize(st));
-        return;
-    }
-    for (unsigned it = 1;; ++it) {
-        if (__atomic_load_n(tok, __ATOMIC_ACQUIRE) == token) return;
-        if ((it & 1023) == 0) {
-            const hipError_t e = hipStreamQuery(st);
-            if (e == hipSuccess) return;
-            if (e != hipErrorNotReady) HIPANN_CHECK(hipStreamSynchronize(st));
+    if (spin_wait()) {
+        const int64_t t_end = mono_ns() + spin_budget_ns();
+        for (unsigned it = 1;; ++it) {
+            if (__atomic_load_n(tok, __ATOMIC_ACQUIRE) == token) return;
+            if ((it & 1023) == 0) {
+                const hipError_t e = hipStreamQuery(st);
+                if (e == hipSuccess) return;
+                if (e != hipErrorNotReady) HIPANN_CHECK(hipStreamSynchronize(st));
+                if (mono_ns() > t_end) break;
+            }
+            __builtin_ia32_pause();
         }
-        __builtin_ia32_pause();
     }
+    HIPANN_CHECK(hipStreamSynchronize(st));
 }
 
 struct StreamFence {
     hipEvent_t ev = nullptr;
     hipStream_t last = nullptr;
     bool armed = false;
+    bool multi = false;  // a call has arrived on a different stream than its predecessor: events from now on
+    bool ev_valid = false;  // ev holds the previous call's end
     int device = 0;
     StreamFence() = default;
     StreamFence(const StreamFence &) = delete;
     StreamFence &operator=(const StreamFence &) = delete;
     ~StreamFence() { if (ev) { DeviceGuard g(device); (void)hipEventDestroy(ev); } }
-    // Default (lazy): nothing is recorded per call — an event record is a marker packet the next kernel waits
-    // behind (≈6 µs of idle GPU between consecutive searches on one stream, r05 kernel traces) — and a call on a
-    // different stream than the previous call first synchronises the device (the previous stream may have been
-    // destroyed since, so no event is recorded on it then).  HIPANN_FENCE_EAGER=1: the event recorded at the end of
-    // every call, waited for by a call on another stream.
+    // Adaptive.  While every call of the handle comes on one stream nothing is recorded per call — an event record is
+    // a marker packet the next kernel waits behind (≈6 µs of idle GPU between consecutive searches on one stream, r05
+    // kernel traces).  The first call on a different stream synchronises the handle's device once (no event of the
+    // previous call exists; its stream may have been destroyed since) and switches the fence to events: from then on
+    // every call records one at its end, and a call on another stream waits for it on the device (hipStreamWaitEvent)
+    // — per-connection streams cost one marker per call, not a device-wide drain per alternation.
+    // HIPANN_FENCE_EAGER=1: events from the first call.
     static bool eager() {
         static const bool v = [] { const char *e = std::getenv("HIPANN_FENCE_EAGER"); return e && std::atoi(e) != 0; }();
         return v;
     }
     void enter(hipStream_t st) {
         if (!armed || st == last) return;
-        if (eager()) {
+        if (ev_valid) {
             HIPANN_CHECK(hipStreamWaitEvent(st, ev, 0));
         } else {
             DeviceGuard g(device);
             HIPANN_CHECK(hipDeviceSynchronize());
         }
+        multi = true;
     }
     void leave(hipStream_t st, int dev) {
-        if (eager()) {
+        if (eager() || multi) {
             if (!ev) {
                 DeviceGuard g(dev);
                 HIPANN_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
             }
             HIPANN_CHECK(hipEventRecord(ev, st));
+            ev_valid = true;
         }
         device = dev;
         last = st;
@@ -302,6 +326,10 @@ struct IndexBase {
     // the last search's path (hipann_last_search_path): the scan form that ran (FlatForm / IvfForm; an exact
     // form's flagged re-runs excluded), its rerank filter depth (0: no rerank) and sub-lists per slot (IVF)
     int last_form = -1, last_kfilt = 0, last_sublists = 0;
+    // per shard, set at create (enable_peer_access): 2 = on shard 0's device (no peer copy), 1 = peer access enabled
+    // both ways between its device and shard 0's (the result gather rides xGMI), 0 = not available (the runtime
+    // stages the gather through host memory)
+    std::vector<int> peer;
     explicit IndexBase(Kind k) : kind(k) {}
     virtual ~IndexBase() = default;
     virtual int64_t ntotal() const = 0;
@@ -387,6 +415,7 @@ struct IvfShard {
     HostBuf app_hassign, app_hup, app_hstat;
     int max_nch = 1;  // largest list's row-chunk count
     StreamFence fence;  // cross-stream ordering of this shard's calls (its coarse quantizer's scratch included)
+    hipEvent_t done = nullptr;  // multi-device search: the shard's search has drained (shard 0's stream waits)
 };
 
 struct IvfIndex : IndexBase {
@@ -414,6 +443,10 @@ struct IvfIndex : IndexBase {
         return b;
     }
 };
+
+// Peer access between every listed device and devs[0] (hipDeviceCanAccessPeer both ways, then
+// hipDeviceEnablePeerAccess; an already-enabled pair counts as enabled).  Returns the per-shard state of IndexBase::peer.
+std::vector<int> enable_peer_access(const std::vector<int> &devs);
 
 // ---- kernel launchers (flat_kernels.hip, ivf_kernels.hip, ivf_mfma.hip) ----
 // host-pointer calls up to this many bytes each way move queries / results with a copy kernel through

@@ -86,6 +86,7 @@ def lib() -> C.CDLL:
             "hipann_available": ([], i32),
             "hipann_device_count": ([], i32),
             "hipann_device_info": ([cp, i32], i32),
+            "hipann_peer_access": ([vp, C.POINTER(C.c_int), i32, cp, i32], i32),
             "hipann_flat_create": ([i32, i32, f, i64, C.POINTER(C.c_int), i32, cp, i32], vp),
             "hipann_flat_add": ([vp, f, i64, cp, i32], i32),
             "hipann_flat_search": ([vp, i64, f, i64, f, i64p, cp, i32], i32),
@@ -239,6 +240,18 @@ class _Handle:
 
     def kernel_ms(self, which: int = 0) -> float:
         return float(lib().hipann_last_kernel_ms(self._h, which))
+
+    PEER_SAME_DEVICE, PEER_ENABLED, PEER_UNAVAILABLE = 2, 1, 0
+
+    def peer_access(self) -> list:
+        """hipann_peer_access: per shard, 2 = on the first shard's device, 1 = peer access enabled both ways with it
+        (the top-k gather rides xGMI), 0 = not available (the gather stages through host memory)."""
+        eb = _err()
+        n = lib().hipann_peer_access(self._h, None, 0, eb, 1024)
+        _check(min(n, 0), eb)
+        st = (C.c_int * max(n, 1))()
+        _check(min(lib().hipann_peer_access(self._h, st, n, eb, 1024), 0), eb)
+        return [int(st[i]) for i in range(n)]
 
     @property
     def handle(self) -> C.c_void_p:

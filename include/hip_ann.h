@@ -57,6 +57,14 @@ int hipann_device_count(void);
  * (src/faiss_fn_gpu.cpp:42-45).  Returns the string length, or -1. */
 int hipann_device_info(char *buf, int buf_len);
 
+/* Peer access of a (multi-device) Flat or IVF handle, set when it was created: hipann_flat_create /
+ * hipann_ivf_create with devices[] call hipDeviceCanAccessPeer both ways between every shard's device and the first
+ * shard's, then hipDeviceEnablePeerAccess, so the per-shard top-k gather (hipMemcpyPeerAsync onto the first device)
+ * rides xGMI.  state[s] (cap >= shard count; NULL to ask the count): 2 = on the first shard's device (no peer copy),
+ * 1 = peer access enabled both ways, 0 = not available (the runtime stages the copy through host memory).  Returns the
+ * shard count, or -1. */
+int hipann_peer_access(void *index, int *state, int cap, char *err_buf, int err_len);
+
 /* ---------------------------------------------------------------------------------------------
  * Flat (brute force) — replaces index_cpu_to_metal + MetalIndexFlat (MetalIndexFlat.mm:504-515,
  * :173-292 add, :294-369 search).
@@ -137,13 +145,17 @@ int hipann_last_search_path(void *index, int *form, int *filter_k, int *sublists
  * included: they are re-run on the device).  Flat: the exact forms (HIPANN_FLAT_FORM_SPLIT2_EXACT,
  * HIPANN_FLAT_FORM_BF16_EXACT, HIPANN_FLAT_FORM_I8_EXACT) synchronise the stream once per call to read the flagged-query count (twice
  * when the bounded passes' candidate rerank ran), and a table's first exact-form search also builds its bf16 /
- * int8 image and bound; the other forms return with their kernels queued.  Calls on one handle may use different streams:
- * a call whose stream differs from the handle's previous call's first synchronises the device (the per-handle scratch is
- * reused, and the previous stream may have been destroyed since), so they execute in the order they were issued; calls
- * on one stream add nothing between them (no event per call — an event marker costs ≈6 µs of idle GPU between
- * back-to-back searches).  HIPANN_FENCE_EAGER=1 instead records an event at the end of every call and makes a call on
- * another stream wait for it (the previous stream must then outlive the next call).  The caller still orders its own
- * buffers (queries written / results read on other streams) with its own events.
+ * int8 image and bound; the other forms return with their kernels queued.  Calls on one handle may use different streams
+ * and execute in the order they were issued (the per-handle scratch is reused).  While every call comes on one stream
+ * nothing is added between them (no event per call — an event marker costs ≈6 µs of idle GPU between back-to-back
+ * searches).  The FIRST call on a different stream synchronises the handle's device once; from then on the handle
+ * records an event at the end of every call and a call on another stream waits for it on the device
+ * (hipStreamWaitEvent), so per-connection streams cost one marker per call, not a device-wide drain per alternation.
+ * HIPANN_FENCE_EAGER=1 records the events from the first call.  The caller still orders its own buffers (queries
+ * written / results read on other streams) with its own events.
+ * Host waits (the Flat exact forms' flag count, host-pointer calls) poll for at most HIPANN_SPIN_US microseconds
+ * (default 2000) and then block in hipStreamSynchronize / hipEventSynchronize: short calls avoid the interrupt
+ * wake-up (tens of µs), long ones do not hold a host core for the whole kernel.  HIPANN_SPIN_WAIT=0: always block.
  * ------------------------------------------------------------------------------------------- */
 
 /* Wrap (copy=0: borrow, caller keeps it alive) or copy (copy=1) an HBM matrix of n*d fp32 on

@@ -236,6 +236,32 @@ void oracle_flat_search(const float *xb, int64_t n, int d, const float *xq, int6
 /* IndexIVFFlat::search                                                                       */
 /* ------------------------------------------------------------------------------------------ */
 
+/* IndexIVF::search_preassigned (FAISS 1.13.2, external; called by IndexIVF::search after the coarse step):
+ * the probe lists ci (nq*nprobe, probe order, -1 = skipped) are given; each query's lists are scanned in probe
+ * order with the direct-form distance and offered to its heap (strict admission, cmp2 eviction). */
+void oracle_ivf_search_preassigned(const int64_t *list_off, const int64_t *ids, const float *codes, int d,
+                                   const float *xq, int64_t nq, int k, int nprobe, const int64_t *ci, int metric,
+                                   float *D, int64_t *I) {
+    const int is_max = metric == ORACLE_L2;
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t i = 0; i < nq; ++i) {
+        float *bv = D + i * k;
+        int64_t *bi = I + i * k;
+        heap_heapify(is_max, k, bv, bi);
+        const float *q = xq + i * (int64_t)d;
+        for (int p = 0; p < nprobe; ++p) {
+            const int64_t l = ci[i * nprobe + p];
+            if (l < 0) continue;
+            for (int64_t r = list_off[l]; r < list_off[l + 1]; ++r) {
+                const float *x = codes + r * (int64_t)d;
+                const float dis = metric == ORACLE_L2 ? l2sqr_f32(q, x, d) : dot_f32(q, x, d);
+                heap_offer(is_max, k, bv, bi, dis, ids[r]);
+            }
+        }
+        heap_reorder(is_max, k, bv, bi);
+    }
+}
+
 /* probes_out (nq*nprobe, may be NULL): coarse assignment in probe order. */
 void oracle_ivf_search(const float *centroids, int nlist, const int64_t *list_off, const int64_t *ids,
                        const float *codes, int d, const float *xq, int64_t nq, int k, int nprobe, int metric, float *D,

@@ -36,6 +36,7 @@ def lib():
         u8, d64 = C.POINTER(C.c_uint8), C.POINTER(C.c_double)
         _lib.oracle_flat_search.argtypes = [f, C.c_int64, i32, f, C.c_int64, i32, i32, C.c_int64, f, i64]
         _lib.oracle_ivf_search.argtypes = [f, i32, i64, i64, f, i32, f, C.c_int64, i32, i32, i32, f, i64, i64]
+        _lib.oracle_ivf_search_preassigned.argtypes = [i64, i64, f, i32, f, C.c_int64, i32, i32, i64, i32, f, i64]
         _lib.oracle_exact_dists.argtypes = [f, i32, f, i64, C.c_int64, i32, d64]
         _lib.oracle_batch_distances.argtypes = [f, f, i32, i32, i32, f]
         _lib.oracle_batch_distances_simd.argtypes = [f, f, i32, i32, i32, f]
@@ -91,6 +92,23 @@ def ivf_search(centroids, list_off, ids, codes, xq, k, nprobe, metric=L2):
                             _p(codes, C.c_float), d, _p(xq, C.c_float), nq, k, nprobe, metric,
                             _p(D, C.c_float), _p(I, C.c_int64), _p(P, C.c_int64))
     return D, I, P
+
+
+def ivf_search_preassigned(list_off, ids, codes, xq, k, probes, metric=L2):
+    """FAISS IndexIVF::search_preassigned restated: the lists of `probes` (nq x nprobe, probe order) scanned in the
+    direct form — the IVF scan of a given probe list (tests hold the GPU scan to it on the GPU's own probe lists)."""
+    codes, xq = _f32(codes), _f32(xq)
+    list_off = np.ascontiguousarray(list_off, np.int64)
+    ids = np.ascontiguousarray(ids, np.int64)
+    probes = np.ascontiguousarray(probes, np.int64)
+    nq, npr = probes.shape
+    d = xq.shape[1]
+    D = np.empty((nq, k), np.float32)
+    I = np.empty((nq, k), np.int64)
+    lib().oracle_ivf_search_preassigned(_p(list_off, C.c_int64), _p(ids, C.c_int64), _p(codes, C.c_float), d,
+                                        _p(xq, C.c_float), nq, k, npr, _p(probes, C.c_int64), metric,
+                                        _p(D, C.c_float), _p(I, C.c_int64))
+    return D, I
 
 
 def exact_dists(xb, q, labels, metric=L2):

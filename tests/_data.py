@@ -79,6 +79,22 @@ def check_probe_parity(cen, xq, P, Po, metric=0, tau=TAU):
     return same
 
 
+def oracle_on_gpu_probes(oracle, cen, off, ids, codes, xq, k, P, Po, Do, Io, metric=0, tau=TAU):
+    """The oracle's IVF answers held to the GPU's own probe lists.  Queries whose probe lists equal the oracle's keep
+    the oracle's IndexIVFFlat::search results; a query whose list differs (only inside the coarse tie window:
+    check_probe_parity asserts that) takes the oracle's IndexIVF::search_preassigned over the GPU's list — the scan
+    the GPU ran — so the id parity check covers EVERY query of the batch instead of dropping those.  Returns
+    (D, I, n_differing_probe_lists); the count is recorded in PARITY_STATS."""
+    same = check_probe_parity(cen, xq, P, Po, metric, tau)
+    D, I = Do.copy(), Io.copy()
+    nd = int((~same).sum())
+    if nd:
+        Dp, Ip = oracle.ivf_search_preassigned(off, ids, codes, xq[~same], k, P[~same], metric)
+        D[~same], I[~same] = Dp, Ip
+    PARITY_STATS.append({"name": CURRENT_TEST, "probe_lists_differing": nd, "nq": int(len(xq))})
+    return D, I, nd
+
+
 def _scale(q64, xmax, metric):
     """Rounding scale of one query's fp32 distances: |q|² + max|x|² (L2) or |q|·max|x| (IP)."""
     qn = float(np.dot(q64, q64))

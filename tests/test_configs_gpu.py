@@ -27,10 +27,14 @@ from pathlib import Path
 import numpy as np
 import pytest
 
-from _data import TAU, check_probe_parity, check_topk_parity
+from _data import TAU, check_probe_parity, check_topk_parity, oracle_on_gpu_probes
 
 pytestmark = pytest.mark.gpu
 ROOT = Path(__file__).resolve().parents[1]
+# identical probe lists given identical centroids.  The search-time coarse keys are fp32-level (a 3-term
+# bf16 split); a list that still differs from the oracle's may do so only inside the coarse tie window
+# (check_probe_parity asserts it) and its query is then checked against search_preassigned over the GPU's list.
+C3_MAX_PROBE_DIFF = 0
 sys.path.insert(0, str(ROOT))
 
 
@@ -165,7 +169,7 @@ def c3_oracle(c3_index, oracle):
 
 
 @pytest.mark.parametrize("form", [6, 5, 3, 0])
-def test_c3_ivf_nlist1024_nprobe32_d768_nq1024(gpu, c3_index, c3_oracle, form):
+def test_c3_ivf_nlist1024_nprobe32_d768_nq1024(gpu, oracle, c3_index, c3_oracle, form):
     """C3 shape: nlist = 1024, nprobe = 32, d = 768, nq = 1024, k = 10 (200k rows of the bench's data,
     lists from the bench's GPU build).  Probe lists equal the oracle's; ids follow the parity rule over
     the scanned set on every query whose probe list is identical (tie-window differences excluded)."""
@@ -177,13 +181,15 @@ def test_c3_ivf_nlist1024_nprobe32_d768_nq1024(gpu, c3_index, c3_oracle, form):
     D, I = _dev_search(index, xq_t, 10, torch)
     P = index.last_probes(len(xq))
     Do, Io, Po = c3_oracle
-    same = check_probe_parity(cen, xq, P, Po, 0)
-    assert same.mean() >= 0.99, same.mean()
-    st = check_topk_parity(xb, xq[same], D[same], I[same], Do[same], Io[same], 0)
-    assert st["exact_fraction"] >= 0.995, st
+    # every query checked: a probe list that differs from the oracle's (inside the coarse tie window only) is held to
+    # the oracle's search_preassigned over the GPU's list; SURVEY §8c: identical probe lists — the count must be 0
+    Do, Io, ndiff = oracle_on_gpu_probes(oracle, cen, off, ids, codes, xq, 10, P, Po, Do, Io, 0)
+    assert ndiff <= C3_MAX_PROBE_DIFF, ndiff
+    st = check_topk_parity(xb, xq, D, I, Do, Io, 0)
+    assert st["exact_fraction"] >= (1.0 if form in (5, 6) else 0.995), st
     if form in (5, 6):  # returned distances are the direct fp32 form, like the oracle's scanner
-        v = I[same] >= 0
-        assert np.allclose(D[same][v], Do[same][v], rtol=2e-6, atol=1e-6)
+        v = I >= 0
+        assert np.allclose(D[v], Do[v], rtol=2e-6, atol=1e-6)
     index.form = 6
 
 
@@ -214,12 +220,12 @@ def test_c3_ivf_2m_rows_full_batch_vs_oracle(gpu, oracle):
     assert index.last_search_path()["form"] == index.FORM_HALF_EXACT
     P = index.last_probes(nq)
     Do, Io, Po = oracle.ivf_search(cen, off, ids, codes, xq, 10, nprobe, 0)
-    same = check_probe_parity(cen, xq, P, Po, 0)
-    assert same.mean() >= 0.99, same.mean()
-    st = check_topk_parity(xb, xq[same], D[same], I[same], Do[same], Io[same], 0)
+    Do, Io, ndiff = oracle_on_gpu_probes(oracle, cen, off, ids, codes, xq, 10, P, Po, Do, Io, 0)
+    assert ndiff <= C3_MAX_PROBE_DIFF, ndiff
+    st = check_topk_parity(xb, xq, D, I, Do, Io, 0)
     assert st["exact_fraction"] == 1.0, st
-    v = I[same] >= 0
-    assert np.allclose(D[same][v], Do[same][v], rtol=2e-6, atol=1e-6)
+    v = I >= 0
+    assert np.allclose(D[v], Do[v], rtol=2e-6, atol=1e-6)
     index.close()
 
 

@@ -597,3 +597,87 @@ def test_ivf_nan_and_overflow_queries_pad_like_faiss(gpu, oracle, metric):
     good = np.array([i for i in range(len(xq)) if i not in bad])
     st = check_topk_parity(xb, xq[good], D[good], I[good], Do[good], Io[good], metric)
     assert st["exact_fraction"] == 1.0, st
+
+
+@pytest.mark.parametrize("form", [6, 5, 0])
+def test_ivf_empty_l2_index_then_append(gpu, oracle, form):
+    """ADVICE r05 (high): an L2 IVF index created with zero rows has no norm array (compute_row_norms skips n = 0);
+    the first append's relayout must give it one, because ivf_append_rows writes the new rows' norms into it and the
+    decomposed / fp16 scans read them.  After the append every exact form's ids equal the oracle's IndexIVFFlat."""
+    rng = np.random.default_rng(31 + form)
+    d, nlist = 48, 16
+    xb = rng.standard_normal((6000, d), dtype=np.float32)
+    xq = rng.standard_normal((64, d), dtype=np.float32)
+    cen = np.ascontiguousarray(xb[:nlist * 100:100])
+    ix = gpu.HipIndexIVFFlat(cen, np.zeros(nlist + 1, np.int64), np.zeros(0, np.int64),
+                             np.zeros((0, d), np.float32), 4)
+    ix.form = form
+    D, I = ix.search(xq[:2], 5)
+    assert (I == -1).all()
+    ix.add(xb[:3000])
+    ix.add(xb[3000:])
+    assert ix.ntotal == len(xb)
+    D, I = ix.search(xq, 10)
+    assert ix.last_search_path()["form"] == form
+    off, ids, codes = build_ivf_lists(xb, cen)
+    Do, Io, Po = oracle.ivf_search(cen, off, ids, codes, xq, 10, 4)
+    assert np.array_equal(ix.last_probes(len(xq)), Po)
+    st = check_topk_parity(xb, xq, D, I, Do, Io)
+    if form in (5, 6):
+        assert st["exact_fraction"] == 1.0, st
+
+
+@pytest.mark.parametrize("form", [5, 0])
+def test_ivf_search_probes_device_reused_buffer(gpu, oracle, form):
+    """search_probes_device (caller-supplied probe lists, no coarse step) must compute ‖q‖² of
+    THIS call's queries: two calls on one device buffer whose contents change in between (same pointer, same nq)
+    each equal the oracle's search of their own queries."""
+    import torch
+    rng = np.random.default_rng(77)
+    d, nlist, nprobe, nq = 64, 32, 6, 48
+    xb = rng.standard_normal((12000, d), dtype=np.float32)
+    cen = np.ascontiguousarray(xb[:nlist * 300:300])
+    off, ids, codes = build_ivf_lists(xb, cen)
+    ix = gpu.HipIndexIVFFlat(cen, off, ids, codes, nprobe)
+    ix.form = form
+    dev = torch.device("cuda", 0)
+    q_t = torch.empty((nq, d), device=dev, dtype=torch.float32)
+    p_t = torch.empty((nq, nprobe), device=dev, dtype=torch.int64)
+    Dt = torch.empty((nq, 10), device=dev)
+    It = torch.empty((nq, 10), device=dev, dtype=torch.int64)
+    stream = torch.cuda.current_stream().cuda_stream
+    for rep in range(2):
+        xq = (rng.standard_normal((nq, d)) * (1.0 + 3.0 * rep)).astype(np.float32)
+        q_t.copy_(torch.from_numpy(xq))
+        Do, Io, Po = oracle.ivf_search(cen, off, ids, codes, xq, 10, nprobe)
+        p_t.copy_(torch.from_numpy(Po))
+        if rep == 0:  # a full search on the same buffer first: the quantizer caches ‖q‖² of this pointer
+            ix.search_device(nq, q_t.data_ptr(), 10, Dt.data_ptr(), It.data_ptr(), stream)
+        ix.search_probes_device(nq, q_t.data_ptr(), p_t.data_ptr(), 10, Dt.data_ptr(), It.data_ptr(), stream)
+        torch.cuda.synchronize()
+        D, I = Dt.cpu().numpy(), It.cpu().numpy()
+        st = check_topk_parity(xb, xq, D, I, Do, Io)
+        if form == 5:
+            assert st["exact_fraction"] == 1.0, (rep, st)
+
+
+def test_peer_access_query_multi_device_handles(gpu, oracle):
+    """a multi-device handle enables peer access between every shard's device and the first
+    shard's at create (hipann_peer_access).  On the one-GPU box every shard sits on device 0: the state is "same
+    device" (not applicable) for each, and searches still equal the oracle.  With >= 2 devices visible the pair
+    must report enabled where hipDeviceCanAccessPeer allows it."""
+    import torch
+    xb, xq = faiss_metal_case(6000, 24, 32)
+    ix, (cen, off, ids, codes) = _ivf(gpu, xb, 16, 4, devices=[0, 0, 0])
+    assert ix.peer_access() == [ix.PEER_SAME_DEVICE] * 3
+    D, I = ix.search(xq, 10)
+    Do, Io, _ = oracle.ivf_search(cen, off, ids, codes, xq, 10, 4)
+    check_topk_parity(xb, xq, D, I, Do, Io)
+    fx = gpu.HipIndexFlat(32, 0, xb, devices=[0, 0])
+    assert fx.peer_access() == [fx.PEER_SAME_DEVICE] * 2
+    single = gpu.HipIndexFlat(32, 0, xb)
+    assert single.peer_access() == [single.PEER_SAME_DEVICE]
+    if torch.cuda.device_count() >= 2:
+        two = gpu.HipIndexFlat(32, 0, xb, devices=[0, 1])
+        can = torch.cuda.can_device_access_peer(0, 1) and torch.cuda.can_device_access_peer(1, 0)
+        assert two.peer_access() == [two.PEER_SAME_DEVICE, two.PEER_ENABLED if can else two.PEER_UNAVAILABLE]

@@ -355,3 +355,22 @@ def test_bench_parity_report_agrees_with_the_test_rule():
     D4[1, 2] *= 1.01
     r = topk_parity(rows, xq, D4, I, D, I, 0, xm, same_rtol=2e-6)
     assert not r["parity_ok"] and r["violations"]["distance"] == 1 and r["violations"]["same_id_distance"] == 1
+
+
+def test_ivf_search_preassigned_equals_search_on_its_own_probes():
+    """IndexIVF::search = coarse step + search_preassigned: the restated search_preassigned on the oracle's own probe
+    lists returns the oracle's IndexIVFFlat::search results bit for bit (the tests then hold the GPU scan to it on the
+    GPU's probe lists when a list differs inside the coarse tie window)."""
+    from oracle import oracle as O
+    xb, xq = faiss_metal_case(4000, 30, 24)
+    cen = np.ascontiguousarray(xb[::200][:20])
+    for metric in (0, 1):
+        off, ids, codes = build_ivf_lists(xb, cen, metric)
+        D, I, P = O.ivf_search(cen, off, ids, codes, xq, 10, 5, metric)
+        D2, I2 = O.ivf_search_preassigned(off, ids, codes, xq, 10, P, metric)
+        assert np.array_equal(I, I2) and np.array_equal(D, D2)
+        P2 = P.copy()
+        P2[:, 0] = -1  # a skipped probe (-1) is not scanned
+        D3, I3 = O.ivf_search_preassigned(off, ids, codes, xq, 10, P2, metric)
+        D4, I4, _ = O.ivf_search(cen, off, ids, codes, xq, 10, 5, metric)
+        assert not np.array_equal(I3, I4)
