@@ -202,6 +202,8 @@ IvfIndex::~IvfIndex() {
         s->quant.reset();
         DeviceGuard g(s->device);
         if (s->done) (void)hipEventDestroy(s->done);
+        for (hipEvent_t e : s->app_ev)
+            if (e) (void)hipEventDestroy(e);
         if (s->stream) (void)hipStreamDestroy(s->stream);
     }
 }
@@ -513,71 +515,61 @@ static void ivf_relayout(IvfIndex &ix, IvfShard &sh, const std::vector<int64_t> 
         off[l + 1] = off[l] + ncap;
     }
     const int64_t N = off[nlist];
-    DevBuf codes_nb, ids_nb, xn_nb, h_nb, t_nb, tp_nb;
-    codes_nb.ensure(sizeof(float) * (size_t)std::max<int64_t>(N, 1) * d, sh.device);
-    ids_nb.ensure(sizeof(int64_t) * (size_t)std::max<int64_t>(N, 1), sh.device);
-    HIPANN_CHECK(hipMemsetAsync(codes_nb.p, 0, codes_nb.bytes, st));
-    // L2 shards always leave with a norm array: a shard created empty (compute_row_norms skips n = 0) has none yet,
-    // and ivf_append_rows writes the new rows' norms into it (the decomposed / fp16 scans read it)
-    const bool xn = ix.metric == kL2, xn_old = xn && sh.xnorm.p;
-    if (xn) {
-        xn_nb.ensure(sizeof(float) * (size_t)std::max<int64_t>(N, 1), sh.device);
-        HIPANN_CHECK(hipMemsetAsync(xn_nb.p, 0, xn_nb.bytes, st));
-    }
     std::vector<int64_t> tp_old(nlist + 1, 0), tp(nlist + 1, 0);
     for (int l = 0; l < nlist; ++l) {
         tp_old[l + 1] = tp_old[l] + ceil_div(sh.h_off[l + 1] - sh.h_off[l], 32);
         tp[l + 1] = tp[l] + ceil_div(off[l + 1] - off[l], 32);
     }
-    const bool img_h = sh.half_state > 0 && sh.codes_h.p, img_t = sh.codes_t.p != nullptr;
-    const size_t hpb = (size_t)ivf_half_pass_bytes(d), tpb = sizeof(float) * (size_t)ivf_mfma_pass_floats(d);
-    if (img_h) {
-        h_nb.ensure(hpb * (size_t)std::max<int64_t>(tp[nlist], 1), sh.device);
-        HIPANN_CHECK(hipMemsetAsync(h_nb.p, 0, h_nb.bytes, st));
-    }
-    if (img_t) {
-        t_nb.ensure(tpb * (size_t)std::max<int64_t>(tp[nlist], 1), sh.device);
-        HIPANN_CHECK(hipMemsetAsync(t_nb.p, 0, t_nb.bytes, st));
-    }
-    for (int l = 0; l < nlist; ++l) {
-        const int64_t len = sh.h_len[l];
-        if (!len) continue;
-        const int64_t o0 = sh.h_off[l], o1 = off[l];
-        HIPANN_CHECK(hipMemcpyAsync(codes_nb.get<float>() + o1 * d, sh.codes + o0 * d, sizeof(float) * (size_t)len * d,
-                                    hipMemcpyDeviceToDevice, st));
-        HIPANN_CHECK(hipMemcpyAsync(ids_nb.get<int64_t>() + o1, sh.ids + o0, sizeof(int64_t) * (size_t)len,
-                                    hipMemcpyDeviceToDevice, st));
-        if (xn_old)
-            HIPANN_CHECK(hipMemcpyAsync(xn_nb.get<float>() + o1, sh.xnorm.get<float>() + o0, sizeof(float) * (size_t)len,
-                                        hipMemcpyDeviceToDevice, st));
-        const int64_t np = ceil_div(len, 32);  // the passes holding live rows (a pass's rows past len are zero)
-        if (img_h)
-            HIPANN_CHECK(hipMemcpyAsync(static_cast<char *>(h_nb.p) + hpb * (size_t)tp[l],
-                                        static_cast<const char *>(sh.codes_h.p) + hpb * (size_t)tp_old[l],
-                                        hpb * (size_t)np, hipMemcpyDeviceToDevice, st));
-        if (img_t)
-            HIPANN_CHECK(hipMemcpyAsync(static_cast<char *>(t_nb.p) + tpb * (size_t)tp[l],
-                                        static_cast<const char *>(sh.codes_t.p) + tpb * (size_t)tp_old[l],
-                                        tpb * (size_t)np, hipMemcpyDeviceToDevice, st));
-    }
-    tp_nb.ensure(sizeof(int64_t) * (nlist + 1), sh.device);
-    HIPANN_CHECK(hipMemcpyAsync(tp_nb.p, tp.data(), sizeof(int64_t) * (nlist + 1), hipMemcpyHostToDevice, st));
-    HIPANN_CHECK(hipStreamSynchronize(st));
     auto take = [](DevBuf &dst, DevBuf &src) {
         std::swap(dst.p, src.p);
         std::swap(dst.bytes, src.bytes);
         std::swap(dst.device, src.device);
     };
-    take(sh.codes_buf, codes_nb);
-    take(sh.ids_buf, ids_nb);
+    // One array at a time — allocate its new layout, move its live lists (device-to-device, list by list, in order),
+    // wait, swap, free the old one — so the transient peak is one array's old + new copy (2× the codes at most), not
+    // every array twice.  `unit` = bytes per row (rows) or per 32-row pass (the tiled images); `pass` = per pass.
+    auto move_array = [&](DevBuf &cur, const void *src_base, size_t unit, bool pass, size_t count) {
+        auto nb = std::make_unique<DevBuf>();
+        nb->ensure(unit * std::max<size_t>(count, 1), sh.device);
+        HIPANN_CHECK(hipMemsetAsync(nb->p, 0, nb->bytes, st));
+        for (int l = 0; l < nlist; ++l) {
+            const int64_t len = sh.h_len[l];
+            if (!len) continue;
+            const int64_t o0 = pass ? tp_old[l] : sh.h_off[l], o1 = pass ? tp[l] : off[l];
+            const int64_t cnt = pass ? ceil_div(len, 32) : len;  // passes holding live rows (past len: zero)
+            HIPANN_CHECK(hipMemcpyAsync(static_cast<char *>(nb->p) + unit * (size_t)o1,
+                                        static_cast<const char *>(src_base) + unit * (size_t)o0, unit * (size_t)cnt,
+                                        hipMemcpyDeviceToDevice, st));
+        }
+        HIPANN_CHECK(hipStreamSynchronize(st));
+        take(cur, *nb);  // nb now holds the old storage; freed here (borrowed storage: cur was empty)
+    };
+    move_array(sh.codes_buf, sh.codes, sizeof(float) * (size_t)d, false, (size_t)N);
     sh.codes = sh.codes_buf.get<float>();  // borrowed storage becomes owned here
+    move_array(sh.ids_buf, sh.ids, sizeof(int64_t), false, (size_t)N);
     sh.ids = sh.ids_buf.get<int64_t>();
     sh.owns_codes = true;
-    if (xn) take(sh.xnorm, xn_nb);
-    if (img_h) take(sh.codes_h, h_nb);
-    if (img_t) take(sh.codes_t, t_nb);
-    if (img_h || img_t) take(sh.tpass_off, tp_nb);
-    else sh.tpass_off.release();  // recomputed from the new capacities when an image is built
+    // L2 shards always leave with a norm array: a shard created empty (compute_row_norms skips n = 0) has none yet,
+    // and ivf_append_rows writes the new rows' norms into it (the decomposed / fp16 scans read it)
+    if (ix.metric == kL2) {
+        if (sh.xnorm.p) {
+            move_array(sh.xnorm, sh.xnorm.p, sizeof(float), false, (size_t)N);
+        } else {
+            sh.xnorm.ensure(sizeof(float) * (size_t)std::max<int64_t>(N, 1), sh.device);
+            HIPANN_CHECK(hipMemsetAsync(sh.xnorm.p, 0, sh.xnorm.bytes, st));
+        }
+    }
+    const bool img_h = sh.half_state > 0 && sh.codes_h.p, img_t = sh.codes_t.p != nullptr;
+    if (img_h) move_array(sh.codes_h, sh.codes_h.p, (size_t)ivf_half_pass_bytes(d), true, (size_t)tp[nlist]);
+    if (img_t)
+        move_array(sh.codes_t, sh.codes_t.p, sizeof(float) * (size_t)ivf_mfma_pass_floats(d), true, (size_t)tp[nlist]);
+    if (img_h || img_t) {
+        sh.tpass_off.ensure(sizeof(int64_t) * (nlist + 1), sh.device);
+        HIPANN_CHECK(hipMemcpyAsync(sh.tpass_off.p, tp.data(), sizeof(int64_t) * (nlist + 1), hipMemcpyHostToDevice, st));
+        HIPANN_CHECK(hipStreamSynchronize(st));  // tp (host) is released on return
+    } else {
+        sh.tpass_off.release();  // recomputed from the new capacities when an image is built
+    }
     upload_list_meta(sh, off, sh.h_len, nlist);
 }
 
@@ -602,13 +594,17 @@ static void ivf_add_rows(IvfIndex &ix, int64_t n, const float *xb, const int64_t
     }
 }
 
-// One block of an add: rows to the device once, coarse assignment on the GPU (shard 0's quantizer; every shard holds
-// all centroids), one readback of the assignment; then per shard owning a list with new rows: grow the lists that
-// overflow (ivf_relayout, amortised), scatter each row straight into its list's slack (one kernel: codes, label,
-// norm), update the live lengths, re-tile the tiled images' touched passes, and fold the new rows into the bounds'
-// running maxima (no rescan of the table).  Two host synchronisations per block.
+// One block of an add: rows to the device once; on shard 0's device the block's norms and, per shard, the block's
+// maxima at that shard's fp16 scale (ivf_append_rows' statistics-only pass), then the coarse assignment on the GPU
+// (shard 0's quantizer; every shard holds all centroids) — assignment and maxima come back in ONE readback, the block's
+// only host wait.  The host folds the maxima (an image the new rows leave is dropped before it is re-tiled) and
+// computes each row's physical destination; then per shard owning a list with new rows: grow the lists that overflow
+// (ivf_relayout, amortised), one pinned upload (double-buffered: the next block writes the other buffer while this
+// one's copy may still be queued), scatter each row straight into its list's slack (one kernel: codes, label, norm),
+// re-tile the tiled images' touched passes.  Nothing waits for that tail: the next search is queued behind it.
 static void ivf_add_block(IvfIndex &ix, int64_t n, const float *xb, const int64_t *ids, int64_t base) {
     const int d = ix.d, nlist = ix.nlist, metric = ix.metric;
+    const int nsh = (int)ix.shards.size();
     IvfShard &s0 = *ix.shards[0];
     DeviceGuard g0(s0.device);
     hipStream_t st = s0.stream;
@@ -626,12 +622,28 @@ static void ivf_add_block(IvfIndex &ix, int64_t n, const float *xb, const int64_
         HIPANN_CHECK(hipStreamSynchronize(st));
         t_h2d = us(t_0);
     }
-    flat_shard_search(*s0.quant, *s0.quant->shards[0], n, s0.app_rows.get<float>(), 1, 1, s0.app_norm.get<float>(),
+    // the block's ‖x‖² (the table kernel's bits, the norms the append writes on shard 0) and per shard the maxima
+    // [max ‖x‖², max |x|, max fp16 residual² at the shard's image scale]
+    launch_row_norms(s0.app_rows.get<float>(), n, d, s0.app_norm.get<float>(), st);
+    s0.app_stat.ensure(sizeof(unsigned) * 4 * (size_t)nsh, s0.device);
+    unsigned *stat = s0.app_stat.get<unsigned>();
+    for (int s = 0; s < nsh; ++s) {
+        const IvfShard &sh = *ix.shards[s];
+        const bool img_h = sh.half_state > 0 && sh.codes_h.p;
+        launch_ivf_append_rows(s0.app_rows.get<float>(), s0.app_norm.get<float>(), nullptr, nullptr, n, d, nullptr,
+                               nullptr, nullptr, nullptr, nullptr, 0, img_h ? std::ldexp(1.f, sh.half_es) : 0.f,
+                               stat + 4 * s, st);
+    }
+    s0.app_cd.ensure(sizeof(float) * (size_t)n, s0.device);  // the assignment's distances (discarded)
+    flat_shard_search(*s0.quant, *s0.quant->shards[0], n, s0.app_rows.get<float>(), 1, 1, s0.app_cd.get<float>(),
                       s0.app_assign.get<int64_t>(), st);
-    s0.app_hassign.ensure(sizeof(int64_t) * (size_t)n);
+    s0.app_hassign.ensure(sizeof(int64_t) * (size_t)n + sizeof(unsigned) * 4 * (size_t)nsh);
     const int64_t *assign = s0.app_hassign.get<int64_t>();
+    const unsigned *hstat = reinterpret_cast<const unsigned *>(assign + n);
     HIPANN_CHECK(hipMemcpyAsync(s0.app_hassign.p, s0.app_assign.p, sizeof(int64_t) * (size_t)n, hipMemcpyDeviceToHost,
                                 st));
+    HIPANN_CHECK(hipMemcpyAsync(const_cast<unsigned *>(hstat), stat, sizeof(unsigned) * 4 * (size_t)nsh,
+                                hipMemcpyDeviceToHost, st));
     HIPANN_CHECK(hipStreamSynchronize(st));
     const double t_assign = prof ? us(t_0) : 0.0;
     std::vector<int64_t> cnt(nlist, 0);
@@ -639,24 +651,45 @@ static void ivf_add_block(IvfIndex &ix, int64_t n, const float *xb, const int64_
         HIPANN_REQUIRE(assign[i] >= 0 && assign[i] < nlist, "coarse assignment out of range");
         ++cnt[assign[i]];
     }
-    for (size_t s = 0; s < ix.shards.size(); ++s) {
+    for (int s = 0; s < nsh; ++s) {
         IvfShard &sh = *ix.shards[s];
         std::vector<int64_t> add(nlist, 0);
         int64_t add_s = 0;
         bool grow = !sh.owns_codes;
         for (int l = 0; l < nlist; ++l) {
-            if (ix.owner[l] != (int)s) continue;
+            if (ix.owner[l] != s) continue;
             add[l] = cnt[l];
             add_s += add[l];
             if (sh.h_len[l] + add[l] > sh.h_off[l + 1] - sh.h_off[l]) grow = true;
         }
         if (!add_s) continue;
+        // the block's maxima (over all its rows: for a shard that takes only some of them the bounds are at worst
+        // slightly loose, never wrong) folded before anything is written
+        const unsigned *hs = hstat + 4 * s;
+        float v;
+        std::memcpy(&v, &hs[0], sizeof(v));
+        if (sh.xmax2 >= 0.f) sh.xmax2 = std::max(sh.xmax2, v);  // max ‖x‖² (the rerank bound's row term)
+        if (sh.half_state > 0 && sh.codes_h.p) {
+            float mx, r2;
+            std::memcpy(&mx, &hs[1], sizeof(mx));
+            std::memcpy(&r2, &hs[2], sizeof(r2));
+            if (hs[1] >= 0x7f800000u) {  // a non-finite new entry: the fp16 form no longer applies (form 5 runs)
+                sh.half_state = -1;
+                sh.codes_h.release();
+            } else if (mx >= std::ldexp(1.f, 14 - sh.half_es)) {  // outside the image's scale: rebuilt at the next search
+                sh.half_state = 0;
+                sh.codes_h.release();
+            } else {
+                sh.half_rxmax = std::max(sh.half_rxmax, std::sqrt(r2) * 1.0001f);
+            }
+        }
         DeviceGuard g(sh.device);
         hipStream_t ss = sh.stream;
-        if (&sh != &s0) {  // the block's rows on this shard's device too
+        if (&sh != &s0) {  // the block's rows (and their norms) on this shard's device too
             sh.app_rows.ensure(sizeof(float) * (size_t)n * d, sh.device);
             sh.app_norm.ensure(sizeof(float) * (size_t)n, sh.device);
             HIPANN_CHECK(hipMemcpyAsync(sh.app_rows.p, xb, sizeof(float) * (size_t)n * d, hipMemcpyHostToDevice, ss));
+            launch_row_norms(sh.app_rows.get<float>(), n, d, sh.app_norm.get<float>(), ss);
         }
         if (grow) ivf_relayout(ix, sh, add);
         // one pinned upload: [physical destination per row (−1: another shard's list) | label per row | the tiled
@@ -670,12 +703,16 @@ static void ivf_add_block(IvfIndex &ix, int64_t n, const float *xb, const int64_
             if (add[l]) np += ceil_div(len[l] + add[l], 32) - len[l] / 32;
         }
         const size_t up_bytes = sizeof(int64_t) * (size_t)(2 * n + np) + sizeof(int) * (size_t)nlist;
-        sh.app_hup.ensure(up_bytes);
-        int64_t *dst = sh.app_hup.get<int64_t>(), *lab = dst + n, *passes = lab + n;
+        const int b = sh.app_buf;
+        sh.app_buf ^= 1;
+        if (sh.app_ev[b]) HIPANN_CHECK(hipEventSynchronize(sh.app_ev[b]));  // its copy two blocks ago (long done)
+        HostBuf &hup = sh.app_hup[b];
+        hup.ensure(up_bytes);
+        int64_t *dst = hup.get<int64_t>(), *lab = dst + n, *passes = lab + n;
         int *newlen = reinterpret_cast<int *>(passes + np);
         for (int64_t i = 0; i < n; ++i) {
             const int64_t l = assign[i];
-            dst[i] = ix.owner[l] == (int)s ? sh.h_off[l] + len[l]++ : -1;
+            dst[i] = ix.owner[l] == s ? sh.h_off[l] + len[l]++ : -1;
             lab[i] = ids ? ids[i] : base + i;
         }
         int64_t pi = 0, maxlen = 0, live = 0;
@@ -687,20 +724,18 @@ static void ivf_add_block(IvfIndex &ix, int64_t n, const float *xb, const int64_
             live += len[l];
         }
         sh.app_up.ensure(up_bytes, sh.device);
-        HIPANN_CHECK(hipMemcpyAsync(sh.app_up.p, sh.app_hup.p, up_bytes, hipMemcpyHostToDevice, ss));
+        HIPANN_CHECK(hipMemcpyAsync(sh.app_up.p, hup.p, up_bytes, hipMemcpyHostToDevice, ss));
+        if (!sh.app_ev[b]) HIPANN_CHECK(hipEventCreateWithFlags(&sh.app_ev[b], hipEventDisableTiming));
+        HIPANN_CHECK(hipEventRecord(sh.app_ev[b], ss));
         const int64_t *ddst = sh.app_up.get<int64_t>(), *dlab = ddst + n, *dpass = dlab + n;
         const int *dlen = reinterpret_cast<const int *>(dpass + np);
         const bool img_h = sh.half_state > 0 && sh.codes_h.p, img_t = sh.codes_t.p != nullptr;
         const float hscale = std::ldexp(1.f, sh.half_es);
-        // norms over the block with the table's own kernel (the bits a rebuild computes), then one kernel: rows,
-        // labels and norms into their CSR rows, the new lengths, this shard's new-row maxima
-        sh.app_stat.ensure(sizeof(unsigned) * 4, sh.device);
-        unsigned *stat = sh.app_stat.get<unsigned>();
-        launch_row_norms(sh.app_rows.get<float>(), n, d, sh.app_norm.get<float>(), ss);
+        // one kernel: rows, labels and norms into their CSR rows, the new lengths
         launch_ivf_append_rows(sh.app_rows.get<float>(), sh.app_norm.get<float>(), ddst, dlab, n, d,
                                sh.codes_buf.get<float>(), sh.ids_buf.get<int64_t>(),
                                metric == kL2 ? sh.xnorm.get<float>() : nullptr, dlen, sh.list_len.get<int>(), nlist,
-                               img_h ? hscale : 0.f, stat, ss);
+                               0.f, nullptr, ss);
         sh.h_len = len;
         sh.live = live;
         sh.max_nch = (int)std::max<int64_t>(1, ceil_div(maxlen, ivf_chunk_rows()));
@@ -711,29 +746,10 @@ static void ivf_add_block(IvfIndex &ix, int64_t n, const float *xb, const int64_
         if (np > 0 && img_t)
             launch_ivf_tile_codes(sh.codes, sh.list_off.get<int64_t>(), sh.list_len.get<int>(),
                                   sh.tpass_off.get<int64_t>(), nlist, np, d, sh.codes_t.get<float>(), ss, dpass);
-        sh.app_hstat.ensure(sizeof(unsigned) * 4);
-        unsigned *hs = sh.app_hstat.get<unsigned>();
-        HIPANN_CHECK(hipMemcpyAsync(hs, stat, sizeof(unsigned) * 4, hipMemcpyDeviceToHost, ss));
-        HIPANN_CHECK(hipStreamSynchronize(ss));  // (the pinned staging above is reused by the next block)
-        if (prof)
-            std::fprintf(stderr, "hipann append: n %lld h2d %.0f us, assign %.0f us, shard %zu done %.0f us (grow %d, %lld passes)\n",
+        if (prof) {
+            HIPANN_CHECK(hipStreamSynchronize(ss));
+            std::fprintf(stderr, "hipann append: n %lld h2d %.0f us, assign %.0f us, shard %d done %.0f us (grow %d, %lld passes)\n",
                          (long long)n, t_h2d, t_assign, s, us(t_0), (int)grow, (long long)np);
-        float v;
-        std::memcpy(&v, &hs[0], sizeof(v));
-        if (sh.xmax2 >= 0.f) sh.xmax2 = std::max(sh.xmax2, v);  // max ‖x‖² (the rerank bound's row term)
-        if (img_h) {
-            float mx, r2;
-            std::memcpy(&mx, &hs[1], sizeof(mx));
-            std::memcpy(&r2, &hs[2], sizeof(r2));
-            if (hs[1] >= 0x7f800000u) {  // a non-finite new entry: the fp16 form no longer applies (form 5 runs)
-                sh.half_state = -1;
-                sh.codes_h.release();
-            } else if (mx >= std::ldexp(1.f, 14 - sh.half_es)) {  // outside the image's scale: rebuilt at the next search
-                sh.half_state = 0;
-                sh.codes_h.release();
-            } else {
-                sh.half_rxmax = std::max(sh.half_rxmax, std::sqrt(r2) * 1.0001f);
-            }
         }
     }
 }

@@ -1029,16 +1029,18 @@ ivf_append_rows(const float *__restrict__ rows, const float *__restrict__ norms,
     const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (j >= n) return;
-    const int64_t r = dst[j];
+    // dst == nullptr: statistics only (every row of the block; nothing written but stat) — the pre-pass whose maxima
+    // come back with the coarse assignment, so the append needs no host wait of its own
+    const int64_t r = dst ? dst[j] : 0;
     if (r < 0) return;
     const float *src = rows + j * (int64_t)d;
-    float *out = codes + r * (int64_t)d;
+    float *out = dst ? codes + r * (int64_t)d : nullptr;
     const float inv = hscale > 0.f ? 1.f / hscale : 0.f;
     unsigned mabs = 0;
     float res = 0.f;
     for (int e = lane; e < d; e += 64) {
         const float x = src[e];
-        out[e] = x;
+        if (out) out[e] = x;
         mabs = max(mabs, __float_as_uint(x) & 0x7fffffffu);
         if (hscale > 0.f) {
             const float q = x - mh_val(mh_half_bits(x * hscale)) * inv;
@@ -1051,8 +1053,11 @@ ivf_append_rows(const float *__restrict__ rows, const float *__restrict__ norms,
         res += __shfl_xor(res, o);
     }
     if (lane == 0) {
-        ids[r] = ids_in[j];
-        if (xnorm) xnorm[r] = norms[j];
+        if (dst) {
+            ids[r] = ids_in[j];
+            if (xnorm) xnorm[r] = norms[j];
+        }
+        if (!stat) return;
         atomicMax(stat + 0, __float_as_uint(norms[j]));
         atomicMax(stat + 1, mabs);
         if (hscale > 0.f) atomicMax(stat + 2, __float_as_uint(res));
@@ -1401,7 +1406,7 @@ void launch_ivf_append_rows(const float *rows, const float *norms, const int64_t
                             float hscale, unsigned *stat, hipStream_t st) {
     const int64_t blocks = std::max(ceil_div(n, (int64_t)4), ceil_div((int64_t)nlist, (int64_t)256));
     HIPANN_REQUIRE(blocks < (int64_t)0x7fffffff, "append block too large");
-    HIPANN_CHECK(hipMemsetAsync(stat, 0, sizeof(unsigned) * 4, st));
+    if (stat) HIPANN_CHECK(hipMemsetAsync(stat, 0, sizeof(unsigned) * 4, st));
     hipLaunchKernelGGL(ivf_append_rows, dim3((unsigned)blocks), dim3(256), 0, st, rows, norms, dst, ids_in, n, d, codes,
                        ids, xnorm, newlen, list_len, nlist, hscale, stat);
     HIPANN_CHECK(hipGetLastError());

@@ -412,7 +412,9 @@ struct IvfShard {
     DevBuf app_cd;  // hipann_ivf_coarse_device: the coarse distances (discarded)
     // pinned: the assignment on its way down, [destinations | labels | touched passes | live lengths] on their way
     // up (one copy), the maxima on their way down
-    HostBuf app_hassign, app_hup, app_hstat;
+    HostBuf app_hassign, app_hup[2];
+    hipEvent_t app_ev[2] = {nullptr, nullptr};  // app_hup[b]'s upload has been consumed (reused two blocks later)
+    int app_buf = 0;
     int max_nch = 1;  // largest list's row-chunk count
     StreamFence fence;  // cross-stream ordering of this shard's calls (its coarse quantizer's scratch included)
     hipEvent_t done = nullptr;  // multi-device search: the shard's search has drained (shard 0's stream waits)

@@ -47,6 +47,7 @@ TAU = 1e-6
 # per q·x (3·2^-16 plus the operands' 2^-17 remainders), i.e. ≤ 3.1e-5 of the L2 / IP scale.
 SPLIT2_TAU = 4e-5
 PARITY_STATS: list = []
+PROBE_STATS: list = []  # oracle_on_gpu_probes: differing probe lists per check
 CURRENT_TEST = None
 
 
@@ -91,7 +92,8 @@ def oracle_on_gpu_probes(oracle, cen, off, ids, codes, xq, k, P, Po, Do, Io, met
     if nd:
         Dp, Ip = oracle.ivf_search_preassigned(off, ids, codes, xq[~same], k, P[~same], metric)
         D[~same], I[~same] = Dp, Ip
-    PARITY_STATS.append({"name": CURRENT_TEST, "probe_lists_differing": nd, "nq": int(len(xq))})
+    PROBE_STATS.append({"name": CURRENT_TEST, "probe_lists_differing": nd, "nq": int(len(xq)),
+                        "queries": np.nonzero(~same)[0][:32].tolist()})
     return D, I, nd
 
 

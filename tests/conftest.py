@@ -36,9 +36,12 @@ def pytest_sessionfinish(session, exitstatus):
     import _data
 
     st = _data.PARITY_STATS
+    out = ROOT / "gpurun_out"
+    if _data.PROBE_STATS:
+        out.mkdir(exist_ok=True)
+        (out / "probe_parity.json").write_text(json.dumps(_data.PROBE_STATS, indent=1) + "\n")
     if not st:
         return
-    out = ROOT / "gpurun_out"
     out.mkdir(exist_ok=True)
     worst = max(st, key=lambda r: r["max_gap_over_scale"])
     summary = {

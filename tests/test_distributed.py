@@ -484,3 +484,64 @@ def test_sharded_ivf_partitioned_coarse_world2_on_one_device(gpu, tmp_path):
         assert np.array_equal(z["P1"], z["P0"])
         assert np.array_equal(z["last"], z["P0"])  # the search ran with those lists
         assert np.array_equal(z["I1"], z["I0"]) and np.array_equal(z["D1"], z["D0"])
+
+
+# ------------------------------------------------------------------------------------------------
+# world-4 list sharding on the C3 headline's own list sizes and probe lists
+# ------------------------------------------------------------------------------------------------
+C3_LISTS = ROOT / "tests" / "golden" / "c3_lists_10m.npz"
+
+
+def _worker_c3_world4(rank, world, port, result_path):
+    dist = _setup(rank, world, port)
+    import torch
+    from sharded import PartitionedProbes, assign_lists
+
+    z = np.load(C3_LISTS)
+    sizes, probes = z["sizes"].astype(np.int64), z["probes"].astype(np.int64)
+    nq, nprobe = probes.shape
+
+    def coarse(qidx, out):  # this rank's slice of the batch: the bench's own probe lists of those queries
+        out.copy_(torch.from_numpy(probes[qidx[:, 0].numpy()]))
+
+    pp = PartitionedProbes(coarse, nq, nprobe, "cpu")
+    P = pp.probes(torch.arange(nq, dtype=torch.int64)[:, None]).numpy().copy()
+    owner = assign_lists(sizes, world)
+    mine = np.unique(P[P >= 0])
+    mine = mine[owner[mine] == rank]
+    row_bytes = 2 * 768 + 4  # the fp16 image + the L2 norm per row (the default scan's algorithmic bytes)
+    b = torch.tensor([float(sizes[mine].sum()) * row_bytes], dtype=torch.float64)
+    allb = [torch.empty_like(b) for _ in range(world)]
+    dist.all_gather(allb, b)
+    if rank == 0:
+        np.savez(result_path, P=P, per_rank=np.array([float(t.item()) for t in allb]), owner=owner)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.skipif(not C3_LISTS.exists(), reason="C3 list fixture not generated")
+def test_c3_list_sharding_gloo_world4_balance(tmp_path):
+    """The headline's 1024 list sizes and one 1024-query batch's probe lists (tests/golden/c3_lists_10m.npz, written
+    by bench.py's C3 run on the MI355X): four gloo ranks each compute their quarter of the probe lists, one all-gather
+    (PartitionedProbes) gives every rank the whole batch's lists, identical to the replicated step, and the
+    size-balanced list assignment (assign_lists, = hipann_ivf_create's rule) leaves every rank within 5 % of the mean
+    per-rank scan bytes; the ranks' bytes add up to the single-GPU scan's."""
+    import torch.multiprocessing as mp
+
+    out = tmp_path / "res.npz"
+    mp.spawn(_worker_c3_world4, args=(4, _free_port(), str(out)), nprocs=4, join=True)
+    r = np.load(out)
+    z = np.load(C3_LISTS)
+    sizes, probes = z["sizes"].astype(np.int64), z["probes"].astype(np.int64)
+    assert np.array_equal(r["P"], probes)
+    per = r["per_rank"]
+    total = float(sizes[np.unique(probes[probes >= 0])].sum()) * (2 * 768 + 4)
+    assert abs(per.sum() - total) <= 1e-6 * total
+    assert per.max() / per.mean() <= 1.05, per / per.mean()
+    for w in (2, 8):  # the other scaling points of the bench, same rule (host-side check)
+        sys.path.insert(0, str(ROOT / "duckdb-annsearch_amd"))
+        from sharded import assign_lists
+        own = assign_lists(sizes, w)
+        lp = np.unique(probes[probes >= 0])
+        pw = np.array([sizes[lp[own[lp] == rr]].sum() for rr in range(w)], np.float64)
+        assert pw.max() / pw.mean() <= 1.05, (w, pw / pw.mean())
