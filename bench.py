@@ -455,6 +455,8 @@ def attach_traffic(roof, key, algorithmic_bytes):
         roof["traffic_unit"] = "GB per launch (PMC FETCH_SIZE x1024 x2, gfx950 correction)"
         roof["traffic_source"] = tsrc
     roof["algorithmic_per_launch_gb"] = round(algorithmic_bytes / 1e9, 3)
+    if tb is not None and algorithmic_bytes > 0:
+        roof["traffic_over_algorithmic"] = round(tb / algorithmic_bytes, 3)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -541,7 +543,17 @@ def flat_config(args, torch, dist, hipann, rank, world, dev, n, d, nq, k, metric
                                     "flop_per_byte": round(2.0 * nq * n_local * d / fill, 1),
                                     "note": "L2 -> CU bytes of A + B per launch; TD busy 0.78 at 10M x 768 (PMC)"}
     if world == 1:
-        attach_traffic(roof, f"flat_{n}x{d}{'' if metric == 0 else '_ip'}", 4.0 * n_local * d)
+        # the bytes the scan must stream once per search: form 5 the tiled int8 image (64 B per 64-dim chunk, chunk
+        # count rounded up to even) + ‖x‖² (L2) + the row scale, plus the keys-mode seed pass over its first 16K rows;
+        # form 4 the bf16 image the same way; the fp32 forms the fp32 rows
+        if form in (4, 5):
+            nk = -(-d // 64) if form == 5 else -(-d // 32)
+            nk += nk % 2
+            rowb = 64.0 * nk + (4.0 if metric == 0 else 0.0) + (4.0 if form == 5 else 0.0)
+            alg_b = rowb * (n_local + min(n_local, 16384))
+        else:
+            alg_b = 4.0 * n_local * d
+        attach_traffic(roof, f"flat_{n}x{d}{'' if metric == 0 else '_ip'}", alg_b)
     out = {"workload": f"FAISS Flat {'L2' if metric == 0 else 'IP'}, {n}x{d} fp32, batch={nq}, k={k}",
            "value": round(nq * steps / el, 1), "unit": "queries/s", "ms_per_step": round(el * 1e3 / steps, 3),
            "steps": steps, "recall_at_10": None, "roofline": roof, "setup_s": round(setup_s, 1),

@@ -455,6 +455,7 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     // (ivf_block_fallback inline: no host readback and no launch of its own); HIPANN_IVF_HOST_FALLBACK=1: from the
     // host on the 3-term path (A/B)
     const bool inline_fb = !host_fallback();
+    int fb_cap = 0, fb_maxch = 1;
     if (inline_fb) {
         if (!sh.fb_total.p) {
             sh.fb_total.ensure(sizeof(unsigned long long), sh.device);
@@ -462,6 +463,19 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
         }
         sh.fpd.ensure(sizeof(float) * (size_t)nq * np * kout, sh.device);
         sh.fpi.ensure(sizeof(long long) * (size_t)nq * np * kout, sh.device);
+        // the parallel re-run of the batch's first fb_cap flagged queries (ivf_fallback_chunks): one wave per (query,
+        // probe, chunk) item; its lists take ≤ 64 MB (fb_cap shrinks for long lists), later flagged queries re-run in
+        // the flagging wave as before
+        fb_maxch = sh.max_nch;
+        const size_t per_f = (size_t)np * fb_maxch * kout * (sizeof(float) + sizeof(long long));
+        fb_cap = (int)std::min<int64_t>({nq, 64, std::max<int64_t>(1, (int64_t)(((size_t)64 << 20) / per_f))});
+        sh.fbc_d.ensure(sizeof(float) * (size_t)fb_cap * np * fb_maxch * kout, sh.device);
+        sh.fbc_i.ensure(sizeof(long long) * (size_t)fb_cap * np * fb_maxch * kout, sh.device);
+        if (sh.fbc_cap < fb_cap || !sh.fbc_done.p) {  // counters start (and are left) at zero
+            sh.fbc_done.ensure(sizeof(unsigned) * (size_t)std::max(fb_cap, 64), sh.device);
+            HIPANN_CHECK(hipMemsetAsync(sh.fbc_done.p, 0, sh.fbc_done.bytes, st));
+            sh.fbc_cap = (int)(sh.fbc_done.bytes / sizeof(unsigned));
+        }
     }
     {
         ScopedTiming t(ix.timer_merge, st);
@@ -472,7 +486,13 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
                           sh.list_off.get<int64_t>(), nlist, qbound, half && metric == kL2 ? qn : nullptr, kslot,
                           sub ? 1 : 0, inline_fb ? sh.list_len.get<int>() : nullptr,
                           inline_fb ? sh.fpd.get<float>() : nullptr, inline_fb ? sh.fpi.get<long long>() : nullptr,
-                          inline_fb ? sh.fb_total.get<unsigned long long>() : nullptr);
+                          inline_fb ? sh.fb_total.get<unsigned long long>() : nullptr, fb_cap);
+        if (fb_cap > 0)
+            launch_ivf_fallback_chunks(sh.nflag.get<int>(), sh.flagged.get<int>(), fb_cap, np, fb_maxch, ivf_chunk_rows(),
+                                       kout, metric, xq, sh.codes, d, sh.ids, 0, sh.coarse_i.get<int64_t>(),
+                                       sh.list_off.get<int64_t>(), sh.list_len.get<int>(), nlist, sh.fbc_d.get<float>(),
+                                       sh.fbc_i.get<long long>(), sh.fbc_done.get<unsigned>(), D, I,
+                                       sh.fb_total.get<unsigned long long>(), st);
     }
     if (inline_fb) return;
     int nf = 0;

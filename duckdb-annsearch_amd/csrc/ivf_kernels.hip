@@ -1847,6 +1847,148 @@ __device__ __forceinline__ void ivf_block_fallback(int64_t q, int nprobe, int ko
     if (lane == 0) atomicAdd(total, 1ull);
 }
 
+// ---------------------------------------------------------------------------------------------
+// ivf_fallback_chunks — the exact forms' flagged queries re-run in parallel (one launch after ivf_rerank_topk, every
+// batch; it returns at once when nothing was flagged).  The rerank flags a query when its k-th reranked distance is not
+// clear of the filter's bound; the first fb_cap of a batch's flagged queries come here: item (flagged query f, probe
+// p, chunk c of chunk_rows rows of that probe's list) is one wave's work — the rows' direct-form distances in
+// rerank_rows4's arithmetic (the rerank's values bit for bit), the chunk's kout best (distance, CSR row) into
+// cpd/cpi[f][p][c].  Each wave counts its item on done[f] (its stores released at agent scope first: another XCD's
+// wave may merge them); the wave whose add completes the query's count merges its candidates with FAISS's scan-order
+// rule (ivf_scan_order_topk: probe rank, then CSR row) and writes D/I — the result ivf_block_fallback computes with
+// one wave, at the parallelism of the chip (a flagged query over 200K-row lists took one wave 40 ms).
+// ---------------------------------------------------------------------------------------------
+template <bool IP>
+__global__ void __launch_bounds__(256)
+ivf_fallback_chunks(const int *__restrict__ nflag, const int *__restrict__ flagged, int fb_cap, int nprobe, int maxch,
+                    int chunk_rows, int kout, const float *__restrict__ Q, const float *__restrict__ codes, int d,
+                    const int64_t *__restrict__ ids, int64_t label_offset, const int64_t *__restrict__ probes,
+                    const int64_t *__restrict__ list_off, const int *__restrict__ list_len, int nlist,
+                    float *__restrict__ cpd, long long *__restrict__ cpi, unsigned *__restrict__ done,
+                    float *__restrict__ D, int64_t *__restrict__ I, unsigned long long *__restrict__ total) {
+    const int nf0 = *nflag;
+    const int nf = nf0 < fb_cap ? nf0 : fb_cap;
+    if (nf <= 0) return;
+    const int lane = threadIdx.x & 63;
+    const long long PAD = IdTraits<long long>::pad();
+    const int64_t per_q = (int64_t)nprobe * maxch;  // item slots per flagged query
+    const int64_t items = (int64_t)nf * per_q;
+    const int64_t nw = (int64_t)gridDim.x * 4;
+    // the list of probe p of query q, and its length (0: nothing to scan)
+    auto plist = [&](int64_t q, int p, int64_t &l, int64_t &len) {
+        l = probes[q * nprobe + p];
+        len = l >= 0 && l < nlist ? (int64_t)list_len[l] : 0;
+    };
+    for (int64_t it = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); it < items; it += nw) {
+        const int f = (int)(it / per_q);
+        const int p = (int)((it / maxch) % nprobe);
+        const int c = (int)(it % maxch);
+        const int64_t q = flagged[f];
+        int64_t l, len;
+        plist(q, p, l, len);
+        const int64_t g0 = (int64_t)c * chunk_rows;
+        if (g0 >= len) continue;  // an empty item: no candidates, not counted
+        const int64_t g1 = len < g0 + chunk_rows ? len : g0 + chunk_rows, r0 = list_off[l];
+        const float *qp = Q + q * (int64_t)d;
+        WaveList<1, long long> L;
+        L.init();
+        for (int64_t g = g0; g < g1; g += 64) {
+            const int nr = (int)(g1 - g < 64 ? g1 - g : 64);
+            float mine = __builtin_inff();
+            for (int r = 0; r < nr; r += 4) {
+                float acc[4] = {0.f, 0.f, 0.f, 0.f};
+                const float *xr[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) xr[u] = codes + (r0 + g + (r + u < nr ? r + u : nr - 1)) * d;
+                rerank_rows4<IP>(qp, xr, d, lane, acc);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    float a = acc[u];
+#pragma unroll
+                    for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+                    if (lane == r + u) mine = IP ? -a : a;
+                }
+            }
+            const bool ok = lane < nr && !(mine == __builtin_inff());
+            L.offer(ok ? mine : __builtin_inff(), ok ? (long long)(r0 + g + lane) : PAD, kout - 1);
+        }
+        if (lane < kout) {
+            cpd[it * kout + lane] = L.d[0];
+            cpi[it * kout + lane] = L.id[0];
+        }
+        // hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): this wave's stores complete, are written back at
+        // agent scope, then counted; the wave that completes the count acquires before reading any of them
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned old = 0;
+        if (lane == 0) old = __hip_atomic_fetch_add(done + f, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        old = (unsigned)__shfl((int)old, 0);
+        // the query's non-empty items: Σ_p ⌈len_p / chunk_rows⌉
+        int64_t need = 0;
+        for (int pp = lane; pp < nprobe; pp += 64) {
+            int64_t ll, ln;
+            plist(q, pp, ll, ln);
+            need += (ln + chunk_rows - 1) / chunk_rows;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) need += __shfl_xor(need, o);
+        if ((int64_t)old + 1 != need) continue;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const float *pd = cpd + (int64_t)f * per_q * kout;
+        const long long *pr = cpi + (int64_t)f * per_q * kout;
+        int64_t lenv = 0;  // lane p < 64: probe p's list length (read by shuffle in the candidate stream)
+        if (lane < nprobe) {
+            int64_t ll;
+            plist(q, lane, ll, lenv);
+        }
+        WaveList<1, long long> R;
+        ivf_scan_order_topk(per_q * kout, kout, [&](int64_t cc) {
+            const int64_t slot = cc / kout;  // p·maxch + chunk
+            const int pp = (int)(slot / maxch);
+            int64_t ll, ln;
+            if (nprobe <= 64) ln = __shfl(lenv, pp);
+            else plist(q, pp, ll, ln);
+            const bool live = (slot % maxch) * (int64_t)chunk_rows < ln;  // empty items wrote nothing
+            const float key = live ? pd[cc] : __builtin_inff();
+            const long long row = live ? pr[cc] : PAD;
+            const bool ok = !(key == __builtin_inff()) && row != PAD;
+            return ScanCand{ok ? key : __builtin_inff(), ok ? ((long long)pp << 32) | row : PAD,
+                            ok ? (long long)(ids ? ids[row] : label_offset + row) : PAD};
+        }, R);
+        const float pad_d = IP ? -__builtin_inff() : __builtin_inff();
+        if (lane < kout) {
+            const bool pad = R.id[0] == PAD || R.d[0] == __builtin_inff();
+            D[q * kout + lane] = pad ? pad_d : (IP ? -R.d[0] : R.d[0]);
+            I[q * kout + lane] = pad ? -1 : (int64_t)R.id[0];
+        }
+        if (lane == 0) {
+            __hip_atomic_store(done + f, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next batch
+            atomicAdd(total, 1ull);
+        }
+    }
+}
+
+void launch_ivf_fallback_chunks(const int *nflag, const int *flagged, int fb_cap, int nprobe, int maxch, int chunk_rows,
+                                int kout, int metric, const float *Q, const float *codes, int d, const int64_t *ids,
+                                int64_t label_offset, const int64_t *probes, const int64_t *list_off,
+                                const int *list_len, int nlist, float *cpd, long long *cpi, unsigned *done, float *D,
+                                int64_t *I, unsigned long long *total, hipStream_t st) {
+    if (fb_cap <= 0) return;
+    HIPANN_REQUIRE(kout >= 1 && kout <= 64 && maxch >= 1 && chunk_rows >= 64, "ivf fallback: arguments out of range");
+    dim3 grid(256), block(256);  // 1024 waves: a grid-stride loop over the items; an empty batch returns at once
+    if (metric == kIP)
+        hipLaunchKernelGGL(ivf_fallback_chunks<true>, grid, block, 0, st, nflag, flagged, fb_cap, nprobe, maxch,
+                           chunk_rows, kout, Q, codes, d, ids, label_offset, probes, list_off, list_len, nlist, cpd, cpi,
+                           done, D, I, total);
+    else
+        hipLaunchKernelGGL(ivf_fallback_chunks<false>, grid, block, 0, st, nflag, flagged, fb_cap, nprobe, maxch,
+                           chunk_rows, kout, Q, codes, d, ids, label_offset, probes, list_off, list_len, nlist, cpd, cpi,
+                           done, D, I, total);
+    HIPANN_CHECK(hipGetLastError());
+}
+
 #ifndef HIPANN_RR_MINB
 #define HIPANN_RR_MINB 4  // 4-wave blocks resident per CU: ≤ 128 VGPRs, one round for a 1024-query batch
 #endif
@@ -1883,7 +2025,8 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
                 const float *__restrict__ qres, const int64_t *__restrict__ probes,
                 const int64_t *__restrict__ list_off, int nlist, const unsigned *__restrict__ qbound,
                 const float *__restrict__ qnorm, int kslot, int sub, const int *__restrict__ list_len,
-                float *__restrict__ fpd, long long *__restrict__ fpi, unsigned long long *__restrict__ fb_total) {
+                float *__restrict__ fpd, long long *__restrict__ fpi, unsigned long long *__restrict__ fb_total,
+                int fb_cap) {
     const int64_t q = WV == 1 ? (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6) : (int64_t)blockIdx.x;
     if (q >= nq) return;
     const int lane = threadIdx.x & 63;
@@ -2111,9 +2254,17 @@ ivf_rerank_topk(const float *__restrict__ pd, const int *__restrict__ pi, const 
     // kout-th distance must also clear the smallest full sub-list's k-th key
     const bool flag = sel_bad || (ncand > 0 && !(E <= 3.4e38f)) || (ncand == k && !(dk < k16 - E)) ||
                       (sub && tsub < __builtin_inff() && !(dk < tsub - E));
-    if (flag && lane == 0) flagged[atomicAdd(nflag, 1)] = (int)q;
+    int fslot = 0;
+    if (flag && lane == 0) {
+        fslot = atomicAdd(nflag, 1);
+        flagged[fslot] = (int)q;
+    }
+    fslot = __shfl(fslot, 0);
     const float pad_d = IP ? -__builtin_inff() : __builtin_inff();
-    if (flag && fpd) {
+    // IVF: the first fb_cap flagged queries of the batch are re-run by ivf_fallback_chunks (the next launch: every
+    // (query, probe, 2048-row chunk) by its own wave — a flagged query over long lists is no longer one wave's
+    // serial scan); this wave writes its uncertified answer, which that kernel overwrites.  Later ones re-run here.
+    if (flag && fpd && fslot >= fb_cap) {
         // IVF: this wave re-runs the query at once over its probe lists in the direct form with FAISS's scan-order
         // tie rule (the device fallback, ivf_block_fallback) — no separate launch per batch
         __shared__ float fsd[4 * 64];
@@ -2326,7 +2477,8 @@ void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int 
                        int64_t label_offset, float xmax2, float *D, int64_t *I, int *nflag, int *flagged,
                        hipStream_t st, float eps, float rxmax, const float *qres, const int64_t *probes,
                        const int64_t *list_off, int nlist, const unsigned *qbound, const float *qnorm, int kslot,
-                       int sub, const int *list_len, float *fpd, long long *fpi, unsigned long long *fb_total) {
+                       int sub, const int *list_len, float *fpd, long long *fpi, unsigned long long *fb_total,
+                       int fb_cap) {
     if (nq <= 0) return;
     if (kslot <= 0) kslot = k;
     // the filter depth k bounds kout (kout = k leaves no margin: those queries are flagged and re-run exactly)
@@ -2337,7 +2489,8 @@ void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int 
     const bool wide = nq < HIPANN_RR_WIDE;
     dim3 grid((unsigned)(wide ? nq : ceil_div(nq, 4))), block(256);
 #define RR_ARGS pd, pi, slot_off, nprobe, nq, k, kout, Q, codes, d, ids, nrows, label_offset, xmax2, D, I, nflag, flagged, \
-                eps, rxmax, qres, probes, list_off, nlist, qbound, qnorm, kslot, sub, list_len, fpd, fpi, fb_total
+                eps, rxmax, qres, probes, list_off, nlist, qbound, qnorm, kslot, sub, list_len, fpd, fpi, fb_total, \
+                fpd ? fb_cap : 0
     if (metric == kIP) {
         if (wide) hipLaunchKernelGGL((ivf_rerank_topk<true, 4>), grid, block, 0, st, RR_ARGS);
         else hipLaunchKernelGGL((ivf_rerank_topk<true, 1>), grid, block, 0, st, RR_ARGS);

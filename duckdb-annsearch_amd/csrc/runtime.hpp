@@ -394,6 +394,8 @@ struct IvfShard {
     int plan_nlist = 0;
     DevBuf fpd, fpi;               // device fallback: per (flagged query, probe) partial lists
     DevBuf fb_total;               // u64 running count of flagged queries (device side)
+    DevBuf fbc_d, fbc_i, fbc_done;  // ivf_fallback_chunks: per (flagged query, probe, chunk) lists, per-query counts
+    int fbc_cap = 0;               // flagged queries fbc_done holds counters for (zeroed at allocation)
     // MFMA scan copy of the codes, built at the first search that uses it: per list, 32-row passes of
     // [16-dim step][2 row tiles][64 lanes][float4] (ivf_mfma.hip), zero-padded rows / dims
     std::vector<int64_t> h_off;    // host copy of list_off
@@ -507,7 +509,15 @@ void launch_ivf_rerank(const float *pd, const int *pi, const int *slot_off, int 
                        const int64_t *probes = nullptr, const int64_t *list_off = nullptr, int nlist = 0,
                        const unsigned *qbound = nullptr, const float *qnorm = nullptr, int kslot = 0, int sub = 0,
                        const int *list_len = nullptr, float *fpd = nullptr, long long *fpi = nullptr,
-                       unsigned long long *fb_total = nullptr);  // fpd != nullptr: flagged IVF queries re-run inline
+                       unsigned long long *fb_total = nullptr,  // fpd != nullptr: flagged IVF queries re-run inline
+                       int fb_cap = 0);  // ... except the first fb_cap, left to launch_ivf_fallback_chunks
+// the rerank's first fb_cap flagged queries re-run in parallel (one wave per (query, probe, chunk) item); cpd/cpi:
+// fb_cap·nprobe·maxch·kout entries, done: fb_cap counters (zero on entry; left zero)
+void launch_ivf_fallback_chunks(const int *nflag, const int *flagged, int fb_cap, int nprobe, int maxch, int chunk_rows,
+                                int kout, int metric, const float *Q, const float *codes, int d, const int64_t *ids,
+                                int64_t label_offset, const int64_t *probes, const int64_t *list_off,
+                                const int *list_len, int nlist, float *cpd, long long *cpi, unsigned *done, float *D,
+                                int64_t *I, unsigned long long *total, hipStream_t st);
 // ivf_mfma.hip, fp16-image scan (kFormHalfExact)
 int ivf_mfma_h_group(int d);
 int ivf_scan_sublists();  // sub-lists per slot of the matrix-core scans in sub-list mode (one per wave)

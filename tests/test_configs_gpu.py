@@ -31,10 +31,14 @@ from _data import TAU, check_probe_parity, check_topk_parity, oracle_on_gpu_prob
 
 pytestmark = pytest.mark.gpu
 ROOT = Path(__file__).resolve().parents[1]
-# identical probe lists given identical centroids.  The search-time coarse keys are fp32-level (a 3-term
-# bf16 split); a list that still differs from the oracle's may do so only inside the coarse tie window
-# (check_probe_parity asserts it) and its query is then checked against search_preassigned over the GPU's list.
-C3_MAX_PROBE_DIFF = 0
+# identical probe lists given identical centroids.  Neither side's fp32 coarse keys are FAISS's own sgemm
+# sums (the oracle's dot products are its compiler's SIMD order, the GPU's a 3-term bf16 split or fp32 MFMA tiles), so
+# a centroid pair whose fp64 distances differ by less than the keys' rounding can swap at the nprobe boundary.  The
+# rule held here: check_probe_parity asserts every differing rank is such a tie (fp64 gap <= 1e-6·(|q|² + max|c|²), the
+# parity window; DESIGN §2 has the key error budget), at most C3_MAX_PROBE_DIFF of the 1024 queries differ
+# (3 on the 200K-row C3 index, 0 on the 2M-row one, r06), and each such query's ids must equal the oracle's
+# IndexIVF::search_preassigned over the GPU's own probe list — every query of the batch is checked.
+C3_MAX_PROBE_DIFF = 5
 sys.path.insert(0, str(ROOT))
 
 
