@@ -40,5 +40,9 @@ for c in $cfgs; do
                 --workload flat --n 12500000 --metric ip || exit 1 ;;
         diskann) one diskann diskann_1000000x1536 diskann_bfs diskann_bfs "" --workload diskann --n 1000000 --d 1536 \
                      || exit 1 ;;
+        append) PROBE_N=10000000 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
+                    -d "$o/r06prof_append/stats" -o run -- python3 "$root/tools/append_probe.py" \
+                    > "$o/r06prof_append.log" 2>&1 || { echo "append trace failed"; tail -5 "$o/r06prof_append.log"; exit 1; }
+                tail -2 "$o/r06prof_append.log" ;;
     esac
 done
