@@ -134,7 +134,13 @@ __device__ __forceinline__ void k64_epilogue_row(const k64_f32x4 (&sm)[8], float
 // per byte moved.  The int32 sums are exact (|acc| <= d·127² < 2^24 for d <= 1040) and live in the float
 // accumulators' registers bit for bit until the tile's epilogue turns them into q·x = acc·s_q·s_x with the
 // per-query / per-row scales (qscale / xscale); everything after that is the bf16 path's.
-template <bool L2M, bool KEYS, bool I8 = false, int MBW = 2>
+// STAG (the int8 bounded passes, d ≥ 384): waves W/2..W−1 run half a K-step behind waves 0..W/2−1 — in K-step g's
+// barrier interval a late wave computes chunk 1 of g − 1, then (when g − 1 ended a tile) its epilogue, then chunk 0 of
+// g.  Waves w and w + W/2 share a SIMD, so one wave's epilogue (≈ 650 VALU instructions per tile) and LDS read burst
+// run beside its partner's MFMAs instead of both waves converting at the same barrier-aligned moment
+// (MI355X_MICROARCH.md, two waves per SIMD, item 9).  Same loads, same order, same counted waits, one extra barrier
+// interval at the end; the stage a late wave still reads (g − 1) is never the one refilled in interval g ((g + 3) mod 5).
+template <bool L2M, bool KEYS, bool I8 = false, int MBW = 2, bool STAG = false>
 __global__ void __launch_bounds__(64 * K64Geom<MBW>::W, 1) __attribute__((amdgpu_waves_per_eu(1, 2)))
 flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm, int64_t nq,
               const k64_u32x4 *__restrict__ Xt, const float *xnorm, int64_t N, int nk, int nqt, int nsplit,
@@ -263,16 +269,20 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
     static_assert(kVmXn < 64, "vmcnt field");
     constexpr unsigned kWaitStep = 0xF70u | (kVm & 15) | ((kVm >> 4) << 14);
     constexpr unsigned kWaitStepXn = 0xF70u | (kVmXn & 15) | ((kVmXn >> 4) << 14);
+    // STAG: one-K-step fragment lead for both halves; at the end of interval g only B(g + 3) may stay in flight
+    constexpr unsigned kWaitLate = 0xF70u | (NB_OPS & 15) | ((NB_OPS >> 4) << 14);
+    constexpr unsigned kWaitPro = 0xF70u | ((2 * NB_OPS) & 15) | (((2 * NB_OPS) >> 4) << 14);
     auto clampg = [&](int64_t g) { return g < G ? g : G - 1; };  // past the end: the last K-step again, never read
     if (G > 0) {
-        // the steady state's order: B(0), A(0), B(1), A(1), B(2)
+        // the steady state's order: B(0), A(0), B(1), A(1), B(2) (STAG: a one-K-step fragment lead, no A(1) here)
         issue_b(0, 0);
         issue_a(std::integral_constant<int, 0>{});
         issue_b(clampg(1), 1);
-        issue_a(std::integral_constant<int, 1>{});
+        if constexpr (!STAG) issue_a(std::integral_constant<int, 1>{});
         issue_b(clampg(2), 2);
     }
-    __builtin_amdgcn_s_waitcnt(kWaitStep);  // B(0), A(0) landed (B(1), A(1), B(2) in flight)
+    if constexpr (STAG) __builtin_amdgcn_s_waitcnt(kWaitPro);  // B(0), A(0) landed (B(1), B(2) in flight)
+    else __builtin_amdgcn_s_waitcnt(kWaitStep);  // B(0), A(0) landed (B(1), A(1), B(2) in flight)
 
     int ks = 0, stage = 0;
     int64_t t = t0;
@@ -439,17 +449,109 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
         }
         ++t;
     };
-    auto step = [&](int64_t g, auto slot_c) __attribute__((always_inline)) {
-        body(g, slot_c);
-        if (++ks == ns) {
-            ks = 0;
-            epilogue();
+
+    // ---- STAG: the staggered schedule (see the template comment) ----
+    // Both halves run ONE instruction stream — the half only selects operands (a branch per half duplicated the
+    // accumulator updates and the allocator spilled ~1000 registers): per barrier interval g a chunk x, an epilogue
+    // site, a chunk y, an epilogue site.  Early half: x = chunk 0 of K-step g, y = chunk 1 of g, epilogue after y when
+    // g ends a tile.  Late half: x = chunk 1 of g − 1, epilogue after x when g − 1 ended a tile, y = chunk 0 of g.
+    // Both issue the query fragments one K-step ahead (A(g + 1) spread over chunk y, into slot SLN) and the tile
+    // piece B(g + 3) at the end of y.
+    auto chunk_rt = [&](int h, int stg, const k64_u32x4 (&a)[MBW], auto vm_c, int sli_dummy, int64_t gb, int stgb,
+                        auto sli_c) __attribute__((always_inline)) {
+        constexpr int VM = decltype(vm_c)::value, SLI = decltype(sli_c)::value;
+        (void)sli_dummy;
+        __builtin_amdgcn_sched_barrier(0);
+        const k64_u32x4 *Bc = smem_k64 + stg * K64_SU + h * K64_BU + g4 * K64_TN + (m16 ^ (g4 << 1));
+        if constexpr ((VM & 1) != 0) issue_a(std::integral_constant<int, SLI>{});
+        k64_b16x8 bf[16];
+#pragma unroll
+        for (int jb = 0; jb < 16; ++jb) bf[jb] = __builtin_bit_cast(k64_b16x8, Bc[16 * jb]);
+#pragma unroll
+        for (int jb = 0; jb < 16; ++jb) {
+#pragma unroll
+            for (int mb = 0; mb < MBW; ++mb) {
+                if constexpr (I8) {
+                    const k64_i32x4 ai = __builtin_bit_cast(k64_i32x4, a[mb]);
+                    const k64_i32x4 bi = __builtin_bit_cast(k64_i32x4, bf[jb]);
+                    acc[mb][jb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(ai, bi, acc[mb][jb], 0, 0, 0);
+                } else {
+                    acc[mb][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(k64_b16x8, a[mb]), bf[jb],
+                                                                          acc[mb][jb], 0, 0, 0);
+                }
+            }
         }
+        if constexpr ((VM & 2) != 0) issue_b(gb, stgb);
+        constexpr int NAv = (VM & 1) != 0 ? 2 * MBW : 0, NBv = (VM & 2) != 0 ? PIECES : 0;
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+        for (int p = 0; p < 16; ++p) {
+            __builtin_amdgcn_sched_group_barrier(0x008, MBW, 0);
+            if (p < 12) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            if constexpr (NAv > 0) {
+                if (p % (16 / NAv) == 1 % (16 / NAv)) __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+            }
+            if constexpr (NBv > 0) {
+                if (p >= 16 - NBv) __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
     };
-    for (int64_t g = 0; g < G; g += 3) {
-        step(g, std::integral_constant<int, 0>{});
-        if (g + 1 < G) step(g + 1, std::integral_constant<int, 1>{});
-        if (g + 2 < G) step(g + 2, std::integral_constant<int, 2>{});
+#ifndef HIPANN_STAG_DBG
+#define HIPANN_STAG_DBG 0
+#endif
+    const bool late = STAG && HIPANN_STAG_DBG != 2 && wave >= K64Geom<MBW>::W / 2;  // wave-uniform
+    auto body_stag = [&](int64_t g, auto slot_c) __attribute__((always_inline)) {
+        constexpr int SL = decltype(slot_c)::value;
+        constexpr int SLP = (SL + 2) % 3, SLN = (SL + 1) % 3;  // slots of K-steps g − 1 and g + 1
+        const bool xn = g < G && ks == ks_xn;
+        if constexpr ((HIPANN_K64_ABLATE & 8) == 0) __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (xn) load_xn(t);
+        __builtin_amdgcn_sched_barrier(0);
+        const int stgb = stage < 2 ? stage + 3 : stage - 2;
+        const int stprev = stage == 0 ? NB - 1 : stage - 1;
+        k64_u32x4 ax[MBW], ay[MBW];
+#pragma unroll
+        for (int mb = 0; mb < MBW; ++mb) {
+            ax[mb] = late ? ar[SLP][1][mb] : ar[SL][0][mb];
+            ay[mb] = late ? ar[SL][0][mb] : ar[SL][1][mb];
+        }
+        if (late ? g >= 1 : g < G)
+            chunk_rt(late ? 1 : 0, late ? stprev : stage, ax, std::integral_constant<int, 0>{}, 0, 0, 0,
+                     std::integral_constant<int, SLN>{});
+#if HIPANN_STAG_DBG != 1
+        if (late && g >= 1 && ks == 0) epilogue();  // g − 1 ended a tile (g = G included: G is whole tiles)
+#endif
+        if (g < G)
+            chunk_rt(late ? 0 : 1, stage, ay, std::integral_constant<int, 3>{}, 0, clampg(g + 3), stgb,
+                     std::integral_constant<int, SLN>{});
+        if (!late && g < G && ks == ns - 1) epilogue();
+        // A(g + 1) and this wave's B(g + 1) landed: only B(g + 3) left in flight (the tile's norms, issued at the top
+        // of the interval, are older and land too)
+        __builtin_amdgcn_s_waitcnt(kWaitLate);
+        ks = ks + 1 < ns ? ks + 1 : 0;
+        stage = stage + 1 < NB ? stage + 1 : 0;
+    };
+    if constexpr (STAG) {
+        for (int64_t g = 0; g <= G; g += 3) {
+            body_stag(g, std::integral_constant<int, 0>{});
+            if (g + 1 <= G) body_stag(g + 1, std::integral_constant<int, 1>{});
+            if (g + 2 <= G) body_stag(g + 2, std::integral_constant<int, 2>{});
+        }
+    } else {
+        auto step = [&](int64_t g, auto slot_c) __attribute__((always_inline)) {
+            body(g, slot_c);
+            if (++ks == ns) {
+                ks = 0;
+                epilogue();
+            }
+        };
+        for (int64_t g = 0; g < G; g += 3) {
+            step(g, std::integral_constant<int, 0>{});
+            if (g + 1 < G) step(g + 1, std::integral_constant<int, 1>{});
+            if (g + 2 < G) step(g + 2, std::integral_constant<int, 2>{});
+        }
     }
     // no LDS-DMA copy may land after the block's LDS is handed to the next block
     __builtin_amdgcn_s_waitcnt(0xF70u);
@@ -1214,10 +1316,17 @@ void launch_flat_bf16_k64(const void *qimg, const float *qn, int64_t nq, const v
         hipLaunchKernelGGL(kern, grid, block, K64_LDS, st, qa, qn, nq, xa, xn, N, nk, nqt, nsplit, tiles_per_split,
                            tile_begin, tile_end, bound, cand_d, cand_i, cand_n, cap, resume ? 1 : 0, qscale, xscale);
     };
+    // HIPANN_K64_STAGGER=0 (A/B): the int8 passes with every wave on the same K-step (the r05 schedule); the staggered
+    // schedule needs ≥ 3 K-steps per tile (the tile's norms are loaded two K-steps before its epilogue)
+    static const bool stag_env = [] { const char *e = std::getenv("HIPANN_K64_STAGGER"); return !e || std::atoi(e); }();
+    const bool stag = stag_env && nk / 2 >= 3;
     if (qscale) {
         if (keys) {
             if (metric == kL2) go(flat_bf16_k64<true, true, true>);
             else go(flat_bf16_k64<false, true, true>);
+        } else if (stag) {
+            if (metric == kL2) go(flat_bf16_k64<true, false, true, 2, true>);
+            else go(flat_bf16_k64<false, false, true, 2, true>);
         } else {
             if (metric == kL2) go(flat_bf16_k64<true, false, true>);
             else go(flat_bf16_k64<false, false, true>);

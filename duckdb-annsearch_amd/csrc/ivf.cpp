@@ -204,6 +204,7 @@ IvfIndex::~IvfIndex() {
         if (s->done) (void)hipEventDestroy(s->done);
         for (hipEvent_t e : s->app_ev)
             if (e) (void)hipEventDestroy(e);
+        if (s->app_sync) (void)hipEventDestroy(s->app_sync);
         if (s->stream) (void)hipStreamDestroy(s->stream);
     }
 }
@@ -664,7 +665,10 @@ static void ivf_add_block(IvfIndex &ix, int64_t n, const float *xb, const int64_
                                 st));
     HIPANN_CHECK(hipMemcpyAsync(const_cast<unsigned *>(hstat), stat, sizeof(unsigned) * 4 * (size_t)nsh,
                                 hipMemcpyDeviceToHost, st));
-    HIPANN_CHECK(hipStreamSynchronize(st));
+    // the block's one host wait, polled (wait_event: no interrupt wake-up on the append's critical path)
+    if (!s0.app_sync) HIPANN_CHECK(hipEventCreateWithFlags(&s0.app_sync, hipEventDisableTiming));
+    HIPANN_CHECK(hipEventRecord(s0.app_sync, st));
+    wait_event(s0.app_sync);
     const double t_assign = prof ? us(t_0) : 0.0;
     std::vector<int64_t> cnt(nlist, 0);
     for (int64_t i = 0; i < n; ++i) {

@@ -984,10 +984,21 @@ ivf_tile_half(const float *__restrict__ codes, const int64_t *__restrict__ list_
         if (row < len) {
             const float *src = codes + (list_off[lo] + row) * (int64_t)d;
             const int d0 = 32 * S + 4 * g, d1 = d0 + 16;
+            if ((d & 3) == 0 && ((uintptr_t)codes & 15) == 0) {  // whole float4s (d0, d1 are multiples of 4)
+                if (d0 < d) {
+                    const float4 a = *reinterpret_cast<const float4 *>(src + d0);
+                    v[0] = a.x * scale; v[1] = a.y * scale; v[2] = a.z * scale; v[3] = a.w * scale;
+                }
+                if (d1 < d) {
+                    const float4 b = *reinterpret_cast<const float4 *>(src + d1);
+                    v[4] = b.x * scale; v[5] = b.y * scale; v[6] = b.z * scale; v[7] = b.w * scale;
+                }
+            } else {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                if (d0 + j < d) v[j] = src[d0 + j] * scale;
-                if (d1 + j < d) v[4 + j] = src[d1 + j] * scale;
+                for (int j = 0; j < 4; ++j) {
+                    if (d0 + j < d) v[j] = src[d0 + j] * scale;
+                    if (d1 + j < d) v[4 + j] = src[d1 + j] * scale;
+                }
             }
         }
         dst[pass * nt + t] = make_uint4(mh_pack(v[0], v[1]), mh_pack(v[2], v[3]), mh_pack(v[4], v[5]), mh_pack(v[6], v[7]));
@@ -1026,21 +1037,60 @@ ivf_append_rows(const float *__restrict__ rows, const float *__restrict__ norms,
                 int *__restrict__ list_len, int nlist, float hscale, unsigned *__restrict__ stat) {
     const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (gid < nlist) list_len[gid] = newlen[gid];
-    const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
+    if (!dst) {
+        // statistics only (every row of the block; nothing written but stat) — the pre-pass whose maxima come back with
+        // the coarse assignment, so the append needs no host wait of its own.  A few blocks stride over the rows and
+        // reduce in the block before one atomic per statistic (one atomic per row on three words serialised: 74 µs
+        // for 2048 rows)
+        __shared__ unsigned red[3][4];
+        const float inv = hscale > 0.f ? 1.f / hscale : 0.f;
+        unsigned mn = 0, ma = 0, mr = 0;
+        for (int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); j < n; j += (int64_t)gridDim.x * 4) {
+            const float *src = rows + j * (int64_t)d;
+            unsigned mabs = 0;
+            float res = 0.f;
+            for (int e = lane; e < d; e += 64) {
+                const float x = src[e];
+                mabs = max(mabs, __float_as_uint(x) & 0x7fffffffu);
+                if (hscale > 0.f) {
+                    const float q = x - mh_val(mh_half_bits(x * hscale)) * inv;
+                    res = fmaf(q, q, res);
+                }
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                mabs = max(mabs, (unsigned)__shfl_xor((int)mabs, o));
+                res += __shfl_xor(res, o);
+            }
+            mn = max(mn, __float_as_uint(norms[j]));
+            ma = max(ma, mabs);
+            mr = max(mr, __float_as_uint(res));
+        }
+        if (lane == 0) {
+            red[0][threadIdx.x >> 6] = mn;
+            red[1][threadIdx.x >> 6] = ma;
+            red[2][threadIdx.x >> 6] = mr;
+        }
+        __syncthreads();
+        if (threadIdx.x < 3 && stat) {
+            const unsigned v = max(max(red[threadIdx.x][0], red[threadIdx.x][1]), max(red[threadIdx.x][2], red[threadIdx.x][3]));
+            if (threadIdx.x < 2 || hscale > 0.f) atomicMax(stat + threadIdx.x, v);
+        }
+        return;
+    }
+    const int64_t j = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (j >= n) return;
-    // dst == nullptr: statistics only (every row of the block; nothing written but stat) — the pre-pass whose maxima
-    // come back with the coarse assignment, so the append needs no host wait of its own
-    const int64_t r = dst ? dst[j] : 0;
+    const int64_t r = dst[j];
     if (r < 0) return;
     const float *src = rows + j * (int64_t)d;
-    float *out = dst ? codes + r * (int64_t)d : nullptr;
+    float *out = codes + r * (int64_t)d;
     const float inv = hscale > 0.f ? 1.f / hscale : 0.f;
     unsigned mabs = 0;
     float res = 0.f;
     for (int e = lane; e < d; e += 64) {
         const float x = src[e];
-        if (out) out[e] = x;
+        out[e] = x;
         mabs = max(mabs, __float_as_uint(x) & 0x7fffffffu);
         if (hscale > 0.f) {
             const float q = x - mh_val(mh_half_bits(x * hscale)) * inv;
@@ -1053,10 +1103,8 @@ ivf_append_rows(const float *__restrict__ rows, const float *__restrict__ norms,
         res += __shfl_xor(res, o);
     }
     if (lane == 0) {
-        if (dst) {
-            ids[r] = ids_in[j];
-            if (xnorm) xnorm[r] = norms[j];
-        }
+        ids[r] = ids_in[j];
+        if (xnorm) xnorm[r] = norms[j];
         if (!stat) return;
         atomicMax(stat + 0, __float_as_uint(norms[j]));
         atomicMax(stat + 1, mabs);
@@ -1404,7 +1452,8 @@ void launch_ivf_half_residual(const float *codes, int64_t n, int d, float scale,
 void launch_ivf_append_rows(const float *rows, const float *norms, const int64_t *dst, const int64_t *ids_in, int64_t n,
                             int d, float *codes, int64_t *ids, float *xnorm, const int *newlen, int *list_len, int nlist,
                             float hscale, unsigned *stat, hipStream_t st) {
-    const int64_t blocks = std::max(ceil_div(n, (int64_t)4), ceil_div((int64_t)nlist, (int64_t)256));
+    int64_t blocks = std::max(ceil_div(n, (int64_t)4), ceil_div((int64_t)nlist, (int64_t)256));
+    if (!dst) blocks = std::min<int64_t>(blocks, 64);  // statistics only: a grid-stride loop, one atomic per block
     HIPANN_REQUIRE(blocks < (int64_t)0x7fffffff, "append block too large");
     if (stat) HIPANN_CHECK(hipMemsetAsync(stat, 0, sizeof(unsigned) * 4, st));
     hipLaunchKernelGGL(ivf_append_rows, dim3((unsigned)blocks), dim3(256), 0, st, rows, norms, dst, ids_in, n, d, codes,

@@ -416,6 +416,7 @@ struct IvfShard {
     // up (one copy), the maxima on their way down
     HostBuf app_hassign, app_hup[2];
     hipEvent_t app_ev[2] = {nullptr, nullptr};  // app_hup[b]'s upload has been consumed (reused two blocks later)
+    hipEvent_t app_sync = nullptr;              // the assignment readback of an append block (polled)
     int app_buf = 0;
     int max_nch = 1;  // largest list's row-chunk count
     StreamFence fence;  // cross-stream ordering of this shard's calls (its coarse quantizer's scratch included)
