@@ -160,7 +160,8 @@ __global__ void __launch_bounds__(256) dist_ids_sq8(const float *__restrict__ qu
                                                     const float2 *__restrict__ ab_g, const unsigned *__restrict__ ids,
                                                     const unsigned *__restrict__ qmap, int total_n, int d,
                                                     int64_t n, float *__restrict__ out, unsigned *__restrict__ vbits,
-                                                    int64_t vwords) {
+                                                    int64_t vwords, unsigned *__restrict__ done_ctr,
+                                                    unsigned *__restrict__ done_tok, unsigned token) {
     extern __shared__ __attribute__((aligned(16))) float2 ab[];
     for (int j = threadIdx.x; j < d; j += 256) ab[j] = ab_g[j];
     __syncthreads();
@@ -209,6 +210,25 @@ __global__ void __launch_bounds__(256) dist_ids_sq8(const float *__restrict__ qu
 #pragma unroll
         for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o);
         if (valid && ql == 0) out[c] = IP ? -s : s;
+    }
+    // done_tok (the host BFS): the launch posts its own completion — every wave's distances (pinned host memory, device
+    // mapping) made visible system-wide, the block counted, and the last block to finish writes `token` into the
+    // host word the BFS polls — instead of an event recorded behind every step's launch (MI355X_MICROARCH.md,
+    // inter-workgroup visibility: release, then the count; the compiler-hazard waits made explicit)
+    if (done_tok) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __threadfence_system();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned old = __hip_atomic_fetch_add(done_ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            if (old == gridDim.x - 1) {
+                __hip_atomic_store(done_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
+                __threadfence_system();
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(done_tok, token, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
     }
 }
 
@@ -313,14 +333,23 @@ struct DiskDB {
     int R = 0;
     DevBuf adj_dev, dupw, visited, flags, bstats, eps_dev;
     DevBuf vbits;  // host BFS: the queries' visited bits on the device (one bit per row and query)
+    DevBuf bfs_ctr;   // host BFS: per group, the id-gather launch's finished-block count (zero between launches)
+    HostBuf bfs_tok;  // host BFS: per group, the token word the launch posts when it is done (polled)
+    unsigned bfs_seq = 0;
     std::vector<uint32_t> adj_host;
     ~DiskDB() {
         if (stream) { DeviceGuard g(device); (void)hipStreamDestroy(stream); }
     }
 };
 
+// Whether launch_ids posts its own completion token for this DB (the SQ8 vector kernel).
+bool ids_post_token(const DiskDB &db, const float *q) {
+    return db.fmt != DISKANN_HIP_FMT_F32 && db.dim % 16 == 0 && db.dim <= 2048 && (uintptr_t)q % 16 == 0;
+}
+
 void launch_ids(DiskDB &db, const float *q, const unsigned *ids, const unsigned *m, int total_n, int metric,
-                float *out, hipStream_t st, unsigned *vbits = nullptr, int64_t vwords = 0) {
+                float *out, hipStream_t st, unsigned *vbits = nullptr, int64_t vwords = 0, unsigned *done_ctr = nullptr,
+                unsigned *done_tok = nullptr, unsigned token = 0) {
     if (total_n <= 0) return;
     const int d = db.dim;
     if (db.fmt == DISKANN_HIP_FMT_F32) {
@@ -341,8 +370,8 @@ void launch_ids(DiskDB &db, const float *q, const unsigned *ids, const unsigned 
             // ≤ 8 blocks per CU, each looping over groups of 16 candidates (dist_ids_sq8)
             dim3 grid((unsigned)std::min<int64_t>(ceil_div(total_n, 16), 2048)), block(256);
             const size_t smem = (size_t)d * sizeof(float2);
-            if (metric == kIP) hipLaunchKernelGGL(dist_ids_sq8<true>, grid, block, smem, st, q, x, ab, ids, m, total_n, d, db.n, out, vbits, vwords);
-            else hipLaunchKernelGGL(dist_ids_sq8<false>, grid, block, smem, st, q, x, ab, ids, m, total_n, d, db.n, out, vbits, vwords);
+            if (metric == kIP) hipLaunchKernelGGL(dist_ids_sq8<true>, grid, block, smem, st, q, x, ab, ids, m, total_n, d, db.n, out, vbits, vwords, done_ctr, done_tok, token);
+            else hipLaunchKernelGGL(dist_ids_sq8<false>, grid, block, smem, st, q, x, ab, ids, m, total_n, d, db.n, out, vbits, vwords, done_ctr, done_tok, token);
         } else {
             dim3 grid((unsigned)ceil_div(total_n, 4)), block(256);
             if (metric == kIP) hipLaunchKernelGGL(dist_ids_sq8_scalar<true>, grid, block, 0, st, q, x, ab, ids, m, total_n, d, db.n, out, vbits, vwords);
@@ -584,8 +613,23 @@ void host_bfs(DiskDB *db, const uint32_t *adj, int R, const uint32_t *eps, int n
         bool seed = true, done = false, launched = false;
         int64_t steps = 0;
         hipEvent_t ev = nullptr;
+        unsigned token = 0;  // the token its last launch posts (tokened launches)
     };
     const int G = bfs_groups(nq);
+    // The SQ8 gather posts its own completion (a token word per group in pinned memory, written by the launch's last
+    // block): no event recorded behind every step's launch, and the wait polls one host word.  HIPANN_BFS_TOKEN=0
+    // (A/B), and other formats: events.
+    static const bool tok_env = [] { const char *e = std::getenv("HIPANN_BFS_TOKEN"); return !e || std::atoi(e); }();
+    const bool tok = tok_env && ids_post_token(*db, db->q.get<float>());
+    if (tok) {
+        if (!db->bfs_ctr.p || db->bfs_ctr.bytes < sizeof(unsigned) * 8) {
+            db->bfs_ctr.ensure(sizeof(unsigned) * 8, db->device);
+            HIPANN_CHECK(hipMemsetAsync(db->bfs_ctr.p, 0, db->bfs_ctr.bytes, st));
+        }
+        if (db->bfs_tok.ensure(sizeof(unsigned) * 8)) std::memset(db->bfs_tok.p, 0, sizeof(unsigned) * 8);
+    }
+    unsigned *tok_dev = tok ? static_cast<unsigned *>(host_device_ptr(db->bfs_tok.p)) : nullptr;
+    const volatile unsigned *tok_host = tok ? db->bfs_tok.get<unsigned>() : nullptr;
     std::vector<Group> grp((size_t)G);
     for (int g = 0; g < G; ++g) {
         grp[g].q0 = (int)((int64_t)nq * g / G);
@@ -613,10 +657,13 @@ void host_bfs(DiskDB *db, const uint32_t *adj, int R, const uint32_t *eps, int n
             // the distances go straight into the pinned host buffer through its device mapping (posted writes: no
             // device-to-host copy and its round trip per step)
             ScopedTiming tm(db->timer, st);
+            const int gi = (int)(&g - grp.data());
+            if (tok) g.token = ++db->bfs_seq == 0 ? ++db->bfs_seq : db->bfs_seq;  // never 0 (the words start at 0)
             launch_ids(*db, db->q.get<float>(), (zc_ids ? hid_dev : db->ids.get<unsigned>()) + o,
-                       db->m.get<unsigned>() + o, (int)span, metric, hout_dev + o, st, vbits, vwords);
+                       db->m.get<unsigned>() + o, (int)span, metric, hout_dev + o, st, vbits, vwords,
+                       tok ? db->bfs_ctr.get<unsigned>() + gi : nullptr, tok ? tok_dev + gi : nullptr, g.token);
         }
-        HIPANN_CHECK(hipEventRecord(g.ev, st));
+        if (!tok) HIPANN_CHECK(hipEventRecord(g.ev, st));
         ncalls++;
         if (!gv) nevals += tot;  // (gv: the first visits, counted as the phases read them)
     };
@@ -763,7 +810,10 @@ void host_bfs(DiskDB *db, const uint32_t *adj, int R, const uint32_t *eps, int n
         for (auto &g : grp) {
             if (g.done) continue;
             auto t0 = clk::now();
-            if (g.launched) wait_event(g.ev);
+            if (g.launched) {
+                if (tok) wait_posted(tok_host + (&g - grp.data()), g.token, st);
+                else wait_event(g.ev);
+            }
             auto t1 = clk::now();
             const int64_t head = phase(g);
             auto t2 = clk::now();

@@ -65,11 +65,11 @@ template <int MBW> struct K64Geom {
 // 16-lane group).  Passing rows (rare) are appended to the query's buffer with key = ‖q‖² − s
 // (L2, clamped at 0) or −s/2 = −q·x (IP); cntv lane j holds the count of the wave's query j (it keeps
 // counting past cap: flat_cand_select flags an overflowed query for the exact fallback).
-template <bool L2M, int MB, int I, int JB0>
-__device__ __forceinline__ void k64_epilogue_row(const k64_f32x4 (&sm)[8], float mxi, const float (&cthm)[4], float qnl,
+template <bool L2M, int MB, int I, int NJ>
+__device__ __forceinline__ void k64_epilogue_row(const k64_f32x4 (&sm)[NJ], float mxi, const float (&cthm)[4], float qnl,
                                                  int &cntv, int64_t x0, float *__restrict__ cand_d,
                                                  int *__restrict__ cand_i, int64_t cbase, int64_t cq, int cap,
-                                                 int lane) {
+                                                 int lane, int JB0) {
     // sm[j] = s of row block JB0 + j (one half of the tile's 16; the halves keep the epilogue's live registers to 32
     // values).  mxi = max over the lane's 8 rows of sm[·][I] (the caller's reduction): one compare for the 8 (NaN
     // never passes: fmaxf drops NaN operands, an all-NaN max compares false)
@@ -82,7 +82,7 @@ __device__ __forceinline__ void k64_epilogue_row(const k64_f32x4 (&sm)[8], float
     // the lane's passing columns (bit j: row block JB0 + j)
     unsigned pm = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) pm |= sm[j][I] >= cthm[I] ? 1u << j : 0u;
+    for (int j = 0; j < NJ; ++j) pm |= sm[j][I] >= cthm[I] ? 1u << j : 0u;
 #pragma unroll 1
     for (int fq = 0; fq < 4; ++fq) {
         unsigned grp = (unsigned)(m >> (16 * fq)) & 0xffffu;  // lanes of query fq holding a passing row
@@ -103,7 +103,7 @@ __device__ __forceinline__ void k64_epilogue_row(const k64_f32x4 (&sm)[8], float
                 const int jb = JB0 + jl;
                 float sv = sm[0][I];
 #pragma unroll
-                for (int j = 1; j < 8; ++j) sv = jl == j ? sm[j][I] : sv;
+                for (int j = 1; j < NJ; ++j) sv = jl == j ? sm[j][I] : sv;
                 sv = readlane_f(sv, src);
                 float key;
                 if (L2M) {
@@ -134,7 +134,8 @@ __device__ __forceinline__ void k64_epilogue_row(const k64_f32x4 (&sm)[8], float
 // per byte moved.  The int32 sums are exact (|acc| <= d·127² < 2^24 for d <= 1040) and live in the float
 // accumulators' registers bit for bit until the tile's epilogue turns them into q·x = acc·s_q·s_x with the
 // per-query / per-row scales (qscale / xscale); everything after that is the bf16 path's.
-// STAG (the int8 bounded passes, d ≥ 384): waves W/2..W−1 run half a K-step behind waves 0..W/2−1 — in K-step g's
+// STAG (A/B only, HIPANN_K64_STAGGER=1; measured slower, see launch_flat_bf16_k64) (the int8 bounded passes,
+// d ≥ 384): waves W/2..W−1 run half a K-step behind waves 0..W/2−1 — in K-step g's
 // barrier interval a late wave computes chunk 1 of g − 1, then (when g − 1 ended a tile) its epilogue, then chunk 0 of
 // g.  Waves w and w + W/2 share a SIMD, so one wave's epilogue (≈ 650 VALU instructions per tile) and LDS read burst
 // run beside its partner's MFMAs instead of both waves converting at the same barrier-aligned moment
@@ -269,20 +270,17 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
     static_assert(kVmXn < 64, "vmcnt field");
     constexpr unsigned kWaitStep = 0xF70u | (kVm & 15) | ((kVm >> 4) << 14);
     constexpr unsigned kWaitStepXn = 0xF70u | (kVmXn & 15) | ((kVmXn >> 4) << 14);
-    // STAG: one-K-step fragment lead for both halves; at the end of interval g only B(g + 3) may stay in flight
-    constexpr unsigned kWaitLate = 0xF70u | (NB_OPS & 15) | ((NB_OPS >> 4) << 14);
-    constexpr unsigned kWaitPro = 0xF70u | ((2 * NB_OPS) & 15) | (((2 * NB_OPS) >> 4) << 14);
+
     auto clampg = [&](int64_t g) { return g < G ? g : G - 1; };  // past the end: the last K-step again, never read
     if (G > 0) {
-        // the steady state's order: B(0), A(0), B(1), A(1), B(2) (STAG: a one-K-step fragment lead, no A(1) here)
+        // the steady state's order: B(0), A(0), B(1), A(1), B(2)
         issue_b(0, 0);
         issue_a(std::integral_constant<int, 0>{});
         issue_b(clampg(1), 1);
-        if constexpr (!STAG) issue_a(std::integral_constant<int, 1>{});
+        issue_a(std::integral_constant<int, 1>{});
         issue_b(clampg(2), 2);
     }
-    if constexpr (STAG) __builtin_amdgcn_s_waitcnt(kWaitPro);  // B(0), A(0) landed (B(1), B(2) in flight)
-    else __builtin_amdgcn_s_waitcnt(kWaitStep);  // B(0), A(0) landed (B(1), A(1), B(2) in flight)
+    __builtin_amdgcn_s_waitcnt(kWaitStep);  // B(0), A(0) landed (B(1), A(1), B(2) in flight)
 
     int ks = 0, stage = 0;
     int64_t t = t0;
@@ -350,6 +348,12 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
         else __builtin_amdgcn_s_waitcnt(kWaitStep);
         stage = stage + 1 < NB ? stage + 1 : 0;
     };
+    // row blocks converted per epilogue part: 8 (32 values + 16 row terms beside the accumulators); STAG: 4, which frees
+    // the 16 registers the staggered halves' longer fragment lifetimes need
+#ifndef HIPANN_K64_EJ
+#define HIPANN_K64_EJ 0
+#endif
+    constexpr int EJ = HIPANN_K64_EJ ? HIPANN_K64_EJ : (STAG ? 4 : 8);
     // the tile's epilogue (after its last K-step)
     auto epilogue = [&]() __attribute__((always_inline)) {
         const int64_t x0 = t * K64_TN;
@@ -358,11 +362,11 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
         // halves), each 16-query row block's accumulators converted, filtered and reset before the next: 32 values
         // and 16 row terms live besides the accumulators.
 #pragma unroll
-        for (int hf = 0; hf < 2; ++hf) {
-            float xvj[8], sxj[8];
+        for (int hf = 0; hf < 16 / EJ; ++hf) {
+            float xvj[EJ], sxj[EJ];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int jb = 8 * hf + j;
+            for (int j = 0; j < EJ; ++j) {
+                const int jb = EJ * hf + j;
                 const float xs = __shfl(xr[jb >> 2], 16 * (jb & 3) + m16);
                 xvj[j] = x0 + 16 * jb + m16 < N ? xs : __builtin_inff();
                 sxj[j] = I8 ? __shfl(xsc[jb >> 2], 16 * (jb & 3) + m16) : 1.f;
@@ -373,17 +377,17 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
                     // accumulators consumed by one xor each and reset, no conversion or filter)
                     k64_f32x4 x = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        x = __builtin_elementwise_max(x, __builtin_convertvector(acc[MB][8 * hf + j], k64_f32x4));
-                        acc[MB][8 * hf + j] = (AccT){0, 0, 0, 0};
+                    for (int j = 0; j < EJ; ++j) {
+                        x = __builtin_elementwise_max(x, __builtin_convertvector(acc[MB][EJ * hf + j], k64_f32x4));
+                        acc[MB][EJ * hf + j] = (AccT){0, 0, 0, 0};
                     }
                     cntv += x[0] + x[1] + x[2] + x[3] == 1234.5f ? 1 : 0;
                     return;
                 }
-                k64_f32x4 sm[8];
+                k64_f32x4 sm[EJ];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const int jb = 8 * hf + j;
+                for (int j = 0; j < EJ; ++j) {
+                    const int jb = EJ * hf + j;
                     if constexpr (I8) {
                         // whole-vector reinterpret + convert: per-element extracts of the bit-cast i32 MFMA result
                         // were miscompiled (only element 0 of each accumulator was read; the others came from stale
@@ -411,8 +415,8 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
                     for (int i = 0; i < 4; ++i) {
                         const int64_t q = q0w + 16 * MB + i;
 #pragma unroll
-                        for (int j = 0; j < 8; ++j) {
-                            const int64_t x = x0 + 16 * (8 * hf + j) + m16;
+                        for (int j = 0; j < EJ; ++j) {
+                            const int64_t x = x0 + 16 * (EJ * hf + j) + m16;
                             float key;
                             if (L2M) {
                                 key = cth[MB][i] - sm[j][i];
@@ -429,18 +433,11 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
                     // the lane's largest s per accumulator row (the filter's one compare per row); NaN-dropping max
                     k64_f32x4 mx = sm[0];
 #pragma unroll
-                    for (int j = 1; j < 8; ++j) mx = __builtin_elementwise_max(mx, sm[j]);
-                    if (hf == 0) {
-                        k64_epilogue_row<L2M, MB, 0, 0>(sm, mx[0], cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
-                        k64_epilogue_row<L2M, MB, 1, 0>(sm, mx[1], cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
-                        k64_epilogue_row<L2M, MB, 2, 0>(sm, mx[2], cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
-                        k64_epilogue_row<L2M, MB, 3, 0>(sm, mx[3], cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
-                    } else {
-                        k64_epilogue_row<L2M, MB, 0, 8>(sm, mx[0], cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
-                        k64_epilogue_row<L2M, MB, 1, 8>(sm, mx[1], cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
-                        k64_epilogue_row<L2M, MB, 2, 8>(sm, mx[2], cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
-                        k64_epilogue_row<L2M, MB, 3, 8>(sm, mx[3], cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane);
-                    }
+                    for (int j = 1; j < EJ; ++j) mx = __builtin_elementwise_max(mx, sm[j]);
+                    k64_epilogue_row<L2M, MB, 0, EJ>(sm, mx[0], cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane, EJ * hf);
+                    k64_epilogue_row<L2M, MB, 1, EJ>(sm, mx[1], cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane, EJ * hf);
+                    k64_epilogue_row<L2M, MB, 2, EJ>(sm, mx[2], cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane, EJ * hf);
+                    k64_epilogue_row<L2M, MB, 3, EJ>(sm, mx[3], cth[MB], qnl, cntv, x0, cand_d, cand_i, cbase, cq, cap, lane, EJ * hf);
                 }
             };
             [&]<int... M>(std::integer_sequence<int, M...>) {
@@ -455,8 +452,8 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
     // accumulator updates and the allocator spilled ~1000 registers): per barrier interval g a chunk x, an epilogue
     // site, a chunk y, an epilogue site.  Early half: x = chunk 0 of K-step g, y = chunk 1 of g, epilogue after y when
     // g ends a tile.  Late half: x = chunk 1 of g − 1, epilogue after x when g − 1 ended a tile, y = chunk 0 of g.
-    // Both issue the query fragments one K-step ahead (A(g + 1) spread over chunk y, into slot SLN) and the tile
-    // piece B(g + 3) at the end of y.
+    // Both issue the query fragments two K-steps ahead (A(g + 2) spread over chunk y, into slot SLP — read by the late
+    // half's chunk x before) and the tile piece B(g + 3) at the end of y: the waits are the unstaggered schedule's.
     auto chunk_rt = [&](int h, int stg, const k64_u32x4 (&a)[MBW], auto vm_c, int sli_dummy, int64_t gb, int stgb,
                         auto sli_c) __attribute__((always_inline)) {
         constexpr int VM = decltype(vm_c)::value, SLI = decltype(sli_c)::value;
@@ -521,19 +518,30 @@ flat_bf16_k64(const k64_u32x4 *__restrict__ Qt, const float *__restrict__ qnorm,
             chunk_rt(late ? 1 : 0, late ? stprev : stage, ax, std::integral_constant<int, 0>{}, 0, 0, 0,
                      std::integral_constant<int, SLN>{});
 #if HIPANN_STAG_DBG != 1
-        if (late && g >= 1 && ks == 0) epilogue();  // g − 1 ended a tile (g = G included: G is whole tiles)
+        if (late && g >= 1 && ks == 0) {  // g − 1 ended a tile (g = G included: G is whole tiles)
+            // the epilogue's VALU at a lower priority than the partner's MFMA issue (MI355X_MICROARCH.md, two waves per
+            // SIMD, item 2: arbitration by priority, then age)
+            __builtin_amdgcn_s_setprio(0);
+            epilogue();
+            __builtin_amdgcn_s_setprio(2);
+        }
 #endif
         if (g < G)
             chunk_rt(late ? 0 : 1, stage, ay, std::integral_constant<int, 3>{}, 0, clampg(g + 3), stgb,
-                     std::integral_constant<int, SLN>{});
-        if (!late && g < G && ks == ns - 1) epilogue();
-        // A(g + 1) and this wave's B(g + 1) landed: only B(g + 3) left in flight (the tile's norms, issued at the top
-        // of the interval, are older and land too)
-        __builtin_amdgcn_s_waitcnt(kWaitLate);
+                     std::integral_constant<int, SLP>{});
+        if (!late && g < G && ks == ns - 1) {
+            __builtin_amdgcn_s_setprio(0);
+            epilogue();
+            __builtin_amdgcn_s_setprio(2);
+        }
+        // A(g + 1), B(g + 1) landed; B(g + 2), A(g + 2), B(g + 3) (and the norms issued at the top) may stay in flight
+        if (xn) __builtin_amdgcn_s_waitcnt(kWaitStepXn);
+        else __builtin_amdgcn_s_waitcnt(kWaitStep);
         ks = ks + 1 < ns ? ks + 1 : 0;
         stage = stage + 1 < NB ? stage + 1 : 0;
     };
     if constexpr (STAG) {
+        __builtin_amdgcn_s_setprio(2);
         for (int64_t g = 0; g <= G; g += 3) {
             body_stag(g, std::integral_constant<int, 0>{});
             if (g + 1 <= G) body_stag(g + 1, std::integral_constant<int, 1>{});
@@ -1316,9 +1324,11 @@ void launch_flat_bf16_k64(const void *qimg, const float *qn, int64_t nq, const v
         hipLaunchKernelGGL(kern, grid, block, K64_LDS, st, qa, qn, nq, xa, xn, N, nk, nqt, nsplit, tiles_per_split,
                            tile_begin, tile_end, bound, cand_d, cand_i, cand_n, cap, resume ? 1 : 0, qscale, xscale);
     };
-    // HIPANN_K64_STAGGER=0 (A/B): the int8 passes with every wave on the same K-step (the r05 schedule); the staggered
-    // schedule needs ≥ 3 K-steps per tile (the tile's norms are loaded two K-steps before its epilogue)
-    static const bool stag_env = [] { const char *e = std::getenv("HIPANN_K64_STAGGER"); return !e || std::atoi(e); }();
+    // HIPANN_K64_STAGGER=1 (A/B, measured and rejected in r06): the staggered schedule (STAG above).  Same-box A/B,
+    // alternating: 10M x 768 kernel 7.86-7.92 → 9.08-9.10 ms, C2 1.00 → 1.23, C5 9.69 → 11.12 (with the epilogue at
+    // s_setprio 0 under the partner's MFMAs: no better) — the default keeps every wave on the same K-step.  It needs
+    // ≥ 3 K-steps per tile (the tile's norms are loaded two K-steps before its epilogue).
+    static const bool stag_env = [] { const char *e = std::getenv("HIPANN_K64_STAGGER"); return e && std::atoi(e); }();
     const bool stag = stag_env && nk / 2 >= 3;
     if (qscale) {
         if (keys) {
