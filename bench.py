@@ -1487,7 +1487,7 @@ def run_suite(args, torch, dist, hipann, dev):
 
     guarded("C1_flat_10k_128_cpu_path", lambda: c1_config(torch, hipann, dev))
     guarded("C2_flat_l2_1m_768", lambda: flat(1_000_000, oracle_queries=1024))
-    guarded("flat_l2_10m_768", lambda: flat(10_000_000, oracle_queries=256, latency=True, steps=5, request_k=True))
+    guarded("flat_l2_10m_768", lambda: flat(10_000_000, oracle_queries=1024, latency=True, steps=5, request_k=True))
     if "request_k30" in cfg["flat_l2_10m_768"]:
         cfg["flat_l2_10m_768_request_k30"] = cfg["flat_l2_10m_768"].pop("request_k30")
     guarded("C4_diskann_1m_1536_sq8", lambda: diskann_config(args, torch, dist, hipann, 0, 1, dev, 1_000_000, 1536,
@@ -1517,7 +1517,7 @@ def c5_config(args, torch, dist, hipann, rank, world, dev):
     steps = max(3, min(args.steps, 10))
     out, index, xb = flat_config(args, torch, dist, hipann, rank, world, dev, n, 768, 1024, args.k, 1, steps, 2,
                                  alt_forms=world == 1 and not args.no_alt_forms, host_rate=False,
-                                 oracle_queries=64 if world == 1 and not args.no_cpu_baseline else 0)
+                                 oracle_queries=256 if world == 1 and not args.no_cpu_baseline else 0)
     index.close()
     del index, xb
     torch.cuda.empty_cache()

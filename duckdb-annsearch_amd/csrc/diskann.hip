@@ -616,17 +616,21 @@ void host_bfs(DiskDB *db, const uint32_t *adj, int R, const uint32_t *eps, int n
         unsigned token = 0;  // the token its last launch posts (tokened launches)
     };
     const int G = bfs_groups(nq);
-    // The SQ8 gather posts its own completion (a token word per group in pinned memory, written by the launch's last
-    // block): no event recorded behind every step's launch, and the wait polls one host word.  HIPANN_BFS_TOKEN=0
-    // (A/B), and other formats: events.
-    static const bool tok_env = [] { const char *e = std::getenv("HIPANN_BFS_TOKEN"); return !e || std::atoi(e); }();
+    // HIPANN_BFS_TOKEN=1 (A/B, measured and rejected in r06): the SQ8 gather posts its own completion (a token word per
+    // group in coherent pinned memory, written by the launch's last block) instead of an event recorded behind every
+    // step's launch.  Every block must release its distance writes at system scope before it is counted — an L2
+    // write-back per block, 2048 per launch — and the C4 host path fell from 71K to 15K QPS (same box, alternating).
+    static const bool tok_env = [] { const char *e = std::getenv("HIPANN_BFS_TOKEN"); return e && std::atoi(e); }();
     const bool tok = tok_env && ids_post_token(*db, db->q.get<float>());
     if (tok) {
         if (!db->bfs_ctr.p || db->bfs_ctr.bytes < sizeof(unsigned) * 8) {
             db->bfs_ctr.ensure(sizeof(unsigned) * 8, db->device);
             HIPANN_CHECK(hipMemsetAsync(db->bfs_ctr.p, 0, db->bfs_ctr.bytes, st));
         }
-        if (db->bfs_tok.ensure(sizeof(unsigned) * 8)) std::memset(db->bfs_tok.p, 0, sizeof(unsigned) * 8);
+        // coherent pinned memory: the launch's system-scope token store is visible to the polling host at once (the
+        // default non-coherent allocation held it back until the stream's end-of-kernel release: 5x slower batches)
+        if (db->bfs_tok.ensure(sizeof(unsigned) * 8, hipHostMallocCoherent))
+            std::memset(db->bfs_tok.p, 0, sizeof(unsigned) * 8);
     }
     unsigned *tok_dev = tok ? static_cast<unsigned *>(host_device_ptr(db->bfs_tok.p)) : nullptr;
     const volatile unsigned *tok_host = tok ? db->bfs_tok.get<unsigned>() : nullptr;
