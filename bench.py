@@ -261,6 +261,8 @@ def parse():
                    help="N=1: add the other BASELINE configurations as sub-objects (default for --workload ivf)")
     p.add_argument("--no-suite", dest="suite", action="store_false")
     p.add_argument("--no-c5", action="store_true", help="skip the C5 sub-line (Flat IP, 12.5M rows per GPU)")
+    p.add_argument("--only", default=None, help="with the suite: run only these comma-separated configurations "
+                   "(profiling runs; e.g. C3_ivf_survey_mixture)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU sample duration (main line)")
     a = p.parse_args()
     if a.n is None:
@@ -740,14 +742,17 @@ def build_ivf(args, torch, hipann, rank, world, dev, n, d, nlist, nprobe, metric
 
 
 def ivf_scan_stats(index, probes, d, nlist, row_bytes=None):
-    from ivf_build import scan_bytes, scan_group_rows, scan_pairs
+    from ivf_build import half_scan_groups, scan_bytes, scan_group_rows, scan_pairs
 
     cnt = np.bincount(probes[probes >= 0].ravel(), minlength=nlist)
+    # the form's query groups: fp16 form (6) narrow / wide (HIPANN_IVF_WIDE=0 disables the wide items), else 32
+    g, w = half_scan_groups(d, os.environ.get("HIPANN_IVF_WIDE", "1") != "0") if index.form == 6 else (32, 0)
     return {"scan_bytes_per_batch_local": scan_bytes(index, probes, d, row_bytes),
             "fp32_rows_bytes_per_batch_local": scan_bytes(index, probes, d),
             "distinct_lists_probed": int(np.unique(probes[probes >= 0]).size),
             "scanned_pairs_per_batch_local": scan_pairs(index, probes),
-            "group_rows_per_batch_local": scan_group_rows(index, probes),
+            "group_rows_per_batch_local": scan_group_rows(index, probes, g, w),
+            "query_groups": [g, w],
             "probes_per_list_p50_p90_max": [int(np.percentile(cnt, 50)), int(np.percentile(cnt, 90)), int(cnt.max())]}
 
 
@@ -1468,6 +1473,8 @@ def run_suite(args, torch, dist, hipann, dev):
     cfg = {}
 
     def guarded(name, fn):
+        if args.only and name not in args.only.split(","):
+            return
         t0 = time.perf_counter()
         try:
             cfg[name] = fn()
@@ -1488,7 +1495,7 @@ def run_suite(args, torch, dist, hipann, dev):
     guarded("C1_flat_10k_128_cpu_path", lambda: c1_config(torch, hipann, dev))
     guarded("C2_flat_l2_1m_768", lambda: flat(1_000_000, oracle_queries=1024))
     guarded("flat_l2_10m_768", lambda: flat(10_000_000, oracle_queries=1024, latency=True, steps=5, request_k=True))
-    if "request_k30" in cfg["flat_l2_10m_768"]:
+    if "request_k30" in cfg.get("flat_l2_10m_768", {}):
         cfg["flat_l2_10m_768_request_k30"] = cfg["flat_l2_10m_768"].pop("request_k30")
     guarded("C4_diskann_1m_1536_sq8", lambda: diskann_config(args, torch, dist, hipann, 0, 1, dev, 1_000_000, 1536,
                                                              1024, args.k, 128, 64, 10, 2))

@@ -96,6 +96,17 @@ constexpr float kSplit2Eps = 0x1p-12f;
 __host__ __device__ inline bool ivf_form_split(int f) { return f == kFormSplit3 || f == kFormSplit2; }
 __host__ __device__ inline int ivf_form_terms(int f) { return f == kFormSplit3 ? 3 : 2; }
 
+// Query groups of an IVF list probed by c queries.  `group` packs the scan's group size (low 16 bits) and an
+// optional wide size (high 16 bits, 0 = none): a list probed by more queries than the narrow size is scanned in
+// groups of up to the wide size instead (the fp16 scan's one-term items, ivf_mfma.hip), so its rows are streamed
+// ceil(c / wide) times rather than ceil(c / narrow).
+__host__ __device__ inline int ivf_group_narrow(int group) { return group & 0xffff; }
+__host__ __device__ inline bool ivf_list_wide(int c, int group) { return (group >> 16) > 0 && c > (group & 0xffff); }
+__host__ __device__ inline int ivf_ngroups(int c, int group) {
+    const int g = ivf_list_wide(c, group) ? group >> 16 : group & 0xffff;
+    return (c + g - 1) / g;
+}
+
 // XCD-aware block remap (cdna_hip_programming.md §5.5 T1, bijective form): blocks b and b+8 are
 // dealt to the same XCD; map so that each XCD receives a contiguous run of logical blocks.
 __device__ __forceinline__ int xcd_remap(int bid, int nblocks) {

@@ -337,7 +337,7 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     if (half) {
         sh.hsplit.ensure((size_t)ivf_half_qsplit_bytes(nq, d), sh.device);
         sh.hits.ensure(sizeof(float) * (size_t)nq, sh.device);
-        sh.hres.ensure(sizeof(float) * (size_t)nq, sh.device);
+        sh.hres.ensure(sizeof(float) * 2 * (size_t)nq, sh.device);  // two- and one-term split residuals
         float *qn_out = nullptr;
         if (metric == kL2) {  // the quantizer's BLAS-form paths (nq >= 20) and the scan's L2 keys read ‖q‖²
             qsh0.qn.ensure(sizeof(float) * (size_t)nq, sh.device);

@@ -61,7 +61,7 @@ __global__ void __launch_bounds__(1024) ivf_plan(const int *__restrict__ cnt, co
     for (int base = 0; base < nlist; base += 1024) {
         const int l = base + threadIdx.x;
         const int c = l < nlist ? cnt[l] : 0;
-        const int items = l < nlist ? ((c + group - 1) / group) * ivf_nch(list_len[l]) : 0;
+        const int items = l < nlist ? ivf_ngroups(c, group) * ivf_nch(list_len[l]) : 0;
         sb[threadIdx.x] = c;
         si[threadIdx.x] = items;
         __syncthreads();
@@ -217,7 +217,7 @@ __global__ void __launch_bounds__(1024) ivf_plan_q(int *__restrict__ ccnt, const
         int c = 0;
         if (l < nlist)
             for (int cp = 0; cp < kPlanCopies; ++cp) c += ccnt[(int64_t)cp * nlist + l];
-        const int items = l < nlist ? ((c + group - 1) / group) * ivf_nch(list_len[l]) : 0;
+        const int items = l < nlist ? ivf_ngroups(c, group) * ivf_nch(list_len[l]) : 0;
         sb[tid] = c;
         si[tid] = items;
         __syncthreads();
@@ -334,7 +334,7 @@ __global__ void __launch_bounds__(256) ivf_planfill_q(const int64_t *__restrict_
             int c = 0;
             for (int cp = 0; cp < kPlanCopies; ++cp) c += ccnt[(int64_t)cp * nlist + l];
             sum += c;
-            if (blockIdx.x == 0) isum += ((c + group - 1) / group) * ivf_nch(list_len[l]);
+            if (blockIdx.x == 0) isum += ivf_ngroups(c, group) * ivf_nch(list_len[l]);
         }
     }
     int b = block_excl_scan256(sum, s_w);
@@ -349,7 +349,7 @@ __global__ void __launch_bounds__(256) ivf_planfill_q(const int64_t *__restrict_
                 cnt[l] = c;
                 bucket_off[l] = b;
                 item_off[l] = ib;
-                ib += ((c + group - 1) / group) * ivf_nch(list_len[l]);
+                ib += ivf_ngroups(c, group) * ivf_nch(list_len[l]);
             }
             b += c;
         }
@@ -1188,8 +1188,8 @@ void launch_ivf_plan(const int64_t *probes, int64_t nq, int nprobe, const int *l
 // Upper bound on work items given the largest list's chunk count.
 // Σ_l ceil(cnt_l/G)·nch_l ≤ Σ_l (cnt_l/G + 1)·nch_l ≤ ceil(npairs/G)·max_nch + Σ_l nch_l.
 int64_t ivf_max_items(int64_t nq, int nprobe, int nlist, int max_nch, int64_t nrows, int group) {
-    const int64_t npairs = nq * nprobe;
-    return ceil_div(npairs, (int64_t)group) * std::max(max_nch, 1) + ceil_div(nrows, IVF_CH) + nlist;
+    const int64_t npairs = nq * nprobe;  // (a wide group size only lowers the count)
+    return ceil_div(npairs, (int64_t)ivf_group_narrow(group)) * std::max(max_nch, 1) + ceil_div(nrows, IVF_CH) + nlist;
 }
 
 int ivf_mfma_group(int d);            // ivf_mfma.hip

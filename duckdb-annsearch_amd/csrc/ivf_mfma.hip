@@ -161,6 +161,15 @@ __device__ __forceinline__ uint64_t row_kth(uint64_t l, int kth, int g) {
     return ((uint64_t)sh << 32) | sl;
 }
 
+// the key word of element kth of every row's list, broadcast to the row's lanes
+__device__ __forceinline__ unsigned row_kth_key(uint64_t l, int kth, int g) {
+    const unsigned hi = (unsigned)(l >> 32);
+    unsigned rh[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) rh[r] = (unsigned)__builtin_amdgcn_readlane((int)hi, 16 * r + kth);
+    return g == 0 ? rh[0] : g == 1 ? rh[1] : g == 2 ? rh[2] : rh[3];
+}
+
 // ---- end of an item: the waves' lists → the slot's partial list ------------------------------------
 // sub = 0: the 8 waves' lists are merged pairwise through LDS (3 rounds) and wave 0 writes the slot's k-list.
 // sub = 1 (the exact forms at request_k > 12, ivf.cpp): no merge — every wave writes its own k-list as
@@ -925,11 +934,32 @@ typedef _Float16 mh_f16x8 __attribute__((ext_vector_type(8)));
 #endif
 constexpr int MH_P = HIPANN_MH_P;  // super-steps in flight per wave: 6 × 2 row tiles × 16 B = 192 B per lane
 __host__ __device__ inline int mh_nsup(int d) { return (int)ceil_div(ceil_div(d, 32), MH_P) * MH_P; }
-// LDS dwords per query: 2 terms × super-steps × 4 groups × 4 dwords, + 8 (≡ 8 mod 64: conflict-free)
-__host__ __device__ inline int mh_stride(int d) { return 2 * mh_nsup(d) * 16 + 8; }
+// LDS dwords per query: NT terms × super-steps × 4 groups × 4 dwords, + 8 (≡ 8 mod 64: conflict-free)
+__host__ __device__ inline int mh_stride(int d, int nt = 2) { return nt * mh_nsup(d) * 16 + 8; }
 inline int mh_group(int d) {
     const int g = (int)(MF_LDS_MAX / ((size_t)mh_stride(d) * 4)) / 16 * 16;
     return g < 16 * MF_QTMAX ? g : 16 * MF_QTMAX;
+}
+// Wide items (lists probed by more queries than one two-term group holds): the queries' high fp16 term only, so
+// twice the queries fit the LDS (96 at d = 768) and the list's rows are streamed half as often; MFMAs per row and
+// query halve too.  The price is the query's own split residual: ‖q − h/t‖ (≈ 2⁻¹² relative) instead of
+// ‖q − (h + l)/t‖ (≈ 2⁻²³), which the scan hands to the rerank's bound for every query of a wide item.
+// On SURVEY §8(d)'s mixture (σ 0.8, nprobe 16) popular lists are probed by up to ~400 queries: 9 two-term
+// groups re-read each 2048-row chunk, 36 % of it from L2 (profiles/r06/mixture_scan_pmc_r06.txt).
+constexpr int MH_QTW = 6;  // query tiles of a wide item
+inline int mh_group_wide(int d) {  // the image + (‖q‖², 1/(t·s)) per query
+    const int g = (int)(MF_LDS_MAX / ((size_t)mh_stride(d, 1) * 4 + 8)) / 16 * 16;
+    return g < 16 * MH_QTW ? g : 16 * MH_QTW;
+}
+// HIPANN_IVF_WIDE=0 (A/B): every item two-term
+inline bool mh_wide_enabled() {
+    static const bool on = [] { const char *e = std::getenv("HIPANN_IVF_WIDE"); return !e || std::atoi(e); }();
+    return on;
+}
+// the packed group of the plan and the scan (ivf_ngroups, common.hpp)
+inline int mh_group_packed(int d) {
+    const int g = mh_group(d), w = mh_group_wide(d);
+    return mh_wide_enabled() && w > g && g >= 16 ? g | (w << 16) : g;
 }
 
 // fp32 → fp16 round to nearest even; subnormal results flushed to zero (the MFMA sees only normal
@@ -1114,7 +1144,7 @@ ivf_append_rows(const float *__restrict__ rows, const float *__restrict__ norms,
 
 // The batch's queries, one wave per query: t = 2^(14 − e_q), q·t split into two fp16 terms in the
 // image's k-slot order, qsplit [query][term][super-step][g][8 halves]; its[q] = 1/(t·s) (a power of
-// two) and qres[q] = ‖q − (h + l)/t‖ (×1.0001 for the fp32 sum).  A query whose scale leaves the safe
+// two), qres[q] = ‖q − (h + l)/t‖ and qres[nq + q] = ‖q − h/t‖ (×1.0001 for the fp32 sum; 2·nq floats).  A query whose scale leaves the safe
 // range (non-finite entries, |e_q| > 100, 1/(t·s) not a normal float) gets zero terms and qres = +inf:
 // the rerank flags it and it re-runs on the device in the direct form.
 // qn (optional): also ‖q‖², in exactly row_norms_f32's order (vec4: float4 j = lane, lane + 64, …, four fmas
@@ -1184,7 +1214,7 @@ __global__ void __launch_bounds__(256) ivf_split_queries_h(const float *__restri
     const int eits = -(et + es);
     const bool ok = mb < 0x7f800000u && eq >= -100 && eq <= 100 && eits >= -120 && eits <= 120;
     const float t = ldexpf(1.f, ok ? et : 0), inv_t = ldexpf(1.f, ok ? -et : 0);
-    float r2 = 0.f;
+    float r2 = 0.f, r1 = 0.f;  // two-term and one-term (high term only) split residuals
     for (int w = lane; w < nsup * 4; w += 64) {
         const int S = w >> 2, gg = w & 3;
         const int d0 = 32 * S + 4 * gg, d1 = d0 + 16;
@@ -1201,6 +1231,8 @@ __global__ void __launch_bounds__(256) ivf_split_queries_h(const float *__restri
             hw[pr] = mh_pack(x0, x1);
             const float m0 = x0 - mh_val((unsigned short)(hw[pr] & 0xffffu)), m1 = x1 - mh_val((unsigned short)(hw[pr] >> 16));
             lw[pr] = mh_pack(m0, m1);
+            r1 = fmaf(m0 * inv_t, m0 * inv_t, r1);
+            r1 = fmaf(m1 * inv_t, m1 * inv_t, r1);
             const float e0 = (m0 - mh_val((unsigned short)(lw[pr] & 0xffffu))) * inv_t;
             const float e1 = (m1 - mh_val((unsigned short)(lw[pr] >> 16))) * inv_t;
             r2 = fmaf(e0, e0, r2);
@@ -1210,18 +1242,23 @@ __global__ void __launch_bounds__(256) ivf_split_queries_h(const float *__restri
         out[((q * 2 + 1) * nsup + S) * 4 + gg] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) r2 += __shfl_xor(r2, o);
+    for (int o = 32; o > 0; o >>= 1) {
+        r2 += __shfl_xor(r2, o);
+        r1 += __shfl_xor(r1, o);
+    }
     if (lane == 0) {
         its[q] = ldexpf(1.f, ok ? eits : 0);
         qres[q] = ok ? sqrtf(r2) * 1.0001f : __builtin_inff();
+        qres[nq + q] = ok ? sqrtf(r1) * 1.0001f : __builtin_inff();  // a wide item's scan copies it over qres[q]
     }
 }
 
-template <int QT, bool IP>
+template <int QT, bool IP, int NT>
 __device__ __forceinline__ void mh_item(int d, const uint4 *__restrict__ codes_h, int64_t tp0,
                                         const float *__restrict__ xn, int64_t r0, int64_t r1, int nqi,
                                         const unsigned *__restrict__ qs, int stride, const float (&qn)[QT][4],
                                         const float (&qits)[QT][4], const unsigned (&qb)[QT][4],
+                                        const float2 *__restrict__ qpar,
                                         const int *__restrict__ bucket, int boff, int nprobe,
                                         const int *__restrict__ slot_off, int chunk, int k, int sub, float *smem,
                                         unsigned *__restrict__ qbound, float *__restrict__ part_d,
@@ -1233,19 +1270,17 @@ __device__ __forceinline__ void mh_item(int d, const uint4 *__restrict__ codes_h
     const int npass_all = (int)ceil_div(r1 - r0, MF_PASS);
     const int npass = npass_all > wave ? (npass_all - wave + MF_WAVES - 1) / MF_WAVES : 0;
 
-    bool qv[QT][4];
-#pragma unroll
-    for (int qt = 0; qt < QT; ++qt)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) qv[qt][v] = qt * 16 + 4 * g + v < nqi;
-    uint64_t lst[QT][4], thr[QT][4];
+    // per query: the sorted list (key, row) and the admission gate = the key of its k-th entry (a 16-row batch
+    // merges when some lane's key is ≤ the gate: a superset of the lexicographic test, the merge itself is exact)
+    uint64_t lst[QT][4];
+    unsigned thr[QT][4];
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
             const uint64_t b = ((uint64_t)qb[qt][v] << 32) | MF_PAD_ID;
             lst[qt][v] = m < k ? b : MF_EMPTY;
-            thr[qt][v] = b;
+            thr[qt][v] = qb[qt][v];
         }
 
     auto row_of = [&](int i, int r) -> int64_t {
@@ -1305,14 +1340,14 @@ __device__ __forceinline__ void mh_item(int d, const uint4 *__restrict__ codes_h
 #pragma unroll
             for (int p = 0; p < MH_P; ++p) {
                 const int S = S0 + p;
-                uint4 qa[QT][2];
+                uint4 qa[QT][NT];
 #pragma unroll
                 for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
-                    for (int j = 0; j < 2; ++j) qa[qt][j] = *reinterpret_cast<const uint4 *>(qrow[qt] + (j * nsup + S) * 16);
+                    for (int j = 0; j < NT; ++j) qa[qt][j] = *reinterpret_cast<const uint4 *>(qrow[qt] + (j * nsup + S) * 16);
                 // the small query term first in every accumulator chain
 #pragma unroll
-                for (int j = 1; j >= 0; --j)
+                for (int j = NT - 1; j >= 0; --j)
 #pragma unroll
                     for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
@@ -1330,19 +1365,29 @@ __device__ __forceinline__ void mh_item(int d, const uint4 *__restrict__ codes_h
             for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
                 for (int v = 0; v < 4; ++v) {
+                    float qnv, qiv;
+                    if constexpr (NT == 1) {  // wide items: (‖q‖², 1/(t·s)) from LDS (registers for 96 queries spill)
+                        const float2 p = qpar[qt * 16 + 4 * g + v];
+                        qnv = p.x;
+                        qiv = p.y;
+                    } else {
+                        qnv = qn[qt][v];
+                        qiv = qits[qt][v];
+                    }
                     float key;
                     if (IP) {
-                        key = -acc[qt][r][v] * qits[qt][v];
+                        key = -acc[qt][r][v] * qiv;
                     } else {
-                        key = fmaf(-2.f * qits[qt][v], acc[qt][r][v], qn[qt][v] + xnr[r]);
+                        key = fmaf(-2.f * qiv, acc[qt][r][v], qnv + xnr[r]);
                         key = key < 0.f ? 0.f : key;
                     }
-                    const bool ok = rok && qv[qt][v];
-                    uint64_t cp = ok ? (((uint64_t)mf_sortable(key) << 32) | rid) : MF_EMPTY;
-                    if (__ballot(cp < thr[qt][v])) {
+                    const bool ok = rok && qt * 16 + 4 * g + v < nqi;
+                    const unsigned ks = mf_sortable(key);
+                    uint64_t cp = ok ? (((uint64_t)ks << 32) | rid) : MF_EMPTY;
+                    if (__ballot(ok && ks <= thr[qt][v])) {
                         row_sort16(cp, m);
                         row_merge16(lst[qt][v], cp, m);
-                        thr[qt][v] = row_kth(lst[qt][v], k - 1, g);
+                        thr[qt][v] = row_kth_key(lst[qt][v], k - 1, g);
                     }
                 }
         }
@@ -1353,6 +1398,20 @@ __device__ __forceinline__ void mh_item(int d, const uint4 *__restrict__ codes_h
     mf_finish_item<QT>(lst, smem, nqi, bucket, boff, nprobe, slot_off, chunk, k, sub, qbound, part_d, part_i);
 }
 
+// Copy the item's queries' first NT fp16 terms (of the two in qsplit [query][term][S][g][4 dwords]) into LDS
+// [query][term][S][g][4].
+template <int NT>
+__device__ __forceinline__ void mh_fill(unsigned *qs, const uint4 *__restrict__ qsplit, int nsup, int stride, int nqi,
+                                        const int *__restrict__ bucket, int boff, int nprobe) {
+    const int per_q = NT * nsup * 4;
+    for (int t = threadIdx.x; t < nqi * per_q; t += MF_THREADS) {
+        const int q = t / per_q, rr = t - q * per_q;
+        const int j = rr / (nsup * 4), r2 = rr - j * (nsup * 4);
+        const int gq = bucket[boff + q] / nprobe;
+        *reinterpret_cast<uint4 *>(qs + q * stride + r2 * 4 + j * nsup * 16) = qsplit[((int64_t)gq * 2 + j) * nsup * 4 + r2];
+    }
+}
+
 template <bool IP>
 __global__ void __launch_bounds__(MF_THREADS, MF_WAVES / 4)
 ivf_scan_mfma_h(const uint4 *__restrict__ qsplit, const float *__restrict__ qnorm, const float *__restrict__ its, int d,
@@ -1360,7 +1419,7 @@ ivf_scan_mfma_h(const uint4 *__restrict__ qsplit, const float *__restrict__ qnor
                 const int64_t *__restrict__ list_off, const int *__restrict__ list_len, const int *__restrict__ cnt, const int *__restrict__ bucket_off,
                 const int *__restrict__ item_off, const int *__restrict__ bucket, const int *__restrict__ slot_off,
                 int nlist, int nprobe, int group, int k, int sub, unsigned *__restrict__ qbound, float *__restrict__ part_d,
-                int *__restrict__ part_i) {
+                int *__restrict__ part_i, float *__restrict__ qres, int nq) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int total = item_off[nlist];
     if ((int)blockIdx.x >= total) return;
@@ -1373,7 +1432,8 @@ ivf_scan_mfma_h(const uint4 *__restrict__ qsplit, const float *__restrict__ qnor
     const int l = lo;
     const int64_t lr0 = list_off[l], lr1 = lr0 + list_len[l];
     const int c = cnt[l];
-    const int ng = (c + group - 1) / group;
+    const bool wide = ivf_list_wide(c, group);  // block-uniform
+    const int ng = ivf_ngroups(c, group);
     const int rem = item - item_off[l];
     const int chunk = rem / ng, grp = rem - chunk * ng;
     const int q_begin = (int)((int64_t)grp * c / ng), q_end = (int)((int64_t)(grp + 1) * c / ng);
@@ -1384,13 +1444,26 @@ ivf_scan_mfma_h(const uint4 *__restrict__ qsplit, const float *__restrict__ qnor
     const int nqt = (nqi + 15) >> 4;
 
     unsigned *qs = reinterpret_cast<unsigned *>(smem);
-    const int stride = mh_stride(d);
-    mb_fill<2, 1>(qs, qsplit, mh_nsup(d), stride, 0, nqi, bucket, boff, nprobe);
+    const int nsup = mh_nsup(d);
+    const int stride = mh_stride(d, wide ? 1 : 2);
+    float2 *qpar = reinterpret_cast<float2 *>(qs + nqi * stride);  // wide items: (‖q‖², 1/(t·s)) after the image
+    if (wide) {
+        mh_fill<1>(qs, qsplit, nsup, stride, nqi, bucket, boff, nprobe);
+        for (int t = threadIdx.x; t < nqi; t += MF_THREADS) {
+            const int qi = bucket[boff + t] / nprobe;
+            qpar[t] = make_float2(IP ? 0.f : qnorm[qi], its[qi]);
+            // these queries' scan keys miss the low term: the rerank bounds them with the one-term residual (every
+            // item of the query's wide lists writes the same value)
+            qres[qi] = qres[nq + qi];
+        }
+    } else {
+        mh_fill<2>(qs, qsplit, nsup, stride, nqi, bucket, boff, nprobe);
+    }
     __syncthreads();
 
     const int lane = threadIdx.x & 63, g = lane >> 4;
     const int64_t tp0 = tpass_off[l] + (int64_t)chunk * (MF_CH / MF_PASS);
-#define MH_ARGS d, codes_h, tp0, xn, r0, r1, nqi, qs, stride, qn, qi_s, qb, bucket, boff, nprobe, slot_off, chunk, k, sub, smem, \
+#define MH_ARGS d, codes_h, tp0, xn, r0, r1, nqi, qs, stride, qn, qi_s, qb, qpar, bucket, boff, nprobe, slot_off, chunk, k, sub, smem, \
                 qbound, part_d, part_i
 #define MH_QN(QTV)                                                                                          \
     float qn[QTV][4], qi_s[QTV][4];                                                                         \
@@ -1398,25 +1471,28 @@ ivf_scan_mfma_h(const uint4 *__restrict__ qsplit, const float *__restrict__ qnor
     _Pragma("unroll") for (int qt = 0; qt < QTV; ++qt) _Pragma("unroll") for (int v = 0; v < 4; ++v) {      \
         const int q = qt * 16 + 4 * g + v;                                                                  \
         const int qi = q < nqi ? bucket[boff + q] / nprobe : 0;                                             \
-        qn[qt][v] = (!IP && q < nqi) ? qnorm[qi] : 0.f;                                                     \
-        qi_s[qt][v] = q < nqi ? its[qi] : 0.f;                                                              \
+        qn[qt][v] = (!IP && !wide && q < nqi) ? qnorm[qi] : 0.f;                                            \
+        qi_s[qt][v] = !wide && q < nqi ? its[qi] : 0.f;                                                     \
         qb[qt][v] = q < nqi ? __atomic_load_n(qbound + qi, __ATOMIC_RELAXED) : 0xffffffffu;                 \
     }
-    if (nqt <= 1) {
-        MH_QN(1)
-        mh_item<1, IP>(MH_ARGS);
-    } else if (nqt == 2) {
-        MH_QN(2)
-        mh_item<2, IP>(MH_ARGS);
+#define MH_CASE(QTV, NTV) { MH_QN(QTV) mh_item<QTV, IP, NTV>(MH_ARGS); }
+    if (wide) {
+        // nqi > group / 2 (a wide list has more than one narrow group of queries, split evenly)
+        if (nqt <= 3) MH_CASE(3, 1)
+        else if (nqt == 4) MH_CASE(4, 1)
+        else if (nqt == 5) MH_CASE(5, 1)
+        else MH_CASE(6, 1)
     } else {
-        MH_QN(3)
-        mh_item<3, IP>(MH_ARGS);
+        if (nqt <= 1) MH_CASE(1, 2)
+        else if (nqt == 2) MH_CASE(2, 2)
+        else MH_CASE(3, 2)
     }
+#undef MH_CASE
 #undef MH_QN
 #undef MH_ARGS
 }
 
-int ivf_mfma_h_group(int d) { return mh_group(d); }
+int ivf_mfma_h_group(int d) { return mh_group_packed(d); }
 int ivf_scan_sublists() { return MF_WAVES; }
 int64_t ivf_half_pass_bytes(int d) { return (int64_t)mh_nsup(d) * MF_RT * 64 * 16; }
 int64_t ivf_half_qsplit_bytes(int64_t nq, int d) { return nq * 2 * mh_nsup(d) * 64; }
@@ -1486,13 +1562,16 @@ void launch_ivf_scan_mfma_h(const float *Q, int64_t nq, void *qsplit, float *its
     if (!split_done)
         hipLaunchKernelGGL(ivf_split_queries_h, dim3((unsigned)ceil_div(nq, 4)), dim3(256), 0, st, Q, nq, d, nsup, es, qs,
                            its, qres, nullptr, (d % 4 == 0) && ((uintptr_t)Q % 16 == 0));
-    const int group = mh_group(d);
-    const size_t merge = (size_t)(MF_WAVES / 2) * MF_QTMAX * 4 * 64 * sizeof(float2);
-    const size_t smem = std::max((size_t)group * mh_stride(d) * 4, merge);
+    const int group = mh_group_packed(d);
+    const int gw = group >> 16;
+    const size_t merge = (size_t)(MF_WAVES / 2) * (gw ? MH_QTW : MF_QTMAX) * 4 * 64 * sizeof(float2);
+    const size_t smem = std::max({(size_t)ivf_group_narrow(group) * mh_stride(d) * 4, (size_t)gw * (mh_stride(d, 1) * 4 + 8), merge});
+    HIPANN_REQUIRE(smem <= MF_LDS_MAX, "fp16 IVF scan: LDS image too large");
+    HIPANN_REQUIRE(nq < (int64_t)0x7fffffff, "fp16 IVF scan: batch too large");
     dim3 grid((unsigned)max_items), block(MF_THREADS);
     const uint4 *ch = static_cast<const uint4 *>(codes_h);
 #define MH_LAUNCH_ARGS qs, qn, its, d, ch, tpass_off, xn, list_off, list_len, cnt, bucket_off, item_off, bucket, slot_off, nlist, nprobe, \
-                       group, k, sub, qbound, pd, pi
+                       group, k, sub, qbound, pd, pi, qres, (int)nq
     if (metric == kIP) hipLaunchKernelGGL((ivf_scan_mfma_h<true>), grid, block, smem, st, MH_LAUNCH_ARGS);
     else hipLaunchKernelGGL((ivf_scan_mfma_h<false>), grid, block, smem, st, MH_LAUNCH_ARGS);
 #undef MH_LAUNCH_ARGS

@@ -220,12 +220,23 @@ def scan_pairs(index, probes: np.ndarray) -> int:
     return int(sizes[p].sum())
 
 
-def scan_group_rows(index, probes: np.ndarray, group: int = 32) -> int:
-    """Rows the scan kernel streams per batch: every list once per group of ≤ `group` of its probing
-    queries, Σ_l ⌈c_l / group⌉·|l| (≥ the distinct-list rows when a list is probed by > group queries)."""
+def half_scan_groups(d: int, wide: bool = True) -> tuple:
+    """(narrow, wide) query-group sizes of the fp16 form's scan (ivf_mfma.hip mh_group / mh_group_wide: the
+    queries' LDS image, two fp16 terms or the high term only, in 160 KiB); wide 0 when disabled."""
+    nsup = -(-(-(-d // 32)) // 6) * 6
+    g = min(48, (163840 // ((2 * nsup * 16 + 8) * 4)) // 16 * 16)
+    w = min(96, (163840 // ((nsup * 16 + 8) * 4 + 8)) // 16 * 16)
+    return g, (w if wide and w > g and g >= 16 else 0)
+
+
+def scan_group_rows(index, probes: np.ndarray, group: int = 32, wide: int = 0) -> int:
+    """Rows the scan kernel streams per batch: every list once per group of its probing queries,
+    Σ_l ⌈c_l / g_l⌉·|l| with g_l = `wide` for a list probed by more than `group` queries (when wide > 0),
+    else `group` (≥ the distinct-list rows when a list is probed by more queries than one group holds)."""
     sizes = np.diff(index._offsets)
     c = np.bincount(probes[probes >= 0].ravel(), minlength=len(sizes))
-    return int((-(-c // group) * sizes).sum())
+    g = np.where((wide > 0) & (c > group), max(wide, 1), group)
+    return int((-(-c // g) * sizes).sum())
 
 
 def flat_ground_truth(torch, hipann, d: int, metric: int, xq, k: int, n_total: int, rank: int, world: int,

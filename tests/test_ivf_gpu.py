@@ -108,6 +108,27 @@ def test_ivf_mfma_query_tiles(gpu, oracle, nq, d, metric, form):
     check_topk_parity(xb, xq, D, I, Do, Io, metric, **_tol(form))
 
 
+@pytest.mark.parametrize("nq", [49, 80, 81, 96, 97, 150, 193, 290])
+@pytest.mark.parametrize("d,metric", [(96, 0), (100, 1), (768, 0), (1536, 0)])
+@pytest.mark.parametrize("k", [10, 20])
+def test_ivf_half_wide_items(gpu, oracle, nq, d, metric, k):
+    """The fp16 form's wide items (ivf_mfma.hip): a list probed by more queries than one two-term group (48 at
+    d ≤ 768, 16 at d = 1536) is scanned with the queries' high term only, in groups of up to 96 (48): one group of
+    49-96 queries (4-6 query tiles), two of 48/49 (3-4 tiles), three or more; k = 20 takes the sub-list slots.
+    The rerank bounds those queries with their one-term residual, so the ids still equal the oracle's."""
+    xb, xq = faiss_metal_case(4500 if d < 1000 else 2500, nq, d)
+    cen = np.ascontiguousarray(xb[:2])
+    off = np.array([0, 2100, len(xb)], np.int64)  # two lists, both probed by every query: 2 row chunks, ragged
+    ids = np.arange(len(xb), dtype=np.int64)
+    ix = gpu.HipIndexIVFFlat(cen, off, ids, xb, 2, metric)
+    ix.form = 6
+    D, I = ix.search(xq, k)
+    assert ix.last_search_path()["form"] == 6
+    Do, Io, Po = oracle.ivf_search(cen, off, ids, xb, xq, k, 2, metric)
+    assert np.array_equal(ix.last_probes(nq), Po)
+    check_topk_parity(xb, xq, D, I, Do, Io, metric, tau=TAU)
+
+
 def test_ivf_full_probe_equals_flat(gpu, oracle):
     xb, xq = faiss_metal_case(6000, 50, 48)
     ix, _ = _ivf(gpu, xb, 32, 32)

@@ -11,6 +11,11 @@ K=ivf_scan_mfma_h
 S=${MIX_SIGMA:-0.8}
 NP=${MIX_NPROBE:-16}
 P="python3 $root/tools/ivf_clustered_probe.py $S 10000000 $NP 6"
+if [ -n "$MIX_BENCH" ]; then  # the bench's mixture configuration alone (its group-row and list statistics)
+    (cd "$root" && timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-alt-forms --no-c5 --steps 5 --warmup 2 \
+        --only C3_ivf_survey_mixture > "$o/r06mix_bench.json" 2> "$o/r06mix_bench.err") \
+        || { echo "bench failed"; tail -5 "$o/r06mix_bench.err"; exit 1; }
+fi
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$o/r06mix_stats" -o run -- $P \
     > "$o/r06mix_stats.log" 2>&1 || { echo "stats failed"; tail -5 "$o/r06mix_stats.log"; exit 1; }
 cat "$o/r06mix_stats.log"
