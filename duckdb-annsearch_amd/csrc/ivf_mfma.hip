@@ -1419,11 +1419,11 @@ ivf_scan_mfma_h(const uint4 *__restrict__ qsplit, const float *__restrict__ qnor
                 const int64_t *__restrict__ list_off, const int *__restrict__ list_len, const int *__restrict__ cnt, const int *__restrict__ bucket_off,
                 const int *__restrict__ item_off, const int *__restrict__ bucket, const int *__restrict__ slot_off,
                 int nlist, int nprobe, int group, int k, int sub, unsigned *__restrict__ qbound, float *__restrict__ part_d,
-                int *__restrict__ part_i, float *__restrict__ qres, int nq) {
+                int *__restrict__ part_i, float *__restrict__ qres, int nq, int remap) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int total = item_off[nlist];
     if ((int)blockIdx.x >= total) return;
-    const int item = xcd_remap((int)blockIdx.x, total);
+    const int item = remap ? xcd_remap((int)blockIdx.x, total) : (int)blockIdx.x;
     int lo = 0, hi = nlist - 1;
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
@@ -1570,8 +1570,11 @@ void launch_ivf_scan_mfma_h(const float *Q, int64_t nq, void *qsplit, float *its
     HIPANN_REQUIRE(nq < (int64_t)0x7fffffff, "fp16 IVF scan: batch too large");
     dim3 grid((unsigned)max_items), block(MF_THREADS);
     const uint4 *ch = static_cast<const uint4 *>(codes_h);
+    // HIPANN_IVF_REMAP=0 (A/B): consecutive items (a chunk's query groups) dealt round-robin over the XCDs instead of
+    // contiguous runs per XCD
+    static const int remap = [] { const char *e = std::getenv("HIPANN_IVF_REMAP"); return !e || std::atoi(e) ? 1 : 0; }();
 #define MH_LAUNCH_ARGS qs, qn, its, d, ch, tpass_off, xn, list_off, list_len, cnt, bucket_off, item_off, bucket, slot_off, nlist, nprobe, \
-                       group, k, sub, qbound, pd, pi, qres, (int)nq
+                       group, k, sub, qbound, pd, pi, qres, (int)nq, remap
     if (metric == kIP) hipLaunchKernelGGL((ivf_scan_mfma_h<true>), grid, block, smem, st, MH_LAUNCH_ARGS);
     else hipLaunchKernelGGL((ivf_scan_mfma_h<false>), grid, block, smem, st, MH_LAUNCH_ARGS);
 #undef MH_LAUNCH_ARGS
