@@ -1083,6 +1083,7 @@ int diskann_hip_search_batch(void *h, const uint32_t *adj, int R, const uint32_t
         auto *db = static_cast<DiskDB *>(h);
         std::lock_guard<std::mutex> lk(db->mu);
         DeviceGuard g(db->device);
+        RoctxRange rr("hipann.diskann.host_bfs");
         host_bfs(db, adj, R, eps, n_ep, queries, nq, k, l_search, metric, out_ids, out_d, stats);
         return 0;
     } catch (const std::exception &e) {
@@ -1123,6 +1124,7 @@ int diskann_hip_register_graph(void *h, const uint32_t *adj, int R) {
 int diskann_hip_search_batch_resident_device(void *h, const uint32_t *eps, int n_ep, const float *queries_dev, int nq,
                                              int k, int l_search, int metric, int64_t *out_ids_dev,
                                              float *out_d_dev, int64_t *stats, void *stream, char *eb, int el) {
+    RoctxRange r_all("hipann.diskann.resident");
     try {
         HIPANN_REQUIRE(h && (n_ep == 0 || eps) && (nq == 0 || (queries_dev && out_ids_dev && out_d_dev)),
                        "null argument");

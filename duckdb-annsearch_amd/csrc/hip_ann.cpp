@@ -9,6 +9,8 @@
 #include "runtime.hpp"
 #include "ivf.hpp"
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -74,6 +76,13 @@ std::vector<int> device_list(const int *devices, int ndev) {
 }  // namespace
 
 namespace hipann {
+bool roctx_enabled() {
+    static const bool on = [] { const char *e = std::getenv("HIPANN_ROCTX"); return e && std::atoi(e); }();
+    return on;
+}
+void roctx_push(const char *name) { roctxRangePushA(name); }
+void roctx_pop() { roctxRangePop(); }
+
 std::vector<int> enable_peer_access(const std::vector<int> &devs) {
     std::vector<int> st(devs.size(), 2);
     if (devs.empty()) return st;
@@ -897,6 +906,7 @@ void flat_shard_finish(FlatIndex &ix, FlatShard &sh, const FlatPending &pend, hi
 
 void flat_shard_search(FlatIndex &ix, FlatShard &sh, int64_t nq, const float *xq, int k, int kout, float *D,
                        int64_t *I, hipStream_t st, int form_override, FlatPending *pend) {
+    RoctxRange r_all("hipann.flat.search_shard");
     FlatPending local;
     flat_shard_launch(ix, sh, nq, xq, k, kout, D, I, st, form_override, pend ? *pend : local);
     if (pend || local.kind == FlatPending::kNone) return;

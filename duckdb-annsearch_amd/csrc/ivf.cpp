@@ -240,6 +240,7 @@ float shard_xmax2(IvfShard &sh, int d, hipStream_t st) {
 
 void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, int k, int kout, float *D, int64_t *I,
                       hipStream_t st, int form_override, const int64_t *probes_in) {
+    RoctxRange r_all("hipann.ivf.search_shard");
     DeviceGuard g(sh.device);
     const int nlist = ix.nlist, d = ix.d, metric = ix.metric;
     const int np = std::min(ix.nprobe, nlist);
@@ -343,6 +344,7 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
             qsh0.qn.ensure(sizeof(float) * (size_t)nq, sh.device);
             qn_out = qsh0.qn.get<float>();
         }
+        RoctxRange rr("hipann.ivf.prepare");
         launch_ivf_split_queries_h(xq, nq, d, sh.half_es, sh.hsplit.p, sh.hits.get<float>(), sh.hres.get<float>(), qn_out,
                                    st);
         qsh0.qn_given = qn_out ? xq : nullptr;
@@ -360,6 +362,7 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
         HIPANN_CHECK(hipMemcpyAsync(sh.coarse_i.p, probes_in, sizeof(int64_t) * (size_t)nq * np, hipMemcpyDeviceToDevice,
                                     st));
     } else {
+        RoctxRange rr("hipann.ivf.coarse");
         qsh.plan_hook = ivf_plan_query_major() && hook_env ? &hook : nullptr;
         CoarseKeysScope ck(qsh);
         try {
@@ -379,10 +382,13 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     sh.bucket.ensure(sizeof(int) * (size_t)nq * np, sh.device);
     HIPANN_REQUIRE((int64_t)nq * np < (int64_t)0x7fffffff, "nq * nprobe too large");
     sh.slot_off.ensure(sizeof(int) * ((size_t)nq * np + 1), sh.device);
+    {
+    RoctxRange rr("hipann.ivf.plan");
     launch_ivf_plan(sh.coarse_i.get<int64_t>(), nq, np, sh.list_len.get<int>(), nlist, group, sh.cnt.get<int>(),
                     sh.bucket_off.get<int>(), sh.item_off.get<int>(), cur_cur, sh.bucket.get<int>(),
                     sh.slot_off.get<int>(), st, exact ? sh.nflag.get<int>() : nullptr, qbound, ccnt_cur,
                     sh.qtot.get<int>(), hook.done, ccnt_next, cur_next);
+    }
     sh.plan_batch++;
     ccnt_reset.armed = false;
     // 3. scan: one k-list per (query, probe, row chunk) slot — every slot is written by exactly one item
@@ -413,6 +419,7 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
         sh.qsplit.ensure((size_t)ivf_mfma_bf_qsplit_bytes(nq, d, ivf_form_terms(form)), sh.device);
     }
     {
+        RoctxRange rr("hipann.ivf.scan");
         ScopedTiming t(ix.timer_main, st);
         if (half)
             launch_ivf_scan_mfma_h(xq, nq, sh.hsplit.p, sh.hits.get<float>(), sh.hres.get<float>(), sh.half_es, qn, d,
@@ -479,6 +486,7 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
         }
     }
     {
+        RoctxRange rr("hipann.ivf.rerank");
         ScopedTiming t(ix.timer_merge, st);
         launch_ivf_rerank(sh.part_d.get<float>(), sh.part_i.get<int>(), sh.slot_off.get<int>(), np, nq, kfilt, kout,
                           metric, xq, sh.codes, d, sh.ids, sh.n, 0, xmax2, D, I, sh.nflag.get<int>(),
@@ -624,6 +632,7 @@ static void ivf_add_rows(IvfIndex &ix, int64_t n, const float *xb, const int64_t
 // one's copy may still be queued), scatter each row straight into its list's slack (one kernel: codes, label, norm),
 // re-tile the tiled images' touched passes.  Nothing waits for that tail: the next search is queued behind it.
 static void ivf_add_block(IvfIndex &ix, int64_t n, const float *xb, const int64_t *ids, int64_t base) {
+    RoctxRange r_all("hipann.ivf.add");
     const int d = ix.d, nlist = ix.nlist, metric = ix.metric;
     const int nsh = (int)ix.shards.size();
     IvfShard &s0 = *ix.shards[0];

@@ -121,6 +121,19 @@ struct ScopedTiming {
     ~ScopedTiming() { if (b) (void)hipEventRecord(b, s); }
 };
 
+// roctx ranges around the host stages of a call (HIPANN_ROCTX=1; off by default, then a scope costs one branch):
+// `rocprofv3 --marker-trace` shows each stage's enqueue span beside the kernels it launched (profiles/r06/).
+bool roctx_enabled();
+void roctx_push(const char *name);
+void roctx_pop();
+struct RoctxRange {
+    bool on;
+    explicit RoctxRange(const char *name) : on(roctx_enabled()) { if (on) roctx_push(name); }
+    ~RoctxRange() { if (on) roctx_pop(); }
+    RoctxRange(const RoctxRange &) = delete;
+    RoctxRange &operator=(const RoctxRange &) = delete;
+};
+
 // Pauses a timer for a scope (the exact forms' re-runs of flagged queries stay out of the main kernel's
 // timing, which the roofline reads).
 struct TimerPause {
