@@ -99,7 +99,7 @@ __host__ __device__ inline int ivf_form_terms(int f) { return f == kFormSplit3 ?
 // Query groups of an IVF list probed by c queries.  `group` packs the scan's group size (low 16 bits) and an
 // optional wide size (high 16 bits, 0 = none): a list probed by more queries than the narrow size is scanned in
 // groups of up to the wide size instead (the fp16 scan's one-term items, ivf_mfma.hip), so its rows are streamed
-// ceil(c / wide) times rather than ceil(c / narrow).
+// ceil(c / wide) times rather than ceil(c / narrow).  A narrow size of 0 makes every list wide (A/B only).
 __host__ __device__ inline int ivf_group_narrow(int group) { return group & 0xffff; }
 __host__ __device__ inline bool ivf_list_wide(int c, int group) { return (group >> 16) > 0 && c > (group & 0xffff); }
 __host__ __device__ inline int ivf_ngroups(int c, int group) {

@@ -951,15 +951,16 @@ inline int mh_group_wide(int d) {  // the image + (‖q‖², 1/(t·s)) per quer
     const int g = (int)(MF_LDS_MAX / ((size_t)mh_stride(d, 1) * 4 + 8)) / 16 * 16;
     return g < 16 * MH_QTW ? g : 16 * MH_QTW;
 }
-// HIPANN_IVF_WIDE=0 (A/B): every item two-term
-inline bool mh_wide_enabled() {
-    static const bool on = [] { const char *e = std::getenv("HIPANN_IVF_WIDE"); return !e || std::atoi(e); }();
-    return on;
+// HIPANN_IVF_WIDE=0 (A/B): every item two-term; =2 (A/B): every item one-term (narrow size 0)
+inline int mh_wide_mode() {
+    static const int mode = [] { const char *e = std::getenv("HIPANN_IVF_WIDE"); return e ? std::atoi(e) : 1; }();
+    return mode;
 }
 // the packed group of the plan and the scan (ivf_ngroups, common.hpp)
 inline int mh_group_packed(int d) {
     const int g = mh_group(d), w = mh_group_wide(d);
-    return mh_wide_enabled() && w > g && g >= 16 ? g | (w << 16) : g;
+    if (!mh_wide_mode() || w <= g || g < 16) return g;
+    return mh_wide_mode() == 2 ? (w << 16) : g | (w << 16);
 }
 
 // fp32 → fp16 round to nearest even; subnormal results flushed to zero (the MFMA sees only normal
@@ -1477,8 +1478,11 @@ ivf_scan_mfma_h(const uint4 *__restrict__ qsplit, const float *__restrict__ qnor
     }
 #define MH_CASE(QTV, NTV) { MH_QN(QTV) mh_item<QTV, IP, NTV>(MH_ARGS); }
     if (wide) {
-        // nqi > group / 2 (a wide list has more than one narrow group of queries, split evenly)
-        if (nqt <= 3) MH_CASE(3, 1)
+        // nqi > narrow / 2 (a wide list has more than one narrow group of queries, split evenly) unless every list
+        // is wide (narrow 0, A/B)
+        if (nqt <= 1) MH_CASE(1, 1)
+        else if (nqt == 2) MH_CASE(2, 1)
+        else if (nqt == 3) MH_CASE(3, 1)
         else if (nqt == 4) MH_CASE(4, 1)
         else if (nqt == 5) MH_CASE(5, 1)
         else MH_CASE(6, 1)
