@@ -103,6 +103,7 @@ __host__ __device__ inline int ivf_form_terms(int f) { return f == kFormSplit3 ?
 __host__ __device__ inline int ivf_group_narrow(int group) { return group & 0xffff; }
 __host__ __device__ inline bool ivf_list_wide(int c, int group) { return (group >> 16) > 0 && c > (group & 0xffff); }
 __host__ __device__ inline int ivf_ngroups(int c, int group) {
+    if (c <= 0) return 0;  // (an unprobed list: no division by a zero narrow size)
     const int g = ivf_list_wide(c, group) ? group >> 16 : group & 0xffff;
     return (c + g - 1) / g;
 }
