@@ -917,8 +917,9 @@ void launch_ivf_scan_mfma_bf(int np, const float *Q, int64_t nq, void *qsplit, c
 // every scaled element ≤ 2^14, far inside fp16's range), round to nearest even, subnormal results
 // flushed to zero; each query is scaled the same way (t = 2^(14 − e_q)) and split into two fp16 terms
 // q·t = h + l (+ ≤ 2⁻²² relative), so q·x ≈ (h + l)·x̂ / (t·s) on v_mfma_f32_16x16x32_f16 (fp16 × fp16
-// products are exact in fp32, fp32 accumulation).  The only non-negligible error is the rows' own
-// fp16 rounding, |q·(x − x̂/s)| ≤ ‖q‖·‖x − x̂/s‖, and the scan is a FILTER: it keeps the 16 best per
+// products are exact in fp32, fp32 accumulation) — or, in the one-term items that are the default since r06
+// (mh_wide_mode), h·x̂ / (t·s) with the query's own one-term residual ‖q − h/t‖ in the bound.  The other error is
+// the rows' own fp16 rounding, |q·(x − x̂/s)| ≤ ‖q‖·‖x − x̂/s‖, and the scan is a FILTER: it keeps the 16 best per
 // (query, list, chunk) like form 5, ivf_rerank_topk recomputes them in FAISS's direct fp32 form and
 // proves with the measured residuals (largest row residual, this query's split residual) that no
 // pruned row reaches the top-k; failing queries re-run on the device in the direct form.
@@ -951,9 +952,12 @@ inline int mh_group_wide(int d) {  // the image + (‖q‖², 1/(t·s)) per quer
     const int g = (int)(MF_LDS_MAX / ((size_t)mh_stride(d, 1) * 4 + 8)) / 16 * 16;
     return g < 16 * MH_QTW ? g : 16 * MH_QTW;
 }
-// HIPANN_IVF_WIDE=0 (A/B): every item two-term; =2 (A/B): every item one-term (narrow size 0)
+// HIPANN_IVF_WIDE: 2 (default) every item one-term (narrow size 0: groups of up to 96 queries); 1 (A/B) two-term items
+// for lists probed by ≤ 48 queries, one-term above; 0 (A/B) every item two-term.  Same box, alternating
+// (tools/gpu_r06_wide.sh MODES="1 2"): the headline 382.2K / 382.0K → 395.9K / 395.9K QPS (scan 2.553 → 2.491 ms: half
+// the MFMAs and LDS reads per row and query), the mixture unchanged, 0 flagged queries in both
 inline int mh_wide_mode() {
-    static const int mode = [] { const char *e = std::getenv("HIPANN_IVF_WIDE"); return e ? std::atoi(e) : 1; }();
+    static const int mode = [] { const char *e = std::getenv("HIPANN_IVF_WIDE"); return e ? std::atoi(e) : 2; }();
     return mode;
 }
 // the packed group of the plan and the scan (ivf_ngroups, common.hpp)

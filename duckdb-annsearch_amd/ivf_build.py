@@ -220,13 +220,16 @@ def scan_pairs(index, probes: np.ndarray) -> int:
     return int(sizes[p].sum())
 
 
-def half_scan_groups(d: int, wide: bool = True) -> tuple:
-    """(narrow, wide) query-group sizes of the fp16 form's scan (ivf_mfma.hip mh_group / mh_group_wide: the
-    queries' LDS image, two fp16 terms or the high term only, in 160 KiB); wide 0 when disabled."""
+def half_scan_groups(d: int, mode: int = 2) -> tuple:
+    """(narrow, wide) query-group sizes of the fp16 form's scan (ivf_mfma.hip mh_group / mh_group_wide /
+    mh_group_packed: the queries' LDS image, two fp16 terms or the high term only, in 160 KiB) for HIPANN_IVF_WIDE =
+    mode: 2 (default) every list wide (narrow 0), 1 wide above the narrow size, 0 no wide items (wide 0)."""
     nsup = -(-(-(-d // 32)) // 6) * 6
     g = min(48, (163840 // ((2 * nsup * 16 + 8) * 4)) // 16 * 16)
     w = min(96, (163840 // ((nsup * 16 + 8) * 4 + 8)) // 16 * 16)
-    return g, (w if wide and w > g and g >= 16 else 0)
+    if not mode or w <= g or g < 16:
+        return g, 0
+    return (0 if mode == 2 else g), w
 
 
 def scan_group_rows(index, probes: np.ndarray, group: int = 32, wide: int = 0) -> int:
@@ -235,7 +238,7 @@ def scan_group_rows(index, probes: np.ndarray, group: int = 32, wide: int = 0) -
     else `group` (≥ the distinct-list rows when a list is probed by more queries than one group holds)."""
     sizes = np.diff(index._offsets)
     c = np.bincount(probes[probes >= 0].ravel(), minlength=len(sizes))
-    g = np.where((wide > 0) & (c > group), max(wide, 1), group)
+    g = np.maximum(np.where((wide > 0) & (c > group), wide, group), 1)
     return int((-(-c // g) * sizes).sum())
 
 
