@@ -930,6 +930,9 @@ typedef _Float16 mh_f16x8 __attribute__((ext_vector_type(8)));
 #ifndef HIPANN_MH_P
 #define HIPANN_MH_P 6
 #endif
+#ifndef HIPANN_MH_EARLY
+#define HIPANN_MH_EARLY 1  // issue the item's first row loads before waiting for its query fill (0: fill, barrier, loads)
+#endif
 #ifndef HIPANN_MH_NT
 #define HIPANN_MH_NT 1  // non-temporal row loads (the image is read once per batch): 2.67 -> 2.59 ms at 10M x 768
 #endif
@@ -1326,6 +1329,10 @@ __device__ __forceinline__ void mh_item(int d, const uint4 *__restrict__ codes_h
             for (int r = 0; r < MF_RT; ++r) xnr[r] = xn[row_of(0, r)];
         }
     }
+    // the item's query image (and the wide items' parameters) were written by every thread before the call: wait for
+    // them only now, with this wave's first MH_P super-steps of rows already in flight
+    // (an LDS-only wait and the barrier: __syncthreads()'s fence would also drain the row loads, vmcnt(0))
+    if (HIPANN_MH_EARLY) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     const unsigned *qrow[QT];
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) qrow[qt] = qs + (qt * 16 + m) * stride + 4 * g;
@@ -1464,7 +1471,7 @@ ivf_scan_mfma_h(const uint4 *__restrict__ qsplit, const float *__restrict__ qnor
     } else {
         mh_fill<2>(qs, qsplit, nsup, stride, nqi, bucket, boff, nprobe);
     }
-    __syncthreads();
+    if (!HIPANN_MH_EARLY) __syncthreads();  // (early: mh_item waits for the fill after issuing its first row loads)
 
     const int lane = threadIdx.x & 63, g = lane >> 4;
     const int64_t tp0 = tpass_off[l] + (int64_t)chunk * (MF_CH / MF_PASS);
