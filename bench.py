@@ -746,13 +746,14 @@ def ivf_scan_stats(index, probes, d, nlist, row_bytes=None):
 
     cnt = np.bincount(probes[probes >= 0].ravel(), minlength=nlist)
     # the form's query groups: fp16 form (6) narrow / wide (HIPANN_IVF_WIDE=0 disables the wide items), else 32
-    g, w = half_scan_groups(d, int(os.environ.get("HIPANN_IVF_WIDE", "2"))) if index.form == 6 else (32, 0)
+    g, w, gm = (half_scan_groups(d, int(os.environ.get("HIPANN_IVF_WIDE", "2")), os.environ.get("HIPANN_IVF_GEMM", "1") != "0")
+                if index.form == 6 else (32, 0, 0))
     return {"scan_bytes_per_batch_local": scan_bytes(index, probes, d, row_bytes),
             "fp32_rows_bytes_per_batch_local": scan_bytes(index, probes, d),
             "distinct_lists_probed": int(np.unique(probes[probes >= 0]).size),
             "scanned_pairs_per_batch_local": scan_pairs(index, probes),
-            "group_rows_per_batch_local": scan_group_rows(index, probes, g, w),
-            "query_groups": [g, w],
+            "group_rows_per_batch_local": scan_group_rows(index, probes, g, w, gm),
+            "query_groups": [g, w, gm],
             "probes_per_list_p50_p90_max": [int(np.percentile(cnt, 50)), int(np.percentile(cnt, 90)), int(cnt.max())]}
 
 

@@ -96,16 +96,30 @@ constexpr float kSplit2Eps = 0x1p-12f;
 __host__ __device__ inline bool ivf_form_split(int f) { return f == kFormSplit3 || f == kFormSplit2; }
 __host__ __device__ inline int ivf_form_terms(int f) { return f == kFormSplit3 ? 3 : 2; }
 
-// Query groups of an IVF list probed by c queries.  `group` packs the scan's group size (low 16 bits) and an
-// optional wide size (high 16 bits, 0 = none): a list probed by more queries than the narrow size is scanned in
-// groups of up to the wide size instead (the fp16 scan's one-term items, ivf_mfma.hip), so its rows are streamed
-// ceil(c / wide) times rather than ceil(c / narrow).  A narrow size of 0 makes every list wide (A/B only).
-__host__ __device__ inline int ivf_group_narrow(int group) { return group & 0xffff; }
-__host__ __device__ inline bool ivf_list_wide(int c, int group) { return (group >> 16) > 0 && c > (group & 0xffff); }
+// Query groups of an IVF list probed by c queries.  `group` packs the scan's group sizes: narrow (bits 0-7), wide
+// (bits 8-15, 0 = none) and GEMM (bits 16-27, 0 = none).  A list probed by more queries than the narrow size is
+// scanned in groups of up to the wide size (the fp16 scan's one-term items, ivf_mfma.hip), and one probed by more
+// than the wide size in groups of up to the GEMM size (the GEMM-shaped items), so its rows are streamed ceil(c / size)
+// times.  A narrow size of 0 makes every probed list at least wide (the default of the fp16 form).
+__host__ __device__ inline int ivf_group_narrow(int group) { return group & 0xff; }
+__host__ __device__ inline int ivf_group_wide(int group) { return (group >> 8) & 0xff; }
+__host__ __device__ inline int ivf_group_gemm(int group) { return group >> 16; }
+// 0 narrow, 1 wide, 2 GEMM
+__host__ __device__ inline int ivf_list_class(int c, int group) {
+    const int n = ivf_group_narrow(group), w = ivf_group_wide(group), m = ivf_group_gemm(group);
+    if (m > 0 && c > (w > 0 ? w : n)) return 2;
+    return w > 0 && c > n ? 1 : 0;
+}
+__host__ __device__ inline bool ivf_list_wide(int c, int group) { return ivf_list_class(c, group) == 1; }
 __host__ __device__ inline int ivf_ngroups(int c, int group) {
     if (c <= 0) return 0;  // (an unprobed list: no division by a zero narrow size)
-    const int g = ivf_list_wide(c, group) ? group >> 16 : group & 0xffff;
+    const int cls = ivf_list_class(c, group);
+    const int g = cls == 2 ? ivf_group_gemm(group) : cls == 1 ? ivf_group_wide(group) : ivf_group_narrow(group);
     return (c + g - 1) / g;
+}
+// the smallest group size (the work-item bound)
+__host__ __device__ inline int ivf_group_min(int group) {
+    return ivf_group_narrow(group) > 0 ? ivf_group_narrow(group) : ivf_group_wide(group);
 }
 
 // XCD-aware block remap (cdna_hip_programming.md §5.5 T1, bijective form): blocks b and b+8 are

@@ -1189,8 +1189,7 @@ void launch_ivf_plan(const int64_t *probes, int64_t nq, int nprobe, const int *l
 // Σ_l ceil(cnt_l/G)·nch_l ≤ Σ_l (cnt_l/G + 1)·nch_l ≤ ceil(npairs/G)·max_nch + Σ_l nch_l.
 int64_t ivf_max_items(int64_t nq, int nprobe, int nlist, int max_nch, int64_t nrows, int group) {
     const int64_t npairs = nq * nprobe;  // (a wide group size only lowers the count)
-    const int g = ivf_group_narrow(group) ? ivf_group_narrow(group) : group >> 16;  // narrow 0: every list wide
-    return ceil_div(npairs, (int64_t)g) * std::max(max_nch, 1) + ceil_div(nrows, IVF_CH) + nlist;
+    return ceil_div(npairs, (int64_t)ivf_group_min(group)) * std::max(max_nch, 1) + ceil_div(nrows, IVF_CH) + nlist;
 }
 
 int ivf_mfma_group(int d);            // ivf_mfma.hip

@@ -963,11 +963,20 @@ inline int mh_wide_mode() {
     static const int mode = [] { const char *e = std::getenv("HIPANN_IVF_WIDE"); return e ? std::atoi(e) : 2; }();
     return mode;
 }
-// the packed group of the plan and the scan (ivf_ngroups, common.hpp)
+// GEMM items (lists probed by more queries than a wide item holds): up to MG_Q queries, database rows and queries both
+// staged through LDS by LDS-DMA (mg_item below); HIPANN_IVF_GEMM=0 (A/B): wide items for every list above the narrow
+// size
+constexpr int MG_Q = 256;
+inline bool mg_enabled() {
+    static const bool on = [] { const char *e = std::getenv("HIPANN_IVF_GEMM"); return !e || std::atoi(e); }();
+    return on;
+}
+// the packed group of the plan and the scan (narrow | wide << 8 | GEMM << 16: ivf_ngroups, common.hpp)
 inline int mh_group_packed(int d) {
     const int g = mh_group(d), w = mh_group_wide(d);
     if (!mh_wide_mode() || w <= g || g < 16) return g;
-    return mh_wide_mode() == 2 ? (w << 16) : g | (w << 16);
+    const int gm = mg_enabled() && w >= 16 ? MG_Q << 16 : 0;
+    return (mh_wide_mode() == 2 ? 0 : g) | (w << 8) | gm;
 }
 
 // fp32 → fp16 round to nearest even; subnormal results flushed to zero (the MFMA sees only normal
@@ -1424,6 +1433,210 @@ __device__ __forceinline__ void mh_fill(unsigned *qs, const uint4 *__restrict__ 
     }
 }
 
+// ---- GEMM items --------------------------------------------------------------------------------------------------
+// A list probed by more queries than a wide item holds (96 one-term queries fill the LDS) is scanned in items of up to
+// MG_Q = 256 of them, shaped as a small GEMM: per 32-dim K-step the block stages, by LDS-DMA, the step's slice of 128
+// database rows (4 passes × 2 row tiles × 1 KiB, straight from the tiled fp16 image) and of its 256 queries' high terms
+// (16 pieces of 16 queries × 64 B, gathered per lane from the batch's query image), four stages deep (three K-steps in
+// flight); wave (wr, wq) multiplies its 64 rows by its 64 queries (4 × 4 tiles of v_mfma_f32_16x16x32_f16) and keeps
+// the same 16-lane DPP-row lists as the wide items for its queries.  A 2048-row chunk is 16 block steps; the list is
+// streamed ceil(c / 256) times instead of ceil(c / 96).  LDS per K-step and wave: 4 + 4 ds_read_b128 for 16 MFMAs.
+// The stored query slice is swizzled (group g of query q at unit 4q + (g ^ F(q)), F(q) = −((q >> 2) & 3) & 3) so that
+// a wave's 16-query fragment read is conflict-free; the DMA lane that fills unit u loads the group that belongs there.
+typedef __attribute__((address_space(3))) void mg_lds_void;
+constexpr int MG_PASSES = 4;                        // 32-row passes per block step (128 rows)
+constexpr int MG_NST = 4;                           // LDS stages
+constexpr int MG_ROWU = MG_PASSES * MF_RT * 64;     // 16-B units of a stage's rows (8 KiB)
+constexpr int MG_STU = MG_ROWU + MG_Q * 4;          // + the queries' slice (16 KiB)
+constexpr size_t MG_XN = (size_t)MG_NST * MG_STU * 16;               // ‖x‖² of a block step's rows, by block parity
+constexpr size_t MG_QPAR = MG_XN + 2 * MG_PASSES * MF_PASS * sizeof(float);  // (‖q‖², 1/(t·s)) per query
+constexpr size_t MG_SCR = MG_QPAR + (size_t)MG_Q * sizeof(float2);  // the row halves' list merge
+constexpr size_t MG_LDS = MG_SCR + (size_t)4 * 4 * 4 * 64 * sizeof(uint64_t);
+static_assert(MG_LDS <= MF_LDS_MAX, "GEMM item LDS");
+static_assert(MF_WAVES == 8, "GEMM items: 2 row halves x 4 query quarters");
+
+template <bool IP>
+__device__ __forceinline__ void mg_item(int d, const uint4 *__restrict__ codes_h, int64_t tp0, const float *xn, int64_t r0,
+                                        int64_t r1, int nqi, const uint4 *__restrict__ qsplit, const float2 *qpar,
+                                        const int *__restrict__ bucket, int boff, int nprobe,
+                                        const int *__restrict__ slot_off, int chunk, int k, int sub, uint4 *stg,
+                                        uint64_t *scr, unsigned *__restrict__ qbound, float *__restrict__ part_d,
+                                        int *__restrict__ part_i) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int m = lane & 15, g = lane >> 4;
+    const int wr = wave & 1, wq = wave >> 1;  // row half (64 rows of a block step), query quarter (64 queries)
+    const int nsup = mh_nsup(d);
+    const int npass = (int)ceil_div(r1 - r0, MF_PASS);
+    const int G = (int)ceil_div(npass, MG_PASSES) * nsup;  // K-steps of the item
+    const int q0w = wq * 64;
+    const int nqt_w = nqi > q0w ? min(4, (nqi - q0w + 15) >> 4) : 0;  // the wave's tiles holding a real query
+
+    uint64_t lst[4][4];
+    unsigned thr[4][4];
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const int q = q0w + qt * 16 + 4 * g + v;
+            const unsigned qb = q < nqi ? __atomic_load_n(qbound + bucket[boff + q] / nprobe, __ATOMIC_RELAXED)
+                                        : 0xffffffffu;
+            lst[qt][v] = m < k ? (((uint64_t)qb << 32) | MF_PAD_ID) : MF_EMPTY;
+            thr[qt][v] = qb;
+        }
+
+    // the wave's DMA pieces per K-step: row piece (pass wave >> 1, tile wave & 1) and query pieces 2·wave, 2·wave + 1
+    const int rp_p = wave >> 1, rp_r = wave & 1;
+    const uint4 *qsrc[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int ql = 16 * (2 * wave + i) + (lane >> 2);
+        const int gq = bucket[boff + (ql < nqi ? ql : 0)] / nprobe;
+        const int gs = (lane & 3) ^ ((-(lane >> 4)) & 3);  // the source group stored at this lane's unit
+        qsrc[i] = qsplit + (int64_t)gq * 2 * nsup * 4 + gs;
+    }
+    // a block step's first K-step also brings its rows' ‖x‖² (L2): one dword DMA per wave, rows 64·(wave & 1) + lane of
+    // the step into the parity-(blk & 1) buffer (the other waves repeat the two halves: every wave issues the same ops)
+    float *xnb = reinterpret_cast<float *>(reinterpret_cast<char *>(stg) + MG_XN);
+    auto issue = [&](int gk) {  // K-step min(gk, G − 1) into stage gk % MG_NST (past the end: a stage never read)
+        const int gs = gk < G ? gk : G - 1;
+        const int blk = gs / nsup, S = gs - blk * nsup;
+        int pass = blk * MG_PASSES + rp_p;
+        pass = pass < npass ? pass : npass - 1;
+        uint4 *dst = stg + (gk % MG_NST) * MG_STU;
+        if (!IP && S == 0) {
+            const int64_t row = r0 + (int64_t)blk * (MG_PASSES * MF_PASS) + 64 * (wave & 1) + lane;
+            __builtin_amdgcn_global_load_lds((const void *)(xn + (row < r1 ? row : r1 - 1)),
+                                             (mg_lds_void *)(xnb + (blk & 1) * (MG_PASSES * MF_PASS) + 64 * (wave & 1)),
+                                             4, 0, 0);
+        }
+        __builtin_amdgcn_global_load_lds(
+            (const void *)(codes_h + ((tp0 + pass) * nsup + S) * (MF_RT * 64) + rp_r * 64 + lane),
+            (mg_lds_void *)(dst + (rp_p * MF_RT + rp_r) * 64), 16, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            __builtin_amdgcn_global_load_lds((const void *)(qsrc[i] + S * 4),
+                                             (mg_lds_void *)(dst + MG_ROWU + (2 * wave + i) * 64), 16, 0, 0);
+    };
+    // waits (vmcnt: loads retire in issue order): at K-step gk the stage of gk must have landed; younger are the two
+    // next K-steps' DMA ops — 3 each, 4 for a block step's first K-step (L2: its ‖x‖²)
+    auto first_of_blk = [&](int x) { const int gs = x < G ? x : G - 1; return !IP && gs % nsup == 0; };
+
+    if (G > 0) {
+        issue(0);
+        issue(1);
+        issue(2);
+    }
+    mf_f32x4 acc[4][4];
+    float xr[4] = {0.f, 0.f, 0.f, 0.f};
+    int blk = 0, S = 0;
+    const int fq = (-(m >> 2)) & 3;  // the swizzle of this lane's query rows
+    for (int gk = 0; gk < G; ++gk) {
+        if (S == 0)
+#pragma unroll
+            for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+                for (int rt = 0; rt < 4; ++rt) acc[qt][rt] = mf_f32x4{0.f, 0.f, 0.f, 0.f};
+        const int younger = (int)first_of_blk(gk + 1) + (int)first_of_blk(gk + 2);  // wave-uniform
+        if (younger == 0) __builtin_amdgcn_s_waitcnt(0xF70u | 6u);
+        else if (younger == 1) __builtin_amdgcn_s_waitcnt(0xF70u | 7u);
+        else __builtin_amdgcn_s_waitcnt(0xF70u | 8u);
+        __builtin_amdgcn_s_barrier();  // every wave's stage gk landed; every wave done reading stage gk − 1
+        asm volatile("" ::: "memory");
+        issue(gk + 3);
+        const uint4 *sb = stg + (gk % MG_NST) * MG_STU;
+        uint4 rb[4], qa[4];
+#pragma unroll
+        for (int rt = 0; rt < 4; ++rt) rb[rt] = sb[((2 * wr + (rt >> 1)) * MF_RT + (rt & 1)) * 64 + lane];
+#pragma unroll
+        for (int qt = 0; qt < 4; ++qt)
+            if (qt < nqt_w) qa[qt] = sb[MG_ROWU + (q0w + qt * 16 + m) * 4 + (g ^ fq)];
+#pragma unroll
+        for (int qt = 0; qt < 4; ++qt)
+            if (qt < nqt_w)
+#pragma unroll
+                for (int rt = 0; rt < 4; ++rt) acc[qt][rt] = mh_mfma(qa[qt], rb[rt], acc[qt][rt]);
+        if (++S == nsup) {
+            // epilogue of block step blk: the wave's 64 rows × its queries into the lists
+            if (!IP)
+#pragma unroll
+                for (int rt = 0; rt < 4; ++rt) xr[rt] = xnb[(blk & 1) * (MG_PASSES * MF_PASS) + wr * 64 + rt * 16 + m];
+#pragma unroll
+            for (int rt = 0; rt < 4; ++rt) {
+                const int64_t row = r0 + (int64_t)blk * (MG_PASSES * MF_PASS) + wr * 64 + rt * 16 + m;
+                const bool rok = row < r1;
+                const unsigned rid = rok ? (unsigned)row : MF_PAD_ID;
+#pragma unroll
+                for (int qt = 0; qt < 4; ++qt) {
+                    if (qt >= nqt_w) continue;  // wave-uniform
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) {
+                        const int q = q0w + qt * 16 + 4 * g + v;
+                        const float2 p = qpar[q];
+                        float key;
+                        if (IP) {
+                            key = -acc[qt][rt][v] * p.y;
+                        } else {
+                            key = fmaf(-2.f * p.y, acc[qt][rt][v], p.x + xr[rt]);
+                            key = key < 0.f ? 0.f : key;
+                        }
+                        const bool ok = rok && q < nqi;
+                        const unsigned ks = mf_sortable(key);
+                        uint64_t cp = ok ? (((uint64_t)ks << 32) | rid) : MF_EMPTY;
+                        if (__ballot(ok && ks <= thr[qt][v])) {
+                            row_sort16(cp, m);
+                            row_merge16(lst[qt][v], cp, m);
+                            thr[qt][v] = row_kth_key(lst[qt][v], k - 1, g);
+                        }
+                    }
+                }
+            }
+            S = 0;
+            ++blk;
+        }
+    }
+    // drain the DMA issued past the end before the LDS is reused or released
+    __builtin_amdgcn_s_waitcnt(0xF70u);
+    __syncthreads();
+    if (!sub) {  // the two row halves' lists of each query quarter: wr = 1 hands its lists to wr = 0
+        uint64_t *sw = scr + (size_t)wq * 4 * 4 * 64;
+        if (wr == 1)
+#pragma unroll
+            for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) sw[(qt * 4 + v) * 64 + lane] = lst[qt][v];
+        __syncthreads();
+        if (wr == 0)
+#pragma unroll
+            for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) row_merge16(lst[qt][v], sw[(qt * 4 + v) * 64 + lane], m);
+    }
+    if ((sub || wr == 0) && m < k) {
+#pragma unroll
+        for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const int q = q0w + qt * 16 + 4 * g + v;
+                if (q >= nqi) continue;
+                const int pr = bucket[boff + q];
+                const int64_t slot = (int64_t)slot_off[pr] + chunk;
+                const uint64_t e = lst[qt][v];
+                const unsigned id = (unsigned)e;
+                const bool real = e != MF_EMPTY && id != MF_PAD_ID;
+                const int64_t off = (sub ? slot * MF_WAVES + wr : slot) * k + m;
+                part_d[off] = real ? mf_unsortable((unsigned)(e >> 32)) : __builtin_inff();
+                part_i[off] = real ? (int)id : (int)MF_PAD_ID;
+                if (m == k - 1 && real) atomicMin(qbound + pr / nprobe, (unsigned)(e >> 32));
+                if (sub && wr == 0)  // the slot's other sub-lists (MF_WAVES per slot; two row halves here) stay empty
+                    for (int s2 = 2; s2 < MF_WAVES; ++s2) {
+                        part_d[(slot * MF_WAVES + s2) * k + m] = __builtin_inff();
+                        part_i[(slot * MF_WAVES + s2) * k + m] = (int)MF_PAD_ID;
+                    }
+            }
+    }
+}
+
 template <bool IP>
 __global__ void __launch_bounds__(MF_THREADS, MF_WAVES / 4)
 ivf_scan_mfma_h(const uint4 *__restrict__ qsplit, const float *__restrict__ qnorm, const float *__restrict__ its, int d,
@@ -1444,7 +1657,8 @@ ivf_scan_mfma_h(const uint4 *__restrict__ qsplit, const float *__restrict__ qnor
     const int l = lo;
     const int64_t lr0 = list_off[l], lr1 = lr0 + list_len[l];
     const int c = cnt[l];
-    const bool wide = ivf_list_wide(c, group);  // block-uniform
+    const int cls = ivf_list_class(c, group);  // block-uniform
+    const bool wide = cls == 1;
     const int ng = ivf_ngroups(c, group);
     const int rem = item - item_off[l];
     const int chunk = rem / ng, grp = rem - chunk * ng;
@@ -1455,6 +1669,20 @@ ivf_scan_mfma_h(const uint4 *__restrict__ qsplit, const float *__restrict__ qnor
     const int boff = bucket_off[l] + q_begin;
     const int nqt = (nqi + 15) >> 4;
 
+    if (cls == 2) {
+        uint4 *stg = reinterpret_cast<uint4 *>(smem);
+        float2 *gpar = reinterpret_cast<float2 *>(reinterpret_cast<char *>(smem) + MG_QPAR);
+        for (int t = threadIdx.x; t < nqi; t += MF_THREADS) {
+            const int qi = bucket[boff + t] / nprobe;
+            gpar[t] = make_float2(IP ? 0.f : qnorm[qi], its[qi]);
+            qres[qi] = qres[nq + qi];  // one-term scan keys: the rerank's bound takes the one-term residual
+        }
+        __syncthreads();
+        const int64_t tpg = tpass_off[l] + (int64_t)chunk * (MF_CH / MF_PASS);
+        mg_item<IP>(d, codes_h, tpg, xn, r0, r1, nqi, qsplit, gpar, bucket, boff, nprobe, slot_off, chunk, k, sub, stg,
+                    reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(smem) + MG_SCR), qbound, part_d, part_i);
+        return;
+    }
     unsigned *qs = reinterpret_cast<unsigned *>(smem);
     const int nsup = mh_nsup(d);
     const int stride = mh_stride(d, wide ? 1 : 2);
@@ -1578,9 +1806,10 @@ void launch_ivf_scan_mfma_h(const float *Q, int64_t nq, void *qsplit, float *its
         hipLaunchKernelGGL(ivf_split_queries_h, dim3((unsigned)ceil_div(nq, 4)), dim3(256), 0, st, Q, nq, d, nsup, es, qs,
                            its, qres, nullptr, (d % 4 == 0) && ((uintptr_t)Q % 16 == 0));
     const int group = mh_group_packed(d);
-    const int gw = group >> 16;
+    const int gw = ivf_group_wide(group);
     const size_t merge = (size_t)(MF_WAVES / 2) * (gw ? MH_QTW : MF_QTMAX) * 4 * 64 * sizeof(float2);
-    const size_t smem = std::max({(size_t)ivf_group_narrow(group) * mh_stride(d) * 4, (size_t)gw * (mh_stride(d, 1) * 4 + 8), merge});
+    const size_t smem = std::max({(size_t)ivf_group_narrow(group) * mh_stride(d) * 4, (size_t)gw * (mh_stride(d, 1) * 4 + 8), merge,
+                                  ivf_group_gemm(group) ? MG_LDS : (size_t)0});
     HIPANN_REQUIRE(smem <= MF_LDS_MAX, "fp16 IVF scan: LDS image too large");
     HIPANN_REQUIRE(nq < (int64_t)0x7fffffff, "fp16 IVF scan: batch too large");
     dim3 grid((unsigned)max_items), block(MF_THREADS);

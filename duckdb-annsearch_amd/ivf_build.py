@@ -220,25 +220,32 @@ def scan_pairs(index, probes: np.ndarray) -> int:
     return int(sizes[p].sum())
 
 
-def half_scan_groups(d: int, mode: int = 2) -> tuple:
-    """(narrow, wide) query-group sizes of the fp16 form's scan (ivf_mfma.hip mh_group / mh_group_wide /
-    mh_group_packed: the queries' LDS image, two fp16 terms or the high term only, in 160 KiB) for HIPANN_IVF_WIDE =
-    mode: 2 (default) every list wide (narrow 0), 1 wide above the narrow size, 0 no wide items (wide 0)."""
+def half_scan_groups(d: int, mode: int = 2, gemm: bool = True) -> tuple:
+    """(narrow, wide, gemm) query-group sizes of the fp16 form's scan (ivf_mfma.hip mh_group / mh_group_wide /
+    mh_group_packed: the queries' LDS image, two fp16 terms or the high term only, in 160 KiB; GEMM items of 256) for
+    HIPANN_IVF_WIDE = mode (2 default: every list at least wide, narrow 0; 1: wide above the narrow size; 0: no wide
+    items) and HIPANN_IVF_GEMM (gemm)."""
     nsup = -(-(-(-d // 32)) // 6) * 6
     g = min(48, (163840 // ((2 * nsup * 16 + 8) * 4)) // 16 * 16)
     w = min(96, (163840 // ((nsup * 16 + 8) * 4 + 8)) // 16 * 16)
     if not mode or w <= g or g < 16:
-        return g, 0
-    return (0 if mode == 2 else g), w
+        return g, 0, 0
+    return (0 if mode == 2 else g), w, (256 if gemm and w >= 16 else 0)
 
 
-def scan_group_rows(index, probes: np.ndarray, group: int = 32, wide: int = 0) -> int:
+def scan_group_rows(index, probes: np.ndarray, group: int = 32, wide: int = 0, gemm: int = 0) -> int:
     """Rows the scan kernel streams per batch: every list once per group of its probing queries,
-    Σ_l ⌈c_l / g_l⌉·|l| with g_l = `wide` for a list probed by more than `group` queries (when wide > 0),
-    else `group` (≥ the distinct-list rows when a list is probed by more queries than one group holds)."""
+    Σ_l ⌈c_l / g_l⌉·|l| with g_l = `gemm` for a list probed by more than the wide size (when gemm > 0), `wide` for
+    one probed by more than `group` (when wide > 0), else `group` (≥ the distinct-list rows when a list is probed by
+    more queries than one group holds) — ivf_ngroups (common.hpp)."""
     sizes = np.diff(index._offsets)
     c = np.bincount(probes[probes >= 0].ravel(), minlength=len(sizes))
-    g = np.maximum(np.where((wide > 0) & (c > group), wide, group), 1)
+    g = np.full_like(c, group)
+    if wide > 0:
+        g = np.where(c > group, wide, g)
+    if gemm > 0:
+        g = np.where(c > (wide if wide > 0 else group), gemm, g)
+    g = np.maximum(g, 1)
     return int((-(-c // g) * sizes).sum())
 
 

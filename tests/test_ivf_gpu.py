@@ -108,14 +108,15 @@ def test_ivf_mfma_query_tiles(gpu, oracle, nq, d, metric, form):
     check_topk_parity(xb, xq, D, I, Do, Io, metric, **_tol(form))
 
 
-@pytest.mark.parametrize("nq", [49, 80, 81, 96, 97, 150, 193, 290])
+@pytest.mark.parametrize("nq", [17, 49, 80, 81, 96, 97, 150, 193, 256, 257, 290, 513, 700])
 @pytest.mark.parametrize("d,metric", [(96, 0), (100, 1), (768, 0), (1536, 0)])
 @pytest.mark.parametrize("k", [10, 20])
 def test_ivf_half_wide_items(gpu, oracle, nq, d, metric, k):
-    """The fp16 form's wide items (ivf_mfma.hip): a list probed by more queries than one two-term group (48 at
-    d ≤ 768, 16 at d = 1536) is scanned with the queries' high term only, in groups of up to 96 (48): one group of
-    49-96 queries (4-6 query tiles), two of 48/49 (3-4 tiles), three or more; k = 20 takes the sub-list slots.
-    The rerank bounds those queries with their one-term residual, so the ids still equal the oracle's."""
+    """The fp16 form's one-term items (ivf_mfma.hip): every list's queries enter on their high fp16 term, in wide
+    items of up to 96 queries (48 at d = 1536) — one item of 17-96 queries (2-6 query tiles) — and, for a list probed
+    by more than that, GEMM items of up to 256 (rows and queries staged by LDS-DMA): one of 97-256 queries, two of
+    128/129, three of 171 (513), ragged last query tiles; k = 20 takes the sub-list slots.  The rerank bounds those
+    queries with their one-term residual, so the ids still equal the oracle's."""
     xb, xq = faiss_metal_case(4500 if d < 1000 else 2500, nq, d)
     cen = np.ascontiguousarray(xb[:2])
     off = np.array([0, 2100, len(xb)], np.int64)  # two lists, both probed by every query: 2 row chunks, ragged
