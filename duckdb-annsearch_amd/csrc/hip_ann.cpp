@@ -500,28 +500,37 @@ static void flat_shard_launch(FlatIndex &ix, FlatShard &sh, int64_t nq, const fl
         const int64_t rpw = ceil_div(sh.n, nwaves);
         nwaves = ceil_div(sh.n, rpw);
         const int64_t nw_alloc = ceil_div(nwaves, 4) * 4;
-        HIPANN_REQUIRE(scan_smem_bytes((int)nq, d) <= 64 * 1024, "dimension too large for the scan path");
-        sh.part_d.ensure((size_t)nw_alloc * nq * k * sizeof(float), sh.device);
-        sh.part_i.ensure((size_t)nw_alloc * nq * k * sizeof(int), sh.device);
-        {
-            ScopedTiming t(ix.timer_main, st);
-            launch_flat_scan_topk(xq, (int)nq, sh.xb, sh.n, d, metric, k, (int)nw_alloc, rpw, sh.part_d.get<float>(),
-                                  sh.part_i.get<int>(), st);
-        }
-        ScopedTiming t(ix.timer_merge, st);
+        // the scan holds its queries in ≤ 64 KiB of LDS: larger d·nq runs as several query chunks (d = 1536 fits 10
+        // queries; one query up to d = 16384)
+        int qc = (int)nq;
+        while (qc > 1 && scan_smem_bytes(qc, d) > 64 * 1024) --qc;
+        HIPANN_REQUIRE(scan_smem_bytes(qc, d) <= 64 * 1024, "dimension too large for the scan path");
+        sh.part_d.ensure((size_t)nw_alloc * qc * k * sizeof(float), sh.device);
+        sh.part_i.ensure((size_t)nw_alloc * qc * k * sizeof(int), sh.device);
+        const int groups = (int)std::min<int64_t>(256, ceil_div(nw_alloc, 32));
         if (nw_alloc > 256) {
-            // thousands of per-wave lists: groups of ~32 merged by one wave each, then the group lists by one
-            // 4-wave block per query (one wave per query took ~1 ms for 8192 lists at 10M rows, nq = 1)
-            const int groups = (int)std::min<int64_t>(256, ceil_div(nw_alloc, 32));
-            sh.mid_d.ensure(sizeof(float) * (size_t)groups * nq * kout, sh.device);
-            sh.mid_i.ensure(sizeof(long long) * (size_t)groups * nq * kout, sh.device);
-            launch_merge_parts_2level<int>(sh.part_d.get<float>(), sh.part_i.get<int>(), (int)nw_alloc, nq, k, kout,
-                                           sh.label_offset, 1.f, out_sign, D, I, sh.mid_d.get<float>(),
-                                           sh.mid_i.get<long long>(), groups, st);
-            return;
+            sh.mid_d.ensure(sizeof(float) * (size_t)groups * qc * kout, sh.device);
+            sh.mid_i.ensure(sizeof(long long) * (size_t)groups * qc * kout, sh.device);
         }
-        launch_merge_parts<int>(sh.part_d.get<float>(), sh.part_i.get<int>(), (int)nw_alloc, nq, k, kout,
-                                sh.label_offset, 1.f, out_sign, D, I, st);
+        for (int64_t q0 = 0; q0 < nq; q0 += qc) {
+            const int64_t nc = std::min<int64_t>(qc, nq - q0);
+            {
+                ScopedTiming t(ix.timer_main, st);
+                launch_flat_scan_topk(xq + q0 * d, (int)nc, sh.xb, sh.n, d, metric, k, (int)nw_alloc, rpw,
+                                      sh.part_d.get<float>(), sh.part_i.get<int>(), st);
+            }
+            ScopedTiming t(ix.timer_merge, st);
+            if (nw_alloc > 256) {
+                // thousands of per-wave lists: groups of ~32 merged by one wave each, then the group lists by one
+                // 4-wave block per query (one wave per query took ~1 ms for 8192 lists at 10M rows, nq = 1)
+                launch_merge_parts_2level<int>(sh.part_d.get<float>(), sh.part_i.get<int>(), (int)nw_alloc, nc, k, kout,
+                                               sh.label_offset, 1.f, out_sign, D + q0 * kout, I + q0 * kout,
+                                               sh.mid_d.get<float>(), sh.mid_i.get<long long>(), groups, st);
+            } else {
+                launch_merge_parts<int>(sh.part_d.get<float>(), sh.part_i.get<int>(), (int)nw_alloc, nc, k, kout,
+                                        sh.label_offset, 1.f, out_sign, D + q0 * kout, I + q0 * kout, st);
+            }
+        }
         return;
     }
     // BLAS form: ‖q‖² + ‖x‖² − 2 q·x on fp32 MFMA.  ‖q‖² is launched by qn_now() ahead of its first reader (the int8

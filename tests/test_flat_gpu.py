@@ -68,6 +68,19 @@ def test_flat_batch_sizes_across_blas_threshold(gpu, oracle, nq, metric):
     check_topk_parity(xb, xq, D, I, Do, Io, metric)
 
 
+@pytest.mark.parametrize("d,nq", [(1536, 11), (1536, 17), (1536, 19), (2048, 9), (4096, 5), (16384, 2)])
+@pytest.mark.parametrize("n", [700, 5000])
+def test_flat_small_batch_large_dimension(gpu, oracle, d, nq, n):
+    """nq < 20 (FAISS's non-BLAS path) with d·nq beyond the direct scan's 64 KiB of queries in LDS: the batch runs as
+    query chunks (before r06 this raised "dimension too large for the scan path", also for an IVF coarse step)."""
+    xb, xq = faiss_metal_case(n, nq, d)
+    for metric in (0, 1):
+        ix = gpu.HipIndexFlat(d, metric, xb)
+        D, I = ix.search(xq, 7)
+        Do, Io = oracle.flat_search(xb, xq, 7, metric)
+        check_topk_parity(xb, xq, D, I, Do, Io, metric)
+
+
 @pytest.mark.parametrize("d", [1, 3, 5, 31, 33, 100, 130, 2048])
 def test_flat_odd_dimensions(gpu, oracle, d):
     xb, xq = faiss_metal_case(700, 24, d)
