@@ -7,7 +7,7 @@ cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
 if [ -z "$NO_TESTS" ]; then
-    timeout -k 10 900 python -u -m pytest tests/test_ivf_gpu.py tests/test_configs_gpu.py tests/test_request_k_gpu.py \
+    timeout -k 10 900 python -u -m pytest tests/test_ivf_gpu.py tests/test_configs_gpu.py tests/test_request_k_gpu.py tests/test_flat_gpu.py \
         -m gpu -q -x --timeout 300 --timeout-method thread > gpurun_out/r06gm_tests.log 2>&1 \
         || { tail -40 gpurun_out/r06gm_tests.log; exit 1; }
     tail -2 gpurun_out/r06gm_tests.log
