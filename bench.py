@@ -746,7 +746,7 @@ def ivf_scan_stats(index, probes, d, nlist, row_bytes=None):
 
     cnt = np.bincount(probes[probes >= 0].ravel(), minlength=nlist)
     # the form's query groups: fp16 form (6) narrow / wide (HIPANN_IVF_WIDE=0 disables the wide items), else 32
-    g, w, gm = (half_scan_groups(d, int(os.environ.get("HIPANN_IVF_WIDE", "2")), os.environ.get("HIPANN_IVF_GEMM", "1") != "0")
+    g, w, gm = (half_scan_groups(d, int(os.environ.get("HIPANN_IVF_WIDE", "2")), os.environ.get("HIPANN_IVF_GEMM", "0") != "0")
                 if index.form == 6 else (32, 0, 0))
     return {"scan_bytes_per_batch_local": scan_bytes(index, probes, d, row_bytes),
             "fp32_rows_bytes_per_batch_local": scan_bytes(index, probes, d),

@@ -964,11 +964,14 @@ inline int mh_wide_mode() {
     return mode;
 }
 // GEMM items (lists probed by more queries than a wide item holds): up to MG_Q queries, database rows and queries both
-// staged through LDS by LDS-DMA (mg_item below); HIPANN_IVF_GEMM=0 (A/B): wide items for every list above the narrow
-// size
+// staged through LDS by LDS-DMA (mg_item below).  HIPANN_IVF_GEMM=1 (A/B) enables them; off by default: measured
+// slower, same box, alternating (tools/gpu_r06_gemm.sh, profiles/r06/ivf_gemm_items_ab_r06.txt) — the SURVEY mixture's
+// scan 5.17 → 8.32 ms at nprobe 16, intrinsic dimension 32 at nprobe 128 185K → 112K QPS.  The item streams its rows
+// with too little in flight: vector-memory loads retire in issue order, so the rows (HBM) and the query slices (L2)
+// share one lead, and four 24 KiB stages keep only 24 KiB of rows in flight per CU against the wide items' 96 KiB.
 constexpr int MG_Q = 256;
 inline bool mg_enabled() {
-    static const bool on = [] { const char *e = std::getenv("HIPANN_IVF_GEMM"); return !e || std::atoi(e); }();
+    static const bool on = [] { const char *e = std::getenv("HIPANN_IVF_GEMM"); return e && std::atoi(e); }();
     return on;
 }
 // the packed group of the plan and the scan (narrow | wide << 8 | GEMM << 16: ivf_ngroups, common.hpp)

@@ -220,7 +220,7 @@ def scan_pairs(index, probes: np.ndarray) -> int:
     return int(sizes[p].sum())
 
 
-def half_scan_groups(d: int, mode: int = 2, gemm: bool = True) -> tuple:
+def half_scan_groups(d: int, mode: int = 2, gemm: bool = False) -> tuple:
     """(narrow, wide, gemm) query-group sizes of the fp16 form's scan (ivf_mfma.hip mh_group / mh_group_wide /
     mh_group_packed: the queries' LDS image, two fp16 terms or the high term only, in 160 KiB; GEMM items of 256) for
     HIPANN_IVF_WIDE = mode (2 default: every list at least wide, narrow 0; 1: wide above the narrow size; 0: no wide

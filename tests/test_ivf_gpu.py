@@ -113,10 +113,11 @@ def test_ivf_mfma_query_tiles(gpu, oracle, nq, d, metric, form):
 @pytest.mark.parametrize("k", [10, 20])
 def test_ivf_half_wide_items(gpu, oracle, nq, d, metric, k):
     """The fp16 form's one-term items (ivf_mfma.hip): every list's queries enter on their high fp16 term, in wide
-    items of up to 96 queries (48 at d = 1536) — one item of 17-96 queries (2-6 query tiles) — and, for a list probed
-    by more than that, GEMM items of up to 256 (rows and queries staged by LDS-DMA): one of 97-256 queries, two of
-    128/129, three of 171 (513), ragged last query tiles; k = 20 takes the sub-list slots.  The rerank bounds those
-    queries with their one-term residual, so the ids still equal the oracle's."""
+    items of up to 96 queries (48 at d = 1536): one item of 17-96 queries (2-6 query tiles), two of 48/49 or 128/129,
+    three or more, ragged last query tiles; k = 20 takes the sub-list slots.  Run with HIPANN_IVF_GEMM=1 (A/B,
+    tools/gpu_r06_gemm.sh) a list probed by more than 96 queries takes GEMM items of up to 256 instead (one of 97-256
+    queries, two of 128/129, three of 171 at 513).  The rerank bounds those queries with their one-term residual, so
+    the ids still equal the oracle's."""
     xb, xq = faiss_metal_case(4500 if d < 1000 else 2500, nq, d)
     cen = np.ascontiguousarray(xb[:2])
     off = np.array([0, 2100, len(xb)], np.int64)  # two lists, both probed by every query: 2 row chunks, ragged
