@@ -421,13 +421,26 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     {
         RoctxRange rr("hipann.ivf.scan");
         ScopedTiming t(ix.timer_main, st);
-        if (half)
+        if (half) {
+            // per 64-pass chunk key the latest item's round (HIPANN_IVF_FOLLOW=0, A/B: every item from round 0); the
+            // words carry the batch number, so a stale word is ignored and the buffer is zeroed only when allocated
+            static const bool follow = [] { const char *e = std::getenv("HIPANN_IVF_FOLLOW"); return !e || std::atoi(e); }();
+            int nprog = 0;
+            if (follow) {
+                nprog = (int)std::min<int64_t>(1 << 20, (sh.h_off[nlist] / 32 + nlist) / 64 + 2);
+                if (!sh.prog.p || sh.prog.bytes < sizeof(unsigned) * (size_t)nprog) {
+                    sh.prog.ensure(sizeof(unsigned) * (size_t)nprog, sh.device);
+                    HIPANN_CHECK(hipMemsetAsync(sh.prog.p, 0, sh.prog.bytes, st));
+                }
+            }
             launch_ivf_scan_mfma_h(xq, nq, sh.hsplit.p, sh.hits.get<float>(), sh.hres.get<float>(), sh.half_es, qn, d,
                                    metric, sh.codes_h.p, sh.tpass_off.get<int64_t>(), sh.xnorm.get<float>(),
                                    sh.list_off.get<int64_t>(), sh.list_len.get<int>(), sh.cnt.get<int>(), sh.bucket_off.get<int>(),
                                    sh.item_off.get<int>(), sh.bucket.get<int>(), sh.slot_off.get<int>(), nlist, np, k,
                                    max_items, qbound, sh.part_d.get<float>(), sh.part_i.get<int>(), st, true,
-                                   sub ? 1 : 0);
+                                   sub ? 1 : 0, follow ? sh.prog.get<unsigned>() : nullptr, nprog,
+                                   (unsigned)(sh.plan_batch + 1));
+        }
         else if (bigk)
             launch_ivf_scan_bigk(xq, d, metric, sh.codes, sh.list_off.get<int64_t>(), sh.list_len.get<int>(),
                                  sh.coarse_i.get<int64_t>(),

@@ -930,6 +930,9 @@ typedef _Float16 mh_f16x8 __attribute__((ext_vector_type(8)));
 #ifndef HIPANN_MH_P
 #define HIPANN_MH_P 6
 #endif
+#ifndef HIPANN_MH_FOLLOW
+#define HIPANN_MH_FOLLOW 1  // items start at the round another group of their chunk last published (0: compiled out)
+#endif
 #ifndef HIPANN_MH_EARLY
 #define HIPANN_MH_EARLY 1  // issue the item's first row loads before waiting for its query fill (0: fill, barrier, loads)
 #endif
@@ -1282,13 +1285,28 @@ __device__ __forceinline__ void mh_item(int d, const uint4 *__restrict__ codes_h
                                         const int *__restrict__ bucket, int boff, int nprobe,
                                         const int *__restrict__ slot_off, int chunk, int k, int sub, float *smem,
                                         unsigned *__restrict__ qbound, float *__restrict__ part_d,
-                                        int *__restrict__ part_i) {
+                                        int *__restrict__ part_i, unsigned *prog, unsigned epoch) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int m = lane & 15, g = lane >> 4;
     const int nsup = mh_nsup(d);
     const int npass_all = (int)ceil_div(r1 - r0, MF_PASS);
     const int npass = npass_all > wave ? (npass_all - wave + MF_WAVES - 1) / MF_WAVES : 0;
+    // Round rotation (prog): the query groups of one chunk run as consecutive items on one XCD, each streaming the
+    // whole chunk; an item that starts while another group of the chunk is under way begins at the round (8 passes)
+    // that item last published and wraps around, so both read the same rows at about the same time and the later
+    // one's reads hit the XCD's L2.  The slot's k-list does not depend on the order its rows are seen.
+    int rr0 = 0;
+    if (HIPANN_MH_FOLLOW && prog && npass > 0) {
+        const unsigned w = (unsigned)__builtin_amdgcn_readfirstlane(
+            (int)__hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if ((w >> 8) == (epoch & 0xffffffu)) rr0 = (int)(w & 0xffu) % npass;
+    }
+    auto rot = [&](int i) {  // i < npass
+        if constexpr (!HIPANN_MH_FOLLOW) return i;
+        const int r = i + rr0;
+        return r < npass ? r : r - npass;
+    };
 
     // per query: the sorted list (key, row) and the admission gate = the key of its k-th entry (a 16-row batch
     // merges when some lane's key is ≤ the gate: a superset of the lexicographic test, the merge itself is exact)
@@ -1304,13 +1322,13 @@ __device__ __forceinline__ void mh_item(int d, const uint4 *__restrict__ codes_h
         }
 
     auto row_of = [&](int i, int r) -> int64_t {
-        const int64_t row = r0 + (int64_t)(wave + MF_WAVES * i) * MF_PASS + 16 * r + m;
+        const int64_t row = r0 + (int64_t)(wave + MF_WAVES * rot(i)) * MF_PASS + 16 * r + m;
         return row < r1 ? row : r1 - 1;
     };
     const int ilast = npass > 0 ? npass - 1 : 0;
     const uint4 *rp;
     int ld_i = 0, ld_s = 0;  // stream position (super-steps), wave-uniform
-    auto set_pass = [&](int i) { rp = codes_h + ((tp0 + wave + MF_WAVES * i) * nsup) * (MF_RT * 64) + lane; };
+    auto set_pass = [&](int i) { rp = codes_h + ((tp0 + wave + MF_WAVES * rot(i)) * nsup) * (MF_RT * 64) + lane; };
     // unconditional loads (past the wave's last step they re-read it): see mf_item
     auto next_load = [&](uint4 (&dst)[MF_RT]) {
         const int s = ld_i <= ilast ? ld_s : nsup - 1;
@@ -1379,7 +1397,11 @@ __device__ __forceinline__ void mh_item(int d, const uint4 *__restrict__ codes_h
                 next_load(ring[p]);
             }
         }
-        const int64_t prow0 = r0 + (int64_t)(wave + MF_WAVES * i) * MF_PASS;
+        const int64_t prow0 = r0 + (int64_t)(wave + MF_WAVES * rot(i)) * MF_PASS;
+        // publish the round this item reaches next (wave 0; a later group of the chunk starts there)
+        if (HIPANN_MH_FOLLOW && prog && wave == 0 && lane == 0)
+            __hip_atomic_store(prog, (epoch << 8) | (unsigned)((rot(i) + 1) % npass), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
         for (int r = 0; r < MF_RT; ++r) {
             const int64_t row = prow0 + 16 * r + m;
@@ -1647,7 +1669,8 @@ ivf_scan_mfma_h(const uint4 *__restrict__ qsplit, const float *__restrict__ qnor
                 const int64_t *__restrict__ list_off, const int *__restrict__ list_len, const int *__restrict__ cnt, const int *__restrict__ bucket_off,
                 const int *__restrict__ item_off, const int *__restrict__ bucket, const int *__restrict__ slot_off,
                 int nlist, int nprobe, int group, int k, int sub, unsigned *__restrict__ qbound, float *__restrict__ part_d,
-                int *__restrict__ part_i, float *__restrict__ qres, int nq, int remap) {
+                int *__restrict__ part_i, float *__restrict__ qres, int nq, int remap, unsigned *__restrict__ prog,
+                int nprog, unsigned epoch) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int total = item_off[nlist];
     if ((int)blockIdx.x >= total) return;
@@ -1706,8 +1729,9 @@ ivf_scan_mfma_h(const uint4 *__restrict__ qsplit, const float *__restrict__ qnor
 
     const int lane = threadIdx.x & 63, g = lane >> 4;
     const int64_t tp0 = tpass_off[l] + (int64_t)chunk * (MF_CH / MF_PASS);
+    unsigned *pw = prog && nprog > 0 ? prog + (int)((tp0 >> 6) % nprog) : nullptr;  // the chunk's progress word
 #define MH_ARGS d, codes_h, tp0, xn, r0, r1, nqi, qs, stride, qn, qi_s, qb, qpar, bucket, boff, nprobe, slot_off, chunk, k, sub, smem, \
-                qbound, part_d, part_i
+                qbound, part_d, part_i, pw, epoch
 #define MH_QN(QTV)                                                                                          \
     float qn[QTV][4], qi_s[QTV][4];                                                                         \
     unsigned qb[QTV][4];                                                                                    \
@@ -1797,7 +1821,7 @@ void launch_ivf_scan_mfma_h(const float *Q, int64_t nq, void *qsplit, float *its
                             const int64_t *list_off, const int *list_len, const int *cnt, const int *bucket_off,
                             const int *item_off, const int *bucket, const int *slot_off, int nlist, int nprobe, int k,
                             int64_t max_items, unsigned *qbound, float *pd, int *pi, hipStream_t st, bool split_done,
-                            int sub) {
+                            int sub, unsigned *prog, int nprog, unsigned epoch) {
     if (max_items <= 0 || nq <= 0) return;
     HIPANN_REQUIRE(max_items < (int64_t)0x7fffffff, "too many IVF work items");
     HIPANN_REQUIRE(qsplit && its && qres && codes_h, "fp16 IVF scan: missing buffers");
@@ -1821,7 +1845,7 @@ void launch_ivf_scan_mfma_h(const float *Q, int64_t nq, void *qsplit, float *its
     // contiguous runs per XCD
     static const int remap = [] { const char *e = std::getenv("HIPANN_IVF_REMAP"); return !e || std::atoi(e) ? 1 : 0; }();
 #define MH_LAUNCH_ARGS qs, qn, its, d, ch, tpass_off, xn, list_off, list_len, cnt, bucket_off, item_off, bucket, slot_off, nlist, nprobe, \
-                       group, k, sub, qbound, pd, pi, qres, (int)nq, remap
+                       group, k, sub, qbound, pd, pi, qres, (int)nq, remap, prog, nprog, epoch
     if (metric == kIP) hipLaunchKernelGGL((ivf_scan_mfma_h<true>), grid, block, smem, st, MH_LAUNCH_ARGS);
     else hipLaunchKernelGGL((ivf_scan_mfma_h<false>), grid, block, smem, st, MH_LAUNCH_ARGS);
 #undef MH_LAUNCH_ARGS

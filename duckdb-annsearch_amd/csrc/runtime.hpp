@@ -421,6 +421,7 @@ struct IvfShard {
     int half_state = 0, half_es = 0;
     float half_rxmax = 0.f;
     DevBuf codes_h, hsplit, hits, hres;
+    DevBuf prog;  // fp16 scan: per 64-pass chunk key, the latest item's position (rounds) and the batch it belongs to
     // an append's staging (hipann_ivf_add): the new rows grouped by list, labels, physical destinations, norms,
     // the tiled passes they touch, and the new rows' maxima (‖x‖², |x|, fp16 residual²)
     DevBuf app_rows, app_norm, app_assign, app_up, app_stat;
@@ -549,7 +550,7 @@ void launch_ivf_scan_mfma_h(const float *Q, int64_t nq, void *qsplit, float *its
                             const int64_t *list_off, const int *list_len, const int *cnt, const int *bucket_off, const int *item_off,
                             const int *bucket, const int *slot_off, int nlist, int nprobe, int k, int64_t max_items,
                             unsigned *qbound, float *pd, int *pi, hipStream_t st, bool split_done = false,
-                            int sub = 0);
+                            int sub = 0, unsigned *prog = nullptr, int nprog = 0, unsigned epoch = 0);
 // the batch's fp16 query terms (+ 1/(t·s), split residuals) and, when qn != nullptr, ‖q‖² (row_norms_f32's bits)
 void launch_ivf_split_queries_h(const float *Q, int64_t nq, int d, int es, void *qsplit, float *its, float *qres,
                                 float *qn, hipStream_t st);
