@@ -1285,7 +1285,7 @@ __device__ __forceinline__ void mh_item(int d, const uint4 *__restrict__ codes_h
                                         const int *__restrict__ bucket, int boff, int nprobe,
                                         const int *__restrict__ slot_off, int chunk, int k, int sub, float *smem,
                                         unsigned *__restrict__ qbound, float *__restrict__ part_d,
-                                        int *__restrict__ part_i, unsigned *prog, unsigned epoch) {
+                                        int *__restrict__ part_i, unsigned *prog, unsigned epoch, unsigned pword) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int m = lane & 15, g = lane >> 4;
@@ -1296,12 +1296,8 @@ __device__ __forceinline__ void mh_item(int d, const uint4 *__restrict__ codes_h
     // whole chunk; an item that starts while another group of the chunk is under way begins at the round (8 passes)
     // that item last published and wraps around, so both read the same rows at about the same time and the later
     // one's reads hit the XCD's L2.  The slot's k-list does not depend on the order its rows are seen.
-    int rr0 = 0;
-    if (HIPANN_MH_FOLLOW && prog && npass > 0) {
-        const unsigned w = (unsigned)__builtin_amdgcn_readfirstlane(
-            (int)__hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        if ((w >> 8) == (epoch & 0xffffffu)) rr0 = (int)(w & 0xffu) % npass;
-    }
+    int rr0 = 0;  // (pword: the chunk's progress word, loaded by the kernel ahead of the query fill)
+    if (HIPANN_MH_FOLLOW && prog && npass > 0 && (pword >> 8) == (epoch & 0xffffffu)) rr0 = (int)(pword & 0xffu) % npass;
     auto rot = [&](int i) {  // i < npass
         if constexpr (!HIPANN_MH_FOLLOW) return i;
         const int r = i + rr0;
@@ -1709,6 +1705,12 @@ ivf_scan_mfma_h(const uint4 *__restrict__ qsplit, const float *__restrict__ qnor
                     reinterpret_cast<uint64_t *>(reinterpret_cast<char *>(smem) + MG_SCR), qbound, part_d, part_i);
         return;
     }
+    // the chunk's progress word, loaded before the query fill so that its latency hides behind it
+    const int64_t tp0 = tpass_off[l] + (int64_t)chunk * (MF_CH / MF_PASS);
+    unsigned *pw = HIPANN_MH_FOLLOW && prog && nprog > 0 ? prog + (int)((tp0 >> 6) % nprog) : nullptr;
+    const unsigned pword = pw ? (unsigned)__builtin_amdgcn_readfirstlane(
+                                    (int)__hip_atomic_load(pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                              : 0u;
     unsigned *qs = reinterpret_cast<unsigned *>(smem);
     const int nsup = mh_nsup(d);
     const int stride = mh_stride(d, wide ? 1 : 2);
@@ -1728,10 +1730,8 @@ ivf_scan_mfma_h(const uint4 *__restrict__ qsplit, const float *__restrict__ qnor
     if (!HIPANN_MH_EARLY) __syncthreads();  // (early: mh_item waits for the fill after issuing its first row loads)
 
     const int lane = threadIdx.x & 63, g = lane >> 4;
-    const int64_t tp0 = tpass_off[l] + (int64_t)chunk * (MF_CH / MF_PASS);
-    unsigned *pw = prog && nprog > 0 ? prog + (int)((tp0 >> 6) % nprog) : nullptr;  // the chunk's progress word
 #define MH_ARGS d, codes_h, tp0, xn, r0, r1, nqi, qs, stride, qn, qi_s, qb, qpar, bucket, boff, nprobe, slot_off, chunk, k, sub, smem, \
-                qbound, part_d, part_i, pw, epoch
+                qbound, part_d, part_i, pw, epoch, pword
 #define MH_QN(QTV)                                                                                          \
     float qn[QTV][4], qi_s[QTV][4];                                                                         \
     unsigned qb[QTV][4];                                                                                    \
