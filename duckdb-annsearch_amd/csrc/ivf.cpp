@@ -422,9 +422,10 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
         RoctxRange rr("hipann.ivf.scan");
         ScopedTiming t(ix.timer_main, st);
         if (half) {
-            // per 64-pass chunk key the latest item's round (HIPANN_IVF_FOLLOW=0, A/B: every item from round 0); the
+            // per 64-pass chunk key the latest item's round (HIPANN_IVF_FOLLOW=1 with a HIPANN_MH_FOLLOW=1 build, A/B
+            // only: measured no better, ivf_mfma.hip); the
             // words carry the batch number, so a stale word is ignored and the buffer is zeroed only when allocated
-            static const bool follow = [] { const char *e = std::getenv("HIPANN_IVF_FOLLOW"); return !e || std::atoi(e); }();
+            static const bool follow = [] { const char *e = std::getenv("HIPANN_IVF_FOLLOW"); return e && std::atoi(e); }();
             int nprog = 0;
             if (follow) {
                 nprog = (int)std::min<int64_t>(1 << 20, (sh.h_off[nlist] / 32 + nlist) / 64 + 2);

@@ -931,7 +931,11 @@ typedef _Float16 mh_f16x8 __attribute__((ext_vector_type(8)));
 #define HIPANN_MH_P 6
 #endif
 #ifndef HIPANN_MH_FOLLOW
-#define HIPANN_MH_FOLLOW 1  // items start at the round another group of their chunk last published (0: compiled out)
+// 1 (tuning builds, with HIPANN_IVF_FOLLOW=1): items start at the round another query group of their chunk last
+// published.  Measured and left out: same box, alternating (tools/gpu_r06_follow.sh, profiles/r06/
+// ivf_follow_ab_r06.txt) the SURVEY mixture's scan 5.14 / 5.25 ms against 5.23 / 5.24 (runtime off) and 5.18 / 5.20
+// (compiled out) — within the noise; the rotation's scalar registers spill to VGPR lanes for nothing
+#define HIPANN_MH_FOLLOW 0
 #endif
 #ifndef HIPANN_MH_EARLY
 #define HIPANN_MH_EARLY 1  // issue the item's first row loads before waiting for its query fill (0: fill, barrier, loads)
