@@ -702,16 +702,25 @@ IVF_FORMS = {0: ("ivf_scan_mfma", "decomposed, fp32 MFMA"), 1: ("ivf_scan_topk",
              6: ("ivf_scan_mfma_h", "fp16 MFMA scan over a tiled fp16 image of the rows (2 B per element, "
                                     "2-term fp16 queries) as a filter (16 per list) + exact fp32 direct-form "
                                     "rerank, bound-checked with the measured fp16 residuals (merge_ms includes "
-                                    "the rerank)")}
+                                    "the rerank)"),
+             7: ("ivf_scan_mfma_h", "int8 MFMA scan over a tiled int8 image of the rows (1 B per element + a "
+                                    "per-row scale, int8 queries, exact int32 sums) as a filter (per-wave sub-lists, "
+                                    "64 reranked) + exact fp32 direct-form rerank, bound-checked with the measured "
+                                    "int8 residuals (merge_ms includes the rerank)")}
 
 
 def ivf_row_bytes(form, d, metric):
     """HBM bytes one scanned row costs the form's list-scan kernel: the fp16 image (2d) + the row norm
-    (L2) for form 6; SURVEY §8d's fp32 codes + label (4d + 8) for the fp32-row forms."""
+    (L2) for form 6; the int8 image (d) + row scale + norm (L2) for form 7; SURVEY §8d's fp32 codes + label (4d + 8)
+    for the fp32-row forms."""
+    if form == 7:
+        return d + 4 + (4 if metric == 0 else 0)
     return 2 * d + (4 if metric == 0 else 0) if form == 6 else 4 * d + 8
 
 
 def ivf_row_bytes_desc(form):
+    if form == 7:
+        return "|l|*(d+8) (int8 image + row scale + L2 row norm)"
     return "|l|*(2d+4) (fp16 image + L2 row norm)" if form == 6 else "|l|*(4d+8)"
 
 
@@ -742,12 +751,12 @@ def build_ivf(args, torch, hipann, rank, world, dev, n, d, nlist, nprobe, metric
 
 
 def ivf_scan_stats(index, probes, d, nlist, row_bytes=None):
-    from ivf_build import half_scan_groups, scan_bytes, scan_group_rows, scan_pairs
+    from ivf_build import half_scan_groups, i8_scan_groups, scan_bytes, scan_group_rows, scan_pairs
 
     cnt = np.bincount(probes[probes >= 0].ravel(), minlength=nlist)
     # the form's query groups: fp16 form (6) narrow / wide (HIPANN_IVF_WIDE=0 disables the wide items), else 32
     g, w, gm = (half_scan_groups(d, int(os.environ.get("HIPANN_IVF_WIDE", "2")), os.environ.get("HIPANN_IVF_GEMM", "0") != "0")
-                if index.form == 6 else (32, 0, 0))
+                if index.form == 6 else i8_scan_groups(d) if index.form == 7 else (32, 0, 0))
     return {"scan_bytes_per_batch_local": scan_bytes(index, probes, d, row_bytes),
             "fp32_rows_bytes_per_batch_local": scan_bytes(index, probes, d),
             "distinct_lists_probed": int(np.unique(probes[probes >= 0]).size),
@@ -1650,6 +1659,7 @@ def main():
             sub, index = ivf_config(args, torch, dist, hipann, rank, world, dev, args.steps, args.warmup,
                                     suite_extras=args.suite and world == 1)
             dtype = ("f32 results (fp16-image certified filter + exact fp32 rerank)" if index.form == 6 else
+                     "f32 results (int8-image certified filter, int32 sums + exact fp32 rerank)" if index.form == 7 else
                      "f32 results (bf16-split certified filter + exact fp32 rerank)" if index.form == 5 else "f32")
             data = "low-intrinsic-dimension gaussian rows (DESIGN.md §8)"
         line = {"metric": METRIC, "value": sub.pop("value"), "unit": "queries/s", "n_gpus": world,

@@ -61,7 +61,10 @@ enum IvfForm : int {
     kFormSplit3 = 3,
     kFormSplit2 = 4,
     kFormSplit2Exact = 5,
-    kFormHalfExact = 6
+    kFormHalfExact = 6,
+    // kFormI8Exact (opt-in): the same filter + rerank over a tiled int8 image with one scale per row (a quarter of the
+    // fp32 rows' bytes), sub-lists always, the rerank certified with the int8 residuals
+    kFormI8Exact = 7
 };
 constexpr int kRerankK = 16, kRerankMaxK = 12;
 // request_k in (kRerankMaxK, kIvfSubMaxK] on the IVF exact forms: sub-list slots (one 16-list per scan wave) and a

@@ -183,6 +183,34 @@ bool ensure_half_codes(IvfShard &sh, int d, int nlist, hipStream_t st) {
     return true;
 }
 
+// kFormI8Exact: the tiled int8 image (one scale per row, ivf_mfma.hip) and its largest row residual, built at the
+// first search that needs them (and again after an append: appends release it)
+bool ensure_i8_codes(IvfShard &sh, int d, int nlist, hipStream_t st) {
+    if (sh.i8_state != 0) return sh.i8_state > 0;
+    if (sh.n == 0) return false;
+    const int64_t np = ensure_tpass(sh, nlist, st);
+    sh.codes_i8.ensure((size_t)std::max<int64_t>(np, 1) * (size_t)ivf_i8_pass_bytes(d), sh.device);
+    sh.xs8.ensure(sizeof(float) * (size_t)sh.n, sh.device);
+    launch_ivf_tile_i8(sh.codes, sh.list_off.get<int64_t>(), sh.list_len.get<int>(), sh.tpass_off.get<int64_t>(), nlist, np,
+                       d, sh.codes_i8.p, sh.xs8.get<float>(), st);
+    sh.nflag.ensure(sizeof(int), sh.device);
+    launch_ivf_i8_residual(sh.codes, sh.n, d, sh.nflag.get<unsigned>(), st);
+    unsigned bits = 0;
+    HIPANN_CHECK(hipMemcpyAsync(&bits, sh.nflag.p, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    HIPANN_CHECK(hipStreamSynchronize(st));
+    float r2;
+    std::memcpy(&r2, &bits, sizeof(r2));
+    if (bits >= 0x7f800000u) {  // a non-finite row: the form does not apply (kFormSplit2Exact runs), as the fp16 image
+        sh.i8_state = -1;
+        sh.codes_i8.release();
+        sh.xs8.release();
+        return false;
+    }
+    sh.i8_rxmax = std::sqrt(r2) * 1.0001f;
+    sh.i8_state = 1;
+    return true;
+}
+
 // ‖x‖² of every stored row (L2 only): the decomposed scan form reads it with the codes
 // (faiss-metal stores the same norms with its lists, MetalIndexIVFFlat.mm:313-318).
 void compute_row_norms(IvfShard &sh, int d, int metric) {
@@ -288,15 +316,21 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     // their 16-lane lists but write every wave's list as a sub-list of the slot (mf_finish_item), and the rerank
     // takes the kf best candidates, certified against its kf-th merged key AND the smallest full sub-list's
     // 16th key (every pruned row lies above both).  Beyond kIvfSubMaxK: the 3-term scan.
-    const bool sub_req = (req == kFormHalfExact || req == kFormSplit2Exact) && kout > kRerankMaxK &&
-                         kout <= kIvfSubMaxK && !bigk;
-    // kFormHalfExact: the fp16-image scan as the filter of the same rerank (else kFormSplit2Exact)
-    bool half = false;
+    // kFormI8Exact always takes the sub-lists (its int8 filter needs the 64-deep rerank, ivf_mfma.hip)
+    const bool sub_req = (((req == kFormHalfExact || req == kFormSplit2Exact) && kout > kRerankMaxK) ||
+                          req == kFormI8Exact) && kout <= kIvfSubMaxK && !bigk;
+    // kFormHalfExact: the fp16-image scan as the filter of the same rerank (else kFormSplit2Exact); kFormI8Exact: the
+    // int8-image scan (else kFormSplit2Exact too)
+    bool half = false, i8 = false;
     if (req == kFormHalfExact) {
         half = (kout <= kRerankMaxK || sub_req) && !bigk && ivf_mfma_h_supported(d, kRerankK) &&
                ensure_half_codes(sh, d, nlist, st);
         req = kFormSplit2Exact;
+    } else if (req == kFormI8Exact) {
+        i8 = sub_req && ivf_mfma_i8_supported(d, kRerankK) && ensure_i8_codes(sh, d, nlist, st);
+        req = kFormSplit2Exact;
     }
+    const bool img = half || i8;  // a tiled fp16 / int8 image and the one-term (or two-term) item scan
     // kFormSplit2Exact: the 2-term scan keeps kRerankK per list (per wave with sub-lists), the rerank makes the
     // results exact
     const bool want_exact = req == kFormSplit2Exact;
@@ -304,8 +338,8 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     const int k_user = k;
     const int kscan = want_exact && req == kFormSplit2 ? kRerankK : k;
     int form = req != kFormDirect && !bigk && ivf_dot_supported(xq, d, sh.codes) ? req : kFormDirect;
-    if (half) form = kFormSplit2;  // any d: the fp16 image is zero-padded to whole super-steps
-    if (!half && ivf_form_split(form) && !ivf_mfma_bf_supported(xq, d, sh.codes, kscan, ivf_form_terms(form)))
+    if (img) form = kFormSplit2;  // any d: the images are zero-padded to whole super-steps
+    if (!img && ivf_form_split(form) && !ivf_mfma_bf_supported(xq, d, sh.codes, kscan, ivf_form_terms(form)))
         form = kFormDecomposed;
     if (form == kFormDecomposed && !ivf_mfma_supported(xq, d, sh.codes, kscan)) form = kFormDecomposedValu;
     const bool exact = want_exact && form == kFormSplit2;
@@ -313,14 +347,14 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     k = kscan;  // per-list k of the scan (the output keeps kout)
     // entries per (query, probe, chunk) slot, and the rerank's filter depth
     const int kslot = sub ? ivf_scan_sublists() * k : k;
-    const int kfilt = sub ? std::min(64, std::max(kout + 4, 2 * kout)) : k;
+    const int kfilt = sub ? (i8 ? 64 : std::min(64, std::max(kout + 4, 2 * kout))) : k;
     if (form_override < 0) {
-        ix.last_form = exact ? (half ? kFormHalfExact : kFormSplit2Exact) : form;
+        ix.last_form = exact ? (i8 ? kFormI8Exact : half ? kFormHalfExact : kFormSplit2Exact) : form;
         ix.last_kfilt = exact ? kfilt : 0;
         ix.last_sublists = sub ? ivf_scan_sublists() : 0;
     }
     const bool tiled = form == kFormDecomposed || ivf_form_split(form);  // the matrix-core scans
-    const int group = half ? ivf_mfma_h_group(d) : ivf_group_size(form, d);
+    const int group = i8 ? ivf_mfma_i8_group(d) : half ? ivf_mfma_h_group(d) : ivf_group_size(form, d);
     float xmax2 = 0.f;
     if (exact) {  // max‖x‖² (once per row set; nflag is its scratch, so before the plan resets the flag count)
         xmax2 = shard_xmax2(sh, d, st);
@@ -347,6 +381,21 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
         RoctxRange rr("hipann.ivf.prepare");
         launch_ivf_split_queries_h(xq, nq, d, sh.half_es, sh.hsplit.p, sh.hits.get<float>(), sh.hres.get<float>(), qn_out,
                                    st);
+        qsh0.qn_given = qn_out ? xq : nullptr;
+        qsh0.qn_given_nq = nq;
+    } else if (i8) {
+        // the int8 queries (units, scales, residuals) and ‖q‖² (row_norms_f32 itself: the coarse step's bits)
+        sh.qi8.ensure((size_t)ivf_i8_qimg_bytes(nq, d), sh.device);
+        sh.qs8.ensure(sizeof(float) * (size_t)nq, sh.device);
+        sh.qres8.ensure(sizeof(float) * (size_t)nq, sh.device);
+        float *qn_out = nullptr;
+        if (metric == kL2) {
+            qsh0.qn.ensure(sizeof(float) * (size_t)nq, sh.device);
+            qn_out = qsh0.qn.get<float>();
+            launch_row_norms(xq, nq, d, qn_out, st);
+        }
+        RoctxRange rr("hipann.ivf.prepare");
+        launch_ivf_split_queries_i8(xq, nq, d, sh.qi8.p, sh.qs8.get<float>(), sh.qres8.get<float>(), st);
         qsh0.qn_given = qn_out ? xq : nullptr;
         qsh0.qn_given_nq = nq;
     }
@@ -400,7 +449,7 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     const float *qn = nullptr;
     if (form != kFormDirect && metric == kL2) {
         const FlatShard &qs = *sh.quant->shards[0];
-        if (probes_in && half) {
+        if (probes_in && img) {
             qn = qsh0.qn.get<float>();  // the query preparation wrote ‖q‖² there (row_norms_f32's bits)
         } else if (!probes_in && qs.qn_of == xq && qs.qn_nq == nq) {
             // the coarse quantizer's ‖q‖² of the same queries, written by THIS call's coarse step (with probes_in
@@ -412,8 +461,8 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
             qn = sh.qn.get<float>();
         }
     }
-    if (tiled && !half) ensure_tiled_codes(sh, d, nlist, st);
-    if (half) {
+    if (tiled && !img) ensure_tiled_codes(sh, d, nlist, st);
+    if (img) {
         // query terms prepared before the coarse step
     } else if (ivf_form_split(form)) {
         sh.qsplit.ensure((size_t)ivf_mfma_bf_qsplit_bytes(nq, d, ivf_form_terms(form)), sh.device);
@@ -421,7 +470,7 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
     {
         RoctxRange rr("hipann.ivf.scan");
         ScopedTiming t(ix.timer_main, st);
-        if (half) {
+        if (img) {
             // per 64-pass chunk key the latest item's round (HIPANN_IVF_FOLLOW=1 with a HIPANN_MH_FOLLOW=1 build, A/B
             // only: measured no better, ivf_mfma.hip); the
             // words carry the batch number, so a stale word is ignored and the buffer is zeroed only when allocated
@@ -434,13 +483,15 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
                     HIPANN_CHECK(hipMemsetAsync(sh.prog.p, 0, sh.prog.bytes, st));
                 }
             }
-            launch_ivf_scan_mfma_h(xq, nq, sh.hsplit.p, sh.hits.get<float>(), sh.hres.get<float>(), sh.half_es, qn, d,
-                                   metric, sh.codes_h.p, sh.tpass_off.get<int64_t>(), sh.xnorm.get<float>(),
+            // (int8: its query units, scales and residuals in the fp16 form's slots)
+            launch_ivf_scan_mfma_h(xq, nq, i8 ? sh.qi8.p : sh.hsplit.p, i8 ? sh.qs8.get<float>() : sh.hits.get<float>(),
+                                   i8 ? sh.qres8.get<float>() : sh.hres.get<float>(), sh.half_es, qn, d,
+                                   metric, i8 ? sh.codes_i8.p : sh.codes_h.p, sh.tpass_off.get<int64_t>(), sh.xnorm.get<float>(),
                                    sh.list_off.get<int64_t>(), sh.list_len.get<int>(), sh.cnt.get<int>(), sh.bucket_off.get<int>(),
                                    sh.item_off.get<int>(), sh.bucket.get<int>(), sh.slot_off.get<int>(), nlist, np, k,
                                    max_items, qbound, sh.part_d.get<float>(), sh.part_i.get<int>(), st, true,
                                    sub ? 1 : 0, follow ? sh.prog.get<unsigned>() : nullptr, nprog,
-                                   (unsigned)(sh.plan_batch + 1));
+                                   (unsigned)(sh.plan_batch + 1), i8 ? 1 : 0, i8 ? sh.xs8.get<float>() : nullptr);
         }
         else if (bigk)
             launch_ivf_scan_bigk(xq, d, metric, sh.codes, sh.list_off.get<int64_t>(), sh.list_len.get<int>(),
@@ -504,9 +555,9 @@ void ivf_shard_search(IvfIndex &ix, IvfShard &sh, int64_t nq, const float *xq, i
         ScopedTiming t(ix.timer_merge, st);
         launch_ivf_rerank(sh.part_d.get<float>(), sh.part_i.get<int>(), sh.slot_off.get<int>(), np, nq, kfilt, kout,
                           metric, xq, sh.codes, d, sh.ids, sh.n, 0, xmax2, D, I, sh.nflag.get<int>(),
-                          sh.flagged.get<int>(), st, kSplit2Eps, half ? sh.half_rxmax : -1.f,
-                          half ? sh.hres.get<float>() : nullptr, sh.coarse_i.get<int64_t>(),
-                          sh.list_off.get<int64_t>(), nlist, qbound, half && metric == kL2 ? qn : nullptr, kslot,
+                          sh.flagged.get<int>(), st, kSplit2Eps, i8 ? sh.i8_rxmax : half ? sh.half_rxmax : -1.f,
+                          i8 ? sh.qres8.get<float>() : half ? sh.hres.get<float>() : nullptr, sh.coarse_i.get<int64_t>(),
+                          sh.list_off.get<int64_t>(), nlist, qbound, img && metric == kL2 ? qn : nullptr, kslot,
                           sub ? 1 : 0, inline_fb ? sh.list_len.get<int>() : nullptr,
                           inline_fb ? sh.fpd.get<float>() : nullptr, inline_fb ? sh.fpi.get<long long>() : nullptr,
                           inline_fb ? sh.fb_total.get<unsigned long long>() : nullptr, fb_cap);
@@ -628,6 +679,12 @@ static void ivf_add_rows(IvfIndex &ix, int64_t n, const float *xb, const int64_t
     // every shard's pending searches (possibly on other streams) finish before its buffers change
     std::vector<std::unique_ptr<FenceScope>> fences;
     for (auto &shp : ix.shards) fences.push_back(std::make_unique<FenceScope>(shp->fence, shp->stream, shp->device));
+    // the int8 image (kFormI8Exact, opt-in) is not maintained in place: released, rebuilt at its next search
+    for (auto &shp : ix.shards) {
+        shp->i8_state = 0;
+        shp->codes_i8.release();
+        shp->xs8.release();
+    }
     // FAISS assigns in blocks of 65536 rows (so the Flat nq < 20 direct-form rule applies per block); each block's
     // rows follow the previous block's in their lists (insertion order)
     const int64_t bs = 65536;
@@ -1211,7 +1268,7 @@ int hipann_ivf_set_nprobe(void *h, int nprobe) {
 }
 
 int hipann_ivf_set_form(void *h, int form) {
-    if (!h || form < kFormDecomposed || form > kFormHalfExact) return -1;
+    if (!h || form < kFormDecomposed || form > kFormI8Exact) return -1;
     auto *ix = static_cast<IndexBase *>(h);
     if (ix->kind != Kind::IVF) return -1;
     auto *vx = static_cast<IvfIndex *>(ix);

@@ -1005,6 +1005,123 @@ __device__ __forceinline__ mf_f32x4 mh_mfma(const uint4 &a, const uint4 &b, cons
                                                   0, 0, 0);
 }
 
+// ---- int8 image (form kFormI8Exact) -------------------------------------------------------------------------
+// The lists as a tiled int8 image with one scale per row (s = max|x| / 127, x̂ = clamp(rint(x / s), ±127): the Flat
+// form 5's quantizer, i8_quant) — a quarter of the fp32 rows' bytes, half the fp16 image's — scanned on
+// v_mfma_i32_16x16x64_i8 (exact int32 sums) against int8 queries (their own scale); key = ‖q‖² + ‖x‖² − 2·s_q·s_x·sum.
+// Same geometry as the fp16 image with 64-dim super-steps: [pass][S][row tile r][lane (g, m)][16 B] = row 16r + m,
+// dims 64S + 16g .. +15 (the queries' units use the same lane order, so the MFMA pairs equal k-slots whatever its
+// internal k mapping).  The filter is coarser (≈ 2⁻⁸ relative): the scan always keeps per-wave sub-lists and the
+// rerank takes 64 candidates, certified with the int8 residuals (max row ‖x − s·x̂‖, the query's own).
+typedef int mf_i32x4 __attribute__((ext_vector_type(4)));
+__host__ __device__ inline int mi_nsup(int d) { return (int)ceil_div(ceil_div(d, 64), MH_P) * MH_P; }
+__device__ __forceinline__ int mi_quant(float x, float s) {
+    return s > 0.f ? (int)fminf(fmaxf(rintf(x / s), -127.f), 127.f) : 0;
+}
+__device__ __forceinline__ uint4 mi_units(const float *x, int dim0, int d, float s) {  // 16 dims → 16 int8
+    unsigned w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int v = dim0 + i < d ? mi_quant(x[dim0 + i], s) : 0;
+        w[i >> 2] |= ((unsigned)v & 0xffu) << (8 * (i & 3));
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+// max|x| / 127 of a row (0 for a zero or non-finite row: its units are 0 and its residual +inf, see mi_resid)
+__device__ __forceinline__ float mi_row_scale(const float *x, int d, int lane) {
+    float mx = 0.f;
+    for (int e = lane; e < d; e += 64) mx = fmaxf(mx, fabsf(x[e]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    return mx > 0.f && mx < 3.0e38f ? mx / 127.f : (mx == 0.f ? 0.f : -1.f);
+}
+
+// one block per 32-row pass (list by binary search over the pass offsets, as ivf_tile_half): the rows' scales (into
+// xs8 at their CSR rows) and the pass's units; rows past the list's live length: zero units, scale 0
+__global__ void __launch_bounds__(256)
+ivf_tile_i8(const float *__restrict__ codes, const int64_t *__restrict__ list_off, const int *__restrict__ list_len,
+            const int64_t *__restrict__ tpass_off, int nlist, int d, int nsup, uint4 *__restrict__ dst,
+            float *__restrict__ xs8, const int64_t *__restrict__ pass_ids) {
+    const int64_t pass = pass_ids ? pass_ids[blockIdx.x] : (int64_t)blockIdx.x;
+    int lo = 0, hi = nlist - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (tpass_off[mid] <= pass) lo = mid; else hi = mid - 1;
+    }
+    const int l = lo;
+    const int64_t r0 = list_off[l] + (pass - tpass_off[l]) * 32, rend = list_off[l] + list_len[l];
+    __shared__ float sc[32];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int rr = wave; rr < 32; rr += 4) {
+        const int64_t row = r0 + rr;
+        float s = 0.f;
+        if (row < rend) {
+            s = mi_row_scale(codes + row * (int64_t)d, d, lane);
+            if (s < 0.f) s = 0.f;  // non-finite row: zero units (its residual is +inf: the rerank re-runs every query)
+        }
+        if (lane == 0) {
+            sc[rr] = s;
+            if (row < list_off[l + 1]) xs8[row] = s;
+        }
+    }
+    __syncthreads();
+    for (int u = threadIdx.x; u < nsup * MF_RT * 64; u += 256) {
+        const int S = u / (MF_RT * 64), rem = u - S * (MF_RT * 64), r = rem >> 6, ln = rem & 63;
+        const int rr = 16 * r + (ln & 15), g = ln >> 4;
+        const int64_t row = r0 + rr;
+        dst[(pass * nsup + S) * (MF_RT * 64) + rem] =
+            row < rend ? mi_units(codes + row * (int64_t)d, 64 * S + 16 * g, d, sc[rr]) : make_uint4(0u, 0u, 0u, 0u);
+    }
+}
+
+// max over rows of ‖x − s·x̂‖² (one wave per row; +inf for a non-finite row) as float bits
+__global__ void __launch_bounds__(256) ivf_i8_residual(const float *__restrict__ codes, int64_t n, int d,
+                                                       unsigned *__restrict__ out) {
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= n) return;
+    const int lane = threadIdx.x & 63;
+    const float *x = codes + row * (int64_t)d;
+    const float s = mi_row_scale(x, d, lane);
+    float r2 = 0.f;
+    if (s >= 0.f) {
+        for (int e = lane; e < d; e += 64) {
+            const float rr = x[e] - s * (float)mi_quant(x[e], s);
+            r2 = fmaf(rr, rr, r2);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) r2 += __shfl_xor(r2, o);
+    } else {
+        r2 = __builtin_inff();
+    }
+    if (lane == 0) atomicMax(out, __float_as_uint(r2));
+}
+
+// The batch's int8 queries, one wave per query: scale qs8 = max|q| / 127, residual qres8 = ‖q − qs8·q̂‖ (×1.0001; +inf
+// for a non-finite query: the rerank re-runs it) and the units [q][S][g] (zero past d)
+__global__ void __launch_bounds__(256) ivf_split_queries_i8(const float *__restrict__ Q, int64_t nq, int d, int nsup,
+                                                            uint4 *__restrict__ out, float *__restrict__ qs8,
+                                                            float *__restrict__ qres8) {
+    const int64_t q = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq) return;
+    const int lane = threadIdx.x & 63;
+    const float *x = Q + q * (int64_t)d;
+    float s = mi_row_scale(x, d, lane);
+    const bool fin = s >= 0.f;
+    if (!fin) s = 0.f;
+    float r2 = 0.f;
+    for (int e = lane; e < d; e += 64) {
+        const float rr = x[e] - s * (float)mi_quant(x[e], s);
+        r2 = fmaf(rr, rr, r2);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) r2 += __shfl_xor(r2, o);
+    if (lane == 0) {
+        qs8[q] = s;
+        qres8[q] = fin ? sqrtf(r2) * 1.0001f : __builtin_inff();
+    }
+    for (int u = lane; u < nsup * 4; u += 64) out[q * nsup * 4 + u] = mi_units(x, 64 * (u >> 2) + 16 * (u & 3), d, s);
+}
+
 // max |x| over cnt floats as the bits of the magnitude (unsigned order = magnitude order; any NaN
 // compares above +inf, so a non-finite table is detected by bits >= 0x7f800000)
 __global__ void __launch_bounds__(256) ivf_max_abs(const float *__restrict__ x, int64_t cnt, unsigned *__restrict__ out) {
@@ -1280,7 +1397,7 @@ __global__ void __launch_bounds__(256) ivf_split_queries_h(const float *__restri
     }
 }
 
-template <int QT, bool IP, int NT>
+template <int QT, bool IP, int NT, bool I8 = false>
 __device__ __forceinline__ void mh_item(int d, const uint4 *__restrict__ codes_h, int64_t tp0,
                                         const float *__restrict__ xn, int64_t r0, int64_t r1, int nqi,
                                         const unsigned *__restrict__ qs, int stride, const float (&qn)[QT][4],
@@ -1289,11 +1406,12 @@ __device__ __forceinline__ void mh_item(int d, const uint4 *__restrict__ codes_h
                                         const int *__restrict__ bucket, int boff, int nprobe,
                                         const int *__restrict__ slot_off, int chunk, int k, int sub, float *smem,
                                         unsigned *__restrict__ qbound, float *__restrict__ part_d,
-                                        int *__restrict__ part_i, unsigned *prog, unsigned epoch, unsigned pword) {
+                                        int *__restrict__ part_i, unsigned *prog, unsigned epoch, unsigned pword,
+                                        const float *__restrict__ xs8) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int m = lane & 15, g = lane >> 4;
-    const int nsup = mh_nsup(d);
+    const int nsup = I8 ? mi_nsup(d) : mh_nsup(d);  // (I8: 64-dim super-steps of the int8 image)
     const int npass_all = (int)ceil_div(r1 - r0, MF_PASS);
     const int npass = npass_all > wave ? (npass_all - wave + MF_WAVES - 1) / MF_WAVES : 0;
     // Round rotation (prog): the query groups of one chunk run as consecutive items on one XCD, each streaming the
@@ -1349,7 +1467,7 @@ __device__ __forceinline__ void mh_item(int d, const uint4 *__restrict__ codes_h
     };
 
     uint4 ring[MH_P][MF_RT];
-    float xnr[MF_RT] = {0.f, 0.f};
+    float xnr[MF_RT] = {0.f, 0.f}, xsr[MF_RT] = {0.f, 0.f};  // (I8: the rows' scales)
     if (npass > 0) {
         set_pass(0);
 #pragma unroll
@@ -1357,6 +1475,10 @@ __device__ __forceinline__ void mh_item(int d, const uint4 *__restrict__ codes_h
         if (!IP) {
 #pragma unroll
             for (int r = 0; r < MF_RT; ++r) xnr[r] = xn[row_of(0, r)];
+        }
+        if constexpr (I8) {
+#pragma unroll
+            for (int r = 0; r < MF_RT; ++r) xsr[r] = xs8[row_of(0, r)];
         }
     }
     // the item's query image (and the wide items' parameters) were written by every thread before the call: wait for
@@ -1368,15 +1490,23 @@ __device__ __forceinline__ void mh_item(int d, const uint4 *__restrict__ codes_h
     for (int qt = 0; qt < QT; ++qt) qrow[qt] = qs + (qt * 16 + m) * stride + 4 * g;
 
     mf_f32x4 acc[QT][MF_RT];
+    mf_i32x4 acci[QT][MF_RT];  // (I8: int32 sums)
     for (int i = 0; i < npass; ++i) {
 #pragma unroll
         for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
-            for (int r = 0; r < MF_RT; ++r) acc[qt][r] = mf_f32x4{0.f, 0.f, 0.f, 0.f};
-        float xnr_next[MF_RT] = {0.f, 0.f};
+            for (int r = 0; r < MF_RT; ++r) {
+                if constexpr (I8) acci[qt][r] = mf_i32x4{0, 0, 0, 0};
+                else acc[qt][r] = mf_f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+        float xnr_next[MF_RT] = {0.f, 0.f}, xsr_next[MF_RT] = {0.f, 0.f};
         if (!IP) {
 #pragma unroll
             for (int r = 0; r < MF_RT; ++r) xnr_next[r] = xn[row_of(i + 1 <= ilast ? i + 1 : ilast, r)];
+        }
+        if constexpr (I8) {
+#pragma unroll
+            for (int r = 0; r < MF_RT; ++r) xsr_next[r] = xs8[row_of(i + 1 <= ilast ? i + 1 : ilast, r)];
         }
         for (int S0 = 0; S0 < nsup; S0 += MH_P) {
 #pragma unroll
@@ -1393,7 +1523,13 @@ __device__ __forceinline__ void mh_item(int d, const uint4 *__restrict__ codes_h
 #pragma unroll
                     for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
-                        for (int r = 0; r < MF_RT; ++r) acc[qt][r] = mh_mfma(qa[qt][j], ring[p][r], acc[qt][r]);
+                        for (int r = 0; r < MF_RT; ++r) {
+                            if constexpr (I8)
+                                acci[qt][r] = __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(mf_i32x4, qa[qt][j]),
+                                                                                   __builtin_bit_cast(mf_i32x4, ring[p][r]),
+                                                                                   acci[qt][r], 0, 0, 0);
+                            else acc[qt][r] = mh_mfma(qa[qt][j], ring[p][r], acc[qt][r]);
+                        }
                 next_load(ring[p]);
             }
         }
@@ -1421,10 +1557,14 @@ __device__ __forceinline__ void mh_item(int d, const uint4 *__restrict__ codes_h
                         qiv = qits[qt][v];
                     }
                     float key;
+                    // I8: the sum as a whole-vector convert (per-element extracts of a bit-cast i32 MFMA result were
+                    // miscompiled in the Flat int8 kernel), scaled by s_q·s_x
+                    const float av = I8 ? __builtin_convertvector(acci[qt][r], mf_f32x4)[v] : acc[qt][r][v];
+                    const float sc = I8 ? qiv * xsr[r] : qiv;
                     if (IP) {
-                        key = -acc[qt][r][v] * qiv;
+                        key = -av * sc;
                     } else {
-                        key = fmaf(-2.f * qiv, acc[qt][r][v], qnv + xnr[r]);
+                        key = fmaf(-2.f * sc, av, qnv + xnr[r]);
                         key = key < 0.f ? 0.f : key;
                     }
                     const bool ok = rok && qt * 16 + 4 * g + v < nqi;
@@ -1438,15 +1578,18 @@ __device__ __forceinline__ void mh_item(int d, const uint4 *__restrict__ codes_h
                 }
         }
 #pragma unroll
-        for (int r = 0; r < MF_RT; ++r) xnr[r] = xnr_next[r];
+        for (int r = 0; r < MF_RT; ++r) {
+            xnr[r] = xnr_next[r];
+            xsr[r] = xsr_next[r];
+        }
     }
 
     mf_finish_item<QT>(lst, smem, nqi, bucket, boff, nprobe, slot_off, chunk, k, sub, qbound, part_d, part_i);
 }
 
-// Copy the item's queries' first NT fp16 terms (of the two in qsplit [query][term][S][g][4 dwords]) into LDS
-// [query][term][S][g][4].
-template <int NT>
+// Copy the item's queries' first NT fp16 terms (of the TS in qsplit [query][term][S][g][4 dwords]: 2, or 1 for the
+// int8 units) into LDS [query][term][S][g][4].
+template <int NT, int TS = 2>
 __device__ __forceinline__ void mh_fill(unsigned *qs, const uint4 *__restrict__ qsplit, int nsup, int stride, int nqi,
                                         const int *__restrict__ bucket, int boff, int nprobe) {
     const int per_q = NT * nsup * 4;
@@ -1454,7 +1597,7 @@ __device__ __forceinline__ void mh_fill(unsigned *qs, const uint4 *__restrict__ 
         const int q = t / per_q, rr = t - q * per_q;
         const int j = rr / (nsup * 4), r2 = rr - j * (nsup * 4);
         const int gq = bucket[boff + q] / nprobe;
-        *reinterpret_cast<uint4 *>(qs + q * stride + r2 * 4 + j * nsup * 16) = qsplit[((int64_t)gq * 2 + j) * nsup * 4 + r2];
+        *reinterpret_cast<uint4 *>(qs + q * stride + r2 * 4 + j * nsup * 16) = qsplit[((int64_t)gq * TS + j) * nsup * 4 + r2];
     }
 }
 
@@ -1662,7 +1805,8 @@ __device__ __forceinline__ void mg_item(int d, const uint4 *__restrict__ codes_h
     }
 }
 
-template <bool IP>
+// I8: the int8 image (every item one-term: units in qsplit, s_q in its, s_x in xs8; no residual copy)
+template <bool IP, bool I8>
 __global__ void __launch_bounds__(MF_THREADS, MF_WAVES / 4)
 ivf_scan_mfma_h(const uint4 *__restrict__ qsplit, const float *__restrict__ qnorm, const float *__restrict__ its, int d,
                 const uint4 *__restrict__ codes_h, const int64_t *__restrict__ tpass_off, const float *__restrict__ xn,
@@ -1670,7 +1814,7 @@ ivf_scan_mfma_h(const uint4 *__restrict__ qsplit, const float *__restrict__ qnor
                 const int *__restrict__ item_off, const int *__restrict__ bucket, const int *__restrict__ slot_off,
                 int nlist, int nprobe, int group, int k, int sub, unsigned *__restrict__ qbound, float *__restrict__ part_d,
                 int *__restrict__ part_i, float *__restrict__ qres, int nq, int remap, unsigned *__restrict__ prog,
-                int nprog, unsigned epoch) {
+                int nprog, unsigned epoch, const float *__restrict__ xs8) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const int total = item_off[nlist];
     if ((int)blockIdx.x >= total) return;
@@ -1684,7 +1828,7 @@ ivf_scan_mfma_h(const uint4 *__restrict__ qsplit, const float *__restrict__ qnor
     const int64_t lr0 = list_off[l], lr1 = lr0 + list_len[l];
     const int c = cnt[l];
     const int cls = ivf_list_class(c, group);  // block-uniform
-    const bool wide = cls == 1;
+    const bool wide = I8 || cls == 1;
     const int ng = ivf_ngroups(c, group);
     const int rem = item - item_off[l];
     const int chunk = rem / ng, grp = rem - chunk * ng;
@@ -1695,7 +1839,7 @@ ivf_scan_mfma_h(const uint4 *__restrict__ qsplit, const float *__restrict__ qnor
     const int boff = bucket_off[l] + q_begin;
     const int nqt = (nqi + 15) >> 4;
 
-    if (cls == 2) {
+    if (!I8 && cls == 2) {
         uint4 *stg = reinterpret_cast<uint4 *>(smem);
         float2 *gpar = reinterpret_cast<float2 *>(reinterpret_cast<char *>(smem) + MG_QPAR);
         for (int t = threadIdx.x; t < nqi; t += MF_THREADS) {
@@ -1716,26 +1860,26 @@ ivf_scan_mfma_h(const uint4 *__restrict__ qsplit, const float *__restrict__ qnor
                                     (int)__hip_atomic_load(pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
                               : 0u;
     unsigned *qs = reinterpret_cast<unsigned *>(smem);
-    const int nsup = mh_nsup(d);
-    const int stride = mh_stride(d, wide ? 1 : 2);
+    const int nsup = I8 ? mi_nsup(d) : mh_nsup(d);
+    const int stride = I8 ? mi_nsup(d) * 16 + 8 : mh_stride(d, wide ? 1 : 2);
     float2 *qpar = reinterpret_cast<float2 *>(qs + nqi * stride);  // wide items: (‖q‖², 1/(t·s)) after the image
     if (wide) {
-        mh_fill<1>(qs, qsplit, nsup, stride, nqi, bucket, boff, nprobe);
+        mh_fill<1, I8 ? 1 : 2>(qs, qsplit, nsup, stride, nqi, bucket, boff, nprobe);
         for (int t = threadIdx.x; t < nqi; t += MF_THREADS) {
             const int qi = bucket[boff + t] / nprobe;
             qpar[t] = make_float2(IP ? 0.f : qnorm[qi], its[qi]);
             // these queries' scan keys miss the low term: the rerank bounds them with the one-term residual (every
             // item of the query's wide lists writes the same value)
-            qres[qi] = qres[nq + qi];
+            if (!I8) qres[qi] = qres[nq + qi];
         }
-    } else {
+    } else if constexpr (!I8) {
         mh_fill<2>(qs, qsplit, nsup, stride, nqi, bucket, boff, nprobe);
     }
     if (!HIPANN_MH_EARLY) __syncthreads();  // (early: mh_item waits for the fill after issuing its first row loads)
 
     const int lane = threadIdx.x & 63, g = lane >> 4;
 #define MH_ARGS d, codes_h, tp0, xn, r0, r1, nqi, qs, stride, qn, qi_s, qb, qpar, bucket, boff, nprobe, slot_off, chunk, k, sub, smem, \
-                qbound, part_d, part_i, pw, epoch, pword
+                qbound, part_d, part_i, pw, epoch, pword, xs8
 #define MH_QN(QTV)                                                                                          \
     float qn[QTV][4], qi_s[QTV][4];                                                                         \
     unsigned qb[QTV][4];                                                                                    \
@@ -1746,7 +1890,7 @@ ivf_scan_mfma_h(const uint4 *__restrict__ qsplit, const float *__restrict__ qnor
         qi_s[qt][v] = !wide && q < nqi ? its[qi] : 0.f;                                                     \
         qb[qt][v] = q < nqi ? __atomic_load_n(qbound + qi, __ATOMIC_RELAXED) : 0xffffffffu;                 \
     }
-#define MH_CASE(QTV, NTV) { MH_QN(QTV) mh_item<QTV, IP, NTV>(MH_ARGS); }
+#define MH_CASE(QTV, NTV) { MH_QN(QTV) mh_item<QTV, IP, NTV, I8>(MH_ARGS); }
     if (wide) {
         // nqi > narrow / 2 (a wide list has more than one narrow group of queries, split evenly) unless every list
         // is wide (narrow 0, A/B)
@@ -1756,7 +1900,7 @@ ivf_scan_mfma_h(const uint4 *__restrict__ qsplit, const float *__restrict__ qnor
         else if (nqt == 4) MH_CASE(4, 1)
         else if (nqt == 5) MH_CASE(5, 1)
         else MH_CASE(6, 1)
-    } else {
+    } else if constexpr (!I8) {
         if (nqt <= 1) MH_CASE(1, 2)
         else if (nqt == 2) MH_CASE(2, 2)
         else MH_CASE(3, 2)
@@ -1771,6 +1915,40 @@ int ivf_scan_sublists() { return MF_WAVES; }
 int64_t ivf_half_pass_bytes(int d) { return (int64_t)mh_nsup(d) * MF_RT * 64 * 16; }
 int64_t ivf_half_qsplit_bytes(int64_t nq, int d) { return nq * 2 * mh_nsup(d) * 64; }
 bool ivf_mfma_h_supported(int d, int k) { return d >= 1 && k >= 1 && k <= MF_KMAX && mh_group(d) >= 16; }
+// int8 image: every item one-term, up to 96 queries (MH_QTW tiles) that fit the LDS with their (‖q‖², s_q)
+int ivf_mfma_i8_group(int d) {
+    const int g = (int)(MF_LDS_MAX / ((size_t)(mi_nsup(d) * 16 + 8) * 4 + 8)) / 16 * 16;
+    return (g < 16 * MH_QTW ? g : 16 * MH_QTW) << 8;
+}
+int64_t ivf_i8_pass_bytes(int d) { return (int64_t)mi_nsup(d) * MF_RT * 64 * 16; }
+int64_t ivf_i8_qimg_bytes(int64_t nq, int d) { return nq * mi_nsup(d) * 64; }
+bool ivf_mfma_i8_supported(int d, int k) {
+    return d >= 1 && k >= 1 && k <= MF_KMAX && ivf_group_wide(ivf_mfma_i8_group(d)) >= 16;
+}
+void launch_ivf_tile_i8(const float *codes, const int64_t *list_off, const int *list_len, const int64_t *tpass_off,
+                        int nlist, int64_t total_pass, int d, void *dst, float *xs8, hipStream_t st,
+                        const int64_t *pass_ids) {
+    if (total_pass <= 0) return;
+    HIPANN_REQUIRE(total_pass < (int64_t)0x7fffffff, "too many passes");
+    hipLaunchKernelGGL(ivf_tile_i8, dim3((unsigned)total_pass), dim3(256), 0, st, codes, list_off, list_len, tpass_off,
+                       nlist, d, mi_nsup(d), static_cast<uint4 *>(dst), xs8, pass_ids);
+    HIPANN_CHECK(hipGetLastError());
+}
+void launch_ivf_i8_residual(const float *codes, int64_t n, int d, unsigned *out, hipStream_t st) {
+    HIPANN_CHECK(hipMemsetAsync(out, 0, sizeof(unsigned), st));
+    if (n <= 0) return;
+    HIPANN_REQUIRE(ceil_div(n, 4) < (int64_t)0x7fffffff, "too many rows");
+    hipLaunchKernelGGL(ivf_i8_residual, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, st, codes, n, d, out);
+    HIPANN_CHECK(hipGetLastError());
+}
+void launch_ivf_split_queries_i8(const float *Q, int64_t nq, int d, void *qi8, float *qs8, float *qres8,
+                                 hipStream_t st) {
+    if (nq <= 0) return;
+    HIPANN_REQUIRE(ceil_div(nq, 4) < (int64_t)0x7fffffff, "too many queries");
+    hipLaunchKernelGGL(ivf_split_queries_i8, dim3((unsigned)ceil_div(nq, 4)), dim3(256), 0, st, Q, nq, d, mi_nsup(d),
+                       static_cast<uint4 *>(qi8), qs8, qres8);
+    HIPANN_CHECK(hipGetLastError());
+}
 
 void launch_ivf_max_abs(const float *x, int64_t cnt, unsigned *out, hipStream_t st) {
     HIPANN_CHECK(hipMemsetAsync(out, 0, sizeof(unsigned), st));
@@ -1825,21 +2003,23 @@ void launch_ivf_scan_mfma_h(const float *Q, int64_t nq, void *qsplit, float *its
                             const int64_t *list_off, const int *list_len, const int *cnt, const int *bucket_off,
                             const int *item_off, const int *bucket, const int *slot_off, int nlist, int nprobe, int k,
                             int64_t max_items, unsigned *qbound, float *pd, int *pi, hipStream_t st, bool split_done,
-                            int sub, unsigned *prog, int nprog, unsigned epoch) {
+                            int sub, unsigned *prog, int nprog, unsigned epoch, int i8mode, const float *xs8) {
     if (max_items <= 0 || nq <= 0) return;
     HIPANN_REQUIRE(max_items < (int64_t)0x7fffffff, "too many IVF work items");
     HIPANN_REQUIRE(qsplit && its && qres && codes_h, "fp16 IVF scan: missing buffers");
-    HIPANN_REQUIRE(ivf_mfma_h_supported(d, k), "fp16 IVF scan needs k <= 16");
+    HIPANN_REQUIRE(i8mode ? ivf_mfma_i8_supported(d, k) && xs8 && split_done : ivf_mfma_h_supported(d, k),
+                   "fp16 / int8 IVF scan needs k <= 16 (int8: scales and prepared queries)");
     HIPANN_REQUIRE(metric == kIP || (qn && xn), "decomposed L2 scan needs query and row norms");
     const int nsup = mh_nsup(d);
     uint4 *qs = static_cast<uint4 *>(qsplit);
     if (!split_done)
         hipLaunchKernelGGL(ivf_split_queries_h, dim3((unsigned)ceil_div(nq, 4)), dim3(256), 0, st, Q, nq, d, nsup, es, qs,
                            its, qres, nullptr, (d % 4 == 0) && ((uintptr_t)Q % 16 == 0));
-    const int group = mh_group_packed(d);
+    const int group = i8mode ? ivf_mfma_i8_group(d) : mh_group_packed(d);
     const int gw = ivf_group_wide(group);
     const size_t merge = (size_t)(MF_WAVES / 2) * (gw ? MH_QTW : MF_QTMAX) * 4 * 64 * sizeof(float2);
-    const size_t smem = std::max({(size_t)ivf_group_narrow(group) * mh_stride(d) * 4, (size_t)gw * (mh_stride(d, 1) * 4 + 8), merge,
+    const size_t wstride = i8mode ? (size_t)(mi_nsup(d) * 16 + 8) * 4 : (size_t)mh_stride(d, 1) * 4;
+    const size_t smem = std::max({(size_t)ivf_group_narrow(group) * mh_stride(d) * 4, (size_t)gw * (wstride + 8), merge,
                                   ivf_group_gemm(group) ? MG_LDS : (size_t)0});
     HIPANN_REQUIRE(smem <= MF_LDS_MAX, "fp16 IVF scan: LDS image too large");
     HIPANN_REQUIRE(nq < (int64_t)0x7fffffff, "fp16 IVF scan: batch too large");
@@ -1849,9 +2029,14 @@ void launch_ivf_scan_mfma_h(const float *Q, int64_t nq, void *qsplit, float *its
     // contiguous runs per XCD
     static const int remap = [] { const char *e = std::getenv("HIPANN_IVF_REMAP"); return !e || std::atoi(e) ? 1 : 0; }();
 #define MH_LAUNCH_ARGS qs, qn, its, d, ch, tpass_off, xn, list_off, list_len, cnt, bucket_off, item_off, bucket, slot_off, nlist, nprobe, \
-                       group, k, sub, qbound, pd, pi, qres, (int)nq, remap, prog, nprog, epoch
-    if (metric == kIP) hipLaunchKernelGGL((ivf_scan_mfma_h<true>), grid, block, smem, st, MH_LAUNCH_ARGS);
-    else hipLaunchKernelGGL((ivf_scan_mfma_h<false>), grid, block, smem, st, MH_LAUNCH_ARGS);
+                       group, k, sub, qbound, pd, pi, qres, (int)nq, remap, prog, nprog, epoch, xs8
+    if (i8mode) {
+        if (metric == kIP) hipLaunchKernelGGL((ivf_scan_mfma_h<true, true>), grid, block, smem, st, MH_LAUNCH_ARGS);
+        else hipLaunchKernelGGL((ivf_scan_mfma_h<false, true>), grid, block, smem, st, MH_LAUNCH_ARGS);
+    } else {
+        if (metric == kIP) hipLaunchKernelGGL((ivf_scan_mfma_h<true, false>), grid, block, smem, st, MH_LAUNCH_ARGS);
+        else hipLaunchKernelGGL((ivf_scan_mfma_h<false, false>), grid, block, smem, st, MH_LAUNCH_ARGS);
+    }
 #undef MH_LAUNCH_ARGS
     HIPANN_CHECK(hipGetLastError());
 }

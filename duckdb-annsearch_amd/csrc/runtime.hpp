@@ -421,6 +421,11 @@ struct IvfShard {
     int half_state = 0, half_es = 0;
     float half_rxmax = 0.f;
     DevBuf codes_h, hsplit, hits, hres;
+    // kFormI8Exact: tiled int8 image (same passes), per-row scales, its largest row residual ‖x − s·x̂‖, the batch's
+    // int8 queries / scales / residuals; i8_state as half_state (released by appends: rebuilt at the next search)
+    int i8_state = 0;
+    float i8_rxmax = 0.f;
+    DevBuf codes_i8, xs8, qi8, qs8, qres8;
     DevBuf prog;  // fp16 scan: per 64-pass chunk key, the latest item's position (rounds) and the batch it belongs to
     // an append's staging (hipann_ivf_add): the new rows grouped by list, labels, physical destinations, norms,
     // the tiled passes they touch, and the new rows' maxima (‖x‖², |x|, fp16 residual²)
@@ -458,7 +463,7 @@ struct IvfIndex : IndexBase {
         int64_t b = 0;
         for (auto &s : shards)
             b += s->n * ((int64_t)d * 4 + 8 + (metric == kL2 ? 4 : 0)) + (int64_t)nlist * d * 4 +
-                 (int64_t)s->codes_h.bytes + (int64_t)s->codes_t.bytes;
+                 (int64_t)s->codes_h.bytes + (int64_t)s->codes_t.bytes + (int64_t)s->codes_i8.bytes + (int64_t)s->xs8.bytes;
         return b;
     }
 };
@@ -550,7 +555,20 @@ void launch_ivf_scan_mfma_h(const float *Q, int64_t nq, void *qsplit, float *its
                             const int64_t *list_off, const int *list_len, const int *cnt, const int *bucket_off, const int *item_off,
                             const int *bucket, const int *slot_off, int nlist, int nprobe, int k, int64_t max_items,
                             unsigned *qbound, float *pd, int *pi, hipStream_t st, bool split_done = false,
-                            int sub = 0, unsigned *prog = nullptr, int nprog = 0, unsigned epoch = 0);
+                            int sub = 0, unsigned *prog = nullptr, int nprog = 0, unsigned epoch = 0, int i8mode = 0,
+                            const float *xs8 = nullptr);
+// int8 image (kFormI8Exact): packed group (wide items only), pass / query-image bytes, support, the tiling (one scale per
+// row into xs8), max row residual² (float bits), the batch's int8 queries (units, scales, residuals)
+int ivf_mfma_i8_group(int d);
+int64_t ivf_i8_pass_bytes(int d);
+int64_t ivf_i8_qimg_bytes(int64_t nq, int d);
+bool ivf_mfma_i8_supported(int d, int k);
+void launch_ivf_tile_i8(const float *codes, const int64_t *list_off, const int *list_len, const int64_t *tpass_off,
+                        int nlist, int64_t total_pass, int d, void *dst, float *xs8, hipStream_t st,
+                        const int64_t *pass_ids = nullptr);
+void launch_ivf_i8_residual(const float *codes, int64_t n, int d, unsigned *out, hipStream_t st);
+void launch_ivf_split_queries_i8(const float *Q, int64_t nq, int d, void *qi8, float *qs8, float *qres8,
+                                 hipStream_t st);
 // the batch's fp16 query terms (+ 1/(t·s), split residuals) and, when qn != nullptr, ‖q‖² (row_norms_f32's bits)
 void launch_ivf_split_queries_h(const float *Q, int64_t nq, int d, int es, void *qsplit, float *its, float *qres,
                                 float *qn, hipStream_t st);

@@ -425,6 +425,7 @@ class HipIndexIVFFlat(_Handle):
     FORM_SPLIT2 = 4           # decomposed, 2-term bf16 split (3 products, ~2^-16 relative per product)
     FORM_SPLIT2_EXACT = 5     # the SPLIT2 scan as a filter + exact direct-form rerank with a bound check
     FORM_HALF_EXACT = 6       # default: the same rerank, the filter scan over a tiled fp16 image (half the bytes)
+    FORM_I8_EXACT = 7         # opt-in: the same rerank, the filter scan over a tiled int8 image (a quarter of the bytes)
 
     @property
     def form(self) -> int:
@@ -434,7 +435,7 @@ class HipIndexIVFFlat(_Handle):
     def form(self, v: int) -> None:
         if lib().hipann_ivf_set_form(self._h, int(v)) != 0:
             raise HipAnnError("form must be 0 (decomposed), 1 (direct), 2 (decomposed, VALU), 3 or 4 (split bf16), "
-                              "5 (split bf16 + exact rerank), 6 (fp16 image + exact rerank)")
+                              "5 (split bf16 + exact rerank), 6 (fp16 image + exact rerank), 7 (int8 image + exact rerank)")
 
     def search(self, x, k: int, nprobe: Optional[int] = None) -> Tuple[np.ndarray, np.ndarray]:
         """search(n, x, k) — with ``nprobe`` the per-call SearchParametersIVF value (hipann_ivf_search_np:

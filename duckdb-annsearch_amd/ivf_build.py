@@ -233,6 +233,13 @@ def half_scan_groups(d: int, mode: int = 2, gemm: bool = False) -> tuple:
     return (0 if mode == 2 else g), w, (256 if gemm and w >= 16 else 0)
 
 
+def i8_scan_groups(d: int) -> tuple:
+    """(narrow, wide, gemm) query-group sizes of the int8 form's scan (ivf_mfma.hip ivf_mfma_i8_group: every item
+    one-term, the queries' int8 units in 64-dim super-steps + (‖q‖², s_q) in 160 KiB, at most 96)."""
+    nsup = -(-(-(-d // 64)) // 6) * 6
+    return 0, min(96, (163840 // ((nsup * 16 + 8) * 4 + 8)) // 16 * 16), 0
+
+
 def scan_group_rows(index, probes: np.ndarray, group: int = 32, wide: int = 0, gemm: int = 0) -> int:
     """Rows the scan kernel streams per batch: every list once per group of its probing queries,
     Σ_l ⌈c_l / g_l⌉·|l| with g_l = `gemm` for a list probed by more than the wide size (when gemm > 0), `wide` for

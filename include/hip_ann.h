@@ -297,6 +297,12 @@ int hipann_ivf_export(void *index, float *centroids, int64_t *list_offsets, int6
  * residuals (largest row ‖x − x̂‖, the query's split residual) plus fp32 accumulation.  Codes with a
  * non-finite entry take SPLIT2_EXACT; k ≤ 12 (larger k: SPLIT3).  Results equal SPLIT2_EXACT's. */
 #define HIPANN_IVF_FORM_HALF_EXACT 6
+/* HIPANN_IVF_FORM_I8_EXACT (opt-in): the same filter + exact rerank over a tiled int8 image (one scale per row,
+ * max|x|/127: a quarter of the fp32 rows' bytes) against int8 queries on the int8 matrix cores (exact int32 sums);
+ * the scan always keeps per-wave sub-lists and the rerank takes 64 candidates, certified with the int8 residuals.
+ * The image is rebuilt at the first search after an add.  Codes with a non-finite entry, or k > 64, take
+ * SPLIT2_EXACT.  Results equal SPLIT2_EXACT's. */
+#define HIPANN_IVF_FORM_I8_EXACT 7
 int hipann_ivf_set_form(void *index, int form);
 int hipann_ivf_get_form(void *index);
 /* Queries the exact forms' bound check flagged since the index was created (each re-run on the device in

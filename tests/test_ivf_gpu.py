@@ -48,7 +48,7 @@ def test_ivf_faiss_metal_shapes(gpu, oracle, nv, d, nlist, nprobe, nq, k, metric
 
 @pytest.mark.parametrize("nq", [1, 7, 19, 20, 64, 333])
 @pytest.mark.parametrize("metric", [0, 1])
-@pytest.mark.parametrize("form", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("form", [0, 1, 2, 3, 4, 5, 6, 7])
 def test_ivf_vs_oracle_probe_sets(gpu, oracle, nq, metric, form):
     xb, xq = faiss_metal_case(20000, nq, 96)
     ix, (cen, off, ids, codes) = _ivf(gpu, xb, 64, 8, metric)
@@ -62,7 +62,7 @@ def test_ivf_vs_oracle_probe_sets(gpu, oracle, nq, metric, form):
 
 @pytest.mark.parametrize("d", [4, 8, 12, 20, 44, 77, 132, 768])
 @pytest.mark.parametrize("metric", [0, 1])
-@pytest.mark.parametrize("form", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("form", [0, 1, 2, 3, 4, 5, 6, 7])
 def test_ivf_dims(gpu, oracle, d, metric, form):
     """Dimensions around the scans' LDS chunks (32 dims MFMA, 32 VALU-decomposed, 24 direct: partial
     last chunk, d < one chunk) and d % 4 != 0 (the decomposed forms fall back to the direct kernel)."""
@@ -76,7 +76,7 @@ def test_ivf_dims(gpu, oracle, d, metric, form):
 
 
 @pytest.mark.parametrize("nq", [5, 70])
-@pytest.mark.parametrize("form", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("form", [0, 1, 2, 3, 4, 5, 6, 7])
 def test_ivf_long_lists(gpu, oracle, nq, form):
     """Lists longer than one work item's row chunk (2048 rows) and ragged 256-row tiles; with nq = 70 a
     list's probing queries split over several query groups."""
@@ -92,7 +92,7 @@ def test_ivf_long_lists(gpu, oracle, nq, form):
 
 @pytest.mark.parametrize("nq", [1, 15, 16, 17, 31, 33, 47, 48, 49, 64, 65, 130])
 @pytest.mark.parametrize("d,metric", [(96, 0), (100, 0), (96, 1)])
-@pytest.mark.parametrize("form", [0, 3, 4, 5, 6])
+@pytest.mark.parametrize("form", [0, 3, 4, 5, 6, 7])
 def test_ivf_mfma_query_tiles(gpu, oracle, nq, d, metric, form):
     """One list probed by every query: items of 1-4 16-query tiles (every wave → work mapping of the
     MFMA scan, incl. the idle wave at 3 tiles and the list merges at 1-2 tiles), several query groups
@@ -111,21 +111,23 @@ def test_ivf_mfma_query_tiles(gpu, oracle, nq, d, metric, form):
 @pytest.mark.parametrize("nq", [17, 49, 80, 81, 96, 97, 150, 193, 256, 257, 290, 513, 700])
 @pytest.mark.parametrize("d,metric", [(96, 0), (100, 1), (768, 0), (1536, 0)])
 @pytest.mark.parametrize("k", [10, 20])
-def test_ivf_half_wide_items(gpu, oracle, nq, d, metric, k):
+@pytest.mark.parametrize("form", [6, 7])
+def test_ivf_half_wide_items(gpu, oracle, nq, d, metric, k, form):
     """The fp16 form's one-term items (ivf_mfma.hip): every list's queries enter on their high fp16 term, in wide
     items of up to 96 queries (48 at d = 1536): one item of 17-96 queries (2-6 query tiles), two of 48/49 or 128/129,
     three or more, ragged last query tiles; k = 20 takes the sub-list slots.  Run with HIPANN_IVF_GEMM=1 (A/B,
     tools/gpu_r06_gemm.sh) a list probed by more than 96 queries takes GEMM items of up to 256 instead (one of 97-256
     queries, two of 128/129, three of 171 at 513).  The rerank bounds those queries with their one-term residual, so
-    the ids still equal the oracle's."""
+    the ids still equal the oracle's.  Form 7 (the int8 image) runs the same items over 64-dim super-steps (96 queries
+    at d = 1536 too) with the sub-lists and 64 reranked candidates at every k."""
     xb, xq = faiss_metal_case(4500 if d < 1000 else 2500, nq, d)
     cen = np.ascontiguousarray(xb[:2])
     off = np.array([0, 2100, len(xb)], np.int64)  # two lists, both probed by every query: 2 row chunks, ragged
     ids = np.arange(len(xb), dtype=np.int64)
     ix = gpu.HipIndexIVFFlat(cen, off, ids, xb, 2, metric)
-    ix.form = 6
+    ix.form = form
     D, I = ix.search(xq, k)
-    assert ix.last_search_path()["form"] == 6
+    assert ix.last_search_path()["form"] == form
     Do, Io, Po = oracle.ivf_search(cen, off, ids, xb, xq, k, 2, metric)
     assert np.array_equal(ix.last_probes(nq), Po)
     check_topk_parity(xb, xq, D, I, Do, Io, metric, tau=TAU)
@@ -332,7 +334,7 @@ def test_ivf_large_nprobe(gpu, oracle, nprobe, k):
         check_topk_parity(xb, xq, D, I, Df, If_)
 
 
-@pytest.mark.parametrize("form", [5, 6])
+@pytest.mark.parametrize("form", [5, 6, 7])
 @pytest.mark.parametrize("metric", [0, 1])
 def test_ivf_exact_form_distances_are_direct(gpu, oracle, metric, form):
     """Forms 5 and 6 (default): the returned distances are the direct-form fp32 distances of the returned
@@ -349,7 +351,7 @@ def test_ivf_exact_form_distances_are_direct(gpu, oracle, metric, form):
     assert np.allclose(D[valid], Do[valid], rtol=2e-6, atol=1e-6)
 
 
-@pytest.mark.parametrize("form", [5, 6])
+@pytest.mark.parametrize("form", [5, 6, 7])
 def test_ivf_exact_form_fallback_on_ties(gpu, oracle, form):
     """Every vector stored 24 times: the 16 rerank candidates tie, the bound check cannot prove the top-k,
     and the flagged queries are re-run on the device in the direct form — results equal the oracle's, slot for
@@ -509,7 +511,7 @@ def test_ivf_device_fallback_labels_and_batch(gpu, oracle, metric):
     assert np.allclose(D[v], Do[v], rtol=2e-6, atol=1e-6)
 
 
-@pytest.mark.parametrize("form", [5, 6])
+@pytest.mark.parametrize("form", [5, 6, 7])
 @pytest.mark.parametrize("metric", [0, 1])
 def test_ivf_exact_ties_scan_order_unflagged(gpu, oracle, form, metric):
     """Exact ties that the rerank resolves itself (no fallback): each vector stored 3 times in its list, the
@@ -537,7 +539,7 @@ def test_ivf_exact_ties_scan_order_unflagged(gpu, oracle, form, metric):
     assert ix.rerank_fallbacks() - before < len(xq) // 2
 
 
-@pytest.mark.parametrize("form", [6, 5, 0])
+@pytest.mark.parametrize("form", [6, 5, 0, 7])
 def test_ivf_successive_appends_incremental(gpu, oracle, form):
     """20 successive 2048-row appends (DuckDB's Append chunks, faiss_index.cpp:469) after the
     scan's tiled image exists.  Each append writes its rows into their lists' slack (ivf_relayout grows only the
@@ -567,7 +569,7 @@ def test_ivf_successive_appends_incremental(gpu, oracle, form):
     Do, Io, Po = oracle.ivf_search(cen, off, ids, codes, xq, 10, 8)
     assert np.array_equal(ix.last_probes(256), Po)
     st = check_topk_parity(xb, xq, D, I, Do, Io)
-    if form in (5, 6):
+    if form in (5, 6, 7):
         assert st["exact_fraction"] == 1.0, st
     # a fresh index over the exported lists answers identically (the slack layout is invisible)
     fresh = gpu.HipIndexIVFFlat(cen, off, ids, codes, 8)
@@ -622,7 +624,7 @@ def test_ivf_nan_and_overflow_queries_pad_like_faiss(gpu, oracle, metric):
     assert st["exact_fraction"] == 1.0, st
 
 
-@pytest.mark.parametrize("form", [6, 5, 0])
+@pytest.mark.parametrize("form", [6, 5, 0, 7])
 def test_ivf_empty_l2_index_then_append(gpu, oracle, form):
     """ADVICE r05 (high): an L2 IVF index created with zero rows has no norm array (compute_row_norms skips n = 0);
     the first append's relayout must give it one, because ivf_append_rows writes the new rows' norms into it and the
@@ -646,11 +648,11 @@ def test_ivf_empty_l2_index_then_append(gpu, oracle, form):
     Do, Io, Po = oracle.ivf_search(cen, off, ids, codes, xq, 10, 4)
     assert np.array_equal(ix.last_probes(len(xq)), Po)
     st = check_topk_parity(xb, xq, D, I, Do, Io)
-    if form in (5, 6):
+    if form in (5, 6, 7):
         assert st["exact_fraction"] == 1.0, st
 
 
-@pytest.mark.parametrize("form", [5, 0])
+@pytest.mark.parametrize("form", [5, 0, 7])
 def test_ivf_search_probes_device_reused_buffer(gpu, oracle, form):
     """search_probes_device (caller-supplied probe lists, no coarse step) must compute ‖q‖² of
     THIS call's queries: two calls on one device buffer whose contents change in between (same pointer, same nq)
@@ -680,7 +682,7 @@ def test_ivf_search_probes_device_reused_buffer(gpu, oracle, form):
         torch.cuda.synchronize()
         D, I = Dt.cpu().numpy(), It.cpu().numpy()
         st = check_topk_parity(xb, xq, D, I, Do, Io)
-        if form == 5:
+        if form in (5, 7):
             assert st["exact_fraction"] == 1.0, (rep, st)
 
 
@@ -704,3 +706,38 @@ def test_peer_access_query_multi_device_handles(gpu, oracle):
         two = gpu.HipIndexFlat(32, 0, xb, devices=[0, 1])
         can = torch.cuda.can_device_access_peer(0, 1) and torch.cuda.can_device_access_peer(1, 0)
         assert two.peer_access() == [two.PEER_SAME_DEVICE, two.PEER_ENABLED if can else two.PEER_UNAVAILABLE]
+
+
+@pytest.mark.parametrize("metric", [0, 1])
+def test_ivf_i8_form_nonfinite_and_scaled(gpu, oracle, metric):
+    """Form 7 (the int8 image, one scale per row): rows at very different magnitudes (each row has its own scale, so
+    small rows keep their relative precision), a NaN query (FAISS's all −1 labels) and an append (the image is released and rebuilt at
+    the next search); ids equal the oracle's throughout."""
+    rng = np.random.default_rng(70 + metric)
+    d = 80
+    xb = rng.standard_normal((12_000, d), dtype=np.float32)
+    xb[::3] *= np.float32(1e-3)
+    xb[1::7] *= np.float32(50.0)
+    xq = rng.standard_normal((60, d), dtype=np.float32)
+    xq[5, 7] = np.nan
+    cen = np.ascontiguousarray(xb[::400][:30])
+    off, ids, codes = build_ivf_lists(xb, cen, metric)
+    ix = gpu.HipIndexIVFFlat(cen, off, ids, codes, 5, metric=metric)
+    ix.form = 7
+    D, I = ix.search(xq, 10)
+    assert ix.last_search_path()["form"] == 7
+    Do, Io, _ = oracle.ivf_search(cen, off, ids, codes, xq, 10, 5, metric)
+    assert (Io[5] == -1).all() and (I[5] == -1).all()
+    good = np.array([i for i in range(len(xq)) if i != 5])
+    st = check_topk_parity(xb, xq[good], D[good], I[good], Do[good], Io[good], metric)
+    assert st["exact_fraction"] == 1.0, st
+    # an append releases the int8 image; the next search rebuilds it over the grown lists
+    xa = (rng.standard_normal((3000, d)) * 3.0).astype(np.float32)
+    ix.add(xa)
+    xall = np.concatenate([xb, xa])
+    off2, ids2, codes2 = build_ivf_lists(xall, cen, metric)
+    D2, I2 = ix.search(xq[good], 10)
+    assert ix.last_search_path()["form"] == 7
+    Do2, Io2, _ = oracle.ivf_search(cen, off2, ids2, codes2, xq[good], 10, 5, metric)
+    st = check_topk_parity(xall, xq[good], D2, I2, Do2, Io2, metric)
+    assert st["exact_fraction"] == 1.0, st
